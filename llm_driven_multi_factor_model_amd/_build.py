@@ -1,0 +1,105 @@
+"""Build the in-tree HIP kernel library for gfx950 (MI355X).
+
+Every ``csrc/*.hip`` file is compiled with ``hipcc --offload-arch=gfx950`` into an object and
+linked into ``_lib/libmfa_hip.so``.  The library exposes a plain C ABI (raw device pointers +
+``hipStream_t``) consumed through :mod:`ctypes` by :mod:`._native`, so the build needs neither
+torch headers nor a JIT cache: the ``.so`` lives in-tree and travels with the repository
+snapshot to the GPU box.
+
+Usage::
+
+    python -m llm_driven_multi_factor_model_amd._build [--force] [-j 8]
+"""
+from __future__ import annotations
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+PKG_DIR = Path(__file__).resolve().parent
+CSRC = PKG_DIR / "csrc"
+OBJ_DIR = PKG_DIR / "_lib" / "obj"
+LIB_PATH = PKG_DIR / "_lib" / "libmfa_hip.so"
+ARCH = os.environ.get("MFA_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and Path(cand).exists():
+            return cand
+    raise RuntimeError("hipcc not found (set HIPCC or install ROCm at /opt/rocm)")
+
+
+def _flags() -> list[str]:
+    return [
+        f"--offload-arch={ARCH}",
+        "-O3",
+        "-std=c++17",
+        "-fPIC",
+        "-ffp-contract=fast",
+        "-munsafe-fp-atomics",
+        f"-I{CSRC}",
+    ]
+
+
+def sources() -> list[Path]:
+    return sorted(CSRC.glob("*.hip"))
+
+
+def _stale(src: Path, obj: Path, headers: list[Path]) -> bool:
+    if not obj.exists():
+        return True
+    t = obj.stat().st_mtime
+    return src.stat().st_mtime > t or any(h.stat().st_mtime > t for h in headers)
+
+
+def _compile(src: Path, obj: Path) -> tuple[Path, str]:
+    cmd = [_hipcc(), *_flags(), "-c", str(src), "-o", str(obj)]
+    p = subprocess.run(cmd, capture_output=True, text=True)
+    if p.returncode != 0:
+        raise RuntimeError(f"hipcc failed for {src.name}:\n{p.stderr}")
+    return obj, p.stderr
+
+
+def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
+    """Compile all kernels (incrementally) and link the shared library; returns its path."""
+    OBJ_DIR.mkdir(parents=True, exist_ok=True)
+    headers = sorted(CSRC.glob("*.h"))
+    srcs = sources()
+    objs = [OBJ_DIR / (s.stem + ".o") for s in srcs]
+    todo = [(s, o) for s, o in zip(srcs, objs) if force or _stale(s, o, headers)]
+    jobs = jobs or min(8, max(1, (os.cpu_count() or 2)))
+    if todo:
+        with cf.ThreadPoolExecutor(max_workers=min(jobs, len(todo))) as ex:
+            for obj, err in ex.map(lambda so: _compile(*so), todo):
+                if verbose:
+                    print(f"[mfa-build] compiled {obj.name}", file=sys.stderr)
+    relink = force or bool(todo) or not LIB_PATH.exists() or any(
+        o.stat().st_mtime > LIB_PATH.stat().st_mtime for o in objs)
+    if relink:
+        tmp = LIB_PATH.with_suffix(".so.tmp")
+        cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]
+        p = subprocess.run(cmd, capture_output=True, text=True)
+        if p.returncode != 0:
+            raise RuntimeError(f"link failed:\n{p.stderr}")
+        os.replace(tmp, LIB_PATH)
+        if verbose:
+            print(f"[mfa-build] linked {LIB_PATH}", file=sys.stderr)
+    return LIB_PATH
+
+
+def main(argv: list[str] | None = None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__)
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=None)
+    a = ap.parse_args(argv)
+    print(build(force=a.force, jobs=a.jobs, verbose=True))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

@@ -1,0 +1,162 @@
+"""Dense (date x stock) risk-model panel resident in device memory.
+
+The reference keeps one long pandas frame and boolean-mask-selects every date
+(``Barra-master/mfm/MFM.py:58``).  Here a panel is a set of dense device tensors:
+
+* ``styles`` [D, Q, N] float32 — style exposures, stocks contiguous per (date, style) so the
+  regression kernel's loads are fully coalesced;
+* ``cap``, ``ret`` [D, N] float32 — capital (``circ_mv``) and t+1 return;
+* ``ind`` [D, N] int16 — industry id in ``[0, P)``, ``-1`` where the stock is absent
+  (ragged universes are masks, industries are ids — never one-hot columns).
+
+At N = 5000, D = 2520 (10y all-A) a panel is 0.6 GB: trivially resident in 288 GB of HBM3E,
+so every stage runs batched over all dates of a rank's shard.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field, replace
+
+import numpy as np
+import torch
+
+
+@dataclass
+class RiskPanel:
+    styles: torch.Tensor          # [D, Q, N] f32
+    cap: torch.Tensor             # [D, N] f32
+    ret: torch.Tensor             # [D, N] f32
+    ind: torch.Tensor | None      # [D, N] int16 or None (P == 0)
+    P: int
+    dates: np.ndarray             # [D] datetime64[ns]
+    stocks: np.ndarray            # [N] object (ts_code)
+    style_names: list[str] = field(default_factory=list)
+    industry_names: list[str] = field(default_factory=list)
+    date_offset: int = 0          # index of dates[0] in the global calendar (sharded panels)
+
+    @property
+    def D(self) -> int:
+        return self.styles.shape[0]
+
+    @property
+    def Q(self) -> int:
+        return self.styles.shape[1]
+
+    @property
+    def N(self) -> int:
+        return self.styles.shape[2]
+
+    @property
+    def K(self) -> int:
+        return 1 + self.P + self.Q
+
+    @property
+    def device(self) -> torch.device:
+        return self.styles.device
+
+    @property
+    def factor_names(self) -> list[str]:
+        ind = self.industry_names or [f"ind{j}" for j in range(self.P)]
+        sty = self.style_names or [f"style{q}" for q in range(self.Q)]
+        return ["country", *ind, *sty]
+
+    def to(self, device) -> "RiskPanel":
+        return replace(self, styles=self.styles.to(device), cap=self.cap.to(device),
+                       ret=self.ret.to(device),
+                       ind=None if self.ind is None else self.ind.to(device))
+
+    def slice_dates(self, a: int, b: int) -> "RiskPanel":
+        return replace(self, styles=self.styles[a:b], cap=self.cap[a:b], ret=self.ret[a:b],
+                       ind=None if self.ind is None else self.ind[a:b], dates=self.dates[a:b],
+                       date_offset=self.date_offset + a)
+
+    def valid(self) -> torch.Tensor:
+        from ..ops.cross_section import valid_mask
+        return valid_mask(self.styles, self.cap, self.ret, self.ind, self.P)
+
+    def nbytes(self) -> int:
+        n = self.styles.numel() * 4 + self.cap.numel() * 4 + self.ret.numel() * 4
+        return n + (0 if self.ind is None else self.ind.numel() * 2)
+
+
+def business_days(D: int, start: str = "2010-01-04") -> np.ndarray:
+    return np.asarray(np.busday_offset(np.datetime64(start, "D"), np.arange(D), roll="forward"),
+                      dtype="datetime64[ns]")
+
+
+def synthetic_panel(D: int, N: int, P: int = 31, Q: int = 10, *, seed: int = 0,
+                    device="cpu", missing_frac: float = 0.0, empty_industries: int = 0,
+                    factor_vol: float = 0.01, noise_vol: float = 0.02,
+                    return_truth: bool = False):
+    """Synthetic Barra panel with planted factor returns (the reference ships no data).
+
+    * caps log-normal (``circ_mv``-like, 10k CNY units), styles N(0,1) with a per-style offset,
+      industries SW-L1-like with uneven sizes;
+    * ``missing_frac`` of (date, stock) cells are absent (``ind = -1``, NaN exposures) to make
+      universes ragged;
+    * ``empty_industries`` industries are emptied on a subset of dates (rank-deficiency
+      edge case of quirk Q3/Q4);
+    * returns follow ``r = f_c + f_ind + sum_q z_q f_q + eps`` on the z-scored styles, so the
+      regression should recover the planted ``f`` up to noise.
+
+    Generation runs on ``device`` (a 5000 x 2520 panel is generated on the GPU in
+    milliseconds).
+    """
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    dev = torch.device(device)
+    styles = torch.randn(D, Q, N, generator=g, device=dev)
+    styles += torch.linspace(-0.5, 0.5, Q, device=dev)[None, :, None]
+    cap = torch.exp(torch.randn(D, N, generator=g, device=dev) * 1.2 + 13.0)
+    if P > 0:
+        # uneven industry sizes, stable per stock with occasional reclassification
+        probs = torch.linspace(1.0, 3.0, P, device=dev)
+        base = torch.multinomial(probs / probs.sum(), N, replacement=True, generator=g)
+        ind = base[None, :].expand(D, N).clone()
+        flip = torch.rand(D, N, generator=g, device=dev) < 0.002
+        ind = torch.where(flip, torch.randint(0, P, (D, N), generator=g, device=dev), ind)
+        ind = ind.to(torch.int16)
+        if empty_industries > 0:
+            nd = max(1, D // 4)
+            for k in range(empty_industries):
+                j = (k * 7 + 3) % P
+                dsel = torch.arange(k % max(1, D - nd), min(D, k % max(1, D - nd) + nd), device=dev)
+                sub = ind[dsel]
+                ind[dsel] = torch.where(sub == j, torch.full_like(sub, (j + 1) % P), sub)
+    else:
+        ind = None
+    K = 1 + P + Q
+    f_true = torch.randn(D, K, generator=g, device=dev, dtype=torch.float64) * factor_vol
+    if P > 0:
+        # make the planted industry returns satisfy the cap-weighted neutrality constraint
+        oh = torch.nn.functional.one_hot(ind.long(), P).double()
+        s = (oh * cap.double()[..., None]).sum(1)
+        fi = f_true[:, 1:1 + P]
+        f_true[:, 1:1 + P] = fi - ((s * fi).sum(1) / s.sum(1))[:, None]
+    z = styles.double()
+    mu = (cap.double()[:, None, :] * z).sum(2) / cap.double().sum(1)[:, None]
+    sig = z.reshape(D, -1).std(1, unbiased=False)
+    zs = (z - mu[..., None]) / sig[:, None, None]
+    r = f_true[:, :1] + (zs * f_true[:, 1 + P:, None]).sum(1)
+    if P > 0:
+        r = r + f_true[:, 1:1 + P].gather(1, ind.long())
+    r = r + torch.randn(D, N, generator=g, device=dev, dtype=torch.float64) * noise_vol
+    ret = r.float()
+    if missing_frac > 0:
+        miss = torch.rand(D, N, generator=g, device=dev) < missing_frac
+        styles = styles.masked_fill(miss[:, None, :], float("nan"))
+        ret = ret.masked_fill(miss, float("nan"))
+        if ind is not None:
+            ind = ind.masked_fill(miss, -1)
+    panel = RiskPanel(
+        styles=styles.contiguous(), cap=cap.contiguous(), ret=ret.contiguous(),
+        ind=None if ind is None else ind.contiguous(), P=P, dates=business_days(D),
+        stocks=np.array([f"{i:06d}.SZ" for i in range(N)], dtype=object),
+        style_names=DEFAULT_STYLE_NAMES[:Q] if Q <= len(DEFAULT_STYLE_NAMES) else [f"style{q}" for q in range(Q)],
+        industry_names=[f"ind{j:02d}" for j in range(P)])
+    return (panel, f_true) if return_truth else panel
+
+
+DEFAULT_STYLE_NAMES = [
+    "size", "beta", "momentum", "residual_volatility", "non_linear_size",
+    "book_to_price_ratio", "liquidity", "earnings_yield", "growth", "leverage",
+]

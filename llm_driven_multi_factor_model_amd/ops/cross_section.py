@@ -1,0 +1,246 @@
+"""Batched cross-sectional WLS factor-return regression (kernel K1+K2+K3).
+
+Semantics follow ``Barra-master/mfm/CrossSection.py``:
+
+* style z-score ``(x - mu_c) / sigma`` with the cap-weighted mean ``mu_c`` and ONE pooled
+  ddof-0 std over all N*Q style entries (``CrossSection.py:12-20``);
+* WLS weights ``sqrt(cap)`` (the reference normalises them, ``:50``; the solution is scale
+  invariant);
+* industry-neutral constraint ``sum_j s_j f_j = 0`` with raw industry caps ``s_j``
+  (``:66-71``), pseudo-inverse solve (``:76``);
+* ``f = Omega r``, ``e = r - X f``, unweighted ``R^2 = 1 - var(e)/var(r)`` (``:101-106``).
+
+Ragged universes are expressed with ``ind < 0`` (absent stock) or any non-finite input.
+
+GPU tensors run the fused HIP kernel ``csrc/xs_wls.hip`` (one launch for all dates);
+CPU tensors run :func:`xs_wls_reference`, a dense float64 transcription of the reference
+formula (batched ``pinv``) that also serves as the numerics oracle for the kernel.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+
+import torch
+
+from .. import _native
+
+# status bits (csrc/xs_wls.hip XsStatus)
+XS_NO_ROWS = 1
+XS_PIVOT_EMPTY = 2
+XS_NEAR_SINGULAR = 4
+XS_ZERO_PIVOT = 8
+XS_BAD_SIGMA = 16
+
+
+@dataclass
+class XsResult:
+    """Per-date regression outputs (all dates of the shard).
+
+    f:      [D, K] float64 factor returns, K = 1 + P + Q (country, industries, styles)
+    resid:  [D, N] float32 specific returns (NaN where the stock is absent) or None
+    r2:     [D]    float64 unweighted R^2
+    stats:  [D, Q+2] float64 = (cap-weighted style means, pooled sigma, n_valid)
+    status: [D]    int32 XS_* bit flags
+    """
+
+    f: torch.Tensor
+    resid: torch.Tensor | None
+    r2: torch.Tensor
+    stats: torch.Tensor
+    status: torch.Tensor
+
+
+def _validate(X, cap, ret, ind, P):
+    if X.dim() != 3:
+        raise ValueError("X must be [D, Q, N]")
+    D, Q, N = X.shape
+    if cap.shape != (D, N) or ret.shape != (D, N):
+        raise ValueError(f"cap/ret must be [D, N] = {(D, N)}; got {tuple(cap.shape)}, {tuple(ret.shape)}")
+    if P > 0 and (ind is None or ind.shape != (D, N)):
+        raise ValueError("ind must be [D, N] when P > 0")
+    if not 1 <= Q <= 16:
+        raise ValueError(f"Q={Q} outside the supported 1..16 range")
+    if P > 128:
+        raise ValueError(f"P={P} > 128 industries is not supported")
+    return D, Q, N
+
+
+def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Tensor | None,
+           P: int, *, pivot_mode: int = 0, tol: float = 1e-14, want_resid: bool = True,
+           waves: int = 0, refine: bool = True, out: XsResult | None = None) -> XsResult:
+    """Regress every date of the panel in one batched call.
+
+    X [D,Q,N] f32 styles, cap/ret [D,N] f32, ind [D,N] int16 industry ids (or None if P == 0).
+    ``pivot_mode`` 0 eliminates the last NON-EMPTY industry (identical solution whenever the
+    reference's choice is valid); 1 reproduces the reference exactly (always the last column,
+    NaN when it is empty, quirk Q3).  ``refine`` re-solves dates the kernel flags as
+    near-singular with the pseudo-inverse reference path (pinv semantics, quirk Q4).
+    ``out`` lets a caller (e.g. a timed loop) reuse preallocated output buffers.
+    """
+    D, Q, N = _validate(X, cap, ret, ind, P)
+    K = 1 + P + Q
+    if not X.is_cuda:
+        return xs_wls_reference(X, cap, ret, ind, P, pivot_mode=pivot_mode, want_resid=want_resid)
+    dev = X.device
+    X = _native.check_device_tensor(X, torch.float32, "X")
+    cap = _native.check_device_tensor(cap, torch.float32, "cap")
+    ret = _native.check_device_tensor(ret, torch.float32, "ret")
+    if P > 0:
+        ind = _native.check_device_tensor(ind, torch.int16, "ind")
+    if out is None:
+        out = XsResult(
+            f=torch.empty(D, K, dtype=torch.float64, device=dev),
+            resid=torch.empty(D, N, dtype=torch.float32, device=dev) if want_resid else None,
+            r2=torch.empty(D, dtype=torch.float64, device=dev),
+            stats=torch.empty(D, Q + 2, dtype=torch.float64, device=dev),
+            status=torch.empty(D, dtype=torch.int32, device=dev),
+        )
+    _native.call("mfa_xs_wls", _native.ptr(X), _native.ptr(cap), _native.ptr(ret),
+                 _native.ptr(ind if P > 0 else None), D, N, P, Q, pivot_mode, tol, waves,
+                 _native.ptr(out.f), _native.ptr(out.resid), _native.ptr(out.r2),
+                 _native.ptr(out.stats), _native.ptr(out.status), _native.stream(dev))
+    if refine:
+        _refine_near_singular(X, cap, ret, ind, P, pivot_mode, out)
+    return out
+
+
+def _refine_near_singular(X, cap, ret, ind, P, pivot_mode, out: XsResult) -> None:
+    bad = torch.nonzero((out.status & XS_NEAR_SINGULAR) != 0).flatten()
+    if bad.numel() == 0:
+        return
+    idx = bad.cpu()
+    sub = xs_wls_reference(X[bad].cpu(), cap[bad].cpu(), ret[bad].cpu(),
+                           ind[bad].cpu() if P > 0 else None, P, pivot_mode=pivot_mode,
+                           want_resid=out.resid is not None)
+    out.f[bad] = sub.f.to(out.f.device)
+    out.r2[bad] = sub.r2.to(out.r2.device)
+    if out.resid is not None:
+        out.resid[bad] = sub.resid.to(out.resid.device)
+    del idx
+
+
+def valid_mask(X, cap, ret, ind, P) -> torch.Tensor:
+    """Rows entering the regression: industry assigned, finite inputs, non-negative capital."""
+    m = torch.isfinite(cap) & (cap >= 0) & torch.isfinite(ret) & torch.isfinite(X).all(dim=1)
+    if P > 0:
+        m &= (ind >= 0) & (ind < P)
+    return m
+
+
+def xs_wls_reference(X, cap, ret, ind, P, *, pivot_mode: int = 0, want_resid: bool = True,
+                     chunk: int = 256) -> XsResult:
+    """Dense float64 oracle, a direct batched transcription of ``CrossSection.reg``.
+
+    Builds ``[1 | one-hot | z-scored styles]``, the constraint matrix ``R`` and solves with a
+    batched ``pinv`` (numpy's rcond=1e-15 semantics), exactly the algebra of
+    ``CrossSection.py:57-106`` minus the dense N x N weight matrix.
+    """
+    D, Q, N = X.shape
+    K = 1 + P + Q
+    fs, es, r2s, stats_l, sts = [], [], [], [], []
+    for a in range(0, D, chunk):
+        b = min(D, a + chunk)
+        Xs = X[a:b].double().transpose(1, 2)  # [d,N,Q]
+        c = cap[a:b].double()
+        r = ret[a:b].double()
+        m = valid_mask(X[a:b], cap[a:b], ret[a:b], ind[a:b] if P > 0 else None, P)
+        mf = m.double()
+        Xs = torch.where(m[..., None], Xs, torch.zeros((), dtype=torch.float64))
+        c = torch.where(m, c, torch.zeros((), dtype=torch.float64))
+        r = torch.where(m, r, torch.zeros((), dtype=torch.float64))
+        n = mf.sum(1)
+        Sc = c.sum(1)
+        mu = (c[..., None] * Xs).sum(1) / Sc[:, None]
+        nq = n * Q
+        mean_all = Xs.sum((1, 2)) / nq
+        sigma = torch.sqrt(torch.clamp((Xs * Xs).sum((1, 2)) / nq - mean_all ** 2, min=0.0))
+        Xz = (Xs - mu[:, None, :]) / sigma[:, None, None] * mf[..., None]
+        cols = [mf[..., None]]
+        status = torch.zeros(b - a, dtype=torch.int32)
+        if P > 0:
+            oh = torch.nn.functional.one_hot(ind[a:b].long().clamp(0, P - 1), P).double() * mf[..., None]
+            cols.append(oh)
+        cols.append(Xz)
+        Xf = torch.cat(cols, dim=2)  # [d,N,K]
+        w = torch.sqrt(c)
+        if P > 0:
+            s = (oh * c[..., None]).sum(1)  # [d,P]
+            if pivot_mode == 1:
+                piv = torch.full((b - a,), P - 1, dtype=torch.long)
+            else:
+                nz = s > 0
+                last = torch.where(nz, torch.arange(P).expand_as(s), torch.full_like(s, -1, dtype=torch.long))
+                piv = last.max(1).values
+                piv = torch.where(piv < 0, torch.full_like(piv, P - 1), piv)
+            sp = s.gather(1, piv[:, None]).squeeze(1)
+            status |= torch.where(sp > 0, 0, XS_PIVOT_EMPTY).int()
+            Rm = torch.eye(K, dtype=torch.float64).repeat(b - a, 1, 1)
+            rows = 1 + piv
+            ratio = -s / sp[:, None]
+            Rm[torch.arange(b - a), rows, 1:1 + P] = ratio
+            keep = torch.ones(b - a, K, dtype=torch.bool)
+            keep[torch.arange(b - a), rows] = False
+            Rm = Rm[keep[:, None, :].expand(-1, K, -1)].view(b - a, K, K - 1)
+            Xt = Xf @ Rm
+        else:
+            Rm = None
+            Xt = Xf
+        A = (Xt * w[..., None]).transpose(1, 2) @ Xt
+        rhs = (Xt * (w * r)[..., None]).sum(1)
+        good = torch.isfinite(A).all(-1).all(-1)
+        Ai = torch.full_like(A, float("nan"))
+        if good.any():
+            Ai[good] = torch.linalg.pinv(A[good], rtol=1e-15, hermitian=False)
+        g = (Ai @ rhs[..., None]).squeeze(-1)
+        f = (Rm @ g[..., None]).squeeze(-1) if Rm is not None else g
+        status |= torch.where(n > 0, 0, XS_NO_ROWS).int()
+        status |= torch.where((sigma > 0) & torch.isfinite(sigma), 0, XS_BAD_SIGMA).int()
+        bad = (status & (XS_NO_ROWS | XS_BAD_SIGMA | XS_PIVOT_EMPTY)) != 0
+        f[bad] = float("nan")
+        fit = (Xf @ f[..., None]).squeeze(-1)
+        e = r - fit
+        e = torch.where(m, e, torch.full_like(e, float("nan")))
+        em = torch.where(m, e, torch.zeros_like(e))
+        ve = (em * em).sum(1) / n - (em.sum(1) / n) ** 2
+        vr = (r * r).sum(1) / n - (r.sum(1) / n) ** 2
+        r2 = 1.0 - ve / vr
+        r2[bad] = float("nan")
+        fs.append(f)
+        es.append(e.float())
+        r2s.append(r2)
+        stats_l.append(torch.cat([mu, sigma[:, None], n[:, None]], 1))
+        sts.append(status)
+    return XsResult(f=torch.cat(fs), resid=torch.cat(es) if want_resid else None,
+                    r2=torch.cat(r2s), stats=torch.cat(stats_l), status=torch.cat(sts))
+
+
+def pure_factor_portfolio(X_d: torch.Tensor, cap_d: torch.Tensor, ind_d: torch.Tensor | None,
+                          P: int, mu: torch.Tensor, sigma: float, pivot: int | None = None):
+    """Pure-factor-portfolio weights ``Omega`` (K x N) and exposures ``Omega X`` for ONE date.
+
+    Only the ``mfm.CrossSection.reg`` compatibility API needs the explicit K x N matrix
+    (``CrossSection.py:76,104``); the batched path never forms it.  Runs with torch ops on
+    whatever device the inputs live on.  ``X_d`` is [Q, N] raw styles of valid rows.
+    """
+    dt = torch.float64
+    Xs = ((X_d.to(dt).T - mu.to(dt)) / sigma)
+    N = Xs.shape[0]
+    c = cap_d.to(dt)
+    cols = [torch.ones(N, 1, dtype=dt, device=Xs.device)]
+    if P > 0:
+        cols.append(torch.nn.functional.one_hot(ind_d.long(), P).to(dt))
+    cols.append(Xs)
+    Xf = torch.cat(cols, 1)
+    K = Xf.shape[1]
+    w = torch.sqrt(c)
+    if P > 0:
+        s = (cols[1] * c[:, None]).sum(0)
+        p = P - 1 if pivot is None else pivot
+        R = torch.eye(K, dtype=dt, device=Xs.device)
+        R[1 + p, 1:1 + P] = -s / s[p]
+        R = torch.cat([R[:, :1 + p], R[:, 2 + p:]], 1)
+        Xt = Xf @ R
+        omega = R @ torch.linalg.pinv((Xt * w[:, None]).T @ Xt, rtol=1e-15) @ (Xt * w[:, None]).T
+    else:
+        omega = torch.linalg.pinv((Xf * w[:, None]).T @ Xf, rtol=1e-15) @ (Xf * w[:, None]).T
+    return omega, omega @ Xf

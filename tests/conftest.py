@@ -1,0 +1,34 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+sys.dont_write_bytecode = True
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (HIP kernels)")
+    config.addinivalue_line("markers", "slow: long-running")
+    config.addinivalue_line("markers", "reference: compares against the read-only reference code")
+
+
+@pytest.fixture(scope="session")
+def cuda():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from llm_driven_multi_factor_model_amd import _native
+    _native.lib()  # fail loudly if the kernel library is missing
+    return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="session")
+def ref():
+    from tests._refshim import load_reference
+    r = load_reference()
+    if r is None:
+        pytest.skip("reference repository not mounted")
+    return r

@@ -1,0 +1,73 @@
+"""Expanding-window Newey-West series: recurrence vs literal reference, HIP scan vs oracle."""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from llm_driven_multi_factor_model_amd.ops import ew_scan
+
+
+def _series(T, K, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    F = torch.randn(T, K, generator=g, dtype=torch.float64) * 0.01
+    F[:, 0] += 0.002  # non-zero mean
+    F[1:] += 0.3 * F[:-1].clone()  # autocorrelation (what NW corrects for)
+    return F
+
+
+@pytest.mark.reference
+@pytest.mark.parametrize("q,tau", [(2, 252.0), (1, 42.0), (0, 90.0)])
+def test_series_matches_reference_newey_west(ref, q, tau):
+    T, K = 40, 6
+    F = _series(T, K)
+    V = ew_scan.newey_west_series(F, q=q, tau=tau)
+    df = pd.DataFrame(F.numpy(), columns=[f"f{k}" for k in range(K)])
+    for t in range(1, T + 1):
+        if t <= q or t <= K:
+            assert torch.isnan(V[t - 1]).all()
+            continue
+        R = ref.utils.Newey_West(df[:t], q, tau).values
+        np.testing.assert_allclose(V[t - 1].numpy(), R, rtol=1e-11, atol=1e-17)
+
+
+def test_single_matches_series_end():
+    F = _series(300, 8, seed=3)
+    V = ew_scan.newey_west_series(F, q=2, tau=60.0)
+    S = ew_scan.newey_west_single(F, q=2, tau=60.0)
+    torch.testing.assert_close(V[-1], S, rtol=1e-10, atol=1e-16)
+
+
+def test_window_slicing_is_consistent():
+    F = _series(120, 5, seed=1)
+    full = ew_scan.newey_west_series(F, q=2, tau=30.0)
+    part = ew_scan.newey_west_series(F, q=2, tau=30.0, t_lo=37, t_hi=90)
+    torch.testing.assert_close(part, full[37:90], equal_nan=True)
+
+
+def test_ew_prefix_mean_reference_semantics():
+    x = torch.tensor([1.0, float("nan"), 3.0, 2.0, float("nan"), 5.0], dtype=torch.float64)
+    out = ew_scan.ew_prefix_mean(x, 2.0)
+    lam = 0.5 ** 0.5
+    # t=3: valid s = 0, 2, 3 with weights lam^3, lam^1, lam^0
+    w = np.array([lam ** 3, lam, 1.0])
+    assert abs(out[3].item() - (w @ np.array([1.0, 3.0, 2.0])) / w.sum()) < 1e-14
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,K,q,tau,lo,hi", [(300, 42, 2, 252.0, 0, 300), (2520, 42, 2, 252.0, 0, 2520),
+                                             (1000, 32, 3, 42.0, 333, 777), (70, 7, 0, 10.0, 0, 70)])
+def test_hip_scan_matches_oracle(cuda, T, K, q, tau, lo, hi):
+    F = _series(T, K, seed=T)
+    ref = ew_scan.newey_west_series_reference(F, q, tau, lo, hi)
+    out = ew_scan.newey_west_series(F.to(cuda), q, tau, lo, hi).cpu()
+    torch.testing.assert_close(out, ref, rtol=1e-9, atol=1e-15, equal_nan=True)
+
+
+@pytest.mark.gpu
+def test_hip_prefix_mean(cuda):
+    g = torch.Generator().manual_seed(0)
+    x = torch.rand(3001, generator=g, dtype=torch.float64)
+    x[::17] = float("nan")
+    ref = ew_scan.ew_prefix_mean_reference(x, 42.0)
+    out = ew_scan.ew_prefix_mean(x.to(cuda), 42.0).cpu()
+    torch.testing.assert_close(out, ref, rtol=1e-11, atol=1e-14)
