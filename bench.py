@@ -39,7 +39,6 @@ def main() -> int:
     ap.add_argument("--stocks", type=int, default=5000)
     ap.add_argument("--industries", type=int, default=31)
     ap.add_argument("--styles", type=int, default=10)
-    ap.add_argument("--waves", type=int, default=0)
     ap.add_argument("--no-resid", action="store_true", help="skip specific-return output (not the headline)")
     ap.add_argument("--check", action="store_true", help="verify a few dates against the fp64 oracle")
     args = ap.parse_args()
@@ -59,7 +58,8 @@ def main() -> int:
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from llm_driven_multi_factor_model_amd.models.panel import synthetic_panel
-    from llm_driven_multi_factor_model_amd.ops.cross_section import xs_wls, xs_wls_reference
+    from llm_driven_multi_factor_model_amd.ops.cross_section import (xs_wls, xs_wls_reference,
+                                                                     xs_wls_workspace)
 
     D, N, P, Q = args.dates, args.stocks, args.industries, args.styles
     K = 1 + P + Q
@@ -67,11 +67,12 @@ def main() -> int:
     gathered = torch.empty(world * D, K, dtype=torch.float64, device=dev)
 
     out = None
+    ws = xs_wls_workspace(D, P, Q, dev) if use_cuda else None
 
     def step():
         nonlocal out
-        out = xs_wls(panel.styles, panel.cap, panel.ret, panel.ind, P, waves=args.waves,
-                     want_resid=not args.no_resid, refine=False, out=out)
+        out = xs_wls(panel.styles, panel.cap, panel.ret, panel.ind, P,
+                     want_resid=not args.no_resid, refine=False, out=out, workspace=ws)
         if world > 1:
             dist.all_gather_into_tensor(gathered, out.f)
         else:

@@ -26,7 +26,9 @@ _vp, _i, _d, _f = C.c_void_p, C.c_int, C.c_double, C.c_float
 # name -> argtypes (all return int hipError_t)
 _SIGS: dict[str, list] = {
     # xs_wls.hip
-    "mfa_xs_wls": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _d, _i, _vp, _vp, _vp, _vp, _vp, _vp],
+    "mfa_xs_wls": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _d, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "mfa_xs_wls_workspace": [_i, _i, _i],
+    "mfa_xs_wls_variant": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
 }
 
 
@@ -40,7 +42,7 @@ def register(name: str, argtypes: list) -> None:
     if _lib is not None:
         fn = getattr(_lib, name)
         fn.argtypes = argtypes
-        fn.restype = C.c_int
+        fn.restype = C.c_size_t if name.endswith("_workspace") or name.endswith("_bytes") else C.c_int
 
 
 def _load() -> C.CDLL:
@@ -59,7 +61,7 @@ def _load() -> C.CDLL:
         for name, argt in _SIGS.items():
             fn = getattr(lib, name)
             fn.argtypes = argt
-            fn.restype = C.c_int
+            fn.restype = C.c_size_t if name.endswith("_workspace") or name.endswith("_bytes") else C.c_int
         _lib = lib
         return lib
 
@@ -80,6 +82,11 @@ def ptr(t: torch.Tensor | None) -> C.c_void_p:
 
 def stream(device: torch.device | None = None) -> C.c_void_p:
     return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def query(name: str, *args) -> int:
+    """Call a size-returning entry point (``*_workspace`` / ``*_bytes``)."""
+    return int(getattr(lib(), name)(*args))
 
 
 def call(name: str, *args) -> None:

@@ -67,7 +67,8 @@ def _validate(X, cap, ret, ind, P):
 
 def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Tensor | None,
            P: int, *, pivot_mode: int = 0, tol: float = 1e-14, want_resid: bool = True,
-           waves: int = 0, refine: bool = True, out: XsResult | None = None) -> XsResult:
+           refine: bool = True, out: XsResult | None = None,
+           workspace: torch.Tensor | None = None) -> XsResult:
     """Regress every date of the panel in one batched call.
 
     X [D,Q,N] f32 styles, cap/ret [D,N] f32, ind [D,N] int16 industry ids (or None if P == 0).
@@ -75,7 +76,9 @@ def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Ten
     reference's choice is valid); 1 reproduces the reference exactly (always the last column,
     NaN when it is empty, quirk Q3).  ``refine`` re-solves dates the kernel flags as
     near-singular with the pseudo-inverse reference path (pinv semantics, quirk Q4).
-    ``out`` lets a caller (e.g. a timed loop) reuse preallocated output buffers.
+    ``out`` / ``workspace`` let a caller (e.g. a timed loop) reuse preallocated buffers.
+    The GPU kernels need N % 8 == 0 (16-byte rows for the LDS-DMA ring); other N are padded
+    here with absent stocks (``ind = -1``), which costs a copy — keep panels padded.
     """
     D, Q, N = _validate(X, cap, ret, ind, P)
     K = 1 + P + Q
@@ -87,6 +90,14 @@ def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Ten
     ret = _native.check_device_tensor(ret, torch.float32, "ret")
     if P > 0:
         ind = _native.check_device_tensor(ind, torch.int16, "ind")
+    Np = (N + 7) // 8 * 8
+    if Np != N:
+        pad = Np - N
+        X = torch.nn.functional.pad(X, (0, pad), value=float("nan"))
+        cap = torch.nn.functional.pad(cap, (0, pad), value=float("nan"))
+        ret = torch.nn.functional.pad(ret, (0, pad), value=float("nan"))
+        if P > 0:
+            ind = torch.nn.functional.pad(ind, (0, pad), value=-1)
     if out is None:
         out = XsResult(
             f=torch.empty(D, K, dtype=torch.float64, device=dev),
@@ -95,13 +106,29 @@ def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Ten
             stats=torch.empty(D, Q + 2, dtype=torch.float64, device=dev),
             status=torch.empty(D, dtype=torch.int32, device=dev),
         )
+    resid_buf = out.resid
+    if resid_buf is not None and Np != N:
+        resid_buf = torch.empty(D, Np, dtype=torch.float32, device=dev)
+    need = _native.query("mfa_xs_wls_workspace", D, P, Q)
+    if workspace is None or workspace.numel() < need:
+        workspace = torch.empty(need, dtype=torch.uint8, device=dev)
     _native.call("mfa_xs_wls", _native.ptr(X), _native.ptr(cap), _native.ptr(ret),
-                 _native.ptr(ind if P > 0 else None), D, N, P, Q, pivot_mode, tol, waves,
-                 _native.ptr(out.f), _native.ptr(out.resid), _native.ptr(out.r2),
-                 _native.ptr(out.stats), _native.ptr(out.status), _native.stream(dev))
+                 _native.ptr(ind if P > 0 else None), D, Np, P, Q, pivot_mode, tol,
+                 _native.ptr(out.f), _native.ptr(resid_buf), _native.ptr(out.r2),
+                 _native.ptr(out.stats), _native.ptr(out.status), _native.ptr(workspace),
+                 _native.stream(dev))
+    if resid_buf is not None and Np != N:
+        out.resid.copy_(resid_buf[:, :N])
     if refine:
-        _refine_near_singular(X, cap, ret, ind, P, pivot_mode, out)
+        _refine_near_singular(X[..., :N], cap[:, :N], ret[:, :N], ind[:, :N] if P > 0 else None,
+                              P, pivot_mode, out)
     return out
+
+
+def xs_wls_workspace(D: int, P: int, Q: int, device) -> torch.Tensor:
+    """Preallocated kernel workspace for repeated :func:`xs_wls` calls on the same shapes."""
+    return torch.empty(_native.query("mfa_xs_wls_workspace", D, P, Q), dtype=torch.uint8,
+                       device=device)
 
 
 def _refine_near_singular(X, cap, ret, ind, P, pivot_mode, out: XsResult) -> None:

@@ -25,9 +25,7 @@ _native.register("mfa_nw_workspace_bytes", [C.c_int, C.c_int, C.c_int])
 
 
 def _ws_bytes(T: int, K: int, q: int) -> int:
-    fn = _native.lib().mfa_nw_workspace_bytes
-    fn.restype = C.c_size_t
-    return int(fn(T, K, q))
+    return _native.query("mfa_nw_workspace_bytes", T, K, q)
 
 
 def newey_west_series(F: torch.Tensor, q: int = 2, tau: float = 252.0, t_lo: int = 0,

@@ -70,4 +70,4 @@ def test_hip_prefix_mean(cuda):
     x[::17] = float("nan")
     ref = ew_scan.ew_prefix_mean_reference(x, 42.0)
     out = ew_scan.ew_prefix_mean(x.to(cuda), 42.0).cpu()
-    torch.testing.assert_close(out, ref, rtol=1e-11, atol=1e-14)
+    torch.testing.assert_close(out, ref, rtol=1e-11, atol=1e-14, equal_nan=True)

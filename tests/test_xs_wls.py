@@ -91,19 +91,20 @@ def test_last_industry_empty_pivot_modes():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("D,N,P,Q,miss,empty,waves", [
-    (7, 300, 31, 10, 0.0, 0, 0),
-    (5, 5000, 31, 10, 0.02, 2, 4),
-    (9, 777, 12, 3, 0.1, 3, 1),
-    (6, 200, 0, 4, 0.05, 0, 2),
-    (4, 1000, 28, 16, 0.0, 1, 0),
-    (3, 64, 3, 1, 0.0, 0, 1),
+@pytest.mark.parametrize("D,N,P,Q,miss,empty", [
+    (7, 300, 31, 10, 0.0, 0),
+    (5, 5000, 31, 10, 0.02, 2),
+    (9, 777, 12, 3, 0.1, 3),
+    (6, 200, 0, 4, 0.05, 0),
+    (4, 1000, 28, 16, 0.0, 1),
+    (3, 64, 3, 1, 0.0, 0),
+    (5, 600, 100, 8, 0.01, 2),
 ])
-def test_kernel_matches_oracle(cuda, D, N, P, Q, miss, empty, waves):
+def test_kernel_matches_oracle(cuda, D, N, P, Q, miss, empty):
     panel = synthetic_panel(D, N, P, Q, seed=D + N, missing_frac=miss, empty_industries=empty)
     ref = X.xs_wls_reference(panel.styles, panel.cap, panel.ret, panel.ind, P)
     g = panel.to(cuda)
-    out = X.xs_wls(g.styles, g.cap, g.ret, g.ind, P, waves=waves)
+    out = X.xs_wls(g.styles, g.cap, g.ret, g.ind, P)
     torch.cuda.synchronize()
     torch.testing.assert_close(out.f.cpu(), ref.f, rtol=1e-8, atol=1e-11)
     torch.testing.assert_close(out.r2.cpu(), ref.r2, rtol=1e-9, atol=1e-11)
