@@ -38,7 +38,7 @@ def _flags() -> list[str]:
     return [
         f"--offload-arch={ARCH}",
         "-O3",
-        "-std=c++17",
+        "-std=c++20",
         "-fPIC",
         "-ffp-contract=fast",
         "-munsafe-fp-atomics",

@@ -22,6 +22,8 @@
 //                   reverse order so the tail of K1's stream is still Infinity-Cache resident.
 #include "common.h"
 
+#include <utility>
+
 namespace {
 
 using namespace mfa;
@@ -48,9 +50,17 @@ __device__ __forceinline__ void lds_add(double* p, double v) {
 // LDS-DMA tile) before any compiler-visible LDS write while a global_load_lds is pending.  The
 // segment tables never alias the DMA ring, so the atomic is hidden from that analysis.  LDS ops
 // complete in order, so the compiler's own lgkmcnt waits stay correct; barriers drain these.
-__device__ __forceinline__ void lds_add_nowait(double* p, double v) {
-  const unsigned a = (unsigned)(uintptr_t)(__attribute__((address_space(3))) double*)p;
-  asm volatile("ds_add_f64 %0, %1" ::"v"(a), "v"(v) : "memory");
+template <int OFF>
+__device__ __forceinline__ void lds_add_nowait(unsigned lds_addr, double v) {
+  asm volatile("ds_add_f64 %0, %1 offset:%2" ::"v"(lds_addr), "v"(v), "i"(OFF) : "memory");
+}
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(__attribute__((address_space(3))) const void*)p;
+}
+
+// 4-byte async global -> LDS copy (one fp32 per lane: a 64-stock row per wave instruction).
+__device__ __forceinline__ void glds4(const void* src, void* wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)wave_base, 4, 0, 0);
 }
 
 // 16-byte async global -> LDS copy; LDS destination = wave-uniform `wave_base` + lane * 16.
@@ -63,7 +73,12 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
 #define MFA_W(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
     MFA_W(1) MFA_W(2) MFA_W(3) MFA_W(4) MFA_W(5) MFA_W(6) MFA_W(7) MFA_W(8) MFA_W(9)
     MFA_W(10) MFA_W(11) MFA_W(12) MFA_W(13) MFA_W(14) MFA_W(15) MFA_W(16) MFA_W(17)
-    MFA_W(18) MFA_W(19) MFA_W(20)
+    MFA_W(18) MFA_W(19) MFA_W(20) MFA_W(21) MFA_W(22) MFA_W(23) MFA_W(24) MFA_W(25)
+    MFA_W(26) MFA_W(27) MFA_W(28) MFA_W(29) MFA_W(30) MFA_W(31) MFA_W(32) MFA_W(33)
+    MFA_W(34) MFA_W(35) MFA_W(36) MFA_W(37) MFA_W(38) MFA_W(39) MFA_W(40) MFA_W(41)
+    MFA_W(42) MFA_W(43) MFA_W(44) MFA_W(45) MFA_W(46) MFA_W(47) MFA_W(48) MFA_W(49)
+    MFA_W(50) MFA_W(51) MFA_W(52) MFA_W(53) MFA_W(54) MFA_W(55) MFA_W(56) MFA_W(57)
+    MFA_W(58) MFA_W(59) MFA_W(60) MFA_W(61) MFA_W(62) MFA_W(63)
 #undef MFA_W
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
@@ -89,9 +104,11 @@ __device__ __forceinline__ double pick(const double (&a)[Q], int i) {
   return r;
 }
 
-constexpr int kTile = 256;            // stocks per staged tile
+constexpr int kTile = 256;            // stocks per staged tile (K3)
 constexpr int kRowBytes = kTile * 4;  // one fp32 field row of a tile
 constexpr int kRep = 4;               // segment-table replicas (lane & 3)
+constexpr int kWT = 64;               // stocks per wave tile (K1: one stock per lane)
+constexpr int kWNB = 4;               // K1 per-wave ring depth
 
 template <int Q>
 struct Layout {
@@ -100,6 +117,7 @@ struct Layout {
   static constexpr int NACC = NG + 2 * Q + 4;  // Swxx | Swxr | Scx | Sc Sx Sxx n
   static constexpr int ND = Q + 1;             // dense block: country + styles
   static constexpr int BUF = (Q + 2) * kRowBytes + kTile * 2;  // one ring slot
+  static constexpr int WSLOT = (Q + 2) * kWT * 4 + kWT * 2;    // K1 per-wave ring slot
   __host__ __device__ static constexpr int msize(int Pseg) { return NACC + Pseg * NS; }
 };
 
@@ -135,16 +153,18 @@ __global__ __launch_bounds__(256) void xs_moments_kernel(
     const int16_t* __restrict__ ind, int N, int Pseg, double* __restrict__ mom) {
   using L = Layout<Q>;
   constexpr int NS = L::NS, NG = L::NG, NACC = L::NACC, BUF = L::BUF, NBUF = 3;
-  // the DMA ring is its own __shared__ object, separate from the atomics' dynamic LDS
-  // (also hosts the 4 per-wave [8][65] fp64 reduction tiles once streaming is done)
-  constexpr int RING = NBUF * BUF > 4 * 8 * 65 * 8 ? NBUF * BUF : 4 * 8 * 65 * 8;
-  __shared__ __attribute__((aligned(16))) char ring[RING];
+  // Per-wave DMA rings (own __shared__ object, separate from the atomics' dynamic LDS): each
+  // wave streams its own 64-stock tiles (k = wid, wid + nw, ...) with no workgroup barrier until
+  // the final reduction, so the 8 waves of a CU drift and overlap HBM, VALU and LDS phases.
+  constexpr int WSLOT = L::WSLOT;
+  constexpr int RINGW = kWNB * WSLOT > 8 * 65 * 8 ? kWNB * WSLOT : 8 * 65 * 8;
+  __shared__ __attribute__((aligned(16))) char ring[4 * RINGW];
   extern __shared__ double dyn[];  // [kRep][Pseg*NS + 1] replicas | [NACC] totals
   const int d = blockIdx.x;
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int lane = tid & 63, wid = tid >> 6, nw = nthr >> 6;
   const int rstride = Pseg * NS + 1;  // odd stride spreads the replicas over banks
-  double* seg = dyn + (lane & (kRep - 1)) * rstride;
+  const unsigned seg_a = lds_addr(dyn + (lane & (kRep - 1)) * rstride);
   double* acc = dyn + kRep * rstride;
   for (int i = tid; i < kRep * rstride + NACC; i += nthr) dyn[i] = 0.0;
   __syncthreads();
@@ -158,40 +178,39 @@ __global__ __launch_bounds__(256) void xs_moments_kernel(
 #pragma unroll
   for (int i = 0; i < NACC; ++i) v[i] = 0.0;
 
-  const int NROWS = id ? Q + 3 : Q + 2;
-  const int ntile = (N + kTile - 1) / kTile;
-  const int my_rows = wid < NROWS ? (NROWS - wid + nw - 1) / nw : 0;
-  auto issue = [&](int k) {  // wave wid stages rows wid, wid+nw, ... of tile k
-    char* buf = ring + (k % NBUF) * BUF;
-    const int s0 = k * kTile;
-    for (int r = wid; r < NROWS; r += nw) {
-      if (r < Q + 2) {
-        const float* row = r == 0 ? cd : (r == 1 ? rd : Xd + (size_t)(r - 2) * N);
-        if (s0 + lane * 4 < N) glds16(row + s0 + lane * 4, buf + r * kRowBytes);
-      } else if (lane < kTile / 8 && s0 + lane * 8 < N) {
-        glds16(id + s0 + lane * 8, buf + (Q + 2) * kRowBytes);
-      }
-    }
+  char* wring = ring + wid * RINGW;
+  const int nrows = id ? Q + 3 : Q + 2;        // glds instructions per tile
+  const int ntile_all = (N + kWT - 1) / kWT;
+  const int ntile = ntile_all > wid ? (ntile_all - wid + nw - 1) / nw : 0;  // this wave's tiles
+  auto issue = [&](int i) {
+    char* slot = wring + (i % kWNB) * WSLOT;
+    const int s0 = (wid + i * nw) * kWT;
+    const bool in = s0 + lane < N;
+    if (in) glds4(cd + s0 + lane, slot);
+    if (in) glds4(rd + s0 + lane, slot + kWT * 4);
+#pragma unroll
+    for (int q = 0; q < Q; ++q)
+      if (in) glds4(Xd + (size_t)q * N + s0 + lane, slot + (2 + q) * kWT * 4);
+    if (id && lane < kWT / 2 && s0 + 2 * lane < N) glds4(id + s0 + 2 * lane, slot + (Q + 2) * kWT * 4);
   };
-  for (int k = 0; k < NBUF - 1 && k < ntile; ++k) issue(k);
-  for (int k = 0; k < ntile; ++k) {
-    const bool tail = (k + NBUF - 1 >= ntile);  // partial last tile in flight: wait exactly
-    wait_vmcnt(tail ? 0 : (NBUF - 2) * my_rows);
-    raw_barrier();  // tile k visible to all waves; slot (k-1)%NBUF free for reuse
-    if (k + NBUF - 1 < ntile) issue(k + NBUF - 1);
-    const char* buf = ring + (k % NBUF) * BUF;
-    const float* bf = (const float*)buf;
-    const int16_t* bi = (const int16_t*)(buf + (Q + 2) * kRowBytes);
-    for (int t = tid; t < kTile && k * kTile + t < N; t += nthr) {
-      const float cf = bf[t], rf = bf[kTile + t];
-      const int j = id ? (int)bi[t] : 0;
-      float xf[Q];
+  for (int i = 0; i < kWNB - 1 && i < ntile; ++i) issue(i);
+  for (int i = 0; i < ntile; ++i) {
+    const bool tail = (i + kWNB - 1 >= ntile);
+    wait_vmcnt(tail ? 0 : (kWNB - 2) * nrows);
+    __builtin_amdgcn_wave_barrier();
+    if (i + kWNB - 1 < ntile) issue(i + kWNB - 1);
+    const char* slot = wring + (i % kWNB) * WSLOT;
+    const float* bf = (const float*)slot;
+    const int s = (wid + i * nw) * kWT + lane;
+    const float cf = bf[lane], rf = bf[kWT + lane];
+    const int j = id ? (int)((const int16_t*)(slot + (Q + 2) * kWT * 4))[lane] : 0;
+    float xf[Q];
 #pragma unroll
-      for (int q = 0; q < Q; ++q) xf[q] = bf[(2 + q) * kTile + t];
-      bool ok = (j >= 0) && (j < Pseg) && finite_f(cf) && (cf >= 0.f) && finite_f(rf);
+    for (int q = 0; q < Q; ++q) xf[q] = bf[(2 + q) * kWT + lane];
+    bool ok = (s < N) && (j >= 0) && (j < Pseg) && finite_f(cf) && (cf >= 0.f) && finite_f(rf);
 #pragma unroll
-      for (int q = 0; q < Q; ++q) ok = ok && finite_f(xf[q]);
-      if (!ok) continue;
+    for (int q = 0; q < Q; ++q) ok = ok && finite_f(xf[q]);
+    if (ok) {
       const double c = cf, r = rf, w = sqrt(c);
       double x[Q], wx[Q];
 #pragma unroll
@@ -199,7 +218,7 @@ __global__ __launch_bounds__(256) void xs_moments_kernel(
 #pragma unroll
       for (int q = 0; q < Q; ++q)
 #pragma unroll
-        for (int s = 0; s <= q; ++s) v[q * (q + 1) / 2 + s] = fma(wx[q], x[s], v[q * (q + 1) / 2 + s]);
+        for (int t = 0; t <= q; ++t) v[q * (q + 1) / 2 + t] = fma(wx[q], x[t], v[q * (q + 1) / 2 + t]);
       double sx = 0.0, sxx = 0.0;
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
@@ -214,19 +233,20 @@ __global__ __launch_bounds__(256) void xs_moments_kernel(
       v[NG + 2 * Q + 3] += 1.0;
       if (VAR & 1) {  // timing-only ablation: skip the segment atomics
         asm volatile("" ::"v"(w), "v"(r));
-        continue;
+      } else {
+        const unsigned a = seg_a + (unsigned)(j * NS * 8);
+        lds_add_nowait<0>(a, w);
+        [&]<int... I>(std::integer_sequence<int, I...>) {
+          (lds_add_nowait<8 * (1 + I)>(a, wx[I]), ...);
+        }(std::make_integer_sequence<int, Q>{});
+        lds_add_nowait<8 * (Q + 1)>(a, w * r);
+        lds_add_nowait<8 * (Q + 2)>(a, c);
       }
-      double* sj = seg + j * NS;
-      lds_add_nowait(sj + 0, w);
-#pragma unroll
-      for (int q = 0; q < Q; ++q) lds_add_nowait(sj + 1 + q, wx[q]);
-      lds_add_nowait(sj + Q + 1, w * r);
-      lds_add_nowait(sj + Q + 2, c);
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  raw_barrier();
-  wg_reduce<NACC>(v, (double*)ring + wid * 8 * 65, acc);
+  __syncthreads();
+  wg_reduce<NACC>(v, (double*)wring, acc);
   __syncthreads();
   double* md = mom + (size_t)d * L::msize(Pseg);
   for (int i = tid; i < NACC; i += nthr) md[i] = acc[i];
@@ -263,7 +283,19 @@ __global__ __launch_bounds__(64) void xs_solve_kernel(const double* __restrict__
   double* fsh = S + ND * (ND + 1);    // [K]
   double* Yb = fsh + K;               // [Pseg][ND+1] M_II^{-1} [M_ID | h_I]
   const double* md = mom + (size_t)d * MS;
-  for (int i = lane; i < MS; i += 64) sm[i] = md[i];
+  for (int i0 = 0; i0 < MS; i0 += 8 * 64) {  // 8 independent loads in flight per lane
+    double tmp[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * 64 + lane;
+      tmp[u] = i < MS ? md[i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * 64 + lane;
+      if (i < MS) sm[i] = tmp[u];
+    }
+  }
   wave_sync_lds();
 
   const double Sc = acc[NG + 2 * Q + 0];
@@ -382,9 +414,16 @@ __global__ __launch_bounds__(64) void xs_solve_kernel(const double* __restrict__
       m = (acc[hi * (hi + 1) / 2 + lo] - muq * pick<Q>(Swx, s) - mus * pick<Q>(Swx, q) +
            muq * mus * Sw) * isig * isig;
     }
-    double t = 0.0;
-    for (int j = 0; j < P; ++j) t = fma(MID[j * (ND + 1) + u], Yb[j * (ND + 1) + w], t);
-    S[e] = m - t;
+    double t0 = 0.0, t1 = 0.0, t2 = 0.0, t3 = 0.0;
+    int j = 0;
+    for (; j + 4 <= P; j += 4) {
+      t0 = fma(MID[(j + 0) * (ND + 1) + u], Yb[(j + 0) * (ND + 1) + w], t0);
+      t1 = fma(MID[(j + 1) * (ND + 1) + u], Yb[(j + 1) * (ND + 1) + w], t1);
+      t2 = fma(MID[(j + 2) * (ND + 1) + u], Yb[(j + 2) * (ND + 1) + w], t2);
+      t3 = fma(MID[(j + 3) * (ND + 1) + u], Yb[(j + 3) * (ND + 1) + w], t3);
+    }
+    for (; j < P; ++j) t0 = fma(MID[j * (ND + 1) + u], Yb[j * (ND + 1) + w], t0);
+    S[e] = m - ((t0 + t1) + (t2 + t3));
   }
   wave_sync_lds();
 
@@ -567,7 +606,8 @@ hipError_t launch_q(const float* X, const float* cap, const float* ret, const in
   const size_t lds1 = ((size_t)kRep * (Pseg * L::NS + 1) + L::NACC) * sizeof(double);
   const size_t lds2 = ((size_t)L::msize(Pseg) + (size_t)Pseg * (L::ND + 1) * 2 +
                        L::ND * (L::ND + 1) + K) * sizeof(double);
-  if (lds1 + 3 * (size_t)L::BUF + 16640 > 160 * 1024 || lds2 > 64 * 1024) return hipErrorInvalidValue;
+  if (lds1 + 4 * (size_t)kWNB * L::WSLOT + 16640 > 160 * 1024 || lds2 > 64 * 1024)
+    return hipErrorInvalidValue;
   hipLaunchKernelGGL((xs_moments_kernel<Q, VAR>), dim3(D), dim3(256), lds1, s, X, cap, ret,
                      P > 0 ? ind : nullptr, N, Pseg, mom);
   hipLaunchKernelGGL(xs_solve_kernel<Q>, dim3(D), dim3(64), lds2, s, mom, P, Pseg, pivot_mode,
