@@ -1,0 +1,135 @@
+"""Batched symmetric eigensolver and Monte-Carlo eigenfactor risk adjustment.
+
+Reference: ``Barra-master/mfm/utils.py:55-92`` (``eigen_risk_adj``) applied per date by
+``MFM.eigen_risk_adj_by_time`` (``MFM.py:105-126``).  GPU path: ``csrc/eigen.hip``.
+
+Semantics kept from the reference:
+
+* the simulation length defaults to the TOTAL number of dates for every date (quirk Q9);
+* the same M draws are used for every date (``np.random.seed(m+1)``, quirk Q8) — here the
+  draw covariances ``cov(z_m)`` come from a counter-based Philox stream keyed by ``(seed, m)``;
+* a date whose covariance has a negative eigenvalue (or is NaN) yields NaN (the reference
+  raises inside a bare ``except`` and stores an empty frame, quirk Q7/Q12).
+
+Deliberate difference (documented, statistical parity only): eigenpairs are paired by
+descending eigenvalue rank (the reference pairs by ``np.linalg.eig``'s unspecified order), and
+the normals come from Philox rather than MT19937 (bitwise parity with numpy is impossible).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import torch
+
+from .. import _native
+
+_native.register("mfa_eigh_batched", [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_double,
+                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p])
+_native.register("mfa_mc_cov", [C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_void_p, C.c_void_p])
+_native.register("mfa_eigen_adjust", [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                       C.c_int, C.c_void_p, C.c_double, C.c_int, C.c_double,
+                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p])
+
+MAX_SWEEPS = 30
+TOL = 1e-15
+
+
+def eigh(A: torch.Tensor, max_sweeps: int = MAX_SWEEPS, tol: float = TOL):
+    """Batched symmetric eigendecomposition, eigenvalues DESCENDING.
+
+    ``A`` [..., K, K] float64 (K <= 64 on the GPU).  Returns ``(w [..., K], U [..., K, K])``
+    with ``A = U diag(w) U^T`` and ``U[..., :, k]`` the k-th eigenvector.  Non-finite input
+    matrices give NaN outputs.
+    """
+    A = A.to(torch.float64)
+    shp = A.shape
+    K = shp[-1]
+    Ab = A.reshape(-1, K, K).contiguous()
+    if not A.is_cuda:
+        return _eigh_reference(Ab, shp)
+    B = Ab.shape[0]
+    w = torch.empty(B, K, dtype=torch.float64, device=A.device)
+    U = torch.empty(B, K, K, dtype=torch.float64, device=A.device)
+    _native.call("mfa_eigh_batched", _native.ptr(Ab), B, K, max_sweeps, tol, _native.ptr(w),
+                 _native.ptr(U), _native.ptr(None), _native.stream(A.device))
+    return w.reshape(shp[:-1]), U.reshape(shp)
+
+
+def _eigh_reference(Ab, shp):
+    K = Ab.shape[-1]
+    ok = torch.isfinite(Ab).all(-1).all(-1)
+    w = torch.full(Ab.shape[:-1], float("nan"), dtype=torch.float64)
+    U = torch.full(Ab.shape, float("nan"), dtype=torch.float64)
+    if ok.any():
+        S = 0.5 * (Ab[ok] + Ab[ok].transpose(-1, -2))
+        ww, UU = torch.linalg.eigh(S)
+        w[ok] = ww.flip(-1)
+        U[ok] = UU.flip(-1)
+    return w.reshape(shp[:-1]), U.reshape(shp)
+
+
+def mc_cov(M: int, K: int, T: int, seed: int = 1, device="cuda") -> torch.Tensor:
+    """Draw covariances ``cov(z_m)`` (ddof 1) of M independent [T x K] standard-normal panels."""
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        g = torch.Generator().manual_seed(int(seed))
+        Cz = torch.empty(M, K, K, dtype=torch.float64)
+        for m in range(M):
+            z = torch.randn(T, K, generator=g, dtype=torch.float64)
+            Cz[m] = torch.cov(z.T)
+        return Cz
+    Cz = torch.empty(M, K, K, dtype=torch.float64, device=dev)
+    _native.call("mfa_mc_cov", M, K, T, int(seed) & 0xFFFFFFFFFFFFFFFF, _native.ptr(Cz),
+                 _native.stream(dev))
+    return Cz
+
+
+def eigen_risk_adjust(F0: torch.Tensor, *, M: int = 100, scale_coef: float = 1.4,
+                      T_sim: int | None = None, seed: int = 1, Cz: torch.Tensor | None = None,
+                      psd_tol: float = 0.0, return_bias: bool = False):
+    """Eigenfactor risk adjustment of a batch of covariance matrices.
+
+    ``F0`` [D, K, K] float64 (NaN matrices allowed -> NaN outputs).  ``T_sim`` defaults to D
+    (the reference passes the total number of dates for every date, quirk Q9).  ``Cz`` may be
+    supplied to share draw covariances between calls (and between CPU and GPU for testing).
+    Returns ``F_hat`` [D, K, K] (and the bias multipliers ``v`` [D, K] if ``return_bias``).
+    """
+    F0 = F0.to(torch.float64).contiguous()
+    D, K, _ = F0.shape
+    T_sim = D if T_sim is None else T_sim
+    dev = F0.device
+    w, U = eigh(F0)
+    valid = torch.isfinite(w).all(-1) & (w.min(-1).values >= -psd_tol * w.abs().max(-1).values.clamp_min(0))
+    w = torch.where(valid[:, None], w.clamp_min(0.0), w)
+    if Cz is None:
+        Cz = mc_cov(M, K, max(T_sim, 2), seed, dev)
+    Cz = Cz.to(device=dev, dtype=torch.float64).contiguous()
+    M = Cz.shape[0]
+    if dev.type != "cuda":
+        return _eigen_adjust_reference(w, U, valid, Cz, scale_coef, return_bias)
+    Fh = torch.empty(D, K, K, dtype=torch.float64, device=dev)
+    vb = torch.empty(D, K, dtype=torch.float64, device=dev)
+    ws = torch.empty(D * M * K, dtype=torch.float64, device=dev)
+    dv = valid.to(torch.int32).contiguous()
+    _native.call("mfa_eigen_adjust", _native.ptr(w.contiguous()), _native.ptr(U.contiguous()),
+                 _native.ptr(dv), D, K, M, _native.ptr(Cz), float(scale_coef), MAX_SWEEPS, TOL,
+                 _native.ptr(ws), _native.ptr(Fh), _native.ptr(vb), _native.stream(dev))
+    return (Fh, vb) if return_bias else Fh
+
+
+def _eigen_adjust_reference(w, U, valid, Cz, scale_coef, return_bias):
+    D, K = w.shape
+    M = Cz.shape[0]
+    Fh = torch.full((D, K, K), float("nan"), dtype=torch.float64)
+    vb = torch.full((D, K), float("nan"), dtype=torch.float64)
+    for d in torch.nonzero(valid).flatten().tolist():
+        s = torch.sqrt(w[d])
+        Cb = s[None, :, None] * Cz * s[None, None, :]          # [M, K, K]
+        lam, V = torch.linalg.eigh(Cb)
+        lam, V = lam.flip(-1), V.flip(-1)                       # descending
+        vm = ((V * V) * w[d][None, :, None]).sum(1) / lam       # [M, K]
+        v = torch.sqrt(vm.mean(0))
+        v = scale_coef * (v - 1.0) + 1.0
+        vb[d] = v
+        Fh[d] = (U[d] * (v * v * w[d])) @ U[d].T
+    return (Fh, vb) if return_bias else Fh

@@ -1,0 +1,115 @@
+"""Date-sharded data parallelism (one process per GPU, RCCL over xGMI via torch.distributed).
+
+The reference is single-process Python.  Here every cross-sectional stage is
+independent per date, so rank r owns a contiguous block of dates; time-axis stages (Newey-West,
+VRA) need the full factor-return series, which is one ``all_gather`` per stage (a few hundred
+KB: latency-bound on xGMI, so the rule is ONE batched collective per stage, never per date).
+
+Collective call sites:
+  C3 factor-return series      all_gather   (D_local x K fp64)
+  C6 VRA bias series           all_gather   (D_local fp64)
+  C7 outputs to rank 0         gather       (only when writing CSVs)
+  C8 benchmark fences          barrier
+Backend ``nccl`` is RCCL on ROCm builds; ``gloo`` serves CPU tests.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import torch
+import torch.distributed as dist
+
+
+@dataclass
+class DistContext:
+    rank: int = 0
+    world: int = 1
+    local_rank: int = 0
+    device: torch.device = torch.device("cpu")
+    backend: str | None = None
+
+    @property
+    def enabled(self) -> bool:
+        return self.world > 1 and dist.is_available() and dist.is_initialized()
+
+
+_CTX: DistContext | None = None
+
+
+def init_distributed(backend: str | None = None, device: str | None = None) -> DistContext:
+    """Initialise from torchrun env vars (RANK/WORLD_SIZE/LOCAL_RANK/MASTER_*)."""
+    global _CTX
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    use_cuda = torch.cuda.is_available() and device != "cpu"
+    dev = torch.device(f"cuda:{local}") if use_cuda else torch.device("cpu")
+    if use_cuda:
+        torch.cuda.set_device(dev)
+    be = backend or ("nccl" if use_cuda else "gloo")
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        kw = {"device_id": dev} if use_cuda else {}
+        dist.init_process_group(be, rank=rank, world_size=world, **kw)
+    _CTX = DistContext(rank, world, local, dev, be if world > 1 else None)
+    return _CTX
+
+
+def context() -> DistContext:
+    if _CTX is not None:
+        return _CTX
+    if dist.is_available() and dist.is_initialized():
+        r, w = dist.get_rank(), dist.get_world_size()
+        dev = torch.device(f"cuda:{torch.cuda.current_device()}") if torch.cuda.is_available() \
+            and dist.get_backend() == "nccl" else torch.device("cpu")
+        return DistContext(r, w, int(os.environ.get("LOCAL_RANK", "0")), dev, dist.get_backend())
+    return DistContext()
+
+
+def shard_range(D: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous, balanced date block [a, b) of rank ``rank``."""
+    base, rem = divmod(D, world)
+    a = rank * base + min(rank, rem)
+    return a, a + base + (1 if rank < rem else 0)
+
+
+def all_gather_rows(x: torch.Tensor, ctx: DistContext | None = None) -> torch.Tensor:
+    """Concatenate every rank's leading-dim block in rank order (blocks may differ in size)."""
+    ctx = ctx or context()
+    if not ctx.enabled:
+        return x
+    n = torch.tensor([x.shape[0]], dtype=torch.int64, device=x.device)
+    sizes = [torch.zeros_like(n) for _ in range(ctx.world)]
+    dist.all_gather(sizes, n)
+    sizes = [int(s.item()) for s in sizes]
+    mx = max(sizes)
+    pad = torch.zeros((mx - x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    xp = torch.cat([x, pad]) if mx > x.shape[0] else x.contiguous()
+    out = torch.empty((ctx.world * mx,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, xp)
+    return torch.cat([out[r * mx:r * mx + sizes[r]] for r in range(ctx.world)])
+
+
+def gather_to_root(x: torch.Tensor, ctx: DistContext | None = None) -> torch.Tensor | None:
+    """Rows of every rank concatenated on rank 0 (None elsewhere)."""
+    ctx = ctx or context()
+    if not ctx.enabled:
+        return x
+    full = all_gather_rows(x, ctx)
+    return full if ctx.rank == 0 else None
+
+
+def all_reduce_max(x: float, ctx: DistContext | None = None, device=None) -> float:
+    ctx = ctx or context()
+    if not ctx.enabled:
+        return x
+    t = torch.tensor([x], dtype=torch.float64, device=device or ctx.device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def barrier(ctx: DistContext | None = None) -> None:
+    ctx = ctx or context()
+    if ctx.enabled:
+        dist.barrier()

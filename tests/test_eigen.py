@@ -1,0 +1,95 @@
+"""Batched Jacobi eigh, MC draw covariances and the eigenfactor risk adjustment."""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from llm_driven_multi_factor_model_amd.ops import eigen
+
+
+def _spd(B, K, seed=0, spread=3.0):
+    g = torch.Generator().manual_seed(seed)
+    Q, _ = torch.linalg.qr(torch.randn(B, K, K, generator=g, dtype=torch.float64))
+    lam = torch.exp(torch.linspace(0, -spread * 2.3, K, dtype=torch.float64))[None] * \
+        (1 + 0.1 * torch.rand(B, K, generator=g, dtype=torch.float64))
+    return (Q * lam[:, None, :]) @ Q.transpose(1, 2)
+
+
+def test_eigh_reference_descending():
+    A = _spd(3, 6)
+    w, U = eigen.eigh(A)
+    assert (w[:, :-1] >= w[:, 1:]).all()
+    torch.testing.assert_close((U * w[:, None, :]) @ U.transpose(1, 2), A, rtol=1e-10, atol=1e-14)
+
+
+def test_eigen_adjust_cpu_shapes_and_nan():
+    F = _spd(4, 5, seed=2) * 1e-4
+    F[1] = float("nan")
+    Cz = eigen.mc_cov(20, 5, 200, seed=3, device="cpu")
+    Fh, v = eigen.eigen_risk_adjust(F, Cz=Cz, return_bias=True)
+    assert torch.isnan(Fh[1]).all() and torch.isfinite(Fh[[0, 2, 3]]).all()
+    # the adjustment only rescales eigenvalues: eigenvectors of F and F_hat coincide
+    w0, U0 = eigen.eigh(F[0])
+    w1, U1 = eigen.eigh(Fh[0])
+    assert torch.allclose((U0.T @ Fh[0] @ U0).diagonal(), (v[0] ** 2) * w0, rtol=1e-9)
+
+
+@pytest.mark.reference
+def test_eigen_adjust_statistical_parity_with_reference(ref):
+    K, T, M = 5, 400, 300
+    F = _spd(1, K, seed=5, spread=1.5)[0] * 1e-4
+    df = pd.DataFrame(F.numpy(), columns=list("abcde"), index=list("abcde"))
+    R = ref.utils.eigen_risk_adj(df, T=T, M=M, scale_coef=1.4).values
+    Cz = eigen.mc_cov(M, K, T, seed=11, device="cpu")
+    Fh = eigen.eigen_risk_adjust(F[None], Cz=Cz, scale_coef=1.4)[0].numpy()
+    w0 = np.linalg.eigvalsh(F.numpy())[::-1]
+    wr = np.linalg.eigvalsh(R)[::-1]
+    wo = np.linalg.eigvalsh(Fh)[::-1]
+    # multipliers v^2 agree within Monte-Carlo noise (both > 1 for the small eigenvalues)
+    np.testing.assert_allclose(wo / w0, wr / w0, rtol=0.03)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K,B", [(42, 50), (7, 10), (64, 5), (1, 3), (33, 9)])
+def test_hip_eigh_matches_torch(cuda, K, B):
+    A = _spd(B, K, seed=K)
+    w, U = eigen.eigh(A.to(cuda))
+    w, U = w.cpu(), U.cpu()
+    wr = torch.linalg.eigvalsh(A).flip(-1)
+    torch.testing.assert_close(w, wr, rtol=1e-10, atol=1e-14 * wr.abs().max().item())
+    torch.testing.assert_close((U * w[:, None, :]) @ U.transpose(1, 2), A, rtol=1e-9, atol=1e-13)
+    torch.testing.assert_close(U.transpose(1, 2) @ U, torch.eye(K, dtype=torch.float64).expand(B, K, K),
+                               rtol=0, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_hip_eigh_nan_input(cuda):
+    A = _spd(2, 8).to(cuda)
+    A[1, 0, 0] = float("nan")
+    w, U = eigen.eigh(A)
+    assert torch.isfinite(w[0]).all() and torch.isnan(w[1]).all()
+
+
+@pytest.mark.gpu
+def test_hip_mc_cov_statistics(cuda):
+    Cz = eigen.mc_cov(64, 42, 2520, seed=1, device=cuda).cpu()
+    assert torch.allclose(Cz, Cz.transpose(1, 2))
+    d = torch.diagonal(Cz, dim1=1, dim2=2)
+    assert abs(d.mean().item() - 1.0) < 0.01
+    off = Cz - torch.diag_embed(d)
+    assert off.abs().mean().item() < 0.03  # ~ sqrt(2/(pi T))
+    assert not torch.equal(Cz[0], Cz[1])
+    again = eigen.mc_cov(64, 42, 2520, seed=1, device=cuda).cpu()
+    assert torch.equal(Cz, again)  # counter-based RNG: bitwise reproducible
+
+
+@pytest.mark.gpu
+def test_hip_eigen_adjust_matches_reference_path(cuda):
+    D, K, M = 12, 42, 16
+    F = _spd(D, K, seed=9, spread=2.0) * 1e-4
+    F[3] = float("nan")
+    Cz = eigen.mc_cov(M, K, 500, seed=2, device=cuda)
+    Fg, vg = eigen.eigen_risk_adjust(F.to(cuda), Cz=Cz, return_bias=True)
+    Fc, vc = eigen.eigen_risk_adjust(F, Cz=Cz.cpu(), return_bias=True)
+    torch.testing.assert_close(vg.cpu(), vc, rtol=1e-8, atol=1e-10, equal_nan=True)
+    torch.testing.assert_close(Fg.cpu(), Fc, rtol=1e-8, atol=1e-16, equal_nan=True)

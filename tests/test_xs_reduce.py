@@ -1,0 +1,94 @@
+"""Post-processing reductions vs the reference's pandas/statsmodels code and HIP vs CPU."""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from llm_driven_multi_factor_model_amd.ops import xs_reduce as R
+
+
+def _panel(D=6, N=120, seed=0, nan_frac=0.1):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.randn(D, N, generator=g) * 2 + 1
+    x[torch.rand(D, N, generator=g) < nan_frac] = float("nan")
+    x[0, :3] = torch.tensor([50.0, -40.0, 30.0])  # outliers
+    x[D - 1, 1:] = float("nan")                    # single valid value -> no clipping
+    return x
+
+
+def _long(cols: dict):
+    D, N = next(iter(cols.values())).shape
+    data = {"trade_date": np.repeat(np.arange(D), N), "ts_code": np.tile(np.arange(N), D)}
+    for k, v in cols.items():
+        data[k] = v.double().numpy().reshape(-1)
+    return pd.DataFrame(data)
+
+
+@pytest.mark.reference
+def test_winsorize_matches_reference(ref, capsys):
+    x = _panel()
+    df = ref.post_processing.winsorize_factors(_long({"a": x}), ["a"], n_std=2.5)
+    exp = df["a"].values.reshape(x.shape)
+    np.testing.assert_allclose(R.winsorize(x).double().numpy(), exp, rtol=1e-6, atol=1e-6, equal_nan=True)
+
+
+@pytest.mark.reference
+def test_composite_matches_reference(ref, capsys):
+    a, b, c = _panel(seed=1), _panel(seed=2), _panel(seed=3)
+    cfg = {"v": {"components": ["a", "b", "c"], "weights": [0.7, 0.15, 0.15]}}
+    df = ref.post_processing.calculate_composite_factors(_long({"a": a, "b": b, "c": c}), cfg)
+    out = R.composite([a, b, c], [0.7, 0.15, 0.15])
+    np.testing.assert_allclose(out.double().numpy(), df["v"].values.reshape(a.shape), rtol=1e-6, equal_nan=True)
+
+
+@pytest.mark.reference
+def test_orthogonalize_matches_reference(ref, capsys):
+    y, b, s = _panel(seed=4), _panel(seed=5), _panel(seed=6)
+    y[2, :100] = float("nan")  # date with too few rows -> NaN
+    df = ref.post_processing.orthogonalize_factors(_long({"y": y, "b": b, "s": s}), {"y": ["b", "s"]})
+    out = R.ols_resid(y, [b, s])
+    np.testing.assert_allclose(out.double().numpy(), df["y"].values.reshape(y.shape), rtol=1e-4, atol=1e-5,
+                               equal_nan=True)
+
+
+@pytest.mark.reference
+def test_bayes_shrink_matches_reference(ref):
+    g = torch.Generator().manual_seed(7)
+    vol = torch.rand(300, generator=g) * 0.05 + 0.01
+    cap = torch.exp(torch.randn(300, generator=g) * 1.3 + 10)
+    exp = ref.utils.bayes_shrink(vol.double().numpy(), cap.double().numpy(), ngroup=10, q=1)
+    out = R.bayes_shrink(vol, cap, 10, 1.0)
+    np.testing.assert_allclose(out.double().numpy(), exp, rtol=1e-5)
+
+
+@pytest.mark.reference
+def test_style_norm_matches_reference(ref):
+    g = torch.Generator().manual_seed(8)
+    X = torch.randn(2, 4, 50, generator=g)
+    cap = torch.exp(torch.randn(2, 50, generator=g))
+    Z, mu, sig = R.style_norm(X, cap)
+    for d in range(2):
+        exp = ref.CrossSection.style_factor_norm(X[d].T.double().numpy(), cap[d].double().numpy())
+        np.testing.assert_allclose(Z[d].T.double().numpy(), exp, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_hip_reductions_match_cpu(cuda):
+    x, y, b, s = _panel(D=9, N=1000, seed=10), _panel(D=9, N=1000, seed=11), _panel(D=9, N=1000, seed=12), \
+        _panel(D=9, N=1000, seed=13)
+    torch.testing.assert_close(R.winsorize(x.to(cuda)).cpu(), R.winsorize(x), rtol=1e-6, atol=1e-6, equal_nan=True)
+    torch.testing.assert_close(R.composite([x.to(cuda), y.to(cuda)], [0.5, 0.5]).cpu(), R.composite([x, y], [0.5, 0.5]),
+                               equal_nan=True)
+    torch.testing.assert_close(R.ols_resid(y.to(cuda), [b.to(cuda), s.to(cuda)]).cpu(), R.ols_resid(y, [b, s]),
+                               rtol=1e-4, atol=1e-5, equal_nan=True)
+    torch.testing.assert_close(R.ols_resid(y.to(cuda), [b.to(cuda)], min_rows=2, sign=-1).cpu(),
+                               R.ols_resid(y, [b], min_rows=2, sign=-1), rtol=1e-4, atol=1e-5, equal_nan=True)
+    X = torch.randn(5, 10, 2000)
+    cap = torch.exp(torch.randn(5, 2000))
+    Zg, mug, sg = R.style_norm(X.to(cuda), cap.to(cuda))
+    Zc, muc, sc = R.style_norm(X, cap)
+    torch.testing.assert_close(Zg.cpu(), Zc, rtol=1e-5, atol=1e-5)
+    vol = torch.rand(4, 3000) * 0.05 + 0.01
+    cap2 = torch.exp(torch.randn(4, 3000))
+    torch.testing.assert_close(R.bayes_shrink(vol.to(cuda), cap2.to(cuda)).cpu(),
+                               R.bayes_shrink(vol, cap2), rtol=1e-5, atol=1e-6)
