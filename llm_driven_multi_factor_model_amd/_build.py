@@ -24,6 +24,8 @@ PKG_DIR = Path(__file__).resolve().parent
 CSRC = PKG_DIR / "csrc"
 OBJ_DIR = PKG_DIR / "_lib" / "obj"
 LIB_PATH = PKG_DIR / "_lib" / "libmfa_hip.so"
+HOST_SRC = PKG_DIR / "csrc_host"
+HOST_LIB_PATH = PKG_DIR / "_lib" / "libmfa_host.so"
 ARCH = os.environ.get("MFA_OFFLOAD_ARCH", "gfx950")
 
 
@@ -65,8 +67,30 @@ def _compile(src: Path, obj: Path) -> tuple[Path, str]:
     return obj, p.stderr
 
 
+def build_host(force: bool = False, verbose: bool = False) -> Path:
+    """Native host runtime (CSV/panel IO, as-of joins): plain C++17 + pthreads, C ABI."""
+    srcs = sorted(HOST_SRC.glob("*.cpp"))
+    if not srcs:
+        return HOST_LIB_PATH
+    if not force and HOST_LIB_PATH.exists() and all(
+            s.stat().st_mtime <= HOST_LIB_PATH.stat().st_mtime for s in srcs):
+        return HOST_LIB_PATH
+    HOST_LIB_PATH.parent.mkdir(parents=True, exist_ok=True)
+    cxx = os.environ.get("CXX", shutil.which("g++") or "c++")
+    tmp = HOST_LIB_PATH.with_suffix(".so.tmp")
+    cmd = [cxx, "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", *map(str, srcs), "-o", str(tmp)]
+    p = subprocess.run(cmd, capture_output=True, text=True)
+    if p.returncode != 0:
+        raise RuntimeError(f"host build failed:\n{p.stderr}")
+    os.replace(tmp, HOST_LIB_PATH)
+    if verbose:
+        print(f"[mfa-build] linked {HOST_LIB_PATH}", file=sys.stderr)
+    return HOST_LIB_PATH
+
+
 def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
     """Compile all kernels (incrementally) and link the shared library; returns its path."""
+    build_host(force=force, verbose=verbose)
     OBJ_DIR.mkdir(parents=True, exist_ok=True)
     headers = sorted(CSRC.glob("*.h"))
     srcs = sources()

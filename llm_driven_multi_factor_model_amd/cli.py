@@ -1,0 +1,130 @@
+"""Command line entry points (the reference has none: scripts with hard-coded paths, Q25).
+
+    python -m llm_driven_multi_factor_model_amd.cli synth  --out data/ --dates 250 --stocks 300
+    python -m llm_driven_multi_factor_model_amd.cli risk   --data data/barra_data_csi.csv \
+        --industry data/industry_info.csv --out results/ [--preset reference] [--sims 100]
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m llm_driven_multi_factor_model_amd.cli risk ...
+    python -m llm_driven_multi_factor_model_amd.cli factors --prices prices.csv --index index.csv \
+        --industry sw_industry.csv --out data/
+
+``risk`` is ``Barra-master/demo.py`` (read -> one-hot -> MFM(data, P, Q) -> 4 stages -> 5 CSVs);
+``factors`` is ``Barra_factor_cal/main.py`` (descriptors -> winsorize -> composite ->
+orthogonalize -> barra_data_csi.csv + industry_info.csv).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import sys
+import time
+
+import numpy as np
+import pandas as pd
+import torch
+
+log = logging.getLogger("mfa")
+
+
+def _setup_logging(rank: int = 0):
+    logging.basicConfig(level=os.environ.get("MFA_LOGLEVEL", "INFO"),
+                        format=f"%(asctime)s [rank{rank}] %(name)s %(levelname)s: %(message)s")
+
+
+def cmd_synth(a):
+    from .models.panel import synthetic_panel
+    p = synthetic_panel(a.dates, a.stocks, a.industries, a.styles, seed=a.seed, missing_frac=a.missing)
+    os.makedirs(a.out, exist_ok=True)
+    D, N = p.D, p.N
+    m = p.valid()
+    dates = pd.DatetimeIndex(p.dates).strftime("%Y/%m/%d")
+    codes = np.array([f"80{j:04d}.SI" for j in range(p.P)])
+    di, si = torch.nonzero(m, as_tuple=True)
+    df = pd.DataFrame({
+        "date": dates.values[di.numpy()], "stocknames": p.stocks[si.numpy()],
+        "capital": p.cap[di, si].double().numpy(), "ret": p.ret[di, si].double().numpy(),
+        "industry": codes[p.ind[di, si].long().numpy()],
+    })
+    for q, name in enumerate(p.style_names):
+        df[name] = p.styles[di, q, si].double().numpy()
+    df.to_csv(os.path.join(a.out, "barra_data_csi.csv"), index=False)
+    pd.DataFrame({"code": codes, "industry_names": [f"industry_{j:02d}" for j in range(p.P)],
+                  "start_date": "20000101"}).to_csv(os.path.join(a.out, "industry_info.csv"), index=False)
+    log.info("wrote %d rows x %d dates x %d stocks to %s", len(df), D, N, a.out)
+
+
+def cmd_risk(a):
+    from .models.risk_model import RiskModel
+    from .parallel import dist as pdist
+    from .utils.config import preset
+    from .utils.io import panel_from_barra_csv, write_risk_results
+
+    ctx = pdist.init_distributed(device=a.device)
+    _setup_logging(ctx.rank)
+    t0 = time.perf_counter()
+    full = panel_from_barra_csv(a.data, a.industry, device="cpu")
+    lo, hi = pdist.shard_range(full.D, ctx.rank, ctx.world)
+    panel = full.slice_dates(lo, hi).to(ctx.device)
+    log.info("panel %d dates x %d stocks x K=%d (shard [%d,%d)) loaded in %.2fs", full.D, full.N,
+             full.K, lo, hi, time.perf_counter() - t0)
+    cfg = preset(a.preset, eigen_sims=a.sims, vra_half_life=a.vra_tau, nw_lags=a.nw_q,
+                 nw_half_life=a.nw_tau, eigen_scale=a.scale)
+    model = RiskModel(panel, cfg, T_global=full.D, ctx=ctx)
+    model.run()
+    paths = write_risk_results(model, a.out, long_specific=a.long_specific)
+    if ctx.rank == 0:
+        log.info("stage ms: %s", json.dumps({k: round(v, 3) for k, v in model.times.ms.items()}))
+        for k, v in paths.items():
+            log.info("wrote %s -> %s", k, v)
+    pdist.barrier(ctx)
+
+
+def cmd_factors(a):
+    from .models.factor_engine import run_factor_pipeline
+    _setup_logging()
+    run_factor_pipeline(a.prices, a.index, a.industry, a.out, device=a.device)
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser(prog="mfa", description=__doc__,
+                                 formatter_class=argparse.RawDescriptionHelpFormatter)
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    s = sub.add_parser("synth", help="write a synthetic barra_data_csi.csv + industry_info.csv")
+    s.add_argument("--out", required=True)
+    s.add_argument("--dates", type=int, default=250)
+    s.add_argument("--stocks", type=int, default=300)
+    s.add_argument("--industries", type=int, default=28)
+    s.add_argument("--styles", type=int, default=10)
+    s.add_argument("--missing", type=float, default=0.02)
+    s.add_argument("--seed", type=int, default=0)
+    s.set_defaults(fn=cmd_synth)
+    r = sub.add_parser("risk", help="demo.py equivalent: risk model on barra_data_csi.csv")
+    r.add_argument("--data", required=True)
+    r.add_argument("--industry", required=True)
+    r.add_argument("--out", default="results")
+    r.add_argument("--preset", default="reference")
+    r.add_argument("--sims", type=int, default=100)
+    r.add_argument("--scale", type=float, default=1.4)
+    r.add_argument("--nw-q", type=int, default=2)
+    r.add_argument("--nw-tau", type=float, default=252.0)
+    r.add_argument("--vra-tau", type=float, default=42.0)
+    r.add_argument("--device", default=None, help="cpu to force the CPU path")
+    r.add_argument("--long-specific", action="store_true")
+    r.set_defaults(fn=cmd_risk)
+    f = sub.add_parser("factors", help="main.py equivalent: descriptors -> Barra exposures")
+    f.add_argument("--prices", required=True)
+    f.add_argument("--index", required=True)
+    f.add_argument("--industry", required=True)
+    f.add_argument("--out", default="data")
+    f.add_argument("--device", default=None)
+    f.set_defaults(fn=cmd_factors)
+    a = ap.parse_args(argv)
+    if a.cmd != "risk":
+        _setup_logging()
+    a.fn(a)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

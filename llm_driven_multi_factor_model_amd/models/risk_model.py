@@ -124,6 +124,8 @@ class RiskModel:
         B2 = (self.factor_ret ** 2 / var).mean(-1)                        # NaN where ER empty
         B2_all = pdist.all_gather_rows(B2, self.ctx)
         lam2 = ew_scan.ew_prefix_mean(B2_all, tau)[self.t_lo:self.t_lo + self.panel.D]
+        # no valid date yet: the reference's sum over an empty selection gives lambda = 0
+        lam2 = torch.nan_to_num(lam2, nan=0.0)
         self.vra_lambda = torch.sqrt(lam2)
         self.vra_cov = self.eigen_cov * lam2[:, None, None]
         self.times.add("vra", t0, self.device)

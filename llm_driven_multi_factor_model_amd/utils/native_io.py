@@ -1,0 +1,102 @@
+"""ctypes front-end of the native multi-threaded CSV reader (``csrc_host/csv_panel.cpp``)."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+import pandas as pd
+
+from .._build import HOST_LIB_PATH, build_host
+
+_lib = None
+
+
+def _load():
+    global _lib
+    if _lib is None:
+        if not HOST_LIB_PATH.exists():
+            build_host()
+        lib = C.CDLL(str(HOST_LIB_PATH))
+        lib.mfa_csv_shape.argtypes = [C.c_char_p, C.POINTER(C.c_int)]
+        lib.mfa_csv_shape.restype = C.c_int64
+        lib.mfa_csv_parse.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_void_p), C.c_int]
+        lib.mfa_csv_parse.restype = C.c_int64
+        _lib = lib
+    return _lib
+
+
+STRING_COLS = {"stocknames", "ts_code", "industry", "l1_code", "code", "industry_names", "date",
+               "trade_date"}
+
+
+def read_csv(path: str, string_cols=STRING_COLS, date_cols=(), nthreads: int = 0) -> pd.DataFrame | None:
+    """Columns in ``string_cols`` stay strings (dates keep their file format, as pandas does),
+    ``date_cols`` become int32 YYYYMMDD, everything else float64."""
+    """Parse a simple (unquoted-comma) CSV with a header into a DataFrame; None if unsupported."""
+    try:
+        lib = _load()
+    except Exception:
+        return None
+    with open(path, "rb") as fh:
+        header = fh.readline().decode("utf-8-sig").strip().split(",")
+    ncol = C.c_int(0)
+    rows = lib.mfa_csv_shape(path.encode(), C.byref(ncol))
+    if rows < 0 or ncol.value != len(header):
+        return None
+    types, bufs = [], []
+    for name in header:
+        if name in date_cols:
+            types.append(2); bufs.append(np.empty(rows, dtype=np.int32))
+        elif name in string_cols:
+            types.append(1); bufs.append(np.zeros(rows, dtype="S16"))
+        else:
+            types.append(0); bufs.append(np.empty(rows, dtype=np.float64))
+    t_arr = (C.c_int * len(types))(*types)
+    p_arr = (C.c_void_p * len(bufs))(*[b.ctypes.data for b in bufs])
+    got = lib.mfa_csv_parse(path.encode(), len(header), t_arr, p_arr, nthreads)
+    if got != rows:
+        bufs = [b[:got] for b in bufs]
+    cols = {}
+    for name, t, b in zip(header, types, bufs):
+        if t == 2:
+            cols[name] = b
+        elif t == 1:
+            u = b.astype("U16").astype(object)
+            u[b == b""] = np.nan
+            cols[name] = u
+        else:
+            cols[name] = b
+    return pd.DataFrame(cols)
+
+
+def read_barra_csv(path: str) -> pd.DataFrame | None:
+    if os.environ.get("MFA_NO_NATIVE_IO"):
+        return None
+    return read_csv(path)
+
+
+def read_columns(path: str, types: dict, nthreads: int = 0):
+    """Raw columnar parse: ``types`` maps column name -> 0 float64 / 1 bytes16 / 2 int YYYYMMDD.
+
+    Returns ``{name: ndarray}`` (bytes columns stay ``S16``), or None if unavailable.
+    """
+    try:
+        lib = _load()
+    except Exception:
+        return None
+    with open(path, "rb") as fh:
+        header = fh.readline().decode("utf-8-sig").strip().split(",")
+    ncol = C.c_int(0)
+    rows = lib.mfa_csv_shape(path.encode(), C.byref(ncol))
+    if rows < 0 or ncol.value != len(header):
+        return None
+    tl, bufs = [], []
+    for name in header:
+        t = types.get(name, 0)
+        tl.append(t)
+        bufs.append(np.zeros(rows, dtype="S16") if t == 1 else
+                    (np.empty(rows, dtype=np.int32) if t == 2 else np.empty(rows, dtype=np.float64)))
+    got = lib.mfa_csv_parse(path.encode(), len(header), (C.c_int * len(tl))(*tl),
+                            (C.c_void_p * len(bufs))(*[b.ctypes.data for b in bufs]), nthreads)
+    return {n: b[:got] for n, b in zip(header, bufs)}

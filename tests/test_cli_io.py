@@ -1,0 +1,61 @@
+"""End-to-end CLI (demo.py equivalent) and the native CSV reader."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pandas as pd
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(*args, env=None):
+    e = dict(os.environ, PYTHONPATH=ROOT, MFA_DEVICE="cpu")
+    e.update(env or {})
+    return subprocess.run([sys.executable, "-m", "llm_driven_multi_factor_model_amd.cli", *args],
+                          capture_output=True, text=True, env=e, timeout=600)
+
+
+def test_synth_then_risk_writes_demo_outputs(tmp_path):
+    d = str(tmp_path)
+    r = _run("synth", "--out", d, "--dates", "60", "--stocks", "90", "--industries", "6")
+    assert r.returncode == 0, r.stderr
+    r = _run("risk", "--data", f"{d}/barra_data_csi.csv", "--industry", f"{d}/industry_info.csv",
+             "--out", f"{d}/results", "--sims", "4", "--device", "cpu")
+    assert r.returncode == 0, r.stderr
+    for f in ["factor_returns.csv", "r_squared.csv", "specific_returns.csv",
+              "final_vol_regime_adj_covariance.csv", "volatility_multiplier_lambda.csv"]:
+        assert os.path.exists(f"{d}/results/{f}"), f
+    fr = pd.read_csv(f"{d}/results/factor_returns.csv", index_col=0)
+    assert fr.shape == (60, 1 + 6 + 10) and fr.columns[0] == "country"
+    cov = pd.read_csv(f"{d}/results/final_vol_regime_adj_covariance.csv", index_col=0)
+    assert np.allclose(cov.values, cov.values.T)
+
+
+def test_native_csv_reader_matches_pandas(tmp_path):
+    from llm_driven_multi_factor_model_amd.utils import native_io
+    rng = np.random.default_rng(0)
+    n = 5000
+    df = pd.DataFrame({"date": np.repeat(["2020/01/02", "2020/01/03"], n // 2),
+                       "stocknames": [f"{i % 2500:06d}.SZ" for i in range(n)],
+                       "capital": rng.random(n) * 1e5, "ret": rng.normal(0, 0.02, n),
+                       "industry": [f"80{i % 28:04d}.SI" for i in range(n)], "size": rng.normal(size=n)})
+    df.loc[3, "size"] = np.nan
+    p = str(tmp_path / "x.csv")
+    df.to_csv(p, index=False)
+    got = native_io.read_csv(p)
+    pd.testing.assert_frame_equal(got, pd.read_csv(p), check_dtype=False)
+
+
+def test_panel_from_barra_csv_native_equals_pandas(tmp_path, monkeypatch):
+    from llm_driven_multi_factor_model_amd.utils.io import panel_from_barra_csv
+    d = str(tmp_path)
+    assert _run("synth", "--out", d, "--dates", "20", "--stocks", "50", "--industries", "5").returncode == 0
+    a = panel_from_barra_csv(f"{d}/barra_data_csi.csv", f"{d}/industry_info.csv")
+    monkeypatch.setenv("MFA_NO_NATIVE_IO", "1")
+    b = panel_from_barra_csv(f"{d}/barra_data_csi.csv", f"{d}/industry_info.csv")
+    import torch
+    for k in ["styles", "cap", "ret", "ind"]:
+        torch.testing.assert_close(getattr(a, k), getattr(b, k), equal_nan=True)
+    assert list(a.stocks) == list(b.stocks) and (a.dates == b.dates).all()
