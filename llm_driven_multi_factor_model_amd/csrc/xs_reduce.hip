@@ -71,6 +71,8 @@ __global__ __launch_bounds__(256) void composite_kernel(CompArgs a, size_t n, fl
 struct OlsArgs {
   const float* x[4];
   int p;
+  int log_x0;  // x_1 := ln(x_1) in fp64 (NLSIZE regresses on ln(total_mv))
+  int ypow;    // > 0: y := x_1^ypow in fp64 (NLSIZE: SIZE^3), y pointer ignored
 };
 __global__ __launch_bounds__(256) void ols_resid_kernel(const float* __restrict__ y, OlsArgs a, int N,
                                                         int min_rows, double sign,
@@ -78,26 +80,35 @@ __global__ __launch_bounds__(256) void ols_resid_kernel(const float* __restrict_
   __shared__ double scratch[16];
   __shared__ double G[5][6];
   const int d = blockIdx.x, p = a.p, m = p + 1;
-  const float* yd = y + (size_t)d * N;
+  const float* yd = y ? y + (size_t)d * N : nullptr;
   double acc[21];  // packed upper Gram (15) + X^T y (5) + count
 #pragma unroll
   for (int i = 0; i < 21; ++i) acc[i] = 0.0;
-  for (int n = threadIdx.x; n < N; n += blockDim.x) {
-    double z[5];
+  auto load_row = [&](int n, double (&z)[5], double& yv) -> bool {
     z[0] = 1.0;
-    bool ok = fin(yd[n]);
+    bool ok = true;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       if (k < p) {
         const float v = a.x[k][(size_t)d * N + n];
         ok = ok && fin(v);
-        z[k + 1] = v;
+        z[k + 1] = (k == 0 && a.log_x0) ? log((double)v) : (double)v;
       } else {
         z[k + 1] = 0.0;
       }
     }
-    if (!ok) continue;
-    const double yv = yd[n];
+    if (a.ypow > 0) {
+      yv = z[1];
+      for (int e = 1; e < a.ypow; ++e) yv *= z[1];
+    } else {
+      ok = ok && fin(yd[n]);
+      yv = yd[n];
+    }
+    return ok && __builtin_isfinite(yv) && __builtin_isfinite(z[1]);
+  };
+  for (int n = threadIdx.x; n < N; n += blockDim.x) {
+    double z[5], yv;
+    if (!load_row(n, z, yv)) continue;
     int idx = 0;
 #pragma unroll
     for (int i = 0; i < 5; ++i)
@@ -138,16 +149,12 @@ __global__ __launch_bounds__(256) void ols_resid_kernel(const float* __restrict_
   for (int i = 0; i < 5; ++i) b[i] = i < m ? G[i][5] : 0.0;
   float* od = out + (size_t)d * N;
   for (int n = threadIdx.x; n < N; n += blockDim.x) {
-    bool ok = enough && fin(yd[n]);
-    double e = yd[n] - b[0];
+    double z[5], yv;
+    const bool ok = load_row(n, z, yv) && enough;
+    double e = yv - b[0];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      if (k < p) {
-        const float v = a.x[k][(size_t)d * N + n];
-        ok = ok && fin(v);
-        e -= b[k + 1] * (double)v;
-      }
-    }
+    for (int k = 0; k < 4; ++k)
+      if (k < p) e -= b[k + 1] * z[k + 1];
     od[n] = ok ? (float)(sign * e) : qnanf();
   }
 }
@@ -318,12 +325,14 @@ MFA_API int mfa_composite(const float* const* xs, const double* w, int C, size_t
 }
 
 MFA_API int mfa_ols_resid(const float* y, const float* const* xs, int p, int D, int N, int min_rows,
-                          double sign, float* out, void* stream) {
+                          double sign, int log_x0, int ypow, float* out, void* stream) {
   if (D <= 0) return 0;
-  if (p < 0 || p > 4) return (int)hipErrorInvalidValue;
+  if (p < 0 || p > 4 || (ypow > 0 && p < 1) || (ypow <= 0 && y == nullptr)) return (int)hipErrorInvalidValue;
   OlsArgs a;
   for (int k = 0; k < 4; ++k) a.x[k] = k < p ? xs[k] : nullptr;
   a.p = p;
+  a.log_x0 = log_x0;
+  a.ypow = ypow;
   hipLaunchKernelGGL(ols_resid_kernel, dim3(D), dim3(256), 0, (hipStream_t)stream, y, a, N, min_rows,
                      sign, out);
   return (int)hipGetLastError();

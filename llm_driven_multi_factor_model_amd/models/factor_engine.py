@@ -1,0 +1,400 @@
+"""Barra descriptor engine + post-processing + Barra export (L4-L6 of SURVEY.md §1).
+
+Reference: ``Barra_factor_cal/factor_calculator.py`` (FactorCalculator, :11-576),
+``post_processing.py`` and ``main.py:42-158``.  Semantics follow SURVEY.md §2.2.
+
+MI355X design: the reference's master frame (sorted by ts_code, trade_date) lives on the device
+as FLAT float32 rows plus three int32 index vectors (``seg_lo`` = first row of the row's stock,
+``date_id``, ``stock_id``).  Time-series descriptors run as one rolling kernel launch each over
+all stocks (``ops.rolling``); cross-sectional steps (NLSIZE, winsorize, orthogonalize) scatter
+the rows into a dense [date, stock] grid in HBM, run one per-date kernel launch
+(``ops.xs_reduce``) and gather back.  No per-stock or per-date Python loop anywhere.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import time
+import warnings
+
+import numpy as np
+import pandas as pd
+import torch
+
+from ..ops import rolling as RL
+from ..ops import xs_reduce as XR
+from ..utils.config import FactorConfig
+
+log = logging.getLogger("mfa.factors")
+
+BARRA_RENAME = {
+    "trade_date": "date", "ts_code": "stocknames", "l1_code": "industry", "circ_mv": "capital",
+    "SIZE": "size", "BETA": "beta", "RSTR": "momentum", "volatility": "residual_volatility",
+    "NLSIZE": "non_linear_size", "BP": "book_to_price_ratio", "earnings": "earnings_yield",
+}
+BARRA_OUTPUT_COLUMNS = [
+    "date", "stocknames", "capital", "ret", "industry",
+    "size", "beta", "momentum", "residual_volatility", "non_linear_size",
+    "book_to_price_ratio", "liquidity", "earnings_yield", "growth", "leverage",
+]
+FACTORS_TO_RUN = ["SIZE", "BETA", "RSTR", "DASTD", "CMRA", "NLSIZE", "BP", "LIQUIDITY",
+                  "EARNINGS", "GROWTH", "LEVERAGE"]
+OUTPUT_ORDER = {  # columns each factor group appends (factor_calculator.py run :525-569)
+    "SIZE": ["SIZE"], "BETA": ["BETA", "HSIGMA"], "RSTR": ["RSTR"], "DASTD": ["DASTD"],
+    "CMRA": ["CMRA"], "NLSIZE": ["NLSIZE"], "BP": ["BP"], "LIQUIDITY": ["STOM", "STOQ", "STOA"],
+    "EARNINGS": ["CETOP", "ETOP"], "GROWTH": ["YOYProfit", "YOYSales"],
+    "LEVERAGE": ["MLEV", "DTOA", "BLEV"],
+}
+
+
+def _default_device():
+    d = os.environ.get("MFA_DEVICE")
+    if d:
+        return torch.device(d)
+    return torch.device("cuda:0" if torch.cuda.is_available() else "cpu")
+
+
+class FactorEngine:
+    """Descriptor computation on a stock-sorted master panel (``FactorCalculator`` semantics)."""
+
+    NUMERIC = ["close", "total_mv", "circ_mv", "pb", "turnover_rate", "pe_ttm", "n_cashflow_act",
+               "total_ncl", "total_hldr_eqy_inc_min_int", "debt_to_assets", "q_profit_yoy",
+               "q_sales_yoy"]
+
+    def __init__(self, prices_df: pd.DataFrame, index_df: pd.DataFrame, device=None,
+                 config: FactorConfig | None = None):
+        self.cfg = config or FactorConfig()
+        self.device = torch.device(device) if device is not None else _default_device()
+        t0 = time.perf_counter()
+        self.master = self._prepare(prices_df, index_df)
+        self.prep_s = time.perf_counter() - t0
+
+    # ---------------------------------------------------------------- _prepare_data (:34-64)
+    def _prepare(self, prices_df, index_df) -> pd.DataFrame:
+        p = prices_df.copy()
+        ix = index_df.copy()
+        for df in (p, ix):
+            td = df["trade_date"]
+            if not isinstance(td.dtype, pd.api.types.DatetimeTZDtype) and not np.issubdtype(td.dtype, np.datetime64):
+                td = pd.to_datetime(td.astype(str), format="mixed")
+            df["trade_date"] = td.dt.strftime("%Y/%m/%d")
+        p = p.sort_values(["ts_code", "trade_date"], kind="stable").reset_index(drop=True)
+        ix = ix.sort_values("trade_date").reset_index(drop=True)
+        ix["market_ret"] = ix["close"].pct_change()
+        master = p.merge(ix[["trade_date", "market_ret"]], on="trade_date", how="left")
+        master = master.reset_index().rename(columns={"index": "original_index"})
+        dev = self.device
+        codes, self.stock_names = pd.factorize(master["ts_code"].astype(str), sort=True)
+        dcodes, self.date_names = pd.factorize(master["trade_date"], sort=True)
+        self.R = len(master)
+        self.D, self.N = len(self.date_names), len(self.stock_names)
+        self.stock_id = torch.from_numpy(codes.astype(np.int32)).to(dev)
+        self.date_id = torch.from_numpy(dcodes.astype(np.int32)).to(dev)
+        self.seg_lo = RL.seg_lo_from_codes(self.stock_id)
+        self.grid_idx = (self.date_id.long() * self.N + self.stock_id.long())
+        self.cols = {}
+        for c in self.NUMERIC + ["market_ret"]:
+            if c in master.columns:
+                self.cols[c] = torch.from_numpy(master[c].to_numpy(dtype=np.float32, na_value=np.nan)).to(dev)
+        self.cols["ret"], self.cols["log_ret"] = RL.returns(self.cols["close"], self.seg_lo)
+        if not master["ts_code"].is_monotonic_increasing:
+            raise AssertionError("master frame must be sorted by ts_code")
+        return master
+
+    # ---------------------------------------------------------------- grid helpers
+    def to_grid(self, x: torch.Tensor) -> torch.Tensor:
+        g = torch.full((self.D * self.N,), float("nan"), dtype=torch.float32, device=self.device)
+        g[self.grid_idx] = x.to(torch.float32)
+        return g.view(self.D, self.N)
+
+    def from_grid(self, g: torch.Tensor) -> torch.Tensor:
+        return g.reshape(-1)[self.grid_idx]
+
+    def _need(self, *names):
+        missing = [n for n in names if n not in self.cols]
+        if missing:
+            print(f"\nERROR: Missing required columns: {missing}\n")
+            return False
+        return True
+
+    # ---------------------------------------------------------------- descriptors
+    def compute_size(self):
+        return {"SIZE": torch.log(self.cols["total_mv"])}
+
+    def compute_beta_hsigma(self):
+        c = self.cfg
+        b, h = RL.beta_hsigma(self.cols["ret"], self.cols["market_ret"], self.seg_lo, c.beta_window,
+                              c.beta_half_life, c.beta_min_periods)
+        return {"BETA": b, "HSIGMA": h}
+
+    def compute_rstr(self):
+        c = self.cfg
+        return {"RSTR": RL.rstr(self.cols["log_ret"], self.seg_lo, c.rstr_window, c.rstr_lag,
+                                c.rstr_half_life, c.rstr_min_periods)}
+
+    def compute_dastd(self):
+        c = self.cfg
+        return {"DASTD": RL.dastd(self.cols["ret"], self.cols["market_ret"], self.seg_lo, c.dastd_window,
+                                  c.dastd_half_life, c.dastd_min_periods)}
+
+    def compute_cmra(self):
+        c = self.cfg
+        return {"CMRA": RL.cmra(self.cols["log_ret"], self.seg_lo, c.cmra_window, c.cmra_partial)}
+
+    def compute_nlsize(self):
+        # per date: -residual of SIZE^3 on [1, SIZE], SIZE = ln(total_mv) formed in fp64 in-kernel
+        mv = self.to_grid(self.cols["total_mv"])
+        out = XR.ols_resid(None, [mv], min_rows=2, sign=-1.0, log_x0=True, ypow=3)
+        return {"NLSIZE": self.from_grid(out)}
+
+    def compute_bp(self):
+        if not self._need("pb"):
+            return None
+        pb = self.cols["pb"]
+        return {"BP": torch.where(pb > 0, 1.0 / pb, torch.full_like(pb, float("nan")))}
+
+    def compute_liquidity(self):
+        if not self._need("turnover_rate"):
+            return None
+        c = self.cfg
+        tr = self.cols["turnover_rate"]
+        out = {}
+        for name, (w, mp) in (("STOM", c.stom), ("STOQ", c.stoq), ("STOA", c.stoa)):
+            out[name] = RL.rolling_sum(tr, self.seg_lo, w, mp, scale=0.01, log=True)
+        return out
+
+    def compute_earnings_yield(self):
+        if not (self._need("n_cashflow_act", "total_mv", "pe_ttm") and "end_date" in self.master.columns):
+            return None
+        m = self.master
+        fin = m[["ts_code", "end_date", "n_cashflow_act"]].drop_duplicates().copy()
+        fin = fin.sort_values(["ts_code", "end_date"], kind="stable").reset_index(drop=True)
+        codes = torch.from_numpy(pd.factorize(fin["ts_code"].astype(str))[0].astype(np.int32))
+        seg = RL.seg_lo_from_codes(codes).to(self.device)
+        v = torch.from_numpy(fin["n_cashflow_act"].to_numpy(np.float32, na_value=np.nan)).to(self.device)
+        ttm = RL.rolling_sum(v, seg, 4, 4)  # statement-row TTM (quirk Q18)
+        fin["n_cashflow_act_ttm"] = ttm.double().cpu().numpy()
+        tmp = m[["original_index", "ts_code", "end_date"]].merge(
+            fin[["ts_code", "end_date", "n_cashflow_act_ttm"]], on=["ts_code", "end_date"], how="left")
+        tmp = tmp.sort_values("original_index", kind="stable")
+        cf = torch.from_numpy(tmp["n_cashflow_act_ttm"].to_numpy(np.float64, na_value=np.nan)).to(self.device)
+        mv = self.cols["total_mv"].double()
+        nan = torch.full_like(mv, float("nan"))
+        cetop = torch.where((mv > 0) & (cf > 0), cf / mv, nan)  # unit mix-up kept (quirk Q17)
+        pe = self.cols["pe_ttm"].double()
+        etop = torch.where(pe > 0, 1.0 / pe, nan)
+        return {"CETOP": cetop.float(), "ETOP": etop.float()}
+
+    def select_growth_factors(self):
+        if not self._need("q_profit_yoy", "q_sales_yoy"):
+            return None
+        return {"YOYProfit": self.cols["q_profit_yoy"] / 100.0, "YOYSales": self.cols["q_sales_yoy"] / 100.0}
+
+    def compute_leverage(self):
+        if not self._need("total_mv", "total_ncl", "total_hldr_eqy_inc_min_int", "debt_to_assets"):
+            return None
+        mv = self.cols["total_mv"].double()
+        ncl = self.cols["total_ncl"].double()
+        be = self.cols["total_hldr_eqy_inc_min_int"].double()
+        nan = torch.full_like(mv, float("nan"))
+        mlev = (mv + ncl) / mv
+        mlev = torch.where(torch.isinf(mlev), nan, mlev)
+        blev = torch.where(be > 0, (be + ncl) / be, nan)
+        return {"MLEV": mlev.float(), "DTOA": self.cols["debt_to_assets"], "BLEV": blev.float()}
+
+    METHODS = {
+        "SIZE": "compute_size", "BETA": "compute_beta_hsigma", "RSTR": "compute_rstr",
+        "DASTD": "compute_dastd", "CMRA": "compute_cmra", "NLSIZE": "compute_nlsize",
+        "BP": "compute_bp", "LIQUIDITY": "compute_liquidity", "EARNINGS": "compute_earnings_yield",
+        "GROWTH": "select_growth_factors", "LEVERAGE": "compute_leverage",
+    }
+
+    def compute(self, factors: list[str]) -> dict:
+        """Run factor groups; returns ordered {column: flat tensor}."""
+        out = {}
+        self.timings = {}
+        for name in factors:
+            meth = self.METHODS.get(name.upper())
+            if meth is None:
+                print(f"Warning: Factor '{name}' not found.")
+                continue
+            t0 = time.perf_counter()
+            res = getattr(self, meth)()
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+            self.timings[name.upper()] = (time.perf_counter() - t0) * 1e3
+            if res is None:
+                print(f"Warning: Method for '{name}' returned None.")
+                continue
+            out.update(res)
+        return out
+
+    def run(self, factors: list[str]) -> pd.DataFrame:
+        """``FactorCalculator.run``: [ts_code, trade_date, ret, circ_mv, <descriptors>] in master order."""
+        res = self.compute(factors)
+        df = self.master[["ts_code", "trade_date"]].copy()
+        df["ret"] = self.cols["ret"].double().cpu().numpy()
+        df["circ_mv"] = self.master["circ_mv"].to_numpy(np.float64, na_value=np.nan) if "circ_mv" in self.master else np.nan
+        for k, v in res.items():
+            df[k] = v.double().cpu().numpy()
+        return df
+
+
+# ---------------------------------------------------------------------------------------------
+# post-processing on a descriptor frame (post_processing.py) — per-date kernels on dense grids
+# ---------------------------------------------------------------------------------------------
+class _Grid:
+    def __init__(self, df: pd.DataFrame, device):
+        self.device = device
+        dcodes, self.dates = pd.factorize(df["trade_date"], sort=True)
+        key = df["ts_code"].astype(str) if "ts_code" in df.columns else pd.Series(np.arange(len(df)))
+        scodes, self.stocks = pd.factorize(key, sort=True)
+        self.D, self.N = len(self.dates), len(self.stocks)
+        self.idx = torch.from_numpy(dcodes.astype(np.int64) * self.N + scodes.astype(np.int64)).to(device)
+        if pd.Index(self.idx.cpu().numpy()).has_duplicates:
+            raise ValueError("duplicate (trade_date, ts_code) rows")
+
+    def put(self, col: np.ndarray) -> torch.Tensor:
+        g = torch.full((self.D * self.N,), float("nan"), dtype=torch.float32, device=self.device)
+        g[self.idx] = torch.from_numpy(np.asarray(col, dtype=np.float32)).to(self.device)
+        return g.view(self.D, self.N)
+
+    def take(self, g: torch.Tensor) -> np.ndarray:
+        return g.reshape(-1)[self.idx].double().cpu().numpy()
+
+
+def winsorize_frame(df: pd.DataFrame, factor_list: list, n_std: float = 2.5, device=None) -> pd.DataFrame:
+    dev = torch.device(device) if device else _default_device()
+    out = df.copy()
+    grid = _Grid(out, dev)
+    for f in factor_list:
+        if f not in out.columns:
+            print(f"Warning: Factor '{f}' not found in DataFrame. Skipping.")
+            continue
+        out[f] = grid.take(XR.winsorize(grid.put(out[f].to_numpy(np.float64, na_value=np.nan)), n_std))
+    return out
+
+
+def composite_frame(df: pd.DataFrame, config: dict, device=None) -> pd.DataFrame:
+    dev = torch.device(device) if device else _default_device()
+    out = df.copy()
+    for new, cfg in config.items():
+        xs, ws = [], []
+        for c, w in zip(cfg["components"], cfg["weights"]):
+            if c in out.columns:
+                xs.append(torch.from_numpy(out[c].to_numpy(np.float32, na_value=np.nan)).to(dev))
+                ws.append(w)
+            else:
+                print(f"Warning: Component '{c}' not found in DataFrame. Skipping.")
+        if xs:
+            out[new] = XR.composite(xs, ws).double().cpu().numpy()
+        else:
+            out[new] = np.nan
+    return out
+
+
+def orthogonalize_frame(df: pd.DataFrame, rules: dict, device=None) -> pd.DataFrame:
+    dev = torch.device(device) if device else _default_device()
+    out = df.copy()
+    grid = _Grid(out, dev)
+    for target, against in rules.items():
+        y = grid.put(out[target].to_numpy(np.float64, na_value=np.nan))
+        xs = [grid.put(out[a].to_numpy(np.float64, na_value=np.nan)) for a in against]
+        out[target] = grid.take(XR.ols_resid(y, xs, min_rows=len(against) + 2))
+    return out
+
+
+def barra_export(processed: pd.DataFrame, sw_industry: pd.DataFrame):
+    """main.py:98-137: industry merge, t+1 return, rename/select; plus industry_info."""
+    barra = processed.merge(sw_industry[["ts_code", "l1_code"]], on="ts_code", how="left")
+    barra["ret"] = barra.groupby("ts_code")["ret"].shift(-1)
+    barra = barra.rename(columns=BARRA_RENAME)
+    final = barra[[c for c in BARRA_OUTPUT_COLUMNS if c in barra.columns]]
+    stk = final[["stocknames"]].drop_duplicates().rename(columns={"stocknames": "ts_code"})
+    cols = [c for c in ["ts_code", "l1_code", "l1_name", "in_date"] if c in sw_industry.columns]
+    info = stk.merge(sw_industry[cols], on="ts_code", how="left")
+    info = info.drop_duplicates(subset=[c for c in ["l1_code", "l1_name"] if c in info.columns]).rename(
+        columns={"l1_code": "code", "l1_name": "industry_names", "in_date": "start_date"})
+    info = info[[c for c in ["code", "industry_names", "start_date"] if c in info.columns]]
+    return final, info
+
+
+def factor_pipeline(prices_df, index_df, sw_industry_df, factors=None, config: FactorConfig | None = None,
+                    device=None):
+    """main.py end to end: raw descriptors -> winsorize -> composite -> orthogonalize -> export."""
+    cfg = config or FactorConfig()
+    t = {}
+    t0 = time.perf_counter()
+    eng = FactorEngine(prices_df, index_df, device=device, config=cfg)
+    raw = eng.run(factors or FACTORS_TO_RUN)
+    t["descriptors_s"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    cols = [c for c in raw.columns if c not in ("ts_code", "trade_date")]
+    w = winsorize_frame(raw, cols, cfg.winsor_n_std, device=eng.device)  # incl. ret, circ_mv (Q23)
+    c = composite_frame(w, cfg.composite, device=eng.device)
+    o = orthogonalize_frame(c, cfg.ortho, device=eng.device)
+    t["postprocess_s"] = time.perf_counter() - t0
+    final, info = barra_export(o, sw_industry_df)
+    return final, info, dict(t, kernel_ms=getattr(eng, "timings", {}))
+
+
+def run_factor_pipeline(prices_csv, index_csv, industry_csv, out_dir, device=None):
+    prices = pd.read_csv(prices_csv)
+    index = pd.read_csv(index_csv)
+    sw = pd.read_csv(industry_csv)
+    for df in (prices, index):
+        df["trade_date"] = pd.to_datetime(df["trade_date"].astype(str), format="mixed")
+    final, info, t = factor_pipeline(prices, index, sw, device=device)
+    os.makedirs(out_dir, exist_ok=True)
+    final.to_csv(os.path.join(out_dir, "barra_data_csi.csv"), index=False)
+    info.to_csv(os.path.join(out_dir, "industry_info.csv"), index=False)
+    log.info("barra_data_csi.csv %s, industry_info %s, timings %s", final.shape, info.shape, t)
+    return final, info
+
+
+def synthetic_prices(N: int = 50, T: int = 300, seed: int = 0, n_ind: int = 8, suspend_frac: float = 0.0,
+                     start: str = "2019-01-02"):
+    """Synthetic (prices_df, index_df, sw_industry_df) in the loader's schema (load_data.py:66-431).
+
+    Random-walk closes with a market component, lognormal caps, quarterly statement fields that
+    step on announcement dates, and optional random suspensions (missing rows).
+    """
+    rng = np.random.default_rng(seed)
+    dates = pd.bdate_range(start, periods=T)
+    mkt = rng.normal(0.0003, 0.012, T)
+    idx_close = 3000 * np.exp(np.cumsum(mkt))
+    rows = []
+    qends = pd.date_range(dates[0] - pd.Timedelta(days=400), dates[-1], freq="QE")
+    for i in range(N):
+        code = f"{600000 + i:06d}.SH" if i % 2 else f"{i:06d}.SZ"
+        beta = rng.uniform(0.5, 1.5)
+        r = beta * mkt + rng.normal(0, 0.02, T)
+        close = 10 * np.exp(np.cumsum(r))
+        shares = rng.lognormal(10, 1)
+        keep = rng.random(T) >= suspend_frac
+        ncf = rng.normal(1e8, 5e7, len(qends))
+        ncl = rng.lognormal(20, 1, len(qends))
+        eq = rng.lognormal(21, 1, len(qends))
+        dta = rng.uniform(20, 80, len(qends))
+        qp = rng.normal(10, 30, len(qends))
+        qs = rng.normal(8, 20, len(qends))
+        for t in range(T):
+            if not keep[t]:
+                continue
+            k = np.searchsorted(qends, dates[t] - pd.Timedelta(days=45)) - 1
+            k = max(k, 0)
+            rows.append((code, dates[t], close[t], close[t] * shares, close[t] * shares * 0.7,
+                         rng.uniform(0.5, 8), rng.uniform(0.1, 5), rng.uniform(5, 60),
+                         ncf[k], qends[k], ncl[k], eq[k], dta[k], qp[k], qs[k]))
+    prices = pd.DataFrame(rows, columns=["ts_code", "trade_date", "close", "total_mv", "circ_mv", "pb",
+                                         "turnover_rate", "pe_ttm", "n_cashflow_act", "end_date",
+                                         "total_ncl", "total_hldr_eqy_inc_min_int", "debt_to_assets",
+                                         "q_profit_yoy", "q_sales_yoy"])
+    for c in ["close", "total_mv", "circ_mv", "pb", "turnover_rate", "pe_ttm"]:
+        prices[c] = prices[c].astype(np.float32).astype(np.float64)  # reference downcasts (Q27)
+    index = pd.DataFrame({"ts_code": "000300.SH", "trade_date": dates, "close": idx_close})
+    codes = prices["ts_code"].unique()
+    sw = pd.DataFrame({"ts_code": codes, "l1_code": [f"80{j % n_ind:04d}.SI" for j in range(len(codes))],
+                       "l1_name": [f"industry_{j % n_ind}" for j in range(len(codes))],
+                       "in_date": "20000101", "out_date": None, "is_new": "Y"})
+    return prices, index, sw

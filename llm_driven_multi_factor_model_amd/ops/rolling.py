@@ -1,0 +1,202 @@
+"""Rolling-window descriptor ops on flat (stock-sorted) rows (K4/K5, ``csrc/rolling.hip``).
+
+Rows follow the reference's master frame order — sorted by (ts_code, trade_date) — and
+``seg_lo[r]`` is the first row of row r's stock, so every window counts the stock's own trading
+rows exactly as ``groupby('ts_code').rolling(...)`` does (factor_calculator.py:79-367).
+CPU paths are direct float64 transcriptions of the pandas callbacks (used as test oracles).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import math
+
+import numpy as np
+import torch
+
+from .. import _native
+
+_vp, _i, _d = C.c_void_p, C.c_int, C.c_double
+_native.register("mfa_beta_hsigma", [_vp, _vp, _vp, _i, _i, _d, _i, _vp, _vp, _vp])
+_native.register("mfa_rstr", [_vp, _vp, _i, _i, _i, _d, _i, _vp, _vp])
+_native.register("mfa_dastd", [_vp, _vp, _vp, _i, _i, _d, _i, _vp, _vp])
+_native.register("mfa_cmra", [_vp, _vp, _i, _i, _i, _vp, _vp])
+_native.register("mfa_rolling_sum", [_vp, _vp, _i, _i, _i, _d, _i, _vp, _vp])
+_native.register("mfa_returns", [_vp, _vp, _i, _vp, _vp, _vp])
+
+
+def _f(t):
+    return t.to(torch.float32).contiguous()
+
+
+def _i32(t):
+    return t.to(torch.int32).contiguous()
+
+
+def seg_lo_from_codes(codes: torch.Tensor) -> torch.Tensor:
+    """First row index of each row's group for a group-sorted code vector."""
+    codes = codes.to(torch.int64)
+    R = codes.numel()
+    start = torch.ones(R, dtype=torch.bool, device=codes.device)
+    if R > 1:
+        start[1:] = codes[1:] != codes[:-1]
+    idx = torch.where(start, torch.arange(R, device=codes.device), torch.zeros_like(codes))
+    return torch.cummax(idx, 0).values.to(torch.int32)
+
+
+# ---------------------------------------------------------------- returns
+def returns(close, seg_lo):
+    close, seg_lo = _f(close), _i32(seg_lo)
+    R = close.numel()
+    if close.is_cuda:
+        ret, lr = torch.empty_like(close), torch.empty_like(close)
+        _native.call("mfa_returns", _native.ptr(close), _native.ptr(seg_lo), R, _native.ptr(ret),
+                     _native.ptr(lr), _native.stream(close.device))
+        return ret, lr
+    c = close.double().numpy()
+    s = seg_lo.numpy()
+    ret = np.full(R, np.nan)
+    lr = np.full(R, np.nan)
+    for r in range(R):
+        if r == s[r]:
+            continue
+        if np.isfinite(c[r]) and np.isfinite(c[r - 1]) and c[r] > 0 and c[r - 1] > 0:
+            lr[r] = math.log(c[r]) - math.log(c[r - 1])
+        i = r
+        while i >= s[r] and not np.isfinite(c[i]):
+            i -= 1
+        k = r - 1
+        while k >= s[r] and not np.isfinite(c[k]):
+            k -= 1
+        if i >= s[r] and k >= s[r]:
+            ret[r] = c[i] / c[k] - 1
+    return torch.from_numpy(ret).float(), torch.from_numpy(lr).float()
+
+
+# ---------------------------------------------------------------- BETA / HSIGMA
+def beta_hsigma(ret, mret, seg_lo, window=252, half_life=63.0, min_periods=42):
+    ret, mret, seg_lo = _f(ret), _f(mret), _i32(seg_lo)
+    R = ret.numel()
+    lam = 0.5 ** (1.0 / half_life)
+    if ret.is_cuda:
+        b, h = torch.empty_like(ret), torch.empty_like(ret)
+        _native.call("mfa_beta_hsigma", _native.ptr(ret), _native.ptr(mret), _native.ptr(seg_lo), R,
+                     window, lam, min_periods, _native.ptr(b), _native.ptr(h), _native.stream(ret.device))
+        return b, h
+    y, x, s = ret.double().numpy(), mret.double().numpy(), seg_lo.numpy()
+    wfull = lam ** np.arange(window - 1, -1, -1)
+    b = np.full(R, np.nan)
+    h = np.full(R, np.nan)
+    for r in range(R):
+        lo = max(s[r], r - window + 1)
+        yy, xx = y[lo:r + 1], x[lo:r + 1]
+        ok = np.isfinite(yy) & np.isfinite(xx)
+        n = int(ok.sum())
+        if n < min_periods or n <= 2:
+            continue
+        w = wfull[-n:]
+        X = np.column_stack([np.ones(n), xx[ok]])
+        sw = np.sqrt(w)
+        coef, *_ = np.linalg.lstsq(X * sw[:, None], yy[ok] * sw, rcond=None)
+        e = yy[ok] - X @ coef
+        b[r] = coef[1]
+        h[r] = math.sqrt((w * e * e).sum() / (n - 2))
+    return torch.from_numpy(b).float(), torch.from_numpy(h).float()
+
+
+# ---------------------------------------------------------------- RSTR
+def rstr(log_ret, seg_lo, T=504, L=21, half_life=126.0, min_periods=42):
+    lr, seg_lo = _f(log_ret), _i32(seg_lo)
+    R = lr.numel()
+    W = T - L
+    lam = 0.5 ** (1.0 / half_life)
+    if lr.is_cuda:
+        out = torch.empty_like(lr)
+        _native.call("mfa_rstr", _native.ptr(lr), _native.ptr(seg_lo), R, L, W, lam, min_periods,
+                     _native.ptr(out), _native.stream(lr.device))
+        return out
+    v, s = lr.double().numpy(), seg_lo.numpy()
+    out = np.full(R, np.nan)
+    for r in range(R):
+        lo = max(s[r], r - W + 1)
+        js = np.arange(lo, r + 1)
+        src = js - L
+        xv = np.where(src >= s[r], v[np.clip(src, 0, None)], np.nan)
+        w = lam ** np.arange(len(js))
+        ok = np.isfinite(xv)
+        if ok.sum() >= min_periods:
+            out[r] = (xv[ok] * w[ok]).sum() / w[ok].sum()
+    return torch.from_numpy(out).float()
+
+
+# ---------------------------------------------------------------- DASTD
+def dastd(ret, mret, seg_lo, window=252, half_life=42.0, min_periods=42):
+    ret, mret, seg_lo = _f(ret), _f(mret), _i32(seg_lo)
+    R = ret.numel()
+    lam = 0.5 ** (1.0 / half_life)
+    if ret.is_cuda:
+        out = torch.empty_like(ret)
+        _native.call("mfa_dastd", _native.ptr(ret), _native.ptr(mret), _native.ptr(seg_lo), R, window,
+                     lam, min_periods, _native.ptr(out), _native.stream(ret.device))
+        return out
+    e, s = (ret.double() - mret.double()).numpy(), seg_lo.numpy()
+    wfull = lam ** np.arange(window - 1, -1, -1)
+    out = np.full(R, np.nan)
+    for r in range(R):
+        lo = max(s[r], r - window + 1)
+        xv = e[lo:r + 1]
+        xv = xv[np.isfinite(xv)]
+        n = len(xv)
+        if n < min_periods:
+            continue
+        w = wfull[-n:] / wfull[-n:].sum()
+        m = (xv * w).sum()
+        out[r] = math.sqrt((w * (xv - m) ** 2).sum())
+    return torch.from_numpy(out).float()
+
+
+# ---------------------------------------------------------------- CMRA
+def cmra(log_ret, seg_lo, window=252, partial=False):
+    lr, seg_lo = _f(log_ret), _i32(seg_lo)
+    R = lr.numel()
+    if lr.is_cuda:
+        out = torch.empty_like(lr)
+        _native.call("mfa_cmra", _native.ptr(lr), _native.ptr(seg_lo), R, window, int(partial),
+                     _native.ptr(out), _native.stream(lr.device))
+        return out
+    v, s = lr.double().numpy(), seg_lo.numpy()
+    out = np.full(R, np.nan)
+    for r in range(R):
+        if not partial:
+            if r - window + 1 < s[r]:
+                continue
+            w = v[r - window + 1:r + 1]
+            if not np.isfinite(w).all():
+                continue
+        else:
+            w = v[max(s[r], r - window + 1):r + 1]
+            w = w[np.isfinite(w)]
+            if len(w) == 0:
+                continue
+        z = np.exp(np.cumsum(w)) - 1
+        out[r] = np.log(1 + z.max()) - np.log(1 + z.min())
+    return torch.from_numpy(out).float()
+
+
+# ---------------------------------------------------------------- rolling sums (liquidity)
+def rolling_sum(x, seg_lo, window, min_periods, scale=1.0, log=False):
+    x, seg_lo = _f(x), _i32(seg_lo)
+    R = x.numel()
+    if x.is_cuda:
+        out = torch.empty_like(x)
+        _native.call("mfa_rolling_sum", _native.ptr(x), _native.ptr(seg_lo), R, window, min_periods,
+                     float(scale), int(log), _native.ptr(out), _native.stream(x.device))
+        return out
+    v, s = x.double().numpy() * scale, seg_lo.numpy()
+    out = np.full(R, np.nan)
+    for r in range(R):
+        w = v[max(s[r], r - window + 1):r + 1]
+        w = w[np.isfinite(w)]
+        if len(w) >= min_periods:
+            t = w.sum()
+            out[r] = (np.nan if t == 0 else math.log(t)) if log else t
+    return torch.from_numpy(out).float()

@@ -24,7 +24,7 @@ from .. import _native
 _native.register("mfa_winsorize", [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p])
 _native.register("mfa_composite", [C.c_void_p, C.c_void_p, C.c_int, C.c_size_t, C.c_void_p, C.c_void_p])
 _native.register("mfa_ols_resid", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int,
-                                    C.c_double, C.c_void_p, C.c_void_p])
+                                    C.c_double, C.c_int, C.c_int, C.c_void_p, C.c_void_p])
 _native.register("mfa_style_norm", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                      C.c_void_p, C.c_void_p])
 _native.register("mfa_bayes_shrink", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_double,
@@ -85,36 +85,41 @@ def composite(xs: list[torch.Tensor], weights: list[float]) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------ OLS residual
-def ols_resid(y: torch.Tensor, xs: list[torch.Tensor], min_rows: int | None = None,
-              sign: float = 1.0) -> torch.Tensor:
+def ols_resid(y: torch.Tensor | None, xs: list[torch.Tensor], min_rows: int | None = None,
+              sign: float = 1.0, log_x0: bool = False, ypow: int = 0) -> torch.Tensor:
     """Per-date residual of ``y`` [D, N] on ``[1, x_1..x_p]`` over rows where all are finite.
 
-    ``min_rows`` defaults to p + 2 (``orthogonalize_factors``); NLSIZE uses 2 and sign -1.
+    ``min_rows`` defaults to p + 2 (``orthogonalize_factors``); NLSIZE uses 2 and sign -1 with
+    ``log_x0=True, ypow=3`` so SIZE = ln(total_mv) and SIZE^3 are formed in float64 in-kernel
+    (as the reference does in numpy) instead of being rounded to float32 first.
     Dates with fewer valid rows are all-NaN (the reference returns a NaN series).
     """
     p = len(xs)
     if p > 4:
         raise ValueError("at most 4 regressors")
     min_rows = p + 2 if min_rows is None else min_rows
-    y = _f32(y)
     xs = [_f32(x) for x in xs]
-    D, N = y.shape
-    if not y.is_cuda:
-        return _ols_resid_ref(y, xs, min_rows, sign)
-    out = torch.empty_like(y)
+    D, N = xs[0].shape if xs else y.shape
+    y = _f32(y) if y is not None else None
+    if not xs[0].is_cuda if xs else not y.is_cuda:
+        return _ols_resid_ref(y, xs, min_rows, sign, log_x0, ypow)
+    out = torch.empty(D, N, dtype=torch.float32, device=(xs[0] if xs else y).device)
     ptrs = (C.c_void_p * max(1, p))(*[x.data_ptr() for x in xs]) if p else (C.c_void_p * 1)(0)
     _native.call("mfa_ols_resid", _native.ptr(y), ptrs, p, D, N, int(min_rows), float(sign),
-                 _native.ptr(out), _native.stream(y.device))
+                 int(log_x0), int(ypow), _native.ptr(out), _native.stream(out.device))
     return out
 
 
-def _ols_resid_ref(y, xs, min_rows, sign):
-    D, N = y.shape
+def _ols_resid_ref(y, xs, min_rows, sign, log_x0=False, ypow=0):
+    D, N = xs[0].shape if xs else y.shape
     out = torch.full((D, N), float("nan"), dtype=torch.float32)
     for d in range(D):
-        cols = [torch.ones(N, dtype=torch.float64)] + [x[d].double() for x in xs]
+        xd = [x[d].double() for x in xs]
+        if log_x0:
+            xd[0] = torch.log(xd[0])
+        cols = [torch.ones(N, dtype=torch.float64)] + xd
         Xd = torch.stack(cols, 1)
-        yd = y[d].double()
+        yd = xd[0] ** ypow if ypow > 0 else y[d].double()
         ok = torch.isfinite(yd) & torch.isfinite(Xd).all(1)
         if int(ok.sum()) < min_rows:
             continue

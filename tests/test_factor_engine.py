@@ -1,0 +1,90 @@
+"""Descriptor engine vs the reference FactorCalculator; HIP rolling kernels vs CPU oracles."""
+import contextlib
+import io
+import warnings
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from llm_driven_multi_factor_model_amd.models import factor_engine as FE
+from llm_driven_multi_factor_model_amd.ops import rolling as RL
+
+COLS = ["SIZE", "BETA", "HSIGMA", "RSTR", "DASTD", "CMRA", "NLSIZE", "BP", "STOM", "STOQ", "STOA",
+        "CETOP", "ETOP", "YOYProfit", "YOYSales", "MLEV", "DTOA", "BLEV"]
+
+
+@pytest.fixture(scope="module")
+def data():
+    return FE.synthetic_prices(N=10, T=330, seed=1, suspend_frac=0.03)
+
+
+@pytest.fixture(scope="module")
+def ref_out(ref, data):
+    prices, index, _ = data
+    warnings.simplefilter("ignore")
+    with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
+        fc = ref.factor_calculator.FactorCalculator(prices.copy(), index.copy())
+        return fc.run(FE.FACTORS_TO_RUN)
+
+
+@pytest.mark.reference
+def test_descriptors_match_reference(ref_out, data, monkeypatch):
+    prices, index, _ = data
+    eng = FE.FactorEngine(prices, index, device="cpu")
+    with contextlib.redirect_stdout(io.StringIO()):
+        out = eng.run(FE.FACTORS_TO_RUN)
+    assert list(out.columns) == list(ref_out.columns)
+    assert (out["ts_code"].values == ref_out["ts_code"].values).all()
+    assert (out["trade_date"].values == ref_out["trade_date"].values).all()
+    for c in ["ret", "circ_mv"] + COLS:
+        a, b = out[c].to_numpy(np.float64), ref_out[c].to_numpy(np.float64)
+        assert (np.isnan(a) == np.isnan(b)).all(), c
+        m = np.isfinite(b)
+        np.testing.assert_allclose(a[m], b[m], rtol=2e-4, atol=1e-6, err_msg=c)
+
+
+@pytest.mark.reference
+def test_post_processing_pipeline_matches_reference(ref, ref_out, data):
+    pp = ref.post_processing
+    cols = [c for c in ref_out.columns if c not in ("ts_code", "trade_date")]
+    with contextlib.redirect_stdout(io.StringIO()):
+        rw = pp.winsorize_factors(ref_out, cols)
+        from llm_driven_multi_factor_model_amd.utils.config import FactorConfig
+        cfg = FactorConfig()
+        rc = pp.calculate_composite_factors(rw, cfg.composite)
+        ro = pp.orthogonalize_factors(rc, cfg.ortho)
+    w = FE.winsorize_frame(ref_out, cols, device="cpu")
+    c = FE.composite_frame(w, cfg.composite, device="cpu")
+    o = FE.orthogonalize_frame(c, cfg.ortho, device="cpu")
+    for col in cols + list(cfg.composite):
+        np.testing.assert_allclose(o[col].to_numpy(np.float64), ro[col].to_numpy(np.float64), rtol=5e-4,
+                                   atol=5e-5, equal_nan=True, err_msg=col)
+
+
+def test_barra_export_schema(data):
+    prices, index, sw = data
+    with contextlib.redirect_stdout(io.StringIO()):
+        final, info, t = FE.factor_pipeline(prices, index, sw, device="cpu")
+    assert list(final.columns) == FE.BARRA_OUTPUT_COLUMNS
+    assert list(info.columns) == ["code", "industry_names", "start_date"]
+    # t+1 return alignment: ret on the last row of each stock is NaN
+    last = final.groupby("stocknames").tail(1)
+    assert last["ret"].isna().all()
+
+
+@pytest.mark.gpu
+def test_hip_rolling_kernels_match_cpu(cuda):
+    prices, index, _ = FE.synthetic_prices(N=24, T=600, seed=3, suspend_frac=0.05)
+    cpu = FE.FactorEngine(prices, index, device="cpu")
+    gpu = FE.FactorEngine(prices, index, device=cuda)
+    with contextlib.redirect_stdout(io.StringIO()):
+        a = cpu.compute(FE.FACTORS_TO_RUN)
+        b = gpu.compute(FE.FACTORS_TO_RUN)
+    for k in a:
+        torch.testing.assert_close(b[k].cpu().float(), a[k].float(), rtol=2e-5, atol=1e-6, equal_nan=True,
+                                   msg=k)
+    lr = cpu.cols["log_ret"]
+    torch.testing.assert_close(RL.cmra(lr.to(cuda), cpu.seg_lo.to(cuda), partial=True).cpu(),
+                               RL.cmra(lr, cpu.seg_lo, partial=True), rtol=1e-5, atol=1e-6, equal_nan=True)
