@@ -1,0 +1,86 @@
+"""load_data.py compatibility API: MongoDB loads + point-in-time assembly.
+
+``load_and_prepare_data(db=None)`` reproduces the reference flow (load_data.py:66-431):
+constituents of the newest ``index_components`` snapshot, 6 collection loads with the same
+filters/projections, statement dedupe, three as-of merges (native two-pointer join instead of
+the per-stock Python loop), ffill + fill.  ``db`` may be any object with pymongo's
+``db[name].find(query, projection)`` / ``find_one(filter, sort=...)`` surface (tests use an
+in-memory fake); by default a ``pymongo.MongoClient`` is opened from MFA_MONGO_URI.
+"""
+from __future__ import annotations
+
+from datetime import date
+
+import pandas as pd
+
+from llm_driven_multi_factor_model_amd.utils.pit import (dedupe_statements, fill_missing,
+                                                         optimize_dtypes, robust_merge_asof)
+
+from . import config
+
+__all__ = ["optimize_dtypes", "load_collection_to_df", "robust_merge_asof", "load_and_prepare_data"]
+
+
+def load_collection_to_df(db, collection_name: str, query: dict, projection: dict) -> pd.DataFrame:
+    print(f"正在从 '{collection_name}' 加载数据...")
+    df = pd.DataFrame(list(db[collection_name].find(query, projection)))
+    if not df.empty:
+        df = optimize_dtypes(df)
+    print(f"-> 成功加载 {len(df):,} 行数据。")
+    return df
+
+
+def load_and_prepare_data(db=None, index_code: str = "000016.SH", start_date: str = "20200101",
+                          start_date_financial: str = "20190101", end_date: str | None = None,
+                          fix_fill_order: bool = False):
+    client = None
+    if db is None:
+        from pymongo import MongoClient
+        client = MongoClient(config.MONGO_CONNECTION_STRING)
+        db = client[config.DB_NAME]
+    end = end_date or date.today().strftime("%Y%m%d")
+    latest = db["index_components"].find_one({"index_code": index_code}, sort=[("trade_date", -1)])
+    if not latest:
+        raise RuntimeError(f"no index_components for {index_code}")
+    cons = load_collection_to_df(db, "index_components",
+                                 {"index_code": index_code, "trade_date": latest["trade_date"]},
+                                 {"con_code": 1, "_id": 0})["con_code"].tolist()
+    px = load_collection_to_df(db, "daily_prices",
+                               {"ts_code": {"$in": cons}, "trade_date": {"$gte": start_date, "$lte": end}},
+                               {k: 1 for k in ["ts_code", "trade_date", "close", "total_mv", "circ_mv", "pb",
+                                               "turnover_rate", "pe_ttm"]} | {"_id": 0})
+    fq = {"ts_code": {"$in": cons}, "end_date": {"$gte": start_date_financial, "$lte": end}}
+    cf = load_collection_to_df(db, "cashflow", fq, {"ts_code": 1, "f_ann_date": 1, "end_date": 1,
+                                                    "n_cashflow_act": 1, "_id": 0})
+    fi = load_collection_to_df(db, "financial_indicators", fq,
+                               {"ts_code": 1, "ann_date": 1, "end_date": 1, "q_profit_yoy": 1,
+                                "q_sales_yoy": 1, "debt_to_assets": 1, "_id": 0})
+    bs = load_collection_to_df(db, "balancesheet", fq, {"ts_code": 1, "f_ann_date": 1, "end_date": 1,
+                                                        "total_ncl": 1, "total_hldr_eqy_inc_min_int": 1,
+                                                        "_id": 0})
+    ix = load_collection_to_df(db, "index_daily_prices",
+                               {"ts_code": index_code, "trade_date": {"$gte": start_date, "$lte": end}},
+                               {"ts_code": 1, "trade_date": 1, "close": 1, "_id": 0})
+    sw = load_collection_to_df(db, "sw_industries", {},
+                               {"ts_code": 1, "l1_code": 1, "l1_name": 1, "in_date": 1, "out_date": 1,
+                                "is_new": 1, "_id": 0})
+    cf, bs = dedupe_statements(cf, "f_ann_date"), dedupe_statements(bs, "f_ann_date")
+    fi = dedupe_statements(fi, "ann_date")
+    px = px.copy()
+    px["trade_date"] = pd.to_datetime(px["trade_date"].astype(str), format="%Y%m%d")
+    ix = ix.copy()
+    ix["trade_date"] = pd.to_datetime(ix["trade_date"].astype(str), format="%Y%m%d")
+    m1 = robust_merge_asof(px, bs, "trade_date", "f_ann_date", "ts_code").rename(
+        columns={"f_ann_date": "balance_sheet_f_ann_date"})
+    m2 = robust_merge_asof(m1, fi, "trade_date", "ann_date", "ts_code").rename(
+        columns={"ann_date": "financial_indicators_ann_date"})
+    m3 = robust_merge_asof(m2, cf, "trade_date", "f_ann_date", "ts_code").rename(
+        columns={"f_ann_date": "cashflow_f_ann_date"})
+    m3 = m3.drop(columns=[c for c in ["end_date_y", "end_date_x"] if c in m3.columns])
+    out = fill_missing(m3, fix_order=fix_fill_order)
+    for c in ["end_date", "balance_sheet_f_ann_date", "financial_indicators_ann_date", "cashflow_f_ann_date"]:
+        if c in out.columns:
+            out[c] = pd.to_datetime(out[c], errors="coerce")
+    if client is not None:
+        client.close()
+    return out, ix, sw

@@ -247,12 +247,13 @@ class _Grid:
     def __init__(self, df: pd.DataFrame, device):
         self.device = device
         dcodes, self.dates = pd.factorize(df["trade_date"], sort=True)
-        key = df["ts_code"].astype(str) if "ts_code" in df.columns else pd.Series(np.arange(len(df)))
-        scodes, self.stocks = pd.factorize(key, sort=True)
+        if "ts_code" in df.columns and not df.duplicated(["trade_date", "ts_code"]).any():
+            scodes, self.stocks = pd.factorize(df["ts_code"].astype(str), sort=True)
+        else:  # no stock key (or duplicates): the row's rank within its date is its column
+            scodes = df.groupby("trade_date").cumcount().to_numpy()
+            self.stocks = np.arange(int(scodes.max()) + 1 if len(scodes) else 0)
         self.D, self.N = len(self.dates), len(self.stocks)
         self.idx = torch.from_numpy(dcodes.astype(np.int64) * self.N + scodes.astype(np.int64)).to(device)
-        if pd.Index(self.idx.cpu().numpy()).has_duplicates:
-            raise ValueError("duplicate (trade_date, ts_code) rows")
 
     def put(self, col: np.ndarray) -> torch.Tensor:
         g = torch.full((self.D * self.N,), float("nan"), dtype=torch.float32, device=self.device)

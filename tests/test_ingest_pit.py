@@ -1,0 +1,134 @@
+"""PIT assembly (native as-of join, dedupe, fill), Mongo loaders and ingestion updaters (offline)."""
+import contextlib
+import io
+
+import numpy as np
+import pandas as pd
+import pytest
+
+from llm_driven_multi_factor_model_amd.utils import pit
+from tests._fakemongo import FakeDB
+
+
+def _ref_merge_asof(left_df, right_df, left_on, right_on, by):
+    """load_data.py:41-62 per-stock loop (the reference algorithm, reproduced for comparison)."""
+    left_df = left_df.reset_index(drop=True).sort_values(by=[by, left_on])
+    right_df = right_df.reset_index(drop=True).sort_values(by=[by, right_on])
+    chunks = []
+    for key in left_df[by].unique():
+        chunks.append(pd.merge_asof(left=left_df[left_df[by] == key], right=right_df[right_df[by] == key],
+                                    left_on=left_on, right_on=right_on, by=by, direction="backward"))
+    return pd.concat(chunks, ignore_index=True)
+
+
+def _frames(seed=0, n=30, days=120):
+    rng = np.random.default_rng(seed)
+    codes = [f"{i:06d}.SZ" for i in range(n)]
+    dates = pd.bdate_range("2020-01-01", periods=days)
+    px = pd.DataFrame([(c, d, rng.random()) for c in codes for d in dates if rng.random() > 0.05],
+                      columns=["ts_code", "trade_date", "close"])
+    rows = []
+    for c in codes[:-2]:  # two stocks without statements
+        for q in pd.date_range("2019-09-30", periods=4, freq="QE"):
+            ann = q + pd.Timedelta(days=int(rng.integers(20, 100)))
+            rows.append((c, ann, q.strftime("%Y%m%d"), rng.normal()))
+    st = pd.DataFrame(rows, columns=["ts_code", "f_ann_date", "end_date", "n_cashflow_act"])
+    return px, st
+
+
+def test_native_asof_matches_reference_loop():
+    px, st = _frames()
+    a = pit.robust_merge_asof(px, st, "trade_date", "f_ann_date", "ts_code")
+    b = _ref_merge_asof(px, st, "trade_date", "f_ann_date", "ts_code")
+    assert list(a.columns) == list(b.columns)
+    pd.testing.assert_frame_equal(a.reset_index(drop=True), b.reset_index(drop=True), check_dtype=False)
+
+
+def test_asof_indices_semantics():
+    out = pit.asof_indices([0, 0, 0, 1, 1], [5, 10, 15, 1, 7], [0, 0, 1], [6, 10, 3])
+    assert out.tolist() == [-1, 1, 1, -1, 2]
+
+
+def test_dedupe_and_fill_quirk():
+    st = pd.DataFrame({"ts_code": ["a", "a", "a"], "f_ann_date": ["20200410", "20200420", "20200420"],
+                       "end_date": ["20200331", "20200331", "20191231"], "v": [1.0, 2.0, 3.0]})
+    d = pit.dedupe_statements(st)
+    assert len(d) == 1 and d["v"].iloc[0] == 2.0  # latest announcement of the latest period
+    df = pd.DataFrame({"ts_code": ["a", "a", "b", "b"], "trade_date": [1, 2, 1, 2],
+                       "pb": [np.nan, 2.0, 4.0, np.nan]})
+    assert pit.fill_missing(df, ["pb"])["pb"].tolist() == [0.0, 2.0, 4.0, 4.0]       # Q19: zero first
+    assert pit.fill_missing(df, ["pb"], fix_order=True)["pb"].tolist() == [4.0, 2.0, 4.0, 4.0]
+
+
+def _seed_db():
+    db = FakeDB()
+    rng = np.random.default_rng(1)
+    codes = ["000001.SZ", "000002.SZ", "600000.SH"]
+    db["index_components"].insert_many([{"index_code": "000016.SH", "trade_date": "20200301", "con_code": c}
+                                        for c in codes])
+    days = pd.bdate_range("2020-01-02", periods=40).strftime("%Y%m%d")
+    db["daily_prices"].insert_many([{"ts_code": c, "trade_date": d, "close": 10 + rng.random(),
+                                     "total_mv": 1e6, "circ_mv": 5e5, "pb": 1.5, "turnover_rate": 1.0,
+                                     "pe_ttm": 12.0} for c in codes for d in days])
+    db["index_daily_prices"].insert_many([{"ts_code": "000016.SH", "trade_date": d, "close": 3000 + i}
+                                          for i, d in enumerate(days)])
+    for name, ann, cols in [("cashflow", "f_ann_date", {"n_cashflow_act": 1e7}),
+                            ("balancesheet", "f_ann_date", {"total_ncl": 2e8, "total_hldr_eqy_inc_min_int": 5e8}),
+                            ("financial_indicators", "ann_date", {"q_profit_yoy": 5.0, "q_sales_yoy": 3.0,
+                                                                  "debt_to_assets": 40.0})]:
+        db[name].insert_many([dict({"ts_code": c, ann: "20200115", "end_date": "20191231"}, **cols) for c in codes])
+    db["sw_industries"].insert_many([{"ts_code": c, "l1_code": "801780.SI", "l1_name": "bank", "in_date": "20000101",
+                                      "out_date": None, "is_new": "Y"} for c in codes])
+    return db
+
+
+def test_load_and_prepare_data_with_fake_mongo():
+    from barra_factor_cal import load_data
+    with contextlib.redirect_stdout(io.StringIO()):
+        stk, idx, sw = load_data.load_and_prepare_data(_seed_db(), end_date="20201231")
+    assert len(stk) == 120 and set(["n_cashflow_act", "total_ncl", "q_profit_yoy", "end_date"]) <= set(stk.columns)
+    early = stk[stk.trade_date < pd.Timestamp("2020-01-15")]
+    assert (early["n_cashflow_act"] == 0).all()     # not yet announced -> fillna(0)
+    late = stk[stk.trade_date >= pd.Timestamp("2020-01-15")]
+    assert np.allclose(late["n_cashflow_act"], 1e7)
+    assert str(stk["ts_code"].dtype) == "category" or stk["ts_code"].dtype == object
+
+
+class _Fetcher:
+    def __init__(self):
+        self.calls = 0
+
+    def fetch_cashflow_by_stock(self, code):
+        self.calls += 1
+        if self.calls == 2:
+            raise RuntimeError("transient")
+        return pd.DataFrame({"ts_code": [code], "end_date": ["20200331"], "n_cashflow_act": [1.0]})
+
+    def fetch_trade_calendar(self, s, e):
+        return ["20200102", "20200103"]
+
+    def fetch_daily_basic_by_date(self, d):
+        return pd.DataFrame({"ts_code": ["a", "b"], "trade_date": [d, d], "close": [1.0, 2.0]})
+
+
+def test_updaters_rate_limit_retry_and_resume():
+    from barra_database import update_mongo_db as U
+    db = FakeDB()
+    sleeps = []
+    t = [0.0]
+    f = _Fetcher()
+    with contextlib.redirect_stdout(io.StringIO()):
+        n = U.update_cashflow(db, [f"{i:06d}.SZ" for i in range(5)], fetcher=f, sleep=sleeps.append,
+                              clock=lambda: t[0])
+    assert n == 5 and len(db["cashflow"].docs) == 5 and 5.0 in sleeps  # retried after 5 s
+    with contextlib.redirect_stdout(io.StringIO()):
+        assert U.update_daily_prices(db, fetcher=f, sleep=lambda s: None,
+                                     today=pd.Timestamp("2020-01-03").date()) == 4
+    from barra_database.ingest import RateLimiter, get_last_update_date
+    assert get_last_update_date(db, "daily_prices") == pd.Timestamp("2020-01-03")
+    slept = []
+    rl = RateLimiter(2, clock=lambda: 10.0, sleep=slept.append, start=0.0)
+    for _ in range(3):
+        rl.acquire()
+        rl.done()
+    assert slept and slept[0] == pytest.approx(51.0)
