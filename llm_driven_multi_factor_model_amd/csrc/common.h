@@ -34,6 +34,38 @@ __device__ __forceinline__ int wave_sum(int v) {
   return v;
 }
 
+// ---- DPP (VALU-only) cross-lane reductions: no LDS traffic, a few cycles per step --------
+// gfx9 dpp_ctrl encodings: quad_perm 0x00-0xFF, row_mirror 0x140, row_half_mirror 0x141.
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+// Sum over each row of 16 lanes; every lane of the row gets the same bits.
+__device__ __forceinline__ double row16_sum(double v) {
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]  (lane ^ 1)
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]  (lane ^ 2)
+  v += dpp_mov<0x141>(v);  // row_half_mirror      (quad 0 <-> quad 1)
+  v += dpp_mov<0x140>(v);  // row_mirror           (half 0 <-> half 1)
+  return v;
+}
+
+__device__ __forceinline__ double readlane(double v, int l) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+// Wave-uniform (SGPR) total over all 64 lanes, deterministic order.
+__device__ __forceinline__ double wave_total(double v) {
+  v = row16_sum(v);
+  return (readlane(v, 0) + readlane(v, 16)) + (readlane(v, 32) + readlane(v, 48));
+}
+
 __device__ __forceinline__ double wave_max(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v = fmax(v, __shfl_xor(v, off, kWave));

@@ -6,12 +6,13 @@
 // unweighted R^2).  Nothing mirrors the reference's dense N x N weight matrix.
 //
 // Three kernels, each shaped for its own regime, all dates of a shard per launch:
-//   K1 xs_moments   HBM streaming.  One 4-wave workgroup per date; [D][Q][N] fp32 styles,
-//                   caps, returns and int16 industry ids stream through a 3-deep LDS ring filled
-//                   by global_load_lds_dwordx4 (counted vmcnt + raw s_barrier, so two tiles stay
-//                   in flight across barriers).  RAW fp64 moments accumulate in registers; the
-//                   one-hot industry block is a segmented sum done with ds_add_f64 into 4 lane-
-//                   interleaved replicas of a [P][Q+3] table (4x fewer same-address conflicts).
+//   K1 xs_moments   HBM streaming.  One 4-wave workgroup per date; every wave streams its own
+//                   64-stock tiles of the [D][Q][N] fp32 styles, caps, returns and int16
+//                   industry ids through a private 4-slot LDS ring filled by
+//                   global_load_lds_dword (counted vmcnt, no workgroup barrier until the date's
+//                   final reduction).  RAW fp64 moments accumulate in registers; the one-hot
+//                   industry block is a segmented sum done with ds_add_f64 into an 8-way
+//                   replicated [P][Q+3] table laid out so one issue group is <= 2-way conflicted.
 //                   z-scoring is folded in algebraically later, so the data is read once.
 //   K2 xs_solve     latency-bound tiny algebra.  One wave per date: after eliminating the pivot
 //                   industry the industry block is diag(W) + rho a a^T (Sherman-Morrison), and
@@ -106,7 +107,12 @@ __device__ __forceinline__ double pick(const double (&a)[Q], int i) {
 
 constexpr int kTile = 256;            // stocks per staged tile (K3)
 constexpr int kRowBytes = kTile * 4;  // one fp32 field row of a tile
-constexpr int kRep = 4;               // segment-table replicas (lane & 3)
+// Segment-table replicas: entry (j, ch) owns R consecutive doubles and lane l adds into slot
+// l & (R-1).  With R = 8 the 16 lanes of a ds_add_f64 issue group land on bank pairs
+// (l & 7) + 8 * ((j*NS + ch) & 1): at most 2-way conflicts whatever the industry mix (4
+// lane-strided replicas measured 8.3 conflict cycles per instruction).
+constexpr int kRepMax = 8;
+constexpr int kSegLdsBudget = 48 * 1024;  // R = 8 only while the table leaves 2 WGs / CU
 constexpr int kWT = 64;               // stocks per wave tile (K1: one stock per lane)
 constexpr int kWNB = 4;               // K1 per-wave ring depth
 
@@ -147,7 +153,7 @@ __device__ __forceinline__ void wg_reduce(const double (&v)[CNT], double* wbuf, 
 // ------------------------------------------------------------------------------------------
 // K1: raw moments.  mom[d] = [ Swxx(NG) | Swxr(Q) | Scx(Q) | Sc Sx Sxx n | seg[Pseg][NS] ]
 // ------------------------------------------------------------------------------------------
-template <int Q, int VAR>
+template <int Q, int VAR, int R>
 __global__ __launch_bounds__(256) void xs_moments_kernel(
     const float* __restrict__ X, const float* __restrict__ cap, const float* __restrict__ ret,
     const int16_t* __restrict__ ind, int N, int Pseg, double* __restrict__ mom) {
@@ -159,14 +165,13 @@ __global__ __launch_bounds__(256) void xs_moments_kernel(
   constexpr int WSLOT = L::WSLOT;
   constexpr int RINGW = kWNB * WSLOT > 8 * 65 * 8 ? kWNB * WSLOT : 8 * 65 * 8;
   __shared__ __attribute__((aligned(16))) char ring[4 * RINGW];
-  extern __shared__ double dyn[];  // [kRep][Pseg*NS + 1] replicas | [NACC] totals
+  extern __shared__ double dyn[];  // [Pseg*NS][R] replicated segment sums | [NACC] totals
   const int d = blockIdx.x;
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int lane = tid & 63, wid = tid >> 6, nw = nthr >> 6;
-  const int rstride = Pseg * NS + 1;  // odd stride spreads the replicas over banks
-  const unsigned seg_a = lds_addr(dyn + (lane & (kRep - 1)) * rstride);
-  double* acc = dyn + kRep * rstride;
-  for (int i = tid; i < kRep * rstride + NACC; i += nthr) dyn[i] = 0.0;
+  const unsigned seg_a = lds_addr(dyn + (lane & (R - 1)));
+  double* acc = dyn + R * Pseg * NS;
+  for (int i = tid; i < R * Pseg * NS + NACC; i += nthr) dyn[i] = 0.0;
   __syncthreads();
 
   const float* Xd = X + (size_t)d * Q * N;
@@ -215,10 +220,15 @@ __global__ __launch_bounds__(256) void xs_moments_kernel(
       double x[Q], wx[Q];
 #pragma unroll
       for (int q = 0; q < Q; ++q) { x[q] = xf[q]; wx[q] = w * x[q]; }
+      if constexpr ((VAR & 2) != 0) {  // timing-only ablation: skip the moment FMAs
+#pragma unroll
+        for (int q = 0; q < Q; ++q) asm volatile("" ::"v"(wx[q]));
+      } else {
 #pragma unroll
       for (int q = 0; q < Q; ++q)
 #pragma unroll
         for (int t = 0; t <= q; ++t) v[q * (q + 1) / 2 + t] = fma(wx[q], x[t], v[q * (q + 1) / 2 + t]);
+      }
       double sx = 0.0, sxx = 0.0;
 #pragma unroll
       for (int q = 0; q < Q; ++q) {
@@ -234,13 +244,13 @@ __global__ __launch_bounds__(256) void xs_moments_kernel(
       if (VAR & 1) {  // timing-only ablation: skip the segment atomics
         asm volatile("" ::"v"(w), "v"(r));
       } else {
-        const unsigned a = seg_a + (unsigned)(j * NS * 8);
+        const unsigned a = seg_a + (unsigned)(j * NS * R * 8);
         lds_add_nowait<0>(a, w);
         [&]<int... I>(std::integer_sequence<int, I...>) {
-          (lds_add_nowait<8 * (1 + I)>(a, wx[I]), ...);
+          (lds_add_nowait<8 * R * (1 + I)>(a, wx[I]), ...);
         }(std::make_integer_sequence<int, Q>{});
-        lds_add_nowait<8 * (Q + 1)>(a, w * r);
-        lds_add_nowait<8 * (Q + 2)>(a, c);
+        lds_add_nowait<8 * R * (Q + 1)>(a, w * r);
+        lds_add_nowait<8 * R * (Q + 2)>(a, c);
       }
     }
   }
@@ -253,7 +263,7 @@ __global__ __launch_bounds__(256) void xs_moments_kernel(
   for (int i = tid; i < Pseg * NS; i += nthr) {
     double t = 0.0;
 #pragma unroll
-    for (int r = 0; r < kRep; ++r) t += dyn[r * rstride + i];
+    for (int r = 0; r < R; ++r) t += dyn[i * R + r];
     md[NACC + i] = t;
   }
 }
@@ -261,27 +271,55 @@ __global__ __launch_bounds__(256) void xs_moments_kernel(
 // ------------------------------------------------------------------------------------------
 // K2: structured constrained solve, one wave per date.
 // coef[d] = [ beta_q (Q) | cst | f_ind (P) ]  for the residual pass (e = r - cst - f_j - b.x)
+//
+// Algebra (CrossSection.py:57-106 with the constraint substituted): with g_j the standardised
+// industry row [W_j, (A_jq - mu_q W_j)/sigma, B_j], pivot p, a_j = -s_j/s_p and
+// m_j = g_j + a_j g_p for the active industries, the industry block is diag(W) + rho a a^T and
+//   S   = M_DD - G + kappa at at^T,    G = sum_j m_j m_j^T / W_j,   at = sum_j a_j m_j / W_j,
+//   kappa = rho / (1 + rho c0),        c0 = sum_j a_j^2 / W_j,
+//   f_j = (m_j . h - kappa a_j z) / W_j,  f_p = z (1 - kappa c0),  h = [-g_D, 1],  z = at . h.
+// G, at, c0 and the industry totals are ONE weighted Gram over industries with augmented
+// channels [m | a | 1], computed by v_mfma_f64_16x16x4f64 straight from the moments in LDS
+// (A[i][k] from lane i + 16k, B[k][j] from lane j + 16k, D[(l>>4) + 4r][l&15] in register r
+// -- layout probed in tools/probes/mfma64_probe.hip).  Only the (1+Q)^2 Cholesky is serial; it
+// runs redundantly in every lane's registers.  All dates are resident at once, so the kernel
+// time is one date's critical path.
 // ------------------------------------------------------------------------------------------
+typedef double v4d __attribute__((ext_vector_type(4)));
+
 template <int Q>
 __global__ __launch_bounds__(64) void xs_solve_kernel(const double* __restrict__ mom, int P,
                                                       int Pseg, int pivot_mode, double tol,
                                                       double* __restrict__ fout,
                                                       double* __restrict__ coef,
                                                       double* __restrict__ stats,
-                                                      int* __restrict__ status) {
+                                                      int* __restrict__ status,
+                                                      long long* __restrict__ stamps) {
   using L = Layout<Q>;
   constexpr int NS = L::NS, NG = L::NG, NACC = L::NACC, ND = L::ND;
+  constexpr int NC = ND + 1;              // standardised industry row incl. the rhs
+  constexpr int CH = NC + 2;              // Gram channels: m (NC) | a | 1
+  constexpr int TT = (CH + 15) / 16;      // MFMA tiles per dimension
+  static_assert(TT <= 2, "Q <= 28");
+  // optional phase timestamps (s_memtime, core clocks) for latency attribution
+  auto stamp = [&](int k) {
+    if (stamps && threadIdx.x == 0) stamps[(size_t)blockIdx.x * 8 + k] = __builtin_amdgcn_s_memtime();
+  };
+  stamp(0);
   extern __shared__ double sm[];
   const int d = blockIdx.x;
   const int lane = threadIdx.x;
   const int K = 1 + P + Q;
   const int MS = L::msize(Pseg);
-  double* acc = sm;                   // [NACC]
-  double* seg = sm + NACC;            // [Pseg][NS]   (A_q standardised in place)
-  double* MID = seg + Pseg * NS;      // [Pseg][ND+1] M_ID | h_I
-  double* S = MID + Pseg * (ND + 1);  // [ND][ND+1]   Schur complement | rhs
-  double* fsh = S + ND * (ND + 1);    // [K]
-  double* Yb = fsh + K;               // [Pseg][ND+1] M_II^{-1} [M_ID | h_I]
+  const int P4 = (Pseg + 3) & ~3;         // industries padded to the MFMA k-step
+  double* acc = sm;                       // [NACC]
+  double* seg = sm + NACC;                // [Pseg][NS]  W, A_q, B, s
+  double* Gs = sm + MS;                   // [CH][CH]    Gram over industries
+  double* S = Gs + CH * CH;               // [ND][NC]    Schur complement | rhs
+  double* gpv = S + ND * NC;              // [NC]        standardised pivot row
+  double* muv = gpv + NC;                 // [Q]
+  double* ajv = muv + Q;                  // [P4]        a_j
+  double* iwv = ajv + P4;                 // [P4]        1 / W_j
   const double* md = mom + (size_t)d * MS;
   for (int i0 = 0; i0 < MS; i0 += 8 * 64) {  // 8 independent loads in flight per lane
     double tmp[8];
@@ -297,6 +335,7 @@ __global__ __launch_bounds__(64) void xs_solve_kernel(const double* __restrict__
     }
   }
   wave_sync_lds();
+  stamp(1);
 
   const double Sc = acc[NG + 2 * Q + 0];
   const double nval = acc[NG + 2 * Q + 3];
@@ -304,35 +343,10 @@ __global__ __launch_bounds__(64) void xs_solve_kernel(const double* __restrict__
   const double mx = acc[NG + 2 * Q + 1] / nq;
   const double sigma = sqrt(fmax(acc[NG + 2 * Q + 2] / nq - mx * mx, 0.0));
   const double isig = 1.0 / sigma;
+  const double iSc = 1.0 / Sc;
   int st = 0;
   if (!(nval > 0.0)) st |= XS_NO_ROWS;
   if (!(sigma > 0.0) || !__builtin_isfinite(sigma)) st |= XS_BAD_SIGMA;
-
-  // industry totals (lane-strided partials + butterfly)
-  double Sw = 0.0, Swr = 0.0, Swx[Q], mu[Q];
-#pragma unroll
-  for (int q = 0; q < Q; ++q) Swx[q] = 0.0;
-  for (int j = lane; j < Pseg; j += 64) {
-    const double* p = seg + j * NS;
-    Sw += p[0];
-    Swr += p[Q + 1];
-#pragma unroll
-    for (int q = 0; q < Q; ++q) Swx[q] += p[1 + q];
-  }
-  Sw = wave_sum(Sw);
-  Swr = wave_sum(Swr);
-#pragma unroll
-  for (int q = 0; q < Q; ++q) {
-    Swx[q] = wave_sum(Swx[q]);
-    mu[q] = acc[NG + Q + q] / Sc;
-  }
-  // standardise the segmented style sums in place: A'_jq = (A_jq - mu_q W_j) / sigma
-  for (int j = lane; j < Pseg; j += 64) {
-    double* p = seg + j * NS;
-#pragma unroll
-    for (int q = 0; q < Q; ++q) p[1 + q] = (p[1 + q] - mu[q] * p[0]) * isig;
-  }
-  wave_sync_lds();
 
   // pivot industry (reference: always the last one, CrossSection.py:69)
   int jp = -1;
@@ -349,180 +363,211 @@ __global__ __launch_bounds__(64) void xs_solve_kernel(const double* __restrict__
     }
     if (!(seg[jp * NS + Q + 2] > 0.0)) st |= XS_PIVOT_EMPTY;
   }
-  const double sp = P > 0 ? seg[jp * NS + Q + 2] : 1.0;
-  const double rho = P > 0 ? seg[jp * NS] : 0.0;
+  const int rp = P > 0 ? jp : 0;          // P == 0: the single segment holds the totals
+  const double sp = P > 0 ? seg[rp * NS + Q + 2] : 1.0;
+  const double rho = P > 0 ? seg[rp * NS] : 0.0;
+  const double isp = 1.0 / sp;
 
-  // M_ID rows (lane = industry): M_ID[j][u] = G[j][u] + a_j G[p][u], h_I = B_j + a_j B_p,
-  // Y = M_II^{-1} [M_ID | h_I] with M_II = diag(W) + rho a a^T (Sherman-Morrison).
-  double den = 0.0, at[ND + 1];
+  // this lane's Gram channels c = t*16 + (lane & 15): mean and pivot-row value
+  const int li = lane & 15, lk = lane >> 4;
+  double muc[TT], gpc[TT];
 #pragma unroll
-  for (int u = 0; u <= ND; ++u) at[u] = 0.0;
-  for (int j = lane; j < P; j += 64) {
-    const double* p = seg + j * NS;
-    const double* pp = seg + jp * NS;
+  for (int t = 0; t < TT; ++t) {
+    const int c = t * 16 + li;
+    muc[t] = (c >= 1 && c <= Q) ? acc[NG + Q + c - 1] * iSc : 0.0;
+    const double W = seg[rp * NS];
+    const double raw = c < NC ? seg[rp * NS + c] : 0.0;
+    gpc[t] = (c >= 1 && c <= Q) ? (raw - muc[t] * W) * isig : raw;
+    if (lk == 0 && c < NC) gpv[c] = gpc[t];
+    if (lk == 0 && c >= 1 && c <= Q) muv[c - 1] = muc[t];
+  }
+
+  // per-industry scalars once, lane-parallel: a_j and 1/W_j (0 for pivot / empty / padding)
+  for (int j = lane; j < P4; j += 64) {
+    const double W = j < P ? seg[j * NS] : 0.0;
+    const bool act = (j < P) && (j != jp) && (W > 0.0);
+    ajv[j] = act ? -seg[j * NS + Q + 2] * isp : 0.0;
+    iwv[j] = act ? 1.0 / W : 0.0;
+  }
+  wave_sync_lds();
+
+  // Gram over active industries: A = [m/W | a/W | 1], B = [m | a | 0]
+  v4d G[TT][TT];
+#pragma unroll
+  for (int ti = 0; ti < TT; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < TT; ++tj) G[ti][tj] = v4d{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+  for (int k0 = 0; k0 < P4; k0 += 4) {
+    const int j = k0 + lk;
+    const double* p = seg + (j < P ? j : 0) * NS;
     const double W = p[0];
-    const bool act = (j != jp) && (W > 0.0);
-    const double aj = act ? -p[Q + 2] / sp : 0.0;
-    const double iW = act ? 1.0 / W : 0.0;
-    double* row = MID + j * (ND + 1);
-    double m[ND + 1];
-    m[0] = act ? W + aj * pp[0] : 0.0;
+    const double aj = ajv[j], iW = iwv[j];
+    const bool act = iW != 0.0;
+    double av[TT], bv[TT];
 #pragma unroll
-    for (int q = 0; q < Q; ++q) m[1 + q] = act ? p[1 + q] + aj * pp[1 + q] : 0.0;
-    m[ND] = act ? p[Q + 1] + aj * pp[Q + 1] : 0.0;
-#pragma unroll
-    for (int u = 0; u <= ND; ++u) {
-      row[u] = m[u];
-      at[u] = fma(aj, m[u] * iW, at[u]);
+    for (int t = 0; t < TT; ++t) {
+      const int c = t * 16 + li;
+      const double raw = c < NC ? p[c] : 0.0;
+      const double g = (c >= 1 && c <= Q) ? (raw - muc[t] * W) * isig : raw;
+      const double m = g + aj * gpc[t];
+      const double v = c < NC ? m : (c == NC ? aj : 0.0);
+      bv[t] = act ? v : 0.0;
+      av[t] = act ? (c == NC + 1 ? 1.0 : v * iW) : 0.0;
     }
-    den = fma(aj * rho, aj * iW, den);
-  }
-  den = wave_sum(den);
 #pragma unroll
-  for (int u = 0; u <= ND; ++u) at[u] = wave_sum(at[u]);
-  const double kappa = rho / (1.0 + den);
-  wave_sync_lds();
-  for (int j = lane; j < P; j += 64) {
-    const double* p = seg + j * NS;
-    const double W = p[0];
-    const bool act = (j != jp) && (W > 0.0);
-    const double aj = act ? -p[Q + 2] / sp : 0.0;
-    const double iW = act ? 1.0 / W : 0.0;
-    const double* row = MID + j * (ND + 1);
-    double* y = Yb + j * (ND + 1);
+    for (int ti = 0; ti < TT; ++ti)
 #pragma unroll
-    for (int u = 0; u <= ND; ++u) y[u] = act ? (row[u] - kappa * at[u] * aj) * iW : 0.0;
+      for (int tj = 0; tj < TT; ++tj)
+        G[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ti], bv[tj], G[ti][tj], 0, 0, 0);
   }
+#pragma unroll
+  for (int ti = 0; ti < TT; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < TT; ++tj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = ti * 16 + lk + 4 * r, w = tj * 16 + li;
+        if (i < CH && w < CH) Gs[i * CH + w] = G[ti][tj][r];
+      }
   wave_sync_lds();
+  stamp(2);
 
-  // dense block (country + z-scored styles) and Schur complement:
-  //   S[u][w] = M_DD[u][w] - sum_j M_ID[j][u] Y[j][w]   (w = ND is the rhs column)
-  for (int e = lane; e < ND * (ND + 1); e += 64) {
-    const int u = e / (ND + 1), w = e % (ND + 1);
-    double m;
-    if (w == ND) {
-      m = u == 0 ? Swr : (acc[NG + u - 1] - pick<Q>(mu, u - 1) * Swr) * isig;
-    } else if (u == 0 && w == 0) {
-      m = Sw;
-    } else if (u == 0 || w == 0) {
-      const int q = (u == 0 ? w : u) - 1;
-      m = (pick<Q>(Swx, q) - pick<Q>(mu, q) * Sw) * isig;
-    } else {
-      const int q = u - 1, s = w - 1;
-      const int hi = q > s ? q : s, lo = q > s ? s : q;
-      const double muq = pick<Q>(mu, q), mus = pick<Q>(mu, s);
-      m = (acc[hi * (hi + 1) / 2 + lo] - muq * pick<Q>(Swx, s) - mus * pick<Q>(Swx, q) +
-           muq * mus * Sw) * isig * isig;
-    }
-    double t0 = 0.0, t1 = 0.0, t2 = 0.0, t3 = 0.0;
-    int j = 0;
-    for (; j + 4 <= P; j += 4) {
-      t0 = fma(MID[(j + 0) * (ND + 1) + u], Yb[(j + 0) * (ND + 1) + w], t0);
-      t1 = fma(MID[(j + 1) * (ND + 1) + u], Yb[(j + 1) * (ND + 1) + w], t1);
-      t2 = fma(MID[(j + 2) * (ND + 1) + u], Yb[(j + 2) * (ND + 1) + w], t2);
-      t3 = fma(MID[(j + 3) * (ND + 1) + u], Yb[(j + 3) * (ND + 1) + w], t3);
-    }
-    for (; j < P; ++j) t0 = fma(MID[j * (ND + 1) + u], Yb[j * (ND + 1) + w], t0);
-    S[e] = m - ((t0 + t1) + (t2 + t3));
-  }
-  wave_sync_lds();
-
-  // Cholesky of the ND x ND Schur complement: lane i holds row i in registers
-  double row[ND], Lkk[ND];
+  // uniform scalars; S = M_DD - G + kappa at at^T in the MFMA output layout
+  const double c0 = Gs[NC * CH + NC];
+  const double kappa = rho / (1.0 + rho * c0);
+  const double sa = Gs[(NC + 1) * CH + NC];  // sum of a_j over active industries
+  // industry totals of the standardised rows: sum_active m + (1 - sum a) g_p
+  auto tot = [&](int w) { return Gs[(NC + 1) * CH + w] + (1.0 - sa) * gpv[w]; };
+  const double Sw = tot(0);
 #pragma unroll
-  for (int w = 0; w < ND; ++w) row[w] = lane < ND ? S[lane * (ND + 1) + w] : 0.0;
-  double yv = lane < ND ? S[lane * (ND + 1) + ND] : 0.0;
+  for (int ti = 0; ti < TT; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < TT; ++tj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int u = ti * 16 + lk + 4 * r, w = tj * 16 + li;
+        if (u >= ND || w >= NC) continue;
+        double m;
+        if (u == 0) {
+          m = tot(w);
+        } else if (w == 0) {
+          m = tot(u);
+        } else if (w == ND) {
+          m = acc[NG + u - 1] * isig - muv[u - 1] * isig * tot(ND);
+        } else {
+          const int q = u - 1, s2 = w - 1;
+          const int hi = q > s2 ? q : s2, lo = q > s2 ? s2 : q;
+          const double muq = muv[q], mus = muv[s2];
+          m = (acc[hi * (hi + 1) / 2 + lo] - muq * mus * Sw) * isig * isig -
+              (muq * tot(w) + mus * tot(u)) * isig;
+        }
+        S[u * NC + w] = m - G[ti][tj][r] + kappa * Gs[NC * CH + u] * Gs[NC * CH + w];
+      }
+  wave_sync_lds();
+  stamp(3);
+
+  // Cholesky of the ND x ND Schur complement, right-looking (one dependent step per column),
+  // in registers, redundantly in every lane; 1/sqrt from v_rsq_f64 + two Newton steps.
+  double Lm[ND * (ND + 1) / 2], b[ND], dorig[ND], il[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) {
+#pragma unroll
+    for (int k = 0; k <= i; ++k) Lm[i * (i + 1) / 2 + k] = S[i * NC + k];
+    b[i] = S[i * NC + ND];
+    dorig[i] = Lm[i * (i + 1) / 2 + i];
+  }
   double dmax = 0.0;
 #pragma unroll
-  for (int k = 0; k < ND; ++k) dmax = fmax(dmax, fabs(S[k * (ND + 1) + k]));
+  for (int k = 0; k < ND; ++k) dmax = fmax(dmax, fabs(dorig[k]));
   const double ztol = tol * dmax;
-  unsigned skip = 0u;
 #pragma unroll
   for (int k = 0; k < ND; ++k) {
-    const double dk = __shfl(row[k], k, 64);  // current pivot
-    const double dorig = S[k * (ND + 1) + k];
+    const double dk = Lm[k * (k + 1) / 2 + k];
     if (!(dk > ztol)) {  // pinv semantics: drop the direction (exactly singular block)
-      skip |= 1u << k;
-      st |= (dorig > ztol) ? XS_NEAR_SINGULAR : XS_ZERO_PIVOT;
-      Lkk[k] = 0.0;
-      if (lane >= k) row[k] = 0.0;
-    } else {
-      if (dk < 1e-12 * dorig) st |= XS_NEAR_SINGULAR;
-      const double l = sqrt(dk);
-      Lkk[k] = l;
-      if (lane > k) row[k] /= l;
-      if (lane == k) row[k] = l;
+      st |= (dorig[k] > ztol) ? XS_NEAR_SINGULAR : XS_ZERO_PIVOT;
+      il[k] = 0.0;
 #pragma unroll
-      for (int w = k + 1; w < ND; ++w) {  // row_i[w] -= L_ik L_wk   (k < w <= i)
-        const double lwk = __shfl(row[k], w, 64);
-        if (lane >= w) row[w] = fma(-row[k], lwk, row[w]);
-      }
+      for (int i = k; i < ND; ++i) Lm[i * (i + 1) / 2 + k] = 0.0;
+      continue;
     }
-  }
-  // forward L y = b, backward L^T g = y  (lane k holds entry k)
+    if (dk < 1e-12 * dorig[k]) st |= XS_NEAR_SINGULAR;
+    double y = __builtin_amdgcn_rsq(dk);
+    y = fma(0.5 * y, fma(-dk * y, y, 1.0), y);
+    y = fma(0.5 * y, fma(-dk * y, y, 1.0), y);
+    il[k] = y;
+    Lm[k * (k + 1) / 2 + k] = dk * y;
 #pragma unroll
-  for (int k = 0; k < ND; ++k) {
-    const double yk = ((skip >> k) & 1u) ? 0.0 : __shfl(yv, k, 64) / Lkk[k];
-    if (lane == k) yv = yk;
-    if (lane > k) yv = fma(-row[k], yk, yv);
-  }
-  double gv = yv;
+    for (int i = k + 1; i < ND; ++i) Lm[i * (i + 1) / 2 + k] *= y;
 #pragma unroll
-  for (int k = ND - 1; k >= 0; --k) {
-    const double gk = ((skip >> k) & 1u) ? 0.0 : __shfl(gv, k, 64) / Lkk[k];
-    if (lane == k) gv = gk;
+    for (int i = k + 1; i < ND; ++i)
 #pragma unroll
-    for (int i = 0; i < k; ++i) {  // g_i -= L_ki g_k ; L_ki is lane k's row[i]
-      const double lki = __shfl(row[i], k, 64);
-      if (lane == i) gv = fma(-lki, gk, gv);
-    }
-  }
-  double gD[ND];
-#pragma unroll
-  for (int u = 0; u < ND; ++u) gD[u] = __shfl(gv, u, 64);
-  // industries: g_j = Y[j][ND] - sum_u Y[j][u] g_u ; the pivot from the constraint
-  double piv = 0.0;
-  for (int j = lane; j < P; j += 64) {
-    const double* y = Yb + j * (ND + 1);
-    double g = y[ND];
-#pragma unroll
-    for (int u = 0; u < ND; ++u) g = fma(-y[u], gD[u], g);
-    if (j != jp) piv = fma(-seg[j * NS + Q + 2] / sp, g, piv);
-    fsh[1 + j] = g;
-  }
-  piv = wave_sum(piv);
-  wave_sync_lds();
-  if (lane == 0) {
-    fsh[0] = gD[0];
-    if (P > 0) fsh[1 + jp] = piv;
+      for (int c = k + 1; c <= i; ++c)
+        Lm[i * (i + 1) / 2 + c] = fma(-Lm[i * (i + 1) / 2 + k], Lm[c * (c + 1) / 2 + k],
+                                      Lm[i * (i + 1) / 2 + c]);
   }
 #pragma unroll
-  for (int q = 0; q < Q; ++q)
-    if (lane == q) fsh[1 + P + q] = gD[1 + q];
-  wave_sync_lds();
+  for (int k = 0; k < ND; ++k) {  // L y = b, column-oriented (il = 0 zeroes dropped directions)
+    b[k] *= il[k];
+#pragma unroll
+    for (int i = k + 1; i < ND; ++i) b[i] = fma(-Lm[i * (i + 1) / 2 + k], b[k], b[i]);
+  }
+#pragma unroll
+  for (int k = ND - 1; k >= 0; --k) {  // L^T g = y
+    b[k] *= il[k];
+#pragma unroll
+    for (int i = 0; i < k; ++i) b[i] = fma(-Lm[k * (k + 1) / 2 + i], b[k], b[i]);
+  }
+  stamp(4);
 
+  // industries: f_j = (m_j . h - kappa a_j z) / W_j with h = [-g_D, 1]; pivot f_p = z (1 - kappa c0)
+  double z = Gs[NC * CH + ND], gph = gpv[ND];
+#pragma unroll
+  for (int u = 0; u < ND; ++u) {
+    z = fma(-Gs[NC * CH + u], b[u], z);
+    gph = fma(-gpv[u], b[u], gph);
+  }
   const bool bad = (st & XS_BAD) != 0;
   double* fo = fout + (size_t)d * K;
   double* co = coef + (size_t)d * (Q + 1 + P);
-  for (int i = lane; i < K; i += 64) fo[i] = bad ? qnan() : fsh[i];
-  // residual coefficients on RAW styles: e = r - cst - f_j - sum_q beta_q x_q
-  if (lane < Q) co[lane] = bad ? qnan() : fsh[1 + P + lane] * isig;
-  if (lane == 0) {
-    double cst = fsh[0];
+  for (int j = lane; j < P; j += 64) {
+    const double* p = seg + j * NS;
+    const double W = p[0];
+    double fj = 0.0;
+    if (j == jp) {
+      fj = z * (1.0 - kappa * c0);
+    } else if (W > 0.0) {
+      const double aj = -p[Q + 2] * isp;
+      double mh = p[ND];  // g_j . h  (g_j[ND] = B_j, h[ND] = 1)
+      mh = fma(-W, b[0], mh);
 #pragma unroll
-    for (int q = 0; q < Q; ++q) cst -= gD[1 + q] * isig * mu[q];
+      for (int q = 0; q < Q; ++q) mh = fma(-(p[1 + q] - muv[q] * W) * isig, b[1 + q], mh);
+      fj = (mh + aj * gph - kappa * aj * z) * iwv[j];
+    }
+    fo[1 + j] = bad ? qnan() : fj;
+    co[Q + 1 + j] = bad ? qnan() : fj;
+  }
+  if (lane == 0) fo[0] = bad ? qnan() : b[0];
+#pragma unroll
+  for (int q = 0; q < Q; ++q)
+    if (lane == q) {
+      fo[1 + P + q] = bad ? qnan() : b[1 + q];
+      co[q] = bad ? qnan() : b[1 + q] * isig;  // residual coefficients on RAW styles
+    }
+  if (lane == 0) {
+    double cst = b[0];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) cst -= b[1 + q] * isig * muv[q];
     co[Q] = bad ? qnan() : cst;
     status[d] = st;
   }
-  for (int j = lane; j < P; j += 64) co[Q + 1 + j] = bad ? qnan() : fsh[1 + j];
   if (stats) {
     double* sd = stats + (size_t)d * (Q + 2);
-#pragma unroll
-    for (int q = 0; q < Q; ++q)
-      if (lane == q) sd[q] = mu[q];
+    if (lane < Q) sd[lane] = muv[lane];
     if (lane == Q) sd[Q] = sigma;
     if (lane == Q + 1) sd[Q + 1] = nval;
   }
+  stamp(5);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -594,6 +639,8 @@ __global__ __launch_bounds__(256) void xs_resid_kernel(
   }
 }
 
+long long* g_stamps = nullptr;  // debug: per-date K2 phase stamps [D][8]
+
 template <int Q, int VAR = 0>
 hipError_t launch_q(const float* X, const float* cap, const float* ret, const int16_t* ind,
                     int D, int N, int P, int pivot_mode, double tol, double* f, float* e,
@@ -601,24 +648,38 @@ hipError_t launch_q(const float* X, const float* cap, const float* ret, const in
   using L = Layout<Q>;
   const int Pseg = P > 0 ? P : 1;
   const int K = 1 + P + Q;
+  const int MS = L::msize(Pseg);
   double* mom = ws;
-  double* coef = ws + (size_t)D * L::msize(Pseg);
-  const size_t lds1 = ((size_t)kRep * (Pseg * L::NS + 1) + L::NACC) * sizeof(double);
-  const size_t lds2 = ((size_t)L::msize(Pseg) + (size_t)Pseg * (L::ND + 1) * 2 +
-                       L::ND * (L::ND + 1) + K) * sizeof(double);
-  if (lds1 + 4 * (size_t)kWNB * L::WSLOT + 16640 > 160 * 1024 || lds2 > 64 * 1024)
-    return hipErrorInvalidValue;
-  hipLaunchKernelGGL((xs_moments_kernel<Q, VAR>), dim3(D), dim3(256), lds1, s, X, cap, ret,
-                     P > 0 ? ind : nullptr, N, Pseg, mom);
-  hipLaunchKernelGGL(xs_solve_kernel<Q>, dim3(D), dim3(64), lds2, s, mom, P, Pseg, pivot_mode,
-                     tol, f, coef, stats, status);
+  double* coef = ws + (size_t)D * MS;
+  const size_t ring = 4 * (size_t)kWNB * L::WSLOT > 4 * 8 * 65 * 8 ? 4 * (size_t)kWNB * L::WSLOT
+                                                                     : 4 * 8 * 65 * 8;
+  const size_t seg8 = (size_t)kRepMax * Pseg * L::NS * sizeof(double);
+  const bool rep8 = seg8 <= kSegLdsBudget;
+  const size_t lds1 = ((rep8 ? (size_t)kRepMax : 1) * Pseg * L::NS + L::NACC) * sizeof(double);
+  constexpr int CH = Q + 4;
+  const size_t P4 = ((size_t)Pseg + 3) & ~(size_t)3;
+  const size_t lds2 = ((size_t)L::msize(Pseg) + CH * CH + L::ND * (L::ND + 1) + (Q + 2) + Q +
+                       2 * P4) * sizeof(double);
+  if (lds1 + ring > 160 * 1024 || lds2 > 64 * 1024) return hipErrorInvalidValue;
+  const int16_t* indp = P > 0 ? ind : nullptr;
+  if (rep8)
+    hipLaunchKernelGGL((xs_moments_kernel<Q, VAR, kRepMax>), dim3(D), dim3(256), lds1, s, X, cap,
+                       ret, indp, N, Pseg, mom);
+  else
+    hipLaunchKernelGGL((xs_moments_kernel<Q, VAR, 1>), dim3(D), dim3(256), lds1, s, X, cap, ret,
+                       indp, N, Pseg, mom);
+  hipLaunchKernelGGL(xs_solve_kernel<Q>, dim3(D), dim3(64), lds2, s, mom, P, Pseg, pivot_mode, tol,
+                     f, coef, stats, status, g_stamps);
   if (!(VAR & 4))
-    hipLaunchKernelGGL(xs_resid_kernel<Q>, dim3(D), dim3(256), 0, s, X, cap, ret,
-                       P > 0 ? ind : nullptr, D, N, P, coef, status, e, r2);
+    hipLaunchKernelGGL(xs_resid_kernel<Q>, dim3(D), dim3(256), 0, s, X, cap, ret, indp, D, N, P,
+                       coef, status, e, r2);
   return hipGetLastError();
 }
 
 }  // namespace
+
+// Debug: record K2 phase timestamps (s_memtime) into buf[D][8] on the next calls (null = off).
+MFA_API void mfa_xs_set_stamps(long long* buf) { g_stamps = buf; }
 
 // Workspace bytes needed by mfa_xs_wls: D * (msize + Q + 1 + P) doubles.
 MFA_API size_t mfa_xs_wls_workspace(int D, int P, int Q) {
@@ -665,7 +726,7 @@ MFA_API int mfa_xs_wls_variant(const float* X, const float* cap, const float* re
   case vv:                                                                                     \
     return (int)launch_q<10, vv>(X, cap, ret, ind, D, N, P, 0, 1e-14, f, e, r2, stats,        \
                                  status, w, s);
-    MFA_V(0) MFA_V(1) MFA_V(4) MFA_V(5)
+    MFA_V(0) MFA_V(1) MFA_V(4) MFA_V(5) MFA_V(6) MFA_V(7)
 #undef MFA_V
   }
   return (int)hipErrorInvalidValue;

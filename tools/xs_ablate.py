@@ -1,8 +1,9 @@
-"""Interleaved A/B timing of xs_wls kernel variants (one process, rule: interleave rounds).
+"""Interleaved A/B timing of xs_wls kernel variants (one process, rounds interleaved).
 
-variant bits: 1 = skip segment LDS atomics, 2 = software prefetch, 4 = skip pass 2 (timing only).
+variant bits: 1 = skip segment LDS atomics, 2 = skip the style Gram FMAs, 4 = skip the residual
+pass (timing only; results are garbage for variants != 0).
+Env: VARIANTS (default 0,1,4,5), D, N.
 """
-import ctypes as C
 import os
 import statistics
 import sys
@@ -12,7 +13,6 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from llm_driven_multi_factor_model_amd import _native  # noqa: E402
 from llm_driven_multi_factor_model_amd.models.panel import synthetic_panel  # noqa: E402
-
 
 
 def main():
@@ -26,25 +26,23 @@ def main():
     st = torch.empty(D, Q + 2, dtype=torch.float64, device=dev)
     s = torch.empty(D, dtype=torch.int32, device=dev)
     variants = [int(v) for v in os.environ.get("VARIANTS", "0,1,4,5").split(",")]
-    waves = [0]
     ws = torch.empty(_native.query("mfa_xs_wls_workspace", D, P, Q), dtype=torch.uint8, device=dev)
-    times = {(v, w): [] for v in variants for w in waves}
+    times = {v: [] for v in variants}
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for rnd in range(12):
         for v in variants:
-            for w in waves:
-                ev0.record()
-                for _ in range(5):
-                    _native.call("mfa_xs_wls_variant", _native.ptr(p.styles), _native.ptr(p.cap),
-                                 _native.ptr(p.ret), _native.ptr(p.ind), D, N, P, v,
-                                 _native.ptr(f), _native.ptr(e), _native.ptr(r2), _native.ptr(st),
-                                 _native.ptr(s), _native.ptr(ws), _native.stream(dev))
-                ev1.record()
-                ev1.synchronize()
-                if rnd >= 2:
-                    times[(v, w)].append(ev0.elapsed_time(ev1) / 5)
-    for (v, w), t in times.items():
-        print(f"variant {v} waves {w}: median {statistics.median(t)*1e3:.1f} us  min {min(t)*1e3:.1f} us")
+            ev0.record()
+            for _ in range(5):
+                _native.call("mfa_xs_wls_variant", _native.ptr(p.styles), _native.ptr(p.cap),
+                             _native.ptr(p.ret), _native.ptr(p.ind), D, N, P, v,
+                             _native.ptr(f), _native.ptr(e), _native.ptr(r2), _native.ptr(st),
+                             _native.ptr(s), _native.ptr(ws), _native.stream(dev))
+            ev1.record()
+            ev1.synchronize()
+            if rnd >= 2:
+                times[v].append(ev0.elapsed_time(ev1) / 5)
+    for v, t in times.items():
+        print(f"variant {v}: median {statistics.median(t)*1e3:.1f} us  min {min(t)*1e3:.1f} us")
 
 
 if __name__ == "__main__":
