@@ -14,8 +14,11 @@
 //     C_z,m = cov(z_m) are date-independent: they are computed ONCE per call with Philox
 //     normals and fp32 MFMA (v_mfma_f32_32x32x2_f32, exact-f32 products, fp64 cross-chunk
 //     accumulation) and C_b = S C_z,m S is formed on the fly per (date, sim);
-//   * eigh: one wave per matrix, parallel cyclic Jacobi (round-robin tournament ordering,
+//   * eigh (F0): one wave per matrix, parallel cyclic Jacobi (round-robin tournament ordering,
 //     K/2 disjoint rotations per round) with A and V resident in LDS, fp64 throughout;
+//   * the (date, sim) Jacobi of the bias statistic carries M = V^T D0 V instead of V, works on
+//     packed (A, M) pairs in tournament-position space and applies each round as 2x2 pair
+//     blocks written straight to their next-round slots (all LDS addresses precomputed);
 //   * grid (date, sim) for the simulations, per-(date, sim) bias vectors reduced by a
 //     separate deterministic pass (no float atomics -> bitwise reproducible).
 #include "common.h"
@@ -270,8 +273,132 @@ __global__ __launch_bounds__(64) void mc_cov_kernel(int K, int T, unsigned long 
   }
 }
 
-// Per (date, sim): C_b = S C_z,m S (S = diag sqrt D0, eigen order of F0), eigh, bias vector
-// vout[d][m][k] = sum_l V[l,k]^2 D0[l] / Lambda[k]   (both spectra sorted descending)
+// ---------------- pair-block Jacobi for the bias statistic ----------------
+// Only v[k] = V[:,k]^T D0 V[:,k] / Lambda[k] is needed, so instead of the eigenvectors the
+// kernel carries M = V^T D0 V, transformed two-sidedly like A (M <- J^T M J, M0 = diag D0):
+// at convergence diag(A) = Lambda and diag(M)[k] = V[:,k]^T D0 V[:,k].  Both symmetric
+// matrices are stored packed (upper triangle) in LDS; one round of K/2 disjoint rotations is
+// applied as 2x2 pair blocks (t <= u), each block read and written once, with the block list
+// of every lane fixed for the whole solve (round-robin ordering moves indices, not blocks).
+__device__ __forceinline__ int pk(int i, int j, int Ke) {  // packed index of (min, max)
+  const int a = i < j ? i : j, b = i < j ? j : i;
+  return ((a * (2 * Ke - a + 1)) >> 1) + b - a;
+}
+
+__device__ __forceinline__ void rot_block(double& x00, double& x01, double& x10, double& x11,
+                                          double ct, double st, double cu, double su) {
+  // rows (pair t): r0 = c r0 - s r1 ; r1 = s r0 + c r1 ; then columns (pair u) likewise
+  const double y00 = ct * x00 - st * x10, y01 = ct * x01 - st * x11;
+  const double y10 = st * x00 + ct * x10, y11 = st * x01 + ct * x11;
+  x00 = cu * y00 - su * y01;
+  x01 = su * y00 + cu * y01;
+  x10 = cu * y10 - su * y11;
+  x11 = su * y10 + cu * y11;
+}
+
+// Returns sweeps used.  AM: packed Ke x Ke (A, M) pairs in TOURNAMENT-POSITION space (Ke = K
+// rounded up to even; padding zero).  Round-robin ordering with positions fixed: every round
+// pairs positions (t, Ke-1-t), and the circle shift (position 0 fixed, x -> x+1, Ke-1 -> 1)
+// is applied by writing each rotated 2x2 pair block straight to its NEXT-round positions.  So
+// every LDS address a lane touches is precomputed once: no per-round index arithmetic.  All of
+// a wave's loads of a round are issued before its stores and LDS executes one wave's accesses
+// in order, so the in-place permuted write-back needs no second buffer.
+// NB = pair blocks per lane (>= nb / 64).
+template <int NB>
+__device__ int jacobi_pairs(double2* AM, double2* rcs, int Ke, int max_sweeps, double tol) {
+  const int lane = threadIdx.x & 63;
+  const int npair = Ke >> 1;
+  const int nb = npair * (npair + 1) / 2;
+  auto nxt = [&](int x) { return x == 0 ? 0 : (x == Ke - 1 ? 1 : x + 1); };
+  // this lane's pair blocks (T, U), T <= U, with fixed read / write slots
+  int rd[NB][4], wr[NB][4];
+  bool has[NB], diag[NB];
+  int bT[NB], bU[NB];
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    const int b = lane + 64 * k;
+    int t = 0, rem = b;
+    while (t < npair && rem >= npair - t) { rem -= npair - t; ++t; }
+    has[k] = b < nb;
+    const int T = has[k] ? t : 0, U = has[k] ? t + rem : 0;
+    bT[k] = T;
+    bU[k] = U;
+    diag[k] = T == U;
+    const int x0 = T, x1 = Ke - 1 - T, y0 = U, y1 = Ke - 1 - U;
+    rd[k][0] = pk(x0, y0, Ke); rd[k][1] = pk(x0, y1, Ke);
+    rd[k][2] = pk(x1, y0, Ke); rd[k][3] = pk(x1, y1, Ke);
+    wr[k][0] = pk(nxt(x0), nxt(y0), Ke); wr[k][1] = pk(nxt(x0), nxt(y1), Ke);
+    wr[k][2] = pk(nxt(x1), nxt(y0), Ke); wr[k][3] = pk(nxt(x1), nxt(y1), Ke);
+  }
+  const int ipp = pk(lane, lane, Ke), iqq = pk(Ke - 1 - lane, Ke - 1 - lane, Ke);
+  const int ipq = pk(lane, Ke - 1 - lane, Ke);
+  int sweep = 0;
+  for (; sweep < max_sweeps; ++sweep) {
+    // every off-diagonal entry lives in exactly one pair block per round, so the squares of
+    // the values written in a sweep's LAST round are the exact post-sweep off / diag mass
+    double offacc = 0.0, dgacc = 0.0;
+    for (int r = 0; r < Ke - 1; ++r) {
+      const bool last = r == Ke - 2;
+      if (lane < npair) {  // rotation of pair `lane`: positions (lane, Ke-1-lane)
+        const double apq = AM[ipq].x, app = AM[ipp].x, aqq = AM[iqq].x;
+        double c = 1.0, s = 0.0;
+        if (fabs(apq) > 1e-300 && fabs(apq) > 1e-18 * sqrt(fabs(app * aqq))) {
+          const double th = (aqq - app) / (2.0 * apq);
+          const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(fma(th, th, 1.0)));
+          c = 1.0 / sqrt(fma(t, t, 1.0));
+          s = t * c;
+        }
+        rcs[lane] = double2{c, s};
+      }
+      wsync();
+      double av[NB][4], mv[NB][4];
+      double2 rt[NB], ru[NB];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {  // load
+        if (has[k]) {
+          rt[k] = rcs[bT[k]];
+          ru[k] = rcs[bU[k]];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const double2 v = AM[rd[k][e]];
+            av[k][e] = v.x;
+            mv[k][e] = v.y;
+          }
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {  // rotate + store at next-round positions
+        if (!has[k]) continue;
+        rot_block(av[k][0], av[k][1], av[k][2], av[k][3], rt[k].x, rt[k].y, ru[k].x, ru[k].y);
+        rot_block(mv[k][0], mv[k][1], mv[k][2], mv[k][3], rt[k].x, rt[k].y, ru[k].x, ru[k].y);
+        if (diag[k]) {  // symmetric diagonal block: off-diagonal of A -> 0
+          const double apq_new = (rt[k].y != 0.0) ? 0.0 : av[k][1];
+          AM[wr[k][0]] = double2{av[k][0], mv[k][0]};
+          AM[wr[k][1]] = double2{apq_new, 0.5 * (mv[k][1] + mv[k][2])};
+          AM[wr[k][3]] = double2{av[k][3], mv[k][3]};
+          if (last) {
+            dgacc = fma(av[k][0], av[k][0], fma(av[k][3], av[k][3], dgacc));
+            offacc = fma(2.0 * apq_new, apq_new, offacc);
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            AM[wr[k][e]] = double2{av[k][e], mv[k][e]};
+            if (last) offacc = fma(2.0 * av[k][e], av[k][e], offacc);
+          }
+        }
+      }
+      wsync();
+    }
+    const double off = wave_total(offacc), dgt = wave_total(dgacc);
+    if (off <= tol * tol * dgt || off == 0.0) { ++sweep; break; }
+  }
+  return sweep;
+}
+
+// Per (date, sim): C_b = S C_z,m S (S = diag sqrt D0, eigen order of F0), Jacobi, bias vector
+// vout[d][m][k] = (V[:,k]^T D0 V[:,k]) / Lambda[k]   (both spectra sorted descending)
+template <int NB>
 __global__ __launch_bounds__(64) void mc_bias_kernel(const double* __restrict__ D0, int K, int M,
                                                      const double* __restrict__ Cz,
                                                      const int* __restrict__ dvalid,
@@ -284,32 +411,43 @@ __global__ __launch_bounds__(64) void mc_bias_kernel(const double* __restrict__ 
     for (int k = lane; k < K; k += 64) vo[k] = qnan();
     return;
   }
-  const int lda = K + 1;
-  double* A = sm;
-  double* V = A + K * lda;
-  double* rot = V + K * lda;
-  double* dd = rot + 4 * 64;
-  int* perm = (int*)(dd + 64);
+  const int Ke = K + (K & 1);
+  const int np = Ke * (Ke + 1) / 2;
+  double2* AM = (double2*)sm;                  // [np] packed (A, M) pairs
+  double* dd = (double*)(AM + np);             // [64]
+  double2* rcs = (double2*)(dd + 64);          // [32]
+  int* perm = (int*)(rcs + 32);                // [64]
   const double* d0 = D0 + (size_t)d * K;
-  for (int k = lane; k < K; k += 64) dd[k] = d0[k];
+  for (int k = lane; k < 64; k += 64) dd[k] = k < K ? sqrt(fmax(d0[k], 0.0)) : 0.0;
   wsync();
   const double* c = Cz + (size_t)m * K * K;
-  for (int e = lane; e < K * K; e += 64) {
-    const int i = e / K, j = e % K;
-    A[i * lda + j] = sqrt(dd[i]) * c[e] * sqrt(dd[j]);
+  for (int i = 0; i < Ke; ++i)
+    for (int j = i + lane; j < Ke; j += 64) {
+      const double a = (i < K && j < K) ? dd[i] * c[i * K + j] * dd[j] : 0.0;
+      AM[pk(i, j, Ke)] = double2{a, (i == j && i < K) ? dd[i] * dd[i] : 0.0};
+    }
+  wsync();
+  jacobi_pairs<NB>(AM, rcs, Ke, max_sweeps, tol);
+  // descending rank of eigenvalue k (ties by index)
+  for (int k = lane; k < K; k += 64) {
+    const double lk = AM[pk(k, k, Ke)].x;
+    int rank = 0;
+    for (int j = 0; j < K; ++j) {
+      const double lj = AM[pk(j, j, Ke)].x;
+      rank += (lj > lk) || (lj == lk && j < k);
+    }
+    perm[rank] = k;
   }
   wsync();
-  jacobi_wave(A, V, K, lda, rot, max_sweeps, tol);
-  sort_desc(A, K, lda, perm);
   for (int k = lane; k < K; k += 64) {
-    const int pk = perm[k];
-    double num = 0.0;
-    for (int l = 0; l < K; ++l) {
-      const double v = V[l * lda + pk];
-      num = fma(v * v, dd[l], num);
-    }
-    vo[k] = num / A[pk * lda + pk];
+    const double2 v = AM[pk(perm[k], perm[k], Ke)];
+    vo[k] = v.y / v.x;
   }
+}
+
+size_t bias_lds(int K) {
+  const int Ke = K + (K & 1);
+  return ((size_t)Ke * (Ke + 1) + 64) * sizeof(double) + 32 * sizeof(double2) + 64 * sizeof(int);
 }
 
 // finalize: v = sqrt(mean_m v_m); v = a (v - 1) + 1; F^ = U0 diag(v^2 D0) U0^T.  Grid (D).
@@ -369,8 +507,13 @@ MFA_API int mfa_eigen_adjust(const double* D0, const double* U0, const int* dval
   if (D <= 0) return 0;
   if (K < 1 || K > 64 || M < 1) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(mc_bias_kernel, dim3(D * M), dim3(64), eigh_lds(K), s, D0, K, M, Cz, dvalid,
-                     max_sweeps, tol, ws);
+  const int Ke = K + (K & 1), npair = Ke / 2, nb = npair * (npair + 1) / 2;
+  if (nb <= 4 * 64)
+    hipLaunchKernelGGL(mc_bias_kernel<4>, dim3(D * M), dim3(64), bias_lds(K), s, D0, K, M, Cz,
+                       dvalid, max_sweeps, tol, ws);
+  else
+    hipLaunchKernelGGL(mc_bias_kernel<9>, dim3(D * M), dim3(64), bias_lds(K), s, D0, K, M, Cz,
+                       dvalid, max_sweeps, tol, ws);
   hipLaunchKernelGGL(eigen_finalize_kernel, dim3(D), dim3(256), 0, s, ws, D0, U0, dvalid, K, M,
                      scale, Fout, vbias);
   return (int)hipGetLastError();
