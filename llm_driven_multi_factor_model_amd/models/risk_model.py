@@ -10,13 +10,12 @@ re-designed for MI355X:
   factor-return series is all-gathered once (RCCL) and the Newey-West scan emits only the
   rank's own dates; the eigen adjustment of a date needs only that date's covariance; the VRA
   bias series is all-gathered once;
-* outputs stay on the device as float64 tensors; pandas objects are built only on request.
+* outputs stay on the device as float64 tensors; pandas objects are built only on request;
+* every stage is traced (ROCTX range, HIP-event GPU time, JSONL metrics: utils/trace.py);
+* checkpoint / resume: :meth:`RiskModel.state_dict` exports the O(T K) history the scans need and
+  :meth:`RiskModel.resume` appends new dates without re-running the old ones (utils/checkpoint.py).
 """
 from __future__ import annotations
-
-import math
-import time
-from dataclasses import dataclass, field
 
 import numpy as np
 import torch
@@ -24,18 +23,10 @@ import torch
 from ..ops import cross_section as xs
 from ..ops import ew_scan, eigen
 from ..parallel import dist as pdist
+from ..utils import checkpoint as ckpt
+from ..utils import trace
 from ..utils.config import RiskConfig
 from .panel import RiskPanel
-
-
-@dataclass
-class StageTimes:
-    ms: dict = field(default_factory=dict)
-
-    def add(self, name: str, t0: float, device) -> None:
-        if device is not None and device.type == "cuda":
-            torch.cuda.synchronize(device)
-        self.ms[name] = self.ms.get(name, 0.0) + (time.perf_counter() - t0) * 1e3
 
 
 class RiskModel:
@@ -48,16 +39,27 @@ class RiskModel:
     """
 
     def __init__(self, panel: RiskPanel, config: RiskConfig | None = None,
-                 T_global: int | None = None, ctx: pdist.DistContext | None = None):
+                 T_global: int | None = None, ctx: pdist.DistContext | None = None,
+                 history: dict | None = None, sync_stages: bool = True):
         self.panel = panel
         self.cfg = config or RiskConfig()
         self.ctx = ctx or pdist.context()
-        self.T = T_global if T_global is not None else panel.D * (self.ctx.world if self.ctx.enabled else 1)
-        self.times = StageTimes()
+        # dates already processed by an earlier run (checkpoint): global index offset
+        self.history = history
+        self.T_hist = int(history["T"]) if history is not None else 0
+        T_new = T_global if T_global is not None else panel.D * (self.ctx.world if self.ctx.enabled else 1)
+        self.T = self.T_hist + T_new
+        self.times = trace.Timer()
+        self.sync_stages = sync_stages
         self.factor_ret = self.specific_ret = self.r2 = self.status = self.stats = None
         self.factor_ret_global = None
         self.nw_cov = self.eigen_cov = self.vra_cov = self.vra_lambda = None
         self.eigen_bias = None
+        self.B2_global = None
+
+    def _stage(self, name: str):
+        return trace.stage(name, self.times, self.device, sync=self.sync_stages,
+                           dates=self.panel.D, K=self.K)
 
     @property
     def device(self):
@@ -69,20 +71,22 @@ class RiskModel:
 
     @property
     def t_lo(self) -> int:
-        return self.panel.date_offset
+        """Global index of this rank's first date (history dates come first)."""
+        return self.T_hist + self.panel.date_offset
 
     # --------------------------------------------------------------- stage 1: regression
     def regress(self, want_resid: bool = True):
-        t0 = time.perf_counter()
         p = self.panel
-        res = xs.xs_wls(p.styles, p.cap, p.ret, p.ind, p.P, pivot_mode=self.cfg.pivot_mode,
-                        want_resid=want_resid)
+        with self._stage("regress"):
+            res = xs.xs_wls(p.styles, p.cap, p.ret, p.ind, p.P, pivot_mode=self.cfg.pivot_mode,
+                            want_resid=want_resid)
         self.factor_ret, self.specific_ret, self.r2 = res.f, res.resid, res.r2
         self.status, self.stats = res.status, res.stats
-        self.times.add("regress", t0, self.device)
-        t0 = time.perf_counter()
-        self.factor_ret_global = pdist.all_gather_rows(self.factor_ret, self.ctx)
-        self.times.add("allgather_f", t0, self.device)
+        with self._stage("allgather_f"):
+            F = pdist.all_gather_rows(self.factor_ret, self.ctx)
+            if self.history is not None:
+                F = torch.cat([self.history["factor_ret"].to(F.device, F.dtype), F])
+            self.factor_ret_global = F
         return self.factor_ret, self.specific_ret, self.r2
 
     # --------------------------------------------------------------- stage 2: Newey-West
@@ -91,10 +95,10 @@ class RiskModel:
             raise RuntimeError("please run regress() to get factor returns first")
         q = self.cfg.nw_lags if q is None else q
         tau = self.cfg.nw_half_life if tau is None else tau
-        t0 = time.perf_counter()
         lo = self.t_lo
-        self.nw_cov = ew_scan.newey_west_series(self.factor_ret_global, q, tau, lo, lo + self.panel.D)
-        self.times.add("newey_west", t0, self.device)
+        with self._stage("newey_west"):
+            self.nw_cov = ew_scan.newey_west_series(self.factor_ret_global, q, tau, lo,
+                                                    lo + self.panel.D)
         return self.nw_cov
 
     # --------------------------------------------------------------- stage 3: eigen adjustment
@@ -106,29 +110,43 @@ class RiskModel:
         scale_coef = self.cfg.eigen_scale if scale_coef is None else scale_coef
         T_sim = T_sim or self.cfg.eigen_sim_length or self.T
         seed = self.cfg.eigen_seed if seed is None else seed
-        t0 = time.perf_counter()
-        self.eigen_cov, self.eigen_bias = eigen.eigen_risk_adjust(
-            self.nw_cov, M=M, scale_coef=scale_coef, T_sim=T_sim, seed=seed,
-            psd_tol=self.cfg.psd_tol, return_bias=True)
-        self.times.add("eigen_adjust", t0, self.device)
+        with self._stage("eigen_adjust"):
+            self.eigen_cov, self.eigen_bias = eigen.eigen_risk_adjust(
+                self.nw_cov, M=M, scale_coef=scale_coef, T_sim=T_sim, seed=seed,
+                psd_tol=self.cfg.psd_tol, return_bias=True)
         return self.eigen_cov
 
     # --------------------------------------------------------------- stage 4: VRA
     def vol_regime_adjust(self, tau: float | None = None):
-        """lambda_t^2 = EW mean of B_s^2 over valid s <= t; B_t^2 = mean_k f_tk^2 / sigma_tk^2."""
+        """lambda_t^2 = EW mean of B_s^2 over valid s <= t; B_t^2 = mean_k f_tk^2 / sigma_tk^2.
+
+        ``sigma_t`` is the eigen-adjusted forecast of date t itself (in-sample, quirk Q10); with
+        ``config.vra_out_of_sample`` the forecast made at t-1 is used instead (USE4 practice).
+        """
         if self.eigen_cov is None:
             raise RuntimeError("please run eigen_adjust() first")
         tau = self.cfg.vra_half_life if tau is None else tau
-        t0 = time.perf_counter()
-        var = torch.diagonal(self.eigen_cov, dim1=-2, dim2=-1)            # [D_loc, K]
-        B2 = (self.factor_ret ** 2 / var).mean(-1)                        # NaN where ER empty
-        B2_all = pdist.all_gather_rows(B2, self.ctx)
-        lam2 = ew_scan.ew_prefix_mean(B2_all, tau)[self.t_lo:self.t_lo + self.panel.D]
-        # no valid date yet: the reference's sum over an empty selection gives lambda = 0
-        lam2 = torch.nan_to_num(lam2, nan=0.0)
-        self.vra_lambda = torch.sqrt(lam2)
-        self.vra_cov = self.eigen_cov * lam2[:, None, None]
-        self.times.add("vra", t0, self.device)
+        with self._stage("vra"):
+            var = torch.diagonal(self.eigen_cov, dim1=-2, dim2=-1)        # [D_loc, K]
+            if self.cfg.vra_out_of_sample:
+                var_all = pdist.all_gather_rows(var.contiguous(), self.ctx)
+                if self.history is not None and "last_var" in self.history:
+                    prev0 = self.history["last_var"].to(var.device, var.dtype)[None]
+                else:
+                    prev0 = torch.full_like(var_all[:1], float("nan"))
+                prev = torch.cat([prev0, var_all[:-1]])
+                lo = self.panel.date_offset
+                var = prev[lo:lo + self.panel.D]
+            B2 = (self.factor_ret ** 2 / var).mean(-1)                    # NaN where ER empty
+            B2_all = pdist.all_gather_rows(B2, self.ctx)
+            if self.history is not None:
+                B2_all = torch.cat([self.history["B2"].to(B2_all.device, B2_all.dtype), B2_all])
+            self.B2_global = B2_all
+            lam2 = ew_scan.ew_prefix_mean(B2_all, tau)[self.t_lo:self.t_lo + self.panel.D]
+            # no valid date yet: the reference's sum over an empty selection gives lambda = 0
+            lam2 = torch.nan_to_num(lam2, nan=0.0)
+            self.vra_lambda = torch.sqrt(lam2)
+            self.vra_cov = self.eigen_cov * lam2[:, None, None]
         return self.vra_cov, self.vra_lambda
 
     def run(self):
@@ -137,6 +155,77 @@ class RiskModel:
         self.eigen_adjust()
         self.vol_regime_adjust()
         return self
+
+    # --------------------------------------------------------------- checkpoint / resume
+    def state_dict(self) -> dict:
+        """History needed to append dates later (identical on every rank), plus artifacts.
+
+        Call after :meth:`run`.  Collective in distributed mode (every rank must call it).
+        """
+        if self.B2_global is None:
+            raise RuntimeError("run all four stages before exporting a checkpoint")
+        r2 = pdist.all_gather_rows(self.r2, self.ctx)
+        status = pdist.all_gather_rows(self.status, self.ctx)
+        var = torch.diagonal(self.eigen_cov, dim1=-2, dim2=-1).contiguous()
+        var_all = pdist.all_gather_rows(var, self.ctx)
+        vra_last = pdist.all_gather_rows(self.vra_cov[-1:].contiguous(), self.ctx)[-1]
+        if self.history is not None:
+            r2 = torch.cat([self.history["r2"].to(r2.device), r2])
+            status = torch.cat([self.history["status"].to(status.device), status])
+        dates = [str(d) for d in self._global_dates()]
+        if self.history is not None:
+            dates = list(self.history["dates"]) + dates
+        cfg = self.cfg.to_dict()
+        return {
+            "T": int(self.factor_ret_global.shape[0]), "K": int(self.K),
+            "factor_names": list(self.panel.factor_names), "dates": dates,
+            "config": {k: v for k, v in cfg.items()}, "config_hash": ckpt.config_hash(cfg),
+            "factor_ret": self.factor_ret_global, "B2": self.B2_global,
+            "r2": r2, "status": status, "last_var": var_all[-1], "last_vra_cov": vra_last,
+        }
+
+    def save(self, path) -> None:
+        """Write a checkpoint (rank 0 writes; collective in distributed mode)."""
+        st = self.state_dict()
+        if self.ctx.rank == 0:
+            ckpt.save_state(st, path)
+        pdist.barrier(self.ctx)
+
+    @classmethod
+    def resume(cls, state, panel: RiskPanel, config: RiskConfig | None = None,
+               T_global: int | None = None, ctx: pdist.DistContext | None = None, **kw):
+        """A model for the NEW dates of ``panel`` continuing the run saved in ``state`` (a dict
+        from :meth:`state_dict` or a checkpoint path).  Old dates are not recomputed: their
+        factor returns feed the Newey-West prefix scan and the VRA series.  Results for the
+        new dates equal those of one run over all dates (the eigen simulation length follows
+        the total number of dates, quirk Q9, as in a full run)."""
+        if not isinstance(state, dict):
+            state = ckpt.load_state(state)
+        cfg = config or RiskConfig(**state["config"])
+        if ckpt.config_hash(cfg.to_dict()) != state["config_hash"]:
+            raise ValueError("checkpoint was produced with a different RiskConfig")
+        if int(state["K"]) != panel.K or list(state["factor_names"]) != list(panel.factor_names):
+            raise ValueError("factor set of the new panel differs from the checkpoint")
+        if len(panel.dates) and len(state["dates"]):
+            import pandas as pd
+            if pd.Timestamp(str(panel.dates[0])) <= pd.Timestamp(str(state["dates"][-1])):
+                raise ValueError("resume panel must start after the last checkpointed date")
+        return cls(panel, cfg, T_global=T_global, ctx=ctx, history=state, **kw)
+
+    def diagnostics(self) -> dict:
+        """Counters of the run (rank-local dates): solver status bits and NaN rates."""
+        st = self.status.cpu() if self.status is not None else torch.zeros(0, dtype=torch.int32)
+        out = {"dates": int(st.numel())}
+        for name, bit in (("no_rows", xs.XS_NO_ROWS), ("pivot_empty", xs.XS_PIVOT_EMPTY),
+                          ("near_singular", xs.XS_NEAR_SINGULAR), ("zero_pivot", xs.XS_ZERO_PIVOT),
+                          ("bad_sigma", xs.XS_BAD_SIGMA)):
+            out[name] = int(((st & bit) != 0).sum())
+        for name, t in (("factor_ret", self.factor_ret), ("nw_cov", self.nw_cov),
+                        ("eigen_cov", self.eigen_cov), ("vra_cov", self.vra_cov)):
+            if t is not None and t.numel():
+                bad = ~torch.isfinite(t.reshape(t.shape[0], -1)).all(-1)
+                out[f"{name}_nan_dates"] = int(bad.sum())
+        return out
 
     # --------------------------------------------------------------- diagnostics
     def eigenfactor_bias(self, which: str = "eigen", start: int = 0, predlen: int = 1):

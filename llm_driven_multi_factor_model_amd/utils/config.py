@@ -24,6 +24,7 @@ class RiskConfig:
     vra_half_life: float = 42.0   # demo.py:42 (MFM default is 84)
     pivot_mode: int = 0           # 0 = last non-empty industry; 1 = reference (quirk Q3)
     psd_tol: float = 0.0          # eigen adj requires D0 >= -psd_tol*max|D0| (reference: 0)
+    vra_out_of_sample: bool = False  # True: B_t uses the forecast of t-1 (reference: in-sample, Q10)
 
     def to_dict(self) -> dict:
         return asdict(self)

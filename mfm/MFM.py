@@ -19,7 +19,13 @@ from ._device import device as _device, verbose as _verbose
 
 
 class MFM:
-    def __init__(self, data: pd.DataFrame, P: int, Q: int, pivot_mode: int = 0):
+    def __init__(self, data: pd.DataFrame, P: int, Q: int, pivot_mode: int = 0,
+                 solver: str = "pinv", config: RiskConfig | None = None):
+        """``solver="inv"`` reproduces the stale ``inv`` build (quirk Q4): reg_by_time raises
+        LinAlgError at an exactly singular date.  ``config`` overrides the stage defaults."""
+        if solver not in ("pinv", "inv"):
+            raise ValueError("solver must be 'pinv' or 'inv'")
+        self._solver = solver
         self.Q = Q
         self.P = P
         self.dates = pd.to_datetime(data.date.values)
@@ -36,7 +42,8 @@ class MFM:
         self.eigen_risk_adj_cov = None
         self.vol_regime_adj_cov = None
         self._panel = panel_from_frame(data, P, Q, device=_device())
-        self._model = RiskModel(self._panel, RiskConfig(pivot_mode=pivot_mode))
+        cfg = config if config is not None else RiskConfig(pivot_mode=pivot_mode)
+        self._model = RiskModel(self._panel, cfg)
 
     def _banner(self, title):
         if _verbose():
@@ -46,6 +53,9 @@ class MFM:
         self._banner("逐时间点进行横截面多因子回归")
         m = self._model
         f, e, r2 = m.regress()
+        if self._solver == "inv":
+            from .CrossSection import check_inv_solvable
+            check_inv_solvable(m.status, m.panel.ind, m.panel.valid(), self.P)
         fr = f.cpu().numpy()
         self.factor_ret = pd.DataFrame(fr, columns=self.columns, index=self.sorted_dates)
         self.R2 = pd.DataFrame(r2.cpu().numpy(), columns=["R2"], index=self.sorted_dates)

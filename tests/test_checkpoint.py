@@ -1,0 +1,75 @@
+"""Checkpoint / resume of the risk model, stage tracing and run diagnostics (CPU)."""
+import json
+
+import pytest
+import torch
+
+from llm_driven_multi_factor_model_amd.models.panel import synthetic_panel
+from llm_driven_multi_factor_model_amd.models.risk_model import RiskModel
+from llm_driven_multi_factor_model_amd.utils import checkpoint as ckpt
+from llm_driven_multi_factor_model_amd.utils.config import RiskConfig
+
+
+def _cfg(**kw):
+    return RiskConfig(eigen_sims=6, nw_half_life=20.0, vra_half_life=10.0, **kw)
+
+
+@pytest.mark.parametrize("oos", [False, True])
+def test_resume_equals_full_run(tmp_path, oos):
+    """Run T1 dates, checkpoint, resume on the rest: new-date outputs == one full run."""
+    p = synthetic_panel(40, 64, P=4, Q=3, seed=3, missing_frac=0.02)
+    cfg = _cfg(vra_out_of_sample=oos)
+    full = RiskModel(p, cfg).run()
+    T1 = 27
+    first = RiskModel(p.slice_dates(0, T1), cfg, T_global=T1)
+    # the eigen simulation length follows the TOTAL number of dates (quirk Q9)
+    first.T = p.D
+    first.run()
+    path = tmp_path / "risk.ckpt"
+    first.save(path)
+    state = ckpt.load_state(path)
+    assert state["T"] == T1 and len(state["dates"]) == T1
+    rest = p.slice_dates(T1, p.D)
+    rest = type(rest)(**{**rest.__dict__, "date_offset": 0})
+    m2 = RiskModel.resume(path, rest, T_global=p.D - T1).run()
+    assert m2.T == p.D and m2.t_lo == T1
+    torch.testing.assert_close(m2.factor_ret, full.factor_ret[T1:], rtol=0, atol=0)
+    for name in ("nw_cov", "eigen_cov", "vra_cov", "vra_lambda"):
+        torch.testing.assert_close(getattr(m2, name), getattr(full, name)[T1:], rtol=1e-12,
+                                   atol=1e-18, equal_nan=True, msg=name)
+    # chained checkpoint covers all dates
+    st2 = m2.state_dict()
+    assert st2["T"] == p.D and len(st2["dates"]) == p.D
+    torch.testing.assert_close(st2["factor_ret"], full.factor_ret_global, rtol=0, atol=0)
+
+
+def test_resume_guards(tmp_path):
+    p = synthetic_panel(20, 48, P=3, Q=2, seed=5)
+    m = RiskModel(p.slice_dates(0, 12), _cfg()).run()
+    st = m.state_dict()
+    rest = p.slice_dates(12, 20)
+    with pytest.raises(ValueError, match="different RiskConfig"):
+        RiskModel.resume(st, rest, config=_cfg(nw_lags=1))
+    with pytest.raises(ValueError, match="start after"):
+        RiskModel.resume(st, p.slice_dates(5, 20))
+    # loader refuses foreign formats
+    torch.save({"format_version": 99}, tmp_path / "bad.ckpt")
+    with pytest.raises(ValueError):
+        ckpt.load_state(tmp_path / "bad.ckpt")
+
+
+def test_trace_metrics_and_diagnostics(tmp_path, monkeypatch):
+    path = tmp_path / "metrics.jsonl"
+    monkeypatch.setenv("MFA_METRICS", str(path))
+    p = synthetic_panel(16, 40, P=3, Q=2, seed=7, empty_industries=1)
+    m = RiskModel(p, _cfg()).run()
+    recs = [json.loads(x) for x in path.read_text().splitlines()]
+    stages = [r["stage"] for r in recs]
+    assert stages == ["regress", "allgather_f", "newey_west", "eigen_adjust", "vra"]
+    assert all(r["wall_ms"] >= 0 and r["dates"] == 16 for r in recs)
+    assert set(m.times.ms) == set(stages)
+    d = m.diagnostics()
+    assert d["dates"] == 16 and d["no_rows"] == 0
+    # the first K dates have no Newey-West estimate (n <= K) -> NaN covariance dates counted
+    assert d["nw_cov_nan_dates"] >= 1
+    assert "regress" in m.times.table()

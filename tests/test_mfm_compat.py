@@ -113,3 +113,25 @@ def test_utils_newey_west_and_bayes(ref, monkeypatch):
         mfm.utils.Newey_West(F[:4], 2, 60)
     vol, cap = rng.random(200) * 0.05, rng.lognormal(10, 1, 200)
     np.testing.assert_allclose(mfm.utils.bayes_shrink(vol, cap), ref.utils.bayes_shrink(vol, cap), rtol=1e-5)
+
+
+def test_inv_solver_raises_on_singular(monkeypatch):
+    """solver='inv' (stale build, quirk Q4): an empty industry raises LinAlgError; pinv does not."""
+    monkeypatch.setenv("MFA_DEVICE", "cpu")
+    df = toy_frame(T=1, N=60, seed=4, missing=0.0)
+    df["ind2"] = 0
+    df.loc[df.stocknames.str[:6].astype(int) % 3 == 2, "ind1"] = 1  # industry 2 now empty
+    base, sty, ind = df.iloc[:, :4], df.iloc[:, -3:], df.iloc[:, 4:7]
+    f, *_ = mfm.CrossSection(base, sty, ind).reg()
+    assert np.isfinite(f).all() and abs(f[3]) < 1e-12  # pinv semantics: empty industry -> 0
+    with pytest.raises(np.linalg.LinAlgError):
+        mfm.CrossSection(base, sty, ind, solver="inv").reg()
+    good = toy_frame(T=1, N=60, seed=4, missing=0.0)
+    fi, *_ = mfm.CrossSection(good.iloc[:, :4], good.iloc[:, -3:], good.iloc[:, 4:7], solver="inv").reg()
+    fp, *_ = mfm.CrossSection(good.iloc[:, :4], good.iloc[:, -3:], good.iloc[:, 4:7]).reg()
+    np.testing.assert_allclose(fi, fp)
+    m = mfm.MFM(pd.concat([good.assign(date="2020/01/02"), df.assign(date="2020/01/03")]), 3, 3,
+                solver="inv")
+    with pytest.raises(np.linalg.LinAlgError):
+        with contextlib.redirect_stdout(io.StringIO()):
+            m.reg_by_time()
