@@ -2,7 +2,8 @@
 
     python -m llm_driven_multi_factor_model_amd.cli synth  --out data/ --dates 250 --stocks 300
     python -m llm_driven_multi_factor_model_amd.cli risk   --data data/barra_data_csi.csv \
-        --industry data/industry_info.csv --out results/ [--preset reference] [--sims 100]
+        --industry data/industry_info.csv --out results/ [--preset reference] [--sims 100] \
+        [--checkpoint risk.ckpt] [--resume risk.ckpt]
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m llm_driven_multi_factor_model_amd.cli risk ...
     python -m llm_driven_multi_factor_model_amd.cli factors --prices prices.csv --index index.csv \
         --industry sw_industry.csv --out data/
@@ -64,14 +65,30 @@ def cmd_risk(a):
     _setup_logging(ctx.rank)
     t0 = time.perf_counter()
     full = panel_from_barra_csv(a.data, a.industry, device="cpu")
+    state = None
+    if a.resume:
+        from .utils.checkpoint import load_state
+        state = load_state(a.resume)
+        last = pd.Timestamp(str(state["dates"][-1]))
+        new = np.nonzero(pd.DatetimeIndex(full.dates) > last)[0]
+        if not len(new):
+            raise SystemExit(f"no dates after the checkpoint's last date {last.date()}")
+        full = full.slice_dates(int(new[0]), full.D)
+        full = type(full)(**{**full.__dict__, "date_offset": 0})
+        log.info("resuming after %s: %d new dates", last.date(), full.D)
     lo, hi = pdist.shard_range(full.D, ctx.rank, ctx.world)
     panel = full.slice_dates(lo, hi).to(ctx.device)
     log.info("panel %d dates x %d stocks x K=%d (shard [%d,%d)) loaded in %.2fs", full.D, full.N,
              full.K, lo, hi, time.perf_counter() - t0)
     cfg = preset(a.preset, eigen_sims=a.sims, vra_half_life=a.vra_tau, nw_lags=a.nw_q,
                  nw_half_life=a.nw_tau, eigen_scale=a.scale)
-    model = RiskModel(panel, cfg, T_global=full.D, ctx=ctx)
+    if state is not None:
+        model = RiskModel.resume(state, panel, cfg, T_global=full.D, ctx=ctx)
+    else:
+        model = RiskModel(panel, cfg, T_global=full.D, ctx=ctx)
     model.run()
+    if a.checkpoint:
+        model.save(a.checkpoint)
     paths = write_risk_results(model, a.out, long_specific=a.long_specific)
     if ctx.rank == 0:
         log.info("stage ms: %s", json.dumps({k: round(v, 3) for k, v in model.times.ms.items()}))
@@ -111,6 +128,9 @@ def main(argv=None):
     r.add_argument("--vra-tau", type=float, default=42.0)
     r.add_argument("--device", default=None, help="cpu to force the CPU path")
     r.add_argument("--long-specific", action="store_true")
+    r.add_argument("--checkpoint", default=None, help="write a resumable checkpoint here")
+    r.add_argument("--resume", default=None,
+                   help="continue from a checkpoint: only dates after its last date are run")
     r.set_defaults(fn=cmd_risk)
     f = sub.add_parser("factors", help="main.py equivalent: descriptors -> Barra exposures")
     f.add_argument("--prices", required=True)

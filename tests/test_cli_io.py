@@ -59,3 +59,24 @@ def test_panel_from_barra_csv_native_equals_pandas(tmp_path, monkeypatch):
     for k in ["styles", "cap", "ret", "ind"]:
         torch.testing.assert_close(getattr(a, k), getattr(b, k), equal_nan=True)
     assert list(a.stocks) == list(b.stocks) and (a.dates == b.dates).all()
+
+
+def test_cli_checkpoint_resume(tmp_path):
+    """risk --checkpoint on the first dates, then risk --resume on the full file runs only the
+    new dates; their factor returns equal a single full run's."""
+    d = str(tmp_path)
+    assert _run("synth", "--out", d, "--dates", "50", "--stocks", "70", "--industries", "5").returncode == 0
+    df = pd.read_csv(f"{d}/barra_data_csi.csv")
+    dates = sorted(df.date.unique())
+    df[df.date.isin(dates[:35])].to_csv(f"{d}/first.csv", index=False)
+    common = ["--industry", f"{d}/industry_info.csv", "--sims", "3", "--device", "cpu"]
+    r = _run("risk", "--data", f"{d}/first.csv", "--out", f"{d}/r1", "--checkpoint", f"{d}/ck.pt", *common)
+    assert r.returncode == 0, r.stderr
+    r = _run("risk", "--data", f"{d}/barra_data_csi.csv", "--out", f"{d}/r2", "--resume", f"{d}/ck.pt", *common)
+    assert r.returncode == 0, r.stderr
+    r = _run("risk", "--data", f"{d}/barra_data_csi.csv", "--out", f"{d}/full", *common)
+    assert r.returncode == 0, r.stderr
+    f2 = pd.read_csv(f"{d}/r2/factor_returns.csv", index_col=0)
+    ff = pd.read_csv(f"{d}/full/factor_returns.csv", index_col=0)
+    assert len(f2) == 15
+    np.testing.assert_allclose(f2.values, ff.values[35:], rtol=1e-12, atol=1e-15)
