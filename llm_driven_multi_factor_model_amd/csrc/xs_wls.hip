@@ -153,20 +153,27 @@ __device__ __forceinline__ void wg_reduce(const double (&v)[CNT], double* wbuf, 
 // ------------------------------------------------------------------------------------------
 // K1: raw moments.  mom[d] = [ Swxx(NG) | Swxr(Q) | Scx(Q) | Sc Sx Sxx n | seg[Pseg][NS] ]
 // ------------------------------------------------------------------------------------------
-template <int Q, int VAR, int R>
-__global__ __launch_bounds__(256) void xs_moments_kernel(
-    const float* __restrict__ X, const float* __restrict__ cap, const float* __restrict__ ret,
-    const int16_t* __restrict__ ind, int N, int Pseg, double* __restrict__ mom) {
-  using L = Layout<Q>;
-  constexpr int NS = L::NS, NG = L::NG, NACC = L::NACC, BUF = L::BUF, NBUF = 3;
+template <int Q>
+struct Ring {
   // Per-wave DMA rings (own __shared__ object, separate from the atomics' dynamic LDS): each
   // wave streams its own 64-stock tiles (k = wid, wid + nw, ...) with no workgroup barrier until
   // the final reduction, so the 8 waves of a CU drift and overlap HBM, VALU and LDS phases.
-  constexpr int WSLOT = L::WSLOT;
-  constexpr int RINGW = kWNB * WSLOT > 8 * 65 * 8 ? kWNB * WSLOT : 8 * 65 * 8;
-  __shared__ __attribute__((aligned(16))) char ring[4 * RINGW];
-  extern __shared__ double dyn[];  // [Pseg*NS][R] replicated segment sums | [NACC] totals
-  const int d = blockIdx.x;
+  static constexpr int WSLOT = Layout<Q>::WSLOT;
+  static constexpr int RINGW = kWNB * WSLOT > 8 * 65 * 8 ? kWNB * WSLOT : 8 * 65 * 8;
+  static constexpr int BYTES = 4 * RINGW;
+};
+
+// Moments of date d.  `ring` = Ring<Q>::BYTES of LDS, `dyn` = [Pseg*NS][R] replicated segment
+// sums | [NACC] totals (LDS), `md` = msize(Pseg) doubles out (global memory or LDS that does
+// not alias `dyn`; may alias `ring`).  Ends with a workgroup barrier.
+template <int Q, int VAR, int R>
+__device__ __forceinline__ void moments_body(
+    const float* __restrict__ X, const float* __restrict__ cap, const float* __restrict__ ret,
+    const int16_t* __restrict__ ind, int N, int Pseg, int d, char* ring, double* dyn,
+    double* md) {
+  using L = Layout<Q>;
+  constexpr int NS = L::NS, NG = L::NG, NACC = L::NACC;
+  constexpr int WSLOT = Ring<Q>::WSLOT, RINGW = Ring<Q>::RINGW;
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int lane = tid & 63, wid = tid >> 6, nw = nthr >> 6;
   const unsigned seg_a = lds_addr(dyn + (lane & (R - 1)));
@@ -258,7 +265,6 @@ __global__ __launch_bounds__(256) void xs_moments_kernel(
   __syncthreads();
   wg_reduce<NACC>(v, (double*)wring, acc);
   __syncthreads();
-  double* md = mom + (size_t)d * L::msize(Pseg);
   for (int i = tid; i < NACC; i += nthr) md[i] = acc[i];
   for (int i = tid; i < Pseg * NS; i += nthr) {
     double t = 0.0;
@@ -266,6 +272,18 @@ __global__ __launch_bounds__(256) void xs_moments_kernel(
     for (int r = 0; r < R; ++r) t += dyn[i * R + r];
     md[NACC + i] = t;
   }
+  __syncthreads();
+}
+
+template <int Q, int VAR, int R>
+__global__ __launch_bounds__(256) void xs_moments_kernel(
+    const float* __restrict__ X, const float* __restrict__ cap, const float* __restrict__ ret,
+    const int16_t* __restrict__ ind, int N, int Pseg, double* __restrict__ mom) {
+  __shared__ __attribute__((aligned(16))) char ring[Ring<Q>::BYTES];
+  extern __shared__ double dyn[];
+  const int d = blockIdx.x;
+  moments_body<Q, VAR, R>(X, cap, ret, ind, N, Pseg, d, ring, dyn,
+                          mom + (size_t)d * Layout<Q>::msize(Pseg));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -288,13 +306,22 @@ __global__ __launch_bounds__(256) void xs_moments_kernel(
 typedef double v4d __attribute__((ext_vector_type(4)));
 
 template <int Q>
-__global__ __launch_bounds__(64) void xs_solve_kernel(const double* __restrict__ mom, int P,
-                                                      int Pseg, int pivot_mode, double tol,
-                                                      double* __restrict__ fout,
-                                                      double* __restrict__ coef,
-                                                      double* __restrict__ stats,
-                                                      int* __restrict__ status,
-                                                      long long* __restrict__ stamps) {
+constexpr size_t solve_lds_doubles(int Pseg) {
+  using L = Layout<Q>;
+  return (size_t)L::msize(Pseg) + (size_t)(Q + 4) * (Q + 4) + (size_t)L::ND * (L::ND + 1) +
+         (Q + 2) + Q + 2 * (((size_t)Pseg + 3) & ~(size_t)3);
+}
+
+// Constrained solve of date d by ONE wave (threadIdx.x < 64).  `sm` (LDS, solve_lds_doubles)
+// holds the date's moments in [0, msize(Pseg)) on entry.  Writes f (global), the residual
+// coefficients `co` [Q+1+P] (global or LDS), stats/status (global) and, if non-null, the
+// status word to `st_lds`.
+template <int Q>
+__device__ __forceinline__ void solve_body(double* sm, int d, int P, int Pseg, int pivot_mode,
+                                           double tol, double* __restrict__ fout,
+                                           double* co, double* __restrict__ stats,
+                                           int* __restrict__ status, int* st_lds,
+                                           long long* __restrict__ stamps) {
   using L = Layout<Q>;
   constexpr int NS = L::NS, NG = L::NG, NACC = L::NACC, ND = L::ND;
   constexpr int NC = ND + 1;              // standardised industry row incl. the rhs
@@ -303,11 +330,8 @@ __global__ __launch_bounds__(64) void xs_solve_kernel(const double* __restrict__
   static_assert(TT <= 2, "Q <= 28");
   // optional phase timestamps (s_memtime, core clocks) for latency attribution
   auto stamp = [&](int k) {
-    if (stamps && threadIdx.x == 0) stamps[(size_t)blockIdx.x * 8 + k] = __builtin_amdgcn_s_memtime();
+    if (stamps && threadIdx.x == 0) stamps[(size_t)d * 8 + k] = __builtin_amdgcn_s_memtime();
   };
-  stamp(0);
-  extern __shared__ double sm[];
-  const int d = blockIdx.x;
   const int lane = threadIdx.x;
   const int K = 1 + P + Q;
   const int MS = L::msize(Pseg);
@@ -320,21 +344,6 @@ __global__ __launch_bounds__(64) void xs_solve_kernel(const double* __restrict__
   double* muv = gpv + NC;                 // [Q]
   double* ajv = muv + Q;                  // [P4]        a_j
   double* iwv = ajv + P4;                 // [P4]        1 / W_j
-  const double* md = mom + (size_t)d * MS;
-  for (int i0 = 0; i0 < MS; i0 += 8 * 64) {  // 8 independent loads in flight per lane
-    double tmp[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = i0 + u * 64 + lane;
-      tmp[u] = i < MS ? md[i] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = i0 + u * 64 + lane;
-      if (i < MS) sm[i] = tmp[u];
-    }
-  }
-  wave_sync_lds();
   stamp(1);
 
   const double Sc = acc[NG + 2 * Q + 0];
@@ -529,7 +538,6 @@ __global__ __launch_bounds__(64) void xs_solve_kernel(const double* __restrict__
   }
   const bool bad = (st & XS_BAD) != 0;
   double* fo = fout + (size_t)d * K;
-  double* co = coef + (size_t)d * (Q + 1 + P);
   for (int j = lane; j < P; j += 64) {
     const double* p = seg + j * NS;
     const double W = p[0];
@@ -560,6 +568,7 @@ __global__ __launch_bounds__(64) void xs_solve_kernel(const double* __restrict__
     for (int q = 0; q < Q; ++q) cst -= b[1 + q] * isig * muv[q];
     co[Q] = bad ? qnan() : cst;
     status[d] = st;
+    if (st_lds) *st_lds = st;
   }
   if (stats) {
     double* sd = stats + (size_t)d * (Q + 2);
@@ -570,22 +579,50 @@ __global__ __launch_bounds__(64) void xs_solve_kernel(const double* __restrict__
   stamp(5);
 }
 
+template <int Q>
+__global__ __launch_bounds__(64) void xs_solve_kernel(const double* __restrict__ mom, int P,
+                                                      int Pseg, int pivot_mode, double tol,
+                                                      double* __restrict__ fout,
+                                                      double* __restrict__ coef,
+                                                      double* __restrict__ stats,
+                                                      int* __restrict__ status,
+                                                      long long* __restrict__ stamps) {
+  extern __shared__ double sm[];
+  const int d = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (stamps && lane == 0) stamps[(size_t)d * 8] = __builtin_amdgcn_s_memtime();
+  const int MS = Layout<Q>::msize(Pseg);
+  const double* md = mom + (size_t)d * MS;
+  for (int i0 = 0; i0 < MS; i0 += 8 * 64) {  // 8 independent loads in flight per lane
+    double tmp[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * 64 + lane;
+      tmp[u] = i < MS ? md[i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * 64 + lane;
+      if (i < MS) sm[i] = tmp[u];
+    }
+  }
+  wave_sync_lds();
+  solve_body<Q>(sm, d, P, Pseg, pivot_mode, tol, fout, coef + (size_t)d * (Q + 1 + P), stats,
+                status, nullptr, stamps);
+}
+
 // ------------------------------------------------------------------------------------------
 // K3: specific returns and R^2 (dates visited in reverse: MALL-resident tail of K1 first)
 // ------------------------------------------------------------------------------------------
+// Specific returns + R^2 of date d from the coefficients `cf_s` [Q+1+P] (LDS) by the whole
+// workgroup (<= 16 waves); `red` = 16 x 5 doubles of LDS.
 template <int Q>
-__global__ __launch_bounds__(256) void xs_resid_kernel(
+__device__ __forceinline__ void resid_body(
     const float* __restrict__ X, const float* __restrict__ cap, const float* __restrict__ ret,
-    const int16_t* __restrict__ ind, int D, int N, int P, const double* __restrict__ coef,
-    const int* __restrict__ status, float* __restrict__ eout, double* __restrict__ r2out) {
-  __shared__ double cf_s[Q + 1 + 128];
-  __shared__ double red[4][5];
-  const int d = D - 1 - blockIdx.x;
+    const int16_t* __restrict__ ind, int d, int N, int P, const double* cf_s, bool bad,
+    float* __restrict__ eout, double* __restrict__ r2out, double (*red)[5]) {
   const int tid = threadIdx.x;
   const int Pseg = P > 0 ? P : 1;
-  const double* co = coef + (size_t)d * (Q + 1 + P);
-  for (int i = tid; i < Q + 1 + P; i += blockDim.x) cf_s[i] = co[i];
-  __syncthreads();
   double beta[Q];
 #pragma unroll
   for (int q = 0; q < Q; ++q) beta[q] = cf_s[q];
@@ -597,12 +634,11 @@ __global__ __launch_bounds__(256) void xs_resid_kernel(
   const int16_t* id = ind ? ind + (size_t)d * N : nullptr;
   float* ed = eout ? eout + (size_t)d * N : nullptr;
   double se = 0.0, see = 0.0, sr = 0.0, srr = 0.0, nn = 0.0;
-  for (int n = tid; n < N; n += blockDim.x) {
-    const float c = cd[n], r = rd[n];
-    const int j = id ? (int)id[n] : 0;
-    float xf[Q];
-#pragma unroll
-    for (int q = 0; q < Q; ++q) xf[q] = Xd[(size_t)q * N + n];
+  // Four consecutive stocks per thread (16-byte loads; N % 8 == 0 keeps rows aligned) and U
+  // iterations' loads issued before any is consumed: the pass is latency-bound otherwise.
+  constexpr int U = 3;
+  const int step = blockDim.x * 4;
+  auto one = [&](float c, float r, int j, const float (&xf)[Q]) -> float {
     bool ok = (j >= 0) && (j < Pseg) && finite_f(c) && (c >= 0.f) && finite_f(r);
     double e = (double)r - cst;
 #pragma unroll
@@ -620,7 +656,41 @@ __global__ __launch_bounds__(256) void xs_resid_kernel(
       nn += 1.0;
       eo = (float)e;
     }
-    if (ed) ed[n] = eo;
+    return eo;
+  };
+  for (int n0 = tid * 4; n0 < N; n0 += U * step) {
+    float4 c4[U], r4[U], x4[U][Q];
+    uint2 j4[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int n = n0 + u * step;
+      if (n < N) {
+        c4[u] = *(const float4*)(cd + n);
+        r4[u] = *(const float4*)(rd + n);
+#pragma unroll
+        for (int q = 0; q < Q; ++q) x4[u][q] = *(const float4*)(Xd + (size_t)q * N + n);
+        j4[u] = id ? *(const uint2*)(id + n) : make_uint2(0u, 0u);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int n = n0 + u * step;
+      if (n < N) {
+        const int js[4] = {(int)(short)(j4[u].x & 0xFFFF), (int)(short)(j4[u].x >> 16),
+                           (int)(short)(j4[u].y & 0xFFFF), (int)(short)(j4[u].y >> 16)};
+        const float cs[4] = {c4[u].x, c4[u].y, c4[u].z, c4[u].w};
+        const float rs[4] = {r4[u].x, r4[u].y, r4[u].z, r4[u].w};
+        float eo[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float xf[Q];
+#pragma unroll
+          for (int q = 0; q < Q; ++q) xf[q] = ((const float*)&x4[u][q])[k];
+          eo[k] = one(cs[k], rs[k], js[k], xf);
+        }
+        if (ed) *(float4*)(ed + n) = make_float4(eo[0], eo[1], eo[2], eo[3]);
+      }
+    }
   }
   se = wave_sum(se); see = wave_sum(see); sr = wave_sum(sr); srr = wave_sum(srr); nn = wave_sum(nn);
   const int w = tid >> 6;
@@ -635,11 +705,74 @@ __global__ __launch_bounds__(256) void xs_resid_kernel(
     }
     const double ve = b / n - (a / n) * (a / n);
     const double vr = e2 / n - (c / n) * (c / n);
-    r2out[d] = (status[d] & XS_BAD) ? qnan() : 1.0 - ve / vr;
+    r2out[d] = bad ? qnan() : 1.0 - ve / vr;
+  }
+}
+
+template <int Q>
+__global__ __launch_bounds__(256) void xs_resid_kernel(
+    const float* __restrict__ X, const float* __restrict__ cap, const float* __restrict__ ret,
+    const int16_t* __restrict__ ind, int D, int N, int P, const double* __restrict__ coef,
+    const int* __restrict__ status, float* __restrict__ eout, double* __restrict__ r2out) {
+  __shared__ double cf_s[Q + 1 + 128];
+  __shared__ double red[16][5];
+  const int d = D - 1 - blockIdx.x;
+  const double* co = coef + (size_t)d * (Q + 1 + P);
+  for (int i = threadIdx.x; i < Q + 1 + P; i += blockDim.x) cf_s[i] = co[i];
+  __syncthreads();
+  resid_body<Q>(X, cap, ret, ind, d, N, P, cf_s, (status[d] & XS_BAD) != 0, eout, r2out, red);
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused K1 -> K2 -> K3: one 4-wave workgroup per date streams the date's panel slice once
+// from HBM (moments), solves it in wave 0, then re-reads the slice for the residual pass.
+// Two workgroups fit per CU, so ~512 dates (~128 MB of panel) are in flight: the re-read is
+// served by the 256 MB Infinity Cache instead of HBM, and the single-wave solve of one date
+// overlaps the other workgroup's streaming.  HBM traffic drops from ~2x to ~1x the panel.
+// ------------------------------------------------------------------------------------------
+template <int Q, int R, int VAR = 0>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void xs_fused_kernel(
+    const float* __restrict__ X, const float* __restrict__ cap, const float* __restrict__ ret,
+    const int16_t* __restrict__ ind, int N, int P, int Pseg, int pivot_mode, double tol,
+    double* __restrict__ fout, float* __restrict__ eout, double* __restrict__ r2out,
+    double* __restrict__ stats, int* __restrict__ status, long long* __restrict__ stamps) {
+  static_assert(solve_lds_doubles<Q>(128) * 8 <= (size_t)Ring<Q>::BYTES, "solve scratch");
+  __shared__ __attribute__((aligned(16))) char ring[Ring<Q>::BYTES];
+  __shared__ double cf_s[Q + 1 + 128];
+  __shared__ double red[4][5];
+  __shared__ int st_s;
+  extern __shared__ double dyn[];
+  const int d = blockIdx.x;
+  // optional per-date phase stamps (s_memtime) + hardware ids for occupancy analysis
+  auto stamp = [&](int k) {
+    if (stamps && threadIdx.x == 0) stamps[(size_t)d * 8 + k] = __builtin_amdgcn_s_memtime();
+  };
+  stamp(0);
+  double* sm = (double*)ring;  // moments, then the solve's scratch (ring is idle by then)
+  moments_body<Q, VAR & 3, R>(X, cap, ret, ind, N, Pseg, d, ring, dyn, sm);
+  stamp(1);
+  if constexpr ((VAR & 8) != 0) {  // timing-only ablation: no solve
+    for (int i = threadIdx.x; i < Q + 1 + P; i += blockDim.x) cf_s[i] = sm[i] * 1e-30;
+    if (threadIdx.x == 0) st_s = 0;
+  } else if (threadIdx.x < 64) {
+    // solve-internal phase stamps go to the second [D][8] block of the stamp buffer
+    long long* ss = stamps ? stamps + (size_t)gridDim.x * 8 : nullptr;
+    if (ss && threadIdx.x == 0) ss[(size_t)d * 8] = __builtin_amdgcn_s_memtime();
+    solve_body<Q>(sm, d, P, Pseg, pivot_mode, tol, fout, cf_s, stats, status, &st_s, ss);
+  }
+  __syncthreads();
+  stamp(2);
+  if constexpr ((VAR & 4) == 0)
+    resid_body<Q>(X, cap, ret, ind, d, N, P, cf_s, (st_s & XS_BAD) != 0, eout, r2out, red);
+  stamp(3);
+  if (stamps && threadIdx.x == 0) {
+    stamps[(size_t)d * 8 + 4] = (long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
+    stamps[(size_t)d * 8 + 5] = (long long)__builtin_amdgcn_s_getreg((31 << 11) | 20);  // XCC_ID
   }
 }
 
 long long* g_stamps = nullptr;  // debug: per-date K2 phase stamps [D][8]
+int g_xs_mode = 0;              // 0 = fused single kernel, 1 = three kernels (ablation)
 
 template <int Q, int VAR = 0>
 hipError_t launch_q(const float* X, const float* cap, const float* ret, const int16_t* ind,
@@ -662,6 +795,16 @@ hipError_t launch_q(const float* X, const float* cap, const float* ret, const in
                        2 * P4) * sizeof(double);
   if (lds1 + ring > 160 * 1024 || lds2 > 64 * 1024) return hipErrorInvalidValue;
   const int16_t* indp = P > 0 ? ind : nullptr;
+  if (g_xs_mode == 0 || g_xs_mode == 2) {
+    long long* st = g_xs_mode == 2 ? g_stamps : nullptr;
+    if (rep8)
+      hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR>), dim3(D), dim3(256), lds1, s, X, cap, ret,
+                         indp, N, P, Pseg, pivot_mode, tol, f, e, r2, stats, status, st);
+    else
+      hipLaunchKernelGGL((xs_fused_kernel<Q, 1>), dim3(D), dim3(256), lds1, s, X, cap, ret, indp,
+                         N, P, Pseg, pivot_mode, tol, f, e, r2, stats, status, st);
+    return hipGetLastError();
+  }
   if (rep8)
     hipLaunchKernelGGL((xs_moments_kernel<Q, VAR, kRepMax>), dim3(D), dim3(256), lds1, s, X, cap,
                        ret, indp, N, Pseg, mom);
@@ -680,6 +823,10 @@ hipError_t launch_q(const float* X, const float* cap, const float* ret, const in
 
 // Debug: record K2 phase timestamps (s_memtime) into buf[D][8] on the next calls (null = off).
 MFA_API void mfa_xs_set_stamps(long long* buf) { g_stamps = buf; }
+
+// Ablation: 0 = fused single-kernel path (default), 1 = three separate kernels, 2 = fused with
+// per-date phase stamps into the mfa_xs_set_stamps buffer.
+MFA_API void mfa_xs_set_mode(int mode) { g_xs_mode = mode; }
 
 // Workspace bytes needed by mfa_xs_wls: D * (msize + Q + 1 + P) doubles.
 MFA_API size_t mfa_xs_wls_workspace(int D, int P, int Q) {
@@ -714,7 +861,8 @@ MFA_API int mfa_xs_wls(const float* X, const float* cap, const float* ret, const
   return (int)hipErrorInvalidValue;
 }
 
-// Timing-only ablation entry (Q = 10): bit 1 = no segment atomics, bit 4 = no residual pass.
+// Timing-only ablation entry (Q = 10): bit 1 = no segment atomics, bit 2 = no style-Gram FMAs,
+// bit 4 = no residual pass, bit 8 = no solve (fused mode only).
 MFA_API int mfa_xs_wls_variant(const float* X, const float* cap, const float* ret,
                                const int16_t* ind, int D, int N, int P, int variant, double* f,
                                float* e, double* r2, double* stats, int* status, void* ws,
@@ -726,7 +874,8 @@ MFA_API int mfa_xs_wls_variant(const float* X, const float* cap, const float* re
   case vv:                                                                                     \
     return (int)launch_q<10, vv>(X, cap, ret, ind, D, N, P, 0, 1e-14, f, e, r2, stats,        \
                                  status, w, s);
-    MFA_V(0) MFA_V(1) MFA_V(4) MFA_V(5) MFA_V(6) MFA_V(7)
+    MFA_V(0) MFA_V(1) MFA_V(2) MFA_V(3) MFA_V(4) MFA_V(5) MFA_V(6) MFA_V(7) MFA_V(8)
+    MFA_V(12) MFA_V(15)
 #undef MFA_V
   }
   return (int)hipErrorInvalidValue;

@@ -78,6 +78,44 @@ class RiskPanel:
         return n + (0 if self.ind is None else self.ind.numel() * 2)
 
 
+def industry_order(ind: torch.Tensor, P: int) -> torch.Tensor:
+    """Stock permutation that groups stocks by their modal industry over the panel's dates.
+
+    SW-L1 membership of a stock changes rarely, so in this order almost every run of
+    consecutive stocks shares one industry on every date.  The regression kernel then folds a
+    whole run into the per-industry sums with one LDS atomic per run boundary instead of one
+    per stock (csrc/xs_wls.hip, K1).  Stocks never assigned an industry go last; ties keep the
+    original order (stable).
+    """
+    D, N = ind.shape
+    if P <= 0:
+        return torch.arange(N, device=ind.device)
+    il = ind.long()
+    ok = (il >= 0) & (il < P)
+    counts = torch.zeros(N, P + 1, dtype=torch.int32, device=ind.device)
+    idx = torch.where(ok, il, torch.full_like(il, P))                  # absent -> bucket P
+    counts.scatter_add_(1, idx.T.contiguous(), torch.ones(N, D, dtype=torch.int32, device=ind.device))
+    modal = counts[:, :P].argmax(1)
+    modal = torch.where(counts[:, :P].sum(1) > 0, modal, torch.full_like(modal, P))
+    key = modal * N + torch.arange(N, device=ind.device)
+    return torch.argsort(key)
+
+
+def order_by_industry(panel: "RiskPanel") -> "RiskPanel":
+    """The same panel with its stock axis permuted by :func:`industry_order`.
+
+    A pure layout change: every per-date regression result is identical up to the order of the
+    stocks (``panel.stocks`` is permuted alongside, so stock labels stay attached).
+    """
+    if panel.ind is None:
+        return panel
+    perm = industry_order(panel.ind, panel.P)
+    pc = perm.cpu().numpy()
+    return replace(panel, styles=panel.styles[:, :, perm].contiguous(),
+                   cap=panel.cap[:, perm].contiguous(), ret=panel.ret[:, perm].contiguous(),
+                   ind=panel.ind[:, perm].contiguous(), stocks=np.asarray(panel.stocks)[pc])
+
+
 def business_days(D: int, start: str = "2010-01-04") -> np.ndarray:
     return np.asarray(np.busday_offset(np.datetime64(start, "D"), np.arange(D), roll="forward"),
                       dtype="datetime64[ns]")
