@@ -105,16 +105,22 @@ __device__ __forceinline__ double pick(const double (&a)[Q], int i) {
   return r;
 }
 
+#ifndef MFA_XS_RING
+#define MFA_XS_RING 4
+#endif
+#ifndef MFA_XS_REP
+#define MFA_XS_REP 8
+#endif
 constexpr int kTile = 256;            // stocks per staged tile (K3)
 constexpr int kRowBytes = kTile * 4;  // one fp32 field row of a tile
 // Segment-table replicas: entry (j, ch) owns R consecutive doubles and lane l adds into slot
 // l & (R-1).  With R = 8 the 16 lanes of a ds_add_f64 issue group land on bank pairs
 // (l & 7) + 8 * ((j*NS + ch) & 1): at most 2-way conflicts whatever the industry mix (4
 // lane-strided replicas measured 8.3 conflict cycles per instruction).
-constexpr int kRepMax = 8;
+constexpr int kRepMax = MFA_XS_REP;
 constexpr int kSegLdsBudget = 48 * 1024;  // R = 8 only while the table leaves 2 WGs / CU
 constexpr int kWT = 64;               // stocks per wave tile (K1: one stock per lane)
-constexpr int kWNB = 4;               // K1 per-wave ring depth
+constexpr int kWNB = MFA_XS_RING;     // K1 per-wave ring depth
 
 template <int Q>
 struct Layout {
@@ -658,7 +664,11 @@ __device__ __forceinline__ void resid_body(
     }
     return eo;
   };
-  for (int n0 = tid * 4; n0 < N; n0 += U * step) {
+  // Blocks of U*step stocks walked from the END of the date: the moments pass streamed the
+  // tail last, so the re-read starts with the lines most likely still in the Infinity Cache.
+  const int nblk = (N + U * step - 1) / (U * step);
+  for (int b = nblk - 1; b >= 0; --b) {
+    const int n0 = b * U * step + tid * 4;
     float4 c4[U], r4[U], x4[U][Q];
     uint2 j4[U];
 #pragma unroll
@@ -764,6 +774,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   stamp(2);
   if constexpr ((VAR & 4) == 0)
     resid_body<Q>(X, cap, ret, ind, d, N, P, cf_s, (st_s & XS_BAD) != 0, eout, r2out, red);
+  if constexpr ((VAR & 16) != 0) {  // timing-only: a second residual pass (cache-hit cost)
+    __syncthreads();
+    resid_body<Q>(X, cap, ret, ind, d, N, P, cf_s, (st_s & XS_BAD) != 0, eout, r2out, red);
+  }
   stamp(3);
   if (stamps && threadIdx.x == 0) {
     stamps[(size_t)d * 8 + 4] = (long long)__builtin_amdgcn_s_getreg((31 << 11) | 4);   // HW_ID
@@ -784,8 +798,7 @@ hipError_t launch_q(const float* X, const float* cap, const float* ret, const in
   const int MS = L::msize(Pseg);
   double* mom = ws;
   double* coef = ws + (size_t)D * MS;
-  const size_t ring = 4 * (size_t)kWNB * L::WSLOT > 4 * 8 * 65 * 8 ? 4 * (size_t)kWNB * L::WSLOT
-                                                                     : 4 * 8 * 65 * 8;
+  const size_t ring = Ring<Q>::BYTES;
   const size_t seg8 = (size_t)kRepMax * Pseg * L::NS * sizeof(double);
   const bool rep8 = seg8 <= kSegLdsBudget;
   const size_t lds1 = ((rep8 ? (size_t)kRepMax : 1) * Pseg * L::NS + L::NACC) * sizeof(double);
@@ -875,7 +888,7 @@ MFA_API int mfa_xs_wls_variant(const float* X, const float* cap, const float* re
     return (int)launch_q<10, vv>(X, cap, ret, ind, D, N, P, 0, 1e-14, f, e, r2, stats,        \
                                  status, w, s);
     MFA_V(0) MFA_V(1) MFA_V(2) MFA_V(3) MFA_V(4) MFA_V(5) MFA_V(6) MFA_V(7) MFA_V(8)
-    MFA_V(12) MFA_V(15)
+    MFA_V(12) MFA_V(15) MFA_V(16) MFA_V(20)
 #undef MFA_V
   }
   return (int)hipErrorInvalidValue;
