@@ -210,8 +210,10 @@ __global__ __launch_bounds__(64) void eigh_kernel(const double* __restrict__ Ain
 // Grid (M).  One wave: KP = 64 padded columns -> 2 x 2 output tiles of 32 x 32.
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 __global__ __launch_bounds__(64) void mc_cov_kernel(int K, int T, unsigned long long seed,
-                                                    double* __restrict__ Cz) {
-  const int m = blockIdx.x, lane = threadIdx.x;
+                                                    int m0, double* __restrict__ Cz) {
+  // simulation m0 + blockIdx.x: the Philox stream depends only on (seed, global sim index), so
+  // any partition of the sims over chunks / ranks draws exactly the single-run covariances
+  const int m = m0 + blockIdx.x, lane = threadIdx.x;
   __shared__ float Z[64][65];   // 64 time rows x 64 (padded) factors
   __shared__ double colsum[64];
   const int col = lane & 31, half = lane >> 5;
@@ -255,7 +257,7 @@ __global__ __launch_bounds__(64) void mc_cov_kernel(int K, int T, unsigned long 
   }
   colsum[lane] = cs;
   wsync();
-  double* C = Cz + (size_t)m * K * K;
+  double* C = Cz + (size_t)blockIdx.x * K * K;
   const double invT1 = 1.0 / (double)(T - 1), invT = 1.0 / (double)T;
 #pragma unroll
   for (int t = 0; t < 3; ++t) {
@@ -450,12 +452,25 @@ size_t bias_lds(int K) {
   return ((size_t)Ke * (Ke + 1) + 64) * sizeof(double) + 32 * sizeof(double2) + 64 * sizeof(int);
 }
 
+// Sum of the per-sim bias values over this chunk's sims, accumulated into S[d][k] (fixed
+// order: deterministic).  Grid (D), block 64.
+__global__ __launch_bounds__(64) void bias_sum_kernel(const double* __restrict__ vin, int K,
+                                                      int M, double* __restrict__ S) {
+  const int d = blockIdx.x;
+  for (int k = threadIdx.x; k < K; k += 64) {
+    double s = 0.0;
+    for (int m = 0; m < M; ++m) s += vin[((size_t)d * M + m) * K + k];
+    S[(size_t)d * K + k] += s;
+  }
+}
+
 // finalize: v = sqrt(mean_m v_m); v = a (v - 1) + 1; F^ = U0 diag(v^2 D0) U0^T.  Grid (D).
+// `vin` holds per-sim values [D][M][K], or (M_sum > 0) per-date sums [D][K] over M_sum sims.
 __global__ __launch_bounds__(256) void eigen_finalize_kernel(const double* __restrict__ vin,
                                                              const double* __restrict__ D0,
                                                              const double* __restrict__ U0,
                                                              const int* __restrict__ dvalid,
-                                                             int K, int M, double scale,
+                                                             int K, int M, int M_sum, double scale,
                                                              double* __restrict__ Fout,
                                                              double* __restrict__ vbias) {
   __shared__ double g[64];
@@ -463,8 +478,12 @@ __global__ __launch_bounds__(256) void eigen_finalize_kernel(const double* __res
   const bool ok = dvalid[d] != 0;
   for (int k = tid; k < K; k += blockDim.x) {
     double s = 0.0;
-    for (int m = 0; m < M; ++m) s += vin[((size_t)d * M + m) * K + k];
-    double v = sqrt(s / M);
+    if (M_sum > 0) {
+      s = vin[(size_t)d * K + k];
+    } else {
+      for (int m = 0; m < M; ++m) s += vin[((size_t)d * M + m) * K + k];
+    }
+    double v = sqrt(s / (M_sum > 0 ? M_sum : M));
     v = scale * (v - 1.0) + 1.0;
     if (vbias) vbias[(size_t)d * K + k] = ok ? v : qnan();
     g[k] = ok ? v * v * D0[(size_t)d * K + k] : qnan();
@@ -495,7 +514,16 @@ MFA_API int mfa_eigh_batched(const double* A, int B, int K, int max_sweeps, doub
 MFA_API int mfa_mc_cov(int M, int K, int T, unsigned long long seed, double* Cz, void* stream) {
   if (M <= 0) return 0;
   if (K < 1 || K > 64 || T < 2) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(mc_cov_kernel, dim3(M), dim3(64), 0, (hipStream_t)stream, K, T, seed, Cz);
+  hipLaunchKernelGGL(mc_cov_kernel, dim3(M), dim3(64), 0, (hipStream_t)stream, K, T, seed, 0, Cz);
+  return (int)hipGetLastError();
+}
+
+// Draw covariances of sims [m0, m0 + M) (identical to those of a single mfa_mc_cov over all sims).
+MFA_API int mfa_mc_cov_range(int M, int m0, int K, int T, unsigned long long seed, double* Cz,
+                             void* stream) {
+  if (M <= 0) return 0;
+  if (K < 1 || K > 64 || T < 2 || m0 < 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(mc_cov_kernel, dim3(M), dim3(64), 0, (hipStream_t)stream, K, T, seed, m0, Cz);
   return (int)hipGetLastError();
 }
 
@@ -515,6 +543,36 @@ MFA_API int mfa_eigen_adjust(const double* D0, const double* U0, const int* dval
     hipLaunchKernelGGL(mc_bias_kernel<9>, dim3(D * M), dim3(64), bias_lds(K), s, D0, K, M, Cz,
                        dvalid, max_sweeps, tol, ws);
   hipLaunchKernelGGL(eigen_finalize_kernel, dim3(D), dim3(256), 0, s, ws, D0, U0, dvalid, K, M,
-                     scale, Fout, vbias);
+                     0, scale, Fout, vbias);
+  return (int)hipGetLastError();
+}
+
+// Chunked / sharded Monte Carlo: S[d][k] += sum over this call's M sims of v_m[d][k].
+// ws: D*M*K doubles.  Invalid dates accumulate NaN (finalize masks them anyway).
+MFA_API int mfa_eigen_bias_accumulate(const double* D0, const int* dvalid, int D, int K, int M,
+                                      const double* Cz, int max_sweeps, double tol, double* ws,
+                                      double* S, void* stream) {
+  if (D <= 0 || M <= 0) return 0;
+  if (K < 1 || K > 64) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  const int Ke = K + (K & 1), npair = Ke / 2, nb = npair * (npair + 1) / 2;
+  if (nb <= 4 * 64)
+    hipLaunchKernelGGL(mc_bias_kernel<4>, dim3(D * M), dim3(64), bias_lds(K), s, D0, K, M, Cz,
+                       dvalid, max_sweeps, tol, ws);
+  else
+    hipLaunchKernelGGL(mc_bias_kernel<9>, dim3(D * M), dim3(64), bias_lds(K), s, D0, K, M, Cz,
+                       dvalid, max_sweeps, tol, ws);
+  hipLaunchKernelGGL(bias_sum_kernel, dim3(D), dim3(64), 0, s, ws, K, M, S);
+  return (int)hipGetLastError();
+}
+
+// Finalize from accumulated sums S [D][K] over M_total sims.
+MFA_API int mfa_eigen_finalize_sum(const double* S, int M_total, const double* D0, const double* U0,
+                                   const int* dvalid, int D, int K, double scale, double* Fout,
+                                   double* vbias, void* stream) {
+  if (D <= 0) return 0;
+  if (K < 1 || K > 64 || M_total < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(eigen_finalize_kernel, dim3(D), dim3(256), 0, (hipStream_t)stream, S, D0, U0,
+                     dvalid, K, 1, M_total, scale, Fout, vbias);
   return (int)hipGetLastError();
 }

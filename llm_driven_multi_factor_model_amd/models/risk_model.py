@@ -111,9 +111,25 @@ class RiskModel:
         T_sim = T_sim or self.cfg.eigen_sim_length or self.T
         seed = self.cfg.eigen_seed if seed is None else seed
         with self._stage("eigen_adjust"):
-            self.eigen_cov, self.eigen_bias = eigen.eigen_risk_adjust(
-                self.nw_cov, M=M, scale_coef=scale_coef, T_sim=T_sim, seed=seed,
-                psd_tol=self.cfg.psd_tol, return_bias=True)
+            if self.cfg.eigen_shard == "sims":
+                # Simulations sharded over ranks (10k-bootstrap configuration): every rank
+                # rebuilds the Newey-West series of ALL new dates (an O(T K^2) scan, cheaper
+                # than gathering [T, K, K]), runs its block of sims on all of them, and one
+                # all_reduce of the [T, K] bias sums (C5) completes the mean over M.
+                lo_new = self.T_hist
+                nw_all = ew_scan.newey_west_series(self.factor_ret_global, self.cfg.nw_lags,
+                                                   self.cfg.nw_half_life, lo_new, self.T)
+                Fh, vb = eigen.eigen_risk_adjust_sharded(
+                    nw_all, M=M, scale_coef=scale_coef, T_sim=T_sim, seed=seed,
+                    chunk=self.cfg.eigen_chunk, ctx=self.ctx, psd_tol=self.cfg.psd_tol,
+                    return_bias=True)
+                a = self.t_lo - lo_new
+                self.eigen_cov = Fh[a:a + self.panel.D].contiguous()
+                self.eigen_bias = vb[a:a + self.panel.D].contiguous()
+            else:
+                self.eigen_cov, self.eigen_bias = eigen.eigen_risk_adjust(
+                    self.nw_cov, M=M, scale_coef=scale_coef, T_sim=T_sim, seed=seed,
+                    psd_tol=self.cfg.psd_tol, return_bias=True)
         return self.eigen_cov
 
     # --------------------------------------------------------------- stage 4: VRA

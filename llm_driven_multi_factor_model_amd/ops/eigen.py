@@ -29,6 +29,14 @@ _native.register("mfa_mc_cov", [C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_void_
 _native.register("mfa_eigen_adjust", [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
                                        C.c_int, C.c_void_p, C.c_double, C.c_int, C.c_double,
                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p])
+_native.register("mfa_mc_cov_range", [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_void_p,
+                                       C.c_void_p])
+_native.register("mfa_eigen_bias_accumulate", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                                C.c_void_p, C.c_int, C.c_double, C.c_void_p,
+                                                C.c_void_p, C.c_void_p])
+_native.register("mfa_eigen_finalize_sum", [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
+                                             C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p,
+                                             C.c_void_p, C.c_void_p])
 
 MAX_SWEEPS = 30
 TOL = 1e-15
@@ -68,20 +76,100 @@ def _eigh_reference(Ab, shp):
     return w.reshape(shp[:-1]), U.reshape(shp)
 
 
-def mc_cov(M: int, K: int, T: int, seed: int = 1, device="cuda") -> torch.Tensor:
-    """Draw covariances ``cov(z_m)`` (ddof 1) of M independent [T x K] standard-normal panels."""
+def mc_cov(M: int, K: int, T: int, seed: int = 1, device="cuda", m0: int = 0) -> torch.Tensor:
+    """Draw covariances ``cov(z_m)`` (ddof 1) of simulations ``m0 .. m0+M-1``, each an
+    independent [T x K] standard-normal panel.
+
+    Every simulation has its own counter-based stream keyed by ``(seed, m)`` (Philox on the GPU,
+    a per-sim ``torch.Generator`` on the CPU), so splitting the sims over chunks or ranks draws
+    exactly the covariances of one unsplit call.
+    """
     dev = torch.device(device)
     if dev.type != "cuda":
-        g = torch.Generator().manual_seed(int(seed))
         Cz = torch.empty(M, K, K, dtype=torch.float64)
-        for m in range(M):
+        for i in range(M):
+            g = torch.Generator().manual_seed((int(seed) * 1_000_003 + m0 + i) & 0x7FFFFFFFFFFFFFFF)
             z = torch.randn(T, K, generator=g, dtype=torch.float64)
-            Cz[m] = torch.cov(z.T)
+            Cz[i] = torch.cov(z.T)
         return Cz
     Cz = torch.empty(M, K, K, dtype=torch.float64, device=dev)
-    _native.call("mfa_mc_cov", M, K, T, int(seed) & 0xFFFFFFFFFFFFFFFF, _native.ptr(Cz),
-                 _native.stream(dev))
+    _native.call("mfa_mc_cov_range", M, int(m0), K, T, int(seed) & 0xFFFFFFFFFFFFFFFF,
+                 _native.ptr(Cz), _native.stream(dev))
     return Cz
+
+
+def sim_shard(M: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous block ``[m0, m1)`` of the M simulations owned by ``rank``."""
+    base, rem = divmod(M, world)
+    m0 = rank * base + min(rank, rem)
+    return m0, m0 + base + (1 if rank < rem else 0)
+
+
+def eigen_risk_adjust_sharded(F0: torch.Tensor, *, M: int = 10_000, scale_coef: float = 1.4,
+                              T_sim: int | None = None, seed: int = 1, chunk: int = 256,
+                              ctx=None, psd_tol: float = 0.0, return_bias: bool = False):
+    """Monte-Carlo eigen adjustment with the simulations sharded over ranks and chunked in time.
+
+    For large M (the 10k-bootstrap configuration) the per-(date, sim) bias values are never
+    materialised: each rank draws only its block of simulations (:func:`sim_shard`), ``chunk``
+    at a time, and accumulates ``S[d, k] = sum_m v_m[d, k]`` on the device; one
+    ``all_reduce(SUM)`` of the [D, K] float64 sums over RCCL (collective C5 of SURVEY.md §2.5)
+    then gives every rank the full-M mean.  ``F0`` must hold the SAME dates on every rank.
+    Results equal :func:`eigen_risk_adjust` with the same M and seed up to summation order.
+    """
+    from ..parallel import dist as pdist
+    ctx = ctx or pdist.context()
+    F0 = F0.to(torch.float64).contiguous()
+    D, K, _ = F0.shape
+    T_sim = D if T_sim is None else T_sim
+    dev = F0.device
+    w, U = eigh(F0)
+    valid = torch.isfinite(w).all(-1) & (w.min(-1).values >= -psd_tol * w.abs().max(-1).values.clamp_min(0))
+    w = torch.where(valid[:, None], w.clamp_min(0.0), w).contiguous()
+    rank, world = (ctx.rank, ctx.world) if ctx.enabled else (0, 1)
+    m0, m1 = sim_shard(M, rank, world)
+    S = torch.zeros(D, K, dtype=torch.float64, device=dev)
+    if dev.type == "cuda":
+        dv = valid.to(torch.int32).contiguous()
+        ws = torch.empty(D * min(chunk, max(1, m1 - m0)) * K, dtype=torch.float64, device=dev)
+        for a in range(m0, m1, chunk):
+            mc = min(chunk, m1 - a)
+            Cz = mc_cov(mc, K, max(T_sim, 2), seed, dev, m0=a)
+            _native.call("mfa_eigen_bias_accumulate", _native.ptr(w), _native.ptr(dv), D, K, mc,
+                         _native.ptr(Cz), MAX_SWEEPS, TOL, _native.ptr(ws), _native.ptr(S),
+                         _native.stream(dev))
+    else:
+        for a in range(m0, m1, chunk):
+            mc = min(chunk, m1 - a)
+            Cz = mc_cov(mc, K, max(T_sim, 2), seed, dev, m0=a)
+            S += _bias_sum_reference(w, valid, Cz)
+    if ctx.enabled:
+        pdist.all_reduce_sum(S, ctx)
+    if dev.type == "cuda":
+        Fh = torch.empty(D, K, K, dtype=torch.float64, device=dev)
+        vb = torch.empty(D, K, dtype=torch.float64, device=dev)
+        _native.call("mfa_eigen_finalize_sum", _native.ptr(S), int(M), _native.ptr(w),
+                     _native.ptr(U.contiguous()), _native.ptr(valid.to(torch.int32).contiguous()),
+                     D, K, float(scale_coef), _native.ptr(Fh), _native.ptr(vb), _native.stream(dev))
+    else:
+        v = scale_coef * (torch.sqrt(S / M) - 1.0) + 1.0
+        vb = torch.where(valid[:, None], v, torch.full_like(v, float("nan")))
+        Fh = (U * (vb * vb * w)[:, None, :]) @ U.transpose(-1, -2)
+        Fh[~valid] = float("nan")
+    return (Fh, vb) if return_bias else Fh
+
+
+def _bias_sum_reference(w, valid, Cz):
+    """sum_m v_m[d, k] over the draw covariances ``Cz`` (CPU oracle of the accumulate kernel)."""
+    D, K = w.shape
+    S = torch.zeros(D, K, dtype=torch.float64)
+    for d in torch.nonzero(valid).flatten().tolist():
+        s = torch.sqrt(w[d])
+        lam, V = torch.linalg.eigh(s[None, :, None] * Cz * s[None, None, :])
+        lam, V = lam.flip(-1), V.flip(-1)
+        S[d] = (((V * V) * w[d][None, :, None]).sum(1) / lam).sum(0)
+    S[~valid] = float("nan")
+    return S
 
 
 def eigen_risk_adjust(F0: torch.Tensor, *, M: int = 100, scale_coef: float = 1.4,

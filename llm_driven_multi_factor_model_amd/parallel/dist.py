@@ -7,6 +7,7 @@ KB: latency-bound on xGMI, so the rule is ONE batched collective per stage, neve
 
 Collective call sites:
   C3 factor-return series      all_gather   (D_local x K fp64)
+  C5 MC bias accumulators      all_reduce   (D x K fp64, sims-sharded eigen adjustment)
   C6 VRA bias series           all_gather   (D_local fp64)
   C7 outputs to rank 0         gather       (only when writing CSVs)
   C8 benchmark fences          barrier
@@ -107,6 +108,14 @@ def all_reduce_max(x: float, ctx: DistContext | None = None, device=None) -> flo
     t = torch.tensor([x], dtype=torch.float64, device=device or ctx.device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def all_reduce_sum(x: torch.Tensor, ctx: DistContext | None = None) -> torch.Tensor:
+    """In-place SUM over ranks (one collective for the whole tensor)."""
+    ctx = ctx or context()
+    if ctx.enabled:
+        dist.all_reduce(x, op=dist.ReduceOp.SUM)
+    return x
 
 
 def barrier(ctx: DistContext | None = None) -> None:

@@ -25,6 +25,13 @@ class RiskConfig:
     pivot_mode: int = 0           # 0 = last non-empty industry; 1 = reference (quirk Q3)
     psd_tol: float = 0.0          # eigen adj requires D0 >= -psd_tol*max|D0| (reference: 0)
     vra_out_of_sample: bool = False  # True: B_t uses the forecast of t-1 (reference: in-sample, Q10)
+    eigen_shard: str = "dates"    # "dates": each rank adjusts its own dates with all M sims;
+                                  # "sims": ranks split the M sims of every date + all_reduce (C5)
+    eigen_chunk: int = 256        # sims per launch in "sims" mode (bounds the [D, chunk, K] buffer)
+
+    def __post_init__(self):
+        if self.eigen_shard not in ("dates", "sims"):
+            raise ValueError(f"eigen_shard must be 'dates' or 'sims', got {self.eigen_shard!r}")
 
     def to_dict(self) -> dict:
         return asdict(self)
@@ -66,6 +73,8 @@ PRESETS = {
     "reference": RiskConfig(),
     "use4s": RiskConfig(nw_lags=5, nw_half_life=84.0, vra_half_life=42.0),
     "use4l": RiskConfig(nw_lags=2, nw_half_life=252.0, vra_half_life=168.0),
+    # BASELINE.json config 5: Newey-West + 10k-simulation eigen "bootstrap", sims over ranks
+    "bootstrap10k": RiskConfig(eigen_sims=10_000, eigen_shard="sims"),
 }
 
 

@@ -93,3 +93,24 @@ def test_hip_eigen_adjust_matches_reference_path(cuda):
     Fc, vc = eigen.eigen_risk_adjust(F, Cz=Cz.cpu(), return_bias=True)
     torch.testing.assert_close(vg.cpu(), vc, rtol=1e-8, atol=1e-10, equal_nan=True)
     torch.testing.assert_close(Fg.cpu(), Fc, rtol=1e-8, atol=1e-16, equal_nan=True)
+
+
+@pytest.mark.gpu
+def test_hip_mc_cov_range_is_a_slice(cuda):
+    full = eigen.mc_cov(12, 42, 300, seed=5, device=cuda)
+    parts = torch.cat([eigen.mc_cov(5, 42, 300, seed=5, device=cuda),
+                       eigen.mc_cov(7, 42, 300, seed=5, device=cuda, m0=5)])
+    assert torch.equal(full, parts)
+
+
+@pytest.mark.gpu
+def test_hip_sharded_eigen_matches_one_shot(cuda):
+    """Chunked sum-accumulate + finalize kernels == the one-shot per-sim kernel (same Philox sims)."""
+    D, K, M = 10, 42, 20
+    F = _spd(D, K, seed=4, spread=2.0) * 1e-4
+    F[2] = float("nan")
+    Fg = F.to(cuda)
+    F1, v1 = eigen.eigen_risk_adjust(Fg, M=M, T_sim=400, seed=6, return_bias=True)
+    F2, v2 = eigen.eigen_risk_adjust_sharded(Fg, M=M, T_sim=400, seed=6, chunk=7, return_bias=True)
+    torch.testing.assert_close(v2.cpu(), v1.cpu(), rtol=1e-12, atol=1e-14, equal_nan=True)
+    torch.testing.assert_close(F2.cpu(), F1.cpu(), rtol=1e-11, atol=1e-18, equal_nan=True)
