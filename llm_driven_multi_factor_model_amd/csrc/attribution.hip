@@ -1,0 +1,101 @@
+// Portfolio factor exposures for risk attribution, all dates per launch (gfx950).
+//
+// For a portfolio h_d (weights over the panel's stocks) the exposure to the K = 1 + P + Q factors
+// of CrossSection.reg's design matrix (Barra-master/mfm/CrossSection.py:48,74: country column,
+// one-hot industries, cap-weighted z-scored styles, :12-20) is
+//   x_country = sum_i h_i,   x_ind[j] = sum_{i in j} h_i,   x_style[q] = sum_i h_i z_iq,
+//   z_iq = (X_iq - mu_q) / sigma   =>   x_style[q] = (sum_i h_i X_iq - mu_q sum_i h_i) / sigma,
+// so the raw panel is read once and never z-scored in memory.  Stocks that are absent or have
+// non-finite inputs (the regression's validity rule) contribute nothing.
+//
+// One 256-thread workgroup per date: fp64 register accumulators for the Q + 1 dense sums, LDS
+// atomics for the (<= 128) industry sums, a fixed-order workgroup reduction.
+#include "common.h"
+
+namespace {
+
+using namespace mfa;
+
+template <int Q>
+__global__ __launch_bounds__(256) void portfolio_exposure_kernel(
+    const float* __restrict__ X, const float* __restrict__ cap, const float* __restrict__ ret,
+    const int16_t* __restrict__ ind, const double* __restrict__ h, const double* __restrict__ stats,
+    int N, int P, int K, double* __restrict__ out) {
+  __shared__ double segs[128];
+  __shared__ double red[4][Q + 1];
+  const int d = blockIdx.x, tid = threadIdx.x;
+  const int Pseg = P > 0 ? P : 1;
+  for (int j = tid; j < 128; j += blockDim.x) segs[j] = 0.0;
+  __syncthreads();
+  const float* Xd = X + (size_t)d * Q * N;
+  const float* cd = cap + (size_t)d * N;
+  const float* rd = ret + (size_t)d * N;
+  const int16_t* id = ind ? ind + (size_t)d * N : nullptr;
+  const double* hd = h + (size_t)d * N;
+  double acc[Q + 1];
+#pragma unroll
+  for (int q = 0; q <= Q; ++q) acc[q] = 0.0;
+  for (int n = tid; n < N; n += blockDim.x) {
+    const float c = cd[n], r = rd[n];
+    const int j = id ? (int)id[n] : 0;
+    const double w = hd[n];
+    bool ok = (j >= 0) && (j < Pseg) && __builtin_isfinite(c) && (c >= 0.f) &&
+              __builtin_isfinite(r) && __builtin_isfinite(w);
+    float xf[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      xf[q] = Xd[(size_t)q * N + n];
+      ok = ok && __builtin_isfinite(xf[q]);
+    }
+    if (!ok || w == 0.0) continue;
+    acc[Q] += w;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) acc[q] = fma(w, (double)xf[q], acc[q]);
+    if (P > 0) atomicAdd(&segs[j], w);
+  }
+  const int lane = tid & 63, wid = tid >> 6;
+#pragma unroll
+  for (int q = 0; q <= Q; ++q) {
+    const double v = wave_sum(acc[q]);
+    if (lane == 0) red[wid][q] = v;
+  }
+  __syncthreads();
+  double* o = out + (size_t)d * K;
+  const double* st = stats + (size_t)d * (Q + 2);
+  if (tid <= Q) {
+    double s = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w][tid];
+    red[0][tid] = s;  // each entry is read back only by its own thread below
+  }
+  __syncthreads();
+  const double hs = red[0][Q];
+  const double isig = 1.0 / st[Q];
+  if (tid == 0) o[0] = hs;
+  for (int j = tid; j < P; j += blockDim.x) o[1 + j] = segs[j];
+  if (tid < Q) o[1 + P + tid] = (red[0][tid] - st[tid] * hs) * isig;
+}
+
+}  // namespace
+
+// X [D][Q][N] f32, cap/ret [D][N] f32 (validity only), ind [D][N] int16 (nullable when P == 0),
+// h [D][N] f64 portfolio weights, stats [D][Q+2] f64 = (mu_q, sigma, n) from mfa_xs_wls.
+// out [D][1+P+Q] f64.
+MFA_API int mfa_portfolio_exposure(const float* X, const float* cap, const float* ret,
+                                   const int16_t* ind, const double* h, const double* stats, int D,
+                                   int N, int P, int Q, double* out, void* stream) {
+  if (D <= 0) return 0;
+  if (Q < 1 || Q > 16 || P < 0 || P > 128 || N <= 0) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  const int K = 1 + P + Q;
+  switch (Q) {
+#define MFA_Q(qq)                                                                              \
+  case qq:                                                                                     \
+    hipLaunchKernelGGL(portfolio_exposure_kernel<qq>, dim3(D), dim3(256), 0, s, X, cap, ret,   \
+                       P > 0 ? ind : nullptr, h, stats, N, P, K, out);                         \
+    break;
+    MFA_Q(1) MFA_Q(2) MFA_Q(3) MFA_Q(4) MFA_Q(5) MFA_Q(6) MFA_Q(7) MFA_Q(8)
+    MFA_Q(9) MFA_Q(10) MFA_Q(11) MFA_Q(12) MFA_Q(13) MFA_Q(14) MFA_Q(15) MFA_Q(16)
+#undef MFA_Q
+  }
+  return (int)hipGetLastError();
+}

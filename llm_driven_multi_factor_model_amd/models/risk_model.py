@@ -256,6 +256,31 @@ class RiskModel:
         cap = self.panel.cap[-1].double()
         return bayes_shrink(vol, cap, ngroup, q)
 
+    def risk_attribution(self, h: torch.Tensor, which: str = "vra",
+                         specific_vol: torch.Tensor | str | None = "shrunk"):
+        """Risk decomposition of holdings ``h`` ([N] held every date, or [D_loc, N]) on this
+        rank's dates against the chosen covariance series (``nw`` / ``eigen`` / ``vra``).
+
+        ``specific_vol``: per-stock specific volatility [N] or [D_loc, N]; ``"shrunk"`` uses
+        :meth:`specific_risk_shrunk` (cap-decile Bayesian shrinkage of trailing residual vol);
+        None ignores specific risk.  Returns :class:`ops.attribution.RiskAttribution`.
+        """
+        from ..ops import attribution as attr
+        if self.stats is None:
+            raise RuntimeError("run regress() first")
+        p = self.panel
+        h = h.to(device=p.device, dtype=torch.float64)
+        if h.dim() == 1:
+            h = h[None, :].expand(p.D, -1)
+        cov = {"nw": self.nw_cov, "eigen": self.eigen_cov, "vra": self.vra_cov}[which]
+        if cov is None:
+            raise RuntimeError(f"covariance series {which!r} not computed yet")
+        x = attr.portfolio_exposure(p.styles, p.cap, p.ret, p.ind, h.contiguous(), self.stats, p.P)
+        if isinstance(specific_vol, str):
+            specific_vol = self.specific_risk_shrunk()
+        svar = None if specific_vol is None else attr.portfolio_specific_var(h, specific_vol)
+        return attr.risk_attribution(x, cov, svar)
+
     # --------------------------------------------------------------- pandas views
     def factor_returns_frame(self):
         import pandas as pd

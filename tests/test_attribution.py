@@ -1,0 +1,75 @@
+"""Portfolio risk attribution: exposure kernel vs dense oracle, decomposition identities, and
+the link to the reference's pure-factor-portfolio exposures (CrossSection.py:76,104)."""
+import pytest
+import torch
+
+from llm_driven_multi_factor_model_amd.models.panel import synthetic_panel
+from llm_driven_multi_factor_model_amd.ops import attribution as attr
+from llm_driven_multi_factor_model_amd.ops.cross_section import (pure_factor_portfolio, valid_mask,
+                                                                 xs_wls)
+
+
+def _panel(D=6, N=120, P=5, Q=4, seed=3):
+    return synthetic_panel(D, N, P, Q, seed=seed, missing_frac=0.05)
+
+
+def test_pure_factor_portfolio_has_unit_exposure():
+    """Holding row k of Omega gives exactly row k of Omega X (the reference's returned
+    pure_factor_portfolio_exposure), which the constraint makes != e_k only in the industries."""
+    p = _panel()
+    out = xs_wls(p.styles, p.cap, p.ret, p.ind, p.P)
+    d = 2
+    m = valid_mask(p.styles, p.cap, p.ret, p.ind, p.P)[d]
+    Q = p.Q
+    omega, omx = pure_factor_portfolio(p.styles[d][:, m], p.cap[d][m], p.ind[d][m], p.P,
+                                       out.stats[d, :Q], float(out.stats[d, Q]))
+    K = 1 + p.P + Q
+    h = torch.zeros(K, p.D, p.N, dtype=torch.float64)
+    h[:, d, m] = omega
+    for k in (0, 2, 1 + p.P, K - 1):
+        x = attr.portfolio_exposure(p.styles, p.cap, p.ret, p.ind, h[k], out.stats, p.P)
+        torch.testing.assert_close(x[d], omx[k], rtol=1e-9, atol=1e-10)
+    # styles of a style pure-factor portfolio: unit exposure, zero on the other styles
+    x = attr.portfolio_exposure(p.styles, p.cap, p.ret, p.ind, h[1 + p.P], out.stats, p.P)[d]
+    torch.testing.assert_close(x[1 + p.P:], torch.eye(Q, dtype=torch.float64)[0], rtol=0, atol=1e-9)
+
+
+def test_decomposition_identities():
+    g = torch.Generator().manual_seed(1)
+    D, K = 5, 7
+    A = torch.randn(D, 40, K, generator=g, dtype=torch.float64)
+    F = A.transpose(1, 2) @ A / 40
+    x = torch.randn(D, K, generator=g, dtype=torch.float64)
+    sv = torch.rand(D, generator=g, dtype=torch.float64) * 1e-2
+    r = attr.risk_attribution(x, F, sv)
+    torch.testing.assert_close(r.total_var, torch.einsum("dk,dkl,dl->d", x, F, x) + sv)
+    torch.testing.assert_close(r.contrib.sum(1), r.factor_var / r.total_vol)
+    torch.testing.assert_close(r.pct_var.sum(1) + sv / r.total_var, torch.ones(D, dtype=torch.float64))
+    gr = r.grouped(3)
+    torch.testing.assert_close(gr["country"] + gr["industry"] + gr["style"] + gr["specific"],
+                               torch.ones(D, dtype=torch.float64))
+
+
+def test_risk_model_attribution_cpu():
+    from llm_driven_multi_factor_model_amd.models.risk_model import RiskModel
+    from llm_driven_multi_factor_model_amd.utils.config import preset
+    p = synthetic_panel(60, 80, 4, 3, seed=5, missing_frac=0.02)
+    m = RiskModel(p, preset("reference", eigen_sims=5)).run()
+    h = torch.full((p.N,), 1.0 / p.N, dtype=torch.float64)
+    r = m.risk_attribution(h)
+    ok = torch.isfinite(r.total_var)
+    assert ok[-10:].all()
+    assert (r.specific_var[ok] > 0).all() and (r.factor_var[ok] > 0).all()
+
+
+@pytest.mark.gpu
+def test_hip_portfolio_exposure_matches_oracle(cuda):
+    p = synthetic_panel(40, 1000, 31, 10, seed=8, missing_frac=0.03)
+    out = xs_wls(p.styles, p.cap, p.ret, p.ind, p.P)
+    g = torch.Generator().manual_seed(2)
+    h = torch.rand(p.D, p.N, generator=g, dtype=torch.float64) / p.N
+    h[:, ::7] = float("nan")
+    ref = attr.portfolio_exposure(p.styles, p.cap, p.ret, p.ind, h, out.stats, p.P)
+    gp = p.to(cuda)
+    got = attr.portfolio_exposure(gp.styles, gp.cap, gp.ret, gp.ind, h.to(cuda), out.stats.to(cuda), p.P)
+    torch.testing.assert_close(got.cpu(), ref, rtol=1e-11, atol=1e-14)
