@@ -32,7 +32,10 @@ def load_collection_to_df(db, collection_name: str, query: dict, projection: dic
 
 def load_and_prepare_data(db=None, index_code: str = "000016.SH", start_date: str = "20200101",
                           start_date_financial: str = "20190101", end_date: str | None = None,
-                          fix_fill_order: bool = False):
+                          fix_fill_order: bool = False, dedupe_indicators: bool = True,
+                          fill: bool = True):
+    """``dedupe_indicators`` / ``fill`` = False reproduce the earlier script
+    ``load_data_v0.py`` (no ann_date dedupe of financial indicators, no ffill/fill step)."""
     client = None
     if db is None:
         from pymongo import MongoClient
@@ -65,7 +68,12 @@ def load_and_prepare_data(db=None, index_code: str = "000016.SH", start_date: st
                                {"ts_code": 1, "l1_code": 1, "l1_name": 1, "in_date": 1, "out_date": 1,
                                 "is_new": 1, "_id": 0})
     cf, bs = dedupe_statements(cf, "f_ann_date"), dedupe_statements(bs, "f_ann_date")
-    fi = dedupe_statements(fi, "ann_date")
+    if dedupe_indicators:
+        fi = dedupe_statements(fi, "ann_date")
+    else:
+        fi = fi.copy()
+        for c in ("ann_date", "end_date"):
+            fi[c] = pd.to_datetime(fi[c].astype(str), format="%Y%m%d")
     px = px.copy()
     px["trade_date"] = pd.to_datetime(px["trade_date"].astype(str), format="%Y%m%d")
     ix = ix.copy()
@@ -77,7 +85,7 @@ def load_and_prepare_data(db=None, index_code: str = "000016.SH", start_date: st
     m3 = robust_merge_asof(m2, cf, "trade_date", "f_ann_date", "ts_code").rename(
         columns={"f_ann_date": "cashflow_f_ann_date"})
     m3 = m3.drop(columns=[c for c in ["end_date_y", "end_date_x"] if c in m3.columns])
-    out = fill_missing(m3, fix_order=fix_fill_order)
+    out = fill_missing(m3, fix_order=fix_fill_order) if fill else m3
     for c in ["end_date", "balance_sheet_f_ann_date", "financial_indicators_ann_date", "cashflow_f_ann_date"]:
         if c in out.columns:
             out[c] = pd.to_datetime(out[c], errors="coerce")

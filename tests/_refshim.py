@@ -13,6 +13,7 @@ Nothing prebuilt from the reference is executed: only its ``.py`` sources.
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
 import sys
 import types
@@ -120,11 +121,19 @@ def load_reference():
             sys.path.remove(fc_dir)
             for k in ("factor_calculator", "post_processing"):
                 sys.modules.pop(k, None)
+        # legacy CSV-era twin at the repository root (/factor.py)
+        legacy = None
+        if os.path.isfile(os.path.join(REF, "factor.py")):
+            spec = importlib.util.spec_from_file_location("_mfa_ref_legacy_factor",
+                                                          os.path.join(REF, "factor.py"))
+            legacy = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(legacy)
     finally:
         for k in [k for k in sys.modules if k == "mfm" or k.startswith("mfm.")]:
             sys.modules.pop(k)
         sys.modules.update(saved)
         sys.dont_write_bytecode = old_dwb
-    r = SimpleNamespace(CrossSection=cs, utils=ut, MFM=mf, factor_calculator=fc, post_processing=pp)
+    r = SimpleNamespace(CrossSection=cs, utils=ut, MFM=mf, factor_calculator=fc, post_processing=pp,
+                        legacy_factor=legacy)
     _CACHE["ref"] = r
     return r

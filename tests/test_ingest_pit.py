@@ -94,6 +94,22 @@ def test_load_and_prepare_data_with_fake_mongo():
     assert str(stk["ts_code"].dtype) == "category" or stk["ts_code"].dtype == object
 
 
+def test_load_data_v0_no_fill_and_csi300():
+    from barra_factor_cal import load_data_v0
+    db = _seed_db()
+    db["index_components"].insert_many([{"index_code": "000300.SH", "trade_date": "20200301",
+                                         "con_code": c} for c in ["000001.SZ", "000002.SZ"]])
+    days = pd.bdate_range("2020-01-02", periods=40).strftime("%Y%m%d")
+    db["index_daily_prices"].insert_many([{"ts_code": "000300.SH", "trade_date": d, "close": 4000 + i}
+                                          for i, d in enumerate(days)])
+    with contextlib.redirect_stdout(io.StringIO()):
+        stk, idx, sw = load_data_v0.load_and_prepare_data_v0(db, end_date="20201231")
+    assert sorted(stk["ts_code"].astype(str).unique()) == ["000001.SZ", "000002.SZ"]
+    assert idx["close"].iloc[0] == 4000
+    early = stk[stk.trade_date < pd.Timestamp("2020-01-15")]
+    assert early["n_cashflow_act"].isna().all()      # v0 has no fill step
+
+
 class _Fetcher:
     def __init__(self):
         self.calls = 0
