@@ -66,36 +66,56 @@ def main() -> int:
     D, N, P, Q = args.dates, args.stocks, args.industries, args.styles
     K = 1 + P + Q
     panel = synthetic_panel(D, N, P, Q, seed=1234 + rank, device=dev, missing_frac=0.01)
-    gathered = torch.empty(world * D, K, dtype=torch.float64, device=dev) if world > 1 else None
-
-    out = None
+    # Two output / gather buffers: step i's RCCL all-gather of the factor-return series runs on
+    # the collective stream underneath step i+1's regression (the write of buffer i%2 at step
+    # i+2 first waits for that gather).  Every collective completes inside the timed region.
+    NB = 2 if world > 1 else 1
+    gathered = [torch.empty(world * D, K, dtype=torch.float64, device=dev) for _ in range(NB)] \
+        if world > 1 else None
+    outs = [None] * NB
+    handles = [None] * NB
     ws = xs_wls_workspace(D, P, Q, dev) if use_cuda else None
+    graphs = [None] * NB
+    it = 0
 
-    graph = None
-
-    def regress():
-        nonlocal out
-        out = xs_wls(panel.styles, panel.cap, panel.ret, panel.ind, P,
-                     want_resid=not args.no_resid, refine=False, out=out, workspace=ws)
+    def regress(b):
+        outs[b] = xs_wls(panel.styles, panel.cap, panel.ret, panel.ind, P,
+                         want_resid=not args.no_resid, refine=False, out=outs[b], workspace=ws)
 
     def step():
-        if graph is not None:
-            graph.replay()
+        nonlocal it
+        b = it % NB
+        it += 1
+        if handles[b] is not None:
+            handles[b].wait()          # buffer b's previous gather has read outs[b].f
+            handles[b] = None
+        if graphs[b] is not None:
+            graphs[b].replay()
         else:
-            regress()
+            regress(b)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, out.f)
+            handles[b] = dist.all_gather_into_tensor(gathered[b], outs[b].f, async_op=True)
 
+    def drain():
+        for b in range(NB):
+            if handles[b] is not None:
+                handles[b].wait()
+                handles[b] = None
+
+    for b in range(NB):
+        regress(b)
     if use_cuda and not args.no_graph:
-        # The three kernels of a step are captured once into a HIP graph and replayed: the same
-        # work, without per-launch host overhead.  The RCCL all-gather stays eager.
-        regress()
+        # The kernel of a step is captured once per buffer into a HIP graph and replayed: the
+        # same work, without per-launch host overhead.  The RCCL all-gather stays eager.
         torch.cuda.synchronize(dev)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            regress()
+        for b in range(NB):
+            graphs[b] = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(graphs[b]):
+                regress(b)
+    out = outs[0]
 
     def sync():
+        drain()
         if use_cuda:
             torch.cuda.synchronize(dev)
         if world > 1:

@@ -740,14 +740,22 @@ __global__ __launch_bounds__(256) void xs_resid_kernel(
 // served by the 256 MB Infinity Cache instead of HBM, and the single-wave solve of one date
 // overlaps the other workgroup's streaming.  HBM traffic drops from ~2x to ~1x the panel.
 // ------------------------------------------------------------------------------------------
-template <int Q, int R, int VAR = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void xs_fused_kernel(
+template <int Q, int NW>
+constexpr int fused_ring_bytes() {
+  constexpr int a = NW * Ring<Q>::RINGW;
+  constexpr int b = (int)(solve_lds_doubles<Q>(128) * 8);
+  return a > b ? a : b;
+}
+
+// NW = waves per workgroup: 4 (two workgroups per CU) or 2 (four per CU: more dates in flight,
+// so a date's solve / residual phase overlaps three streaming dates instead of one).
+template <int Q, int R, int VAR = 0, int NW = 4>
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void xs_fused_kernel(
     const float* __restrict__ X, const float* __restrict__ cap, const float* __restrict__ ret,
     const int16_t* __restrict__ ind, int N, int P, int Pseg, int pivot_mode, double tol,
     double* __restrict__ fout, float* __restrict__ eout, double* __restrict__ r2out,
     double* __restrict__ stats, int* __restrict__ status, long long* __restrict__ stamps) {
-  static_assert(solve_lds_doubles<Q>(128) * 8 <= (size_t)Ring<Q>::BYTES, "solve scratch");
-  __shared__ __attribute__((aligned(16))) char ring[Ring<Q>::BYTES];
+  __shared__ __attribute__((aligned(16))) char ring[fused_ring_bytes<Q, NW>()];
   __shared__ double cf_s[Q + 1 + 128];
   __shared__ double red[4][5];
   __shared__ int st_s;
@@ -808,8 +816,17 @@ hipError_t launch_q(const float* X, const float* cap, const float* ret, const in
                        2 * P4) * sizeof(double);
   if (lds1 + ring > 160 * 1024 || lds2 > 64 * 1024) return hipErrorInvalidValue;
   const int16_t* indp = P > 0 ? ind : nullptr;
-  if (g_xs_mode == 0 || g_xs_mode == 2) {
-    long long* st = g_xs_mode == 2 ? g_stamps : nullptr;
+  if (g_xs_mode == 3 || g_xs_mode == 4) {  // 2-wave workgroups, 2 segment replicas
+    long long* st = g_xs_mode == 4 ? g_stamps : nullptr;
+    const size_t lds2w = ((size_t)2 * Pseg * L::NS + L::NACC) * sizeof(double);
+    if (lds2w + fused_ring_bytes<Q, 2>() + 2048 <= 40 * 1024) {
+      hipLaunchKernelGGL((xs_fused_kernel<Q, 2, VAR, 2>), dim3(D), dim3(128), lds2w, s, X, cap, ret,
+                         indp, N, P, Pseg, pivot_mode, tol, f, e, r2, stats, status, st);
+      return hipGetLastError();
+    }
+  }
+  if (g_xs_mode == 0 || g_xs_mode == 2 || g_xs_mode == 3 || g_xs_mode == 4) {
+    long long* st = (g_xs_mode == 2 || g_xs_mode == 4) ? g_stamps : nullptr;
     if (rep8)
       hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR>), dim3(D), dim3(256), lds1, s, X, cap, ret,
                          indp, N, P, Pseg, pivot_mode, tol, f, e, r2, stats, status, st);
@@ -838,7 +855,8 @@ hipError_t launch_q(const float* X, const float* cap, const float* ret, const in
 MFA_API void mfa_xs_set_stamps(long long* buf) { g_stamps = buf; }
 
 // Ablation: 0 = fused single-kernel path (default), 1 = three separate kernels, 2 = fused with
-// per-date phase stamps into the mfa_xs_set_stamps buffer.
+// per-date phase stamps into the mfa_xs_set_stamps buffer, 3 / 4 = fused with 2-wave
+// workgroups (without / with stamps).
 MFA_API void mfa_xs_set_mode(int mode) { g_xs_mode = mode; }
 
 // Workspace bytes needed by mfa_xs_wls: D * (msize + Q + 1 + P) doubles.

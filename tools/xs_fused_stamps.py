@@ -27,7 +27,7 @@ buf = torch.zeros(2 * D, 8, dtype=torch.int64, device=dev)
 _native.register("mfa_xs_set_stamps", [C.c_void_p])
 _native.register("mfa_xs_set_mode", [C.c_int])
 _native.lib().mfa_xs_set_stamps(_native.ptr(buf))
-_native.lib().mfa_xs_set_mode(2)
+_native.lib().mfa_xs_set_mode(int(os.environ.get("MODE", "2")))
 torch.cuda.synchronize()
 for _ in range(3):
     xs_wls(p.styles, p.cap, p.ret, p.ind, P, refine=False, out=out)
