@@ -88,3 +88,48 @@ def test_hip_rolling_kernels_match_cpu(cuda):
     lr = cpu.cols["log_ret"]
     torch.testing.assert_close(RL.cmra(lr.to(cuda), cpu.seg_lo.to(cuda), partial=True).cpu(),
                                RL.cmra(lr, cpu.seg_lo, partial=True), rtol=1e-5, atol=1e-6, equal_nan=True)
+
+
+@pytest.mark.gpu
+def test_hip_sliding_window_kernels_match_direct(cuda):
+    """O(1)-per-row sliding kernels == the direct per-row kernels (suspensions, stock edges)."""
+    import ctypes as C
+    from llm_driven_multi_factor_model_amd import _native
+    _native.register("mfa_rolling_set_mode", [C.c_int])
+    g = torch.Generator().manual_seed(4)
+    N, T = 37, 700                      # T not a multiple of the 64-row chunk
+    R = N * T
+    mkt = torch.randn(T, generator=g) * 0.012
+    ret = (mkt[None, :] * 1.1 + torch.randn(N, T, generator=g) * 0.02).reshape(-1).float()
+    ret[torch.rand(R, generator=g) < 0.05] = float("nan")
+    mret = mkt[None, :].expand(N, T).reshape(-1).contiguous().float()
+    lr = torch.log1p(ret)
+    turn = torch.rand(R, generator=g) * 5
+    turn[torch.rand(R, generator=g) < 0.3] = 0.0
+    lens = torch.randint(50, T, (N,), generator=g)   # ragged stock lengths via NaN-free cut
+    stock = torch.arange(N, dtype=torch.int32).repeat_interleave(T)
+    seg = RL.seg_lo_from_codes(stock).to(cuda)
+    args = [t.to(cuda) for t in (ret, mret, lr, turn)]
+    r_, m_, l_, t_ = args
+    fns = {
+        "beta": lambda: RL.beta_hsigma(r_, m_, seg, 252, 63.0, 42),
+        "rstr": lambda: RL.rstr(l_, seg, 504, 21, 126.0, 42),
+        "dastd": lambda: RL.dastd(r_, m_, seg, 252, 42.0, 42),
+        "stom": lambda: RL.rolling_sum(t_, seg, 21, 15, 0.01, log=True),
+        "stoa": lambda: RL.rolling_sum(t_, seg, 252, 126, 0.01, log=True),
+        "cmra": lambda: RL.cmra(l_, seg, 252),
+        "cmra_partial": lambda: RL.cmra(l_, seg, 252, partial=True),
+    }
+    try:
+        _native.lib().mfa_rolling_set_mode(1)
+        direct = {k: f() for k, f in fns.items()}
+        _native.lib().mfa_rolling_set_mode(0)
+        scan = {k: f() for k, f in fns.items()}
+    finally:
+        _native.lib().mfa_rolling_set_mode(0)
+    del lens
+    for k in fns:
+        a = direct[k] if isinstance(direct[k], tuple) else (direct[k],)
+        b = scan[k] if isinstance(scan[k], tuple) else (scan[k],)
+        for x, y in zip(a, b):
+            torch.testing.assert_close(y.cpu(), x.cpu(), rtol=2e-5, atol=2e-7, equal_nan=True, msg=k)

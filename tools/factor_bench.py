@@ -3,6 +3,7 @@
 BASELINE.md: the reference's rolling BETA/HSIGMA runs at ~1.2k stock-days/s (a lower bound),
 RSTR / DASTD / CMRA at 8.6 / 9.1 / 2.7 s per 30k stock-days.
 """
+import ctypes as C
 import json
 import os
 import sys
@@ -11,7 +12,10 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from llm_driven_multi_factor_model_amd import _native  # noqa: E402
 from llm_driven_multi_factor_model_amd.ops import rolling as RL  # noqa: E402
+
+_native.register("mfa_rolling_set_mode", [C.c_int])
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 5000
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 3780
@@ -32,16 +36,41 @@ cases = {
     "rstr": lambda: RL.rstr(lr, seg_lo, 504, 21, 126.0, 42),
     "dastd": lambda: RL.dastd(ret, mret, seg_lo, 252, 42.0, 42),
     "cmra": lambda: RL.cmra(lr, seg_lo, 252),
+    "cmra_partial": lambda: RL.cmra(lr, seg_lo, 252, partial=True),
     "stom": lambda: RL.rolling_sum(turn, seg_lo, 21, 15, 0.01, log=True),
+    "stoa": lambda: RL.rolling_sum(turn, seg_lo, 252, 126, 0.01, log=True),
 }
-res = {}
-for name, fn in cases.items():
-    fn()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(3):
-        fn()
-    torch.cuda.synchronize()
-    el = (time.perf_counter() - t0) / 3
-    res[name] = {"ms": round(el * 1e3, 3), "Mstock_days_per_s": round(R / el / 1e6, 1)}
-print(json.dumps({"N": N, "T": T, "stock_days": R, "kernels": res}))
+
+
+def run(mode):
+    _native.lib().mfa_rolling_set_mode(mode)
+    res, outs = {}, {}
+    for name, fn in cases.items():
+        outs[name] = fn()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) / 3
+        res[name] = {"ms": round(el * 1e3, 3), "Mstock_days_per_s": round(R / el / 1e6, 1)}
+    return res, outs
+
+
+direct, od = run(1)
+scan, os_ = run(0)
+_native.lib().mfa_rolling_set_mode(0)
+agree = {}
+for name in cases:
+    a, b = od[name], os_[name]
+    a = a if isinstance(a, tuple) else (a,)
+    b = b if isinstance(b, tuple) else (b,)
+    worst = 0.0
+    for x, y in zip(a, b):
+        same_nan = bool((torch.isnan(x) == torch.isnan(y)).all())
+        m = torch.isfinite(x) & torch.isfinite(y)
+        rel = ((x[m].double() - y[m].double()).abs() / y[m].double().abs().clamp_min(1e-6)).max().item()
+        worst = max(worst, rel if same_nan else float("inf"))
+    agree[name] = worst
+print(json.dumps({"N": N, "T": T, "stock_days": R, "kernels": scan, "direct_kernels": direct,
+                  "scan_vs_direct_max_rel": agree}))
