@@ -447,6 +447,188 @@ __global__ __launch_bounds__(64) void mc_bias_kernel(const double* __restrict__ 
   }
 }
 
+// ---------------- pair-block Jacobi WITH eigenvectors (batched eigh of F0) ----------------
+// Same tournament-position scheme as jacobi_pairs, carrying packed A and the full eigenvector
+// matrix V [K][Ke] whose COLUMNS are positions: a round's column rotation of V uses the same
+// (c, s) as A's and writes every rotated column pair straight to its next-round positions, so
+// V[:, x] is always the eigenvector belonging to A's diagonal position x.
+template <int NB, int NBV>
+__device__ int jacobi_pairs_vec(double* A, double* V, double2* rcs, int K, int Ke,
+                                int max_sweeps, double tol) {
+  const int lane = threadIdx.x & 63;
+  const int npair = Ke >> 1;
+  const int nb = npair * (npair + 1) / 2;
+  auto nxt = [&](int x) { return x == 0 ? 0 : (x == Ke - 1 ? 1 : x + 1); };
+  int rd[NB][4], wr[NB][4];
+  bool has[NB], diag[NB];
+  int bT[NB], bU[NB];
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    const int b = lane + 64 * k;
+    int t = 0, rem = b;
+    while (t < npair && rem >= npair - t) { rem -= npair - t; ++t; }
+    has[k] = b < nb;
+    const int T = has[k] ? t : 0, U = has[k] ? t + rem : 0;
+    bT[k] = T; bU[k] = U; diag[k] = T == U;
+    const int x0 = T, x1 = Ke - 1 - T, y0 = U, y1 = Ke - 1 - U;
+    rd[k][0] = pk(x0, y0, Ke); rd[k][1] = pk(x0, y1, Ke);
+    rd[k][2] = pk(x1, y0, Ke); rd[k][3] = pk(x1, y1, Ke);
+    wr[k][0] = pk(nxt(x0), nxt(y0), Ke); wr[k][1] = pk(nxt(x0), nxt(y1), Ke);
+    wr[k][2] = pk(nxt(x1), nxt(y0), Ke); wr[k][3] = pk(nxt(x1), nxt(y1), Ke);
+  }
+  // V items: every lane serves ONE pair t (columns t and Ke-1-t) for rows sub, sub + lpp, ...
+  // (lpp = lanes per pair), so one (c, s) per lane covers all of its items.
+  const int lpp = 64 / npair;
+  const int vt = lane % npair, vsub = lane / npair;
+  const bool vlane = vsub < lpp;
+  const int nvrow = vlane ? (K - vsub + lpp - 1) / lpp : 0;  // rows of this lane (<= NBV)
+  const int ipp = pk(lane, lane, Ke), iqq = pk(Ke - 1 - lane, Ke - 1 - lane, Ke);
+  const int ipq = pk(lane, Ke - 1 - lane, Ke);
+  int sweep = 0;
+  for (; sweep < max_sweeps; ++sweep) {
+    double offacc = 0.0, dgacc = 0.0;
+    for (int r = 0; r < Ke - 1; ++r) {
+      const bool last = r == Ke - 2;
+      if (lane < npair) {
+        const double apq = A[ipq], app = A[ipp], aqq = A[iqq];
+        double c = 1.0, s = 0.0;
+        if (fabs(apq) > 1e-300 && fabs(apq) > 1e-18 * sqrt(fabs(app * aqq))) {
+          const double th = (aqq - app) / (2.0 * apq);
+          const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(fma(th, th, 1.0)));
+          c = 1.0 / sqrt(fma(t, t, 1.0));
+          s = t * c;
+        }
+        rcs[lane] = double2{c, s};
+      }
+      wsync();
+      double av[NB][4];
+      double2 rt[NB], ru[NB];
+      double v0[NBV], v1[NBV];
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        if (has[k]) {
+          rt[k] = rcs[bT[k]];
+          ru[k] = rcs[bU[k]];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) av[k][e] = A[rd[k][e]];
+        }
+      }
+      const double2 rv = rcs[vt];
+#pragma unroll
+      for (int k = 0; k < NBV; ++k) {
+        if (k < nvrow) {
+          const int base = (vsub + lpp * k) * Ke;
+          v0[k] = V[base + vt];
+          v1[k] = V[base + Ke - 1 - vt];
+        }
+      }
+#pragma unroll
+      for (int k = 0; k < NB; ++k) {
+        if (!has[k]) continue;
+        rot_block(av[k][0], av[k][1], av[k][2], av[k][3], rt[k].x, rt[k].y, ru[k].x, ru[k].y);
+        if (diag[k]) {
+          const double apq_new = (rt[k].y != 0.0) ? 0.0 : av[k][1];
+          A[wr[k][0]] = av[k][0];
+          A[wr[k][1]] = apq_new;
+          A[wr[k][3]] = av[k][3];
+          if (last) {
+            dgacc = fma(av[k][0], av[k][0], fma(av[k][3], av[k][3], dgacc));
+            offacc = fma(2.0 * apq_new, apq_new, offacc);
+          }
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            A[wr[k][e]] = av[k][e];
+            if (last) offacc = fma(2.0 * av[k][e], av[k][e], offacc);
+          }
+        }
+      }
+      // columns: V <- V J, written to next-round positions:
+      // nxt(t) = t == 0 ? 0 : t + 1 ;  nxt(Ke-1-t) = t == 0 ? 1 : Ke - t
+      const int c0 = vt == 0 ? 0 : vt + 1, c1 = vt == 0 ? 1 : Ke - vt;
+#pragma unroll
+      for (int k = 0; k < NBV; ++k) {
+        if (k < nvrow) {
+          const int base = (vsub + lpp * k) * Ke;
+          V[base + c0] = rv.x * v0[k] - rv.y * v1[k];
+          V[base + c1] = rv.y * v0[k] + rv.x * v1[k];
+        }
+      }
+      wsync();
+    }
+    const double off = wave_total(offacc), dgt = wave_total(dgacc);
+    if (off <= tol * tol * dgt || off == 0.0) { ++sweep; break; }
+  }
+  return sweep;
+}
+
+size_t eigh_pairs_lds(int K) {
+  const int Ke = K + (K & 1);
+  return ((size_t)Ke * (Ke + 1) / 2 + (size_t)K * Ke + 64) * sizeof(double) +
+         32 * sizeof(double2) + 64 * sizeof(int);
+}
+
+template <int NB, int NBV>
+__global__ __launch_bounds__(64) void eigh_pairs_kernel(const double* __restrict__ Ain, int K,
+                                                        int max_sweeps, double tol,
+                                                        double* __restrict__ w,
+                                                        double* __restrict__ U,
+                                                        int* __restrict__ sweeps) {
+  extern __shared__ double sm[];
+  const int b = blockIdx.x, lane = threadIdx.x;
+  const int Ke = K + (K & 1);
+  const int np = Ke * (Ke + 1) / 2;
+  double* A = sm;
+  double* V = A + np;
+  double2* rcs = (double2*)(V + (size_t)K * Ke + ((np + K * Ke) & 1));
+  int* perm = (int*)(rcs + 32);
+  const double* a = Ain + (size_t)b * K * K;
+  bool finite = true;
+  for (int e = lane; e < K * K; e += 64) finite = finite && __builtin_isfinite(a[e]);
+  if (!__all(finite)) {  // propagate NaN (reference: eig raises -> empty frame)
+    for (int k = lane; k < K; k += 64) w[(size_t)b * K + k] = qnan();
+    for (int e = lane; e < K * K; e += 64) U[(size_t)b * K * K + e] = qnan();
+    if (lane == 0 && sweeps) sweeps[b] = -1;
+    return;
+  }
+  // packed upper triangle of the symmetrised input (padding row / column zero), V = I
+  for (int i = 0; i < Ke; ++i)
+    for (int j = i + lane; j < Ke; j += 64)
+      A[pk(i, j, Ke)] = (i < K && j < K) ? 0.5 * (a[i * K + j] + a[j * K + i]) : 0.0;
+  for (int e = lane; e < K * Ke; e += 64) V[e] = (e / Ke == e % Ke) ? 1.0 : 0.0;
+  wsync();
+  const int ns = jacobi_pairs_vec<NB, NBV>(A, V, rcs, K, Ke, max_sweeps, tol);
+  // descending rank of each real position's eigenvalue (ties by position); padding excluded:
+  // the padded position holds an exact-zero row/column that no rotation ever mixes in
+  int pad = -1;
+  if (Ke != K) {  // find the padded coordinate's position: the column of V with V[:, x] == 0
+    for (int x = lane; x < Ke; x += 64) {
+      double nrm = 0.0;
+      for (int i = 0; i < K; ++i) nrm = fma(V[i * Ke + x], V[i * Ke + x], nrm);
+      if (nrm == 0.0) pad = x;
+    }
+    for (int off = 32; off > 0; off >>= 1) pad = max(pad, __shfl_xor(pad, off, 64));
+  }
+  for (int x = lane; x < Ke; x += 64) {
+    if (x == pad) continue;
+    const double lx = A[pk(x, x, Ke)];
+    int rank = 0;
+    for (int y = 0; y < Ke; ++y) {
+      if (y == pad) continue;
+      const double ly = A[pk(y, y, Ke)];
+      rank += (ly > lx) || (ly == lx && y < x);
+    }
+    perm[rank] = x;
+  }
+  wsync();
+  for (int k = lane; k < K; k += 64) w[(size_t)b * K + k] = A[pk(perm[k], perm[k], Ke)];
+  for (int e = lane; e < K * K; e += 64) {
+    const int i = e / K, k = e % K;
+    U[(size_t)b * K * K + e] = V[i * Ke + perm[k]];
+  }
+  if (lane == 0 && sweeps) sweeps[b] = ns;
+}
+
 size_t bias_lds(int K) {
   const int Ke = K + (K & 1);
   return ((size_t)Ke * (Ke + 1) + 64) * sizeof(double) + 32 * sizeof(double2) + 64 * sizeof(int);
@@ -498,16 +680,31 @@ __global__ __launch_bounds__(256) void eigen_finalize_kernel(const double* __res
   }
 }
 
+int g_eigh_mode = 0;  // 0 = pair-block tournament Jacobi, 1 = row/column cyclic Jacobi (A/B)
+
 size_t eigh_lds(int K) { return ((size_t)2 * K * (K + 1) + 4 * 64 + 64) * sizeof(double) + 64 * sizeof(int); }
 
 }  // namespace
+
+MFA_API void mfa_eigh_set_mode(int mode) { g_eigh_mode = mode; }
 
 MFA_API int mfa_eigh_batched(const double* A, int B, int K, int max_sweeps, double tol, double* w,
                              double* U, int* sweeps, void* stream) {
   if (B <= 0) return 0;
   if (K < 1 || K > 64) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(eigh_kernel, dim3(B), dim3(64), eigh_lds(K), (hipStream_t)stream, A, K,
-                     max_sweeps, tol, w, U, sweeps);
+  const int Ke = K + (K & 1), npair = Ke / 2, nb = npair * (npair + 1) / 2, nv = K * npair;
+  hipStream_t s = (hipStream_t)stream;
+  const int lpp = 64 / npair, rows_per_lane = (K + lpp - 1) / lpp;
+  (void)nv;
+  if (g_eigh_mode == 0 && nb <= 4 * 64 && rows_per_lane <= 14)
+    hipLaunchKernelGGL((eigh_pairs_kernel<4, 14>), dim3(B), dim3(64), eigh_pairs_lds(K), s, A, K,
+                       max_sweeps, tol, w, U, sweeps);
+  else if (g_eigh_mode == 0)
+    hipLaunchKernelGGL((eigh_pairs_kernel<9, 32>), dim3(B), dim3(64), eigh_pairs_lds(K), s, A, K,
+                       max_sweeps, tol, w, U, sweeps);
+  else
+    hipLaunchKernelGGL(eigh_kernel, dim3(B), dim3(64), eigh_lds(K), s, A, K, max_sweeps, tol, w, U,
+                       sweeps);
   return (int)hipGetLastError();
 }
 

@@ -39,8 +39,11 @@ def seg_lo_from_codes(codes: torch.Tensor) -> torch.Tensor:
     start = torch.ones(R, dtype=torch.bool, device=codes.device)
     if R > 1:
         start[1:] = codes[1:] != codes[:-1]
-    idx = torch.where(start, torch.arange(R, device=codes.device), torch.zeros_like(codes))
-    return torch.cummax(idx, 0).values.to(torch.int32)
+    # segment id by an int32 prefix sum (rocPRIM scan) + gather of the segment starts; the
+    # cummax-with-indices formulation took 57 ms at 18.9M rows on the MI355X
+    sid = torch.cumsum(start.to(torch.int32), 0, dtype=torch.int32) - 1
+    starts = torch.nonzero(start).flatten().to(torch.int32)
+    return starts[sid.long()].contiguous()
 
 
 # ---------------------------------------------------------------- returns
