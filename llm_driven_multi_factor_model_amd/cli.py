@@ -80,8 +80,13 @@ def cmd_risk(a):
     panel = full.slice_dates(lo, hi).to(ctx.device)
     log.info("panel %d dates x %d stocks x K=%d (shard [%d,%d)) loaded in %.2fs", full.D, full.N,
              full.K, lo, hi, time.perf_counter() - t0)
-    cfg = preset(a.preset, eigen_sims=a.sims, vra_half_life=a.vra_tau, nw_lags=a.nw_q,
-                 nw_half_life=a.nw_tau, eigen_scale=a.scale)
+    # only flags the user actually set override the preset (e.g. bootstrap10k keeps M = 10000)
+    over = {k: v for k, v in dict(eigen_sims=a.sims, vra_half_life=a.vra_tau, nw_lags=a.nw_q,
+                                  nw_half_life=a.nw_tau, eigen_scale=a.scale,
+                                  eigen_shard=a.eigen_shard, eigen_chunk=a.eigen_chunk).items()
+            if v is not None}
+    cfg = preset(a.preset, **over)
+    log.info("config %s: %s", a.preset, json.dumps(cfg.to_dict()))
     if state is not None:
         model = RiskModel.resume(state, panel, cfg, T_global=full.D, ctx=ctx)
     else:
@@ -90,11 +95,44 @@ def cmd_risk(a):
     if a.checkpoint:
         model.save(a.checkpoint)
     paths = write_risk_results(model, a.out, long_specific=a.long_specific)
+    if a.attribution:
+        paths["risk_attribution"] = _write_attribution(model, a.attribution, a.out, ctx)
     if ctx.rank == 0:
         log.info("stage ms: %s", json.dumps({k: round(v, 3) for k, v in model.times.ms.items()}))
         for k, v in paths.items():
             log.info("wrote %s -> %s", k, v)
     pdist.barrier(ctx)
+
+
+def _write_attribution(model, spec: str, out_dir: str, ctx):
+    """Per-date risk decomposition of a portfolio: ``spec`` = "equal" (equal weight over the
+    panel's stocks) or a CSV with columns ``stocknames, weight`` (held on every date).
+    Writes ``risk_attribution.csv`` (rank 0): total / factor / specific volatility and the
+    country / industry / style / specific shares of variance."""
+    from .parallel import dist as pdist
+    N = model.panel.N
+    if spec == "equal":
+        h = torch.full((N,), 1.0 / N, dtype=torch.float64)
+    else:
+        w = pd.read_csv(spec)
+        pos = {str(s): i for i, s in enumerate(model.panel.stocks)}
+        h = torch.zeros(N, dtype=torch.float64)
+        for s, v in zip(w["stocknames"].astype(str), w["weight"].astype(float)):
+            if s in pos:
+                h[pos[s]] = v
+    r = model.risk_attribution(h.to(model.device))
+    g = r.grouped(model.panel.P)
+    cols = {"total_vol": torch.sqrt(r.total_var), "factor_vol": torch.sqrt(r.factor_var),
+            "specific_vol": torch.sqrt(r.specific_var), **{f"{k}_share": v for k, v in g.items()}}
+    got = {k: pdist.gather_to_root(v.contiguous(), ctx) for k, v in cols.items()}
+    dates = model._global_dates()
+    path = os.path.join(out_dir, "risk_attribution.csv")
+    if ctx.rank == 0:
+        df = pd.DataFrame({k: v.cpu().numpy() for k, v in got.items()},
+                          index=pd.DatetimeIndex(dates, name="date"))
+        os.makedirs(out_dir, exist_ok=True)
+        df.to_csv(path)
+    return path
 
 
 def cmd_factors(a):
@@ -120,12 +158,18 @@ def main(argv=None):
     r.add_argument("--data", required=True)
     r.add_argument("--industry", required=True)
     r.add_argument("--out", default="results")
-    r.add_argument("--preset", default="reference")
-    r.add_argument("--sims", type=int, default=100)
-    r.add_argument("--scale", type=float, default=1.4)
-    r.add_argument("--nw-q", type=int, default=2)
-    r.add_argument("--nw-tau", type=float, default=252.0)
-    r.add_argument("--vra-tau", type=float, default=42.0)
+    r.add_argument("--preset", default="reference",
+                   help="reference | use4s | use4l | bootstrap10k (flags below override it)")
+    r.add_argument("--sims", type=int, default=None, help="eigen-adjustment sims (preset: 100)")
+    r.add_argument("--scale", type=float, default=None, help="eigen scale_coef (preset: 1.4)")
+    r.add_argument("--nw-q", type=int, default=None, help="Newey-West lags (preset: 2)")
+    r.add_argument("--nw-tau", type=float, default=None, help="Newey-West half-life (preset: 252)")
+    r.add_argument("--vra-tau", type=float, default=None, help="VRA half-life (preset: 42)")
+    r.add_argument("--eigen-shard", choices=["dates", "sims"], default=None,
+                   help="shard the eigen adjustment over dates or Monte-Carlo sims across ranks")
+    r.add_argument("--eigen-chunk", type=int, default=None, help="sims per launch in sims mode")
+    r.add_argument("--attribution", default=None,
+                   help="'equal' or a CSV (stocknames, weight): write risk_attribution.csv")
     r.add_argument("--device", default=None, help="cpu to force the CPU path")
     r.add_argument("--long-specific", action="store_true")
     r.add_argument("--checkpoint", default=None, help="write a resumable checkpoint here")

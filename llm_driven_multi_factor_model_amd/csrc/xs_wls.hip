@@ -622,11 +622,46 @@ __global__ __launch_bounds__(64) void xs_solve_kernel(const double* __restrict__
 // ------------------------------------------------------------------------------------------
 // Specific returns + R^2 of date d from the coefficients `cf_s` [Q+1+P] (LDS) by the whole
 // workgroup (<= 16 waves); `red` = 16 x 5 doubles of LDS.
+// Residual-pass data of 4 consecutive stocks x UP iterations, loaded by waves 1..3 while wave 0
+// solves (fused kernel, `kPre`): the pass then starts with 1536 stocks already in registers.
+constexpr int kPreU = 2;
+constexpr int kPreStocks = 3 * 64 * 4 * kPreU;
 template <int Q>
+struct ResidPre {
+  float4 c4[kPreU], r4[kPreU], x4[kPreU][Q];
+  uint2 j4[kPreU];
+};
+
+template <int Q>
+__device__ __forceinline__ void resid_prefetch(const float* __restrict__ X,
+                                               const float* __restrict__ cap,
+                                               const float* __restrict__ ret,
+                                               const int16_t* __restrict__ ind, int d, int N,
+                                               ResidPre<Q>& pr) {
+  const int nlo = N > kPreStocks ? N - kPreStocks : 0;
+  const int t = threadIdx.x - 64;  // waves 1..3
+  const float* Xd = X + (size_t)d * Q * N;
+#pragma unroll
+  for (int u = 0; u < kPreU; ++u) {
+    const int n = nlo + t * 4 + u * 768;
+    if (n < N) {
+      pr.c4[u] = *(const float4*)(cap + (size_t)d * N + n);
+      pr.r4[u] = *(const float4*)(ret + (size_t)d * N + n);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) pr.x4[u][q] = *(const float4*)(Xd + (size_t)q * N + n);
+      pr.j4[u] = ind ? *(const uint2*)(ind + (size_t)d * N + n) : make_uint2(0u, 0u);
+    }
+  }
+}
+
+// pre != nullptr: waves 1..3 hold the last kPreStocks stocks in `pre` (resid_prefetch) and the
+// main loop covers [0, N - kPreStocks) only.
+template <int Q, bool PRE = false>
 __device__ __forceinline__ void resid_body(
     const float* __restrict__ X, const float* __restrict__ cap, const float* __restrict__ ret,
     const int16_t* __restrict__ ind, int d, int N, int P, const double* cf_s, bool bad,
-    float* __restrict__ eout, double* __restrict__ r2out, double (*red)[5]) {
+    float* __restrict__ eout, double* __restrict__ r2out, double (*red)[5],
+    const ResidPre<Q>& pre = ResidPre<Q>{}) {
   const int tid = threadIdx.x;
   const int Pseg = P > 0 ? P : 1;
   double beta[Q];
@@ -664,9 +699,36 @@ __device__ __forceinline__ void resid_body(
     }
     return eo;
   };
+  auto consume4 = [&](const float4& c4, const float4& r4, const float4 (&x4)[Q], uint2 j4, int n) {
+    const int js[4] = {(int)(short)(j4.x & 0xFFFF), (int)(short)(j4.x >> 16),
+                       (int)(short)(j4.y & 0xFFFF), (int)(short)(j4.y >> 16)};
+    const float cs[4] = {c4.x, c4.y, c4.z, c4.w};
+    const float rs[4] = {r4.x, r4.y, r4.z, r4.w};
+    float eo[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float xf[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) xf[q] = ((const float*)&x4[q])[k];
+      eo[k] = one(cs[k], rs[k], js[k], xf);
+    }
+    if (ed) *(float4*)(ed + n) = make_float4(eo[0], eo[1], eo[2], eo[3]);
+  };
+  int Nmain = N;
+  if constexpr (PRE) {
+    const int nlo = N > kPreStocks ? N - kPreStocks : 0;
+    Nmain = nlo;
+    if (tid >= 64) {
+#pragma unroll
+      for (int u = 0; u < kPreU; ++u) {
+        const int n = nlo + (tid - 64) * 4 + u * 768;
+        if (n < N) consume4(pre.c4[u], pre.r4[u], pre.x4[u], pre.j4[u], n);
+      }
+    }
+  }
   // Blocks of U*step stocks walked from the END of the date: the moments pass streamed the
   // tail last, so the re-read starts with the lines most likely still in the Infinity Cache.
-  const int nblk = (N + U * step - 1) / (U * step);
+  const int nblk = (Nmain + U * step - 1) / (U * step);
   for (int b = nblk - 1; b >= 0; --b) {
     const int n0 = b * U * step + tid * 4;
     float4 c4[U], r4[U], x4[U][Q];
@@ -674,7 +736,7 @@ __device__ __forceinline__ void resid_body(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int n = n0 + u * step;
-      if (n < N) {
+      if (n < Nmain) {
         c4[u] = *(const float4*)(cd + n);
         r4[u] = *(const float4*)(rd + n);
 #pragma unroll
@@ -685,21 +747,7 @@ __device__ __forceinline__ void resid_body(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int n = n0 + u * step;
-      if (n < N) {
-        const int js[4] = {(int)(short)(j4[u].x & 0xFFFF), (int)(short)(j4[u].x >> 16),
-                           (int)(short)(j4[u].y & 0xFFFF), (int)(short)(j4[u].y >> 16)};
-        const float cs[4] = {c4[u].x, c4[u].y, c4[u].z, c4[u].w};
-        const float rs[4] = {r4[u].x, r4[u].y, r4[u].z, r4[u].w};
-        float eo[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          float xf[Q];
-#pragma unroll
-          for (int q = 0; q < Q; ++q) xf[q] = ((const float*)&x4[u][q])[k];
-          eo[k] = one(cs[k], rs[k], js[k], xf);
-        }
-        if (ed) *(float4*)(ed + n) = make_float4(eo[0], eo[1], eo[2], eo[3]);
-      }
+      if (n < Nmain) consume4(c4[u], r4[u], x4[u], j4[u], n);
     }
   }
   se = wave_sum(se); see = wave_sum(see); sr = wave_sum(sr); srr = wave_sum(srr); nn = wave_sum(nn);
@@ -749,7 +797,7 @@ constexpr int fused_ring_bytes() {
 
 // NW = waves per workgroup: 4 (two workgroups per CU) or 2 (four per CU: more dates in flight,
 // so a date's solve / residual phase overlaps three streaming dates instead of one).
-template <int Q, int R, int VAR = 0, int NW = 4>
+template <int Q, int R, int VAR = 0, int NW = 4, bool PRE = false>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void xs_fused_kernel(
     const float* __restrict__ X, const float* __restrict__ cap, const float* __restrict__ ret,
     const int16_t* __restrict__ ind, int N, int P, int Pseg, int pivot_mode, double tol,
@@ -778,10 +826,16 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     if (ss && threadIdx.x == 0) ss[(size_t)d * 8] = __builtin_amdgcn_s_memtime();
     solve_body<Q>(sm, d, P, Pseg, pivot_mode, tol, fout, cf_s, stats, status, &st_s, ss);
   }
+  ResidPre<Q> pre;
+  if constexpr (PRE && NW == 4) {
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) != 0)
+      resid_prefetch<Q>(X, cap, ret, ind, d, N, pre);
+  }
   __syncthreads();
   stamp(2);
   if constexpr ((VAR & 4) == 0)
-    resid_body<Q>(X, cap, ret, ind, d, N, P, cf_s, (st_s & XS_BAD) != 0, eout, r2out, red);
+    resid_body<Q, PRE && NW == 4>(X, cap, ret, ind, d, N, P, cf_s, (st_s & XS_BAD) != 0, eout,
+                                  r2out, red, pre);
   if constexpr ((VAR & 16) != 0) {  // timing-only: a second residual pass (cache-hit cost)
     __syncthreads();
     resid_body<Q>(X, cap, ret, ind, d, N, P, cf_s, (st_s & XS_BAD) != 0, eout, r2out, red);
@@ -825,7 +879,17 @@ hipError_t launch_q(const float* X, const float* cap, const float* ret, const in
       return hipGetLastError();
     }
   }
-  if (g_xs_mode == 0 || g_xs_mode == 2 || g_xs_mode == 3 || g_xs_mode == 4) {
+  // default: residual prefetch by waves 1..3 during the wave-0 solve (mode 0 / 5; 6 = stamps)
+  if (g_xs_mode == 0 || g_xs_mode == 5 || g_xs_mode == 6) {
+    long long* st = g_xs_mode == 6 ? g_stamps : nullptr;
+    if (rep8) {
+      hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR, 4, true>), dim3(D), dim3(256), lds1, s,
+                         X, cap, ret, indp, N, P, Pseg, pivot_mode, tol, f, e, r2, stats, status, st);
+      return hipGetLastError();
+    }
+  }
+  if (g_xs_mode == 0 || g_xs_mode == 2 || g_xs_mode == 3 || g_xs_mode == 4 || g_xs_mode >= 5) {
+    // (mode 7: fused without the residual prefetch; also the fallback for large P)
     long long* st = (g_xs_mode == 2 || g_xs_mode == 4) ? g_stamps : nullptr;
     if (rep8)
       hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR>), dim3(D), dim3(256), lds1, s, X, cap, ret,
@@ -854,9 +918,10 @@ hipError_t launch_q(const float* X, const float* cap, const float* ret, const in
 // Debug: record K2 phase timestamps (s_memtime) into buf[D][8] on the next calls (null = off).
 MFA_API void mfa_xs_set_stamps(long long* buf) { g_stamps = buf; }
 
-// Ablation: 0 = fused single-kernel path (default), 1 = three separate kernels, 2 = fused with
-// per-date phase stamps into the mfa_xs_set_stamps buffer, 3 / 4 = fused with 2-wave
-// workgroups (without / with stamps).
+// Ablation: 0 = fused single-kernel path with the residual prefetch during the solve (default),
+// 1 = three separate kernels, 2 = fused (no prefetch) with per-date phase stamps into the
+// mfa_xs_set_stamps buffer, 3 / 4 = fused with 2-wave workgroups (without / with stamps),
+// 5 / 6 = default path (without / with stamps), 7 = fused without the prefetch.
 MFA_API void mfa_xs_set_mode(int mode) { g_xs_mode = mode; }
 
 // Workspace bytes needed by mfa_xs_wls: D * (msize + Q + 1 + P) doubles.

@@ -33,6 +33,28 @@ def test_synth_then_risk_writes_demo_outputs(tmp_path):
     assert np.allclose(cov.values, cov.values.T)
 
 
+def test_cli_preset_kept_and_attribution(tmp_path):
+    """Unset flags must not override the preset (use4l keeps its 168-day VRA half-life);
+    --attribution equal writes the per-date decomposition."""
+    d = str(tmp_path)
+    r = _run("synth", "--out", d, "--dates", "70", "--stocks", "80", "--industries", "5")
+    assert r.returncode == 0, r.stderr
+    r = _run("risk", "--data", f"{d}/barra_data_csi.csv", "--industry", f"{d}/industry_info.csv",
+             "--out", f"{d}/res", "--preset", "use4l", "--sims", "3", "--eigen-shard", "sims",
+             "--eigen-chunk", "2", "--attribution", "equal", "--device", "cpu")
+    assert r.returncode == 0, r.stderr
+    att = pd.read_csv(f"{d}/res/risk_attribution.csv", index_col=0)
+    assert len(att) == 70
+    ok = att.dropna()
+    assert len(ok) > 10
+    shares = ok[["country_share", "industry_share", "style_share", "specific_share"]].sum(1)
+    assert np.allclose(shares, 1.0)
+    assert (ok["total_vol"] >= ok["factor_vol"]).all()
+    # the resolved config (logged by cmd_risk): use4l's VRA half-life survives, --sims wins
+    assert '"vra_half_life": 168.0' in r.stderr and '"eigen_sims": 3' in r.stderr
+    assert '"eigen_shard": "sims"' in r.stderr
+
+
 def test_native_csv_reader_matches_pandas(tmp_path):
     from llm_driven_multi_factor_model_amd.utils import native_io
     rng = np.random.default_rng(0)
