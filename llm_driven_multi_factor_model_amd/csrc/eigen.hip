@@ -14,8 +14,8 @@
 //     C_z,m = cov(z_m) are date-independent: they are computed ONCE per call with Philox
 //     normals and fp32 MFMA (v_mfma_f32_32x32x2_f32, exact-f32 products, fp64 cross-chunk
 //     accumulation) and C_b = S C_z,m S is formed on the fly per (date, sim);
-//   * eigh (F0): one wave per matrix, parallel cyclic Jacobi (round-robin tournament ordering,
-//     K/2 disjoint rotations per round) with A and V resident in LDS, fp64 throughout;
+//   * eigh (F0): one wave per matrix, pair-block tournament Jacobi (round-robin ordering,
+//     K/2 disjoint rotations per round), packed A + position-space V in LDS, fp64 throughout;
 //   * the (date, sim) Jacobi of the bias statistic carries M = V^T D0 V instead of V, works on
 //     packed (A, M) pairs in tournament-position space and applies each round as 2x2 pair
 //     blocks written straight to their next-round slots (all LDS addresses precomputed);
@@ -298,6 +298,47 @@ __device__ __forceinline__ void rot_block(double& x00, double& x01, double& x10,
   x11 = su * y10 + cu * y11;
 }
 
+// Jacobi rotation (c, s) zeroing a_pq.  FAST = 1 replaces the IEEE-exact fp64 divisions and
+// square roots (~50 dependent instructions) by v_rcp_f64 / v_rsq_f64 seeds refined with two
+// Newton steps each (~28): the rotation only needs ~1 ulp, and this chain runs once per round
+// on the critical path of every wave.
+__device__ __forceinline__ double rcp_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(r, fma(-x, r, 1.0), r);
+  return fma(r, fma(-x, r, 1.0), r);
+}
+__device__ __forceinline__ double rsq_nr(double x) {
+  double y = __builtin_amdgcn_rsq(x);
+  y = fma(0.5 * y, fma(-x * y, y, 1.0), y);
+  return fma(0.5 * y, fma(-x * y, y, 1.0), y);
+}
+template <int FAST>
+__device__ __forceinline__ double2 jacobi_cs(double app, double aqq, double apq) {
+  double c = 1.0, s = 0.0;
+  if constexpr (FAST) {
+    if (fabs(apq) > 1e-300 && apq * apq > 1e-36 * fabs(app * aqq)) {
+      const double th = (aqq - app) * (0.5 * rcp_nr(apq));
+      double t;
+      if (fabs(th) > 1e150) {
+        t = 0.5 * rcp_nr(th);
+      } else {
+        const double u = fma(th, th, 1.0);
+        t = copysign(rcp_nr(fabs(th) + u * rsq_nr(u)), th);
+      }
+      c = rsq_nr(fma(t, t, 1.0));
+      s = t * c;
+    }
+  } else {
+    if (fabs(apq) > 1e-300 && fabs(apq) > 1e-18 * sqrt(fabs(app * aqq))) {
+      const double th = (aqq - app) / (2.0 * apq);
+      const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(fma(th, th, 1.0)));
+      c = 1.0 / sqrt(fma(t, t, 1.0));
+      s = t * c;
+    }
+  }
+  return double2{c, s};
+}
+
 // Returns sweeps used.  AM: packed Ke x Ke (A, M) pairs in TOURNAMENT-POSITION space (Ke = K
 // rounded up to even; padding zero).  Round-robin ordering with positions fixed: every round
 // pairs positions (t, Ke-1-t), and the circle shift (position 0 fixed, x -> x+1, Ke-1 -> 1)
@@ -306,7 +347,7 @@ __device__ __forceinline__ void rot_block(double& x00, double& x01, double& x10,
 // a wave's loads of a round are issued before its stores and LDS executes one wave's accesses
 // in order, so the in-place permuted write-back needs no second buffer.
 // NB = pair blocks per lane (>= nb / 64).
-template <int NB>
+template <int NB, int FAST = 0>
 __device__ int jacobi_pairs(double2* AM, double2* rcs, int Ke, int max_sweeps, double tol) {
   const int lane = threadIdx.x & 63;
   const int npair = Ke >> 1;
@@ -341,17 +382,8 @@ __device__ int jacobi_pairs(double2* AM, double2* rcs, int Ke, int max_sweeps, d
     double offacc = 0.0, dgacc = 0.0;
     for (int r = 0; r < Ke - 1; ++r) {
       const bool last = r == Ke - 2;
-      if (lane < npair) {  // rotation of pair `lane`: positions (lane, Ke-1-lane)
-        const double apq = AM[ipq].x, app = AM[ipp].x, aqq = AM[iqq].x;
-        double c = 1.0, s = 0.0;
-        if (fabs(apq) > 1e-300 && fabs(apq) > 1e-18 * sqrt(fabs(app * aqq))) {
-          const double th = (aqq - app) / (2.0 * apq);
-          const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(fma(th, th, 1.0)));
-          c = 1.0 / sqrt(fma(t, t, 1.0));
-          s = t * c;
-        }
-        rcs[lane] = double2{c, s};
-      }
+      if (lane < npair)  // rotation of pair `lane`: positions (lane, Ke-1-lane)
+        rcs[lane] = jacobi_cs<FAST>(AM[ipp].x, AM[iqq].x, AM[ipq].x);
       wsync();
       double av[NB][4], mv[NB][4];
       double2 rt[NB], ru[NB];
@@ -400,7 +432,7 @@ __device__ int jacobi_pairs(double2* AM, double2* rcs, int Ke, int max_sweeps, d
 
 // Per (date, sim): C_b = S C_z,m S (S = diag sqrt D0, eigen order of F0), Jacobi, bias vector
 // vout[d][m][k] = (V[:,k]^T D0 V[:,k]) / Lambda[k]   (both spectra sorted descending)
-template <int NB>
+template <int NB, int FAST = 0>
 __global__ __launch_bounds__(64) void mc_bias_kernel(const double* __restrict__ D0, int K, int M,
                                                      const double* __restrict__ Cz,
                                                      const int* __restrict__ dvalid,
@@ -429,7 +461,7 @@ __global__ __launch_bounds__(64) void mc_bias_kernel(const double* __restrict__ 
       AM[pk(i, j, Ke)] = double2{a, (i == j && i < K) ? dd[i] * dd[i] : 0.0};
     }
   wsync();
-  jacobi_pairs<NB>(AM, rcs, Ke, max_sweeps, tol);
+  jacobi_pairs<NB, FAST>(AM, rcs, Ke, max_sweeps, tol);
   // descending rank of eigenvalue k (ties by index)
   for (int k = lane; k < K; k += 64) {
     const double lk = AM[pk(k, k, Ke)].x;
@@ -452,7 +484,7 @@ __global__ __launch_bounds__(64) void mc_bias_kernel(const double* __restrict__ 
 // matrix V [K][Ke] whose COLUMNS are positions: a round's column rotation of V uses the same
 // (c, s) as A's and writes every rotated column pair straight to its next-round positions, so
 // V[:, x] is always the eigenvector belonging to A's diagonal position x.
-template <int NB, int NBV>
+template <int NB, int NBV, int FAST = 0>
 __device__ int jacobi_pairs_vec(double* A, double* V, double2* rcs, int K, int Ke,
                                 int max_sweeps, double tol) {
   const int lane = threadIdx.x & 63;
@@ -489,17 +521,7 @@ __device__ int jacobi_pairs_vec(double* A, double* V, double2* rcs, int K, int K
     double offacc = 0.0, dgacc = 0.0;
     for (int r = 0; r < Ke - 1; ++r) {
       const bool last = r == Ke - 2;
-      if (lane < npair) {
-        const double apq = A[ipq], app = A[ipp], aqq = A[iqq];
-        double c = 1.0, s = 0.0;
-        if (fabs(apq) > 1e-300 && fabs(apq) > 1e-18 * sqrt(fabs(app * aqq))) {
-          const double th = (aqq - app) / (2.0 * apq);
-          const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(fma(th, th, 1.0)));
-          c = 1.0 / sqrt(fma(t, t, 1.0));
-          s = t * c;
-        }
-        rcs[lane] = double2{c, s};
-      }
+      if (lane < npair) rcs[lane] = jacobi_cs<FAST>(A[ipp], A[iqq], A[ipq]);
       wsync();
       double av[NB][4];
       double2 rt[NB], ru[NB];
@@ -568,7 +590,7 @@ size_t eigh_pairs_lds(int K) {
          32 * sizeof(double2) + 64 * sizeof(int);
 }
 
-template <int NB, int NBV>
+template <int NB, int NBV, int FAST = 0>
 __global__ __launch_bounds__(64) void eigh_pairs_kernel(const double* __restrict__ Ain, int K,
                                                         int max_sweeps, double tol,
                                                         double* __restrict__ w,
@@ -597,7 +619,7 @@ __global__ __launch_bounds__(64) void eigh_pairs_kernel(const double* __restrict
       A[pk(i, j, Ke)] = (i < K && j < K) ? 0.5 * (a[i * K + j] + a[j * K + i]) : 0.0;
   for (int e = lane; e < K * Ke; e += 64) V[e] = (e / Ke == e % Ke) ? 1.0 : 0.0;
   wsync();
-  const int ns = jacobi_pairs_vec<NB, NBV>(A, V, rcs, K, Ke, max_sweeps, tol);
+  const int ns = jacobi_pairs_vec<NB, NBV, FAST>(A, V, rcs, K, Ke, max_sweeps, tol);
   // descending rank of each real position's eigenvalue (ties by position); padding excluded:
   // the padded position holds an exact-zero row/column that no rotation ever mixes in
   int pad = -1;
@@ -681,12 +703,24 @@ __global__ __launch_bounds__(256) void eigen_finalize_kernel(const double* __res
 }
 
 int g_eigh_mode = 0;  // 0 = pair-block tournament Jacobi, 1 = row/column cyclic Jacobi (A/B)
+int g_fast_rot = 1;   // 1 = rcp/rsq + Newton rotation parameters (jacobi_cs<1>); 0 = IEEE div/sqrt
 
 size_t eigh_lds(int K) { return ((size_t)2 * K * (K + 1) + 4 * 64 + 64) * sizeof(double) + 64 * sizeof(int); }
 
 }  // namespace
 
 MFA_API void mfa_eigh_set_mode(int mode) { g_eigh_mode = mode; }
+MFA_API void mfa_eigen_set_fast_rotation(int on) { g_fast_rot = on; }
+
+#define MFA_BIAS_LAUNCH(NBV_)                                                                   \
+  {                                                                                            \
+    if (g_fast_rot)                                                                            \
+      hipLaunchKernelGGL((mc_bias_kernel<NBV_, 1>), dim3(D * M), dim3(64), bias_lds(K), s, D0, \
+                         K, M, Cz, dvalid, max_sweeps, tol, ws);                               \
+    else                                                                                       \
+      hipLaunchKernelGGL((mc_bias_kernel<NBV_, 0>), dim3(D * M), dim3(64), bias_lds(K), s, D0, \
+                         K, M, Cz, dvalid, max_sweeps, tol, ws);                               \
+  }
 
 MFA_API int mfa_eigh_batched(const double* A, int B, int K, int max_sweeps, double tol, double* w,
                              double* U, int* sweeps, void* stream) {
@@ -696,7 +730,10 @@ MFA_API int mfa_eigh_batched(const double* A, int B, int K, int max_sweeps, doub
   hipStream_t s = (hipStream_t)stream;
   const int lpp = 64 / npair, rows_per_lane = (K + lpp - 1) / lpp;
   (void)nv;
-  if (g_eigh_mode == 0 && nb <= 4 * 64 && rows_per_lane <= 14)
+  if (g_eigh_mode == 0 && nb <= 4 * 64 && rows_per_lane <= 14 && g_fast_rot)
+    hipLaunchKernelGGL((eigh_pairs_kernel<4, 14, 1>), dim3(B), dim3(64), eigh_pairs_lds(K), s, A,
+                       K, max_sweeps, tol, w, U, sweeps);
+  else if (g_eigh_mode == 0 && nb <= 4 * 64 && rows_per_lane <= 14)
     hipLaunchKernelGGL((eigh_pairs_kernel<4, 14>), dim3(B), dim3(64), eigh_pairs_lds(K), s, A, K,
                        max_sweeps, tol, w, U, sweeps);
   else if (g_eigh_mode == 0)
@@ -734,11 +771,9 @@ MFA_API int mfa_eigen_adjust(const double* D0, const double* U0, const int* dval
   hipStream_t s = (hipStream_t)stream;
   const int Ke = K + (K & 1), npair = Ke / 2, nb = npair * (npair + 1) / 2;
   if (nb <= 4 * 64)
-    hipLaunchKernelGGL(mc_bias_kernel<4>, dim3(D * M), dim3(64), bias_lds(K), s, D0, K, M, Cz,
-                       dvalid, max_sweeps, tol, ws);
+    MFA_BIAS_LAUNCH(4)
   else
-    hipLaunchKernelGGL(mc_bias_kernel<9>, dim3(D * M), dim3(64), bias_lds(K), s, D0, K, M, Cz,
-                       dvalid, max_sweeps, tol, ws);
+    MFA_BIAS_LAUNCH(9)
   hipLaunchKernelGGL(eigen_finalize_kernel, dim3(D), dim3(256), 0, s, ws, D0, U0, dvalid, K, M,
                      0, scale, Fout, vbias);
   return (int)hipGetLastError();
@@ -754,11 +789,9 @@ MFA_API int mfa_eigen_bias_accumulate(const double* D0, const int* dvalid, int D
   hipStream_t s = (hipStream_t)stream;
   const int Ke = K + (K & 1), npair = Ke / 2, nb = npair * (npair + 1) / 2;
   if (nb <= 4 * 64)
-    hipLaunchKernelGGL(mc_bias_kernel<4>, dim3(D * M), dim3(64), bias_lds(K), s, D0, K, M, Cz,
-                       dvalid, max_sweeps, tol, ws);
+    MFA_BIAS_LAUNCH(4)
   else
-    hipLaunchKernelGGL(mc_bias_kernel<9>, dim3(D * M), dim3(64), bias_lds(K), s, D0, K, M, Cz,
-                       dvalid, max_sweeps, tol, ws);
+    MFA_BIAS_LAUNCH(9)
   hipLaunchKernelGGL(bias_sum_kernel, dim3(D), dim3(64), 0, s, ws, K, M, S);
   return (int)hipGetLastError();
 }
