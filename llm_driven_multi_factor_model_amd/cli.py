@@ -3,7 +3,7 @@
     python -m llm_driven_multi_factor_model_amd.cli synth  --out data/ --dates 250 --stocks 300
     python -m llm_driven_multi_factor_model_amd.cli risk   --data data/barra_data_csi.csv \
         --industry data/industry_info.csv --out results/ [--preset reference] [--sims 100] \
-        [--checkpoint risk.ckpt] [--resume risk.ckpt]
+        [--checkpoint risk.ckpt] [--resume risk.ckpt] [--attribution equal] [--mongo-uri URI]
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m llm_driven_multi_factor_model_amd.cli risk ...
     python -m llm_driven_multi_factor_model_amd.cli factors --prices prices.csv --index index.csv \
         --industry sw_industry.csv --out data/
@@ -64,7 +64,16 @@ def cmd_risk(a):
     ctx = pdist.init_distributed(device=a.device)
     _setup_logging(ctx.rank)
     t0 = time.perf_counter()
-    full = panel_from_barra_csv(a.data, a.industry, device="cpu")
+    if a.mongo_uri:  # demo.ipynb: barra_factors + sw_industry_info_for_factors from MongoDB
+        from pymongo import MongoClient
+        from .utils.io import panel_from_mongo
+        client = MongoClient(a.mongo_uri)
+        full = panel_from_mongo(client[a.mongo_db], device="cpu")
+        client.close()
+    else:
+        if not (a.data and a.industry):
+            raise SystemExit("risk: give --data and --industry (CSV) or --mongo-uri")
+        full = panel_from_barra_csv(a.data, a.industry, device="cpu")
     state = None
     if a.resume:
         from .utils.checkpoint import load_state
@@ -155,8 +164,11 @@ def main(argv=None):
     s.add_argument("--seed", type=int, default=0)
     s.set_defaults(fn=cmd_synth)
     r = sub.add_parser("risk", help="demo.py equivalent: risk model on barra_data_csi.csv")
-    r.add_argument("--data", required=True)
-    r.add_argument("--industry", required=True)
+    r.add_argument("--data", default=None, help="barra_data_csi.csv")
+    r.add_argument("--industry", default=None, help="industry_info.csv")
+    r.add_argument("--mongo-uri", default=None,
+                   help="read barra_factors / sw_industry_info_for_factors from MongoDB instead")
+    r.add_argument("--mongo-db", default=os.environ.get("MFA_MONGO_DB", "barra_financial_data"))
     r.add_argument("--out", default="results")
     r.add_argument("--preset", default="reference",
                    help="reference | use4s | use4l | bootstrap10k (flags below override it)")

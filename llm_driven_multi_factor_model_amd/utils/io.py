@@ -145,6 +145,27 @@ def panel_from_barra_csv(path: str, industry_info_path: str, device="cpu") -> Ri
         industry_names=list(info["industry_names"].astype(str).values))
 
 
+def panel_from_mongo(db, factors_collection: str = "barra_factors",
+                     industry_collection: str = "sw_industry_info_for_factors",
+                     device="cpu") -> RiskPanel:
+    """Mongo-driven risk run (``Barra-master/demo.ipynb#c1``): the ``barra_factors`` collection
+    written by ``Barra_factor_cal/main.py:150`` and its industry table
+    (``sw_industry_info_for_factors``, ``main.py:153``) -> dense panel, with demo.py's NaN-row
+    drop and one-hot semantics.  ``db`` is anything with pymongo's ``db[name].find`` surface."""
+    barra = pd.DataFrame(list(db[factors_collection].find({}, {"_id": 0})))
+    info = pd.DataFrame(list(db[industry_collection].find({}, {"_id": 0})))
+    if barra.empty or info.empty:
+        raise ValueError(f"empty collection: {factors_collection} ({len(barra)} docs), "
+                         f"{industry_collection} ({len(info)} docs)")
+    cols = [c for c in BARRA_COLUMNS if c in barra.columns]
+    missing = [c for c in BARRA_COLUMNS[:5] if c not in barra.columns]
+    if missing:
+        raise ValueError(f"{factors_collection} lacks columns {missing}")
+    barra = barra[cols]
+    frame = mfm_frame(barra, info)
+    return panel_from_frame(frame, len(info), barra.shape[1] - 5, device=device)
+
+
 def write_barra_csv(df: pd.DataFrame, path: str) -> None:
     cols = [c for c in BARRA_COLUMNS if c in df.columns]
     df[cols].to_csv(path, index=False)

@@ -27,9 +27,12 @@ class FakeCollection:
         out = []
         for d in self.docs:
             if _match(d, query or {}):
-                if projection:
+                if projection and any(v for k, v in projection.items() if k != "_id"):
                     keep = [k for k, v in projection.items() if v and k != "_id"]
                     out.append({k: d[k] for k in keep if k in d})
+                elif projection:  # exclusion-only projection, e.g. {"_id": 0}
+                    drop = {k for k, v in projection.items() if not v}
+                    out.append({k: v for k, v in d.items() if k not in drop})
                 else:
                     out.append(copy.copy(d))
         return out

@@ -148,3 +148,28 @@ def test_updaters_rate_limit_retry_and_resume():
         rl.acquire()
         rl.done()
     assert slept and slept[0] == pytest.approx(51.0)
+
+
+def test_mongo_driven_risk_run_matches_csv_path(tmp_path):
+    """demo.ipynb#c1 flow: barra_factors + sw_industry_info_for_factors from Mongo -> panel;
+    identical to the barra_data_csi.csv path on the same rows."""
+    import torch
+    from llm_driven_multi_factor_model_amd.models.factor_engine import (factor_pipeline,
+                                                                        synthetic_prices)
+    from llm_driven_multi_factor_model_amd.utils.io import panel_from_barra_csv, panel_from_mongo
+    from barra_factor_cal.main import save_df_to_mongodb
+    prices, index, sw = synthetic_prices(N=12, T=330, seed=3)
+    with contextlib.redirect_stdout(io.StringIO()):
+        final, info, _ = factor_pipeline(prices, index, sw, device="cpu")
+        db = FakeDB()
+        save_df_to_mongodb(db, final, "barra_factors")
+        save_df_to_mongodb(db, info, "sw_industry_info_for_factors")
+    pm = panel_from_mongo(db)
+    final.to_csv(tmp_path / "b.csv", index=False)
+    info.to_csv(tmp_path / "i.csv", index=False)
+    pc = panel_from_barra_csv(str(tmp_path / "b.csv"), str(tmp_path / "i.csv"))
+    assert pm.D == pc.D and pm.N == pc.N and pm.P == pc.P and pm.Q == pc.Q
+    assert list(pm.stocks) == list(pc.stocks)
+    torch.testing.assert_close(pm.styles, pc.styles, equal_nan=True)
+    torch.testing.assert_close(pm.ret, pc.ret, equal_nan=True)
+    assert torch.equal(pm.ind, pc.ind)
