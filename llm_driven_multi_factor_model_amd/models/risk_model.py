@@ -316,7 +316,8 @@ def eigenfactor_bias_stat(cov: torch.Tensor, ret: torch.Tensor, predlen: int = 1
     w, U = eigen.eigh(cov[:n])
     U = U / U.sum(-2, keepdim=True)
     sig = torch.sqrt(predlen * torch.einsum("dki,dkl,dli->di", U, cov[:n], U))
-    growth = torch.stack([(ret[i + 1:i + 1 + predlen] + 1).prod(0) - 1 for i in range(n)])
+    # realised compounded return over the next predlen dates, all n dates at once
+    growth = (ret[1:1 + n + predlen - 1] + 1.0).unfold(0, predlen, 1).prod(-1) - 1.0   # [n, K]
     r = torch.einsum("dki,dk->di", U, growth)
     z = r / sig
     ok = torch.isfinite(z).all(-1)

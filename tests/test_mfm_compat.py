@@ -135,3 +135,25 @@ def test_inv_solver_raises_on_singular(monkeypatch):
     with pytest.raises(np.linalg.LinAlgError):
         with contextlib.redirect_stdout(io.StringIO()):
             m.reg_by_time()
+
+
+@pytest.mark.gpu
+def test_mfm_gpu_matches_cpu(cuda, monkeypatch):
+    """The drop-in mfm.MFM on the MI355X (HIP kernels) == the CPU float64 path: factor returns,
+    R^2 and the Newey-West series (the eigen adjustment draws device-specific sims and is
+    covered statistically in test_eigen.py)."""
+    df = toy_frame(T=120, N=60, P=4, Q=3, seed=2)
+    out = {}
+    for dev in ("cpu", "cuda:0"):
+        monkeypatch.setenv("MFA_DEVICE", dev)
+        with contextlib.redirect_stdout(io.StringIO()):
+            m = mfm.MFM(df, 4, 3)
+            f, e, r2 = m.reg_by_time()
+            nw = m.Newey_West_by_time(q=2, tao=252)
+        out[dev] = (f, r2, nw)
+    fc, rc, nc = out["cpu"]
+    fg, rg, ng = out["cuda:0"]
+    np.testing.assert_allclose(fg.values, fc.values, rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(rg.values, rc.values, rtol=1e-9, atol=1e-12)
+    for a, b in zip(ng[-5:], nc[-5:]):
+        np.testing.assert_allclose(a.values, b.values, rtol=1e-9, atol=1e-15)
