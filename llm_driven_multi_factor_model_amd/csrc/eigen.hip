@@ -279,12 +279,30 @@ __global__ __launch_bounds__(64) void mc_cov_kernel(int K, int T, unsigned long 
 // Only v[k] = V[:,k]^T D0 V[:,k] / Lambda[k] is needed, so instead of the eigenvectors the
 // kernel carries M = V^T D0 V, transformed two-sidedly like A (M <- J^T M J, M0 = diag D0):
 // at convergence diag(A) = Lambda and diag(M)[k] = V[:,k]^T D0 V[:,k].  Both symmetric
-// matrices are stored packed (upper triangle) in LDS; one round of K/2 disjoint rotations is
-// applied as 2x2 pair blocks (t <= u), each block read and written once, with the block list
-// of every lane fixed for the whole solve (round-robin ordering moves indices, not blocks).
-__device__ __forceinline__ int pk(int i, int j, int Ke) {  // packed index of (min, max)
-  const int a = i < j ? i : j, b = i < j ? j : i;
-  return ((a * (2 * Ke - a + 1)) >> 1) + b - a;
+// matrices are stored packed in LDS; one round of K/2 disjoint rotations is applied as 2x2
+// pair blocks (t <= u), each block read and written once, with the block list of every lane
+// fixed for the whole solve (round-robin ordering moves indices, not blocks).
+//
+// Packed layout = BLOCK-INTERLEAVED: element (i, j) lives at slot e * nbp + b, where b is the
+// pair block (T, U) = (pair(i), pair(j)) sorted, and e = 2 side(i) + side(j) its entry (side =
+// first / second position of the pair).  Lane l reads entry e of blocks l, l + 64, ...: 16
+// consecutive lanes touch 16 consecutive 16-B slots (conflict-free ds_read_b128), and the
+// next-round writes land on neighbouring blocks too.  The triangular packing it replaces had
+// bank-conflict cycles at 89 % of LDS-active cycles (rocprofv3, mc_bias_kernel).
+__host__ __device__ constexpr int pk_blocks_padded(int Ke) {
+  return ((((Ke >> 1) * ((Ke >> 1) + 1)) >> 1) + 15) & ~15;
+}
+__host__ __device__ constexpr int pk_size(int Ke) { return 4 * pk_blocks_padded(Ke); }
+__device__ __forceinline__ int pk(int i, int j, int Ke) {
+  const int h = Ke >> 1;
+  int pi = i < h ? i : Ke - 1 - i, si = i < h ? 0 : 1;
+  int pj = j < h ? j : Ke - 1 - j, sj = j < h ? 0 : 1;
+  if (pi > pj || (pi == pj && si > sj)) {  // symmetric: (i, j) and (j, i) share one slot
+    const int tp = pi; pi = pj; pj = tp;
+    const int ts = si; si = sj; sj = ts;
+  }
+  const int b = pi * h - ((pi * (pi - 1)) >> 1) + (pj - pi);
+  return (2 * si + sj) * pk_blocks_padded(Ke) + b;
 }
 
 __device__ __forceinline__ void rot_block(double& x00, double& x01, double& x10, double& x11,
@@ -446,7 +464,7 @@ __global__ __launch_bounds__(64) void mc_bias_kernel(const double* __restrict__ 
     return;
   }
   const int Ke = K + (K & 1);
-  const int np = Ke * (Ke + 1) / 2;
+  const int np = pk_size(Ke);
   double2* AM = (double2*)sm;                  // [np] packed (A, M) pairs
   double* dd = (double*)(AM + np);             // [64]
   double2* rcs = (double2*)(dd + 64);          // [32]
@@ -586,7 +604,7 @@ __device__ int jacobi_pairs_vec(double* A, double* V, double2* rcs, int K, int K
 
 size_t eigh_pairs_lds(int K) {
   const int Ke = K + (K & 1);
-  return ((size_t)Ke * (Ke + 1) / 2 + (size_t)K * Ke + 64) * sizeof(double) +
+  return ((size_t)pk_size(Ke) + (size_t)K * Ke + 64) * sizeof(double) +
          32 * sizeof(double2) + 64 * sizeof(int);
 }
 
@@ -599,7 +617,7 @@ __global__ __launch_bounds__(64) void eigh_pairs_kernel(const double* __restrict
   extern __shared__ double sm[];
   const int b = blockIdx.x, lane = threadIdx.x;
   const int Ke = K + (K & 1);
-  const int np = Ke * (Ke + 1) / 2;
+  const int np = pk_size(Ke);
   double* A = sm;
   double* V = A + np;
   double2* rcs = (double2*)(V + (size_t)K * Ke + ((np + K * Ke) & 1));
@@ -653,7 +671,7 @@ __global__ __launch_bounds__(64) void eigh_pairs_kernel(const double* __restrict
 
 size_t bias_lds(int K) {
   const int Ke = K + (K & 1);
-  return ((size_t)Ke * (Ke + 1) + 64) * sizeof(double) + 32 * sizeof(double2) + 64 * sizeof(int);
+  return ((size_t)2 * pk_size(Ke) + 64) * sizeof(double) + 32 * sizeof(double2) + 64 * sizeof(int);
 }
 
 // Sum of the per-sim bias values over this chunk's sims, accumulated into S[d][k] (fixed
