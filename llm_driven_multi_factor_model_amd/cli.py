@@ -146,8 +146,12 @@ def _write_attribution(model, spec: str, out_dir: str, ctx):
 
 def cmd_factors(a):
     from .models.factor_engine import run_factor_pipeline
-    _setup_logging()
-    run_factor_pipeline(a.prices, a.index, a.industry, a.out, device=a.device)
+    from .parallel import dist as pdist
+    ctx = pdist.init_distributed(device=a.device)  # torchrun: date blocks per rank (+ halo)
+    _setup_logging(ctx.rank)
+    run_factor_pipeline(a.prices, a.index, a.industry, a.out,
+                        device=a.device if not ctx.enabled else None, ctx=ctx)
+    pdist.barrier(ctx)
 
 
 def main(argv=None):
@@ -196,7 +200,7 @@ def main(argv=None):
     f.add_argument("--device", default=None)
     f.set_defaults(fn=cmd_factors)
     a = ap.parse_args(argv)
-    if a.cmd != "risk":
+    if a.cmd not in ("risk", "factors"):
         _setup_logging()
     a.fn(a)
     return 0

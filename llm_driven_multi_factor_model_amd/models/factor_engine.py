@@ -9,6 +9,12 @@ as FLAT float32 rows plus three int32 index vectors (``seg_lo`` = first row of t
 all stocks (``ops.rolling``); cross-sectional steps (NLSIZE, winsorize, orthogonalize) scatter
 the rows into a dense [date, stock] grid in HBM, run one per-date kernel launch
 (``ops.xs_reduce``) and gather back.  No per-stock or per-date Python loop anywhere.
+
+Multi-GPU (DP with halos): every rank prepares the replicated master, keeps its
+contiguous date block plus each stock's ``halo_rows()`` preceding rows (the longest window reach,
+504 for RSTR), and runs descriptors and the per-date post-processing on that slice only
+(:meth:`FactorEngine.date_shard`); rank 0 gathers the blocks for the Barra export.  Returns are
+formed on the full history before slicing, so no halo row starts a fresh ``pct_change``.
 """
 from __future__ import annotations
 
@@ -68,6 +74,7 @@ class FactorEngine:
         t0 = time.perf_counter()
         self.master = self._prepare(prices_df, index_df)
         self.prep_s = time.perf_counter() - t0
+        self.own = None  # row mask of the owned date block (date_shard); None = every row
 
     # ---------------------------------------------------------------- _prepare_data (:34-64)
     def _prepare(self, prices_df, index_df) -> pd.DataFrame:
@@ -100,6 +107,44 @@ class FactorEngine:
         if not master["ts_code"].is_monotonic_increasing:
             raise AssertionError("master frame must be sorted by ts_code")
         return master
+
+    # ---------------------------------------------------------------- date sharding (DP + halo)
+    def halo_rows(self) -> int:
+        """Rows of history any descriptor of this config reads before an output row."""
+        c = self.cfg
+        return max(c.beta_window, c.rstr_window, c.dastd_window, c.cmra_window,
+                   c.stom[0], c.stoq[0], c.stoa[0])
+
+    def date_shard(self, lo: int, hi: int, halo: int | None = None) -> "FactorEngine":
+        """Engine over the rows of dates [lo, hi) plus each stock's ``halo`` preceding rows.
+
+        Every window of an owned row then lies inside the slice, or starts at the stock's true
+        first row, so the rolling descriptors of owned rows equal the full-panel ones (up to the
+        summation order of the sliding kernels); per-date steps only see owned dates whole.
+        Rows outside [lo, hi) are dropped again by :meth:`run`.
+        """
+        H = self.halo_rows() if halo is None else int(halo)
+        dev = self.device
+        sid = self.stock_id.long()
+        row = torch.arange(self.R, device=dev, dtype=torch.int64)
+        own = (self.date_id >= lo) & (self.date_id < hi)
+        first = torch.full((self.N,), self.R, dtype=torch.int64, device=dev)
+        first = first.scatter_reduce(0, sid[own], row[own], reduce="amin")  # first owned row
+        f = first[sid]
+        keep = own | ((f < self.R) & (row < f) & (row >= f - H))
+        idx = torch.nonzero(keep).flatten()
+        sub = object.__new__(type(self))
+        sub.cfg, sub.device, sub.prep_s = self.cfg, dev, 0.0
+        sub.stock_names, sub.date_names = self.stock_names, self.date_names
+        sub.D, sub.N, sub.R = self.D, self.N, int(idx.numel())
+        sub.master = self.master.iloc[idx.cpu().numpy()].reset_index(drop=True)
+        sub.stock_id, sub.date_id = self.stock_id[idx], self.date_id[idx]
+        sub.seg_lo = RL.seg_lo_from_codes(sub.stock_id)
+        sub.grid_idx = sub.date_id.long() * sub.N + sub.stock_id.long()
+        sub.cols = {k: v[idx] for k, v in self.cols.items()}
+        sub.own = own[idx]
+        sub.lo, sub.hi = lo, hi
+        return sub
 
     # ---------------------------------------------------------------- grid helpers
     def to_grid(self, x: torch.Tensor) -> torch.Tensor:
@@ -237,6 +282,8 @@ class FactorEngine:
         df["circ_mv"] = self.master["circ_mv"].to_numpy(np.float64, na_value=np.nan) if "circ_mv" in self.master else np.nan
         for k, v in res.items():
             df[k] = v.double().cpu().numpy()
+        if self.own is not None:  # date shard: drop the halo rows
+            df = df.loc[self.own.cpu().numpy()].reset_index(drop=True)
         return df
 
 
@@ -321,12 +368,23 @@ def barra_export(processed: pd.DataFrame, sw_industry: pd.DataFrame):
 
 
 def factor_pipeline(prices_df, index_df, sw_industry_df, factors=None, config: FactorConfig | None = None,
-                    device=None):
-    """main.py end to end: raw descriptors -> winsorize -> composite -> orthogonalize -> export."""
+                    device=None, ctx=None):
+    """main.py end to end: raw descriptors -> winsorize -> composite -> orthogonalize -> export.
+
+    With an enabled ``ctx`` (torchrun, one rank per GPU) each rank computes its date block
+    (``date_shard``: descriptors with a halo, then the per-date post-processing) and rank 0
+    gathers the blocks and writes the export; other ranks return ``(None, None, timings)``.
+    """
+    from ..parallel import dist as pdist
     cfg = config or FactorConfig()
+    dist_on = ctx is not None and ctx.enabled
+    if dist_on and device is None:
+        device = ctx.device
     t = {}
     t0 = time.perf_counter()
     eng = FactorEngine(prices_df, index_df, device=device, config=cfg)
+    if dist_on:
+        eng = eng.date_shard(*pdist.shard_range(eng.D, ctx.rank, ctx.world))
     raw = eng.run(factors or FACTORS_TO_RUN)
     t["descriptors_s"] = time.perf_counter() - t0
     t0 = time.perf_counter()
@@ -335,17 +393,25 @@ def factor_pipeline(prices_df, index_df, sw_industry_df, factors=None, config: F
     c = composite_frame(w, cfg.composite, device=eng.device)
     o = orthogonalize_frame(c, cfg.ortho, device=eng.device)
     t["postprocess_s"] = time.perf_counter() - t0
+    if dist_on:  # C7: date blocks to rank 0, back in master order (ts_code, trade_date)
+        parts = pdist.gather_objects(o, ctx)
+        if ctx.rank != 0:
+            return None, None, dict(t, kernel_ms=getattr(eng, "timings", {}))
+        o = pd.concat(parts, ignore_index=True).sort_values(["ts_code", "trade_date"], kind="stable")
+        o = o.reset_index(drop=True)
     final, info = barra_export(o, sw_industry_df)
     return final, info, dict(t, kernel_ms=getattr(eng, "timings", {}))
 
 
-def run_factor_pipeline(prices_csv, index_csv, industry_csv, out_dir, device=None):
+def run_factor_pipeline(prices_csv, index_csv, industry_csv, out_dir, device=None, ctx=None):
     prices = pd.read_csv(prices_csv)
     index = pd.read_csv(index_csv)
     sw = pd.read_csv(industry_csv)
     for df in (prices, index):
         df["trade_date"] = pd.to_datetime(df["trade_date"].astype(str), format="mixed")
-    final, info, t = factor_pipeline(prices, index, sw, device=device)
+    final, info, t = factor_pipeline(prices, index, sw, device=device, ctx=ctx)
+    if final is None:  # non-root rank of a sharded run
+        return None, None
     os.makedirs(out_dir, exist_ok=True)
     final.to_csv(os.path.join(out_dir, "barra_data_csi.csv"), index=False)
     info.to_csv(os.path.join(out_dir, "industry_info.csv"), index=False)

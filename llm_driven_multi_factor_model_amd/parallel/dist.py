@@ -9,7 +9,7 @@ Collective call sites:
   C3 factor-return series      all_gather   (D_local x K fp64)
   C5 MC bias accumulators      all_reduce   (D x K fp64, sims-sharded eigen adjustment)
   C6 VRA bias series           all_gather   (D_local fp64)
-  C7 outputs to rank 0         gather       (only when writing CSVs)
+  C7 outputs to rank 0         gather       (only when writing CSVs; factor-pipeline frames)
   C8 benchmark fences          barrier
 Backend ``nccl`` is RCCL on ROCm builds; ``gloo`` serves CPU tests.
 """
@@ -99,6 +99,17 @@ def gather_to_root(x: torch.Tensor, ctx: DistContext | None = None) -> torch.Ten
         return x
     full = all_gather_rows(x, ctx)
     return full if ctx.rank == 0 else None
+
+
+def gather_objects(obj, ctx: DistContext | None = None) -> list | None:
+    """Every rank's picklable ``obj`` in rank order on rank 0 (None elsewhere); C7 for
+    host-side frames (the sharded factor pipeline's per-rank date blocks)."""
+    ctx = ctx or context()
+    if not ctx.enabled:
+        return [obj]
+    out = [None] * ctx.world if ctx.rank == 0 else None
+    dist.gather_object(obj, out, dst=0)
+    return out
 
 
 def all_reduce_max(x: float, ctx: DistContext | None = None, device=None) -> float:
