@@ -135,7 +135,9 @@ struct Layout {
 
 // Reduce a compile-time register array across the workgroup into out[0..CNT) (LDS, zeroed by
 // the caller) through a per-wave [8][65] fp64 tile: keeps the register footprint flat.
-template <int CNT>
+// DET: `out` is this wave's own partial row (plain stores, summed in wave order by the caller)
+// instead of the shared total (LDS atomics: order-dependent rounding).
+template <int CNT, bool DET = false>
 __device__ __forceinline__ void wg_reduce(const double (&v)[CNT], double* wbuf, double* out) {
   const int lane = threadIdx.x & (kWave - 1);
   const int a = lane & 7, slice = lane >> 3;
@@ -151,7 +153,10 @@ __device__ __forceinline__ void wg_reduce(const double (&v)[CNT], double* wbuf, 
     t += __shfl_xor(t, 8, kWave);
     t += __shfl_xor(t, 16, kWave);
     t += __shfl_xor(t, 32, kWave);
-    if (slice == 0 && c0 + a < CNT) lds_add(out + c0 + a, t);
+    if (slice == 0 && c0 + a < CNT) {
+      if constexpr (DET) out[c0 + a] = t;
+      else lds_add(out + c0 + a, t);
+    }
     wave_sync_lds();
   }
 }
@@ -165,13 +170,20 @@ struct Ring {
   // wave streams its own 64-stock tiles (k = wid, wid + nw, ...) with no workgroup barrier until
   // the final reduction, so the 8 waves of a CU drift and overlap HBM, VALU and LDS phases.
   static constexpr int WSLOT = Layout<Q>::WSLOT;
-  static constexpr int RINGW = kWNB * WSLOT > 8 * 65 * 8 ? kWNB * WSLOT : 8 * 65 * 8;
+  // >= the reduction tile [8][65] fp64 + one partial row (deterministic wg_reduce)
+  static constexpr int RED = (8 * 65 + Layout<Q>::NACC) * 8;
+  static constexpr int RINGW = kWNB * WSLOT > RED ? kWNB * WSLOT : RED;
   static constexpr int BYTES = 4 * RINGW;
 };
 
 // Moments of date d.  `ring` = Ring<Q>::BYTES of LDS, `dyn` = [Pseg*NS][R] replicated segment
 // sums | [NACC] totals (LDS), `md` = msize(Pseg) doubles out (global memory or LDS that does
 // not alias `dyn`; may alias `ring`).  Ends with a workgroup barrier.
+//
+// VAR & 32 = bitwise-deterministic mode (4-wave workgroups): every segment replica is owned by
+// ONE wave (R/4 per wave), so its atomics land in that wave's program order, and the per-lane
+// totals are reduced through per-wave partial rows summed in wave order.  The default mode
+// shares replicas across waves (fewer bank conflicts) and is reproducible to rounding only.
 template <int Q, int VAR, int R>
 __device__ __forceinline__ void moments_body(
     const float* __restrict__ X, const float* __restrict__ cap, const float* __restrict__ ret,
@@ -182,7 +194,10 @@ __device__ __forceinline__ void moments_body(
   constexpr int WSLOT = Ring<Q>::WSLOT, RINGW = Ring<Q>::RINGW;
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int lane = tid & 63, wid = tid >> 6, nw = nthr >> 6;
-  const unsigned seg_a = lds_addr(dyn + (lane & (R - 1)));
+  constexpr bool DET = (VAR & 32) != 0;
+  static_assert(!DET || (R % 4 == 0 && NACC <= 256), "deterministic mode: 4 waves, R/4 replicas each");
+  const int rep = DET ? wid * (R / 4) + (lane & (R / 4 - 1)) : (lane & (R - 1));
+  const unsigned seg_a = lds_addr(dyn + rep);
   double* acc = dyn + R * Pseg * NS;
   for (int i = tid; i < R * Pseg * NS + NACC; i += nthr) dyn[i] = 0.0;
   __syncthreads();
@@ -269,9 +284,20 @@ __device__ __forceinline__ void moments_body(
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  wg_reduce<NACC>(v, (double*)wring, acc);
-  __syncthreads();
-  for (int i = tid; i < NACC; i += nthr) md[i] = acc[i];
+  if constexpr (DET) {
+    static_assert(Ring<Q>::RINGW >= 8 * 65 * 8 + NACC * 8, "partial row must fit the wave ring");
+    wg_reduce<NACC, true>(v, (double*)wring, (double*)(wring + 8 * 65 * 8));
+    __syncthreads();
+    double t = 0.0;
+    if (tid < NACC)
+      for (int w = 0; w < nw; ++w) t += ((const double*)(ring + w * RINGW + 8 * 65 * 8))[tid];
+    __syncthreads();  // md may alias the ring
+    if (tid < NACC) md[tid] = t;
+  } else {
+    wg_reduce<NACC>(v, (double*)wring, acc);
+    __syncthreads();
+    for (int i = tid; i < NACC; i += nthr) md[i] = acc[i];
+  }
   for (int i = tid; i < Pseg * NS; i += nthr) {
     double t = 0.0;
 #pragma unroll
@@ -815,7 +841,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   };
   stamp(0);
   double* sm = (double*)ring;  // moments, then the solve's scratch (ring is idle by then)
-  moments_body<Q, VAR & 3, R>(X, cap, ret, ind, N, Pseg, d, ring, dyn, sm);
+  moments_body<Q, VAR & 35, R>(X, cap, ret, ind, N, Pseg, d, ring, dyn, sm);
   stamp(1);
   if constexpr ((VAR & 8) != 0) {  // timing-only ablation: no solve
     for (int i = threadIdx.x; i < Q + 1 + P; i += blockDim.x) cf_s[i] = sm[i] * 1e-30;
@@ -847,6 +873,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   }
 }
 
+constexpr int kXsDeterministic = 0x100;  // pivot_mode flag: bitwise-deterministic kernel
 long long* g_stamps = nullptr;  // debug: per-date K2 phase stamps [D][8]
 int g_xs_mode = 0;              // 0 = fused single kernel, 1 = three kernels (ablation)
 
@@ -870,6 +897,13 @@ hipError_t launch_q(const float* X, const float* cap, const float* ret, const in
                        2 * P4) * sizeof(double);
   if (lds1 + ring > 160 * 1024 || lds2 > 64 * 1024) return hipErrorInvalidValue;
   const int16_t* indp = P > 0 ? ind : nullptr;
+  if (pivot_mode & kXsDeterministic) {  // bitwise-reproducible variant of the default path
+    if (!rep8) return hipErrorNotSupported;
+    hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR | 32, 4, true>), dim3(D), dim3(256), lds1,
+                       s, X, cap, ret, indp, N, P, Pseg, pivot_mode & 0xff, tol, f, e, r2, stats,
+                       status, nullptr);
+    return hipGetLastError();
+  }
   if (g_xs_mode == 3 || g_xs_mode == 4) {  // 2-wave workgroups, 2 segment replicas
     long long* st = g_xs_mode == 4 ? g_stamps : nullptr;
     const size_t lds2w = ((size_t)2 * Pseg * L::NS + L::NACC) * sizeof(double);
@@ -935,7 +969,8 @@ MFA_API size_t mfa_xs_wls_workspace(int D, int P, int Q) {
 // may be null when P == 0).  N must be a multiple of 8 (16-byte aligned rows; pad with absent
 // stocks).  Outputs: f [D][1+P+Q] fp64 (country, industries, styles), e [D][N] fp32 specific
 // returns (nullable), r2 [D] fp64, stats [D][Q+2] fp64 = (mu_q, sigma, n_valid) (nullable),
-// status [D] int32 XsStatus bits.  pivot_mode: 0 = last non-empty industry, 1 = reference.
+// status [D] int32 XsStatus bits.  pivot_mode: 0 = last non-empty industry, 1 = reference;
+// | 0x100 = bitwise-deterministic kernel (needs the 8-replica segment table: P <= 59 at Q = 10).
 MFA_API int mfa_xs_wls(const float* X, const float* cap, const float* ret, const int16_t* ind,
                        int D, int N, int P, int Q, int pivot_mode, double tol, double* f,
                        float* e, double* r2, double* stats, int* status, void* ws,

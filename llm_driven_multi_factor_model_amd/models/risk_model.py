@@ -79,7 +79,7 @@ class RiskModel:
         p = self.panel
         with self._stage("regress"):
             res = xs.xs_wls(p.styles, p.cap, p.ret, p.ind, p.P, pivot_mode=self.cfg.pivot_mode,
-                            want_resid=want_resid)
+                            want_resid=want_resid, deterministic=self.cfg.deterministic)
         self.factor_ret, self.specific_ret, self.r2 = res.f, res.resid, res.r2
         self.status, self.stats = res.status, res.stats
         with self._stage("allgather_f"):

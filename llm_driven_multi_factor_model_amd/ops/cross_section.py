@@ -30,6 +30,7 @@ XS_PIVOT_EMPTY = 2
 XS_NEAR_SINGULAR = 4
 XS_ZERO_PIVOT = 8
 XS_BAD_SIGMA = 16
+XS_DETERMINISTIC = 0x100  # pivot_mode flag of mfa_xs_wls: bitwise-deterministic kernel
 
 
 @dataclass
@@ -68,7 +69,7 @@ def _validate(X, cap, ret, ind, P):
 def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Tensor | None,
            P: int, *, pivot_mode: int = 0, tol: float = 1e-14, want_resid: bool = True,
            refine: bool = True, out: XsResult | None = None,
-           workspace: torch.Tensor | None = None) -> XsResult:
+           workspace: torch.Tensor | None = None, deterministic: bool = False) -> XsResult:
     """Regress every date of the panel in one batched call.
 
     X [D,Q,N] f32 styles, cap/ret [D,N] f32, ind [D,N] int16 industry ids (or None if P == 0).
@@ -79,6 +80,9 @@ def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Ten
     ``out`` / ``workspace`` let a caller (e.g. a timed loop) reuse preallocated buffers.
     The GPU kernels need N % 8 == 0 (16-byte rows for the LDS-DMA ring); other N are padded
     here with absent stocks (``ind = -1``), which costs a copy — keep panels padded.
+    ``deterministic`` selects the bitwise-reproducible kernel variant (each LDS segment replica
+    owned by one wave, wave partials summed in order); the default shares replicas across waves
+    for fewer bank conflicts and reproduces to rounding only.
     """
     D, Q, N = _validate(X, cap, ret, ind, P)
     K = 1 + P + Q
@@ -113,7 +117,8 @@ def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Ten
     if workspace is None or workspace.numel() < need:
         workspace = torch.empty(need, dtype=torch.uint8, device=dev)
     _native.call("mfa_xs_wls", _native.ptr(X), _native.ptr(cap), _native.ptr(ret),
-                 _native.ptr(ind if P > 0 else None), D, Np, P, Q, pivot_mode, tol,
+                 _native.ptr(ind if P > 0 else None), D, Np, P, Q,
+                 pivot_mode | (XS_DETERMINISTIC if deterministic else 0), tol,
                  _native.ptr(out.f), _native.ptr(resid_buf), _native.ptr(out.r2),
                  _native.ptr(out.stats), _native.ptr(out.status), _native.ptr(workspace),
                  _native.stream(dev))

@@ -125,3 +125,23 @@ def test_kernel_reference_pivot_and_determinism(cuda):
     torch.cuda.synchronize()
     # LDS fp64 atomics are order-dependent: results agree to rounding, not bitwise
     torch.testing.assert_close(b.f, c.f, rtol=1e-12, atol=1e-15)
+
+
+@pytest.mark.gpu
+def test_deterministic_kernel_is_bitwise_reproducible(cuda):
+    """run twice, compare bitwise.  The deterministic variant gives each LDS
+    segment replica to one wave and sums wave partials in order; the default path agrees with
+    it to rounding."""
+    panel = synthetic_panel(64, 3000, 31, 10, seed=9, missing_frac=0.02, empty_industries=2).to(cuda)
+    runs = [X.xs_wls(panel.styles, panel.cap, panel.ret, panel.ind, 31, deterministic=True)
+            for _ in range(3)]
+    torch.cuda.synchronize()
+    for r in runs[1:]:
+        assert torch.equal(r.f, runs[0].f)
+        assert torch.equal(r.r2, runs[0].r2)
+        assert torch.equal(r.resid.nan_to_num(7.0), runs[0].resid.nan_to_num(7.0))
+        assert torch.equal(r.stats, runs[0].stats) and torch.equal(r.status, runs[0].status)
+    fast = X.xs_wls(panel.styles, panel.cap, panel.ret, panel.ind, 31)
+    torch.testing.assert_close(runs[0].f, fast.f, rtol=1e-12, atol=1e-15)
+    ref = X.xs_wls_reference(panel.styles.cpu(), panel.cap.cpu(), panel.ret.cpu(), panel.ind.cpu(), 31)
+    torch.testing.assert_close(runs[0].f.cpu(), ref.f, rtol=1e-8, atol=1e-11)
