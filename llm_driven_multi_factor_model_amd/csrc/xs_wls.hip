@@ -687,7 +687,7 @@ __device__ __forceinline__ void resid_body(
     const float* __restrict__ X, const float* __restrict__ cap, const float* __restrict__ ret,
     const int16_t* __restrict__ ind, int d, int N, int P, const double* cf_s, bool bad,
     float* __restrict__ eout, double* __restrict__ r2out, double (*red)[5],
-    const ResidPre<Q>& pre = ResidPre<Q>{}) {
+    const ResidPre<Q>& pre = ResidPre<Q>{}, double* __restrict__ sums_out = nullptr) {
   const int tid = threadIdx.x;
   const int Pseg = P > 0 ? P : 1;
   double beta[Q];
@@ -787,9 +787,14 @@ __device__ __forceinline__ void resid_body(
     for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
       a += red[i][0]; b += red[i][1]; c += red[i][2]; e2 += red[i][3]; n += red[i][4];
     }
-    const double ve = b / n - (a / n) * (a / n);
-    const double vr = e2 / n - (c / n) * (c / n);
-    r2out[d] = bad ? qnan() : 1.0 - ve / vr;
+    if (sums_out) {  // stock-sharded regression: the caller all-reduces, then forms R^2
+      double* so = sums_out + (size_t)d * 5;
+      so[0] = a; so[1] = b; so[2] = c; so[3] = e2; so[4] = n;
+    } else {
+      const double ve = b / n - (a / n) * (a / n);
+      const double vr = e2 / n - (c / n) * (c / n);
+      r2out[d] = bad ? qnan() : 1.0 - ve / vr;
+    }
   }
 }
 
@@ -797,14 +802,16 @@ template <int Q>
 __global__ __launch_bounds__(256) void xs_resid_kernel(
     const float* __restrict__ X, const float* __restrict__ cap, const float* __restrict__ ret,
     const int16_t* __restrict__ ind, int D, int N, int P, const double* __restrict__ coef,
-    const int* __restrict__ status, float* __restrict__ eout, double* __restrict__ r2out) {
+    const int* __restrict__ status, float* __restrict__ eout, double* __restrict__ r2out,
+    double* __restrict__ sums_out = nullptr) {
   __shared__ double cf_s[Q + 1 + 128];
   __shared__ double red[16][5];
   const int d = D - 1 - blockIdx.x;
   const double* co = coef + (size_t)d * (Q + 1 + P);
   for (int i = threadIdx.x; i < Q + 1 + P; i += blockDim.x) cf_s[i] = co[i];
   __syncthreads();
-  resid_body<Q>(X, cap, ret, ind, d, N, P, cf_s, (status[d] & XS_BAD) != 0, eout, r2out, red);
+  resid_body<Q>(X, cap, ret, ind, d, N, P, cf_s, (status[d] & XS_BAD) != 0, eout, r2out, red,
+                ResidPre<Q>{}, sums_out);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1010,4 +1017,94 @@ MFA_API int mfa_xs_wls_variant(const float* X, const float* cap, const float* re
 #undef MFA_V
   }
   return (int)hipErrorInvalidValue;
+}
+
+// ------------------------------------------------------------------------------------------
+// Stock-sharded (TP) regression pieces, SURVEY.md §2.5: every rank streams ITS stocks of every
+// date into raw moments (additive: the caller all-reduces them), solves redundantly from the
+// summed moments, and forms its stocks' specific returns plus the five R^2 sums
+// [sum e, sum e^2, sum r, sum r^2, n] per date (all-reduced again by the caller).
+// ------------------------------------------------------------------------------------------
+namespace {
+template <int Q>
+hipError_t split_q(int what, const float* X, const float* cap, const float* ret,
+                   const int16_t* ind, int D, int N, int P, int pivot_mode, double tol,
+                   double* mom, double* f, double* coef, double* stats, int* status, float* e,
+                   double* sums, hipStream_t s) {
+  using L = Layout<Q>;
+  const int Pseg = P > 0 ? P : 1;
+  const int16_t* indp = P > 0 ? ind : nullptr;
+  if (what == 0) {
+    const size_t seg8 = (size_t)kRepMax * Pseg * L::NS * sizeof(double);
+    const bool rep8 = seg8 <= kSegLdsBudget;
+    const size_t lds1 = ((rep8 ? (size_t)kRepMax : 1) * Pseg * L::NS + L::NACC) * sizeof(double);
+    if (lds1 + Ring<Q>::BYTES > 160 * 1024) return hipErrorInvalidValue;
+    if (rep8)
+      hipLaunchKernelGGL((xs_moments_kernel<Q, 0, kRepMax>), dim3(D), dim3(256), lds1, s, X, cap,
+                         ret, indp, N, Pseg, mom);
+    else
+      hipLaunchKernelGGL((xs_moments_kernel<Q, 0, 1>), dim3(D), dim3(256), lds1, s, X, cap, ret,
+                         indp, N, Pseg, mom);
+  } else if (what == 1) {
+    constexpr int CH = Q + 4;
+    const size_t P4 = ((size_t)Pseg + 3) & ~(size_t)3;
+    const size_t lds2 = ((size_t)L::msize(Pseg) + CH * CH + L::ND * (L::ND + 1) + (Q + 2) + Q +
+                         2 * P4) * sizeof(double);
+    if (lds2 > 64 * 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(xs_solve_kernel<Q>, dim3(D), dim3(64), lds2, s, mom, P, Pseg, pivot_mode,
+                       tol, f, coef, stats, status, (long long*)nullptr);
+  } else {
+    hipLaunchKernelGGL(xs_resid_kernel<Q>, dim3(D), dim3(256), 0, s, X, cap, ret, indp, D, N, P,
+                       coef, status, e, (double*)nullptr, sums);
+  }
+  return hipGetLastError();
+}
+
+int split_dispatch(int what, const float* X, const float* cap, const float* ret,
+                   const int16_t* ind, int D, int N, int P, int Q, int pivot_mode, double tol,
+                   double* mom, double* f, double* coef, double* stats, int* status, float* e,
+                   double* sums, void* stream) {
+  if (D <= 0) return 0;
+  if (Q < 1 || Q > 16 || P < 0 || P > 128 || N < 0 || (N % 8) != 0)
+    return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  switch (Q) {
+#define MFA_Q(qq)                                                                              \
+  case qq:                                                                                     \
+    return (int)split_q<qq>(what, X, cap, ret, ind, D, N, P, pivot_mode, tol, mom, f, coef,     \
+                            stats, status, e, sums, s);
+    MFA_Q(1) MFA_Q(2) MFA_Q(3) MFA_Q(4) MFA_Q(5) MFA_Q(6) MFA_Q(7) MFA_Q(8)
+    MFA_Q(9) MFA_Q(10) MFA_Q(11) MFA_Q(12) MFA_Q(13) MFA_Q(14) MFA_Q(15) MFA_Q(16)
+#undef MFA_Q
+  }
+  return (int)hipErrorInvalidValue;
+}
+}  // namespace
+
+// Raw moments [D][msize] of this rank's stocks (layout: Layout<Q>, see K1 above).
+MFA_API int mfa_xs_moments(const float* X, const float* cap, const float* ret, const int16_t* ind,
+                           int D, int N, int P, int Q, double* mom, void* stream) {
+  return split_dispatch(0, X, cap, ret, ind, D, N, P, Q, 0, 0.0, mom, nullptr, nullptr, nullptr,
+                        nullptr, nullptr, nullptr, stream);
+}
+
+// Constrained solve from (summed) moments: f [D][1+P+Q], coef [D][Q+1+P], stats, status.
+MFA_API int mfa_xs_solve(const double* mom, int D, int P, int Q, int pivot_mode, double tol,
+                         double* f, double* coef, double* stats, int* status, void* stream) {
+  return split_dispatch(1, nullptr, nullptr, nullptr, nullptr, D, 0, P, Q, pivot_mode, tol,
+                        (double*)mom, f, coef, stats, status, nullptr, nullptr, stream);
+}
+
+// Specific returns of this rank's stocks (e nullable) + per-date R^2 sums [D][5].
+MFA_API int mfa_xs_resid_sums(const float* X, const float* cap, const float* ret,
+                              const int16_t* ind, int D, int N, int P, int Q, const double* coef,
+                              const int* status, float* e, double* sums, void* stream) {
+  return split_dispatch(2, X, cap, ret, ind, D, N, P, Q, 0, 0.0, nullptr, nullptr,
+                        (double*)coef, nullptr, (int*)status, e, sums, stream);
+}
+
+// Bytes per date of the raw-moment layout (msize doubles).
+MFA_API size_t mfa_xs_moments_bytes(int P, int Q) {
+  const int Pseg = P > 0 ? P : 1;
+  return ((size_t)Q * (Q + 1) / 2 + 2 * Q + 4 + (size_t)Pseg * (Q + 3)) * sizeof(double);
 }

@@ -11,6 +11,8 @@ Collective call sites:
   C6 VRA bias series           all_gather   (D_local fp64)
   C7 outputs to rank 0         gather       (only when writing CSVs; factor-pipeline frames)
   C8 benchmark fences          barrier
+  C9 stock-sharded (TP) CS-WLS all_reduce   (D x msize moments, then D x 5 R^2 sums;
+                                             ops/xs_sharded.py)
 Backend ``nccl`` is RCCL on ROCm builds; ``gloo`` serves CPU tests.
 """
 from __future__ import annotations
