@@ -77,22 +77,48 @@ class FactorEngine:
         self.own = None  # row mask of the owned date block (date_shard); None = every row
 
     # ---------------------------------------------------------------- _prepare_data (:34-64)
+    @staticmethod
+    def _date_strings(td: pd.Series):
+        """(codes, unique "%Y/%m/%d" strings) of a date column, formatting only the uniques
+        (per-row strftime / to_datetime dominated host prep: 4.3 s at 2.5M rows)."""
+        codes, uniq = pd.factorize(td)
+        u = pd.Series(uniq)
+        if not isinstance(u.dtype, pd.api.types.DatetimeTZDtype) and not np.issubdtype(u.dtype, np.datetime64):
+            u = pd.to_datetime(u.astype(str), format="mixed")
+        return codes, u.dt.strftime("%Y/%m/%d").to_numpy(dtype=object)
+
     def _prepare(self, prices_df, index_df) -> pd.DataFrame:
-        p = prices_df.copy()
-        ix = index_df.copy()
-        for df in (p, ix):
-            td = df["trade_date"]
-            if not isinstance(td.dtype, pd.api.types.DatetimeTZDtype) and not np.issubdtype(td.dtype, np.datetime64):
-                td = pd.to_datetime(td.astype(str), format="mixed")
-            df["trade_date"] = td.dt.strftime("%Y/%m/%d")
-        p = p.sort_values(["ts_code", "trade_date"], kind="stable").reset_index(drop=True)
+        # _prepare_data (:34-64): "%Y/%m/%d" dates, stable sort by (ts_code, trade_date), the
+        # index's pct_change merged per date.  Done on integer codes: factorize the keys once,
+        # format only the unique dates, lexsort, and look market_ret up by date code.
+        dc, dstr = self._date_strings(prices_df["trade_date"])
+        dnames = np.unique(dstr)                      # sorted "%Y/%m/%d" == chronological
+        drank = np.searchsorted(dnames, dstr)         # unique-date code -> sorted date code
+        scodes, snames = pd.factorize(prices_df["ts_code"].astype(str), sort=True)
+        row_d = drank[dc]
+        order = np.lexsort((row_d, scodes))           # stable: ts_code, then trade_date
+        p = pd.DataFrame({c: prices_df[c].to_numpy()[order] for c in prices_df.columns})
+        p["trade_date"] = dnames[row_d[order]]
+        ix = index_df[["trade_date", "close"]].copy()
+        ic, istr = self._date_strings(ix["trade_date"])
+        ix["trade_date"] = istr[ic]
         ix = ix.sort_values("trade_date").reset_index(drop=True)
         ix["market_ret"] = ix["close"].pct_change()
-        master = p.merge(ix[["trade_date", "market_ret"]], on="trade_date", how="left")
-        master = master.reset_index().rename(columns={"index": "original_index"})
+        if ix["trade_date"].is_unique:
+            pos = pd.Index(ix["trade_date"]).get_indexer(dnames)
+            mr = np.where(pos >= 0, ix["market_ret"].to_numpy(np.float64)[np.maximum(pos, 0)], np.nan)
+            master = p
+            master["market_ret"] = mr[row_d[order]]
+        else:  # duplicate index dates: keep the merge's row multiplication
+            master = p.merge(ix[["trade_date", "market_ret"]], on="trade_date", how="left")
+        master.insert(0, "original_index", np.arange(len(master)))
         dev = self.device
-        codes, self.stock_names = pd.factorize(master["ts_code"].astype(str), sort=True)
-        dcodes, self.date_names = pd.factorize(master["trade_date"], sort=True)
+        if len(master) == len(p):
+            codes, self.stock_names = scodes[order], pd.Index(snames)
+            dcodes, self.date_names = row_d[order], pd.Index(dnames)
+        else:
+            codes, self.stock_names = pd.factorize(master["ts_code"].astype(str), sort=True)
+            dcodes, self.date_names = pd.factorize(master["trade_date"], sort=True)
         self.R = len(master)
         self.D, self.N = len(self.date_names), len(self.stock_names)
         self.stock_id = torch.from_numpy(codes.astype(np.int32)).to(dev)
@@ -212,6 +238,36 @@ class FactorEngine:
         if not (self._need("n_cashflow_act", "total_mv", "pe_ttm") and "end_date" in self.master.columns):
             return None
         m = self.master
+        cf = self._ttm_by_codes(m)
+        if cf is None:
+            cf = self._ttm_by_merge(m)
+        mv = self.cols["total_mv"].double()
+        nan = torch.full_like(mv, float("nan"))
+        cetop = torch.where((mv > 0) & (cf > 0), cf / mv, nan)  # unit mix-up kept (quirk Q17)
+        pe = self.cols["pe_ttm"].double()
+        etop = torch.where(pe > 0, 1.0 / pe, nan)
+        return {"CETOP": cetop.float(), "ETOP": etop.float()}
+
+    def _ttm_by_codes(self, m: pd.DataFrame):
+        """Statement-row TTM (:392-410) on integer keys: (stock, end_date) rows deduplicated by
+        np.unique, a 4-row rolling sum per stock on the device, gathered back by the inverse
+        index.  None when one (stock, end_date) carries several values (the merge path's row
+        multiplication is then kept by :meth:`_ttm_by_merge`)."""
+        ecodes, _ = pd.factorize(m["end_date"], sort=True)
+        ne = int(ecodes.max()) + 1 if len(ecodes) else 0
+        sc = self.stock_id.cpu().numpy().astype(np.int64)
+        key = sc * (ne + 1) + np.where(ecodes < 0, ne, ecodes)  # NaT last, as sort_values
+        uk, first, inv = np.unique(key, return_index=True, return_inverse=True)
+        v = m["n_cashflow_act"].to_numpy(np.float64, na_value=np.nan)
+        vf = v[first]
+        same = (v == vf[inv]) | (np.isnan(v) & np.isnan(vf[inv]))
+        if not same.all():
+            return None
+        seg = RL.seg_lo_from_codes(torch.from_numpy(uk // (ne + 1))).to(self.device)
+        ttm = RL.rolling_sum(torch.from_numpy(vf.astype(np.float32)).to(self.device), seg, 4, 4)
+        return ttm.double()[torch.from_numpy(inv).to(self.device)]
+
+    def _ttm_by_merge(self, m: pd.DataFrame):
         fin = m[["ts_code", "end_date", "n_cashflow_act"]].drop_duplicates().copy()
         fin = fin.sort_values(["ts_code", "end_date"], kind="stable").reset_index(drop=True)
         codes = torch.from_numpy(pd.factorize(fin["ts_code"].astype(str))[0].astype(np.int32))
@@ -222,13 +278,7 @@ class FactorEngine:
         tmp = m[["original_index", "ts_code", "end_date"]].merge(
             fin[["ts_code", "end_date", "n_cashflow_act_ttm"]], on=["ts_code", "end_date"], how="left")
         tmp = tmp.sort_values("original_index", kind="stable")
-        cf = torch.from_numpy(tmp["n_cashflow_act_ttm"].to_numpy(np.float64, na_value=np.nan)).to(self.device)
-        mv = self.cols["total_mv"].double()
-        nan = torch.full_like(mv, float("nan"))
-        cetop = torch.where((mv > 0) & (cf > 0), cf / mv, nan)  # unit mix-up kept (quirk Q17)
-        pe = self.cols["pe_ttm"].double()
-        etop = torch.where(pe > 0, 1.0 / pe, nan)
-        return {"CETOP": cetop.float(), "ETOP": etop.float()}
+        return torch.from_numpy(tmp["n_cashflow_act_ttm"].to_numpy(np.float64, na_value=np.nan)).to(self.device)
 
     def select_growth_factors(self):
         if not self._need("q_profit_yoy", "q_sales_yoy"):
@@ -311,10 +361,13 @@ class _Grid:
         return g.reshape(-1)[self.idx].double().cpu().numpy()
 
 
-def winsorize_frame(df: pd.DataFrame, factor_list: list, n_std: float = 2.5, device=None) -> pd.DataFrame:
+def winsorize_frame(df: pd.DataFrame, factor_list: list, n_std: float = 2.5, device=None,
+                    grid: _Grid | None = None, copy: bool = True) -> pd.DataFrame:
+    """``grid`` (a :class:`_Grid` of the same keys) and ``copy=False`` let a pipeline build the
+    (date, stock) index once and work in place; the defaults keep ``post_processing`` semantics."""
     dev = torch.device(device) if device else _default_device()
-    out = df.copy()
-    grid = _Grid(out, dev)
+    out = df.copy() if copy else df
+    grid = grid if grid is not None else _Grid(out, dev)
     for f in factor_list:
         if f not in out.columns:
             print(f"Warning: Factor '{f}' not found in DataFrame. Skipping.")
@@ -323,9 +376,9 @@ def winsorize_frame(df: pd.DataFrame, factor_list: list, n_std: float = 2.5, dev
     return out
 
 
-def composite_frame(df: pd.DataFrame, config: dict, device=None) -> pd.DataFrame:
+def composite_frame(df: pd.DataFrame, config: dict, device=None, copy: bool = True) -> pd.DataFrame:
     dev = torch.device(device) if device else _default_device()
-    out = df.copy()
+    out = df.copy() if copy else df
     for new, cfg in config.items():
         xs, ws = [], []
         for c, w in zip(cfg["components"], cfg["weights"]):
@@ -341,10 +394,11 @@ def composite_frame(df: pd.DataFrame, config: dict, device=None) -> pd.DataFrame
     return out
 
 
-def orthogonalize_frame(df: pd.DataFrame, rules: dict, device=None) -> pd.DataFrame:
+def orthogonalize_frame(df: pd.DataFrame, rules: dict, device=None, grid: _Grid | None = None,
+                        copy: bool = True) -> pd.DataFrame:
     dev = torch.device(device) if device else _default_device()
-    out = df.copy()
-    grid = _Grid(out, dev)
+    out = df.copy() if copy else df
+    grid = grid if grid is not None else _Grid(out, dev)
     for target, against in rules.items():
         y = grid.put(out[target].to_numpy(np.float64, na_value=np.nan))
         xs = [grid.put(out[a].to_numpy(np.float64, na_value=np.nan)) for a in against]
@@ -352,12 +406,45 @@ def orthogonalize_frame(df: pd.DataFrame, rules: dict, device=None) -> pd.DataFr
     return out
 
 
-def barra_export(processed: pd.DataFrame, sw_industry: pd.DataFrame):
-    """main.py:98-137: industry merge, t+1 return, rename/select; plus industry_info."""
-    barra = processed.merge(sw_industry[["ts_code", "l1_code"]], on="ts_code", how="left")
-    barra["ret"] = barra.groupby("ts_code")["ret"].shift(-1)
-    barra = barra.rename(columns=BARRA_RENAME)
-    final = barra[[c for c in BARRA_OUTPUT_COLUMNS if c in barra.columns]]
+def _next_in_group(keys: pd.Series, values: np.ndarray) -> np.ndarray:
+    """``values`` shifted by -1 within groups of ``keys`` in frame order (groupby().shift(-1));
+    NaN keys are their own non-group (pandas dropna) and get NaN."""
+    codes = pd.factorize(keys)[0]
+    order = np.argsort(codes, kind="stable")
+    out = np.full(len(values), np.nan)
+    same = codes[order[1:]] == codes[order[:-1]]
+    nxt = np.where(same, values[order[1:]], np.nan)
+    out[order[:-1]] = nxt
+    out[codes < 0] = np.nan
+    return out
+
+
+def barra_export(processed: pd.DataFrame, sw_industry: pd.DataFrame, _merge_path: bool = False):
+    """main.py:98-137: industry merge, t+1 return, rename/select; plus industry_info.
+
+    When every stock has one industry row (the usual case) the merge is an index lookup and
+    only the exported columns are materialised; a stock with several memberships (quirk Q21:
+    the merge multiplies its rows) takes the pandas merge path.
+    """
+    if not _merge_path and sw_industry["ts_code"].is_unique and "l1_code" not in processed.columns:
+        pos = pd.Index(sw_industry["ts_code"]).get_indexer(processed["ts_code"])
+        l1 = sw_industry["l1_code"].to_numpy(dtype=object)
+        src = {"l1_code": pd.Series(np.where(pos >= 0, l1[np.maximum(pos, 0)], np.nan), dtype=object)}
+        src["ret"] = _next_in_group(processed["ts_code"], processed["ret"].to_numpy(np.float64))
+        inv = {v: k for k, v in BARRA_RENAME.items()}
+        cols = {}
+        for c in BARRA_OUTPUT_COLUMNS:
+            s0 = inv.get(c, c)
+            if s0 in src:
+                cols[c] = src[s0]
+            elif s0 in processed.columns and (s0 == c or c not in processed.columns):
+                cols[c] = processed[s0].to_numpy()
+        final = pd.DataFrame(cols)
+    else:
+        barra = processed.merge(sw_industry[["ts_code", "l1_code"]], on="ts_code", how="left")
+        barra["ret"] = barra.groupby("ts_code")["ret"].shift(-1)
+        barra = barra.rename(columns=BARRA_RENAME)
+        final = barra[[c for c in BARRA_OUTPUT_COLUMNS if c in barra.columns]]
     stk = final[["stocknames"]].drop_duplicates().rename(columns={"stocknames": "ts_code"})
     cols = [c for c in ["ts_code", "l1_code", "l1_name", "in_date"] if c in sw_industry.columns]
     info = stk.merge(sw_industry[cols], on="ts_code", how="left")
@@ -389,9 +476,11 @@ def factor_pipeline(prices_df, index_df, sw_industry_df, factors=None, config: F
     t["descriptors_s"] = time.perf_counter() - t0
     t0 = time.perf_counter()
     cols = [c for c in raw.columns if c not in ("ts_code", "trade_date")]
-    w = winsorize_frame(raw, cols, cfg.winsor_n_std, device=eng.device)  # incl. ret, circ_mv (Q23)
-    c = composite_frame(w, cfg.composite, device=eng.device)
-    o = orthogonalize_frame(c, cfg.ortho, device=eng.device)
+    # raw is this pipeline's own frame: one (date, stock) grid index, in-place steps
+    grid = _Grid(raw, eng.device)
+    w = winsorize_frame(raw, cols, cfg.winsor_n_std, device=eng.device, grid=grid, copy=False)  # incl. ret, circ_mv (Q23)
+    c = composite_frame(w, cfg.composite, device=eng.device, copy=False)
+    o = orthogonalize_frame(c, cfg.ortho, device=eng.device, grid=grid, copy=False)
     t["postprocess_s"] = time.perf_counter() - t0
     if dist_on:  # C7: date blocks to rank 0, back in master order (ts_code, trade_date)
         parts = pdist.gather_objects(o, ctx)

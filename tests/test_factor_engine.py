@@ -133,3 +133,32 @@ def test_hip_sliding_window_kernels_match_direct(cuda):
         b = scan[k] if isinstance(scan[k], tuple) else (scan[k],)
         for x, y in zip(a, b):
             torch.testing.assert_close(y.cpu(), x.cpu(), rtol=2e-5, atol=2e-7, equal_nan=True, msg=k)
+
+
+
+def test_barra_export_fast_path_equals_merge_path(data):
+    """The index-lookup export (unique industry rows) equals the pandas merge / groupby-shift
+    path it replaces, including suspended stocks and a stock missing from the industry table."""
+    prices, index, sw = data
+    eng = FE.FactorEngine(prices, index, device="cpu")
+    raw = eng.run(FE.FACTORS_TO_RUN)
+    for table in (sw, sw.iloc[1:].reset_index(drop=True)):
+        fast, info_f = FE.barra_export(raw, table)
+        slow, info_s = FE.barra_export(raw, table, _merge_path=True)
+        pd.testing.assert_frame_equal(fast, slow.reset_index(drop=True), check_dtype=False)
+        pd.testing.assert_frame_equal(info_f, info_s)
+
+
+def test_cetop_ttm_code_path_equals_merge_path():
+    """CETOP's statement-row TTM on integer keys equals the drop_duplicates / merge path,
+    with missing cash flows and NaT statement dates (no statement yet) in the panel."""
+    prices, index, _ = FE.synthetic_prices(N=60, T=400, seed=2, suspend_frac=0.05)
+    ed = prices["end_date"].unique()
+    prices.loc[prices.end_date.isin(ed[::3]) & (prices.ts_code < "000030"), "n_cashflow_act"] = np.nan
+    m = prices.end_date.isin(ed[1::5]) & (prices.ts_code > "600010")
+    prices.loc[m, "end_date"] = np.datetime64("NaT")
+    prices.loc[m, "n_cashflow_act"] = np.nan
+    eng = FE.FactorEngine(prices, index, device="cpu")
+    a, b = eng._ttm_by_codes(eng.master), eng._ttm_by_merge(eng.master)
+    assert a is not None and int(torch.isfinite(a).sum()) > 1000
+    torch.testing.assert_close(a, b, rtol=0, atol=0, equal_nan=True)
