@@ -195,12 +195,16 @@ def write_risk_results(model, out_dir: str, long_specific: bool = False) -> dict
     paths["r_squared"] = os.path.join(out_dir, "r_squared.csv")
     pd.DataFrame(R2.cpu().numpy(), index=idx, columns=["R2"]).to_csv(paths["r_squared"])
     paths["specific_returns"] = os.path.join(out_dir, "specific_returns.csv")
-    e = pd.DataFrame(E.cpu().numpy(), index=idx, columns=model.panel.stocks)
+    En = E.cpu().numpy()
     if long_specific:  # demo.ipynb#c5 variant: date, ts_code, specific_ret
+        e = pd.DataFrame(En, index=idx, columns=model.panel.stocks)
         e.stack().rename("specific_ret").rename_axis(["date", "ts_code"]).reset_index().to_csv(
             paths["specific_returns"], index=False)
-    else:
-        e.to_csv(paths["specific_returns"])
+    else:  # dates x stocks: the native multi-threaded writer (pandas format), pandas fallback
+        from .native_io import write_matrix_csv
+        if En.dtype != np.float32 or not write_matrix_csv(
+                paths["specific_returns"], En, idx.strftime("%Y-%m-%d"), model.panel.stocks):
+            pd.DataFrame(En, index=idx, columns=model.panel.stocks).to_csv(paths["specific_returns"])
     if last is not None:
         paths["final_cov"] = os.path.join(out_dir, "final_vol_regime_adj_covariance.csv")
         pd.DataFrame(last.cpu().numpy(), index=names, columns=names).to_csv(paths["final_cov"])

@@ -22,6 +22,9 @@ def _load():
         lib.mfa_csv_shape.restype = C.c_int64
         lib.mfa_csv_parse.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_void_p), C.c_int]
         lib.mfa_csv_parse.restype = C.c_int64
+        lib.mfa_write_matrix_csv.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.c_char_p),
+                                             C.c_longlong, C.c_longlong, C.c_void_p, C.c_int]
+        lib.mfa_write_matrix_csv.restype = C.c_int
         _lib = lib
     return _lib
 
@@ -100,3 +103,34 @@ def read_columns(path: str, types: dict, nthreads: int = 0):
     got = lib.mfa_csv_parse(path.encode(), len(header), (C.c_int * len(tl))(*tl),
                             (C.c_void_p * len(bufs))(*[b.ctypes.data for b in bufs]), nthreads)
     return {n: b[:got] for n, b in zip(header, bufs)}
+
+
+_NEEDS_QUOTING = set(',"\n\r')
+
+
+def write_matrix_csv(path: str, values: np.ndarray, row_labels, col_labels, index_label: str = "",
+                     nthreads: int = 0) -> bool:
+    """Write a float32 [rows, cols] matrix with row / column labels as pandas ``to_csv`` would
+    (``csrc_host/csv_write.cpp``, multi-threaded).  Returns False (nothing written) when the
+    native library is unavailable or a label would need CSV quoting: the caller then uses
+    pandas."""
+    if os.environ.get("MFA_NO_NATIVE_IO"):
+        return False
+    labels = [str(x) for x in row_labels]
+    cols = [str(x) for x in col_labels]
+    if any(_NEEDS_QUOTING & set(x) for x in labels + cols + [index_label]):
+        return False
+    try:
+        lib = _load()
+    except Exception:
+        return False
+    v = np.ascontiguousarray(values, dtype=np.float32)
+    if v.shape != (len(labels), len(cols)):
+        raise ValueError(f"matrix {v.shape} vs {len(labels)} x {len(cols)} labels")
+    header = ",".join([index_label] + cols).encode()
+    arr = (C.c_char_p * len(labels))(*[x.encode() for x in labels])
+    rc = lib.mfa_write_matrix_csv(path.encode(), header, arr, v.shape[0], v.shape[1],
+                                  v.ctypes.data, nthreads)
+    if rc != 0:
+        raise OSError(f"mfa_write_matrix_csv failed for {path}")
+    return True

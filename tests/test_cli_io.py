@@ -102,3 +102,21 @@ def test_cli_checkpoint_resume(tmp_path):
     ff = pd.read_csv(f"{d}/full/factor_returns.csv", index_col=0)
     assert len(f2) == 15
     np.testing.assert_allclose(f2.values, ff.values[35:], rtol=1e-12, atol=1e-15)
+
+
+def test_native_matrix_csv_writer_matches_pandas(tmp_path):
+    """specific_returns.csv through the native writer is byte-identical to pandas to_csv
+    (numpy float32 repr: positional / scientific switch, integral '.0', NaN -> empty)."""
+    from llm_driven_multi_factor_model_amd.utils import native_io
+    rng = np.random.default_rng(1)
+    v = (rng.normal(0, 0.02, (37, 23)) * rng.choice([1, 1e-6, 1e3, 1e17], (37, 23))).astype(np.float32)
+    v[0, :6] = [0.0, -0.0, 1.0, -3.0, 1e-4, 9.999e-5]
+    v[1, :4] = [np.nan, np.inf, -np.inf, 123456.0]
+    v[2, :2] = [1e16, 9.9e15]
+    idx = pd.date_range("2021-01-04", periods=37, freq="B")
+    cols = [f"{i:06d}.SZ" for i in range(23)]
+    a, b = str(tmp_path / "a.csv"), str(tmp_path / "b.csv")
+    assert native_io.write_matrix_csv(a, v, idx.strftime("%Y-%m-%d"), cols)
+    pd.DataFrame(v, index=idx, columns=cols).to_csv(b)
+    assert open(a).read() == open(b).read()
+    assert not native_io.write_matrix_csv(a, v, idx.strftime("%Y-%m-%d"), ["a,b"] + cols[1:])

@@ -12,7 +12,8 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SRC = [os.path.join(ROOT, "tools", "sanitize", "host_runtime_check.cpp"),
        os.path.join(ROOT, "llm_driven_multi_factor_model_amd", "csrc_host", "csv_panel.cpp"),
-       os.path.join(ROOT, "llm_driven_multi_factor_model_amd", "csrc_host", "asof.cpp")]
+       os.path.join(ROOT, "llm_driven_multi_factor_model_amd", "csrc_host", "asof.cpp"),
+       os.path.join(ROOT, "llm_driven_multi_factor_model_amd", "csrc_host", "csv_write.cpp")]
 
 
 def _build_and_run(tmp_path, flags, env_extra):
