@@ -91,6 +91,24 @@ def panel_from_frame(data: pd.DataFrame, P: int, Q: int, device="cpu",
         style_names=sty_names, industry_names=ind_names)
 
 
+def _unique_s16(a: np.ndarray):
+    """``np.unique(a, return_inverse=True)`` for an ``S16`` array via hash factorisation of its
+    two 8-byte words (O(n); the string sort took ~0.4 s per million rows), then a sort of the
+    few uniques only."""
+    if a.dtype != np.dtype("S16") or not a.flags.c_contiguous:
+        return np.unique(a, return_inverse=True)
+    w = a.view(np.uint64).reshape(-1, 2)
+    c0, u0 = pd.factorize(w[:, 0])
+    c1, u1 = pd.factorize(w[:, 1])
+    codes, pairs = pd.factorize(c0.astype(np.int64) * len(u1) + c1)
+    uw = np.stack([u0[pairs // len(u1)], u1[pairs % len(u1)]], 1).astype(np.uint64)
+    uniq = np.ascontiguousarray(uw).view("S16").reshape(-1)
+    order = np.argsort(uniq, kind="stable")
+    rank = np.empty_like(order)
+    rank[order] = np.arange(len(order))
+    return uniq[order], rank[codes]
+
+
 def panel_from_barra_csv(path: str, industry_info_path: str, device="cpu") -> RiskPanel:
     """barra_data_csi.csv + industry_info.csv -> dense panel (demo.py:22-35 semantics).
 
@@ -109,9 +127,9 @@ def panel_from_barra_csv(path: str, industry_info_path: str, device="cpu") -> Ri
     styles = names[5:]
     Q = len(styles)
     P = len(info)
-    num = np.stack([cols[c] for c in ["capital", "ret", *styles]], 1)
-    ok = np.isfinite(num).all(1) & (cols["date"] != b"") & (cols["stocknames"] != b"") & \
-        (cols["industry"] != b"")  # demo.py:25-27 drops rows with any NaN
+    ok = (cols["date"] != b"") & (cols["stocknames"] != b"") & (cols["industry"] != b"")
+    for c in ["capital", "ret", *styles]:  # demo.py:25-27 drops rows with any NaN
+        ok &= np.isfinite(cols[c])
     codes = np.asarray(info["code"].astype(str).values).astype("S16")
     order = np.argsort(codes)
     pos = np.searchsorted(codes[order], cols["industry"])
@@ -122,19 +140,20 @@ def panel_from_barra_csv(path: str, industry_info_path: str, device="cpu") -> Ri
         warnings.warn(f"{int((~hit[ok]).sum())} rows have an industry code missing from "
                       "industry_info and are excluded")
     sel = ok & hit
-    d_uni, d_codes = np.unique(cols["date"][sel], return_inverse=True)
-    s_uni, s_codes = np.unique(cols["stocknames"][sel], return_inverse=True)
+    d_uni, d_codes = _unique_s16(cols["date"][sel])
+    s_uni, s_codes = _unique_s16(cols["stocknames"][sel])
     D, N = len(d_uni), len(s_uni)
     cap = np.full((D, N), np.nan, dtype=np.float32)
     ret = np.full((D, N), np.nan, dtype=np.float32)
     sty = np.full((D, Q, N), np.nan, dtype=np.float32)
     ind = np.full((D, N), -1, dtype=np.int16)
-    v = num[sel].astype(np.float32)
-    cap[d_codes, s_codes] = v[:, 0]
-    ret[d_codes, s_codes] = v[:, 1]
-    for q in range(Q):
-        sty[d_codes, q, s_codes] = v[:, 2 + q]
-    ind[d_codes, s_codes] = ind_id[sel].astype(np.int16)
+    flat = d_codes * N + s_codes
+    cap.reshape(-1)[flat] = cols["capital"][sel]
+    ret.reshape(-1)[flat] = cols["ret"][sel]
+    sflat = d_codes * (Q * N) + s_codes
+    for q, c in enumerate(styles):
+        sty.reshape(-1)[sflat + q * N] = cols[c][sel]
+    ind.reshape(-1)[flat] = ind_id[sel].astype(np.int16)
     dates = pd.to_datetime(pd.Index(d_uni.astype("U16")), format="mixed").values
     dev = torch.device(device)
     return RiskPanel(
