@@ -12,6 +12,22 @@ from .._build import HOST_LIB_PATH, build_host
 _lib = None
 
 
+_warned = False
+
+
+def _load_or_none():
+    """The host library, or None with ONE logged warning (callers then use pandas / numpy)."""
+    global _warned
+    try:
+        return _load()
+    except Exception as e:  # missing toolchain / unbuildable: the pure-Python path still works
+        if not _warned:
+            import logging
+            logging.getLogger("mfa").warning("native host IO unavailable (%s); using pandas", e)
+            _warned = True
+        return None
+
+
 def _load():
     global _lib
     if _lib is None:
@@ -37,9 +53,8 @@ def read_csv(path: str, string_cols=STRING_COLS, date_cols=(), nthreads: int = 0
     """Columns in ``string_cols`` stay strings (dates keep their file format, as pandas does),
     ``date_cols`` become int32 YYYYMMDD, everything else float64."""
     """Parse a simple (unquoted-comma) CSV with a header into a DataFrame; None if unsupported."""
-    try:
-        lib = _load()
-    except Exception:
+    lib = _load_or_none()
+    if lib is None:
         return None
     with open(path, "rb") as fh:
         header = fh.readline().decode("utf-8-sig").strip().split(",")
@@ -84,9 +99,8 @@ def read_columns(path: str, types: dict, nthreads: int = 0):
 
     Returns ``{name: ndarray}`` (bytes columns stay ``S16``), or None if unavailable.
     """
-    try:
-        lib = _load()
-    except Exception:
+    lib = _load_or_none()
+    if lib is None:
         return None
     with open(path, "rb") as fh:
         header = fh.readline().decode("utf-8-sig").strip().split(",")
@@ -120,9 +134,8 @@ def write_matrix_csv(path: str, values: np.ndarray, row_labels, col_labels, inde
     cols = [str(x) for x in col_labels]
     if any(_NEEDS_QUOTING & set(x) for x in labels + cols + [index_label]):
         return False
-    try:
-        lib = _load()
-    except Exception:
+    lib = _load_or_none()
+    if lib is None:
         return False
     v = np.ascontiguousarray(values, dtype=np.float32)
     if v.shape != (len(labels), len(cols)):

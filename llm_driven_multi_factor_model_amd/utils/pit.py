@@ -60,7 +60,9 @@ def asof_indices(left_groups, left_keys, right_groups, right_keys) -> np.ndarray
     out = np.empty(len(lg), dtype=np.int64)
     try:
         lib = _load()
-    except Exception:
+    except Exception as e:  # no host toolchain: the numpy loop below is the same join
+        import logging
+        logging.getLogger("mfa").warning("native as-of join unavailable (%s); using numpy", e)
         lib = None
     if lib is None:
         for i in range(len(lg)):
