@@ -650,7 +650,10 @@ __global__ __launch_bounds__(64) void xs_solve_kernel(const double* __restrict__
 // workgroup (<= 16 waves); `red` = 16 x 5 doubles of LDS.
 // Residual-pass data of 4 consecutive stocks x UP iterations, loaded by waves 1..3 while wave 0
 // solves (fused kernel, `kPre`): the pass then starts with 1536 stocks already in registers.
-constexpr int kPreU = 2;
+#ifndef MFA_XS_PREU
+#define MFA_XS_PREU 2
+#endif
+constexpr int kPreU = MFA_XS_PREU;
 constexpr int kPreStocks = 3 * 64 * 4 * kPreU;
 template <int Q>
 struct ResidPre {
