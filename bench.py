@@ -8,7 +8,8 @@ WLS on [country | 31 SW-L1 industries | 10 styles] with the industry-neutral con
 (K = 42 columns, 41 free parameters), factor returns, specific returns for every stock and R^2.
 
 A step regresses every date of a rank's shard (weak scaling: ``--dates`` per GPU, default 2520
-= 10 years of trading days; three kernels replayed as one captured HIP graph), then all-gathers
+= 10 years of trading days; the fused moments -> solve -> residual kernel, one workgroup per
+date, replayed from a captured HIP graph), then all-gathers
 the factor-return series across ranks over RCCL (the collective the downstream Newey-West stage
 needs).  Data is a synthetic panel of the named shape with random-init exposures (the reference ships no data).
 
