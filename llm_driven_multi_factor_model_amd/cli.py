@@ -7,6 +7,8 @@
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m llm_driven_multi_factor_model_amd.cli risk ...
     python -m llm_driven_multi_factor_model_amd.cli factors --prices prices.csv --index index.csv \
         --industry sw_industry.csv --out data/
+    python -m llm_driven_multi_factor_model_amd.cli serve --data barra_data_csi.csv \
+        --industry industry_info.csv --port 8000      # POST /risk {"portfolios": [...]}
 
 ``risk`` is ``Barra-master/demo.py`` (read -> one-hot -> MFM(data, P, Q) -> 4 stages -> 5 CSVs);
 ``factors`` is ``Barra_factor_cal/main.py`` (descriptors -> winsorize -> composite ->
@@ -144,6 +146,24 @@ def _write_attribution(model, spec: str, out_dir: str, ctx):
     return path
 
 
+def cmd_serve(a):
+    """Fit the risk model on a barra_data_csi.csv (single process) and serve portfolio risk of
+    its last date over HTTP (``serving.make_app``)."""
+    from .models.risk_model import RiskModel
+    from .serving import RiskService, make_app
+    from .utils.config import preset
+    from .utils.io import panel_from_barra_csv
+    _setup_logging()
+    dev = a.device or ("cuda:0" if torch.cuda.is_available() else "cpu")
+    panel = panel_from_barra_csv(a.data, a.industry, device=dev)
+    over = {"eigen_sims": a.sims} if a.sims is not None else {}
+    model = RiskModel(panel, preset(a.preset, **over)).run()
+    svc = RiskService(model, which=a.covariance)
+    log.info("serving %s", json.dumps(svc.info()))
+    import uvicorn
+    uvicorn.run(make_app(svc), host=a.host, port=a.port, log_level="info")
+
+
 def cmd_factors(a):
     from .models.factor_engine import run_factor_pipeline
     from .parallel import dist as pdist
@@ -192,6 +212,16 @@ def main(argv=None):
     r.add_argument("--resume", default=None,
                    help="continue from a checkpoint: only dates after its last date are run")
     r.set_defaults(fn=cmd_risk)
+    v = sub.add_parser("serve", help="fit the risk model, then serve portfolio risk over HTTP")
+    v.add_argument("--data", required=True, help="barra_data_csi.csv")
+    v.add_argument("--industry", required=True, help="industry_info.csv")
+    v.add_argument("--preset", default="reference")
+    v.add_argument("--sims", type=int, default=None)
+    v.add_argument("--covariance", choices=["nw", "eigen", "vra"], default="vra")
+    v.add_argument("--device", default=None)
+    v.add_argument("--host", default="127.0.0.1")
+    v.add_argument("--port", type=int, default=8000)
+    v.set_defaults(fn=cmd_serve)
     f = sub.add_parser("factors", help="main.py equivalent: descriptors -> Barra exposures")
     f.add_argument("--prices", required=True)
     f.add_argument("--index", required=True)
@@ -200,7 +230,7 @@ def main(argv=None):
     f.add_argument("--device", default=None)
     f.set_defaults(fn=cmd_factors)
     a = ap.parse_args(argv)
-    if a.cmd not in ("risk", "factors"):
+    if a.cmd not in ("risk", "factors", "serve"):
         _setup_logging()
     a.fn(a)
     return 0
