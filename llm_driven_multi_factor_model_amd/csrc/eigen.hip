@@ -289,8 +289,11 @@ __global__ __launch_bounds__(64) void mc_cov_kernel(int K, int T, unsigned long 
 // consecutive lanes touch 16 consecutive 16-B slots (conflict-free ds_read_b128), and the
 // next-round writes land on neighbouring blocks too.  The triangular packing it replaces had
 // bank-conflict cycles at 89 % of LDS-active cycles (rocprofv3, mc_bias_kernel).
+#ifndef MFA_PK_PAD
+#define MFA_PK_PAD 16  // entry stride rounding (power of 2)
+#endif
 __host__ __device__ constexpr int pk_blocks_padded(int Ke) {
-  return ((((Ke >> 1) * ((Ke >> 1) + 1)) >> 1) + 15) & ~15;
+  return ((((Ke >> 1) * ((Ke >> 1) + 1)) >> 1) + MFA_PK_PAD - 1) & ~(MFA_PK_PAD - 1);
 }
 __host__ __device__ constexpr int pk_size(int Ke) { return 4 * pk_blocks_padded(Ke); }
 __device__ __forceinline__ int pk(int i, int j, int Ke) {
