@@ -77,11 +77,13 @@ def asof_indices(left_groups, left_keys, right_groups, right_keys) -> np.ndarray
 
 
 def robust_merge_asof(left_df: pd.DataFrame, right_df: pd.DataFrame, left_on: str, right_on: str,
-                      by: str) -> pd.DataFrame:
+                      by: str, device: str | None = None) -> pd.DataFrame:
     """Per-``by`` backward as-of merge (semantics of load_data.py:41-62).
 
     Output rows are ordered like the reference (sorted by [by, left_on]); right-side columns
-    that collide with left ones get pandas' ``_x`` / ``_y`` suffixes.
+    that collide with left ones get pandas' ``_x`` / ``_y`` suffixes.  ``device="cuda"`` runs
+    the index search on the GPU (``ops.asof``, HIP kernel ``csrc/asof.hip``); the default is the
+    multi-threaded host join.
     """
     left = left_df.reset_index(drop=True).sort_values(by=[by, left_on], kind="stable").reset_index(drop=True)
     right = right_df.reset_index(drop=True).sort_values(by=[by, right_on], kind="stable").reset_index(drop=True)
@@ -89,7 +91,14 @@ def robust_merge_asof(left_df: pd.DataFrame, right_df: pd.DataFrame, left_on: st
     lg = cats.get_indexer(left[by].astype(str))
     rg = cats.get_indexer(right[by].astype(str))
     # keys must be non-decreasing within each group on both sides (they are: sorted above)
-    idx = asof_indices(lg, _keys(left[left_on]), rg, _keys(right[right_on]))
+    if device is not None and str(device).startswith("cuda"):
+        import torch
+        from ..ops.asof import asof_search
+        t = lambda a, dt: torch.as_tensor(np.ascontiguousarray(a, dtype=dt), device=device)  # noqa: E731
+        idx = asof_search(t(lg, np.int32), t(_keys(left[left_on]), np.int64), t(rg, np.int32),
+                          t(_keys(right[right_on]), np.int64), check_sorted=False).cpu().numpy()
+    else:
+        idx = asof_indices(lg, _keys(left[left_on]), rg, _keys(right[right_on]))
     rcols = [c for c in right.columns if c != by]
     taken = right.iloc[np.where(idx >= 0, idx, 0)][rcols].reset_index(drop=True)
     taken.loc[idx < 0, :] = np.nan
