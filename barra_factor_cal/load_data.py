@@ -14,18 +14,24 @@ from datetime import date
 import pandas as pd
 
 from llm_driven_multi_factor_model_amd.utils.pit import (dedupe_statements, fill_missing,
-                                                         optimize_dtypes, robust_merge_asof)
+                                                         load_collection_chunked, optimize_dtypes,
+                                                         robust_merge_asof)
 
 from . import config
 
 __all__ = ["optimize_dtypes", "load_collection_to_df", "robust_merge_asof", "load_and_prepare_data"]
 
 
-def load_collection_to_df(db, collection_name: str, query: dict, projection: dict) -> pd.DataFrame:
+def load_collection_to_df(db, collection_name: str, query: dict, projection: dict,
+                          chunk_size: int | None = None) -> pd.DataFrame:
+    """``chunk_size`` streams the cursor in bounded chunks (datause.ipynb#c6 pattern)."""
     print(f"正在从 '{collection_name}' 加载数据...")
-    df = pd.DataFrame(list(db[collection_name].find(query, projection)))
-    if not df.empty:
-        df = optimize_dtypes(df)
+    if chunk_size:
+        df = load_collection_chunked(db, collection_name, query, projection, chunk_size)
+    else:
+        df = pd.DataFrame(list(db[collection_name].find(query, projection)))
+        if not df.empty:
+            df = optimize_dtypes(df)
     print(f"-> 成功加载 {len(df):,} 行数据。")
     return df
 

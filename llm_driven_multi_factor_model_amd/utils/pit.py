@@ -11,6 +11,7 @@ gather the matched columns.  Results are identical to the reference's per-stock 
 from __future__ import annotations
 
 import ctypes as C
+import itertools
 
 import numpy as np
 import pandas as pd
@@ -39,6 +40,47 @@ def optimize_dtypes(df: pd.DataFrame) -> pd.DataFrame:
         df[col] = df[col].astype("float32")
     for col in df.select_dtypes(include=["int64"]).columns:
         df[col] = df[col].astype("int32")
+    if "ts_code" in df.columns:
+        df["ts_code"] = df["ts_code"].astype("category")
+    return df
+
+
+def stream_collection(db, collection_name: str, query: dict | None = None,
+                      projection: dict | None = None, chunk_size: int = 500_000):
+    """Yield dtype-optimised DataFrames of at most ``chunk_size`` documents from one cursor.
+
+    Memory-bounded load pattern of ``Barra_database/database/datause.ipynb#c6`` (500k-document
+    chunks over the 6.6 M-row ``daily_prices``): only one chunk of Python dicts is alive at a
+    time; each chunk is downcast (float32/int32) before the next is read.
+    """
+    if chunk_size < 1:
+        raise ValueError("chunk_size must be >= 1")
+    cursor = db[collection_name].find(query or {}, projection)
+    if hasattr(cursor, "batch_size"):
+        cursor = cursor.batch_size(min(chunk_size, 100_000))
+    it = iter(cursor)
+    while True:
+        docs = list(itertools.islice(it, chunk_size))
+        if not docs:
+            return
+        df = pd.DataFrame(docs)
+        del docs
+        if "_id" in df.columns:
+            df = df.drop(columns="_id")
+        yield optimize_dtypes(df)
+
+
+def load_collection_chunked(db, collection_name: str, query: dict | None = None,
+                            projection: dict | None = None, chunk_size: int = 500_000) -> pd.DataFrame:
+    """Concatenate :func:`stream_collection` chunks; ``ts_code`` ends as one categorical."""
+    parts = list(stream_collection(db, collection_name, query, projection, chunk_size))
+    if not parts:
+        return pd.DataFrame()
+    for p in parts:
+        if "ts_code" in p.columns:
+            p["ts_code"] = p["ts_code"].astype(str)
+    df = pd.concat(parts, ignore_index=True)
+    del parts
     if "ts_code" in df.columns:
         df["ts_code"] = df["ts_code"].astype("category")
     return df

@@ -173,3 +173,20 @@ def test_mongo_driven_risk_run_matches_csv_path(tmp_path):
     torch.testing.assert_close(pm.styles, pc.styles, equal_nan=True)
     torch.testing.assert_close(pm.ret, pc.ret, equal_nan=True)
     assert torch.equal(pm.ind, pc.ind)
+
+
+def test_chunked_collection_stream_matches_single_load():
+    """datause.ipynb#c6 memory-bounded cursor streaming: same frame as one list() load."""
+    from barra_factor_cal.load_data import load_collection_to_df
+    db = FakeDB()
+    rng = np.random.default_rng(5)
+    db["daily_prices"].insert_many([{"ts_code": f"{i % 13:06d}.SZ", "trade_date": f"2020{i % 12 + 1:02d}01",
+                                     "close": float(rng.random()), "vol": int(i)} for i in range(1037)])
+    proj = {"_id": 0, "ts_code": 1, "trade_date": 1, "close": 1, "vol": 1}
+    with contextlib.redirect_stdout(io.StringIO()):
+        whole = load_collection_to_df(db, "daily_prices", {}, proj)
+        chunked = load_collection_to_df(db, "daily_prices", {}, proj, chunk_size=100)
+    sizes = [len(c) for c in pit.stream_collection(db, "daily_prices", {}, proj, chunk_size=100)]
+    assert sizes == [100] * 10 + [37]
+    assert chunked["ts_code"].dtype.name == "category" and chunked["close"].dtype == np.float32
+    pd.testing.assert_frame_equal(whole.astype({"ts_code": str}), chunked.astype({"ts_code": str}))
