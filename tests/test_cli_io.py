@@ -120,3 +120,25 @@ def test_native_matrix_csv_writer_matches_pandas(tmp_path):
     pd.DataFrame(v, index=idx, columns=cols).to_csv(b)
     assert open(a).read() == open(b).read()
     assert not native_io.write_matrix_csv(a, v, idx.strftime("%Y-%m-%d"), ["a,b"] + cols[1:])
+
+
+def test_upstream_barra_data1_schema(tmp_path):
+    """Original upstream dataset schema (Barra-master/dda_0921.ipynb#c1-c2: data/Barra_data1.csv,
+    same 15 columns, ``HY00x`` industry codes): the loader is code-agnostic, so relabelling the
+    industries and re-reading gives the same panel through both the native and pandas readers."""
+    from llm_driven_multi_factor_model_amd.utils.io import panel_from_barra_csv
+    d = str(tmp_path)
+    assert _run("synth", "--out", d, "--dates", "15", "--stocks", "40", "--industries", "4").returncode == 0
+    df = pd.read_csv(f"{d}/barra_data_csi.csv")
+    info = pd.read_csv(f"{d}/industry_info.csv")
+    relabel = {c: f"HY{i + 1:03d}" for i, c in enumerate(info["code"])}
+    df["industry"] = df["industry"].map(relabel)
+    info["code"] = info["code"].map(relabel)
+    df.to_csv(f"{d}/Barra_data1.csv", index=False)
+    info.to_csv(f"{d}/industry_info_hy.csv", index=False)
+    a = panel_from_barra_csv(f"{d}/barra_data_csi.csv", f"{d}/industry_info.csv")
+    b = panel_from_barra_csv(f"{d}/Barra_data1.csv", f"{d}/industry_info_hy.csv")
+    import torch
+    for k in ["styles", "cap", "ret", "ind"]:
+        torch.testing.assert_close(getattr(a, k), getattr(b, k), equal_nan=True)
+    assert b.P == 4 and list(a.stocks) == list(b.stocks)
