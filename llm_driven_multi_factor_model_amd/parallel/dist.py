@@ -14,11 +14,17 @@ Collective call sites:
   C9 stock-sharded (TP) CS-WLS all_reduce   (D x msize moments, then D x 5 R^2 sums;
                                              ops/xs_sharded.py)
 Backend ``nccl`` is RCCL on ROCm builds; ``gloo`` serves CPU tests.
+
+Failure detection: every process group gets a collective timeout
+(``MFA_DIST_TIMEOUT_S``, default 600 s) and RCCL async error handling is on, so a dead or hung
+rank turns into an exception on the others (fail fast; single node, no elastic restart) instead
+of a silent hang.
 """
 from __future__ import annotations
 
 import os
 from dataclasses import dataclass
+from datetime import timedelta
 
 import torch
 import torch.distributed as dist
@@ -53,10 +59,16 @@ def init_distributed(backend: str | None = None, device: str | None = None) -> D
     be = backend or ("nccl" if use_cuda else "gloo")
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         kw = {"device_id": dev} if use_cuda else {}
-        dist.init_process_group(be, rank=rank, world_size=world, **kw)
+        dist.init_process_group(be, rank=rank, world_size=world, timeout=collective_timeout(), **kw)
     _CTX = DistContext(rank, world, local, dev, be if world > 1 else None)
     return _CTX
+
+
+def collective_timeout() -> timedelta:
+    """Per-collective timeout of the process group (``MFA_DIST_TIMEOUT_S``, default 600 s)."""
+    return timedelta(seconds=float(os.environ.get("MFA_DIST_TIMEOUT_S", "600")))
 
 
 def context() -> DistContext:

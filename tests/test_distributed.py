@@ -85,3 +85,34 @@ def test_sharded_eigen_equals_unsharded_cpu():
     torch.testing.assert_close(torch.cat([eigen.mc_cov(4, 6, 50, 9, "cpu"),
                                           eigen.mc_cov(6, 6, 50, 9, "cpu", m0=4)]),
                                eigen.mc_cov(10, 6, 50, 9, "cpu"), rtol=0, atol=0)
+
+
+def _hang_worker(rank, world, port, out_path):
+    import time
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MFA_DIST_TIMEOUT_S="3")
+    from llm_driven_multi_factor_model_amd.parallel import dist as pdist
+    ctx = pdist.init_distributed(device="cpu")
+    if ctx.rank == 1:      # a rank that stops participating (hung / dead)
+        time.sleep(8)
+        return
+    t0 = time.time()
+    try:
+        pdist.all_reduce_sum(torch.ones(4), ctx)
+        msg = "no error"
+    except Exception as e:  # noqa: BLE001
+        msg = type(e).__name__
+    with open(out_path, "w") as f:
+        f.write(f"{msg} {time.time() - t0:.1f}")
+
+
+def test_hung_rank_fails_fast_with_collective_timeout():
+    """Failure detection: with MFA_DIST_TIMEOUT_S=3 a collective whose peer never joins raises
+    on the waiting rank after ~3 s instead of hanging."""
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "hang.txt")
+        mp.start_processes(_hang_worker, args=(2, _free_port(), path), nprocs=2, join=True,
+                           start_method="spawn")
+        msg, secs = open(path).read().split()
+    assert msg != "no error"
+    assert float(secs) < 8.0
