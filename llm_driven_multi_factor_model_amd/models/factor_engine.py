@@ -253,6 +253,9 @@ class FactorEngine:
         np.unique, a 4-row rolling sum per stock on the device, gathered back by the inverse
         index.  None when one (stock, end_date) carries several values (the merge path's row
         multiplication is then kept by :meth:`_ttm_by_merge`)."""
+        runs = self._ttm_runs(m)
+        if runs is not None:
+            return runs
         ecodes, _ = pd.factorize(m["end_date"], sort=True)
         ne = int(ecodes.max()) + 1 if len(ecodes) else 0
         sc = self.stock_id.cpu().numpy().astype(np.int64)
@@ -264,6 +267,36 @@ class FactorEngine:
         if not same.all():
             return None
         seg = RL.seg_lo_from_codes(torch.from_numpy(uk // (ne + 1))).to(self.device)
+        ttm = RL.rolling_sum(torch.from_numpy(vf.astype(np.float32)).to(self.device), seg, 4, 4)
+        return ttm.double()[torch.from_numpy(inv).to(self.device)]
+
+    def _ttm_runs(self, m: pd.DataFrame):
+        """O(n) fast path of :meth:`_ttm_by_codes`: the master frame is sorted by (stock,
+        trade_date) and a point-in-time as-of join makes end_date non-decreasing within a stock,
+        so the distinct (stock, end_date) rows are the RUN STARTS of the row order — no sort, no
+        factorize.  None (caller falls back) when the order does not hold, e.g. a restatement
+        that moves end_date backwards, or when a run carries several values."""
+        ed = m["end_date"]
+        if not np.issubdtype(ed.dtype, np.datetime64) or len(ed) == 0:
+            return None
+        ev = ed.to_numpy("datetime64[ns]").view(np.int64).copy()
+        ev[ed.isna().to_numpy()] = np.iinfo(np.int64).max  # NaT last, as sort_values
+        sc = self.stock_id.cpu().numpy().astype(np.int64)
+        ds, de = np.diff(sc), np.diff(ev)
+        if (ds < 0).any() or ((ds == 0) & (de < 0)).any():
+            return None
+        start = np.empty(len(ev), dtype=bool)
+        start[0] = True
+        np.not_equal(sc[1:], sc[:-1], out=start[1:])
+        start[1:] |= de != 0
+        first = np.flatnonzero(start)
+        inv = np.cumsum(start) - 1
+        v = m["n_cashflow_act"].to_numpy(np.float64, na_value=np.nan)
+        vf = v[first]
+        same = (v == vf[inv]) | (np.isnan(v) & np.isnan(vf[inv]))
+        if not same.all():
+            return None
+        seg = RL.seg_lo_from_codes(torch.from_numpy(sc[first])).to(self.device)
         ttm = RL.rolling_sum(torch.from_numpy(vf.astype(np.float32)).to(self.device), seg, 4, 4)
         return ttm.double()[torch.from_numpy(inv).to(self.device)]
 

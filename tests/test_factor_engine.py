@@ -162,3 +162,24 @@ def test_cetop_ttm_code_path_equals_merge_path():
     a, b = eng._ttm_by_codes(eng.master), eng._ttm_by_merge(eng.master)
     assert a is not None and int(torch.isfinite(a).sum()) > 1000
     torch.testing.assert_close(a, b, rtol=0, atol=0, equal_nan=True)
+
+
+def test_cetop_ttm_run_path_equals_merge_path_and_falls_back():
+    """O(n) run-start TTM (end_date non-decreasing within each stock after the PIT join) equals
+    the merge path; a restatement that moves end_date backwards disables it (fallback)."""
+    prices, index, _ = FE.synthetic_prices(N=50, T=400, seed=4, suspend_frac=0.05)
+    ed = prices["end_date"].unique()
+    prices.loc[prices.end_date.isin(ed[::4]) & (prices.ts_code < "000020"), "n_cashflow_act"] = np.nan
+    eng = FE.FactorEngine(prices, index, device="cpu")
+    a = eng._ttm_runs(eng.master)
+    assert a is not None and int(torch.isfinite(a).sum()) > 1000
+    torch.testing.assert_close(a, eng._ttm_by_merge(eng.master), rtol=0, atol=0, equal_nan=True)
+    code = prices.ts_code.iloc[0]
+    rows = prices.index[prices.ts_code == code]
+    prices.loc[rows[-5:], "end_date"] = prices.loc[rows[0], "end_date"]   # backwards restatement
+    eng2 = FE.FactorEngine(prices, index, device="cpu")
+    assert eng2._ttm_runs(eng2.master) is None
+    b = eng2._ttm_by_codes(eng2.master)
+    if b is None:
+        b = eng2._ttm_by_merge(eng2.master)
+    torch.testing.assert_close(b, eng2._ttm_by_merge(eng2.master), rtol=0, atol=0, equal_nan=True)
