@@ -281,24 +281,26 @@ class FactorEngine:
             return None
         ev = ed.to_numpy("datetime64[ns]").view(np.int64).copy()
         ev[ed.isna().to_numpy()] = np.iinfo(np.int64).max  # NaT last, as sort_values
-        sc = self.stock_id.cpu().numpy().astype(np.int64)
-        ds, de = np.diff(sc), np.diff(ev)
-        if (ds < 0).any() or ((ds == 0) & (de < 0)).any():
+        dev = self.device
+        # the run detection, dedupe and gather run as device tensor ops (one sync: nonzero)
+        e = torch.from_numpy(ev).to(dev)
+        sc = self.stock_id.to(dev, torch.int64)
+        ds, de = sc[1:] - sc[:-1], e[1:] - e[:-1]
+        start = torch.ones(len(ev), dtype=torch.bool, device=dev)
+        start[1:] = (ds != 0) | (de != 0)
+        bad = (ds < 0) | ((ds == 0) & (de < 0))
+        first = torch.nonzero(start).flatten()
+        if bool(bad.any()):
             return None
-        start = np.empty(len(ev), dtype=bool)
-        start[0] = True
-        np.not_equal(sc[1:], sc[:-1], out=start[1:])
-        start[1:] |= de != 0
-        first = np.flatnonzero(start)
-        inv = np.cumsum(start) - 1
-        v = m["n_cashflow_act"].to_numpy(np.float64, na_value=np.nan)
+        inv = torch.cumsum(start, 0) - 1
+        v = torch.from_numpy(m["n_cashflow_act"].to_numpy(np.float64, na_value=np.nan)).to(dev)
         vf = v[first]
-        same = (v == vf[inv]) | (np.isnan(v) & np.isnan(vf[inv]))
-        if not same.all():
+        vb = vf[inv]
+        if not bool(((v == vb) | (v.isnan() & vb.isnan())).all()):
             return None
-        seg = RL.seg_lo_from_codes(torch.from_numpy(sc[first])).to(self.device)
-        ttm = RL.rolling_sum(torch.from_numpy(vf.astype(np.float32)).to(self.device), seg, 4, 4)
-        return ttm.double()[torch.from_numpy(inv).to(self.device)]
+        seg = RL.seg_lo_from_codes(sc[first].to(torch.int32))
+        ttm = RL.rolling_sum(vf.float(), seg, 4, 4)
+        return ttm.double()[inv]
 
     def _ttm_by_merge(self, m: pd.DataFrame):
         fin = m[["ts_code", "end_date", "n_cashflow_act"]].drop_duplicates().copy()
