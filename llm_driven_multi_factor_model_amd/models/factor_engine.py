@@ -379,9 +379,16 @@ class _Grid:
     def __init__(self, df: pd.DataFrame, device):
         self.device = device
         dcodes, self.dates = pd.factorize(df["trade_date"], sort=True)
-        if "ts_code" in df.columns and not df.duplicated(["trade_date", "ts_code"]).any():
+        scodes = None
+        if "ts_code" in df.columns:
             scodes, self.stocks = pd.factorize(df["ts_code"].astype(str), sort=True)
-        else:  # no stock key (or duplicates): the row's rank within its date is its column
+            # frames in master order (ts_code, trade_date) are duplicate-free iff this key is
+            # strictly increasing: an O(n) check instead of DataFrame.duplicated's hashing
+            k = scodes.astype(np.int64) * (len(self.dates) + 1) + dcodes
+            if not (len(k) < 2 or bool((k[1:] > k[:-1]).all())) and \
+                    df.duplicated(["trade_date", "ts_code"]).any():
+                scodes = None
+        if scodes is None:  # no stock key (or duplicates): the row's rank within its date is its column
             scodes = df.groupby("trade_date").cumcount().to_numpy()
             self.stocks = np.arange(int(scodes.max()) + 1 if len(scodes) else 0)
         self.D, self.N = len(self.dates), len(self.stocks)
