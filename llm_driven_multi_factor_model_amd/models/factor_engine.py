@@ -452,7 +452,10 @@ def _next_in_group(keys: pd.Series, values: np.ndarray) -> np.ndarray:
     """``values`` shifted by -1 within groups of ``keys`` in frame order (groupby().shift(-1));
     NaN keys are their own non-group (pandas dropna) and get NaN."""
     codes = pd.factorize(keys)[0]
-    order = np.argsort(codes, kind="stable")
+    if len(codes) < 2 or bool((codes[1:] >= codes[:-1]).all()):
+        order = np.arange(len(codes))  # frame already grouped (master order): no sort
+    else:
+        order = np.argsort(codes, kind="stable")
     out = np.full(len(values), np.nan)
     same = codes[order[1:]] == codes[order[:-1]]
     nxt = np.where(same, values[order[1:]], np.nan)
@@ -487,7 +490,7 @@ def barra_export(processed: pd.DataFrame, sw_industry: pd.DataFrame, _merge_path
         barra["ret"] = barra.groupby("ts_code")["ret"].shift(-1)
         barra = barra.rename(columns=BARRA_RENAME)
         final = barra[[c for c in BARRA_OUTPUT_COLUMNS if c in barra.columns]]
-    stk = final[["stocknames"]].drop_duplicates().rename(columns={"stocknames": "ts_code"})
+    stk = pd.DataFrame({"ts_code": pd.unique(final["stocknames"].to_numpy())})  # first-seen order
     cols = [c for c in ["ts_code", "l1_code", "l1_name", "in_date"] if c in sw_industry.columns]
     info = stk.merge(sw_industry[cols], on="ts_code", how="left")
     info = info.drop_duplicates(subset=[c for c in ["l1_code", "l1_name"] if c in info.columns]).rename(
