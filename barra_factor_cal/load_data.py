@@ -39,9 +39,10 @@ def load_collection_to_df(db, collection_name: str, query: dict, projection: dic
 def load_and_prepare_data(db=None, index_code: str = "000016.SH", start_date: str = "20200101",
                           start_date_financial: str = "20190101", end_date: str | None = None,
                           fix_fill_order: bool = False, dedupe_indicators: bool = True,
-                          fill: bool = True):
+                          fill: bool = True, asof_device: str | None = None):
     """``dedupe_indicators`` / ``fill`` = False reproduce the earlier script
-    ``load_data_v0.py`` (no ann_date dedupe of financial indicators, no ffill/fill step)."""
+    ``load_data_v0.py`` (no ann_date dedupe of financial indicators, no ffill/fill step).
+    ``asof_device="cuda"`` runs the three as-of joins' index search on the GPU (``csrc/asof.hip``)."""
     client = None
     if db is None:
         from pymongo import MongoClient
@@ -84,11 +85,11 @@ def load_and_prepare_data(db=None, index_code: str = "000016.SH", start_date: st
     px["trade_date"] = pd.to_datetime(px["trade_date"].astype(str), format="%Y%m%d")
     ix = ix.copy()
     ix["trade_date"] = pd.to_datetime(ix["trade_date"].astype(str), format="%Y%m%d")
-    m1 = robust_merge_asof(px, bs, "trade_date", "f_ann_date", "ts_code").rename(
+    m1 = robust_merge_asof(px, bs, "trade_date", "f_ann_date", "ts_code", device=asof_device).rename(
         columns={"f_ann_date": "balance_sheet_f_ann_date"})
-    m2 = robust_merge_asof(m1, fi, "trade_date", "ann_date", "ts_code").rename(
+    m2 = robust_merge_asof(m1, fi, "trade_date", "ann_date", "ts_code", device=asof_device).rename(
         columns={"ann_date": "financial_indicators_ann_date"})
-    m3 = robust_merge_asof(m2, cf, "trade_date", "f_ann_date", "ts_code").rename(
+    m3 = robust_merge_asof(m2, cf, "trade_date", "f_ann_date", "ts_code", device=asof_device).rename(
         columns={"f_ann_date": "cashflow_f_ann_date"})
     m3 = m3.drop(columns=[c for c in ["end_date_y", "end_date_x"] if c in m3.columns])
     out = fill_missing(m3, fix_order=fix_fill_order) if fill else m3

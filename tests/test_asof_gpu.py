@@ -80,3 +80,17 @@ def test_gpu_robust_merge_asof_matches_host():
     a = pit.robust_merge_asof(px, st, "trade_date", "f_ann_date", "ts_code")
     b = pit.robust_merge_asof(px, st, "trade_date", "f_ann_date", "ts_code", device="cuda:0")
     pd.testing.assert_frame_equal(a, b)
+
+
+@pytest.mark.gpu
+def test_load_and_prepare_data_gpu_asof_equals_host():
+    """load_data.py flow (three chained as-of merges) with the HIP join equals the host join."""
+    import contextlib
+    import io
+    from barra_factor_cal import load_data
+    from tests.test_ingest_pit import _seed_db
+    with contextlib.redirect_stdout(io.StringIO()):
+        a = load_data.load_and_prepare_data(_seed_db(), end_date="20201231")
+        b = load_data.load_and_prepare_data(_seed_db(), end_date="20201231", asof_device="cuda:0")
+    for x, y in zip(a, b):
+        pd.testing.assert_frame_equal(x, y)
