@@ -7,6 +7,8 @@ built from the device results at the end of each stage.
 """
 from __future__ import annotations
 
+from collections.abc import MutableSequence
+
 import numpy as np
 import pandas as pd
 import torch
@@ -16,6 +18,66 @@ from llm_driven_multi_factor_model_amd.utils.config import RiskConfig
 from llm_driven_multi_factor_model_amd.utils.io import panel_from_frame
 
 from ._device import device as _device, verbose as _verbose
+
+
+class SpecificReturns(MutableSequence):
+    """``MFM.reg_by_time``'s list of per-date ``DataFrame[1, N_t]`` (MFM.py:66), built lazily.
+
+    Materialising thousands of one-row frames costs more than the whole GPU regression
+    (SURVEY.md §7.3 item 7), so the frames are created on first access from the dense [T, N]
+    residual matrix and cached.  It behaves as a list (len, index, slice, iteration, append,
+    ``pd.concat``, ``==`` with a list); :meth:`dense` returns the [T, N] frame directly.
+    """
+
+    def __init__(self, E: np.ndarray, valid: np.ndarray, stocks: np.ndarray, dates):
+        self._E, self._valid, self._stocks, self._dates = E, valid, stocks, dates
+        self._items: list = [None] * len(E)
+
+    def _build(self, t: int) -> pd.DataFrame:
+        v = self._valid[t]
+        return pd.DataFrame([self._E[t][v].astype(np.float64)], columns=list(self._stocks[v]),
+                            index=[self._dates[t]])
+
+    def __len__(self) -> int:
+        return len(self._items)
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        if i < 0:
+            i += len(self)
+        if not 0 <= i < len(self):
+            raise IndexError("list index out of range")
+        if self._items[i] is None:
+            self._items[i] = self._build(i)
+        return self._items[i]
+
+    def __setitem__(self, i, value):
+        if isinstance(i, slice):
+            for j in range(*i.indices(len(self))):
+                self[j]  # materialise the rest of the slice before replacing it
+        self._items[i] = value
+
+    def __delitem__(self, i):
+        for j in range(len(self)):
+            self[j]
+        del self._items[i]
+
+    def insert(self, i, value):
+        for j in range(len(self)):
+            self[j]
+        self._items.insert(i, value)
+
+    def __eq__(self, other):
+        return list(self) == list(other)
+
+    def __repr__(self) -> str:
+        return f"SpecificReturns({len(self)} dates, lazily materialised)"
+
+    def dense(self) -> pd.DataFrame:
+        """[T, N] specific returns (NaN where a stock is absent) without per-date frames."""
+        E = np.where(self._valid, self._E, np.nan).astype(np.float64)
+        return pd.DataFrame(E, index=self._dates, columns=list(self._stocks))
 
 
 class MFM:
@@ -62,11 +124,7 @@ class MFM:
         E = e.cpu().numpy()
         valid = m.panel.valid().cpu().numpy()
         stocks = np.asarray(m.panel.stocks)
-        self.specific_ret = [
-            pd.DataFrame([E[t][valid[t]].astype(np.float64)], columns=list(stocks[valid[t]]),
-                         index=[self.sorted_dates[t]])
-            for t in range(self.T)
-        ]
+        self.specific_ret = SpecificReturns(E, valid, stocks, self.sorted_dates)
         last = valid[-1]
         self.last_capital = m.panel.cap[-1].cpu().numpy()[last].astype(np.float64)
         return self.factor_ret, self.specific_ret, self.R2

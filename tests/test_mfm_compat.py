@@ -157,3 +157,28 @@ def test_mfm_gpu_matches_cpu(cuda, monkeypatch):
     np.testing.assert_allclose(rg.values, rc.values, rtol=1e-9, atol=1e-12)
     for a, b in zip(ng[-5:], nc[-5:]):
         np.testing.assert_allclose(a.values, b.values, rtol=1e-9, atol=1e-15)
+
+
+def test_specific_returns_lazy_list_semantics(monkeypatch):
+    """reg_by_time's specific returns are built lazily but behave as the reference's list of
+    one-row DataFrames (len / index / negative index / slice / iteration / pd.concat)."""
+    monkeypatch.setenv("MFA_DEVICE", "cpu")
+    df = toy_frame(T=12, N=20, P=3, Q=2, seed=5)
+    with contextlib.redirect_stdout(io.StringIO()):
+        m = mfm.MFM(df, 3, 2)
+        f, e, r2 = m.reg_by_time()
+    assert len(e) == 12 and all(x is None for x in e._items)
+    first = e[0]
+    assert first.shape[0] == 1 and first.index[0] == f.index[0] and e[0] is first
+    assert e[-1].index[0] == f.index[-1]
+    assert [x.index[0] for x in e[2:5]] == list(f.index[2:5])
+    cat = pd.concat(list(e))
+    assert cat.shape[0] == 12
+    dense = e.dense()
+    for t in (0, 7, 11):
+        row = e[t].iloc[0]
+        np.testing.assert_array_equal(row.values, dense.loc[e[t].index[0], row.index].values)
+    e.append(e[0])
+    assert len(e) == 13
+    with pytest.raises(IndexError):
+        e[20]
