@@ -20,23 +20,23 @@ from llm_driven_multi_factor_model_amd.utils.io import panel_from_frame
 from ._device import device as _device, verbose as _verbose
 
 
-class SpecificReturns(MutableSequence):
-    """``MFM.reg_by_time``'s list of per-date ``DataFrame[1, N_t]`` (MFM.py:66), built lazily.
+class LazyFrames(MutableSequence):
+    """A list of per-date pandas objects built on first access.
 
-    Materialising thousands of one-row frames costs more than the whole GPU regression
-    (SURVEY.md §7.3 item 7), so the frames are created on first access from the dense [T, N]
-    residual matrix and cached.  It behaves as a list (len, index, slice, iteration, append,
-    ``pd.concat``, ``==`` with a list); :meth:`dense` returns the [T, N] frame directly.
+    ``MFM``'s stages return Python lists of thousands of small DataFrames (MFM.py:66, :92-98,
+    :117-123, :156-166); materialising them costs more than the batched GPU stage itself.  This
+    sequence holds a builder and the dense device results instead, creates item t when it is
+    first read and caches it.  It behaves as a list: len, index, negative index, slice,
+    iteration, append / insert / del, ``pd.concat`` and ``==`` with a list.
     """
 
-    def __init__(self, E: np.ndarray, valid: np.ndarray, stocks: np.ndarray, dates):
-        self._E, self._valid, self._stocks, self._dates = E, valid, stocks, dates
-        self._items: list = [None] * len(E)
+    def __init__(self, n: int, builder):
+        self._build = builder
+        self._items: list = [None] * n
 
-    def _build(self, t: int) -> pd.DataFrame:
-        v = self._valid[t]
-        return pd.DataFrame([self._E[t][v].astype(np.float64)], columns=list(self._stocks[v]),
-                            index=[self._dates[t]])
+    def _all(self):
+        for j in range(len(self._items)):
+            self[j]
 
     def __len__(self) -> int:
         return len(self._items)
@@ -54,25 +54,36 @@ class SpecificReturns(MutableSequence):
 
     def __setitem__(self, i, value):
         if isinstance(i, slice):
-            for j in range(*i.indices(len(self))):
-                self[j]  # materialise the rest of the slice before replacing it
+            self._all()  # materialise before a structural replace
         self._items[i] = value
 
     def __delitem__(self, i):
-        for j in range(len(self)):
-            self[j]
+        self._all()
         del self._items[i]
 
     def insert(self, i, value):
-        for j in range(len(self)):
-            self[j]
+        self._all()
         self._items.insert(i, value)
 
     def __eq__(self, other):
         return list(self) == list(other)
 
     def __repr__(self) -> str:
-        return f"SpecificReturns({len(self)} dates, lazily materialised)"
+        done = sum(x is not None for x in self._items)
+        return f"{type(self).__name__}({len(self)} items, {done} materialised)"
+
+
+class SpecificReturns(LazyFrames):
+    """``reg_by_time``'s per-date ``DataFrame[1, N_t]`` list; :meth:`dense` gives [T, N] directly."""
+
+    def __init__(self, E: np.ndarray, valid: np.ndarray, stocks: np.ndarray, dates):
+        self._E, self._valid, self._stocks, self._dates = E, valid, stocks, dates
+        super().__init__(len(E), self._frame)
+
+    def _frame(self, t: int) -> pd.DataFrame:
+        v = self._valid[t]
+        return pd.DataFrame([self._E[t][v].astype(np.float64)], columns=list(self._stocks[v]),
+                            index=[self._dates[t]])
 
     def dense(self) -> pd.DataFrame:
         """[T, N] specific returns (NaN where a stock is absent) without per-date frames."""
@@ -129,15 +140,12 @@ class MFM:
         self.last_capital = m.panel.cap[-1].cpu().numpy()[last].astype(np.float64)
         return self.factor_ret, self.specific_ret, self.R2
 
-    def _cov_list(self, V: torch.Tensor):
+    def _cov_list(self, V: torch.Tensor) -> LazyFrames:
         Vn = V.cpu().numpy()
-        out = []
-        for t in range(Vn.shape[0]):
-            if np.isnan(Vn[t]).any():
-                out.append(pd.DataFrame())
-            else:
-                out.append(pd.DataFrame(Vn[t], columns=self.columns, index=self.columns))
-        return out
+        bad = np.isnan(Vn).any(axis=(1, 2))
+        cols = self.columns
+        return LazyFrames(Vn.shape[0], lambda t: pd.DataFrame() if bad[t] else
+                          pd.DataFrame(Vn[t], columns=cols, index=cols))
 
     def Newey_West_by_time(self, q=2, tao=252):
         if self.factor_ret is None:
@@ -162,10 +170,13 @@ class MFM:
                             "eigenfactor risk adjustment first")
         self._banner("逐时间点进行Volatility Regime调整")
         V, lam = self._model.vol_regime_adjust(tao)
-        Vn = V.cpu().numpy()
-        out = []
-        for t in range(self.T):
-            er = self.eigen_risk_adj_cov[t]
-            out.append(er * float(lam[t]) ** 2 if not er.empty else er)
+        lam_h = [float(x) for x in lam.cpu().numpy()]
+        er_list = self.eigen_risk_adj_cov
+
+        def vra(t):
+            er = er_list[t]
+            return er * lam_h[t] ** 2 if not er.empty else er
+
+        out = LazyFrames(self.T, vra)
         self.vol_regime_adj_cov = out
-        return out, [float(x) for x in lam.cpu().numpy()]
+        return out, lam_h
