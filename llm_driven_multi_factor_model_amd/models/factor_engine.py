@@ -130,7 +130,9 @@ class FactorEngine:
             if c in master.columns:
                 self.cols[c] = torch.from_numpy(master[c].to_numpy(dtype=np.float32, na_value=np.nan)).to(dev)
         self.cols["ret"], self.cols["log_ret"] = RL.returns(self.cols["close"], self.seg_lo)
-        if not master["ts_code"].is_monotonic_increasing:
+        # sorted by construction on the lexsort path (codes are sort=True factorize ranks);
+        # only the merge path needs the O(n) string comparison
+        if len(master) != len(p) and not master["ts_code"].is_monotonic_increasing:
             raise AssertionError("master frame must be sorted by ts_code")
         return master
 
