@@ -1,20 +1,26 @@
 // Expanding-window exponentially-weighted Newey-West covariance series as a blocked scan (K8),
 // plus the decayed prefix mean used by the volatility-regime adjustment (K10).
 //
-// Reference: Barra-master/mfm/utils.py:16-50 (Newey_West on one prefix) called for EVERY
-// prefix f[:t], t = 1..T, by MFM.Newey_West_by_time (MFM.py:80-101): O(T^2 K^2) Python.
+// Reference: Barra-master/mfm/utils.py:16-50 (Newey_West on one prefix, any lag count q < T)
+// called for EVERY prefix f[:t], t = 1..T, by MFM.Newey_West_by_time (MFM.py:80-101):
+// O(T^2 K^2) Python.
 //
-// Here every prefix is produced in O(T K^2) from decayed moments (lambda = 0.5^(1/tau)):
-//   Z   = sum_u l^(n-1-u)              m  = sum_u l^(n-1-u) f_u       S0 = sum_u l^(n-1-u) f_u f_u^T
-//   A_i = sum_{u>=i} l^(n-1-u) f_{u-i} f_u^T   a_i = sum_{u>=i} l^(n-1-u) f_{u-i}
-//   b_i = sum_{u>=i} l^(n-1-u) f_u             z_i = sum_{u>=i} l^(n-1-u)
-//   mu = m/Z,  G0 = S0/Z - mu mu^T,  Gi = (A_i - a_i mu^T - mu b_i^T + z_i mu mu^T)/Z
-//   V  = G0 + sum_i (1 - i/(q+1)) (Gi + Gi^T)
-// Work decomposition: thread = one (k,l) output entry, which carries its own scalar copy of
-// every moment it needs (18 fp64 at q = 2); dates are cut into chunks of CH rows:
-//   pass A  chunk-local decayed sums      grid (chunks, ceil(K^2/256))
-//   pass B  exclusive scan of chunk carries (sequential over chunks, parallel over moments)
-//   pass C  re-scan each chunk from its carry and write V_t      grid (out chunks, ...)
+// Here every prefix is produced in O(T K^2 q) from decayed moments (l = 0.5^(1/tau)); with
+// n = u + 1 the prefix length at date u and M[u] = sum_{s<=u} l^(u-s) f_s the decayed sum series:
+//   Z(n) = (1 - l^n) / (1 - l)                          mu = M[u] / Z(n)
+//   S0   = sum_s l^(u-s) f_s f_s^T                        G0 = S0 / Z - mu mu^T
+//   A_i  = sum_{s>=i} l^(u-s) f_{s-i} f_s^T               a_i = M[u-i]
+//   b_i  = M[u] - l^(u+1-i) M[i-1]                        z_i = Z(n-i)
+//   G_i  = (A_i - a_i mu^T - mu b_i^T + z_i mu mu^T) / Z
+//   V    = G0 + sum_{i=1..q} (1 - i/(q+1)) (G_i + G_i^T)
+// Only S0 and the A_i are carried per (k,l) entry (1 + 2q fp64); the lag-shifted sums a_i, b_i,
+// z_i come from the K-vector series M (one small scan) and Z's closed form.  Lags are processed
+// in groups of at most G per launch triple, each group ADDING its terms to V, so q is limited
+// only by the LDS rows [t0 - q, t1) of a chunk, never by registers.
+// Work decomposition: thread = one (k,l) output entry; dates are cut into chunks of CH rows:
+//   pass A  chunk-local decayed sums                 grid (chunks, ceil(K^2/256))
+//   pass B  exclusive scan of chunk carries          sequential over chunks, parallel over moments
+//   pass C  re-scan each chunk from its carry and write / accumulate V_t
 // The output range [t_lo, t_hi) lets each data-parallel rank emit only its own date shard.
 #include "common.h"
 
@@ -22,137 +28,188 @@ namespace {
 
 using namespace mfa;
 
-constexpr int CH = 32;        // dates per chunk
-constexpr int MAXQ = 4;       // max Newey-West lag
-constexpr int NSTATE = 2 + 7 * MAXQ + 4;  // per-thread moment count (upper bound)
+constexpr int CH = 32;  // dates per chunk
+constexpr int G = 8;    // lags per launch group (register state: 1 + 2G fp64 per thread)
 
-// state layout per thread (k,l):
-//   0 Z | 1 S0 | 2 mk | 3 ml | then per lag i (0-based ii): A_kl, A_lk, a_k, a_l, b_k, b_l, z
 struct NwDims {
-  int T, K, q;
+  int T, K, q;      // series length, factors, total lag count (weights 1 - i/(q+1))
+  int i0, i1;       // this launch's lag group [i0, i1), 1-based lags
   double lam;
 };
 
-__device__ __forceinline__ int st_idx(int ii, int w) { return 4 + ii * 7 + w; }
-
-template <bool STAGE_OUT>
-__device__ void nw_run_chunk(const double* __restrict__ Fs,  // LDS rows [t0-q, t1)
-                             int t0, int t1, int k, int l, const NwDims& dm, double* s,
-                             double* __restrict__ V, int t_lo, int t_hi, int qoff) {
-  const int K = dm.K, q = dm.q;
-  const double lam = dm.lam;
-  for (int u = t0; u < t1; ++u) {
-    const double* fu = Fs + (size_t)(u - t0 + qoff) * K;
-    const double fk = fu[k], fl = fu[l];
-    s[0] = fma(lam, s[0], 1.0);
-    s[1] = fma(lam, s[1], fk * fl);
-    s[2] = fma(lam, s[2], fk);
-    s[3] = fma(lam, s[3], fl);
-#pragma unroll
-    for (int ii = 0; ii < MAXQ; ++ii) {
-      if (ii >= q) break;
-      const int i = ii + 1;
-      double* si = s + st_idx(ii, 0);
-      const bool has = u >= i;
-      const double gk = has ? Fs[(size_t)(u - i - t0 + qoff) * K + k] : 0.0;
-      const double gl = has ? Fs[(size_t)(u - i - t0 + qoff) * K + l] : 0.0;
-      si[0] = fma(lam, si[0], gk * fl);
-      si[1] = fma(lam, si[1], gl * fk);
-      si[2] = fma(lam, si[2], gk);
-      si[3] = fma(lam, si[3], gl);
-      si[4] = fma(lam, si[4], has ? fk : 0.0);
-      si[5] = fma(lam, si[5], has ? fl : 0.0);
-      si[6] = fma(lam, si[6], has ? 1.0 : 0.0);
-    }
-    if (STAGE_OUT && u >= t_lo && u < t_hi) {
-      const int n = u + 1;  // prefix length
-      double v;
-      if (n <= q || n <= K) {
-        v = qnan();
-      } else {
-        const double iz = 1.0 / s[0];
-        const double mk = s[2] * iz, ml = s[3] * iz;
-        v = s[1] * iz - mk * ml;
-#pragma unroll
-        for (int ii = 0; ii < MAXQ; ++ii) {
-          if (ii >= q) break;
-          const int i = ii + 1;
-          const double* si = s + st_idx(ii, 0);
-          // G_i[k][l] + G_i[l][k]
-          const double gkl = si[0] - si[2] * ml - mk * si[5] + si[6] * mk * ml;
-          const double glk = si[1] - si[3] * mk - ml * si[4] + si[6] * ml * mk;
-          v = fma(1.0 - (double)i / (q + 1), (gkl + glk) * iz, v);
-        }
-      }
-      V[(size_t)(u - t_lo) * K * K + (size_t)k * K + l] = v;
-    }
-  }
-}
-
-__device__ void stage_rows(const double* __restrict__ F, double* Fs, int t0, int t1, int q, int K) {
-  const int lo = t0 - q;
+// LDS image of a chunk: F rows [t0 - i1 + 1, t1) and M rows [t0 - i1 + 1, t1), then M rows
+// [0, i1 - 1) (the b_i boundary terms).  Rows before date 0 are zero.
+__device__ void stage_rows(const double* __restrict__ F, const double* __restrict__ M, double* Fs,
+                           double* Ms, double* M0, int t0, int t1, const NwDims& dm, bool want_m) {
+  const int K = dm.K;
+  const int lo = t0 - (dm.i1 - 1);
   const int rows = t1 - lo;
   for (int e = threadIdx.x; e < rows * K; e += blockDim.x) {
     const int r = e / K, c = e % K;
     const int t = lo + r;
     Fs[e] = t >= 0 ? F[(size_t)t * K + c] : 0.0;
+    if (want_m) Ms[e] = t >= 0 ? M[(size_t)t * K + c] : 0.0;
+  }
+  if (want_m)
+    for (int e = threadIdx.x; e < (dm.i1 - 1) * K; e += blockDim.x) {
+      const int t = e / K;
+      M0[e] = t < dm.T ? M[e] : 0.0;
+    }
+}
+
+// Advance the (k,l) state over dates [t0, t1).  s[0] = S0 (group 0 only), s[1 + 2g + {0,1}] =
+// A_{i0+g}[k][l], A_{i0+g}[l][k].  EMIT: write (or add) V for dates in [t_lo, t_hi).
+template <bool EMIT>
+__device__ void nw_run_chunk(const double* Fs, const double* Ms, const double* M0, int t0, int t1,
+                             int k, int l, const NwDims& dm, double (&s)[1 + 2 * G],
+                             double* __restrict__ V, int t_lo, int t_hi, bool add) {
+  const int K = dm.K, q = dm.q;
+  const int off = dm.i1 - 1;  // LDS row of date t0
+  const double lam = dm.lam;
+  const double il = 1.0 / (1.0 - lam);
+  const bool base = dm.i0 == 1;
+  for (int u = t0; u < t1; ++u) {
+    const int r = u - t0 + off;
+    const double fk = Fs[r * K + k], fl = Fs[r * K + l];
+    if (base) s[0] = fma(lam, s[0], fk * fl);
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const int i = dm.i0 + g;
+      if (i >= dm.i1) break;
+      const bool has = u >= i;
+      const double gk = has ? Fs[(r - i) * K + k] : 0.0;
+      const double gl = has ? Fs[(r - i) * K + l] : 0.0;
+      s[1 + 2 * g] = fma(lam, s[1 + 2 * g], gk * fl);
+      s[2 + 2 * g] = fma(lam, s[2 + 2 * g], gl * fk);
+    }
+    if (EMIT && u >= t_lo && u < t_hi) {
+      const int n = u + 1;  // prefix length
+      double* vo = V + (size_t)(u - t_lo) * K * K + (size_t)k * K + l;
+      if (n <= q || n <= K) {
+        if (base) *vo = qnan();
+        continue;
+      }
+      const double Z = (1.0 - pow(lam, (double)n)) * il;
+      const double iz = 1.0 / Z;
+      const double mk = Ms[r * K + k] * iz, ml = Ms[r * K + l] * iz;
+      double v = base ? s[0] * iz - mk * ml : 0.0;
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const int i = dm.i0 + g;
+        if (i >= dm.i1) break;
+        const double ak = Ms[(r - i) * K + k], al = Ms[(r - i) * K + l];  // a_i = M[u-i]
+        const double dec = pow(lam, (double)(n - i));
+        const double bk = Ms[r * K + k] - dec * M0[(i - 1) * K + k];     // b_i
+        const double bl = Ms[r * K + l] - dec * M0[(i - 1) * K + l];
+        const double zi = (1.0 - dec) * il;                               // z_i = Z(n - i)
+        // G_i[k][l] + G_i[l][k]
+        const double gkl = s[1 + 2 * g] - ak * ml - mk * bl + zi * mk * ml;
+        const double glk = s[2 + 2 * g] - al * mk - ml * bk + zi * ml * mk;
+        v = fma(1.0 - (double)i / (q + 1), (gkl + glk) * iz, v);
+      }
+      *vo = add ? *vo + v : v;
+    }
   }
 }
 
-// pass A: chunk-local sums.  C[chunk][m][kk] (m = moment index, kk = k*K+l)
+__device__ __forceinline__ int nstate(const NwDims& dm) {
+  return (dm.i0 == 1 ? 1 : 0) + 2 * (dm.i1 - dm.i0);
+}
+
+// moment m of the compact carry layout -> register slot
+__device__ __forceinline__ int slot_of(const NwDims& dm, int m) {
+  return dm.i0 == 1 ? m : m + 1;
+}
+
+// pass A: chunk-local sums.  C[chunk][m][kk] (m = compact moment index, kk = k*K+l)
 __global__ __launch_bounds__(256) void nw_chunk_sums(const double* __restrict__ F, NwDims dm,
-                                                     int nchunks, double* __restrict__ C) {
+                                                     double* __restrict__ C) {
   extern __shared__ double Fs[];
   const int c = blockIdx.x;
   const int t0 = c * CH, t1 = min(dm.T, t0 + CH);
-  stage_rows(F, Fs, t0, t1, dm.q, dm.K);
+  stage_rows(F, nullptr, Fs, nullptr, nullptr, t0, t1, dm, false);
   __syncthreads();
   const int KK = dm.K * dm.K;
   const int kk = blockIdx.y * blockDim.x + threadIdx.x;
   if (kk >= KK) return;
-  double s[NSTATE];
+  double s[1 + 2 * G];
 #pragma unroll
-  for (int i = 0; i < NSTATE; ++i) s[i] = 0.0;
-  nw_run_chunk<false>(Fs, t0, t1, kk / dm.K, kk % dm.K, dm, s, nullptr, 0, 0, dm.q);
-  const int ns = 4 + 7 * dm.q;
+  for (int i = 0; i < 1 + 2 * G; ++i) s[i] = 0.0;
+  nw_run_chunk<false>(Fs, nullptr, nullptr, t0, t1, kk / dm.K, kk % dm.K, dm, s, nullptr, 0, 0,
+                      false);
+  const int ns = nstate(dm);
 #pragma unroll
-  for (int m = 0; m < NSTATE; ++m)
-    if (m < ns) C[((size_t)c * ns + m) * KK + kk] = s[m];
+  for (int m = 0; m < 1 + 2 * G; ++m)
+    if (m < ns) C[((size_t)c * ns + m) * KK + kk] = s[slot_of(dm, m)];
 }
 
 // pass B: in-place exclusive scan over chunks: C[c] <- sum_{c'<c} l^(t0_c - t1_c') C[c']
 __global__ __launch_bounds__(256) void nw_carry_scan(NwDims dm, int nchunks, double* __restrict__ C) {
   const int KK = dm.K * dm.K;
-  const int ns = 4 + 7 * dm.q;
+  const int ns = nstate(dm);
   const int e = blockIdx.x * blockDim.x + threadIdx.x;  // (m, kk)
   if (e >= ns * KK) return;
+  const double dch = pow(dm.lam, (double)CH);
   double carry = 0.0;
   for (int c = 0; c < nchunks; ++c) {
     const int len = min(dm.T, (c + 1) * CH) - c * CH;
     double* p = C + (size_t)c * ns * KK + e;
     const double loc = *p;
     *p = carry;
-    carry = fma(pow(dm.lam, (double)len), carry, loc);
+    carry = fma(len == CH ? dch : pow(dm.lam, (double)len), carry, loc);
   }
 }
 
 // pass C: outputs for chunks overlapping [t_lo, t_hi)
-__global__ __launch_bounds__(256) void nw_emit(const double* __restrict__ F, NwDims dm,
+__global__ __launch_bounds__(256) void nw_emit(const double* __restrict__ F,
+                                               const double* __restrict__ M, NwDims dm,
                                                const double* __restrict__ C, int c_first,
-                                               int t_lo, int t_hi, double* __restrict__ V) {
+                                               int t_lo, int t_hi, double* __restrict__ V,
+                                               int add) {
   extern __shared__ double Fs[];
   const int c = c_first + blockIdx.x;
   const int t0 = c * CH, t1 = min(dm.T, t0 + CH);
-  stage_rows(F, Fs, t0, t1, dm.q, dm.K);
+  const int rows = t1 - t0 + dm.i1 - 1;
+  double* Ms = Fs + (size_t)rows * dm.K;
+  double* M0 = Ms + (size_t)rows * dm.K;
+  stage_rows(F, M, Fs, Ms, M0, t0, t1, dm, true);
   __syncthreads();
   const int KK = dm.K * dm.K;
   const int kk = blockIdx.y * blockDim.x + threadIdx.x;
   if (kk >= KK) return;
-  const int ns = 4 + 7 * dm.q;
-  double s[NSTATE];
+  const int ns = nstate(dm);
+  double s[1 + 2 * G];
 #pragma unroll
-  for (int m = 0; m < NSTATE; ++m) s[m] = m < ns ? C[((size_t)c * ns + m) * KK + kk] : 0.0;
-  nw_run_chunk<true>(Fs, t0, t1, kk / dm.K, kk % dm.K, dm, s, V, t_lo, t_hi, dm.q);
+  for (int m = 0; m < 1 + 2 * G; ++m) s[m] = 0.0;
+#pragma unroll
+  for (int m = 0; m < 1 + 2 * G; ++m)
+    if (m < ns) s[slot_of(dm, m)] = C[((size_t)c * ns + m) * KK + kk];
+  nw_run_chunk<true>(Fs, Ms, M0, t0, t1, kk / dm.K, kk % dm.K, dm, s, V, t_lo, t_hi, add != 0);
+}
+
+// Decayed running sums of K series: M[t][k] = sum_{s<=t} l^(t-s) x[s][k] (no masking).
+// One wave per column; lane-chunked two-level scan.
+__global__ __launch_bounds__(64) void ew_cumsum_cols(const double* __restrict__ x, int T, int K,
+                                                    double lam, double* __restrict__ M) {
+  const int k = blockIdx.x, lane = threadIdx.x;
+  const int per = (T + 63) / 64;
+  const int a = min(T, lane * per), b = min(T, a + per);
+  double num = 0.0;
+  for (int t = a; t < b; ++t) num = fma(lam, num, x[(size_t)t * K + k]);
+  double cn = num, dk = pow(lam, (double)(b - a));
+  for (int off = 1; off < 64; off <<= 1) {
+    const double pn = __shfl_up(cn, off, 64), pk = __shfl_up(dk, off, 64);
+    if (lane >= off) {
+      cn = fma(pn, dk, cn);
+      dk = dk * pk;
+    }
+  }
+  double en = __shfl_up(cn, 1, 64);
+  if (lane == 0) en = 0.0;
+  for (int t = a; t < b; ++t) {
+    en = fma(lam, en, x[(size_t)t * K + k]);
+    M[(size_t)t * K + k] = en;
+  }
 }
 
 // Decayed prefix mean with validity: out[t] = sum_{s<=t, ok} l^(t-s) x_s / sum_{s<=t, ok} l^(t-s)
@@ -161,7 +218,7 @@ __global__ __launch_bounds__(64) void ew_prefix_mean(const double* __restrict__ 
                                                      double* __restrict__ out) {
   const int lane = threadIdx.x;
   const int per = (T + 63) / 64;
-  const int a = lane * per, b = min(T, a + per);
+  const int a = min(T, lane * per), b = min(T, a + per);
   double num = 0.0, den = 0.0;
   for (int t = a; t < b; ++t) {
     const double v = x[t];
@@ -192,35 +249,54 @@ __global__ __launch_bounds__(64) void ew_prefix_mean(const double* __restrict__ 
   }
 }
 
+size_t nw_carry_bytes(int T, int K, int q) {
+  const int nch = (T + CH - 1) / CH;
+  const int g = q < G ? q : G;
+  return (size_t)nch * (1 + 2 * g) * K * K * sizeof(double);
+}
+
 }  // namespace
 
 // F: [T][K] fp64 factor-return series (global calendar, all dates up to t_hi).
 // V: [t_hi - t_lo][K][K] fp64; V[t - t_lo] = Newey-West(F[:t+1]) (NaN where t+1 <= q or <= K).
-// ws: workspace of mfa_nw_workspace_bytes(T, K, q) bytes.
+// ws: workspace of mfa_nw_workspace_bytes(T, K, q) bytes (chunk carries + the M series).
 MFA_API size_t mfa_nw_workspace_bytes(int T, int K, int q) {
-  const int nch = (T + CH - 1) / CH;
-  return (size_t)nch * (4 + 7 * q) * K * K * sizeof(double);
+  return nw_carry_bytes(T, K, q) + (size_t)T * K * sizeof(double);
+}
+
+// Largest lag count the kernels accept for K factors (LDS rows of one chunk).
+MFA_API int mfa_nw_max_lags(int K) {
+  const int rows = (int)(160 * 1024 / (3 * (size_t)K * sizeof(double)));
+  return rows - CH;
 }
 
 MFA_API int mfa_nw_series(const double* F, int T, int K, int q, double tau, int t_lo, int t_hi,
                           double* V, void* ws, void* stream) {
   if (T <= 0 || t_hi <= t_lo) return 0;
-  if (q < 0 || q > MAXQ || K <= 0 || t_lo < 0 || t_hi > T) return (int)hipErrorInvalidValue;
+  if (q < 0 || K <= 0 || t_lo < 0 || t_hi > T || q > mfa_nw_max_lags(K))
+    return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  NwDims dm{T, K, q, pow(0.5, 1.0 / tau)};
-  // only chunks up to the one containing t_hi-1 are needed
-  const int nch = (t_hi - 1) / CH + 1;
+  const double lam = pow(0.5, 1.0 / tau);
+  const int Tn = t_hi;  // only dates up to t_hi - 1 are needed
+  const int nch = (Tn - 1) / CH + 1;
   const int KK = K * K;
-  const size_t lds = (size_t)(CH + q) * K * sizeof(double);
-  if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
   double* C = (double*)ws;
-  dim3 blk(256);
-  hipLaunchKernelGGL(nw_chunk_sums, dim3(nch, (KK + 255) / 256), blk, lds, s, F, dm, nch, C);
-  const int ns = 4 + 7 * q;
-  hipLaunchKernelGGL(nw_carry_scan, dim3((ns * KK + 255) / 256), blk, 0, s, dm, nch, C);
+  double* M = (double*)((char*)ws + nw_carry_bytes(Tn, K, q));
+  hipLaunchKernelGGL(ew_cumsum_cols, dim3(K), dim3(64), 0, s, F, Tn, K, lam, M);
   const int c_first = t_lo / CH;
-  hipLaunchKernelGGL(nw_emit, dim3(nch - c_first, (KK + 255) / 256), blk, lds, s, F, dm, C,
-                     c_first, t_lo, t_hi, V);
+  dim3 blk(256);
+  // lag groups [i0, i1): group 0 also carries S0 and writes V; later groups add their lags
+  for (int i0 = 1, grp = 0; grp == 0 || i0 <= q; i0 += G, ++grp) {
+    const int i1 = std::min(q + 1, i0 + G);
+    NwDims dm{Tn, K, q, i0, i1, lam};
+    const int ns = (i0 == 1 ? 1 : 0) + 2 * (i1 - i0);
+    const size_t ldsA = (size_t)(CH + i1 - 1) * K * sizeof(double);
+    const size_t ldsC = (size_t)(2 * (CH + i1 - 1) + (i1 - 1)) * K * sizeof(double);
+    hipLaunchKernelGGL(nw_chunk_sums, dim3(nch, (KK + 255) / 256), blk, ldsA, s, F, dm, C);
+    hipLaunchKernelGGL(nw_carry_scan, dim3((ns * KK + 255) / 256), blk, 0, s, dm, nch, C);
+    hipLaunchKernelGGL(nw_emit, dim3(nch - c_first, (KK + 255) / 256), blk, ldsC, s, F, M, dm, C,
+                       c_first, t_lo, t_hi, V, grp > 0 ? 1 : 0);
+  }
   return (int)hipGetLastError();
 }
 

@@ -47,7 +47,12 @@ class RiskModel:
         # dates already processed by an earlier run (checkpoint): global index offset
         self.history = history
         self.T_hist = int(history["T"]) if history is not None else 0
-        T_new = T_global if T_global is not None else panel.D * (self.ctx.world if self.ctx.enabled else 1)
+        # every rank's date-block length, exchanged once: the per-stage all-gathers then run
+        # as single collectives without host synchronisation
+        self.sizes = pdist.shard_sizes(panel.D, self.ctx)
+        T_new = sum(self.sizes)
+        if T_global is not None and int(T_global) != T_new:
+            raise ValueError(f"T_global={T_global} but the ranks' date blocks sum to {T_new}")
         self.T = self.T_hist + T_new
         self.times = trace.Timer()
         self.sync_stages = sync_stages
@@ -56,6 +61,7 @@ class RiskModel:
         self.nw_cov = self.eigen_cov = self.vra_cov = self.vra_lambda = None
         self.eigen_bias = None
         self.B2_global = None
+        self.nw_params = None     # (q, tau) of the last newey_west() call
 
     def _stage(self, name: str):
         return trace.stage(name, self.times, self.device, sync=self.sync_stages,
@@ -83,7 +89,7 @@ class RiskModel:
         self.factor_ret, self.specific_ret, self.r2 = res.f, res.resid, res.r2
         self.status, self.stats = res.status, res.stats
         with self._stage("allgather_f"):
-            F = pdist.all_gather_rows(self.factor_ret, self.ctx)
+            F = pdist.all_gather_rows(self.factor_ret, self.ctx, self.sizes)
             if self.history is not None:
                 F = torch.cat([self.history["factor_ret"].to(F.device, F.dtype), F])
             self.factor_ret_global = F
@@ -96,6 +102,7 @@ class RiskModel:
         q = self.cfg.nw_lags if q is None else q
         tau = self.cfg.nw_half_life if tau is None else tau
         lo = self.t_lo
+        self.nw_params = (int(q), float(tau))
         with self._stage("newey_west"):
             self.nw_cov = ew_scan.newey_west_series(self.factor_ret_global, q, tau, lo,
                                                     lo + self.panel.D)
@@ -117,8 +124,9 @@ class RiskModel:
                 # than gathering [T, K, K]), runs its block of sims on all of them, and one
                 # all_reduce of the [T, K] bias sums (C5) completes the mean over M.
                 lo_new = self.T_hist
-                nw_all = ew_scan.newey_west_series(self.factor_ret_global, self.cfg.nw_lags,
-                                                   self.cfg.nw_half_life, lo_new, self.T)
+                q_nw, tau_nw = self.nw_params  # the (q, tau) newey_west() actually used
+                nw_all = ew_scan.newey_west_series(self.factor_ret_global, q_nw, tau_nw, lo_new,
+                                                   self.T)
                 Fh, vb = eigen.eigen_risk_adjust_sharded(
                     nw_all, M=M, scale_coef=scale_coef, T_sim=T_sim, seed=seed,
                     chunk=self.cfg.eigen_chunk, ctx=self.ctx, psd_tol=self.cfg.psd_tol,
@@ -145,7 +153,7 @@ class RiskModel:
         with self._stage("vra"):
             var = torch.diagonal(self.eigen_cov, dim1=-2, dim2=-1)        # [D_loc, K]
             if self.cfg.vra_out_of_sample:
-                var_all = pdist.all_gather_rows(var.contiguous(), self.ctx)
+                var_all = pdist.all_gather_rows(var.contiguous(), self.ctx, self.sizes)
                 if self.history is not None and "last_var" in self.history:
                     prev0 = self.history["last_var"].to(var.device, var.dtype)[None]
                 else:
@@ -154,7 +162,7 @@ class RiskModel:
                 lo = self.panel.date_offset
                 var = prev[lo:lo + self.panel.D]
             B2 = (self.factor_ret ** 2 / var).mean(-1)                    # NaN where ER empty
-            B2_all = pdist.all_gather_rows(B2, self.ctx)
+            B2_all = pdist.all_gather_rows(B2, self.ctx, self.sizes)
             if self.history is not None:
                 B2_all = torch.cat([self.history["B2"].to(B2_all.device, B2_all.dtype), B2_all])
             self.B2_global = B2_all
@@ -180,10 +188,10 @@ class RiskModel:
         """
         if self.B2_global is None:
             raise RuntimeError("run all four stages before exporting a checkpoint")
-        r2 = pdist.all_gather_rows(self.r2, self.ctx)
-        status = pdist.all_gather_rows(self.status, self.ctx)
+        r2 = pdist.all_gather_rows(self.r2, self.ctx, self.sizes)
+        status = pdist.all_gather_rows(self.status, self.ctx, self.sizes)
         var = torch.diagonal(self.eigen_cov, dim1=-2, dim2=-1).contiguous()
-        var_all = pdist.all_gather_rows(var, self.ctx)
+        var_all = pdist.all_gather_rows(var, self.ctx, self.sizes)
         vra_last = pdist.all_gather_rows(self.vra_cov[-1:].contiguous(), self.ctx)[-1]
         if self.history is not None:
             r2 = torch.cat([self.history["r2"].to(r2.device), r2])

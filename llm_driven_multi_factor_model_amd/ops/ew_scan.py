@@ -4,9 +4,12 @@ Reference: ``Barra-master/mfm/utils.py:16-50`` (``Newey_West``) evaluated on eve
 ``MFM.Newey_West_by_time`` (``MFM.py:80-101``), and the VRA multiplier of
 ``MFM.vol_regime_adj_by_time`` (``MFM.py:149-164``).
 
-The GPU path (``csrc/ew_scan.hip``) is a blocked decayed-moment scan: O(T K^2) work for the
-whole series instead of the reference's O(T^2 K^2), one launch per pass, and an output window
-``[t_lo, t_hi)`` so a data-parallel rank writes only its own dates.  The CPU path is the same
+The GPU path (``csrc/ew_scan.hip``) is a blocked decayed-moment scan: O(T K^2 q) work for the
+whole series instead of the reference's O(T^2 K^2 q), one launch per pass and lag group, and an
+output window ``[t_lo, t_hi)`` so a data-parallel rank writes only its own dates.  Any lag
+count is accepted (the reference's ``Newey_West`` takes any ``q < T``; USE4-S uses 5): lags run
+in register groups of 8, so only the chunk's LDS rows bound q (``mfa_nw_max_lags``, ~450 at
+K = 42).  The CPU path is the same
 recurrence in float64 torch.
 """
 from __future__ import annotations
@@ -22,6 +25,7 @@ _native.register("mfa_nw_series", [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_do
                                     C.c_int, C.c_void_p, C.c_void_p, C.c_void_p])
 _native.register("mfa_ew_prefix_mean", [C.c_void_p, C.c_int, C.c_double, C.c_void_p, C.c_void_p])
 _native.register("mfa_nw_workspace_bytes", [C.c_int, C.c_int, C.c_int])
+_native.register("mfa_nw_max_lags", [C.c_int])
 
 
 def _ws_bytes(T: int, K: int, q: int) -> int:
@@ -40,11 +44,14 @@ def newey_west_series(F: torch.Tensor, q: int = 2, tau: float = 252.0, t_lo: int
     t_hi = T if t_hi is None else t_hi
     if not (0 <= t_lo <= t_hi <= T):
         raise ValueError("invalid output window")
-    if not 0 <= q <= 4:
-        raise ValueError("q must be in 0..4")
+    if q < 0:
+        raise ValueError("q must be >= 0")
     F = F.to(torch.float64).contiguous()
     if not F.is_cuda:
         return newey_west_series_reference(F, q, tau, t_lo, t_hi)
+    qmax = _native.query("mfa_nw_max_lags", K)
+    if q > qmax:
+        raise ValueError(f"q={q} exceeds the GPU scan's LDS limit of {qmax} lags at K={K}")
     V = torch.empty(t_hi - t_lo, K, K, dtype=torch.float64, device=F.device)
     if t_hi == t_lo:
         return V

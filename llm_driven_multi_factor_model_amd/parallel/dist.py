@@ -89,16 +89,37 @@ def shard_range(D: int, rank: int, world: int) -> tuple[int, int]:
     return a, a + base + (1 if rank < rem else 0)
 
 
-def all_gather_rows(x: torch.Tensor, ctx: DistContext | None = None) -> torch.Tensor:
-    """Concatenate every rank's leading-dim block in rank order (blocks may differ in size)."""
+def shard_sizes(n_local: int, ctx: DistContext | None = None) -> list[int]:
+    """Leading-dim block size of every rank (one small collective; callers cache the result
+    and pass it to :func:`all_gather_rows` so the per-stage gathers need no size exchange)."""
+    ctx = ctx or context()
+    if not ctx.enabled:
+        return [int(n_local)]
+    n = torch.tensor([n_local], dtype=torch.int64, device=ctx.device)
+    out = torch.empty(ctx.world, dtype=torch.int64, device=ctx.device)
+    dist.all_gather_into_tensor(out, n)
+    return [int(v) for v in out.cpu().tolist()]
+
+
+def all_gather_rows(x: torch.Tensor, ctx: DistContext | None = None,
+                    sizes: list[int] | None = None) -> torch.Tensor:
+    """Concatenate every rank's leading-dim block in rank order (blocks may differ in size).
+
+    With ``sizes`` (every rank's block length, e.g. from :func:`shard_sizes`) this is ONE
+    collective with no host synchronisation; without it the sizes are exchanged first."""
     ctx = ctx or context()
     if not ctx.enabled:
         return x
-    n = torch.tensor([x.shape[0]], dtype=torch.int64, device=x.device)
-    sizes = [torch.zeros_like(n) for _ in range(ctx.world)]
-    dist.all_gather(sizes, n)
-    sizes = [int(s.item()) for s in sizes]
+    if sizes is None:
+        sizes = shard_sizes(x.shape[0], ctx)
+    if sizes[ctx.rank] != x.shape[0]:
+        raise ValueError(f"all_gather_rows: local block has {x.shape[0]} rows, sizes say "
+                         f"{sizes[ctx.rank]}")
     mx = max(sizes)
+    if all(s == mx for s in sizes):
+        out = torch.empty((ctx.world * mx,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+        dist.all_gather_into_tensor(out, x.contiguous())
+        return out
     pad = torch.zeros((mx - x.shape[0],) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
     xp = torch.cat([x, pad]) if mx > x.shape[0] else x.contiguous()
     out = torch.empty((ctx.world * mx,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)

@@ -15,6 +15,17 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "reference: compares against the read-only reference code")
 
 
+def pytest_collection_modifyitems(config, items):
+    """``-m gpu`` tests need a HIP device: on a CPU-only host they are skipped, not failed."""
+    import torch
+    if torch.cuda.is_available():
+        return
+    skip = pytest.mark.skip(reason="no GPU (HIP device) available")
+    for item in items:
+        if "gpu" in item.keywords:
+            item.add_marker(skip)
+
+
 @pytest.fixture(scope="session")
 def cuda():
     import torch

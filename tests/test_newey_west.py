@@ -16,7 +16,7 @@ def _series(T, K, seed=0):
 
 
 @pytest.mark.reference
-@pytest.mark.parametrize("q,tau", [(2, 252.0), (1, 42.0), (0, 90.0)])
+@pytest.mark.parametrize("q,tau", [(2, 252.0), (1, 42.0), (0, 90.0), (5, 84.0), (8, 30.0)])
 def test_series_matches_reference_newey_west(ref, q, tau):
     T, K = 40, 6
     F = _series(T, K)
@@ -61,6 +61,31 @@ def test_hip_scan_matches_oracle(cuda, T, K, q, tau, lo, hi):
     ref = ew_scan.newey_west_series_reference(F, q, tau, lo, hi)
     out = ew_scan.newey_west_series(F.to(cuda), q, tau, lo, hi).cpu()
     torch.testing.assert_close(out, ref, rtol=1e-9, atol=1e-15, equal_nan=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,K,q,tau,lo,hi", [(600, 42, 5, 84.0, 0, 600), (1000, 42, 8, 84.0, 100, 1000),
+                                             (400, 12, 10, 42.0, 0, 400), (300, 9, 17, 60.0, 250, 300),
+                                             (200, 6, 40, 90.0, 0, 200)])
+def test_hip_scan_any_lag_count(cuda, T, K, q, tau, lo, hi):
+    """q beyond one register lag group (8): the launch loops over lag groups and accumulates."""
+    F = _series(T, K, seed=q)
+    ref = ew_scan.newey_west_series_reference(F, q, tau, lo, hi)
+    out = ew_scan.newey_west_series(F.to(cuda), q, tau, lo, hi).cpu()
+    torch.testing.assert_close(out, ref, rtol=1e-9, atol=1e-15, equal_nan=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.reference
+def test_hip_scan_use4s_lags_match_reference(cuda, ref):
+    """USE4-S 5-lag Newey-West on the GPU against the reference utils.Newey_West itself."""
+    T, K, q, tau = 60, 8, 5, 84.0
+    F = _series(T, K, seed=11)
+    V = ew_scan.newey_west_series(F.to(cuda), q=q, tau=tau).cpu()
+    df = pd.DataFrame(F.numpy(), columns=[f"f{k}" for k in range(K)])
+    for t in (K + 1, 20, 41, T):
+        R = ref.utils.Newey_West(df[:t], q, tau).values
+        np.testing.assert_allclose(V[t - 1].numpy(), R, rtol=1e-10, atol=1e-17)
 
 
 @pytest.mark.gpu

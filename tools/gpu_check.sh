@@ -7,7 +7,7 @@ OUT=gpurun_out
 mkdir -p $OUT
 export TMPDIR=/tmp
 STEPS=${STEPS:-30}
-timeout -k 10 600 python -m pytest tests -m gpu -x -q ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1 \
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1 \
  && tail -3 $OUT/pytest_gpu.log \
  && timeout -k 10 300 python __graft_entry__.py smoke > $OUT/smoke.log 2>&1 && tail -1 $OUT/smoke.log \
  && timeout -k 10 300 python bench.py --steps $STEPS --warmup 5 --check > $OUT/bench.log 2>&1 && cat $OUT/bench.log \
