@@ -1,14 +1,19 @@
 """Tushare Pro fetchers (reference: Barra_database/database/tushare_fetcher.py:17-315).
 
 The token comes from TUSHARE_TOKEN; with no token or no ``tushare`` package every fetcher
-returns an empty DataFrame.  Field lists cover every column the factor pipeline consumes plus
-the identifiers; pass ``fields=`` to request more.
+returns an empty DataFrame.  The statement tables request the reference's full column sets
+(``tushare_fields.py``: 167 fina_indicator, 158 balancesheet, 97 cashflow, 94 income fields)
+with ``update_flag='1'`` (latest revision only), so the stored Mongo collections have the
+reference's schema; pass ``fields=`` to request a different set.
 """
 from __future__ import annotations
 
 import os
 
 import pandas as pd
+
+from .tushare_fields import (BALANCESHEET_FIELDS, CASHFLOW_FIELDS, FINA_INDICATOR_FIELDS,
+                             INCOME_FIELDS)
 
 TOKEN = os.environ.get("TUSHARE_TOKEN")
 try:  # optional dependency
@@ -20,15 +25,6 @@ except Exception:
 DAILY_BASIC_FIELDS = ["ts_code", "trade_date", "close", "turnover_rate", "turnover_rate_f", "volume_ratio",
                       "pe", "pe_ttm", "pb", "ps", "ps_ttm", "dv_ratio", "dv_ttm", "total_share",
                       "float_share", "free_share", "total_mv", "circ_mv"]
-FINA_INDICATOR_FIELDS = ["ts_code", "ann_date", "end_date", "eps", "roe", "roa", "debt_to_assets",
-                         "q_profit_yoy", "q_sales_yoy", "netprofit_yoy", "or_yoy", "update_flag"]
-BALANCESHEET_FIELDS = ["ts_code", "ann_date", "f_ann_date", "end_date", "report_type", "total_assets",
-                       "total_liab", "total_ncl", "total_hldr_eqy_inc_min_int", "total_hldr_eqy_exc_min_int",
-                       "update_flag"]
-CASHFLOW_FIELDS = ["ts_code", "ann_date", "f_ann_date", "end_date", "report_type", "n_cashflow_act",
-                   "n_cashflow_inv_act", "n_cash_flows_fnc_act", "update_flag"]
-INCOME_FIELDS = ["ts_code", "ann_date", "f_ann_date", "end_date", "report_type", "total_revenue",
-                 "revenue", "operate_profit", "n_income", "n_income_attr_p", "update_flag"]
 
 
 def _call(api: str, **kw) -> pd.DataFrame:
@@ -61,19 +57,19 @@ def fetch_daily_basic_by_date(trade_date: str, fields=DAILY_BASIC_FIELDS) -> pd.
 
 
 def fetch_financial_indicators_by_stock(ts_code: str, fields=FINA_INDICATOR_FIELDS) -> pd.DataFrame:
-    return _call("fina_indicator", ts_code=ts_code, fields=fields)
+    return _call("fina_indicator", ts_code=ts_code, update_flag="1", fields=fields)
 
 
 def fetch_balancesheet_by_stock(ts_code: str, fields=BALANCESHEET_FIELDS) -> pd.DataFrame:
-    return _call("balancesheet", ts_code=ts_code, fields=fields)
+    return _call("balancesheet", ts_code=ts_code, update_flag="1", fields=fields)
 
 
 def fetch_cashflow_by_stock(ts_code: str, fields=CASHFLOW_FIELDS) -> pd.DataFrame:
-    return _call("cashflow", ts_code=ts_code, fields=fields)
+    return _call("cashflow", ts_code=ts_code, update_flag="1", fields=fields)
 
 
 def fetch_income_by_stock(ts_code: str, fields=INCOME_FIELDS) -> pd.DataFrame:
-    return _call("income", ts_code=ts_code, fields=fields)
+    return _call("income", ts_code=ts_code, update_flag="1", fields=fields)
 
 
 def fetch_index_info(market: str = "SSE") -> pd.DataFrame:

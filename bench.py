@@ -13,6 +13,13 @@ date, replayed from a captured HIP graph), then all-gathers
 the factor-return series across ranks over RCCL (the collective the downstream Newey-West stage
 needs).  Data is a synthetic panel of the named shape with random-init exposures (the reference ships no data).
 
+Storage: ``--storage fp64`` (default, the headline) keeps the panel in float64, the precision
+the reference regresses (``demo.py:21`` reads float64 CSV columns into ``CrossSection.reg``);
+``--storage fp32`` is the factor pipeline's downcast (``load_data.py:18-21``).  Moments, solve
+and reductions are float64 in both.  Every step runs the production path of
+``RiskModel.regress``: the fused kernel plus the device pseudo-inverse pass for near-singular
+dates (``refine=True``), both inside the captured graph.
+
     python bench.py --gpus 1 --steps 20 --warmup 3
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 bench.py --gpus 8
 """
@@ -40,6 +47,8 @@ def main() -> int:
     ap.add_argument("--stocks", type=int, default=5000)
     ap.add_argument("--industries", type=int, default=31)
     ap.add_argument("--styles", type=int, default=10)
+    ap.add_argument("--storage", choices=["fp64", "fp32"], default="fp64",
+                    help="panel storage dtype (fp64 = the reference's input precision)")
     ap.add_argument("--no-resid", action="store_true", help="skip specific-return output (not the headline)")
     ap.add_argument("--check", action="store_true", help="verify a few dates against the fp64 oracle")
     ap.add_argument("--no-graph", action="store_true",
@@ -68,7 +77,9 @@ def main() -> int:
 
     D, N, P, Q = args.dates, args.stocks, args.industries, args.styles
     K = 1 + P + Q
-    panel = synthetic_panel(D, N, P, Q, seed=1234 + rank, device=dev, missing_frac=0.01)
+    sdt = torch.float64 if args.storage == "fp64" else torch.float32
+    panel = synthetic_panel(D, N, P, Q, seed=1234 + rank, device=dev, missing_frac=0.01,
+                            dtype=sdt)
     # Two output / gather buffers: step i's RCCL all-gather of the factor-return series runs on
     # the collective stream underneath step i+1's regression (the write of buffer i%2 at step
     # i+2 first waits for that gather).  Every collective completes inside the timed region.
@@ -83,7 +94,7 @@ def main() -> int:
 
     def regress(b):
         outs[b] = xs_wls(panel.styles, panel.cap, panel.ret, panel.ind, P,
-                         want_resid=not args.no_resid, refine=False, out=outs[b], workspace=ws)
+                         want_resid=not args.no_resid, refine=True, out=outs[b], workspace=ws)
 
     def step():
         nonlocal it
@@ -180,7 +191,7 @@ def main() -> int:
                 "dates_per_gpu": D,
                 "parallelism": f"dp{world}",
                 "specific_returns": not args.no_resid,
-                "storage": "fp32 panel (reference downcasts inputs to float32, load_data.py:18-21)",
+                "storage": args.storage,
             },
         }), flush=True)
     if world > 1:

@@ -27,6 +27,7 @@ _vp, _i, _d, _f = C.c_void_p, C.c_int, C.c_double, C.c_float
 _SIGS: dict[str, list] = {
     # xs_wls.hip
     "mfa_xs_wls": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _d, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "mfa_xs_wls_f64": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _d, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "mfa_xs_wls_workspace": [_i, _i, _i],
     "mfa_xs_wls_variant": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
 }

@@ -16,9 +16,9 @@ namespace {
 
 using namespace mfa;
 
-template <int Q>
+template <int Q, typename T>
 __global__ __launch_bounds__(256) void portfolio_exposure_kernel(
-    const float* __restrict__ X, const float* __restrict__ cap, const float* __restrict__ ret,
+    const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
     const int16_t* __restrict__ ind, const double* __restrict__ h, const double* __restrict__ stats,
     int N, int P, int K, double* __restrict__ out) {
   __shared__ double segs[128];
@@ -27,21 +27,21 @@ __global__ __launch_bounds__(256) void portfolio_exposure_kernel(
   const int Pseg = P > 0 ? P : 1;
   for (int j = tid; j < 128; j += blockDim.x) segs[j] = 0.0;
   __syncthreads();
-  const float* Xd = X + (size_t)d * Q * N;
-  const float* cd = cap + (size_t)d * N;
-  const float* rd = ret + (size_t)d * N;
+  const T* Xd = X + (size_t)d * Q * N;
+  const T* cd = cap + (size_t)d * N;
+  const T* rd = ret + (size_t)d * N;
   const int16_t* id = ind ? ind + (size_t)d * N : nullptr;
   const double* hd = h + (size_t)d * N;
   double acc[Q + 1];
 #pragma unroll
   for (int q = 0; q <= Q; ++q) acc[q] = 0.0;
   for (int n = tid; n < N; n += blockDim.x) {
-    const float c = cd[n], r = rd[n];
+    const T c = cd[n], r = rd[n];
     const int j = id ? (int)id[n] : 0;
     const double w = hd[n];
-    bool ok = (j >= 0) && (j < Pseg) && __builtin_isfinite(c) && (c >= 0.f) &&
+    bool ok = (j >= 0) && (j < Pseg) && __builtin_isfinite(c) && (c >= T(0)) &&
               __builtin_isfinite(r) && __builtin_isfinite(w);
-    float xf[Q];
+    T xf[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
       xf[q] = Xd[(size_t)q * N + n];
@@ -75,6 +75,27 @@ __global__ __launch_bounds__(256) void portfolio_exposure_kernel(
   if (tid < Q) o[1 + P + tid] = (red[0][tid] - st[tid] * hs) * isig;
 }
 
+template <typename T>
+int portfolio_exposure_dispatch(const T* X, const T* cap, const T* ret, const int16_t* ind,
+                                const double* h, const double* stats, int D, int N, int P, int Q,
+                                double* out, void* stream) {
+  if (D <= 0) return 0;
+  if (Q < 1 || Q > 16 || P < 0 || P > 128 || N <= 0) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  const int K = 1 + P + Q;
+  switch (Q) {
+#define MFA_Q(qq)                                                                              \
+  case qq:                                                                                     \
+    hipLaunchKernelGGL((portfolio_exposure_kernel<qq, T>), dim3(D), dim3(256), 0, s, X, cap,   \
+                       ret, P > 0 ? ind : nullptr, h, stats, N, P, K, out);                    \
+    break;
+    MFA_Q(1) MFA_Q(2) MFA_Q(3) MFA_Q(4) MFA_Q(5) MFA_Q(6) MFA_Q(7) MFA_Q(8)
+    MFA_Q(9) MFA_Q(10) MFA_Q(11) MFA_Q(12) MFA_Q(13) MFA_Q(14) MFA_Q(15) MFA_Q(16)
+#undef MFA_Q
+  }
+  return (int)hipGetLastError();
+}
+
 }  // namespace
 
 // X [D][Q][N] f32, cap/ret [D][N] f32 (validity only), ind [D][N] int16 (nullable when P == 0),
@@ -83,19 +104,12 @@ __global__ __launch_bounds__(256) void portfolio_exposure_kernel(
 MFA_API int mfa_portfolio_exposure(const float* X, const float* cap, const float* ret,
                                    const int16_t* ind, const double* h, const double* stats, int D,
                                    int N, int P, int Q, double* out, void* stream) {
-  if (D <= 0) return 0;
-  if (Q < 1 || Q > 16 || P < 0 || P > 128 || N <= 0) return (int)hipErrorInvalidValue;
-  hipStream_t s = (hipStream_t)stream;
-  const int K = 1 + P + Q;
-  switch (Q) {
-#define MFA_Q(qq)                                                                              \
-  case qq:                                                                                     \
-    hipLaunchKernelGGL(portfolio_exposure_kernel<qq>, dim3(D), dim3(256), 0, s, X, cap, ret,   \
-                       P > 0 ? ind : nullptr, h, stats, N, P, K, out);                         \
-    break;
-    MFA_Q(1) MFA_Q(2) MFA_Q(3) MFA_Q(4) MFA_Q(5) MFA_Q(6) MFA_Q(7) MFA_Q(8)
-    MFA_Q(9) MFA_Q(10) MFA_Q(11) MFA_Q(12) MFA_Q(13) MFA_Q(14) MFA_Q(15) MFA_Q(16)
-#undef MFA_Q
-  }
-  return (int)hipGetLastError();
+  return portfolio_exposure_dispatch<float>(X, cap, ret, ind, h, stats, D, N, P, Q, out, stream);
+}
+
+// Same with an fp64 panel.
+MFA_API int mfa_portfolio_exposure_f64(const double* X, const double* cap, const double* ret,
+                                       const int16_t* ind, const double* h, const double* stats,
+                                       int D, int N, int P, int Q, double* out, void* stream) {
+  return portfolio_exposure_dispatch<double>(X, cap, ret, ind, h, stats, D, N, P, Q, out, stream);
 }

@@ -1,0 +1,1225 @@
+// Batched cross-sectional WLS factor-return regression (Barra CNE5/USE4 style) for gfx950,
+// templated on the panel's storage type T (float or double).  Included by xs_wls.hip (fp32
+// panels) and xs_wls_f64.hip (fp64 panels: the reference reads float64 CSV exposures,
+// Barra-master/demo.py:21-35, and regresses them in float64, mfm/CrossSection.py:57-108).
+//
+// Reference semantics: Barra-master/mfm/CrossSection.py:12-20 (style z-score: cap-weighted mean,
+// ONE pooled ddof-0 std) and :57-108 (sqrt-cap WLS, industry-neutral constraint
+// sum_j s_j f_j = 0 via the K x (K-1) matrix R, pinv solve, f = Omega r, e = r - X f,
+// unweighted R^2).  Nothing mirrors the reference's dense N x N weight matrix.
+//
+// Three phases, all dates of a shard per launch (fused into one kernel by default):
+//   K1 moments   HBM streaming.  Every wave streams its own 64-stock tiles of the [D][Q][N]
+//                styles, caps, returns and int16 industry ids through a private LDS ring
+//                filled by global_load_lds (4 B per lane for fp32 rows; 16 B per lane, two
+//                512-B fp64 rows per instruction, for fp64), with counted vmcnt and no workgroup
+//                barrier until the date's final reduction.  RAW fp64 moments accumulate in
+//                registers; the one-hot industry block is a segmented sum done with ds_add_f64
+//                into an R-way replicated [P][Q+3] table laid out so one issue group is <= 2-way
+//                conflicted.  z-scoring is folded in algebraically later: the data is read once.
+//   K2 solve     latency-bound tiny algebra.  One wave per date: after eliminating the pivot
+//                industry the industry block is diag(W) + rho a a^T (Sherman-Morrison), and
+//                only the (1+Q) x (1+Q) Schur complement is Cholesky-factorised, row-per-lane
+//                in registers.  Exactly-empty industries get f = 0 (pinv semantics); near-
+//                singular dates are flagged for the pseudo-inverse refinement pass.
+//   K3 resid     HBM / Infinity-Cache streaming, low VGPR count: specific returns (stored in T)
+//                + R^2.  16-byte vector loads (4 fp32 / 2 fp64 stocks per lane).
+#pragma once
+#include "common.h"
+#include "jacobi.h"
+
+#include <utility>
+
+// CS-WLS execution mode shared by the fp32 and fp64 translation units (mfa_xs_set_mode):
+// 0 = fused single kernel (fp32: with the residual prefetch during the solve), 1 = three
+// separate kernels (ablation / large-P fallback), 7 = fused without the prefetch.
+extern int g_mfa_xs_mode;
+
+namespace {
+
+using namespace mfa;
+
+enum XsStatus : int {
+  XS_NO_ROWS = 1,        // no valid stock on the date
+  XS_PIVOT_EMPTY = 2,    // constraint pivot industry has zero capital
+  XS_NEAR_SINGULAR = 4,  // Schur Cholesky lost > 12 digits: refined with the pseudo-inverse
+  XS_ZERO_PIVOT = 8,     // exactly-zero pivots / empty industries (pinv semantics -> f = 0)
+  XS_BAD_SIGMA = 16,     // pooled style std is zero / NaN
+  XS_REFINED = 32,       // re-solved on the device with the eigen pseudo-inverse (pinv)
+};
+constexpr int XS_BAD = XS_NO_ROWS | XS_BAD_SIGMA | XS_PIVOT_EMPTY;
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) void gbl_void_t;
+
+template <typename T>
+__device__ __forceinline__ bool finite_v(T v) { return __builtin_isfinite(v); }
+
+__device__ __forceinline__ void lds_add(double* p, double v) {
+  __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+// ds_add_f64 from inline asm: hipcc's waitcnt pass emits vmcnt(0) (draining every in-flight
+// LDS-DMA tile) before any compiler-visible LDS write while a global_load_lds is pending.  The
+// segment tables never alias the DMA ring, so the atomic is hidden from that analysis.  LDS ops
+// complete in order, so the compiler's own lgkmcnt waits stay correct; barriers drain these.
+template <int OFF>
+__device__ __forceinline__ void lds_add_nowait(unsigned lds_addr, double v) {
+  asm volatile("ds_add_f64 %0, %1 offset:%2" ::"v"(lds_addr), "v"(v), "i"(OFF) : "memory");
+}
+__device__ __forceinline__ unsigned lds_addr(const void* p) {
+  return (unsigned)(uintptr_t)(__attribute__((address_space(3))) const void*)p;
+}
+
+// 4-byte async global -> LDS copy (one fp32 per lane: a 64-stock row per wave instruction).
+__device__ __forceinline__ void glds4(const void* src, void* wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)wave_base, 4, 0, 0);
+}
+
+// 16-byte async global -> LDS copy; LDS destination = wave-uniform `wave_base` + lane * 16.
+__device__ __forceinline__ void glds16(const void* src, void* wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)wave_base, 16, 0, 0);
+}
+
+__device__ __forceinline__ void wait_vmcnt(int n) {
+  switch (n) {
+#define MFA_W(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    MFA_W(1) MFA_W(2) MFA_W(3) MFA_W(4) MFA_W(5) MFA_W(6) MFA_W(7) MFA_W(8) MFA_W(9)
+    MFA_W(10) MFA_W(11) MFA_W(12) MFA_W(13) MFA_W(14) MFA_W(15) MFA_W(16) MFA_W(17)
+    MFA_W(18) MFA_W(19) MFA_W(20) MFA_W(21) MFA_W(22) MFA_W(23) MFA_W(24) MFA_W(25)
+    MFA_W(26) MFA_W(27) MFA_W(28) MFA_W(29) MFA_W(30) MFA_W(31) MFA_W(32) MFA_W(33)
+    MFA_W(34) MFA_W(35) MFA_W(36) MFA_W(37) MFA_W(38) MFA_W(39) MFA_W(40) MFA_W(41)
+    MFA_W(42) MFA_W(43) MFA_W(44) MFA_W(45) MFA_W(46) MFA_W(47) MFA_W(48) MFA_W(49)
+    MFA_W(50) MFA_W(51) MFA_W(52) MFA_W(53) MFA_W(54) MFA_W(55) MFA_W(56) MFA_W(57)
+    MFA_W(58) MFA_W(59) MFA_W(60) MFA_W(61) MFA_W(62) MFA_W(63)
+#undef MFA_W
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+__device__ __forceinline__ void wave_sync_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+#ifndef MFA_XS_REP
+#define MFA_XS_REP 8
+#endif
+// Segment-table replicas: entry (j, ch) owns R consecutive doubles and lane l adds into slot
+// l & (R-1).  With R = 8 the 16 lanes of a ds_add_f64 issue group land on bank pairs
+// (l & 7) + 8 * ((j*NS + ch) & 1): at most 2-way conflicts whatever the industry mix (4
+// lane-strided replicas measured 8.3 conflict cycles per instruction).
+constexpr int kRepMax = MFA_XS_REP;
+constexpr int kSegLdsBudget = 48 * 1024;  // R = 8 only while the table leaves 2 WGs / CU
+constexpr int kWT = 64;                   // stocks per wave tile (K1: one stock per lane)
+
+// Per-type streaming parameters.  fp32: 4-slot ring of 3.2 KB tiles; fp64: 2-slot ring of
+// 6.3 KB tiles (4 waves x 2 x 6.3 KB + the segment table keeps 2 workgroups per CU).
+template <typename T> struct Stream;
+template <> struct Stream<float> {
+  static constexpr int RING = 4;
+  static constexpr int VEC = 4;  // residual pass: stocks per 16-byte load
+  static constexpr int U = 3;    // residual iterations in flight
+};
+template <> struct Stream<double> {
+  static constexpr int RING = 2;
+  static constexpr int VEC = 2;
+  static constexpr int U = 2;
+};
+
+template <int Q, typename T>
+struct Layout {
+  static constexpr int NS = Q + 3;             // per-industry channels: W, A_q, B, s
+  static constexpr int NG = Q * (Q + 1) / 2;   // packed symmetric raw Gram
+  static constexpr int NACC = NG + 2 * Q + 4;  // Swxx | Swxr | Scx | Sc Sx Sxx n
+  static constexpr int ND = Q + 1;             // dense block: country + styles
+  static constexpr int ROWB = kWT * (int)sizeof(T);            // one field row of a wave tile
+  static constexpr int WSLOT = (Q + 2) * ROWB + kWT * 2;       // K1 per-wave ring slot
+  __host__ __device__ static constexpr int msize(int Pseg) { return NACC + Pseg * NS; }
+};
+
+// Reduce a compile-time register array across the workgroup into out[0..CNT) (LDS, zeroed by
+// the caller) through a per-wave [8][65] fp64 tile: keeps the register footprint flat.
+// DET: `out` is this wave's own partial row (plain stores, summed in wave order by the caller)
+// instead of the shared total (LDS atomics: order-dependent rounding).
+template <int CNT, bool DET = false>
+__device__ __forceinline__ void wg_reduce(const double (&v)[CNT], double* wbuf, double* out) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int a = lane & 7, slice = lane >> 3;
+#pragma unroll
+  for (int c0 = 0; c0 < CNT; c0 += 8) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      if (c0 + i < CNT) wbuf[i * 65 + lane] = v[c0 + i];
+    wave_sync_lds();
+    double t = 0.0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t += wbuf[a * 65 + slice * 8 + i];
+    t += __shfl_xor(t, 8, kWave);
+    t += __shfl_xor(t, 16, kWave);
+    t += __shfl_xor(t, 32, kWave);
+    if (slice == 0 && c0 + a < CNT) {
+      if constexpr (DET) out[c0 + a] = t;
+      else lds_add(out + c0 + a, t);
+    }
+    wave_sync_lds();
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K1: raw moments.  mom[d] = [ Swxx(NG) | Swxr(Q) | Scx(Q) | Sc Sx Sxx n | seg[Pseg][NS] ]
+// ------------------------------------------------------------------------------------------
+template <int Q, typename T>
+struct Ring {
+  // Per-wave DMA rings (own __shared__ object, separate from the atomics' dynamic LDS): each
+  // wave streams its own 64-stock tiles (k = wid, wid + nw, ...) with no workgroup barrier until
+  // the final reduction, so the 8 waves of a CU drift and overlap HBM, VALU and LDS phases.
+  static constexpr int WSLOT = Layout<Q, T>::WSLOT;
+  static constexpr int NB = Stream<T>::RING;
+  // >= the reduction tile [8][65] fp64 + one partial row (deterministic wg_reduce)
+  static constexpr int RED = (8 * 65 + Layout<Q, T>::NACC) * 8;
+  static constexpr int RINGW = NB * WSLOT > RED ? NB * WSLOT : RED;
+  static constexpr int BYTES = 4 * RINGW;
+};
+
+// LDS-DMA instructions one wave issues per tile (the vmcnt unit of the ring).
+template <int Q, typename T>
+__device__ __forceinline__ constexpr int dma_per_tile(bool has_ind) {
+  return (sizeof(T) == 4 ? Q + 2 : (Q + 3) / 2) + (has_ind ? 1 : 0);
+}
+
+// Moments of date d.  `ring` = Ring<Q,T>::BYTES of LDS, `dyn` = [Pseg*NS][R] replicated
+// segment sums | [NACC] totals (LDS), `md` = msize(Pseg) doubles out (global memory or LDS that
+// does not alias `dyn`; may alias `ring`).  Ends with a workgroup barrier.
+//
+// VAR & 32 = bitwise-deterministic mode (4-wave workgroups): every segment replica is owned by
+// ONE wave (R/4 per wave), so its atomics land in that wave's program order, and the per-lane
+// totals are reduced through per-wave partial rows summed in wave order.  The default mode
+// shares replicas across waves (fewer bank conflicts) and is reproducible to rounding only.
+// VAR & 1 / & 2: timing-only ablations (no segment atomics / no style-Gram FMAs).
+template <int Q, int VAR, int R, typename T>
+__device__ __forceinline__ void moments_body(
+    const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
+    const int16_t* __restrict__ ind, int N, int Pseg, int d, char* ring, double* dyn,
+    double* md) {
+  using L = Layout<Q, T>;
+  constexpr int NS = L::NS, NG = L::NG, NACC = L::NACC;
+  constexpr int WSLOT = Ring<Q, T>::WSLOT, RINGW = Ring<Q, T>::RINGW, NB = Ring<Q, T>::NB;
+  constexpr int ROWB = L::ROWB;
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int lane = tid & 63, wid = tid >> 6, nw = nthr >> 6;
+  constexpr bool DET = (VAR & 32) != 0;
+  static_assert(!DET || (R % 4 == 0 && NACC <= 256), "deterministic mode: 4 waves, R/4 replicas each");
+  const int rep = DET ? wid * (R / 4) + (lane & (R / 4 - 1)) : (lane & (R - 1));
+  const unsigned seg_a = lds_addr(dyn + rep);
+  double* acc = dyn + R * Pseg * NS;
+  for (int i = tid; i < R * Pseg * NS + NACC; i += nthr) dyn[i] = 0.0;
+  __syncthreads();
+
+  const T* Xd = X + (size_t)d * Q * N;
+  const T* cd = cap + (size_t)d * N;
+  const T* rd = ret + (size_t)d * N;
+  const int16_t* id = ind ? ind + (size_t)d * N : nullptr;
+
+  double v[NACC];
+#pragma unroll
+  for (int i = 0; i < NACC; ++i) v[i] = 0.0;
+
+  char* wring = ring + wid * RINGW;
+  const int nrows = dma_per_tile<Q, T>(id != nullptr);  // DMA instructions per tile
+  const int ntile_all = (N + kWT - 1) / kWT;
+  const int ntile = ntile_all > wid ? (ntile_all - wid + nw - 1) / nw : 0;  // this wave's tiles
+  auto issue = [&](int i) {
+    char* slot = wring + (i % NB) * WSLOT;
+    const int s0 = (wid + i * nw) * kWT;
+    if constexpr (sizeof(T) == 4) {
+      const bool in = s0 + lane < N;
+      if (in) glds4(cd + s0 + lane, slot);
+      if (in) glds4(rd + s0 + lane, slot + ROWB);
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (in) glds4(Xd + (size_t)q * N + s0 + lane, slot + (2 + q) * ROWB);
+    } else {
+      // two 512-B fp64 rows per instruction: lanes 0-31 -> row rr, lanes 32-63 -> row rr + 1
+      const int half = lane >> 5, s = s0 + 2 * (lane & 31);
+      const bool in = s < N;  // N is even: both stocks of the pair exist
+#pragma unroll
+      for (int rr = 0; rr < Q + 2; rr += 2) {
+        const int row = rr + half;
+        const T* src = row == 0 ? cd : (row == 1 ? rd : Xd + (size_t)(row - 2) * N);
+        if (in && row < Q + 2) glds16(src + s, slot + rr * ROWB);
+      }
+    }
+    if (id && lane < kWT / 2 && s0 + 2 * lane < N) glds4(id + s0 + 2 * lane, slot + (Q + 2) * ROWB);
+  };
+  for (int i = 0; i < NB - 1 && i < ntile; ++i) issue(i);
+  for (int i = 0; i < ntile; ++i) {
+    const bool tail = (i + NB - 1 >= ntile);
+    wait_vmcnt(tail ? 0 : (NB - 2) * nrows);
+    __builtin_amdgcn_wave_barrier();
+    if (i + NB - 1 < ntile) issue(i + NB - 1);
+    const char* slot = wring + (i % NB) * WSLOT;
+    const T* bf = (const T*)slot;
+    const int s = (wid + i * nw) * kWT + lane;
+    const T cf = bf[lane], rf = bf[kWT + lane];
+    const int j = id ? (int)((const int16_t*)(slot + (Q + 2) * ROWB))[lane] : 0;
+    T xf[Q];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) xf[q] = bf[(2 + q) * kWT + lane];
+    bool ok = (s < N) && (j >= 0) && (j < Pseg) && finite_v(cf) && (cf >= T(0)) && finite_v(rf);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) ok = ok && finite_v(xf[q]);
+    if (ok) {
+      const double c = cf, r = rf, w = sqrt(c);
+      double x[Q], wx[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) { x[q] = xf[q]; wx[q] = w * x[q]; }
+      if constexpr ((VAR & 2) != 0) {  // timing-only ablation: skip the moment FMAs
+#pragma unroll
+        for (int q = 0; q < Q; ++q) asm volatile("" ::"v"(wx[q]));
+      } else {
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+#pragma unroll
+        for (int t = 0; t <= q; ++t) v[q * (q + 1) / 2 + t] = fma(wx[q], x[t], v[q * (q + 1) / 2 + t]);
+      }
+      double sx = 0.0, sxx = 0.0;
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        v[NG + q] = fma(wx[q], r, v[NG + q]);
+        v[NG + Q + q] = fma(c, x[q], v[NG + Q + q]);
+        sx += x[q];
+        sxx = fma(x[q], x[q], sxx);
+      }
+      v[NG + 2 * Q + 0] += c;
+      v[NG + 2 * Q + 1] += sx;
+      v[NG + 2 * Q + 2] += sxx;
+      v[NG + 2 * Q + 3] += 1.0;
+      if (VAR & 1) {  // timing-only ablation: skip the segment atomics
+        asm volatile("" ::"v"(w), "v"(r));
+      } else {
+        const unsigned a = seg_a + (unsigned)(j * NS * R * 8);
+        lds_add_nowait<0>(a, w);
+        [&]<int... I>(std::integer_sequence<int, I...>) {
+          (lds_add_nowait<8 * R * (1 + I)>(a, wx[I]), ...);
+        }(std::make_integer_sequence<int, Q>{});
+        lds_add_nowait<8 * R * (Q + 1)>(a, w * r);
+        lds_add_nowait<8 * R * (Q + 2)>(a, c);
+      }
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if constexpr (DET) {
+    static_assert(RINGW >= 8 * 65 * 8 + NACC * 8, "partial row must fit the wave ring");
+    wg_reduce<NACC, true>(v, (double*)wring, (double*)(wring + 8 * 65 * 8));
+    __syncthreads();
+    double t = 0.0;
+    if (tid < NACC)
+      for (int w = 0; w < nw; ++w) t += ((const double*)(ring + w * RINGW + 8 * 65 * 8))[tid];
+    __syncthreads();  // md may alias the ring
+    if (tid < NACC) md[tid] = t;
+  } else {
+    wg_reduce<NACC>(v, (double*)wring, acc);
+    __syncthreads();
+    for (int i = tid; i < NACC; i += nthr) md[i] = acc[i];
+  }
+  for (int i = tid; i < Pseg * NS; i += nthr) {
+    double t = 0.0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) t += dyn[i * R + r];
+    md[NACC + i] = t;
+  }
+  __syncthreads();
+}
+
+template <int Q, int VAR, int R, typename T>
+__global__ __launch_bounds__(256) void xs_moments_kernel(
+    const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
+    const int16_t* __restrict__ ind, int N, int Pseg, double* __restrict__ mom) {
+  __shared__ __attribute__((aligned(16))) char ring[Ring<Q, T>::BYTES];
+  extern __shared__ double dyn[];
+  const int d = blockIdx.x;
+  moments_body<Q, VAR, R, T>(X, cap, ret, ind, N, Pseg, d, ring, dyn,
+                             mom + (size_t)d * Layout<Q, T>::msize(Pseg));
+}
+
+// ------------------------------------------------------------------------------------------
+// K2: structured constrained solve, one wave per date (storage-type independent).
+// coef[d] = [ beta_q (Q) | cst | f_ind (P) ]  for the residual pass (e = r - cst - f_j - b.x)
+//
+// Algebra (CrossSection.py:57-106 with the constraint substituted): with g_j the standardised
+// industry row [W_j, (A_jq - mu_q W_j)/sigma, B_j], pivot p, a_j = -s_j/s_p and
+// m_j = g_j + a_j g_p for the active industries, the industry block is diag(W) + rho a a^T and
+//   S   = M_DD - G + kappa at at^T,    G = sum_j m_j m_j^T / W_j,   at = sum_j a_j m_j / W_j,
+//   kappa = rho / (1 + rho c0),        c0 = sum_j a_j^2 / W_j,
+//   f_j = (m_j . h - kappa a_j z) / W_j,  f_p = z (1 - kappa c0),  h = [-g_D, 1],  z = at . h.
+// G, at, c0 and the industry totals are ONE weighted Gram over industries with augmented
+// channels [m | a | 1], computed by v_mfma_f64_16x16x4f64 straight from the moments in LDS
+// (A[i][k] from lane i + 16k, B[k][j] from lane j + 16k, D[(l>>4) + 4r][l&15] in register r
+// -- layout probed in tools/probes/mfma64_probe.hip).  Only the (1+Q)^2 Cholesky is serial; it
+// runs redundantly in every lane's registers.  All dates are resident at once, so the kernel
+// time is one date's critical path.
+// ------------------------------------------------------------------------------------------
+typedef double v4d __attribute__((ext_vector_type(4)));
+
+template <int Q>
+constexpr size_t solve_lds_doubles(int Pseg) {
+  using L = Layout<Q, double>;
+  return (size_t)L::msize(Pseg) + (size_t)(Q + 4) * (Q + 4) + (size_t)L::ND * (L::ND + 1) +
+         (Q + 2) + Q + 2 * (((size_t)Pseg + 3) & ~(size_t)3);
+}
+
+// Constrained solve of date d by ONE wave (threadIdx.x < 64).  `sm` (LDS, solve_lds_doubles)
+// holds the date's moments in [0, msize(Pseg)) on entry.  Writes f (global), the residual
+// coefficients `co` [Q+1+P] (global or LDS), stats/status (global) and, if non-null, the
+// status word to `st_lds`.
+template <int Q>
+__device__ __forceinline__ void solve_body(double* sm, int d, int P, int Pseg, int pivot_mode,
+                                           double tol, double* __restrict__ fout,
+                                           double* co, double* __restrict__ stats,
+                                           int* __restrict__ status, int* st_lds) {
+  using L = Layout<Q, double>;
+  constexpr int NS = L::NS, NG = L::NG, NACC = L::NACC, ND = L::ND;
+  constexpr int NC = ND + 1;              // standardised industry row incl. the rhs
+  constexpr int CH = NC + 2;              // Gram channels: m (NC) | a | 1
+  constexpr int TT = (CH + 15) / 16;      // MFMA tiles per dimension
+  static_assert(TT <= 2, "Q <= 28");
+  const int lane = threadIdx.x;
+  const int K = 1 + P + Q;
+  const int MS = L::msize(Pseg);
+  const int P4 = (Pseg + 3) & ~3;         // industries padded to the MFMA k-step
+  double* acc = sm;                       // [NACC]
+  double* seg = sm + NACC;                // [Pseg][NS]  W, A_q, B, s
+  double* Gs = sm + MS;                   // [CH][CH]    Gram over industries
+  double* S = Gs + CH * CH;               // [ND][NC]    Schur complement | rhs
+  double* gpv = S + ND * NC;              // [NC]        standardised pivot row
+  double* muv = gpv + NC;                 // [Q]
+  double* ajv = muv + Q;                  // [P4]        a_j
+  double* iwv = ajv + P4;                 // [P4]        1 / W_j
+
+  const double Sc = acc[NG + 2 * Q + 0];
+  const double nval = acc[NG + 2 * Q + 3];
+  const double nq = nval * Q;
+  const double mx = acc[NG + 2 * Q + 1] / nq;
+  const double sigma = sqrt(fmax(acc[NG + 2 * Q + 2] / nq - mx * mx, 0.0));
+  const double isig = 1.0 / sigma;
+  const double iSc = 1.0 / Sc;
+  int st = 0;
+  if (!(nval > 0.0)) st |= XS_NO_ROWS;
+  if (!(sigma > 0.0) || !__builtin_isfinite(sigma)) st |= XS_BAD_SIGMA;
+
+  // pivot industry (reference: always the last one, CrossSection.py:69)
+  int jp = -1;
+  if (P > 0) {
+    if (pivot_mode == 1) {
+      jp = P - 1;
+    } else {
+      for (int jb = 0; jb < P; jb += 64) {
+        const int j = jb + lane;
+        const unsigned long long m = __ballot(j < P && seg[j * NS + Q + 2] > 0.0);
+        if (m) jp = jb + 63 - __builtin_clzll(m);
+      }
+      if (jp < 0) jp = P - 1;
+    }
+    if (!(seg[jp * NS + Q + 2] > 0.0)) st |= XS_PIVOT_EMPTY;
+  }
+  const int rp = P > 0 ? jp : 0;          // P == 0: the single segment holds the totals
+  const double sp = P > 0 ? seg[rp * NS + Q + 2] : 1.0;
+  const double rho = P > 0 ? seg[rp * NS] : 0.0;
+  const double isp = 1.0 / sp;
+
+  // this lane's Gram channels c = t*16 + (lane & 15): mean and pivot-row value
+  const int li = lane & 15, lk = lane >> 4;
+  double muc[TT], gpc[TT];
+#pragma unroll
+  for (int t = 0; t < TT; ++t) {
+    const int c = t * 16 + li;
+    muc[t] = (c >= 1 && c <= Q) ? acc[NG + Q + c - 1] * iSc : 0.0;
+    const double W = seg[rp * NS];
+    const double raw = c < NC ? seg[rp * NS + c] : 0.0;
+    gpc[t] = (c >= 1 && c <= Q) ? (raw - muc[t] * W) * isig : raw;
+    if (lk == 0 && c < NC) gpv[c] = gpc[t];
+    if (lk == 0 && c >= 1 && c <= Q) muv[c - 1] = muc[t];
+  }
+
+  // per-industry scalars once, lane-parallel: a_j and 1/W_j (0 for pivot / empty / padding)
+  for (int j = lane; j < P4; j += 64) {
+    const double W = j < P ? seg[j * NS] : 0.0;
+    const bool act = (j < P) && (j != jp) && (W > 0.0);
+    ajv[j] = act ? -seg[j * NS + Q + 2] * isp : 0.0;
+    iwv[j] = act ? 1.0 / W : 0.0;
+  }
+  wave_sync_lds();
+
+  // Gram over active industries: A = [m/W | a/W | 1], B = [m | a | 0]
+  v4d G[TT][TT];
+#pragma unroll
+  for (int ti = 0; ti < TT; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < TT; ++tj) G[ti][tj] = v4d{0.0, 0.0, 0.0, 0.0};
+#pragma unroll 4
+  for (int k0 = 0; k0 < P4; k0 += 4) {
+    const int j = k0 + lk;
+    const double* p = seg + (j < P ? j : 0) * NS;
+    const double W = p[0];
+    const double aj = ajv[j], iW = iwv[j];
+    const bool act = iW != 0.0;
+    double av[TT], bv[TT];
+#pragma unroll
+    for (int t = 0; t < TT; ++t) {
+      const int c = t * 16 + li;
+      const double raw = c < NC ? p[c] : 0.0;
+      const double g = (c >= 1 && c <= Q) ? (raw - muc[t] * W) * isig : raw;
+      const double m = g + aj * gpc[t];
+      const double v = c < NC ? m : (c == NC ? aj : 0.0);
+      bv[t] = act ? v : 0.0;
+      av[t] = act ? (c == NC + 1 ? 1.0 : v * iW) : 0.0;
+    }
+#pragma unroll
+    for (int ti = 0; ti < TT; ++ti)
+#pragma unroll
+      for (int tj = 0; tj < TT; ++tj)
+        G[ti][tj] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[ti], bv[tj], G[ti][tj], 0, 0, 0);
+  }
+#pragma unroll
+  for (int ti = 0; ti < TT; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < TT; ++tj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int i = ti * 16 + lk + 4 * r, w = tj * 16 + li;
+        if (i < CH && w < CH) Gs[i * CH + w] = G[ti][tj][r];
+      }
+  wave_sync_lds();
+
+  // uniform scalars; S = M_DD - G + kappa at at^T in the MFMA output layout
+  const double c0 = Gs[NC * CH + NC];
+  const double kappa = rho / (1.0 + rho * c0);
+  const double sa = Gs[(NC + 1) * CH + NC];  // sum of a_j over active industries
+  // industry totals of the standardised rows: sum_active m + (1 - sum a) g_p
+  auto tot = [&](int w) { return Gs[(NC + 1) * CH + w] + (1.0 - sa) * gpv[w]; };
+  const double Sw = tot(0);
+#pragma unroll
+  for (int ti = 0; ti < TT; ++ti)
+#pragma unroll
+    for (int tj = 0; tj < TT; ++tj)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int u = ti * 16 + lk + 4 * r, w = tj * 16 + li;
+        if (u >= ND || w >= NC) continue;
+        double m;
+        if (u == 0) {
+          m = tot(w);
+        } else if (w == 0) {
+          m = tot(u);
+        } else if (w == ND) {
+          m = acc[NG + u - 1] * isig - muv[u - 1] * isig * tot(ND);
+        } else {
+          const int q = u - 1, s2 = w - 1;
+          const int hi = q > s2 ? q : s2, lo = q > s2 ? s2 : q;
+          const double muq = muv[q], mus = muv[s2];
+          m = (acc[hi * (hi + 1) / 2 + lo] - muq * mus * Sw) * isig * isig -
+              (muq * tot(w) + mus * tot(u)) * isig;
+        }
+        S[u * NC + w] = m - G[ti][tj][r] + kappa * Gs[NC * CH + u] * Gs[NC * CH + w];
+      }
+  wave_sync_lds();
+
+  // Cholesky of the ND x ND Schur complement, right-looking (one dependent step per column),
+  // in registers, redundantly in every lane; 1/sqrt from v_rsq_f64 + two Newton steps.
+  double Lm[ND * (ND + 1) / 2], b[ND], dorig[ND], il[ND];
+#pragma unroll
+  for (int i = 0; i < ND; ++i) {
+#pragma unroll
+    for (int k = 0; k <= i; ++k) Lm[i * (i + 1) / 2 + k] = S[i * NC + k];
+    b[i] = S[i * NC + ND];
+    dorig[i] = Lm[i * (i + 1) / 2 + i];
+  }
+  double dmax = 0.0;
+#pragma unroll
+  for (int k = 0; k < ND; ++k) dmax = fmax(dmax, fabs(dorig[k]));
+  const double ztol = tol * dmax;
+#pragma unroll
+  for (int k = 0; k < ND; ++k) {
+    const double dk = Lm[k * (k + 1) / 2 + k];
+    if (!(dk > ztol)) {  // pinv semantics: drop the direction (exactly singular block)
+      st |= (dorig[k] > ztol) ? XS_NEAR_SINGULAR : XS_ZERO_PIVOT;
+      il[k] = 0.0;
+#pragma unroll
+      for (int i = k; i < ND; ++i) Lm[i * (i + 1) / 2 + k] = 0.0;
+      continue;
+    }
+    if (dk < 1e-12 * dorig[k]) st |= XS_NEAR_SINGULAR;
+    double y = __builtin_amdgcn_rsq(dk);
+    y = fma(0.5 * y, fma(-dk * y, y, 1.0), y);
+    y = fma(0.5 * y, fma(-dk * y, y, 1.0), y);
+    il[k] = y;
+    Lm[k * (k + 1) / 2 + k] = dk * y;
+#pragma unroll
+    for (int i = k + 1; i < ND; ++i) Lm[i * (i + 1) / 2 + k] *= y;
+#pragma unroll
+    for (int i = k + 1; i < ND; ++i)
+#pragma unroll
+      for (int c = k + 1; c <= i; ++c)
+        Lm[i * (i + 1) / 2 + c] = fma(-Lm[i * (i + 1) / 2 + k], Lm[c * (c + 1) / 2 + k],
+                                      Lm[i * (i + 1) / 2 + c]);
+  }
+#pragma unroll
+  for (int k = 0; k < ND; ++k) {  // L y = b, column-oriented (il = 0 zeroes dropped directions)
+    b[k] *= il[k];
+#pragma unroll
+    for (int i = k + 1; i < ND; ++i) b[i] = fma(-Lm[i * (i + 1) / 2 + k], b[k], b[i]);
+  }
+#pragma unroll
+  for (int k = ND - 1; k >= 0; --k) {  // L^T g = y
+    b[k] *= il[k];
+#pragma unroll
+    for (int i = 0; i < k; ++i) b[i] = fma(-Lm[k * (k + 1) / 2 + i], b[k], b[i]);
+  }
+
+  // industries: f_j = (m_j . h - kappa a_j z) / W_j with h = [-g_D, 1]; pivot f_p = z (1 - kappa c0)
+  double z = Gs[NC * CH + ND], gph = gpv[ND];
+#pragma unroll
+  for (int u = 0; u < ND; ++u) {
+    z = fma(-Gs[NC * CH + u], b[u], z);
+    gph = fma(-gpv[u], b[u], gph);
+  }
+  const bool bad = (st & XS_BAD) != 0;
+  double* fo = fout + (size_t)d * K;
+  for (int j = lane; j < P; j += 64) {
+    const double* p = seg + j * NS;
+    const double W = p[0];
+    double fj = 0.0;
+    if (j == jp) {
+      fj = z * (1.0 - kappa * c0);
+    } else if (W > 0.0) {
+      const double aj = -p[Q + 2] * isp;
+      double mh = p[ND];  // g_j . h  (g_j[ND] = B_j, h[ND] = 1)
+      mh = fma(-W, b[0], mh);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) mh = fma(-(p[1 + q] - muv[q] * W) * isig, b[1 + q], mh);
+      fj = (mh + aj * gph - kappa * aj * z) * iwv[j];
+    }
+    fo[1 + j] = bad ? qnan() : fj;
+    co[Q + 1 + j] = bad ? qnan() : fj;
+  }
+  if (lane == 0) fo[0] = bad ? qnan() : b[0];
+#pragma unroll
+  for (int q = 0; q < Q; ++q)
+    if (lane == q) {
+      fo[1 + P + q] = bad ? qnan() : b[1 + q];
+      co[q] = bad ? qnan() : b[1 + q] * isig;  // residual coefficients on RAW styles
+    }
+  if (lane == 0) {
+    double cst = b[0];
+#pragma unroll
+    for (int q = 0; q < Q; ++q) cst -= b[1 + q] * isig * muv[q];
+    co[Q] = bad ? qnan() : cst;
+    status[d] = st;
+    if (st_lds) *st_lds = st;
+  }
+  if (stats) {
+    double* sd = stats + (size_t)d * (Q + 2);
+    if (lane < Q) sd[lane] = muv[lane];
+    if (lane == Q) sd[Q] = sigma;
+    if (lane == Q + 1) sd[Q + 1] = nval;
+  }
+}
+
+template <int Q>
+__global__ __launch_bounds__(64) void xs_solve_kernel(const double* __restrict__ mom, int P,
+                                                      int Pseg, int pivot_mode, double tol,
+                                                      double* __restrict__ fout,
+                                                      double* __restrict__ coef,
+                                                      double* __restrict__ stats,
+                                                      int* __restrict__ status) {
+  extern __shared__ double sm[];
+  const int d = blockIdx.x;
+  const int lane = threadIdx.x;
+  const int MS = Layout<Q, double>::msize(Pseg);
+  const double* md = mom + (size_t)d * MS;
+  for (int i0 = 0; i0 < MS; i0 += 8 * 64) {  // 8 independent loads in flight per lane
+    double tmp[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * 64 + lane;
+      tmp[u] = i < MS ? md[i] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int i = i0 + u * 64 + lane;
+      if (i < MS) sm[i] = tmp[u];
+    }
+  }
+  wave_sync_lds();
+  solve_body<Q>(sm, d, P, Pseg, pivot_mode, tol, fout, coef + (size_t)d * (Q + 1 + P), stats,
+                status, nullptr);
+}
+
+// ------------------------------------------------------------------------------------------
+// K3: specific returns and R^2.
+// Residual-pass data of the last stocks, loaded by waves 1..3 while wave 0 solves (fused fp32
+// kernel, PRE): the pass then starts with 1536 stocks already in registers.
+// ------------------------------------------------------------------------------------------
+#ifndef MFA_XS_PREU
+#define MFA_XS_PREU 2
+#endif
+constexpr int kPreU = MFA_XS_PREU;
+constexpr int kPreStocks = 3 * 64 * 4 * kPreU;
+template <int Q>
+struct ResidPre {
+  float4 c4[kPreU], r4[kPreU], x4[kPreU][Q];
+  uint2 j4[kPreU];
+};
+
+template <int Q>
+__device__ __forceinline__ void resid_prefetch(const float* __restrict__ X,
+                                               const float* __restrict__ cap,
+                                               const float* __restrict__ ret,
+                                               const int16_t* __restrict__ ind, int d, int N,
+                                               ResidPre<Q>& pr) {
+  const int nlo = N > kPreStocks ? N - kPreStocks : 0;
+  const int t = threadIdx.x - 64;  // waves 1..3
+  const float* Xd = X + (size_t)d * Q * N;
+#pragma unroll
+  for (int u = 0; u < kPreU; ++u) {
+    const int n = nlo + t * 4 + u * 768;
+    if (n < N) {
+      pr.c4[u] = *(const float4*)(cap + (size_t)d * N + n);
+      pr.r4[u] = *(const float4*)(ret + (size_t)d * N + n);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) pr.x4[u][q] = *(const float4*)(Xd + (size_t)q * N + n);
+      pr.j4[u] = ind ? *(const uint2*)(ind + (size_t)d * N + n) : make_uint2(0u, 0u);
+    }
+  }
+}
+
+template <typename T, int V> struct VecT;
+template <> struct VecT<float, 4> { typedef float type __attribute__((ext_vector_type(4))); };
+template <> struct VecT<double, 2> { typedef double type __attribute__((ext_vector_type(2))); };
+template <int V> struct IdxVec;
+template <> struct IdxVec<4> { typedef short type __attribute__((ext_vector_type(4))); };
+template <> struct IdxVec<2> { typedef short type __attribute__((ext_vector_type(2))); };
+
+// Specific returns + R^2 of date d from the coefficients `cf_s` [Q+1+P] (LDS) by the whole
+// workgroup (<= 16 waves); `red` = 16 x 5 doubles of LDS.
+// PRE (fp32 only): waves 1..3 hold the last kPreStocks stocks in `pre` (resid_prefetch) and the
+// main loop covers [0, N - kPreStocks) only.
+// sums_out != nullptr: stock-sharded regression: write the 5 R^2 sums instead of R^2.
+template <int Q, typename T, bool PRE = false>
+__device__ __forceinline__ void resid_body(
+    const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
+    const int16_t* __restrict__ ind, int d, int N, int P, const double* cf_s, bool bad,
+    T* __restrict__ eout, double* __restrict__ r2out, double (*red)[5],
+    const ResidPre<Q>& pre = ResidPre<Q>{}, double* __restrict__ sums_out = nullptr) {
+  static_assert(!PRE || sizeof(T) == 4, "residual prefetch is the fp32 path");
+  constexpr int V = Stream<T>::VEC, U = Stream<T>::U;
+  typedef typename VecT<T, V>::type vec;
+  typedef typename IdxVec<V>::type ivec;
+  const int tid = threadIdx.x;
+  const int Pseg = P > 0 ? P : 1;
+  double beta[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) beta[q] = cf_s[q];
+  const double cst = cf_s[Q];
+  const double* fI = cf_s + Q + 1;
+  const T* Xd = X + (size_t)d * Q * N;
+  const T* cd = cap + (size_t)d * N;
+  const T* rd = ret + (size_t)d * N;
+  const int16_t* id = ind ? ind + (size_t)d * N : nullptr;
+  T* ed = eout ? eout + (size_t)d * N : nullptr;
+  double se = 0.0, see = 0.0, sr = 0.0, srr = 0.0, nn = 0.0;
+  // V consecutive stocks per thread (16-byte loads; N % 8 == 0 keeps rows aligned) and U
+  // iterations' loads issued before any is consumed: the pass is latency-bound otherwise.
+  const int step = blockDim.x * V;
+  auto one = [&](T c, T r, int j, const T (&xf)[Q]) -> T {
+    bool ok = (j >= 0) && (j < Pseg) && finite_v(c) && (c >= T(0)) && finite_v(r);
+    double e = (double)r - cst;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      ok = ok && finite_v(xf[q]);
+      e = fma(-beta[q], (double)xf[q], e);
+    }
+    T eo = (T)qnan();
+    if (ok) {
+      if (P > 0) e -= fI[j];
+      se += e;
+      see = fma(e, e, see);
+      sr += (double)r;
+      srr = fma((double)r, (double)r, srr);
+      nn += 1.0;
+      eo = (T)e;
+    }
+    return eo;
+  };
+  auto consume = [&](const vec& cv, const vec& rv, const vec (&xv)[Q], ivec jv, int n) {
+    vec eo;
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      T xf[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) xf[q] = xv[q][k];
+      eo[k] = one(cv[k], rv[k], (int)jv[k], xf);
+    }
+    if (ed) *(vec*)(ed + n) = eo;
+  };
+  int Nmain = N;
+  if constexpr (PRE) {
+    const int nlo = N > kPreStocks ? N - kPreStocks : 0;
+    Nmain = nlo;
+    if (tid >= 64) {
+#pragma unroll
+      for (int u = 0; u < kPreU; ++u) {
+        const int n = nlo + (tid - 64) * 4 + u * 768;
+        if (n < N) {
+          vec xv[Q];
+#pragma unroll
+          for (int q = 0; q < Q; ++q) xv[q] = __builtin_bit_cast(vec, pre.x4[u][q]);
+          const ivec jv = __builtin_bit_cast(ivec, pre.j4[u]);
+          consume(__builtin_bit_cast(vec, pre.c4[u]), __builtin_bit_cast(vec, pre.r4[u]), xv,
+                  jv, n);
+        }
+      }
+    }
+  }
+  // Blocks of U*step stocks walked from the END of the date: the moments pass streamed the
+  // tail last, so the re-read starts with the lines most likely still in the Infinity Cache.
+  const int nblk = (Nmain + U * step - 1) / (U * step);
+  for (int b = nblk - 1; b >= 0; --b) {
+    const int n0 = b * U * step + tid * V;
+    vec cv[U], rv[U], xv[U][Q];
+    ivec jv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int n = n0 + u * step;
+      if (n < Nmain) {
+        cv[u] = *(const vec*)(cd + n);
+        rv[u] = *(const vec*)(rd + n);
+#pragma unroll
+        for (int q = 0; q < Q; ++q) xv[u][q] = *(const vec*)(Xd + (size_t)q * N + n);
+        jv[u] = id ? *(const ivec*)(id + n) : ivec{};
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int n = n0 + u * step;
+      if (n < Nmain) consume(cv[u], rv[u], xv[u], jv[u], n);
+    }
+  }
+  se = wave_sum(se); see = wave_sum(see); sr = wave_sum(sr); srr = wave_sum(srr); nn = wave_sum(nn);
+  const int w = tid >> 6;
+  if ((tid & 63) == 0) {
+    red[w][0] = se; red[w][1] = see; red[w][2] = sr; red[w][3] = srr; red[w][4] = nn;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    double a = 0, b = 0, c = 0, e2 = 0, n = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+      a += red[i][0]; b += red[i][1]; c += red[i][2]; e2 += red[i][3]; n += red[i][4];
+    }
+    if (sums_out) {  // stock-sharded regression: the caller all-reduces, then forms R^2
+      double* so = sums_out + (size_t)d * 5;
+      so[0] = a; so[1] = b; so[2] = c; so[3] = e2; so[4] = n;
+    } else {
+      const double ve = b / n - (a / n) * (a / n);
+      const double vr = e2 / n - (c / n) * (c / n);
+      r2out[d] = bad ? qnan() : 1.0 - ve / vr;
+    }
+  }
+}
+
+template <int Q, typename T>
+__global__ __launch_bounds__(256) void xs_resid_kernel(
+    const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
+    const int16_t* __restrict__ ind, int D, int N, int P, const double* __restrict__ coef,
+    const int* __restrict__ status, T* __restrict__ eout, double* __restrict__ r2out,
+    double* __restrict__ sums_out = nullptr) {
+  __shared__ double cf_s[Q + 1 + 128];
+  __shared__ double red[16][5];
+  const int d = D - 1 - blockIdx.x;  // reverse: the MALL-resident tail of K1's stream first
+  const double* co = coef + (size_t)d * (Q + 1 + P);
+  for (int i = threadIdx.x; i < Q + 1 + P; i += blockDim.x) cf_s[i] = co[i];
+  __syncthreads();
+  resid_body<Q, T>(X, cap, ret, ind, d, N, P, cf_s, (status[d] & XS_BAD) != 0, eout, r2out, red,
+                   ResidPre<Q>{}, sums_out);
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused K1 -> K2 -> K3: one 4-wave workgroup per date streams the date's panel slice once
+// from HBM (moments), solves it in wave 0, then re-reads the slice for the residual pass.
+// Two workgroups fit per CU, so ~512 dates are in flight: the re-read is served mostly by the
+// 256 MB Infinity Cache instead of HBM, and the single-wave solve of one date overlaps the
+// other workgroup's streaming.
+// ------------------------------------------------------------------------------------------
+template <int Q, typename T>
+constexpr int fused_ring_bytes() {
+  constexpr int a = Ring<Q, T>::BYTES;
+  constexpr int b = (int)(solve_lds_doubles<Q>(128) * 8);
+  return a > b ? a : b;
+}
+
+template <int Q, int R, int VAR, bool PRE, typename T>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void xs_fused_kernel(
+    const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
+    const int16_t* __restrict__ ind, int N, int P, int Pseg, int pivot_mode, double tol,
+    double* __restrict__ fout, T* __restrict__ eout, double* __restrict__ r2out,
+    double* __restrict__ stats, int* __restrict__ status, double* __restrict__ mom_out) {
+  __shared__ __attribute__((aligned(16))) char ring[fused_ring_bytes<Q, T>()];
+  __shared__ double cf_s[Q + 1 + 128];
+  __shared__ double red[4][5];
+  __shared__ int st_s;
+  extern __shared__ double dyn[];
+  const int d = blockIdx.x;
+  double* sm = (double*)ring;  // moments, then the solve's scratch (ring is idle by then)
+  moments_body<Q, VAR & 35, R, T>(X, cap, ret, ind, N, Pseg, d, ring, dyn, sm);
+  if constexpr ((VAR & 8) != 0) {  // timing-only ablation: no solve
+    for (int i = threadIdx.x; i < Q + 1 + P; i += blockDim.x) cf_s[i] = sm[i] * 1e-30;
+    if (threadIdx.x == 0) st_s = 0;
+  } else if (threadIdx.x < 64) {
+    solve_body<Q>(sm, d, P, Pseg, pivot_mode, tol, fout, cf_s, stats, status, &st_s);
+    // near-singular date: export its moments for the device pseudo-inverse pass
+    if (mom_out && (__builtin_amdgcn_readfirstlane(st_s) & XS_NEAR_SINGULAR)) {
+      const int MS = Layout<Q, T>::msize(Pseg);
+      for (int i = threadIdx.x; i < MS; i += 64) mom_out[(size_t)d * MS + i] = sm[i];
+    }
+  }
+  ResidPre<Q> pre;
+  if constexpr (PRE) {
+    if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) != 0)
+      resid_prefetch<Q>(X, cap, ret, ind, d, N, pre);
+  }
+  __syncthreads();
+  if constexpr ((VAR & 4) == 0)
+    resid_body<Q, T, PRE>(X, cap, ret, ind, d, N, P, cf_s, (st_s & XS_BAD) != 0, eout, r2out,
+                          red, pre);
+  if constexpr ((VAR & 16) != 0) {  // timing-only: a second residual pass (cache-hit cost)
+    __syncthreads();
+    resid_body<Q, T>(X, cap, ret, ind, d, N, P, cf_s, (st_s & XS_BAD) != 0, eout, r2out, red);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Device pseudo-inverse refinement (pinv semantics of CrossSection.py:76,98) for dates the
+// Cholesky flagged near-singular (e.g. an exactly collinear style pair).  Grid D; a workgroup
+// whose date is not flagged exits at once, so the pass rides in the same stream / HIP graph as
+// the regression with no host synchronisation.  A flagged date rebuilds the reference's
+// constrained normal matrix A = R^T X^T W X R (Kr x Kr, Kr = K - 1 with industries) and rhs
+// from its exported raw moments, eigen-decomposes A with the one-wave Jacobi (jacobi.h), and
+// applies pinv(A) = V diag(1/lambda) V^T over |lambda| > 1e-15 max|lambda| (numpy's pinv rcond
+// on the singular values |lambda|).  f = R g, then the whole workgroup redoes the date's
+// specific returns and R^2.
+// ------------------------------------------------------------------------------------------
+constexpr int kXsRefineMaxK = 64;
+
+template <int Q>
+__host__ __device__ constexpr size_t refine_lds_doubles(int P) {
+  const int Pseg = P > 0 ? P : 1;
+  const int K = 1 + P + Q, Kr = P > 0 ? K - 1 : K;
+  return (size_t)Layout<Q, double>::msize(Pseg) + 2 * (size_t)Kr * (Kr + 1) + 4 * 64 +
+         4 * (size_t)Kr + (Q + 4);
+}
+
+template <int Q, typename T>
+__global__ __launch_bounds__(256) void xs_refine_kernel(
+    const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
+    const int16_t* __restrict__ ind, int N, int P, int pivot_mode,
+    const double* __restrict__ mom, double* __restrict__ fout, T* __restrict__ eout,
+    double* __restrict__ r2out, int* __restrict__ status) {
+  using L = Layout<Q, double>;
+  constexpr int NS = L::NS, NG = L::NG, NACC = L::NACC;
+  const int d = blockIdx.x;
+  const int st0 = status[d];
+  if (!(st0 & XS_NEAR_SINGULAR) || (st0 & XS_BAD)) return;  // uniform: whole workgroup exits
+  extern __shared__ double sm[];
+  __shared__ double cf_s[Q + 1 + 128];
+  __shared__ double red[4][5];
+  __shared__ double sc[4];   // W_tot, B_tot, sigma, s_pivot
+  __shared__ int piv_s;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int Pseg = P > 0 ? P : 1;
+  const int MS = L::msize(Pseg);
+  const int K = 1 + P + Q, Kr = P > 0 ? K - 1 : K, lda = Kr + 1;
+  double* md = sm;                 // [MS] raw moments
+  double* A = md + MS;             // [Kr][lda]
+  double* V = A + Kr * lda;        // [Kr][lda]
+  double* rot = V + Kr * lda;      // [4*64]
+  double* rhs = rot + 4 * 64;      // [Kr]
+  double* alp = rhs + Kr;          // [Kr]  constraint weights alpha_u
+  double* g = alp + Kr;            // [Kr]  eigen-space coefficients
+  double* mu = g + Kr;             // [Q]   cap-weighted style means
+  for (int i = tid; i < MS; i += blockDim.x) md[i] = mom[(size_t)d * MS + i];
+  __syncthreads();
+  const double* acc = md;
+  const double* seg = md + NACC;
+  if (tid == 0) {
+    double Wt = 0.0, Bt = 0.0;
+    for (int j = 0; j < Pseg; ++j) { Wt += seg[j * NS]; Bt += seg[j * NS + Q + 1]; }
+    const double nq = acc[NG + 2 * Q + 3] * Q;
+    const double mx = acc[NG + 2 * Q + 1] / nq;
+    sc[0] = Wt; sc[1] = Bt;
+    sc[2] = sqrt(fmax(acc[NG + 2 * Q + 2] / nq - mx * mx, 0.0));
+    int jp = -1;
+    if (P > 0) {
+      if (pivot_mode == 1) jp = P - 1;
+      else for (int j = 0; j < P; ++j) if (seg[j * NS + Q + 2] > 0.0) jp = j;
+      if (jp < 0) jp = P - 1;
+    }
+    piv_s = jp;
+    sc[3] = P > 0 ? seg[jp * NS + Q + 2] : 1.0;
+  }
+  if (tid < Q) mu[tid] = acc[NG + Q + tid] / acc[NG + 2 * Q];
+  __syncthreads();
+  const double Wt = sc[0], Bt = sc[1], sig = sc[2], isig = 1.0 / sig, sp = sc[3];
+  const int jp = piv_s;
+  // Aq_tot[q] = sum_j A_jq
+  auto aqt = [&](int q) {
+    double t = 0.0;
+    for (int j = 0; j < Pseg; ++j) t += seg[j * NS + 1 + q];
+    return t;
+  };
+  // entries of the full X^T W X over the ORIGINAL columns [country | industries | z-styles]
+  auto mfull = [&](int i, int j) -> double {
+    if (i > j) { const int t = i; i = j; j = t; }
+    const int s0 = 1 + P;
+    if (j < s0) {  // country / industry block
+      if (i == 0) return j == 0 ? Wt : seg[(j - 1) * NS];
+      return i == j ? seg[(i - 1) * NS] : 0.0;
+    }
+    const int qj = j - s0;
+    if (i == 0) return (aqt(qj) - mu[qj] * Wt) * isig;
+    if (i < s0) return (seg[(i - 1) * NS + 1 + qj] - mu[qj] * seg[(i - 1) * NS]) * isig;
+    const int qi = i - s0;
+    const int hi = qi > qj ? qi : qj, lo = qi > qj ? qj : qi;
+    return (acc[hi * (hi + 1) / 2 + lo] - mu[qi] * aqt(qj) - mu[qj] * aqt(qi) +
+            mu[qi] * mu[qj] * Wt) * isig * isig;
+  };
+  auto bfull = [&](int i) -> double {
+    const int s0 = 1 + P;
+    if (i == 0) return Bt;
+    if (i < s0) return seg[(i - 1) * NS + Q + 1];
+    const int q = i - s0;
+    return (acc[NG + q] - mu[q] * Bt) * isig;
+  };
+  const int pc = 1 + jp;  // pivot column (P > 0)
+  auto orig = [&](int u) { return (P > 0 && u >= pc) ? u + 1 : u; };
+  for (int u = tid; u < Kr; u += blockDim.x) {
+    const int ou = orig(u);
+    alp[u] = (P > 0 && ou >= 1 && ou <= P) ? -seg[(ou - 1) * NS + Q + 2] / sp : 0.0;
+  }
+  __syncthreads();
+  for (int e = tid; e < Kr * Kr; e += blockDim.x) {
+    const int u = e / Kr, v = e % Kr;
+    if (v < u) continue;
+    const int ou = orig(u), ov = orig(v);
+    double a = mfull(ou, ov);
+    if (P > 0) {
+      const double au = alp[u], av = alp[v];
+      a += au * mfull(pc, ov) + av * mfull(ou, pc) + au * av * mfull(pc, pc);
+    }
+    A[u * lda + v] = a;
+    A[v * lda + u] = a;
+  }
+  for (int u = tid; u < Kr; u += blockDim.x)
+    rhs[u] = bfull(orig(u)) + (P > 0 ? alp[u] * bfull(pc) : 0.0);
+  __syncthreads();
+  if (tid < 64) {
+    jacobi_wave(A, V, Kr, lda, rot, 40, 1e-17);
+    double lmax = 0.0;
+    for (int k = lane; k < Kr; k += 64) lmax = fmax(lmax, fabs(A[k * lda + k]));
+    lmax = wave_max(lmax);
+    const double cut = 1e-15 * lmax;
+    // c_k = (v_k . rhs) / lambda_k over the kept spectrum
+    for (int k = lane; k < Kr; k += 64) {
+      const double lk = A[k * lda + k];
+      double t = 0.0;
+      for (int i = 0; i < Kr; ++i) t = fma(V[i * lda + k], rhs[i], t);
+      g[k] = fabs(lk) > cut ? t / lk : 0.0;
+    }
+    wsync();
+    for (int i = lane; i < Kr; i += 64) {  // g <- V c
+      double t = 0.0;
+      for (int k = 0; k < Kr; ++k) t = fma(V[i * lda + k], g[k], t);
+      rot[i < 256 ? i : 0] = t;  // rot is free again: stage V c (Kr <= 64)
+    }
+    wsync();
+    // f in original order: f[orig(u)] = g[u], f[pivot] = sum_u alpha_u g[u]
+    double* fo = fout + (size_t)d * K;
+    double fp = 0.0;
+    for (int u = lane; u < Kr; u += 64) fp = fma(alp[u], rot[u], fp);
+    fp = wave_sum(fp);
+    for (int u = lane; u < Kr; u += 64) {
+      const int ou = orig(u);
+      fo[ou] = rot[u];
+      if (ou >= 1 && ou <= P) cf_s[Q + ou] = rot[u];          // industry f_j at Q + 1 + j
+      if (ou > P) cf_s[ou - 1 - P] = rot[u] * isig;           // raw-style coefficient
+    }
+    if (P > 0 && lane == 0) { fo[pc] = fp; cf_s[Q + pc] = fp; }
+    wsync();
+    if (lane == 0) {
+      double cst = rot[0];  // country (column 0 is never the pivot)
+      for (int q = 0; q < Q; ++q) cst -= cf_s[q] * mu[q];
+      cf_s[Q] = cst;
+      status[d] = st0 | XS_REFINED;
+    }
+  }
+  __syncthreads();
+  resid_body<Q, T>(X, cap, ret, ind, d, N, P, cf_s, false, eout, r2out, red);
+}
+
+constexpr int kXsDeterministic = 0x100;  // pivot_mode flag: bitwise-deterministic kernel
+constexpr int kXsRefine = 0x200;         // pivot_mode flag: device pinv pass for flagged dates
+
+template <int Q, typename T>
+size_t solve_lds_bytes(int Pseg) {
+  return solve_lds_doubles<Q>(Pseg) * sizeof(double);
+}
+
+template <int Q, int VAR, typename T>
+hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, int D, int N,
+                    int P, int pivot_mode, double tol, double* f, T* e, double* r2, double* stats,
+                    int* status, double* ws, hipStream_t s) {
+  using L = Layout<Q, T>;
+  const int Pseg = P > 0 ? P : 1;
+  const int MS = L::msize(Pseg);
+  const bool det = (pivot_mode & kXsDeterministic) != 0;
+  const bool refine = (pivot_mode & kXsRefine) != 0;
+  const int pm = pivot_mode & 0xff;
+  double* mom = ws;
+  double* coef = ws + (size_t)D * MS;
+  const size_t seg8 = (size_t)kRepMax * Pseg * L::NS * sizeof(double);
+  const bool rep8 = seg8 <= kSegLdsBudget;
+  const size_t lds1 = ((rep8 ? (size_t)kRepMax : 1) * Pseg * L::NS + L::NACC) * sizeof(double);
+  const size_t lds2 = solve_lds_bytes<Q, T>(Pseg);
+  if (lds1 + fused_ring_bytes<Q, T>() > 160 * 1024 || lds2 > 64 * 1024) return hipErrorInvalidValue;
+  if (refine && 1 + P + Q > kXsRefineMaxK) return hipErrorInvalidValue;
+  const int16_t* indp = P > 0 ? ind : nullptr;
+  constexpr bool PRE = sizeof(T) == 4;
+  const int mode = g_mfa_xs_mode;
+  if (det) {  // bitwise-reproducible variant of the default path
+    if (!rep8) return hipErrorNotSupported;
+    hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR | 32, PRE, T>), dim3(D), dim3(256), lds1,
+                       s, X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom);
+  } else if (mode == 0 && rep8) {
+    hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR, PRE, T>), dim3(D), dim3(256), lds1, s, X,
+                       cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom);
+  } else if (mode == 0 || mode == 7) {
+    if (rep8)
+      hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR, false, T>), dim3(D), dim3(256), lds1, s,
+                         X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom);
+    else
+      hipLaunchKernelGGL((xs_fused_kernel<Q, 1, VAR, false, T>), dim3(D), dim3(256), lds1, s, X,
+                         cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom);
+  } else {
+    if (rep8)
+      hipLaunchKernelGGL((xs_moments_kernel<Q, VAR, kRepMax, T>), dim3(D), dim3(256), lds1, s, X,
+                         cap, ret, indp, N, Pseg, mom);
+    else
+      hipLaunchKernelGGL((xs_moments_kernel<Q, VAR, 1, T>), dim3(D), dim3(256), lds1, s, X, cap,
+                         ret, indp, N, Pseg, mom);
+    hipLaunchKernelGGL(xs_solve_kernel<Q>, dim3(D), dim3(64), lds2, s, mom, P, Pseg, pm, tol, f,
+                       coef, stats, status);
+    if (!(VAR & 4))
+      hipLaunchKernelGGL((xs_resid_kernel<Q, T>), dim3(D), dim3(256), 0, s, X, cap, ret, indp, D,
+                         N, P, coef, status, e, r2);
+  }
+  if (refine) {
+    const size_t lds3 = refine_lds_doubles<Q>(P) * sizeof(double);
+    hipLaunchKernelGGL((xs_refine_kernel<Q, T>), dim3(D), dim3(256), lds3, s, X, cap, ret, indp,
+                       N, P, pm, mom, f, e, r2, status);
+  }
+  return hipGetLastError();
+}
+
+// Workspace bytes needed by the fused / split paths: D * (msize + Q + 1 + P) doubles.
+inline size_t xs_workspace_bytes(int D, int P, int Q) {
+  const int Pseg = P > 0 ? P : 1;
+  const size_t ms = (size_t)Q * (Q + 1) / 2 + 2 * Q + 4 + (size_t)Pseg * (Q + 3);
+  return (size_t)D * (ms + Q + 1 + P) * sizeof(double);
+}
+
+template <typename T>
+int xs_wls_dispatch(const T* X, const T* cap, const T* ret, const int16_t* ind, int D, int N,
+                    int P, int Q, int pivot_mode, double tol, double* f, T* e, double* r2,
+                    double* stats, int* status, void* ws, void* stream) {
+  if (D <= 0) return 0;
+  if (Q < 1 || Q > 16 || P < 0 || P > 128 || N <= 0 || (N % 8) != 0)
+    return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  double* w = (double*)ws;
+  switch (Q) {
+#define MFA_Q(qq)                                                                              \
+  case qq:                                                                                     \
+    return (int)launch_q<qq, 0, T>(X, cap, ret, ind, D, N, P, pivot_mode, tol, f, e, r2,       \
+                                   stats, status, w, s);
+    MFA_Q(1) MFA_Q(2) MFA_Q(3) MFA_Q(4) MFA_Q(5) MFA_Q(6) MFA_Q(7) MFA_Q(8)
+    MFA_Q(9) MFA_Q(10) MFA_Q(11) MFA_Q(12) MFA_Q(13) MFA_Q(14) MFA_Q(15) MFA_Q(16)
+#undef MFA_Q
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+// ------------------------------------------------------------------------------------------
+// Stock-sharded (TP) regression pieces, SURVEY.md §2.5: every rank streams ITS stocks of every
+// date into raw moments (additive: the caller all-reduces them), solves redundantly from the
+// summed moments, and forms its stocks' specific returns plus the five R^2 sums
+// [sum e, sum e^2, sum r, sum r^2, n] per date (all-reduced again by the caller).
+// what: 0 = moments, 1 = solve (type independent), 2 = residual sums.
+// ------------------------------------------------------------------------------------------
+template <int Q, typename T>
+hipError_t split_q(int what, const T* X, const T* cap, const T* ret, const int16_t* ind, int D,
+                   int N, int P, int pivot_mode, double tol, double* mom, double* f,
+                   double* coef, double* stats, int* status, T* e, double* sums, hipStream_t s) {
+  using L = Layout<Q, T>;
+  const int Pseg = P > 0 ? P : 1;
+  const int16_t* indp = P > 0 ? ind : nullptr;
+  if (what == 0) {
+    const size_t seg8 = (size_t)kRepMax * Pseg * L::NS * sizeof(double);
+    const bool rep8 = seg8 <= kSegLdsBudget;
+    const size_t lds1 = ((rep8 ? (size_t)kRepMax : 1) * Pseg * L::NS + L::NACC) * sizeof(double);
+    if (lds1 + Ring<Q, T>::BYTES > 160 * 1024) return hipErrorInvalidValue;
+    if (rep8)
+      hipLaunchKernelGGL((xs_moments_kernel<Q, 0, kRepMax, T>), dim3(D), dim3(256), lds1, s, X,
+                         cap, ret, indp, N, Pseg, mom);
+    else
+      hipLaunchKernelGGL((xs_moments_kernel<Q, 0, 1, T>), dim3(D), dim3(256), lds1, s, X, cap,
+                         ret, indp, N, Pseg, mom);
+  } else if (what == 1) {
+    const size_t lds2 = solve_lds_bytes<Q, T>(Pseg);
+    if (lds2 > 64 * 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(xs_solve_kernel<Q>, dim3(D), dim3(64), lds2, s, mom, P, Pseg, pivot_mode,
+                       tol, f, coef, stats, status);
+  } else {
+    hipLaunchKernelGGL((xs_resid_kernel<Q, T>), dim3(D), dim3(256), 0, s, X, cap, ret, indp, D, N,
+                       P, coef, status, e, (double*)nullptr, sums);
+  }
+  return hipGetLastError();
+}
+
+template <typename T>
+int split_dispatch(int what, const T* X, const T* cap, const T* ret, const int16_t* ind, int D,
+                   int N, int P, int Q, int pivot_mode, double tol, double* mom, double* f,
+                   double* coef, double* stats, int* status, T* e, double* sums, void* stream) {
+  if (D <= 0) return 0;
+  if (Q < 1 || Q > 16 || P < 0 || P > 128 || N < 0 || (N % 8) != 0)
+    return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  switch (Q) {
+#define MFA_Q(qq)                                                                              \
+  case qq:                                                                                     \
+    return (int)split_q<qq, T>(what, X, cap, ret, ind, D, N, P, pivot_mode, tol, mom, f, coef, \
+                               stats, status, e, sums, s);
+    MFA_Q(1) MFA_Q(2) MFA_Q(3) MFA_Q(4) MFA_Q(5) MFA_Q(6) MFA_Q(7) MFA_Q(8)
+    MFA_Q(9) MFA_Q(10) MFA_Q(11) MFA_Q(12) MFA_Q(13) MFA_Q(14) MFA_Q(15) MFA_Q(16)
+#undef MFA_Q
+  }
+  return (int)hipErrorInvalidValue;
+}
+
+inline size_t xs_moments_bytes(int P, int Q) {
+  const int Pseg = P > 0 ? P : 1;
+  return ((size_t)Q * (Q + 1) / 2 + 2 * Q + 4 + (size_t)Pseg * (Q + 3)) * sizeof(double);
+}
+
+}  // namespace

@@ -3,14 +3,17 @@
 The reference keeps one long pandas frame and boolean-mask-selects every date
 (``Barra-master/mfm/MFM.py:58``).  Here a panel is a set of dense device tensors:
 
-* ``styles`` [D, Q, N] float32 — style exposures, stocks contiguous per (date, style) so the
+* ``styles`` [D, Q, N] — style exposures, stocks contiguous per (date, style) so the
   regression kernel's loads are fully coalesced;
-* ``cap``, ``ret`` [D, N] float32 — capital (``circ_mv``) and t+1 return;
+* ``cap``, ``ret`` [D, N] — capital (``circ_mv``) and t+1 return;
 * ``ind`` [D, N] int16 — industry id in ``[0, P)``, ``-1`` where the stock is absent
   (ragged universes are masks, industries are ids — never one-hot columns).
 
-At N = 5000, D = 2520 (10y all-A) a panel is 0.6 GB: trivially resident in 288 GB of HBM3E,
-so every stage runs batched over all dates of a rank's shard.
+``styles`` / ``cap`` / ``ret`` share one storage dtype: float64 (the reference's own input
+precision: ``demo.py:21`` reads float64 CSV columns into ``CrossSection.reg``) or float32 (the
+factor pipeline's downcast, ``load_data.py:18-21``).  Regression math is float64 either way.
+At N = 5000, D = 2520 (10y all-A) an fp64 panel is 1.2 GB (fp32: 0.6 GB): trivially resident in
+288 GB of HBM3E, so every stage runs batched over all dates of a rank's shard.
 """
 from __future__ import annotations
 
@@ -22,9 +25,9 @@ import torch
 
 @dataclass
 class RiskPanel:
-    styles: torch.Tensor          # [D, Q, N] f32
-    cap: torch.Tensor             # [D, N] f32
-    ret: torch.Tensor             # [D, N] f32
+    styles: torch.Tensor          # [D, Q, N] f64 or f32
+    cap: torch.Tensor             # [D, N]    same dtype
+    ret: torch.Tensor             # [D, N]    same dtype
     ind: torch.Tensor | None      # [D, N] int16 or None (P == 0)
     P: int
     dates: np.ndarray             # [D] datetime64[ns]
@@ -54,6 +57,15 @@ class RiskPanel:
         return self.styles.device
 
     @property
+    def dtype(self) -> torch.dtype:
+        return self.styles.dtype
+
+    def astype(self, dtype) -> "RiskPanel":
+        """The same panel with styles / cap / ret stored in ``dtype``."""
+        return replace(self, styles=self.styles.to(dtype), cap=self.cap.to(dtype),
+                       ret=self.ret.to(dtype))
+
+    @property
     def factor_names(self) -> list[str]:
         ind = self.industry_names or [f"ind{j}" for j in range(self.P)]
         sty = self.style_names or [f"style{q}" for q in range(self.Q)]
@@ -74,7 +86,8 @@ class RiskPanel:
         return valid_mask(self.styles, self.cap, self.ret, self.ind, self.P)
 
     def nbytes(self) -> int:
-        n = self.styles.numel() * 4 + self.cap.numel() * 4 + self.ret.numel() * 4
+        e = self.styles.element_size()
+        n = (self.styles.numel() + self.cap.numel() + self.ret.numel()) * e
         return n + (0 if self.ind is None else self.ind.numel() * 2)
 
 
@@ -124,7 +137,7 @@ def business_days(D: int, start: str = "2010-01-04") -> np.ndarray:
 def synthetic_panel(D: int, N: int, P: int = 31, Q: int = 10, *, seed: int = 0,
                     device="cpu", missing_frac: float = 0.0, empty_industries: int = 0,
                     factor_vol: float = 0.01, noise_vol: float = 0.02,
-                    return_truth: bool = False):
+                    return_truth: bool = False, dtype=torch.float32):
     """Synthetic Barra panel with planted factor returns (the reference ships no data).
 
     * caps log-normal (``circ_mv``-like, 10k CNY units), styles N(0,1) with a per-style offset,
@@ -136,15 +149,16 @@ def synthetic_panel(D: int, N: int, P: int = 31, Q: int = 10, *, seed: int = 0,
     * returns follow ``r = f_c + f_ind + sum_q z_q f_q + eps`` on the z-scored styles, so the
       regression should recover the planted ``f`` up to noise.
 
-    Generation runs on ``device`` (a 5000 x 2520 panel is generated on the GPU in
-    milliseconds).
+    ``dtype`` is the storage dtype of styles / cap / ret (float64 draws are not rounded
+    through float32).  Generation runs on ``device`` (a 5000 x 2520 panel is generated on the
+    GPU in milliseconds).
     """
     g = torch.Generator(device=device)
     g.manual_seed(seed)
     dev = torch.device(device)
-    styles = torch.randn(D, Q, N, generator=g, device=dev)
-    styles += torch.linspace(-0.5, 0.5, Q, device=dev)[None, :, None]
-    cap = torch.exp(torch.randn(D, N, generator=g, device=dev) * 1.2 + 13.0)
+    styles = torch.randn(D, Q, N, generator=g, device=dev, dtype=dtype)
+    styles += torch.linspace(-0.5, 0.5, Q, device=dev, dtype=dtype)[None, :, None]
+    cap = torch.exp(torch.randn(D, N, generator=g, device=dev, dtype=dtype) * 1.2 + 13.0)
     if P > 0:
         # uneven industry sizes, stable per stock with occasional reclassification
         probs = torch.linspace(1.0, 3.0, P, device=dev)
@@ -178,7 +192,7 @@ def synthetic_panel(D: int, N: int, P: int = 31, Q: int = 10, *, seed: int = 0,
     if P > 0:
         r = r + f_true[:, 1:1 + P].gather(1, ind.long())
     r = r + torch.randn(D, N, generator=g, device=dev, dtype=torch.float64) * noise_vol
-    ret = r.float()
+    ret = r.to(dtype)
     if missing_frac > 0:
         miss = torch.rand(D, N, generator=g, device=dev) < missing_frac
         styles = styles.masked_fill(miss[:, None, :], float("nan"))

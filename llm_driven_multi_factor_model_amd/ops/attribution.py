@@ -24,6 +24,8 @@ from .cross_section import valid_mask
 _native.register("mfa_portfolio_exposure", [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                              C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                              C.c_int, C.c_void_p, C.c_void_p])
+_native.register("mfa_portfolio_exposure_f64", [C.c_void_p] * 6 + [C.c_int] * 4 +
+                 [C.c_void_p, C.c_void_p])
 
 
 def portfolio_exposure(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor,
@@ -41,15 +43,17 @@ def portfolio_exposure(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor,
         raise ValueError(f"h must be [D, N] = {(D, N)}, got {tuple(h.shape)}")
     if not X.is_cuda:
         return _portfolio_exposure_reference(X, cap, ret, ind, h, stats, P)
-    X = _native.check_device_tensor(X, torch.float32, "X")
-    cap = _native.check_device_tensor(cap, torch.float32, "cap")
-    ret = _native.check_device_tensor(ret, torch.float32, "ret")
+    dt = X.dtype if X.dtype == torch.float64 else torch.float32
+    X = _native.check_device_tensor(X, dt, "X")
+    cap = _native.check_device_tensor(cap, dt, "cap")
+    ret = _native.check_device_tensor(ret, dt, "ret")
     if P > 0:
         ind = _native.check_device_tensor(ind, torch.int16, "ind")
     h = h.contiguous()
     stats = stats.to(torch.float64).contiguous()
     out = torch.empty(D, K, dtype=torch.float64, device=X.device)
-    _native.call("mfa_portfolio_exposure", _native.ptr(X), _native.ptr(cap), _native.ptr(ret),
+    _native.call("mfa_portfolio_exposure_f64" if dt == torch.float64 else "mfa_portfolio_exposure",
+                 _native.ptr(X), _native.ptr(cap), _native.ptr(ret),
                  _native.ptr(ind if P > 0 else None), _native.ptr(h), _native.ptr(stats), D, N, P,
                  Q, _native.ptr(out), _native.stream(X.device))
     return out

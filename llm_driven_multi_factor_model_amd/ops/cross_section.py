@@ -12,9 +12,16 @@ Semantics follow ``Barra-master/mfm/CrossSection.py``:
 
 Ragged universes are expressed with ``ind < 0`` (absent stock) or any non-finite input.
 
-GPU tensors run the fused HIP kernel ``csrc/xs_wls.hip`` (one launch for all dates);
-CPU tensors run :func:`xs_wls_reference`, a dense float64 transcription of the reference
-formula (batched ``pinv``) that also serves as the numerics oracle for the kernel.
+Panels may be stored in float64 (the reference's own input precision: ``demo.py:21-35`` reads
+float64 CSV columns) or float32 (the factor pipeline's downcast, ``load_data.py:18-21``); the
+moments, the solve and every reduction are float64 either way, and specific returns come back
+in the storage dtype.
+
+GPU tensors run the fused HIP kernel (``csrc/xs_wls_impl.h``; ``mfa_xs_wls`` / ``mfa_xs_wls_f64``,
+one launch for all dates) followed, with ``refine=True``, by the device pseudo-inverse pass
+for near-singular dates (no host synchronisation).  CPU tensors run :func:`xs_wls_reference`,
+a dense float64 transcription of the reference formula (batched ``pinv``) that also serves as
+the numerics oracle for the kernel.
 """
 from __future__ import annotations
 
@@ -30,7 +37,10 @@ XS_PIVOT_EMPTY = 2
 XS_NEAR_SINGULAR = 4
 XS_ZERO_PIVOT = 8
 XS_BAD_SIGMA = 16
+XS_REFINED = 32          # re-solved by the device pseudo-inverse pass
 XS_DETERMINISTIC = 0x100  # pivot_mode flag of mfa_xs_wls: bitwise-deterministic kernel
+XS_REFINE = 0x200         # pivot_mode flag: device pinv pass for near-singular dates
+REFINE_MAX_K = 64         # largest K the device pinv pass holds in LDS (host fallback above)
 
 
 @dataclass
@@ -38,7 +48,7 @@ class XsResult:
     """Per-date regression outputs (all dates of the shard).
 
     f:      [D, K] float64 factor returns, K = 1 + P + Q (country, industries, styles)
-    resid:  [D, N] float32 specific returns (NaN where the stock is absent) or None
+    resid:  [D, N] specific returns in the panel's dtype (NaN where the stock is absent) or None
     r2:     [D]    float64 unweighted R^2
     stats:  [D, Q+2] float64 = (cap-weighted style means, pooled sigma, n_valid)
     status: [D]    int32 XS_* bit flags
@@ -72,11 +82,13 @@ def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Ten
            workspace: torch.Tensor | None = None, deterministic: bool = False) -> XsResult:
     """Regress every date of the panel in one batched call.
 
-    X [D,Q,N] f32 styles, cap/ret [D,N] f32, ind [D,N] int16 industry ids (or None if P == 0).
+    X [D,Q,N] styles, cap/ret [D,N] (all float64 or all float32), ind [D,N] int16 industry ids
+    (or None if P == 0).
     ``pivot_mode`` 0 eliminates the last NON-EMPTY industry (identical solution whenever the
     reference's choice is valid); 1 reproduces the reference exactly (always the last column,
     NaN when it is empty, quirk Q3).  ``refine`` re-solves dates the kernel flags as
-    near-singular with the pseudo-inverse reference path (pinv semantics, quirk Q4).
+    near-singular with the pseudo-inverse (pinv semantics, quirk Q4): on the GPU a device pass
+    in the same stream (eigen-pinv of the constrained normal matrix, K <= 64), no host sync.
     ``out`` / ``workspace`` let a caller (e.g. a timed loop) reuse preallocated buffers.
     The GPU kernels need N % 8 == 0 (16-byte rows for the LDS-DMA ring); other N are padded
     here with absent stocks (``ind = -1``), which costs a copy — keep panels padded.
@@ -89,9 +101,12 @@ def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Ten
     if not X.is_cuda:
         return xs_wls_reference(X, cap, ret, ind, P, pivot_mode=pivot_mode, want_resid=want_resid)
     dev = X.device
-    X = _native.check_device_tensor(X, torch.float32, "X")
-    cap = _native.check_device_tensor(cap, torch.float32, "cap")
-    ret = _native.check_device_tensor(ret, torch.float32, "ret")
+    dt = X.dtype
+    if dt not in (torch.float32, torch.float64):
+        raise TypeError(f"X: expected float32 or float64, got {dt}")
+    X = _native.check_device_tensor(X, dt, "X")
+    cap = _native.check_device_tensor(cap, dt, "cap")
+    ret = _native.check_device_tensor(ret, dt, "ret")
     if P > 0:
         ind = _native.check_device_tensor(ind, torch.int16, "ind")
     Np = (N + 7) // 8 * 8
@@ -105,26 +120,28 @@ def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Ten
     if out is None:
         out = XsResult(
             f=torch.empty(D, K, dtype=torch.float64, device=dev),
-            resid=torch.empty(D, N, dtype=torch.float32, device=dev) if want_resid else None,
+            resid=torch.empty(D, N, dtype=dt, device=dev) if want_resid else None,
             r2=torch.empty(D, dtype=torch.float64, device=dev),
             stats=torch.empty(D, Q + 2, dtype=torch.float64, device=dev),
             status=torch.empty(D, dtype=torch.int32, device=dev),
         )
     resid_buf = out.resid
     if resid_buf is not None and Np != N:
-        resid_buf = torch.empty(D, Np, dtype=torch.float32, device=dev)
+        resid_buf = torch.empty(D, Np, dtype=dt, device=dev)
     need = _native.query("mfa_xs_wls_workspace", D, P, Q)
     if workspace is None or workspace.numel() < need:
         workspace = torch.empty(need, dtype=torch.uint8, device=dev)
-    _native.call("mfa_xs_wls", _native.ptr(X), _native.ptr(cap), _native.ptr(ret),
-                 _native.ptr(ind if P > 0 else None), D, Np, P, Q,
-                 pivot_mode | (XS_DETERMINISTIC if deterministic else 0), tol,
+    dev_refine = refine and K <= REFINE_MAX_K
+    flags = (XS_DETERMINISTIC if deterministic else 0) | (XS_REFINE if dev_refine else 0)
+    _native.call("mfa_xs_wls_f64" if dt == torch.float64 else "mfa_xs_wls", _native.ptr(X),
+                 _native.ptr(cap), _native.ptr(ret),
+                 _native.ptr(ind if P > 0 else None), D, Np, P, Q, pivot_mode | flags, tol,
                  _native.ptr(out.f), _native.ptr(resid_buf), _native.ptr(out.r2),
                  _native.ptr(out.stats), _native.ptr(out.status), _native.ptr(workspace),
                  _native.stream(dev))
     if resid_buf is not None and Np != N:
         out.resid.copy_(resid_buf[:, :N])
-    if refine:
+    if refine and not dev_refine:  # K > 64: host pinv for the flagged dates (syncs)
         _refine_near_singular(X[..., :N], cap[:, :N], ret[:, :N], ind[:, :N] if P > 0 else None,
                               P, pivot_mode, out)
     return out
@@ -146,8 +163,9 @@ def _refine_near_singular(X, cap, ret, ind, P, pivot_mode, out: XsResult) -> Non
                            want_resid=out.resid is not None)
     out.f[bad] = sub.f.to(out.f.device)
     out.r2[bad] = sub.r2.to(out.r2.device)
+    out.status[bad] |= XS_REFINED
     if out.resid is not None:
-        out.resid[bad] = sub.resid.to(out.resid.device)
+        out.resid[bad] = sub.resid.to(out.resid.device, out.resid.dtype)
     del idx
 
 
@@ -238,7 +256,7 @@ def xs_wls_reference(X, cap, ret, ind, P, *, pivot_mode: int = 0, want_resid: bo
         r2 = 1.0 - ve / vr
         r2[bad] = float("nan")
         fs.append(f)
-        es.append(e.float())
+        es.append(e.to(X.dtype) if X.dtype in (torch.float32, torch.float64) else e.float())
         r2s.append(r2)
         stats_l.append(torch.cat([mu, sigma[:, None], n[:, None]], 1))
         sts.append(status)

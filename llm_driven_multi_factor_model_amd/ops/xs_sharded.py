@@ -34,6 +34,9 @@ _native.register("mfa_xs_moments", [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp
 _native.register("mfa_xs_solve", [_vp, _i, _i, _i, _i, _d, _vp, _vp, _vp, _vp, _vp])
 _native.register("mfa_xs_resid_sums", [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp])
 _native.register("mfa_xs_moments_bytes", [_i, _i])
+_native.register("mfa_xs_moments_f64", [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp])
+_native.register("mfa_xs_resid_sums_f64", [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp,
+                                           _vp])
 
 _BAD = XS_NO_ROWS | XS_BAD_SIGMA | XS_PIVOT_EMPTY
 
@@ -148,7 +151,7 @@ def _resid_cpu(X, cap, ret, ind, P, f_raw):
     em = torch.where(m, e, torch.zeros_like(e))
     r = torch.where(m, ret.double(), torch.zeros_like(e))
     sums = torch.stack([em.sum(1), (em * em).sum(1), r.sum(1), (r * r).sum(1), m.double().sum(1)], 1)
-    return e.float(), sums
+    return e.to(X.dtype) if X.dtype in (torch.float32, torch.float64) else e.float(), sums
 
 
 def _xs_sharded_cpu(X, cap, ret, ind, P, ctx, pivot_mode, want_resid):
@@ -176,9 +179,11 @@ def xs_wls_stock_sharded(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor,
         return _xs_sharded_cpu(X, cap, ret, ind, P, ctx, pivot_mode, want_resid)
     dev = X.device
     K = 1 + P + Q
-    X = _native.check_device_tensor(X, torch.float32, "X")
-    cap = _native.check_device_tensor(cap, torch.float32, "cap")
-    ret = _native.check_device_tensor(ret, torch.float32, "ret")
+    dt = X.dtype if X.dtype == torch.float64 else torch.float32
+    sfx = "_f64" if dt == torch.float64 else ""
+    X = _native.check_device_tensor(X, dt, "X")
+    cap = _native.check_device_tensor(cap, dt, "cap")
+    ret = _native.check_device_tensor(ret, dt, "ret")
     if P > 0:
         ind = _native.check_device_tensor(ind, torch.int16, "ind")
     Np = (N + 7) // 8 * 8  # 16-byte rows for the residual pass; padding = absent stocks
@@ -194,7 +199,7 @@ def xs_wls_stock_sharded(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor,
     mom = torch.empty(D, MS, dtype=torch.float64, device=dev)
     st = _native.stream(dev)
     iptr = _native.ptr(ip if P > 0 else None)
-    _native.call("mfa_xs_moments", _native.ptr(Xp), _native.ptr(cp), _native.ptr(rp), iptr, D, Np,
+    _native.call("mfa_xs_moments" + sfx, _native.ptr(Xp), _native.ptr(cp), _native.ptr(rp), iptr, D, Np,
                  P, Q, _native.ptr(mom), st)
     _all_reduce(mom, ctx)                                      # collective 1: D x msize fp64
     f = torch.empty(D, K, dtype=torch.float64, device=dev)
@@ -203,9 +208,9 @@ def xs_wls_stock_sharded(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor,
     status = torch.empty(D, dtype=torch.int32, device=dev)
     _native.call("mfa_xs_solve", _native.ptr(mom), D, P, Q, pivot_mode, tol, _native.ptr(f),
                  _native.ptr(coef), _native.ptr(stats), _native.ptr(status), st)
-    e = torch.empty(D, Np, dtype=torch.float32, device=dev) if want_resid else None
+    e = torch.empty(D, Np, dtype=dt, device=dev) if want_resid else None
     sums = torch.empty(D, 5, dtype=torch.float64, device=dev)
-    _native.call("mfa_xs_resid_sums", _native.ptr(Xp), _native.ptr(cp), _native.ptr(rp), iptr, D,
+    _native.call("mfa_xs_resid_sums" + sfx, _native.ptr(Xp), _native.ptr(cp), _native.ptr(rp), iptr, D,
                  Np, P, Q, _native.ptr(coef), _native.ptr(status), _native.ptr(e),
                  _native.ptr(sums), st)
     _all_reduce(sums, ctx)                                     # collective 2: D x 5 fp64
@@ -220,5 +225,5 @@ def xs_wls_stock_sharded(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor,
             out.f[bad] = sub.f.to(dev)
             out.r2[bad] = sub.r2.to(dev)
             if want_resid:
-                out.resid[bad] = sub.resid.to(dev)
+                out.resid[bad] = sub.resid.to(dev, out.resid.dtype)
     return out

@@ -30,7 +30,8 @@ def _pinned(t: torch.Tensor) -> torch.Tensor:
 def streamed_xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Tensor | None,
                     P: int, device: torch.device | str = "cuda", chunk: int = 512, depth: int = 3,
                     want_resid: bool = True, pivot_mode: int = 0, refine: bool = True) -> XsResult:
-    """Regress a HOST panel (X [D,Q,N] f32, cap/ret [D,N] f32, ind [D,N] int16) chunk by chunk.
+    """Regress a HOST panel (X [D,Q,N], cap/ret [D,N] in f64 or f32, ind [D,N] int16) chunk by
+    chunk.
 
     Returns host (pinned) tensors identical to ``xs_wls`` on the whole panel.  CPU ``device``
     runs the reference path directly.
@@ -43,25 +44,26 @@ def streamed_xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: 
     if chunk < 1 or depth < 1:
         raise ValueError("chunk and depth must be >= 1")
     chunk = min(chunk, D)
-    X, cap, ret = _pinned(X.contiguous()), _pinned(cap.contiguous()), _pinned(ret.contiguous())
+    dt = X.dtype if X.dtype == torch.float64 else torch.float32
+    X, cap, ret = (_pinned(t.to(dt).contiguous()) for t in (X, cap, ret))
     ind = _pinned(ind.contiguous()) if P > 0 else None
 
     pin = dict(dtype=torch.float64, pin_memory=True)
     res = XsResult(f=torch.empty(D, K, **pin),
-                   resid=torch.empty(D, N, dtype=torch.float32, pin_memory=True) if want_resid else None,
+                   resid=torch.empty(D, N, dtype=dt, pin_memory=True) if want_resid else None,
                    r2=torch.empty(D, **pin), stats=torch.empty(D, Q + 2, **pin),
                    status=torch.empty(D, dtype=torch.int32, pin_memory=True))
 
     nslot = min(depth, (D + chunk - 1) // chunk)
     dev_in, dev_out, ws = [], [], []
     for _ in range(nslot):
-        dev_in.append((torch.empty(chunk, Q, N, dtype=torch.float32, device=device),
-                       torch.empty(chunk, N, dtype=torch.float32, device=device),
-                       torch.empty(chunk, N, dtype=torch.float32, device=device),
+        dev_in.append((torch.empty(chunk, Q, N, dtype=dt, device=device),
+                       torch.empty(chunk, N, dtype=dt, device=device),
+                       torch.empty(chunk, N, dtype=dt, device=device),
                        torch.empty(chunk, N, dtype=torch.int16, device=device) if P > 0 else None))
         dev_out.append(XsResult(
             f=torch.empty(chunk, K, dtype=torch.float64, device=device),
-            resid=torch.empty(chunk, N, dtype=torch.float32, device=device) if want_resid else None,
+            resid=torch.empty(chunk, N, dtype=dt, device=device) if want_resid else None,
             r2=torch.empty(chunk, dtype=torch.float64, device=device),
             stats=torch.empty(chunk, Q + 2, dtype=torch.float64, device=device),
             status=torch.empty(chunk, dtype=torch.int32, device=device)))

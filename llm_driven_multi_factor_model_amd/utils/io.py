@@ -50,8 +50,11 @@ def mfm_frame(barra: pd.DataFrame, industry_info: pd.DataFrame) -> pd.DataFrame:
 
 
 def panel_from_frame(data: pd.DataFrame, P: int, Q: int, device="cpu",
-                     industry_from_onehot: bool = True) -> RiskPanel:
+                     industry_from_onehot: bool = True, dtype=torch.float64) -> RiskPanel:
     """Dense panel from the MFM positional frame ([date, stocknames, capital, ret, P inds, Q styles]).
+
+    ``dtype`` = panel storage: float64 (default) keeps the frame's values exactly as the
+    reference regresses them (``demo.py:21`` -> ``CrossSection.reg``); float32 halves HBM.
 
     Positional contract of ``MFM.py:36,61`` (quirk Q13).  Rows whose industry one-hot is all
     zero cannot be expressed as an industry id and are dropped with a warning (the reference
@@ -62,15 +65,16 @@ def panel_from_frame(data: pd.DataFrame, P: int, Q: int, device="cpu",
     names = data.iloc[:, 1].astype(str).values
     s_codes, s_uni = pd.factorize(names, sort=True)
     D, N = len(d_uni), len(s_uni)
-    cap = np.full((D, N), np.nan, dtype=np.float32)
-    ret = np.full((D, N), np.nan, dtype=np.float32)
-    sty = np.full((D, Q, N), np.nan, dtype=np.float32)
+    npdt = np.float64 if dtype == torch.float64 else np.float32
+    cap = np.full((D, N), np.nan, dtype=npdt)
+    ret = np.full((D, N), np.nan, dtype=npdt)
+    sty = np.full((D, Q, N), np.nan, dtype=npdt)
     ind = np.full((D, N), -1, dtype=np.int16)
     if pd.Index(d_codes * N + s_codes).has_duplicates:
         warnings.warn("duplicate (date, stock) rows: keeping the last occurrence")
-    cap[d_codes, s_codes] = data.iloc[:, 2].values.astype(np.float32)
-    ret[d_codes, s_codes] = data.iloc[:, 3].values.astype(np.float32)
-    styles = data.iloc[:, data.shape[1] - Q:].values.astype(np.float32)
+    cap[d_codes, s_codes] = data.iloc[:, 2].values.astype(npdt)
+    ret[d_codes, s_codes] = data.iloc[:, 3].values.astype(npdt)
+    styles = data.iloc[:, data.shape[1] - Q:].values.astype(npdt)
     for q in range(Q):
         sty[d_codes, q, s_codes] = styles[:, q]
     if P > 0:
@@ -109,8 +113,11 @@ def _unique_s16(a: np.ndarray):
     return uniq[order], rank[codes]
 
 
-def panel_from_barra_csv(path: str, industry_info_path: str, device="cpu") -> RiskPanel:
+def panel_from_barra_csv(path: str, industry_info_path: str, device="cpu",
+                         dtype=torch.float64) -> RiskPanel:
     """barra_data_csi.csv + industry_info.csv -> dense panel (demo.py:22-35 semantics).
+
+    ``dtype`` = panel storage; float64 (default) is the reference's precision (pd.read_csv).
 
     Fast path: the native reader's columnar buffers are factorised directly (no per-row Python
     objects); falls back to pandas + :func:`mfm_frame`.
@@ -122,7 +129,7 @@ def panel_from_barra_csv(path: str, industry_info_path: str, device="cpu") -> Ri
     if cols is None:
         barra = read_barra_csv(path)
         frame = mfm_frame(barra, info)
-        return panel_from_frame(frame, len(info), barra.shape[1] - 5, device=device)
+        return panel_from_frame(frame, len(info), barra.shape[1] - 5, device=device, dtype=dtype)
     names = list(cols)
     styles = names[5:]
     Q = len(styles)
@@ -143,9 +150,10 @@ def panel_from_barra_csv(path: str, industry_info_path: str, device="cpu") -> Ri
     d_uni, d_codes = _unique_s16(cols["date"][sel])
     s_uni, s_codes = _unique_s16(cols["stocknames"][sel])
     D, N = len(d_uni), len(s_uni)
-    cap = np.full((D, N), np.nan, dtype=np.float32)
-    ret = np.full((D, N), np.nan, dtype=np.float32)
-    sty = np.full((D, Q, N), np.nan, dtype=np.float32)
+    npdt = np.float64 if dtype == torch.float64 else np.float32
+    cap = np.full((D, N), np.nan, dtype=npdt)
+    ret = np.full((D, N), np.nan, dtype=npdt)
+    sty = np.full((D, Q, N), np.nan, dtype=npdt)
     ind = np.full((D, N), -1, dtype=np.int16)
     flat = d_codes * N + s_codes
     cap.reshape(-1)[flat] = cols["capital"][sel]
@@ -166,7 +174,7 @@ def panel_from_barra_csv(path: str, industry_info_path: str, device="cpu") -> Ri
 
 def panel_from_mongo(db, factors_collection: str = "barra_factors",
                      industry_collection: str = "sw_industry_info_for_factors",
-                     device="cpu") -> RiskPanel:
+                     device="cpu", dtype=torch.float64) -> RiskPanel:
     """Mongo-driven risk run (``Barra-master/demo.ipynb#c1``): the ``barra_factors`` collection
     written by ``Barra_factor_cal/main.py:150`` and its industry table
     (``sw_industry_info_for_factors``, ``main.py:153``) -> dense panel, with demo.py's NaN-row
@@ -182,7 +190,7 @@ def panel_from_mongo(db, factors_collection: str = "barra_factors",
         raise ValueError(f"{factors_collection} lacks columns {missing}")
     barra = barra[cols]
     frame = mfm_frame(barra, info)
-    return panel_from_frame(frame, len(info), barra.shape[1] - 5, device=device)
+    return panel_from_frame(frame, len(info), barra.shape[1] - 5, device=device, dtype=dtype)
 
 
 def write_barra_csv(df: pd.DataFrame, path: str) -> None:

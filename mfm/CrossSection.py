@@ -79,9 +79,10 @@ class CrossSection:
     def _tensors(self, dev):
         if self.Q < 1:
             raise ValueError("at least one style factor is required")
-        X = torch.from_numpy(self._raw_styles.T.astype(np.float32))[None].to(dev)
-        cap = torch.from_numpy(np.asarray(self.capital, dtype=np.float32))[None].to(dev)
-        ret = torch.from_numpy(np.asarray(self.ret, dtype=np.float32))[None].to(dev)
+        # float64 storage: the reference regresses its float64 inputs as they are
+        X = torch.from_numpy(np.ascontiguousarray(self._raw_styles.T))[None].to(dev)
+        cap = torch.from_numpy(np.asarray(self.capital, dtype=np.float64))[None].to(dev)
+        ret = torch.from_numpy(np.asarray(self.ret, dtype=np.float64))[None].to(dev)
         ind = None
         if self.P > 0:
             oh = np.asarray(self.industry_factors)

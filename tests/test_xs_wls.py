@@ -35,17 +35,43 @@ def run_ref(ref, base, sty, oh):
 
 
 @pytest.mark.reference
-@pytest.mark.parametrize("P,Q,N", [(5, 3, 60), (0, 4, 40), (12, 10, 300)])
+@pytest.mark.parametrize("P,Q,N", [(5, 3, 60), (0, 4, 40), (12, 10, 300), (31, 10, 500)])
 def test_oracle_matches_reference_crosssection(ref, P, Q, N):
-    panel = synthetic_panel(4, N, P, Q, seed=P * 10 + Q, missing_frac=0.05)
+    """Unrounded float64 inputs (the reference's precision): f, e, R^2 at 1e-9 or better."""
+    panel = synthetic_panel(4, N, P, Q, seed=P * 10 + Q, missing_frac=0.05, dtype=torch.float64)
     res = X.xs_wls_reference(panel.styles, panel.cap, panel.ret, panel.ind, P)
+    assert res.resid.dtype == torch.float64
+    for d in range(panel.D):
+        base, sty, oh, m = ref_date_inputs(panel, d)
+        f, e, expo, r2 = run_ref(ref, base, sty, oh)
+        np.testing.assert_allclose(res.f[d].numpy(), f, rtol=1e-9, atol=1e-13)
+        np.testing.assert_allclose(res.resid[d].numpy()[m], e, rtol=1e-9, atol=1e-13)
+        assert abs(res.r2[d].item() - r2) < 1e-12
+        assert np.all(np.isnan(res.resid[d].numpy()[~m]))
+
+
+@pytest.mark.reference
+def test_collinear_styles_and_singleton_industry_match_reference_pinv(ref):
+    """An exactly duplicated style column (rank-deficient style block) and a one-stock industry:
+    the reference's pinv gives the minimum-norm solution (CrossSection.py:76)."""
+    panel = _degenerate_panel()
+    res = X.xs_wls_reference(panel.styles, panel.cap, panel.ret, panel.ind, panel.P)
     for d in range(panel.D):
         base, sty, oh, m = ref_date_inputs(panel, d)
         f, e, expo, r2 = run_ref(ref, base, sty, oh)
         np.testing.assert_allclose(res.f[d].numpy(), f, rtol=1e-9, atol=1e-12)
-        np.testing.assert_allclose(res.resid[d].numpy()[m], e, rtol=1e-5, atol=1e-7)
         assert abs(res.r2[d].item() - r2) < 1e-10
-        assert np.all(np.isnan(res.resid[d].numpy()[~m]))
+
+
+def _degenerate_panel(D=3, N=400, P=6, Q=4, seed=21, device="cpu"):
+    p = synthetic_panel(D, N, P, Q, seed=seed, dtype=torch.float64)
+    p.styles[:, 3] = p.styles[:, 1]            # exactly collinear styles
+    ind = p.ind.clone()
+    ind[:, 0] = 2                              # industry 2 keeps ...
+    ind[ind == 2] = 1
+    ind[:, 0] = 2                              # ... exactly one stock
+    p.ind = ind
+    return p.to(device)
 
 
 @pytest.mark.reference
@@ -100,16 +126,44 @@ def test_last_industry_empty_pivot_modes():
     (3, 64, 3, 1, 0.0, 0),
     (5, 600, 100, 8, 0.01, 2),
 ])
-def test_kernel_matches_oracle(cuda, D, N, P, Q, miss, empty):
-    panel = synthetic_panel(D, N, P, Q, seed=D + N, missing_frac=miss, empty_industries=empty)
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_kernel_matches_oracle(cuda, D, N, P, Q, miss, empty, dtype):
+    panel = synthetic_panel(D, N, P, Q, seed=D + N, missing_frac=miss, empty_industries=empty,
+                            dtype=dtype)
     ref = X.xs_wls_reference(panel.styles, panel.cap, panel.ret, panel.ind, P)
     g = panel.to(cuda)
     out = X.xs_wls(g.styles, g.cap, g.ret, g.ind, P)
     torch.cuda.synchronize()
-    torch.testing.assert_close(out.f.cpu(), ref.f, rtol=1e-8, atol=1e-11)
+    assert out.resid.dtype == dtype
+    torch.testing.assert_close(out.f.cpu(), ref.f, rtol=1e-9, atol=1e-12)
     torch.testing.assert_close(out.r2.cpu(), ref.r2, rtol=1e-9, atol=1e-11)
-    torch.testing.assert_close(out.resid.cpu(), ref.resid, rtol=1e-4, atol=1e-6, equal_nan=True)
+    if dtype == torch.float64:
+        torch.testing.assert_close(out.resid.cpu(), ref.resid, rtol=1e-9, atol=1e-13, equal_nan=True)
+    else:
+        torch.testing.assert_close(out.resid.cpu(), ref.resid, rtol=1e-4, atol=1e-6, equal_nan=True)
     torch.testing.assert_close(out.stats.cpu(), ref.stats, rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_device_pinv_refine_matches_oracle(cuda):
+    """Near-singular dates (duplicated style, singleton industry) are re-solved on the device
+    by the eigen pseudo-inverse pass: f matches the pinv oracle (== reference pinv, see
+    test_collinear_styles_and_singleton_industry_match_reference_pinv) to 1e-9, no host sync."""
+    p = _degenerate_panel(D=5, N=800, P=8, Q=5, seed=4)
+    ref = X.xs_wls_reference(p.styles, p.cap, p.ret, p.ind, p.P)
+    g = p.to(cuda)
+    out = X.xs_wls(g.styles, g.cap, g.ret, g.ind, p.P)
+    torch.cuda.synchronize()
+    st = out.status.cpu()
+    assert ((st & X.XS_REFINED) != 0).all(), st
+    torch.testing.assert_close(out.f.cpu(), ref.f, rtol=1e-9, atol=1e-12)
+    torch.testing.assert_close(out.r2.cpu(), ref.r2, rtol=1e-9, atol=1e-12)
+    torch.testing.assert_close(out.resid.cpu(), ref.resid, rtol=1e-9, atol=1e-12, equal_nan=True)
+    # fp32 storage and the three-kernel path take the same device refinement
+    g32 = g.astype(torch.float32)
+    o32 = X.xs_wls(g32.styles, g32.cap, g32.ret, g32.ind, p.P)
+    ref32 = X.xs_wls_reference(g32.styles.cpu(), g32.cap.cpu(), g32.ret.cpu(), g32.ind.cpu(), p.P)
+    torch.testing.assert_close(o32.f.cpu(), ref32.f, rtol=1e-8, atol=1e-11)
 
 
 @pytest.mark.gpu
