@@ -28,7 +28,10 @@ _SIGS: dict[str, list] = {
     # xs_wls.hip
     "mfa_xs_wls": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _d, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "mfa_xs_wls_f64": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _i, _d, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
-    "mfa_xs_wls_workspace": [_i, _i, _i],
+    "mfa_xs_wls_workspace": [_i, _i, _i, _i],
+    "mfa_xs_chunks": [_i, _i],
+    "mfa_xs_set_chunks": [_i],
+    "mfa_xs_set_mode": [_i],
     "mfa_xs_wls_variant": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
 }
 

@@ -3,14 +3,24 @@
 #include "xs_wls_impl.h"
 
 int g_mfa_xs_mode = 0;
+int g_mfa_xs_chunks = 0;
 
 // Ablation: 0 = fused single-kernel path with the residual prefetch during the wave-0 solve
 // (default), 1 = three separate kernels, 7 = fused without the prefetch.  Applies to both the
 // fp32 and fp64 entry points.
 MFA_API void mfa_xs_set_mode(int mode) { g_mfa_xs_mode = mode; }
 
-// Workspace bytes needed by mfa_xs_wls / mfa_xs_wls_f64: D * (msize + Q + 1 + P) doubles.
-MFA_API size_t mfa_xs_wls_workspace(int D, int P, int Q) { return xs_workspace_bytes(D, P, Q); }
+// Stock chunks per date for the next calls: 0 = automatic (default; chunked when a launch has
+// fewer than 1024 dates), > 0 = forced chunk count, < 0 = always one workgroup per date.
+MFA_API void mfa_xs_set_chunks(int S) { g_mfa_xs_chunks = S; }
+
+// Chunks per date the next mfa_xs_wls / mfa_xs_wls_f64 call on (D, N) will use.
+MFA_API int mfa_xs_chunks(int D, int N) { return xs_chunks(D, N); }
+
+// Workspace bytes needed by mfa_xs_wls / mfa_xs_wls_f64 on (D, N, P, Q).
+MFA_API size_t mfa_xs_wls_workspace(int D, int N, int P, int Q) {
+  return xs_workspace_bytes(D, N, P, Q);
+}
 
 // X: [D][Q][N] fp32 styles, cap/ret: [D][N] fp32, ind: [D][N] int16 industry id (<0 = absent;
 // may be null when P == 0).  N must be a multiple of 8 (16-byte aligned rows; pad with absent

@@ -34,6 +34,8 @@
 // 0 = fused single kernel (fp32: with the residual prefetch during the solve), 1 = three
 // separate kernels (ablation / large-P fallback), 7 = fused without the prefetch.
 extern int g_mfa_xs_mode;
+// Stock chunks per date: 0 = automatic (chunked below kXsChunkMinD dates), > 0 forced, < 0 never.
+extern int g_mfa_xs_chunks;
 
 namespace {
 
@@ -189,7 +191,8 @@ __device__ __forceinline__ constexpr int dma_per_tile(bool has_ind) {
   return (sizeof(T) == 4 ? Q + 2 : (Q + 3) / 2) + (has_ind ? 1 : 0);
 }
 
-// Moments of date d.  `ring` = Ring<Q,T>::BYTES of LDS, `dyn` = [Pseg*NS][R] replicated
+// Moments of stocks [nb, ne) of date d (a chunk, or the whole date with nb = 0, ne = N; nb is
+// a multiple of 64).  `ring` = Ring<Q,T>::BYTES of LDS, `dyn` = [Pseg*NS][R] replicated
 // segment sums | [NACC] totals (LDS), `md` = msize(Pseg) doubles out (global memory or LDS that
 // does not alias `dyn`; may alias `ring`).  Ends with a workgroup barrier.
 //
@@ -202,8 +205,9 @@ template <int Q, int VAR, int R, typename T>
 __device__ __forceinline__ void moments_body(
     const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
     const int16_t* __restrict__ ind, int N, int Pseg, int d, char* ring, double* dyn,
-    double* md) {
+    double* md, int nb = 0, int ne = -1, double* __restrict__ gout = nullptr) {
   using L = Layout<Q, T>;
+  if (ne < 0) ne = N;
   constexpr int NS = L::NS, NG = L::NG, NACC = L::NACC;
   constexpr int WSLOT = Ring<Q, T>::WSLOT, RINGW = Ring<Q, T>::RINGW, NB = Ring<Q, T>::NB;
   constexpr int ROWB = L::ROWB;
@@ -228,13 +232,13 @@ __device__ __forceinline__ void moments_body(
 
   char* wring = ring + wid * RINGW;
   const int nrows = dma_per_tile<Q, T>(id != nullptr);  // DMA instructions per tile
-  const int ntile_all = (N + kWT - 1) / kWT;
+  const int ntile_all = (ne - nb + kWT - 1) / kWT;
   const int ntile = ntile_all > wid ? (ntile_all - wid + nw - 1) / nw : 0;  // this wave's tiles
   auto issue = [&](int i) {
     char* slot = wring + (i % NB) * WSLOT;
-    const int s0 = (wid + i * nw) * kWT;
+    const int s0 = nb + (wid + i * nw) * kWT;
     if constexpr (sizeof(T) == 4) {
-      const bool in = s0 + lane < N;
+      const bool in = s0 + lane < ne;
       if (in) glds4(cd + s0 + lane, slot);
       if (in) glds4(rd + s0 + lane, slot + ROWB);
 #pragma unroll
@@ -243,7 +247,7 @@ __device__ __forceinline__ void moments_body(
     } else {
       // two 512-B fp64 rows per instruction: lanes 0-31 -> row rr, lanes 32-63 -> row rr + 1
       const int half = lane >> 5, s = s0 + 2 * (lane & 31);
-      const bool in = s < N;  // N is even: both stocks of the pair exist
+      const bool in = s < ne;  // ne is even: both stocks of the pair exist
 #pragma unroll
       for (int rr = 0; rr < Q + 2; rr += 2) {
         const int row = rr + half;
@@ -251,7 +255,7 @@ __device__ __forceinline__ void moments_body(
         if (in && row < Q + 2) glds16(src + s, slot + rr * ROWB);
       }
     }
-    if (id && lane < kWT / 2 && s0 + 2 * lane < N) glds4(id + s0 + 2 * lane, slot + (Q + 2) * ROWB);
+    if (id && lane < kWT / 2 && s0 + 2 * lane < ne) glds4(id + s0 + 2 * lane, slot + (Q + 2) * ROWB);
   };
   for (int i = 0; i < NB - 1 && i < ntile; ++i) issue(i);
   for (int i = 0; i < ntile; ++i) {
@@ -261,13 +265,13 @@ __device__ __forceinline__ void moments_body(
     if (i + NB - 1 < ntile) issue(i + NB - 1);
     const char* slot = wring + (i % NB) * WSLOT;
     const T* bf = (const T*)slot;
-    const int s = (wid + i * nw) * kWT + lane;
+    const int s = nb + (wid + i * nw) * kWT + lane;
     const T cf = bf[lane], rf = bf[kWT + lane];
     const int j = id ? (int)((const int16_t*)(slot + (Q + 2) * ROWB))[lane] : 0;
     T xf[Q];
 #pragma unroll
     for (int q = 0; q < Q; ++q) xf[q] = bf[(2 + q) * kWT + lane];
-    bool ok = (s < N) && (j >= 0) && (j < Pseg) && finite_v(cf) && (cf >= T(0)) && finite_v(rf);
+    bool ok = (s < ne) && (j >= 0) && (j < Pseg) && finite_v(cf) && (cf >= T(0)) && finite_v(rf);
 #pragma unroll
     for (int q = 0; q < Q; ++q) ok = ok && finite_v(xf[q]);
     if (ok) {
@@ -320,29 +324,38 @@ __device__ __forceinline__ void moments_body(
       for (int w = 0; w < nw; ++w) t += ((const double*)(ring + w * RINGW + 8 * 65 * 8))[tid];
     __syncthreads();  // md may alias the ring
     if (tid < NACC) md[tid] = t;
+    if (gout && tid < NACC) gout[tid] = t;
   } else {
     wg_reduce<NACC>(v, (double*)wring, acc);
     __syncthreads();
-    for (int i = tid; i < NACC; i += nthr) md[i] = acc[i];
+    for (int i = tid; i < NACC; i += nthr) {
+      const double t = acc[i];
+      md[i] = t;
+      if (gout) gout[i] = t;
+    }
   }
   for (int i = tid; i < Pseg * NS; i += nthr) {
     double t = 0.0;
 #pragma unroll
     for (int r = 0; r < R; ++r) t += dyn[i * R + r];
     md[NACC + i] = t;
+    if (gout) gout[NACC + i] = t;
   }
   __syncthreads();
 }
 
+// Grid D * S: workgroup b handles stock chunk s = b % S ([s*C, min(N, s*C + C))) of date
+// d = b / S and writes its partial moments to mom[b] (S = 1: the whole date).
 template <int Q, int VAR, int R, typename T>
 __global__ __launch_bounds__(256) void xs_moments_kernel(
     const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
-    const int16_t* __restrict__ ind, int N, int Pseg, double* __restrict__ mom) {
+    const int16_t* __restrict__ ind, int N, int Pseg, int S, int C, double* __restrict__ mom) {
   __shared__ __attribute__((aligned(16))) char ring[Ring<Q, T>::BYTES];
   extern __shared__ double dyn[];
-  const int d = blockIdx.x;
+  const int b = blockIdx.x, d = b / S, sc = b - d * S;
+  const int nb = sc * C, ne = min(N, nb + C);
   moments_body<Q, VAR, R, T>(X, cap, ret, ind, N, Pseg, d, ring, dyn,
-                             mom + (size_t)d * Layout<Q, T>::msize(Pseg));
+                             mom + (size_t)b * Layout<Q, T>::msize(Pseg), nb, ne);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -375,7 +388,7 @@ constexpr size_t solve_lds_doubles(int Pseg) {
 // holds the date's moments in [0, msize(Pseg)) on entry.  Writes f (global), the residual
 // coefficients `co` [Q+1+P] (global or LDS), stats/status (global) and, if non-null, the
 // status word to `st_lds`.
-template <int Q>
+template <int Q, bool ROWL = false>
 __device__ __forceinline__ void solve_body(double* sm, int d, int P, int Pseg, int pivot_mode,
                                            double tol, double* __restrict__ fout,
                                            double* co, double* __restrict__ stats,
@@ -527,9 +540,13 @@ __device__ __forceinline__ void solve_body(double* sm, int d, int P, int Pseg, i
       }
   wave_sync_lds();
 
-  // Cholesky of the ND x ND Schur complement, right-looking (one dependent step per column),
-  // in registers, redundantly in every lane; 1/sqrt from v_rsq_f64 + two Newton steps.
-  double Lm[ND * (ND + 1) / 2], b[ND], dorig[ND], il[ND];
+  // Cholesky of the ND x ND Schur complement, right-looking (one dependent step per column).
+  // Default: in registers, redundantly in every lane (shortest chain); ROWL: row per lane with
+  // readlane broadcasts (one row of registers instead of the triangle, for the low-VGPR
+  // MFMA-moments kernel).  1/sqrt from v_rsq_f64 + two Newton steps.
+  double b[ND];
+  if constexpr (!ROWL) {
+  double Lm[ND * (ND + 1) / 2], dorig[ND], il[ND];
 #pragma unroll
   for (int i = 0; i < ND; ++i) {
 #pragma unroll
@@ -577,6 +594,70 @@ __device__ __forceinline__ void solve_body(double* sm, int d, int P, int Pseg, i
     b[k] *= il[k];
 #pragma unroll
     for (int i = 0; i < k; ++i) b[i] = fma(-Lm[k * (k + 1) / 2 + i], b[k], b[i]);
+  }
+  } else {
+  // Cholesky of the ND x ND Schur complement, right-looking, ROW PER LANE: lane i < ND keeps
+  // row i of L (ND doubles) and the pivot column is broadcast by readlane, so the register
+  // footprint is one row, not the whole triangle (which set the kernel's VGPR count).  L is
+  // staged in LDS (over S, already consumed) for the column-oriented back substitution.
+  double Li[ND], bi = 0.0, dori = 0.0;
+#pragma unroll
+  for (int k = 0; k < ND; ++k) Li[k] = (lane < ND && k <= lane) ? S[lane * NC + k] : 0.0;
+  if (lane < ND) {
+    bi = S[lane * NC + ND];
+    dori = S[lane * NC + lane];
+  }
+  double dmax = 0.0;
+#pragma unroll
+  for (int k = 0; k < ND; ++k) dmax = fmax(dmax, fabs(readlane(dori, k)));
+  const double ztol = tol * dmax;
+  double il[ND];
+#pragma unroll
+  for (int k = 0; k < ND; ++k) {
+    const double dk = readlane(Li[k], k);
+    const double dok = readlane(dori, k);
+    if (!(dk > ztol)) {  // pinv semantics: drop the direction (exactly singular block)
+      st |= (dok > ztol) ? XS_NEAR_SINGULAR : XS_ZERO_PIVOT;
+      il[k] = 0.0;
+      if (lane >= k) Li[k] = 0.0;
+      continue;
+    }
+    if (dk < 1e-12 * dok) st |= XS_NEAR_SINGULAR;
+    double y = __builtin_amdgcn_rsq(dk);
+    y = fma(0.5 * y, fma(-dk * y, y, 1.0), y);
+    y = fma(0.5 * y, fma(-dk * y, y, 1.0), y);
+    il[k] = y;
+    if (lane == k) Li[k] = dk * y;
+    else if (lane > k) Li[k] *= y;
+#pragma unroll
+    for (int c = k + 1; c < ND; ++c) {
+      const double lck = readlane(Li[k], c);
+      if (lane >= c) Li[c] = fma(-Li[k], lck, Li[c]);
+    }
+  }
+  // L y = b (column oriented; il = 0 zeroes dropped directions): lane i holds b_i / y_i
+#pragma unroll
+  for (int k = 0; k < ND; ++k) {
+    const double yk = readlane(bi, k) * il[k];
+    if (lane == k) bi = yk;
+    else if (lane > k) bi = fma(-Li[k], yk, bi);
+  }
+  wave_sync_lds();
+  double* Ls = S;  // [ND][ND] row-major L (S is consumed)
+  if (lane < ND) {
+#pragma unroll
+    for (int k = 0; k < ND; ++k) Ls[lane * ND + k] = Li[k];
+  }
+  wave_sync_lds();
+  // L^T g = y: g_k = (y_k - sum_{i>k} L[i][k] g_i) il_k ; lane i keeps its running value
+#pragma unroll
+  for (int k = ND - 1; k >= 0; --k) {
+    const double gk = readlane(bi, k) * il[k];
+    if (lane == k) bi = gk;
+    else if (lane < k) bi = fma(-Ls[k * ND + lane], gk, bi);
+  }
+#pragma unroll
+  for (int k = 0; k < ND; ++k) b[k] = readlane(bi, k);  // the solution, wave-uniform
   }
 
   // industries: f_j = (m_j . h - kappa a_j z) / W_j with h = [-g_D, 1]; pivot f_p = z (1 - kappa c0)
@@ -628,8 +709,30 @@ __device__ __forceinline__ void solve_body(double* sm, int d, int P, int Pseg, i
   }
 }
 
+// Sum of the S partial-moment rows of date d in chunk order (deterministic) into LDS `sm`.
 template <int Q>
-__global__ __launch_bounds__(64) void xs_solve_kernel(const double* __restrict__ mom, int P,
+__device__ __forceinline__ void load_moments(const double* __restrict__ mom, int d, int S,
+                                             int Pseg, double* sm) {
+  const int MS = Layout<Q, double>::msize(Pseg);
+  const double* md = mom + (size_t)d * S * MS;
+  for (int i0 = (int)threadIdx.x; i0 < MS; i0 += 4 * (int)blockDim.x) {
+    double tmp[4] = {0.0, 0.0, 0.0, 0.0};  // 4 independent load chains per lane
+    for (int sc = 0; sc < S; ++sc)
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = i0 + u * (int)blockDim.x;
+        if (i < MS) tmp[u] += md[(size_t)sc * MS + i];
+      }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = i0 + u * (int)blockDim.x;
+      if (i < MS) sm[i] = tmp[u];
+    }
+  }
+}
+
+template <int Q>
+__global__ __launch_bounds__(64) void xs_solve_kernel(const double* __restrict__ mom, int S, int P,
                                                       int Pseg, int pivot_mode, double tol,
                                                       double* __restrict__ fout,
                                                       double* __restrict__ coef,
@@ -637,22 +740,7 @@ __global__ __launch_bounds__(64) void xs_solve_kernel(const double* __restrict__
                                                       int* __restrict__ status) {
   extern __shared__ double sm[];
   const int d = blockIdx.x;
-  const int lane = threadIdx.x;
-  const int MS = Layout<Q, double>::msize(Pseg);
-  const double* md = mom + (size_t)d * MS;
-  for (int i0 = 0; i0 < MS; i0 += 8 * 64) {  // 8 independent loads in flight per lane
-    double tmp[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = i0 + u * 64 + lane;
-      tmp[u] = i < MS ? md[i] : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const int i = i0 + u * 64 + lane;
-      if (i < MS) sm[i] = tmp[u];
-    }
-  }
+  load_moments<Q>(mom, d, S, Pseg, sm);
   wave_sync_lds();
   solve_body<Q>(sm, d, P, Pseg, pivot_mode, tol, fout, coef + (size_t)d * (Q + 1 + P), stats,
                 status, nullptr);
@@ -696,28 +784,54 @@ __device__ __forceinline__ void resid_prefetch(const float* __restrict__ X,
   }
 }
 
-template <typename T, int V> struct VecT;
-template <> struct VecT<float, 4> { typedef float type __attribute__((ext_vector_type(4))); };
-template <> struct VecT<double, 2> { typedef double type __attribute__((ext_vector_type(2))); };
-template <int V> struct IdxVec;
-template <> struct IdxVec<4> { typedef short type __attribute__((ext_vector_type(4))); };
-template <> struct IdxVec<2> { typedef short type __attribute__((ext_vector_type(2))); };
+// Residual-pass vector types: HIP's float4 / double2 (16-byte rows) and packed int16 ids.
+// (With clang ext_vector types instead, hipcc scheduled a full vmcnt(0) drain at the top of
+// every residual iteration: +30 us on the fp32 step.)
+template <typename T> struct RVec;
+template <> struct RVec<float> {
+  typedef float4 vec;
+  typedef uint2 ivec;
+  static __device__ __forceinline__ void unpack(const vec& v, float (&a)[4]) {
+    a[0] = v.x; a[1] = v.y; a[2] = v.z; a[3] = v.w;
+  }
+  static __device__ __forceinline__ void unpack(const ivec& v, int (&a)[4]) {
+    a[0] = (int)(short)(v.x & 0xFFFF); a[1] = (int)(short)(v.x >> 16);
+    a[2] = (int)(short)(v.y & 0xFFFF); a[3] = (int)(short)(v.y >> 16);
+  }
+  static __device__ __forceinline__ vec pack(const float (&a)[4]) {
+    return make_float4(a[0], a[1], a[2], a[3]);
+  }
+  static __device__ __forceinline__ ivec izero() { return make_uint2(0u, 0u); }
+};
+template <> struct RVec<double> {
+  typedef double2 vec;
+  typedef unsigned ivec;
+  static __device__ __forceinline__ void unpack(const vec& v, double (&a)[2]) { a[0] = v.x; a[1] = v.y; }
+  static __device__ __forceinline__ void unpack(const ivec& v, int (&a)[2]) {
+    a[0] = (int)(short)(v & 0xFFFF); a[1] = (int)(short)(v >> 16);
+  }
+  static __device__ __forceinline__ vec pack(const double (&a)[2]) { return make_double2(a[0], a[1]); }
+  static __device__ __forceinline__ ivec izero() { return 0u; }
+};
 
 // Specific returns + R^2 of date d from the coefficients `cf_s` [Q+1+P] (LDS) by the whole
 // workgroup (<= 16 waves); `red` = 16 x 5 doubles of LDS.
 // PRE (fp32 only): waves 1..3 hold the last kPreStocks stocks in `pre` (resid_prefetch) and the
 // main loop covers [0, N - kPreStocks) only.
 // sums_out != nullptr: stock-sharded regression: write the 5 R^2 sums instead of R^2.
-template <int Q, typename T, bool PRE = false>
+template <int Q, typename T, bool PRE = false, int UU = 0>
 __device__ __forceinline__ void resid_body(
     const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
     const int16_t* __restrict__ ind, int d, int N, int P, const double* cf_s, bool bad,
     T* __restrict__ eout, double* __restrict__ r2out, double (*red)[5],
-    const ResidPre<Q>& pre = ResidPre<Q>{}, double* __restrict__ sums_out = nullptr) {
+    const ResidPre<Q>& pre = ResidPre<Q>{}, double* __restrict__ sums_out = nullptr, int nb = 0,
+    int ne = -1) {
   static_assert(!PRE || sizeof(T) == 4, "residual prefetch is the fp32 path");
-  constexpr int V = Stream<T>::VEC, U = Stream<T>::U;
-  typedef typename VecT<T, V>::type vec;
-  typedef typename IdxVec<V>::type ivec;
+  if (ne < 0) ne = N;
+  constexpr int V = Stream<T>::VEC, U = UU > 0 ? UU : Stream<T>::U;
+  using RV = RVec<T>;
+  typedef typename RV::vec vec;
+  typedef typename RV::ivec ivec;
   const int tid = threadIdx.x;
   const int Pseg = P > 0 ? P : 1;
   double beta[Q];
@@ -754,18 +868,24 @@ __device__ __forceinline__ void resid_body(
     }
     return eo;
   };
-  auto consume = [&](const vec& cv, const vec& rv, const vec (&xv)[Q], ivec jv, int n) {
-    vec eo;
+  auto compute = [&](const vec& cv, const vec& rv, const vec (&xv)[Q], ivec jv) -> vec {
+    T cs[V], rs[V], xs[Q][V], eo[V];
+    int js[V];
+    RV::unpack(cv, cs);
+    RV::unpack(rv, rs);
+    RV::unpack(jv, js);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) RV::unpack(xv[q], xs[q]);
 #pragma unroll
     for (int k = 0; k < V; ++k) {
       T xf[Q];
 #pragma unroll
-      for (int q = 0; q < Q; ++q) xf[q] = xv[q][k];
-      eo[k] = one(cv[k], rv[k], (int)jv[k], xf);
+      for (int q = 0; q < Q; ++q) xf[q] = xs[q][k];
+      eo[k] = one(cs[k], rs[k], js[k], xf);
     }
-    if (ed) *(vec*)(ed + n) = eo;
+    return RV::pack(eo);
   };
-  int Nmain = N;
+  int Nmain = ne;
   if constexpr (PRE) {
     const int nlo = N > kPreStocks ? N - kPreStocks : 0;
     Nmain = nlo;
@@ -774,23 +894,23 @@ __device__ __forceinline__ void resid_body(
       for (int u = 0; u < kPreU; ++u) {
         const int n = nlo + (tid - 64) * 4 + u * 768;
         if (n < N) {
-          vec xv[Q];
-#pragma unroll
-          for (int q = 0; q < Q; ++q) xv[q] = __builtin_bit_cast(vec, pre.x4[u][q]);
-          const ivec jv = __builtin_bit_cast(ivec, pre.j4[u]);
-          consume(__builtin_bit_cast(vec, pre.c4[u]), __builtin_bit_cast(vec, pre.r4[u]), xv,
-                  jv, n);
+          const vec eo = compute(pre.c4[u], pre.r4[u], pre.x4[u], pre.j4[u]);
+          if (ed) *(vec*)(ed + n) = eo;
         }
       }
     }
   }
   // Blocks of U*step stocks walked from the END of the date: the moments pass streamed the
   // tail last, so the re-read starts with the lines most likely still in the Infinity Cache.
-  const int nblk = (Nmain + U * step - 1) / (U * step);
-  for (int b = nblk - 1; b >= 0; --b) {
-    const int n0 = b * U * step + tid * V;
-    vec cv[U], rv[U], xv[U][Q];
-    ivec jv[U];
+  // Software-pipelined: block b-1's loads are issued before block b's specific returns are
+  // stored, and the store data lives in its own registers, so no iteration waits for the
+  // previous one's stores to drain (register reuse of store data made hipcc insert
+  // vmcnt(1..2) waits at the top of every iteration: +30 us on the fp32 step).
+  const int nblk = (Nmain - nb + U * step - 1) / (U * step);
+  vec cv[U], rv[U], xv[U][Q];
+  ivec jv[U];
+  auto load_blk = [&](int b) {
+    const int n0 = nb + b * U * step + tid * V;
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int n = n0 + u * step;
@@ -799,13 +919,26 @@ __device__ __forceinline__ void resid_body(
         rv[u] = *(const vec*)(rd + n);
 #pragma unroll
         for (int q = 0; q < Q; ++q) xv[u][q] = *(const vec*)(Xd + (size_t)q * N + n);
-        jv[u] = id ? *(const ivec*)(id + n) : ivec{};
+        jv[u] = id ? *(const ivec*)(id + n) : RV::izero();
       }
     }
+  };
+  if (nblk > 0) load_blk(nblk - 1);
+  for (int b = nblk - 1; b >= 0; --b) {
+    const int n0 = nb + b * U * step + tid * V;
+    vec eo[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int n = n0 + u * step;
-      if (n < Nmain) consume(cv[u], rv[u], xv[u], jv[u], n);
+      if (n < Nmain) eo[u] = compute(cv[u], rv[u], xv[u], jv[u]);
+    }
+    if (b > 0) load_blk(b - 1);
+    if (ed) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int n = n0 + u * step;
+        if (n < Nmain) *(vec*)(ed + n) = eo[u];
+      }
     }
   }
   se = wave_sum(se); see = wave_sum(see); sr = wave_sum(sr); srr = wave_sum(srr); nn = wave_sum(nn);
@@ -819,8 +952,8 @@ __device__ __forceinline__ void resid_body(
     for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
       a += red[i][0]; b += red[i][1]; c += red[i][2]; e2 += red[i][3]; n += red[i][4];
     }
-    if (sums_out) {  // stock-sharded regression: the caller all-reduces, then forms R^2
-      double* so = sums_out + (size_t)d * 5;
+    if (sums_out) {  // chunk / stock-shard partial sums: R^2 is formed after the combine
+      double* so = sums_out;
       so[0] = a; so[1] = b; so[2] = c; so[3] = e2; so[4] = n;
     } else {
       const double ve = b / n - (a / n) * (a / n);
@@ -830,20 +963,315 @@ __device__ __forceinline__ void resid_body(
   }
 }
 
+// Grid D * S (dates in reverse: the MALL-resident tail of K1's stream first).  S = 1 and no
+// sums_out: R^2 per date; otherwise the five R^2 sums of chunk s go to sums_out[d * S + s].
 template <int Q, typename T>
 __global__ __launch_bounds__(256) void xs_resid_kernel(
     const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
-    const int16_t* __restrict__ ind, int D, int N, int P, const double* __restrict__ coef,
-    const int* __restrict__ status, T* __restrict__ eout, double* __restrict__ r2out,
-    double* __restrict__ sums_out = nullptr) {
+    const int16_t* __restrict__ ind, int D, int N, int P, int S, int C,
+    const double* __restrict__ coef, const int* __restrict__ status, T* __restrict__ eout,
+    double* __restrict__ r2out, double* __restrict__ sums_out = nullptr) {
   __shared__ double cf_s[Q + 1 + 128];
   __shared__ double red[16][5];
-  const int d = D - 1 - blockIdx.x;  // reverse: the MALL-resident tail of K1's stream first
+  const int b = (int)(gridDim.x - 1 - blockIdx.x), d = b / S, sc = b - d * S;
+  const int nb = sc * C, ne = min(N, nb + C);
   const double* co = coef + (size_t)d * (Q + 1 + P);
   for (int i = threadIdx.x; i < Q + 1 + P; i += blockDim.x) cf_s[i] = co[i];
   __syncthreads();
   resid_body<Q, T>(X, cap, ret, ind, d, N, P, cf_s, (status[d] & XS_BAD) != 0, eout, r2out, red,
-                   ResidPre<Q>{}, sums_out);
+                   ResidPre<Q>{}, sums_out ? sums_out + (size_t)b * 5 : nullptr, nb, ne);
+}
+
+// R^2 of every date from its S chunk sums [sum e, sum e^2, sum r, sum r^2, n], in chunk order.
+__global__ __launch_bounds__(256) void xs_r2_combine_kernel(const double* __restrict__ sums, int D,
+                                                            int S, const int* __restrict__ status,
+                                                            double* __restrict__ r2out) {
+  const int d = blockIdx.x * blockDim.x + threadIdx.x;
+  if (d >= D) return;
+  double a = 0, b = 0, c = 0, e2 = 0, n = 0;
+  for (int sc = 0; sc < S; ++sc) {
+    const double* p = sums + ((size_t)d * S + sc) * 5;
+    a += p[0]; b += p[1]; c += p[2]; e2 += p[3]; n += p[4];
+  }
+  const double ve = b / n - (a / n) * (a / n);
+  const double vr = e2 / n - (c / n) * (c / n);
+  r2out[d] = (status[d] & XS_BAD) ? qnan() : 1.0 - ve / vr;
+}
+
+// ------------------------------------------------------------------------------------------
+// K1 on the matrix cores: the dense moments as ONE 16 x 16 fp64 MFMA accumulator per wave.
+//
+// Lane l owns Gram channel c = l & 15 and, per k-step, stock k0 + (l >> 4) of its 64-stock
+// tile: v_mfma_f64_16x16x4f64 accumulates G[i][j] += sum_k alpha_i(k) beta_j(k) over 4 stocks
+// with (for a valid stock, weight w = sqrt(cap); invalid stocks contribute 0):
+//   channel  c < Q : alpha = x_c,  beta = w x_c        -> G[p][q] = Swxx,  G[p][Q] = Swxr
+//            c = Q : alpha = r,    beta = w r           G[p][Q+1] = Scx (beta = w w = cap)
+//          c = Q+1 : alpha = w,    beta = w w           G[Q+2][Q+1] = Sc, G[Q+2][Q+2] = n
+//          c = Q+2 : alpha = 1,    beta = 1             G[p][Q+2] summed over p = Sx
+//          c = Q+3 : alpha = sum_q x_q^2, beta = 0      G[Q+3][Q+2] = Sxx
+// The 79 per-lane fp64 accumulators of the VALU body (158 VGPRs: 2 waves / SIMD) become 8
+// VGPRs per lane, so 3-4 workgroups fit on a CU.  A per-stock prep pass (lane = stock) checks
+// validity, does the industry segment atomics and writes {w or -1, sum x^2} to a per-wave aux
+// row; ring rows are padded (+8 B fp32 / +16 B fp64) so the 16 channel reads of one k-step hit
+// distinct LDS banks.  The 4 waves' accumulators are summed in wave order (deterministic).
+// ------------------------------------------------------------------------------------------
+template <typename T> struct MfGeo;
+template <> struct MfGeo<float> {
+  static constexpr int ROWP = kWT * 4 + 8;    // padded fp32 row
+  static constexpr int NB = 2;                // ring slots per wave
+};
+template <> struct MfGeo<double> {
+  static constexpr int ROWP = kWT * 8 + 16;   // padded fp64 row
+  static constexpr int NB = 2;
+};
+
+template <int Q, typename T>
+struct RingMF {
+  static constexpr int ROWP = MfGeo<T>::ROWP;
+  static constexpr int NB = MfGeo<T>::NB;
+  static constexpr int WSLOT = (Q + 2) * ROWP + kWT * 2;     // rows | int16 ids
+  static constexpr int AUX = kWT * 16;                        // {w | -1, sum x^2} per stock
+  static constexpr int RED = 256 * 8;                          // this wave's 16x16 tile
+  static constexpr int RW0 = NB * WSLOT + AUX;
+  static constexpr int RINGW = RW0 > RED ? RW0 : RED;
+  static constexpr int BYTES = 4 * RINGW;
+};
+
+template <int Q, typename T>
+__device__ __forceinline__ constexpr int dma_per_tile_mf(bool has_ind) {
+  return Q + 2 + (has_ind ? 1 : 0);  // one (padded) row per instruction
+}
+
+template <int Q, int VAR, int R, typename T>
+__device__ __forceinline__ void moments_body_mf(
+    const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
+    const int16_t* __restrict__ ind, int N, int Pseg, int d, char* ring, double* dyn,
+    double* md, int nb = 0, int ne = -1, double* __restrict__ gout = nullptr) {
+  static_assert(Q + 4 <= 16, "one 16x16 MFMA tile: Q <= 12");
+  using L = Layout<Q, T>;
+  using G = RingMF<Q, T>;
+  constexpr int NS = L::NS, NG = L::NG, NACC = L::NACC;
+  constexpr int WSLOT = G::WSLOT, RINGW = G::RINGW, NB = G::NB, ROWP = G::ROWP;
+  if (ne < 0) ne = N;
+  const int tid = threadIdx.x, nthr = blockDim.x;
+  const int lane = tid & 63, wid = tid >> 6, nw = nthr >> 6;
+  constexpr bool DET = (VAR & 32) != 0;
+  const int rep = DET ? wid * (R / 4) + (lane & (R / 4 - 1)) : (lane & (R - 1));
+  const unsigned seg_a = lds_addr(dyn + rep);
+  for (int i = tid; i < R * Pseg * NS; i += nthr) dyn[i] = 0.0;
+  __syncthreads();
+
+  const T* Xd = X + (size_t)d * Q * N;
+  const T* cd = cap + (size_t)d * N;
+  const T* rd = ret + (size_t)d * N;
+  const int16_t* id = ind ? ind + (size_t)d * N : nullptr;
+
+  char* wring = ring + wid * RINGW;
+  double2* aux = (double2*)(wring + NB * WSLOT);
+  const int nrows = dma_per_tile_mf<Q, T>(id != nullptr);
+  const int ntile_all = (ne - nb + kWT - 1) / kWT;
+  const int ntile = ntile_all > wid ? (ntile_all - wid + nw - 1) / nw : 0;
+  auto issue = [&](int i) {
+    char* slot = wring + (i % NB) * WSLOT;
+    const int s0 = nb + (wid + i * nw) * kWT;
+    if constexpr (sizeof(T) == 4) {
+      const bool in = s0 + lane < ne;
+      if (in) glds4(cd + s0 + lane, slot);
+      if (in) glds4(rd + s0 + lane, slot + ROWP);
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (in) glds4(Xd + (size_t)q * N + s0 + lane, slot + (2 + q) * ROWP);
+    } else {  // one 512-B fp64 row per instruction (lanes 0-31, 16 B each)
+      const int s = s0 + 2 * (lane & 31);
+      const bool in = lane < 32 && s < ne;
+      if (in) glds16(cd + s, slot);
+      if (in) glds16(rd + s, slot + ROWP);
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        if (in) glds16(Xd + (size_t)q * N + s, slot + (2 + q) * ROWP);
+    }
+    if (id && lane < kWT / 2 && s0 + 2 * lane < ne) glds4(id + s0 + 2 * lane, slot + (Q + 2) * ROWP);
+  };
+  // this lane's Gram channel: ring row (x_c: 2 + c, r: 1, aux channels: row 0 as a dummy)
+  const int ch = lane & 15, kq = lane >> 4;
+  const int crow = ch < Q ? 2 + ch : (ch == Q ? 1 : 0);
+  v4d acc4[4];  // 4 independent accumulation chains (the f64 MFMA's dependent latency)
+#pragma unroll
+  for (int a = 0; a < 4; ++a) acc4[a] = v4d{0.0, 0.0, 0.0, 0.0};
+  for (int i = 0; i < NB - 1 && i < ntile; ++i) issue(i);
+  for (int i = 0; i < ntile; ++i) {
+    const bool tail = (i + NB - 1 >= ntile);
+    wait_vmcnt(tail ? 0 : (NB - 2) * nrows);
+    __builtin_amdgcn_wave_barrier();
+    if (i + NB - 1 < ntile) issue(i + NB - 1);
+    const char* slot = wring + (i % NB) * WSLOT;
+    const T* bf = (const T*)slot;
+    // ---- prep: lane = stock
+    {
+      const int s = nb + (wid + i * nw) * kWT + lane;
+      const T cf = *(const T*)(slot + lane * sizeof(T));
+      const T rf = *(const T*)(slot + ROWP + lane * sizeof(T));
+      const int j = id ? (int)((const int16_t*)(slot + (Q + 2) * ROWP))[lane] : 0;
+      T xf[Q];
+#pragma unroll
+      for (int q = 0; q < Q; ++q) xf[q] = *(const T*)(slot + (2 + q) * ROWP + lane * sizeof(T));
+      bool ok = (s < ne) && (j >= 0) && (j < Pseg) && finite_v(cf) && (cf >= T(0)) && finite_v(rf);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) ok = ok && finite_v(xf[q]);
+      double w = -1.0, s2 = 0.0;
+      if (ok) {
+        const double c = cf, r = rf;
+        w = sqrt(c);
+        double wx[Q];
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          wx[q] = w * (double)xf[q];
+          s2 = fma((double)xf[q], (double)xf[q], s2);
+        }
+        if (VAR & 1) {  // timing-only ablation: skip the segment atomics
+          asm volatile("" ::"v"(w), "v"(r));
+        } else {
+          const unsigned a = seg_a + (unsigned)(j * NS * R * 8);
+          lds_add_nowait<0>(a, w);
+          [&]<int... I>(std::integer_sequence<int, I...>) {
+            (lds_add_nowait<8 * R * (1 + I)>(a, wx[I]), ...);
+          }(std::make_integer_sequence<int, Q>{});
+          lds_add_nowait<8 * R * (Q + 1)>(a, w * r);
+          lds_add_nowait<8 * R * (Q + 2)>(a, c);
+        }
+      }
+      // aux row: asm store (like the segment atomics) so hipcc's waitcnt pass does not drain
+      // the in-flight DMA tile for it; LDS ops of one wave complete in order
+      const unsigned aa = lds_addr(aux + lane);
+      asm volatile("ds_write_b64 %0, %1\n\tds_write_b64 %0, %2 offset:8" ::"v"(aa), "v"(w),
+                   "v"(s2) : "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    // ---- matrix cores: 16 k-steps of 4 stocks
+    if constexpr ((VAR & 2) == 0) {
+      const T* rowp = (const T*)(slot + crow * ROWP);
+#pragma unroll
+      for (int k0 = 0; k0 < kWT; k0 += 4) {
+        const int k = k0 + kq;
+        const double2 a2 = aux[k];
+        const double raw = (double)rowp[k];
+        const bool okk = a2.x >= 0.0;
+        const double wp = okk ? a2.x : 0.0;
+        double al, be;
+        if (ch <= Q) {
+          al = okk ? raw : 0.0;
+          be = al * wp;
+        } else if (ch == Q + 1) {
+          al = wp;
+          be = wp * wp;
+        } else if (ch == Q + 2) {
+          al = okk ? 1.0 : 0.0;
+          be = al;
+        } else {
+          al = ch == Q + 3 ? a2.y : 0.0;
+          be = 0.0;
+        }
+        acc4[(k0 >> 2) & 3] = __builtin_amdgcn_mfma_f64_16x16x4f64(al, be, acc4[(k0 >> 2) & 3], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __syncthreads();
+  const v4d acc = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
+  // the 4 waves' 16x16 tiles, summed in wave order
+  double* tile = (double*)wring;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) tile[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = acc[r];
+  __syncthreads();
+  auto gsum = [&](int i, int j) {
+    double t = 0.0;
+    for (int w = 0; w < nw; ++w) t += ((const double*)(ring + w * RINGW))[i * 16 + j];
+    return t;
+  };
+  double mv = 0.0;
+  if (tid < NG) {
+    int q = 0;
+    while ((q + 1) * (q + 2) / 2 <= tid) ++q;
+    mv = gsum(q, tid - q * (q + 1) / 2);
+  } else if (tid < NG + Q) {
+    mv = gsum(tid - NG, Q);
+  } else if (tid < NG + 2 * Q) {
+    mv = gsum(tid - NG - Q, Q + 1);
+  } else if (tid == NG + 2 * Q) {
+    mv = gsum(Q + 2, Q + 1);
+  } else if (tid == NG + 2 * Q + 1) {
+    for (int q = 0; q < Q; ++q) mv += gsum(q, Q + 2);
+  } else if (tid == NG + 2 * Q + 2) {
+    mv = gsum(Q + 3, Q + 2);
+  } else if (tid == NG + 2 * Q + 3) {
+    mv = gsum(Q + 2, Q + 2);
+  }
+  static_assert(NACC <= 256, "one thread per moment");
+  __syncthreads();  // md may alias the ring
+  if (tid < NACC) {
+    md[tid] = mv;
+    if (gout) gout[tid] = mv;
+  }
+  for (int i = tid; i < Pseg * NS; i += nthr) {
+    double t = 0.0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) t += dyn[i * R + r];
+    md[NACC + i] = t;
+    if (gout) gout[NACC + i] = t;
+  }
+  __syncthreads();
+}
+
+template <int Q, int VAR, int R, typename T>
+__global__ __launch_bounds__(256) void xs_moments_mf_kernel(
+    const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
+    const int16_t* __restrict__ ind, int N, int Pseg, int S, int C, double* __restrict__ mom) {
+  __shared__ __attribute__((aligned(16))) char ring[RingMF<Q, T>::BYTES];
+  extern __shared__ double dyn[];
+  const int b = blockIdx.x, d = b / S, sc = b - d * S;
+  const int nb = sc * C, ne = min(N, nb + C);
+  moments_body_mf<Q, VAR, R, T>(X, cap, ret, ind, N, Pseg, d, ring, dyn,
+                                mom + (size_t)b * Layout<Q, T>::msize(Pseg), nb, ne);
+}
+
+// High-occupancy fused kernel: MFMA moments (few VGPRs, small padded ring) -> wave-0 solve
+// -> residual pass with UU iterations in flight; 3-4 workgroups per CU.
+template <int Q, typename T>
+constexpr int fused_mf_ring_bytes() {
+  constexpr int a = RingMF<Q, T>::BYTES;
+  constexpr int b = (int)(solve_lds_doubles<Q>(128) * 8);
+  return a > b ? a : b;
+}
+
+template <int Q, int R, int VAR, typename T, int WPE>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void xs_fused_mf_kernel(
+    const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
+    const int16_t* __restrict__ ind, int N, int P, int Pseg, int pivot_mode, double tol,
+    double* __restrict__ fout, T* __restrict__ eout, double* __restrict__ r2out,
+    double* __restrict__ stats, int* __restrict__ status, double* __restrict__ mom_out) {
+  __shared__ __attribute__((aligned(16))) char ring[fused_mf_ring_bytes<Q, T>()];
+  __shared__ double cf_s[Q + 1 + 128];
+  __shared__ double red[4][5];
+  __shared__ int st_s;
+  extern __shared__ double dyn[];
+  const int d = blockIdx.x;
+  double* sm = (double*)ring;
+  moments_body_mf<Q, VAR & 35, R, T>(X, cap, ret, ind, N, Pseg, d, ring, dyn, sm, 0, -1,
+                                     mom_out ? mom_out + (size_t)d * Layout<Q, T>::msize(Pseg)
+                                             : nullptr);
+  if constexpr ((VAR & 8) != 0) {  // timing-only ablation: no solve
+    for (int i = threadIdx.x; i < Q + 1 + P; i += blockDim.x) cf_s[i] = sm[i] * 1e-30;
+    if (threadIdx.x == 0) st_s = 0;
+  } else if (threadIdx.x < 64) {
+    solve_body<Q, true>(sm, d, P, Pseg, pivot_mode, tol, fout, cf_s, stats, status, &st_s);
+  }
+  __syncthreads();
+  constexpr int UR = sizeof(T) == 4 ? 2 : 1;
+  if constexpr ((VAR & 4) == 0)
+    resid_body<Q, T, false, UR>(X, cap, ret, ind, d, N, P, cf_s, (st_s & XS_BAD) != 0, eout,
+                                r2out, red);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -873,17 +1301,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   extern __shared__ double dyn[];
   const int d = blockIdx.x;
   double* sm = (double*)ring;  // moments, then the solve's scratch (ring is idle by then)
-  moments_body<Q, VAR & 35, R, T>(X, cap, ret, ind, N, Pseg, d, ring, dyn, sm);
+  // every date's moments also go to mom_out (from registers, ~9.7 MB per 2520 dates): the
+  // device pseudo-inverse pass reads them for near-singular dates.  (Exporting only flagged
+  // dates from LDS after the solve cost ~30 us per 2520-date step: the extra LDS read of the
+  // DMA ring region made hipcc add conservative vmcnt drains.)
+  moments_body<Q, VAR & 35, R, T>(X, cap, ret, ind, N, Pseg, d, ring, dyn, sm, 0, -1,
+                                  mom_out ? mom_out + (size_t)d * Layout<Q, T>::msize(Pseg)
+                                          : nullptr);
   if constexpr ((VAR & 8) != 0) {  // timing-only ablation: no solve
     for (int i = threadIdx.x; i < Q + 1 + P; i += blockDim.x) cf_s[i] = sm[i] * 1e-30;
     if (threadIdx.x == 0) st_s = 0;
   } else if (threadIdx.x < 64) {
     solve_body<Q>(sm, d, P, Pseg, pivot_mode, tol, fout, cf_s, stats, status, &st_s);
-    // near-singular date: export its moments for the device pseudo-inverse pass
-    if (mom_out && (__builtin_amdgcn_readfirstlane(st_s) & XS_NEAR_SINGULAR)) {
-      const int MS = Layout<Q, T>::msize(Pseg);
-      for (int i = threadIdx.x; i < MS; i += 64) mom_out[(size_t)d * MS + i] = sm[i];
-    }
   }
   ResidPre<Q> pre;
   if constexpr (PRE) {
@@ -924,7 +1353,7 @@ __host__ __device__ constexpr size_t refine_lds_doubles(int P) {
 template <int Q, typename T>
 __global__ __launch_bounds__(256) void xs_refine_kernel(
     const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
-    const int16_t* __restrict__ ind, int N, int P, int pivot_mode,
+    const int16_t* __restrict__ ind, int N, int P, int pivot_mode, int S,
     const double* __restrict__ mom, double* __restrict__ fout, T* __restrict__ eout,
     double* __restrict__ r2out, int* __restrict__ status) {
   using L = Layout<Q, double>;
@@ -949,7 +1378,7 @@ __global__ __launch_bounds__(256) void xs_refine_kernel(
   double* alp = rhs + Kr;          // [Kr]  constraint weights alpha_u
   double* g = alp + Kr;            // [Kr]  eigen-space coefficients
   double* mu = g + Kr;             // [Q]   cap-weighted style means
-  for (int i = tid; i < MS; i += blockDim.x) md[i] = mom[(size_t)d * MS + i];
+  load_moments<Q>(mom, d, S, Pseg, md);
   __syncthreads();
   const double* acc = md;
   const double* seg = md + NACC;
@@ -1076,6 +1505,41 @@ size_t solve_lds_bytes(int Pseg) {
   return solve_lds_doubles<Q>(Pseg) * sizeof(double);
 }
 
+// ------------------------------------------------------------------------------------------
+// Path selection.  Default: the fused kernel, one workgroup per date, ~512 dates in flight.
+// Chunked path (mfa_xs_set_chunks(S > 0), or automatic below kXsChunkMinD dates): each date is
+// cut into S stock chunks of C stocks, for shards too small to fill the chip:
+//   moments (D*S WGs, partial moments) -> solve (D waves, partials summed in chunk order)
+//   -> residuals (D*S WGs, partial R^2 sums) -> R^2 combine (chunk order).
+// Chunk sums are combined in a fixed order, so the chunked path is as deterministic as the
+// per-workgroup reductions it is built from.
+// ------------------------------------------------------------------------------------------
+constexpr int kXsChunkMinD = 0;      // automatic chunking off: measured slower than the fused
+                                     // kernel at every D in 315..2520 (profiles/r02_xs_paths.md)
+constexpr int kXsChunkTargetWG = 2048;
+constexpr int kXsMinChunk = 256;     // stocks
+
+inline int xs_chunk_size(int N, int S) { return ((N + S - 1) / S + kWT - 1) / kWT * kWT; }
+
+inline int xs_chunks(int D, int N) {
+  const int maxS = N / kXsMinChunk > 1 ? N / kXsMinChunk : 1;
+  int S;
+  if (g_mfa_xs_chunks > 0) S = g_mfa_xs_chunks;
+  else if (g_mfa_xs_chunks < 0 || D >= kXsChunkMinD) S = 1;
+  else S = (kXsChunkTargetWG + D - 1) / D;
+  S = S < 1 ? 1 : (S > maxS ? maxS : S);
+  const int C = xs_chunk_size(N, S);
+  return (N + C - 1) / C;  // no empty trailing chunk after rounding C up to 64
+}
+
+// Workspace: partial moments [D][S][msize] | coef [D][Q+1+P] | partial R^2 sums [D][S][5].
+inline size_t xs_workspace_bytes(int D, int N, int P, int Q) {
+  const int Pseg = P > 0 ? P : 1;
+  const size_t ms = (size_t)Q * (Q + 1) / 2 + 2 * Q + 4 + (size_t)Pseg * (Q + 3);
+  const size_t S = (size_t)xs_chunks(D, N);
+  return (size_t)D * (S * ms + Q + 1 + P + S * 5) * sizeof(double);
+}
+
 template <int Q, int VAR, typename T>
 hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, int D, int N,
                     int P, int pivot_mode, double tol, double* f, T* e, double* r2, double* stats,
@@ -1086,57 +1550,79 @@ hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, 
   const bool det = (pivot_mode & kXsDeterministic) != 0;
   const bool refine = (pivot_mode & kXsRefine) != 0;
   const int pm = pivot_mode & 0xff;
+  const int mode = g_mfa_xs_mode;
+  const int S = xs_chunks(D, N);
+  const int C = xs_chunk_size(N, S);
+  const bool chunked = S > 1 || mode == 1;
   double* mom = ws;
-  double* coef = ws + (size_t)D * MS;
+  double* coef = ws + (size_t)D * S * MS;
+  double* sums = coef + (size_t)D * (Q + 1 + P);
   const size_t seg8 = (size_t)kRepMax * Pseg * L::NS * sizeof(double);
   const bool rep8 = seg8 <= kSegLdsBudget;
   const size_t lds1 = ((rep8 ? (size_t)kRepMax : 1) * Pseg * L::NS + L::NACC) * sizeof(double);
   const size_t lds2 = solve_lds_bytes<Q, T>(Pseg);
   if (lds1 + fused_ring_bytes<Q, T>() > 160 * 1024 || lds2 > 64 * 1024) return hipErrorInvalidValue;
   if (refine && 1 + P + Q > kXsRefineMaxK) return hipErrorInvalidValue;
+  if (det && !rep8) return hipErrorNotSupported;
   const int16_t* indp = P > 0 ? ind : nullptr;
   constexpr bool PRE = sizeof(T) == 4;
-  const int mode = g_mfa_xs_mode;
-  if (det) {  // bitwise-reproducible variant of the default path
-    if (!rep8) return hipErrorNotSupported;
+  if (chunked) {
+    const dim3 g(D * S);
+    if (det)
+      hipLaunchKernelGGL((xs_moments_kernel<Q, VAR | 32, kRepMax, T>), g, dim3(256), lds1, s, X,
+                         cap, ret, indp, N, Pseg, S, C, mom);
+    else if (rep8)
+      hipLaunchKernelGGL((xs_moments_kernel<Q, VAR, kRepMax, T>), g, dim3(256), lds1, s, X, cap,
+                         ret, indp, N, Pseg, S, C, mom);
+    else
+      hipLaunchKernelGGL((xs_moments_kernel<Q, VAR, 1, T>), g, dim3(256), lds1, s, X, cap, ret,
+                         indp, N, Pseg, S, C, mom);
+    hipLaunchKernelGGL(xs_solve_kernel<Q>, dim3(D), dim3(64), lds2, s, mom, S, P, Pseg, pm, tol, f,
+                       coef, stats, status);
+    if (!(VAR & 4)) {
+      hipLaunchKernelGGL((xs_resid_kernel<Q, T>), g, dim3(256), 0, s, X, cap, ret, indp, D, N, P,
+                         S, C, coef, status, e, r2, S > 1 ? sums : nullptr);
+      if (S > 1)
+        hipLaunchKernelGGL(xs_r2_combine_kernel, dim3((D + 255) / 256), dim3(256), 0, s, sums, D,
+                           S, status, r2);
+    }
+  } else if (Q == 10 && (mode == 10 || mode == 11 || mode == 12)) {
+    // A/B only (headline Q): MFMA-moments fused kernel, 3 / 4 / 2 workgroups per CU (segment
+    // replicas 4 / 2 / 8).  Measured slower than the VALU body at every occupancy
+    // (profiles/r02_xs_mfma_ab.md), so never the default.
+    const int Rm = mode == 12 ? 8 : (mode == 10 ? 4 : 2);
+    const size_t ldsm = ((size_t)Rm * Pseg * L::NS + L::NACC) * sizeof(double);
+    if (ldsm + fused_mf_ring_bytes<10, T>() > 160 * 1024) return hipErrorInvalidValue;
+    if constexpr (Q == 10) {
+      if (mode == 12)
+        hipLaunchKernelGGL((xs_fused_mf_kernel<Q, 8, VAR, T, 2>), dim3(D), dim3(256), ldsm, s, X,
+                           cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom);
+      else if (mode == 10)
+        hipLaunchKernelGGL((xs_fused_mf_kernel<Q, 4, VAR, T, 3>), dim3(D), dim3(256), ldsm, s, X,
+                           cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom);
+      else
+        hipLaunchKernelGGL((xs_fused_mf_kernel<Q, 2, VAR, T, 4>), dim3(D), dim3(256), ldsm, s, X,
+                           cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom);
+    }
+  } else if (det) {  // bitwise-reproducible variant of the default path
     hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR | 32, PRE, T>), dim3(D), dim3(256), lds1,
                        s, X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom);
   } else if (mode == 0 && rep8) {
     hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR, PRE, T>), dim3(D), dim3(256), lds1, s, X,
                        cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom);
-  } else if (mode == 0 || mode == 7) {
-    if (rep8)
-      hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR, false, T>), dim3(D), dim3(256), lds1, s,
-                         X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom);
-    else
-      hipLaunchKernelGGL((xs_fused_kernel<Q, 1, VAR, false, T>), dim3(D), dim3(256), lds1, s, X,
-                         cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom);
+  } else if (rep8) {
+    hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR, false, T>), dim3(D), dim3(256), lds1, s,
+                       X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom);
   } else {
-    if (rep8)
-      hipLaunchKernelGGL((xs_moments_kernel<Q, VAR, kRepMax, T>), dim3(D), dim3(256), lds1, s, X,
-                         cap, ret, indp, N, Pseg, mom);
-    else
-      hipLaunchKernelGGL((xs_moments_kernel<Q, VAR, 1, T>), dim3(D), dim3(256), lds1, s, X, cap,
-                         ret, indp, N, Pseg, mom);
-    hipLaunchKernelGGL(xs_solve_kernel<Q>, dim3(D), dim3(64), lds2, s, mom, P, Pseg, pm, tol, f,
-                       coef, stats, status);
-    if (!(VAR & 4))
-      hipLaunchKernelGGL((xs_resid_kernel<Q, T>), dim3(D), dim3(256), 0, s, X, cap, ret, indp, D,
-                         N, P, coef, status, e, r2);
+    hipLaunchKernelGGL((xs_fused_kernel<Q, 1, VAR, false, T>), dim3(D), dim3(256), lds1, s, X,
+                       cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom);
   }
   if (refine) {
     const size_t lds3 = refine_lds_doubles<Q>(P) * sizeof(double);
     hipLaunchKernelGGL((xs_refine_kernel<Q, T>), dim3(D), dim3(256), lds3, s, X, cap, ret, indp,
-                       N, P, pm, mom, f, e, r2, status);
+                       N, P, pm, S, mom, f, e, r2, status);
   }
   return hipGetLastError();
-}
-
-// Workspace bytes needed by the fused / split paths: D * (msize + Q + 1 + P) doubles.
-inline size_t xs_workspace_bytes(int D, int P, int Q) {
-  const int Pseg = P > 0 ? P : 1;
-  const size_t ms = (size_t)Q * (Q + 1) / 2 + 2 * Q + 4 + (size_t)Pseg * (Q + 3);
-  return (size_t)D * (ms + Q + 1 + P) * sizeof(double);
 }
 
 template <typename T>
@@ -1181,18 +1667,18 @@ hipError_t split_q(int what, const T* X, const T* cap, const T* ret, const int16
     if (lds1 + Ring<Q, T>::BYTES > 160 * 1024) return hipErrorInvalidValue;
     if (rep8)
       hipLaunchKernelGGL((xs_moments_kernel<Q, 0, kRepMax, T>), dim3(D), dim3(256), lds1, s, X,
-                         cap, ret, indp, N, Pseg, mom);
+                         cap, ret, indp, N, Pseg, 1, N, mom);
     else
       hipLaunchKernelGGL((xs_moments_kernel<Q, 0, 1, T>), dim3(D), dim3(256), lds1, s, X, cap,
-                         ret, indp, N, Pseg, mom);
+                         ret, indp, N, Pseg, 1, N, mom);
   } else if (what == 1) {
     const size_t lds2 = solve_lds_bytes<Q, T>(Pseg);
     if (lds2 > 64 * 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(xs_solve_kernel<Q>, dim3(D), dim3(64), lds2, s, mom, P, Pseg, pivot_mode,
+    hipLaunchKernelGGL(xs_solve_kernel<Q>, dim3(D), dim3(64), lds2, s, mom, 1, P, Pseg, pivot_mode,
                        tol, f, coef, stats, status);
   } else {
     hipLaunchKernelGGL((xs_resid_kernel<Q, T>), dim3(D), dim3(256), 0, s, X, cap, ret, indp, D, N,
-                       P, coef, status, e, (double*)nullptr, sums);
+                       P, 1, N, coef, status, e, (double*)nullptr, sums);
   }
   return hipGetLastError();
 }

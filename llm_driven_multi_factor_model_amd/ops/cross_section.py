@@ -128,7 +128,7 @@ def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Ten
     resid_buf = out.resid
     if resid_buf is not None and Np != N:
         resid_buf = torch.empty(D, Np, dtype=dt, device=dev)
-    need = _native.query("mfa_xs_wls_workspace", D, P, Q)
+    need = _native.query("mfa_xs_wls_workspace", D, Np, P, Q)
     if workspace is None or workspace.numel() < need:
         workspace = torch.empty(need, dtype=torch.uint8, device=dev)
     dev_refine = refine and K <= REFINE_MAX_K
@@ -147,9 +147,11 @@ def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Ten
     return out
 
 
-def xs_wls_workspace(D: int, P: int, Q: int, device) -> torch.Tensor:
-    """Preallocated kernel workspace for repeated :func:`xs_wls` calls on the same shapes."""
-    return torch.empty(_native.query("mfa_xs_wls_workspace", D, P, Q), dtype=torch.uint8,
+def xs_wls_workspace(D: int, P: int, Q: int, device, N: int = 5000) -> torch.Tensor:
+    """Preallocated kernel workspace for repeated :func:`xs_wls` calls on the same shapes
+    (its size depends on the path, i.e. on the stock chunks per date chosen for (D, N))."""
+    Np = (N + 7) // 8 * 8
+    return torch.empty(_native.query("mfa_xs_wls_workspace", D, Np, P, Q), dtype=torch.uint8,
                        device=device)
 
 

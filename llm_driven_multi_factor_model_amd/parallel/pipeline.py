@@ -67,7 +67,7 @@ def streamed_xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: 
             r2=torch.empty(chunk, dtype=torch.float64, device=device),
             stats=torch.empty(chunk, Q + 2, dtype=torch.float64, device=device),
             status=torch.empty(chunk, dtype=torch.int32, device=device)))
-        ws.append(xs_wls_workspace(chunk, P, Q, device))
+        ws.append(xs_wls_workspace(chunk, P, Q, device, N))
 
     s_h2d, s_cmp, s_d2h = (torch.cuda.Stream(device) for _ in range(3))
     loaded = [torch.cuda.Event() for _ in range(nslot)]

@@ -17,9 +17,9 @@ def _port():
     return p
 
 
-def _run(n):
+def _run(n, extra=()):
     args = ["--gpus", str(n), "--steps", "2", "--warmup", "1", "--dates", "6", "--stocks", "64",
-            "--industries", "3", "--styles", "2"]
+            "--industries", "3", "--styles", "2", *extra]
     if n == 1:
         cmd = [sys.executable, "bench.py", *args]
     else:
@@ -48,3 +48,12 @@ def test_bench_two_ranks_aggregate():
     assert r["n_gpus"] == 2
     assert r["config"]["global_batch"] == 12 and r["config"]["parallelism"] == "dp2"
     assert abs(r["value"] - 12 * 2 / (r["ms_per_step"] * 2 / 1e3)) / r["value"] < 0.02
+
+
+def test_bench_strong_scaling_two_ranks():
+    """--scaling strong: the global date count is fixed and sharded over the ranks."""
+    r = _run(2, ["--scaling", "strong"])
+    assert r["scaling"] == "strong" and r["n_gpus"] == 2
+    assert r["config"]["global_batch"] == 6 and r["config"]["dates_per_gpu"] == 3
+    assert abs(r["value"] - 6 * 2 / (r["ms_per_step"] * 2 / 1e3)) / r["value"] < 0.02
+    assert r["config"]["storage"] == "fp64"

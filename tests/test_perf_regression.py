@@ -28,7 +28,7 @@ def test_xs_wls_headline_shape_throughput():
     from llm_driven_multi_factor_model_amd.ops.cross_section import xs_wls, xs_wls_workspace
     D, N, P, Q = 1000, 5000, 31, 10
     g = synthetic_panel(D, N, P, Q, seed=0, missing_frac=0.02).to("cuda:0")
-    ws = xs_wls_workspace(D, P, Q, "cuda:0")
+    ws = xs_wls_workspace(D, P, Q, "cuda:0", N)
     out = xs_wls(g.styles, g.cap, g.ret, g.ind, P, workspace=ws, refine=False)
     ms = _time_ms(lambda: xs_wls(g.styles, g.cap, g.ret, g.ind, P, out=out, workspace=ws, refine=False))
     reg_per_s = D / (ms * 1e-3)

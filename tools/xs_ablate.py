@@ -26,7 +26,7 @@ def main():
     st = torch.empty(D, Q + 2, dtype=torch.float64, device=dev)
     s = torch.empty(D, dtype=torch.int32, device=dev)
     variants = [int(v) for v in os.environ.get("VARIANTS", "0,1,4,5").split(",")]
-    ws = torch.empty(_native.query("mfa_xs_wls_workspace", D, P, Q), dtype=torch.uint8, device=dev)
+    ws = torch.empty(_native.query("mfa_xs_wls_workspace", D, N, P, Q), dtype=torch.uint8, device=dev)
     times = {v: [] for v in variants}
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for rnd in range(12):

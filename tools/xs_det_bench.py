@@ -12,7 +12,7 @@ from llm_driven_multi_factor_model_amd.ops import cross_section as X  # noqa: E4
 p = synthetic_panel(2520, 5000, 31, 10, seed=3, device="cuda:0", missing_frac=0.01)
 for det in (False, True, False, True):
     out = X.xs_wls(p.styles, p.cap, p.ret, p.ind, 31, deterministic=det, refine=False)
-    ws = X.xs_wls_workspace(2520, 31, 10, p.styles.device)
+    ws = X.xs_wls_workspace(2520, 31, 10, p.styles.device, 5000)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(50):

@@ -25,7 +25,7 @@ def main():
     p = pn.synthetic_panel(D, N, P, Q, seed=1, device=dev, missing_frac=0.01)
     if os.environ.get("SORT", "0") == "1" and hasattr(pn, "order_by_industry"):
         p = pn.order_by_industry(p)
-    ws = xs_wls_workspace(D, P, Q, dev)
+    ws = xs_wls_workspace(D, P, Q, dev, N)
     modes = [int(m) for m in os.environ.get("MODES", "0,1").split(",")]
     outs = {}
     for m in modes:

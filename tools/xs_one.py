@@ -21,7 +21,7 @@ e = torch.empty(D, N, dtype=torch.float32, device=dev)
 r2 = torch.empty(D, dtype=torch.float64, device=dev)
 st = torch.empty(D, Q + 2, dtype=torch.float64, device=dev)
 s = torch.empty(D, dtype=torch.int32, device=dev)
-ws = torch.empty(_native.query("mfa_xs_wls_workspace", D, P, Q), dtype=torch.uint8, device=dev)
+ws = torch.empty(_native.query("mfa_xs_wls_workspace", D, N, P, Q), dtype=torch.uint8, device=dev)
 for _ in range(3):
     _native.call("mfa_xs_wls_variant", _native.ptr(p.styles), _native.ptr(p.cap), _native.ptr(p.ret),
                  _native.ptr(p.ind), D, N, P, v, _native.ptr(f), _native.ptr(e), _native.ptr(r2),
