@@ -17,6 +17,7 @@ the normals come from Philox rather than MT19937 (bitwise parity with numpy is i
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 
 import torch
@@ -40,6 +41,36 @@ _native.register("mfa_eigen_finalize_sum", [C.c_void_p, C.c_int, C.c_void_p, C.c
 
 MAX_SWEEPS = 30
 TOL = 1e-15
+
+# Per-(date, sim) solver of the bias statistic (csrc/eigen.hip): "jacobi" = pair-block
+# tournament Jacobi carrying M = V^T D0 V; "tridiag" = Householder tridiagonalisation,
+# count-guided Laguerre eigenvalues, twisted-factorisation eigenvectors, back-transform.
+BIAS_SOLVERS = {"jacobi": 0, "tridiag": 3}
+_bias_solver = "tridiag"
+
+
+def set_bias_solver(name: str) -> None:
+    """Select the GPU bias-statistic solver (process-wide)."""
+    global _bias_solver
+    if name not in BIAS_SOLVERS:
+        raise ValueError(f"bias solver must be one of {sorted(BIAS_SOLVERS)}, got {name!r}")
+    _bias_solver = name
+    if torch.cuda.is_available():
+        _native.lib().mfa_eigen_set_bias_mode(BIAS_SOLVERS[name])
+
+
+def bias_solver() -> str:
+    return _bias_solver
+
+
+@contextlib.contextmanager
+def using_bias_solver(name: str):
+    old = _bias_solver
+    set_bias_solver(name)
+    try:
+        yield
+    finally:
+        set_bias_solver(old)
 
 
 def eigh(A: torch.Tensor, max_sweeps: int = MAX_SWEEPS, tol: float = TOL):

@@ -84,15 +84,35 @@ def test_hip_mc_cov_statistics(cuda):
 
 
 @pytest.mark.gpu
-def test_hip_eigen_adjust_matches_reference_path(cuda):
-    D, K, M = 12, 42, 16
-    F = _spd(D, K, seed=9, spread=2.0) * 1e-4
+@pytest.mark.parametrize("solver", sorted(eigen.BIAS_SOLVERS))
+@pytest.mark.parametrize("K", [42, 5, 17, 64])
+def test_hip_eigen_adjust_matches_reference_path(cuda, solver, K):
+    D, M = 12, 16
+    F = _spd(D, K, seed=9 + K, spread=2.0) * 1e-4
     F[3] = float("nan")
     Cz = eigen.mc_cov(M, K, 500, seed=2, device=cuda)
-    Fg, vg = eigen.eigen_risk_adjust(F.to(cuda), Cz=Cz, return_bias=True)
+    with eigen.using_bias_solver(solver):
+        Fg, vg = eigen.eigen_risk_adjust(F.to(cuda), Cz=Cz, return_bias=True)
     Fc, vc = eigen.eigen_risk_adjust(F, Cz=Cz.cpu(), return_bias=True)
     torch.testing.assert_close(vg.cpu(), vc, rtol=1e-8, atol=1e-10, equal_nan=True)
     torch.testing.assert_close(Fg.cpu(), Fc, rtol=1e-8, atol=1e-16, equal_nan=True)
+
+
+@pytest.mark.gpu
+def test_hip_bias_solvers_agree_on_pipeline_like_inputs(cuda):
+    """Both GPU solvers give the same per-sim bias ratios on graded, nearly-diagonal draw
+    covariances (the shape of the MC problem: C_b = S C_z S, S spanning decades)."""
+    D, K, M = 40, 42, 24
+    g = torch.Generator().manual_seed(7)
+    Q, _ = torch.linalg.qr(torch.randn(D, K, K, generator=g, dtype=torch.float64))
+    lam = torch.exp(torch.randn(D, K, generator=g, dtype=torch.float64) * 1.5 - 9.0)
+    F = ((Q * lam[:, None, :]) @ Q.transpose(1, 2)).to(cuda)
+    Cz = eigen.mc_cov(M, K, 2520, seed=3, device=cuda)
+    out = {}
+    for solver in eigen.BIAS_SOLVERS:
+        with eigen.using_bias_solver(solver):
+            out[solver] = eigen.eigen_risk_adjust(F, Cz=Cz, return_bias=True)[1].cpu()
+    torch.testing.assert_close(out["tridiag"], out["jacobi"], rtol=1e-10, atol=0)
 
 
 @pytest.mark.gpu
@@ -104,13 +124,16 @@ def test_hip_mc_cov_range_is_a_slice(cuda):
 
 
 @pytest.mark.gpu
-def test_hip_sharded_eigen_matches_one_shot(cuda):
+@pytest.mark.parametrize("solver", sorted(eigen.BIAS_SOLVERS))
+def test_hip_sharded_eigen_matches_one_shot(cuda, solver):
     """Chunked sum-accumulate + finalize kernels == the one-shot per-sim kernel (same Philox sims)."""
     D, K, M = 10, 42, 20
     F = _spd(D, K, seed=4, spread=2.0) * 1e-4
     F[2] = float("nan")
     Fg = F.to(cuda)
-    F1, v1 = eigen.eigen_risk_adjust(Fg, M=M, T_sim=400, seed=6, return_bias=True)
-    F2, v2 = eigen.eigen_risk_adjust_sharded(Fg, M=M, T_sim=400, seed=6, chunk=7, return_bias=True)
+    with eigen.using_bias_solver(solver):
+        F1, v1 = eigen.eigen_risk_adjust(Fg, M=M, T_sim=400, seed=6, return_bias=True)
+        F2, v2 = eigen.eigen_risk_adjust_sharded(Fg, M=M, T_sim=400, seed=6, chunk=7,
+                                                 return_bias=True)
     torch.testing.assert_close(v2.cpu(), v1.cpu(), rtol=1e-12, atol=1e-14, equal_nan=True)
     torch.testing.assert_close(F2.cpu(), F1.cpu(), rtol=1e-11, atol=1e-18, equal_nan=True)
