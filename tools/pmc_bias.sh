@@ -3,7 +3,7 @@
 # Two passes of <= 8 SQ counters each.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp
-O=gpurun_out/pmc_bias; mkdir -p $O
+O=gpurun_out/pmc_bias; rm -rf $O; mkdir -p $O
 export SETTINGS="${SETTINGS:-1e-15:30}" SUB=2
 timeout -s KILL 150 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS -d $O/a -o run --output-format csv -- python3 tools/eigen_tol.py > $O/a.log 2>&1 || exit 1
 timeout -s KILL 150 rocprofv3 --kernel-trace --pmc SQ_LDS_IDX_ACTIVE SQ_WAVES SQ_WAIT_ANY SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 -d $O/b -o run --output-format csv -- python3 tools/eigen_tol.py > $O/b.log 2>&1 || exit 1
