@@ -404,6 +404,281 @@ __global__ __launch_bounds__(256) void dastd_scan_kernel(
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Anchored-prefix EW window kernels (BETA/HSIGMA, DASTD): no per-chunk direct pass.
+//
+// With compressed weights (newest valid row 1, lam^k for k valid rows newer), the EW prefix
+// from an anchor g0, E_r = lam E_{r-1} + v_r (valid rows only; reset to 0 at a stock start),
+// gives every window sum exactly:  S_r = E_r - lam^{n_r} E_{r-W},  n_r = valid rows in
+// (r-W, r]  (a window that crosses the stock start is just E_r).  lam^W >= 1/64 for the
+// reference's half-lives, so the subtraction costs < 2 bits.  Persistent 256-thread blocks
+// loop over tiles of 2048 rows [g0, g0 + 2048) (the first H >= W are halo); thread t owns the
+// 8-row chunk t, kept in registers, and prefetches its chunk of the NEXT tile before computing:
+//   A. the chunk's affine map E -> lam^c E + B (or B after a reset), c = valid rows;
+//   B. inclusive scan of the 256 maps (wave shuffles, then the 4 wave totals in order);
+//   C. own rows from the chunk's carry-in, lagged rows r - W (LDS copy of the tile) from the
+//      carry-in of chunk (8t - W) / 8, O(1) per output row.
+// Measured (5000 x 3780, 1x MI355X, tools/rolling_ab.py): BETA/HSIGMA 0.62 -> 0.21 ms,
+// DASTD 0.55 -> 0.16 ms (profiles/r02_rolling_ab.jsonl).
+// Work per row ~3 recurrence steps instead of W / 16 direct taps + 1.
+// ------------------------------------------------------------------------------------------
+template <int NS>
+struct EwMap {
+  double A;      // lam^(valid rows), multiplier of the carry-in
+  double B[NS];  // contribution of the chunk's own rows
+  int cnt;       // valid rows since the last reset (or chunk start)
+  int reset;     // a stock starts inside: the carry-in is discarded
+};
+
+template <int NS>
+__device__ __forceinline__ void ew_compose(EwMap<NS>& m, const EwMap<NS>& p) {  // m <- m o p
+  if (m.reset) return;
+#pragma unroll
+  for (int k = 0; k < NS; ++k) m.B[k] = fma(m.A, p.B[k], m.B[k]);
+  m.A *= p.A;
+  m.cnt += p.cnt;
+  m.reset = p.reset;
+}
+
+template <int NS>
+__device__ __forceinline__ EwMap<NS> ew_shfl_up(const EwMap<NS>& m, int d) {
+  EwMap<NS> p;
+  p.A = __shfl_up(m.A, d, 64);
+#pragma unroll
+  for (int k = 0; k < NS; ++k) p.B[k] = __shfl_up(m.B[k], d, 64);
+  p.cnt = __shfl_up(m.cnt, d, 64);
+  p.reset = __shfl_up(m.reset, d, 64);
+  return p;
+}
+
+struct BetaOp {  // y ~ 1 + x (ret ~ mret): sums of 1, x, y, xx, xy, yy
+  static constexpr int NS = 6;
+  // v = 0 for an invalid row (NaN in either series); returns validity
+  __device__ static bool value(float yv, float xv, double (&v)[NS]) {
+    const bool ok = fin(yv) && fin(xv);
+    const double x = ok ? (double)xv : 0.0, y = ok ? (double)yv : 0.0;
+    v[0] = ok ? 1.0 : 0.0; v[1] = x; v[2] = y; v[3] = x * x; v[4] = x * y; v[5] = y * y;
+    return ok;
+  }
+  __device__ static void emit(const double (&S)[NS], int n, int minp, int r, float* o0, float* o1) {
+    float b = qnanf(), h = qnanf();
+    if (n >= minp && n > 2) {
+      const double iw = 1.0 / S[0];
+      const double mx = S[1] * iw, my = S[2] * iw;
+      const double vxx = S[3] * iw - mx * mx;
+      const double cxy = S[4] * iw - mx * my;
+      const double vyy = S[5] * iw - my * my;
+      const double bb = cxy / vxx;
+      const double ssr = fmax(S[0] * (vyy - bb * cxy), 0.0);
+      b = (float)bb;
+      h = (float)sqrt(ssr / (double)(n - 2));
+    }
+    o0[r] = b;
+    o1[r] = h;
+  }
+};
+
+struct DastdOp {  // e = ret - mret: sums of 1, e, ee; weighted population std
+  static constexpr int NS = 3;
+  __device__ static bool value(float a, float bm, double (&v)[NS]) {
+    const bool ok = fin(a) && fin(bm);
+    const double e = ok ? (double)a - (double)bm : 0.0;
+    v[0] = ok ? 1.0 : 0.0; v[1] = e; v[2] = e * e;
+    return ok;
+  }
+  __device__ static void emit(const double (&S)[NS], int n, int minp, int r, float* o0, float*) {
+    float o = qnanf();
+    if (n >= minp) {
+      const double m = S[1] / S[0];
+      o = (float)sqrt(fmax(S[2] / S[0] - m * m, 0.0));
+    }
+    o0[r] = o;
+  }
+};
+
+
+// padded staging index for C-row chunks: one spare word per chunk (odd lane stride C + 1)
+template <int C>
+__device__ __forceinline__ int ew_idx(int p) { return p + p / C; }
+
+// lam^k by binary powering (k < 512): no libm pow per table entry
+__device__ __forceinline__ double ipow(double lam, int k) {
+  double r = 1.0, b = lam;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    if (k & (1 << i)) r *= b;
+    b *= b;
+  }
+  return r;
+}
+
+// Persistent, software-pipelined variant: each block loops over tiles of TR staged rows; a
+// thread keeps its own C rows in registers (phase A and its own-row steps read them there, the
+// LDS copy only serves other threads' lagged rows) and issues the NEXT tile's loads before
+// computing the current one, so HBM latency hides behind the scan / window math.
+template <class Op, int C, int TR>
+__global__ __launch_bounds__(TR / C) void ew_window_pipe_kernel(
+    const float* __restrict__ in_a, const float* __restrict__ in_b,
+    const int* __restrict__ seg_lo, int R, int W, int H, double lam, int minp,
+    float* __restrict__ o0, float* __restrict__ o1, int ntiles) {
+  constexpr int NS = Op::NS, NT = TR / C, LEN = TR + TR / C;
+  __shared__ float sa[LEN], sb[LEN];
+  __shared__ short sd[LEN];  // rows since the stock start (clamped); -1 = outside [0, R)
+  __shared__ double carry[NT][NS];
+  __shared__ int ccnt[NT];
+  __shared__ EwMap<NS> wtot[NT / 64];
+  __shared__ double pw[257];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  for (int k = t; k <= W; k += NT) pw[k] = ipow(lam, k);
+  const int p0 = t * C;
+  auto load = [&](int tile, float (&xa)[C], float (&xb)[C], short (&xd)[C]) {
+    const int g = tile * (TR - H) - H + p0;
+    if (g >= 0 && g + C <= R) {
+#pragma unroll
+      for (int i = 0; i < C; i += 4) {
+        const float4 va = *(const float4*)(in_a + g + i), vb = *(const float4*)(in_b + g + i);
+        const int4 vs = *(const int4*)(seg_lo + g + i);
+        xa[i] = va.x; xa[i + 1] = va.y; xa[i + 2] = va.z; xa[i + 3] = va.w;
+        xb[i] = vb.x; xb[i + 1] = vb.y; xb[i + 2] = vb.z; xb[i + 3] = vb.w;
+        xd[i] = (short)min(g + i - vs.x, 32767);
+        xd[i + 1] = (short)min(g + i + 1 - vs.y, 32767);
+        xd[i + 2] = (short)min(g + i + 2 - vs.z, 32767);
+        xd[i + 3] = (short)min(g + i + 3 - vs.w, 32767);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < C; ++i) {
+        const int gi = g + i;
+        const bool in = gi >= 0 && gi < R;
+        xa[i] = in ? in_a[gi] : qnanf();
+        xb[i] = in ? in_b[gi] : qnanf();
+        xd[i] = (short)(in ? min(gi - seg_lo[gi], 32767) : -1);
+      }
+    }
+  };
+  // one row: reset at a stock start, decay only on valid rows (branchless, v = 0 if invalid)
+  auto row = [&](float av, float bv, short d, double (&S)[NS], int& c, double& A, int& rs) {
+    if (d < 0) return;
+    const bool st = d == 0;
+    double v[NS];
+    const bool ok = Op::value(av, bv, v);
+    const double f = st ? 0.0 : (ok ? lam : 1.0);
+#pragma unroll
+    for (int k = 0; k < NS; ++k) S[k] = fma(f, S[k], v[k]);
+    A = st ? (ok ? lam : 1.0) : A * (ok ? lam : 1.0);
+    c = (st ? 0 : c) + (ok ? 1 : 0);
+    rs |= st;
+  };
+  int tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  float ra[C], rb[C];
+  short rd[C];
+  load(tile, ra, rb, rd);
+  for (; tile < ntiles; tile += gridDim.x) {
+    const int g0 = tile * (TR - H) - H;
+#pragma unroll
+    for (int i = 0; i < C; ++i) {
+      const int q = ew_idx<C>(p0 + i);
+      sa[q] = ra[i];
+      sb[q] = rb[i];
+      sd[q] = rd[i];
+    }
+    float na[C], nb[C];
+    short nd[C];
+    const int nxt = tile + gridDim.x;
+    if (nxt < ntiles) load(nxt, na, nb, nd);
+    // A. chunk map from registers
+    EwMap<NS> m;
+    m.A = 1.0;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) m.B[k] = 0.0;
+    m.cnt = 0;
+    m.reset = 0;
+#pragma unroll
+    for (int i = 0; i < C; ++i) row(ra[i], rb[i], rd[i], m.B, m.cnt, m.A, m.reset);
+    // B. inclusive scan over the NT chunks
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const EwMap<NS> pm = ew_shfl_up(m, d);
+      if (lane >= d) ew_compose(m, pm);
+    }
+    if (lane == 63) wtot[wid] = m;
+    __syncthreads();
+    for (int w = wid - 1; w >= 0; --w) ew_compose(m, wtot[w]);
+#pragma unroll
+    for (int k = 0; k < NS; ++k) carry[t][k] = m.B[k];
+    ccnt[t] = m.cnt;
+    __syncthreads();
+    // C. outputs: own rows (registers) and lagged rows r - W (LDS)
+    if (p0 >= H) {
+      const int lp = p0 - W, lc = lp / C;
+      double E[NS], L[NS];
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        E[k] = t > 0 ? carry[t - 1][k] : 0.0;
+        L[k] = lc > 0 ? carry[lc - 1][k] : 0.0;
+      }
+      int ce = t > 0 ? ccnt[t - 1] : 0, cl = lc > 0 ? ccnt[lc - 1] : 0;
+      double dA = 1.0;
+      int drs = 0;
+      for (int p = lc * C; p < lp; ++p) {
+        const int q = ew_idx<C>(p);
+        row(sa[q], sb[q], sd[q], L, cl, dA, drs);
+      }
+#pragma unroll
+      for (int i = 0; i < C; ++i) {
+        const int r = g0 + p0 + i;
+        if (rd[i] < 0) break;  // past the end of the panel
+        const int q = ew_idx<C>(lp + i);
+        row(sa[q], sb[q], sd[q], L, cl, dA, drs);
+        row(ra[i], rb[i], rd[i], E, ce, dA, drs);
+        double S[NS];
+        int nv;
+        if (rd[i] >= W) {  // whole window inside the stock: subtract the lagged prefix
+          nv = ce - cl;
+          const double f = pw[nv];
+#pragma unroll
+          for (int k = 0; k < NS; ++k) S[k] = fma(-f, L[k], E[k]);
+        } else {
+          nv = ce;
+#pragma unroll
+          for (int k = 0; k < NS; ++k) S[k] = E[k];
+        }
+        Op::emit(S, nv, minp, r, o0, o1);
+      }
+    }
+    __syncthreads();  // LDS tile / carries are rewritten by the next iteration
+#pragma unroll
+    for (int i = 0; i < C; ++i) {
+      ra[i] = na[i];
+      rb[i] = nb[i];
+      rd[i] = nd[i];
+    }
+  }
+}
+
+template <class Op, int C, int TR>
+void launch_ew_pipe(const float* a, const float* b, const int* seg, int R, int W, int H,
+                    double lam, int minp, float* o0, float* o1, hipStream_t s) {
+  static int blocks = 0;
+  if (blocks == 0) {
+    int dev = 0, cus = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, ew_window_pipe_kernel<Op, C, TR>, TR / C, 0);
+    blocks = max(1, cus * max(per, 1));
+  }
+  const int ntiles = (R + TR - H - 1) / (TR - H);
+  hipLaunchKernelGGL((ew_window_pipe_kernel<Op, C, TR>), dim3(min(ntiles, blocks)), dim3(TR / C), 0,
+                     s, a, b, seg, R, W, H, lam, minp, o0, o1, ntiles);
+}
+
+template <class Op>
+void launch_ew(const float* a, const float* b, const int* seg, int R, int W, int H, double lam,
+               int minp, float* o0, float* o1, hipStream_t s) {
+  launch_ew_pipe<Op, 8, 2048>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
+}
+
 template <int H>
 struct Stage1 {  // one float series + seg_lo
   float a[lds_len(H + kBlockRows)];
@@ -612,7 +887,10 @@ __global__ __launch_bounds__(256) void cmra_scan_kernel(const float* __restrict_
   }
 }
 
-int g_roll_mode = 0;  // 0 = sliding-window kernels, 1 = direct per-row kernels (A/B, tests)
+int g_roll_mode = 0;  // 0 = default (anchored-prefix / sliding-window kernels), 1 = direct per-row
+                      // kernels (A/B, tests), 2 = round-1 sliding-window BETA / DASTD (A/B)
+
+int ew_halo(int W) { return (W + kChunk - 1) / kChunk * kChunk; }
 
 }  // namespace
 
@@ -624,7 +902,9 @@ MFA_API void mfa_rolling_set_mode(int mode) { g_roll_mode = mode; }
 MFA_API int mfa_beta_hsigma(const float* y, const float* x, const int* seg_lo, int R, int W,
                             double lam, int minp, float* beta, float* hsig, void* s) {
   if (R <= 0) return 0;
-  if (g_roll_mode == 0 && W <= 256)
+  if (g_roll_mode == 0 && W >= 1 && W <= 256) {
+    launch_ew<BetaOp>(y, x, seg_lo, R, W, ew_halo(W), lam, minp, beta, hsig, (hipStream_t)s);
+  } else if (g_roll_mode == 2 && W <= 256)
     hipLaunchKernelGGL(beta_hsigma_scan_kernel<256>, MFA_SCAN_GRID(R), 0, (hipStream_t)s, y, x,
                        seg_lo, R, W, lam, minp, beta, hsig);
   else
@@ -635,7 +915,7 @@ MFA_API int mfa_beta_hsigma(const float* y, const float* x, const int* seg_lo, i
 MFA_API int mfa_rstr(const float* lr, const int* seg_lo, int R, int L, int W, double lam,
                      int minp, float* out, void* s) {
   if (R <= 0) return 0;
-  if (g_roll_mode == 0 && W + L <= 512 && W + kChunk + 1 <= kPowMax)
+  if (g_roll_mode != 1 && W + L <= 512 && W + kChunk + 1 <= kPowMax)
     hipLaunchKernelGGL(rstr_scan_kernel<512>, MFA_SCAN_GRID(R), 0, (hipStream_t)s, lr, seg_lo, R, L,
                        W, lam, minp, out);
   else
@@ -645,7 +925,9 @@ MFA_API int mfa_rstr(const float* lr, const int* seg_lo, int R, int L, int W, do
 MFA_API int mfa_dastd(const float* ret, const float* mret, const int* seg_lo, int R, int W,
                       double lam, int minp, float* out, void* s) {
   if (R <= 0) return 0;
-  if (g_roll_mode == 0 && W <= 256)
+  if (g_roll_mode == 0 && W >= 1 && W <= 256) {
+    launch_ew<DastdOp>(ret, mret, seg_lo, R, W, ew_halo(W), lam, minp, out, out, (hipStream_t)s);
+  } else if (g_roll_mode == 2 && W <= 256)
     hipLaunchKernelGGL(dastd_scan_kernel<256>, MFA_SCAN_GRID(R), 0, (hipStream_t)s, ret, mret,
                        seg_lo, R, W, lam, minp, out);
   else
@@ -656,7 +938,7 @@ MFA_API int mfa_dastd(const float* ret, const float* mret, const int* seg_lo, in
 MFA_API int mfa_cmra(const float* lr, const int* seg_lo, int R, int W, int partial, float* out,
                      void* s) {
   if (R <= 0) return 0;
-  if (g_roll_mode == 0 && W <= 256 && W >= kChunk)
+  if (g_roll_mode != 1 && W <= 256 && W >= kChunk)
     hipLaunchKernelGGL(cmra_scan_kernel<256>, MFA_SCAN_GRID(R), 0, (hipStream_t)s, lr, seg_lo, R, W,
                        partial, out);
   else
@@ -666,7 +948,7 @@ MFA_API int mfa_cmra(const float* lr, const int* seg_lo, int R, int W, int parti
 MFA_API int mfa_rolling_sum(const float* x, const int* seg_lo, int R, int W, int minp,
                             double scale, int mode, float* out, void* s) {
   if (R <= 0) return 0;
-  if (g_roll_mode == 0 && W <= 256)
+  if (g_roll_mode != 1 && W <= 256)
     hipLaunchKernelGGL(rolling_sum_scan_kernel<256>, MFA_SCAN_GRID(R), 0, (hipStream_t)s, x, seg_lo,
                        R, W, minp, scale, mode, out);
   else

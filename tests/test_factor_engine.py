@@ -135,6 +135,90 @@ def test_hip_sliding_window_kernels_match_direct(cuda):
             torch.testing.assert_close(y.cpu(), x.cpu(), rtol=2e-5, atol=2e-7, equal_nan=True, msg=k)
 
 
+_FIXTURE = __import__("pathlib").Path(__file__).parent / "fixtures" / "ref_descriptors_n50_t800_seed5.npz"
+
+
+def _check_against_fixture(out):
+    """Descriptors vs the reference FactorCalculator's output for synthetic_prices(N=50, T=800,
+    seed=5, suspend_frac=0.03), computed once by running the reference source and stored as
+    npz (tests/fixtures; loaded with allow_pickle=False)."""
+    fx = np.load(_FIXTURE, allow_pickle=False)
+    assert (out["ts_code"].astype(str).to_numpy() == fx["ts_code"]).all()
+    assert (out["trade_date"].astype(str).to_numpy() == fx["trade_date"]).all()
+    for c in ["ret", "circ_mv"] + COLS:
+        a, b = out[c].to_numpy(np.float64), fx["col_" + c]
+        assert (np.isnan(a) == np.isnan(b)).all(), c
+        m = np.isfinite(b)
+        np.testing.assert_allclose(a[m], b[m], rtol=2e-4, atol=1e-6, err_msg=c)
+
+
+def test_descriptors_match_reference_fixture_n50_t800():
+    prices, index, _ = FE.synthetic_prices(N=50, T=800, seed=5, suspend_frac=0.03)
+    eng = FE.FactorEngine(prices, index, device="cpu")
+    with contextlib.redirect_stdout(io.StringIO()):
+        _check_against_fixture(eng.run(FE.FACTORS_TO_RUN))
+
+
+@pytest.mark.gpu
+def test_hip_descriptors_match_reference_fixture_n50_t800(cuda):
+    prices, index, _ = FE.synthetic_prices(N=50, T=800, seed=5, suspend_frac=0.03)
+    eng = FE.FactorEngine(prices, index, device=cuda)
+    with contextlib.redirect_stdout(io.StringIO()):
+        _check_against_fixture(eng.run(FE.FACTORS_TO_RUN))
+
+
+@pytest.mark.gpu
+def test_hip_rolling_kernels_large_ragged_panel(cuda):
+    """500 stocks with ragged histories of 300..9000 rows (2.3 M flat rows; many stocks longer
+    than the 4096-row LDS block, stock starts anywhere inside blocks), 2 % suspensions: the
+    default kernels == the direct per-row kernels, and the anchored-prefix BETA / DASTD ==
+    the round-1 sliding-window kernels."""
+    from llm_driven_multi_factor_model_amd import _native
+    g = torch.Generator().manual_seed(11)
+    N = 500
+    lens = torch.randint(300, 9000, (N,), generator=g)
+    R = int(lens.sum())
+    stock = torch.repeat_interleave(torch.arange(N, dtype=torch.int32), lens)
+    day = torch.cat([torch.arange(int(n)) for n in lens])
+    T = int(lens.max())
+    mkt = torch.randn(T, generator=g) * 0.012
+    ret = (mkt[day] * 1.1 + torch.randn(R, generator=g) * 0.02).float()
+    ret[torch.rand(R, generator=g) < 0.02] = float("nan")
+    mret = mkt[day].float().contiguous()
+    lr = torch.log1p(ret)
+    turn = torch.rand(R, generator=g) * 5
+    turn[torch.rand(R, generator=g) < 0.2] = 0.0
+    seg = RL.seg_lo_from_codes(stock).to(cuda)
+    r_, m_, l_, t_ = (x.to(cuda) for x in (ret, mret, lr, turn))
+    fns = {
+        "beta": lambda: RL.beta_hsigma(r_, m_, seg, 252, 63.0, 42),
+        "dastd": lambda: RL.dastd(r_, m_, seg, 252, 42.0, 42),
+        "beta_short": lambda: RL.beta_hsigma(r_, m_, seg, 20, 5.0, 10),
+        "dastd_short": lambda: RL.dastd(r_, m_, seg, 17, 7.0, 5),
+        "rstr": lambda: RL.rstr(l_, seg, 504, 21, 126.0, 42),
+        "stom": lambda: RL.rolling_sum(t_, seg, 21, 15, 0.01, log=True),
+        "stoa": lambda: RL.rolling_sum(t_, seg, 252, 126, 0.01, log=True),
+        "cmra": lambda: RL.cmra(l_, seg, 252),
+        "cmra_partial": lambda: RL.cmra(l_, seg, 252, partial=True),
+    }
+    lib = _native.lib()
+    out = {}
+    try:
+        for mode in (1, 2, 0):
+            lib.mfa_rolling_set_mode(mode)
+            out[mode] = {k: f() for k, f in fns.items()}
+    finally:
+        lib.mfa_rolling_set_mode(0)
+    for k in fns:
+        for ref_mode in (1, 2):
+            a = out[ref_mode][k] if isinstance(out[ref_mode][k], tuple) else (out[ref_mode][k],)
+            b = out[0][k] if isinstance(out[0][k], tuple) else (out[0][k],)
+            for x, y in zip(a, b):
+                # full-window CMRA needs 252 NaN-free rows: rare at 2 % suspensions
+                assert int(torch.isfinite(x).sum()) > (1000 if k == "cmra" else R // 2), k
+                torch.testing.assert_close(y.cpu(), x.cpu(), rtol=2e-5, atol=2e-7, equal_nan=True,
+                                           msg=f"{k} vs mode {ref_mode}")
+
 
 def test_barra_export_fast_path_equals_merge_path(data):
     """The index-lookup export (unique industry rows) equals the pandas merge / groupby-shift

@@ -15,8 +15,10 @@ for f in glob.glob("gpurun_out/pmc_roll/k/**/run_kernel_stats.csv", recursive=Tr
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob("gpurun_out/pmc_roll/a/**/run_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "scan_kernel" in r["Kernel_Name"]:
-            agg[r["Kernel_Name"].split("(")[0][-60:]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        kn = r["Kernel_Name"]
+        if "scan_kernel" in kn or "ew_window" in kn:
+            key = kn[kn.find("::") + 2:kn.find("_kernel") + 7] + ("<" + kn.split("::")[2][:8] + ">" if "ew_window" in kn else "")
+            agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in agg.items():
     v = {c: sum(x) / len(x) for c, x in d.items()}
     wc = v.get("SQ_WAVE_CYCLES", 1)

@@ -1,0 +1,59 @@
+"""A/B of the BETA/HSIGMA and DASTD window kernels on a 5000 x 3780 flat panel (event timing):
+round-1 sliding-window kernels (mode 2) vs the default anchored-prefix pipelined kernel.  Prints ms and effective HBM bandwidth (inputs + outputs, 4 B each)."""
+import json
+import os
+import statistics
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from llm_driven_multi_factor_model_amd import _native  # noqa: E402
+from llm_driven_multi_factor_model_amd.ops import rolling as RL  # noqa: E402
+
+N = int(os.environ.get("N", 5000))
+T = int(os.environ.get("T", 3780))
+dev = torch.device("cuda:0")
+g = torch.Generator(device=dev).manual_seed(0)
+R = N * T
+mkt = torch.randn(T, device=dev, generator=g) * 0.012
+ret = (mkt[None, :] * 1.1 + torch.randn(N, T, device=dev, generator=g) * 0.02).reshape(-1).float()
+ret[torch.rand(R, device=dev, generator=g) < 0.02] = float("nan")
+mret = mkt[None, :].expand(N, T).reshape(-1).contiguous().float()
+stock = torch.arange(N, device=dev, dtype=torch.int32).repeat_interleave(T)
+seg = RL.seg_lo_from_codes(stock)
+lib = _native.lib()
+beta, hsig, dast = (torch.empty(R, device=dev) for _ in range(3))
+cases = {
+    "beta_hsigma": (lambda: _native.call("mfa_beta_hsigma", _native.ptr(ret), _native.ptr(mret),
+                                         _native.ptr(seg), R, 252, 0.5 ** (1 / 63), 42,
+                                         _native.ptr(beta), _native.ptr(hsig), _native.stream(dev)), 20),
+    "dastd": (lambda: _native.call("mfa_dastd", _native.ptr(ret), _native.ptr(mret), _native.ptr(seg),
+                                   R, 252, 0.5 ** (1 / 42), 42, _native.ptr(dast), _native.stream(dev)), 16),
+}
+variants = [("mode2_r01", 2), ("anchored_prefix", 0)]
+ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+ref = {}
+for name, (fn, bpr) in cases.items():
+    res = {}
+    for vname, mode in variants:
+        lib.mfa_rolling_set_mode(mode)
+        fn()
+        torch.cuda.synchronize()
+        out = (beta.clone(), hsig.clone()) if name == "beta_hsigma" else (dast.clone(),)
+        if vname == "mode2_r01":
+            ref[name] = out
+        err = max(((a - b).abs() / b.abs().clamp_min(1e-6)).nan_to_num(0).max().item()
+                  for a, b in zip(out, ref[name]))
+        ts = []
+        for _ in range(5):
+            ev0.record()
+            for _ in range(10):
+                fn()
+            ev1.record()
+            ev1.synchronize()
+            ts.append(ev0.elapsed_time(ev1) / 10)
+        ms = statistics.median(ts)
+        res[vname] = {"ms": round(ms, 4), "TB_s": round(R * bpr / ms / 1e9, 3), "max_rel_vs_r01": err}
+    print(json.dumps({"kernel": name, "N": N, "T": T, **res}), flush=True)
+lib.mfa_rolling_set_mode(0)
