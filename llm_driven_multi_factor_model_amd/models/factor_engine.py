@@ -94,10 +94,22 @@ class FactorEngine:
         dc, dstr = self._date_strings(prices_df["trade_date"])
         dnames = np.unique(dstr)                      # sorted "%Y/%m/%d" == chronological
         drank = np.searchsorted(dnames, dstr)         # unique-date code -> sorted date code
-        scodes, snames = pd.factorize(prices_df["ts_code"].astype(str), sort=True)
+        tc = prices_df["ts_code"]
+        if not (tc.dtype == object and pd.api.types.infer_dtype(tc, skipna=False) == "string"):
+            tc = tc.astype(str)                       # (skip the 2.5M-string copy when already str)
+        scodes, snames = pd.factorize(tc, sort=True)
         row_d = drank[dc]
-        order = np.lexsort((row_d, scodes))           # stable: ts_code, then trade_date
-        p = pd.DataFrame({c: prices_df[c].to_numpy()[order] for c in prices_df.columns})
+        # stable sort by (ts_code, trade_date) on one int64 key; input already in that order
+        # (the usual case for stored panels) is detected in O(n) and not permuted at all
+        key = scodes.astype(np.int64) * len(dnames) + row_d
+        if len(key) < 2 or bool((key[1:] >= key[:-1]).all()):
+            order = np.arange(len(key))
+            p = prices_df.copy(deep=False)
+            p.index = pd.RangeIndex(len(p))
+        else:
+            order = np.argsort(key, kind="stable")
+            p = prices_df.take(order)
+            p.index = pd.RangeIndex(len(p))
         p["trade_date"] = dnames[row_d[order]]
         ix = index_df[["trade_date", "close"]].copy()
         ic, istr = self._date_strings(ix["trade_date"])
@@ -501,10 +513,99 @@ def barra_export(processed: pd.DataFrame, sw_industry: pd.DataFrame, _merge_path
     return final, info
 
 
+def _pipeline_columnar(eng: "FactorEngine", factors, cfg: FactorConfig, sw_industry: pd.DataFrame, t: dict):
+    """Single-process fast path of :func:`factor_pipeline` (same output frames, bit for bit):
+    the descriptors stay device tensors through winsorize / composite / orthogonalize on the
+    engine's own (date, stock) grid index (no re-factorisation of string keys), the t+1 return
+    is a shift on stock ids, and the export frame is built once from ONE device->host copy.
+    Mirrors main.py:42-137 (winsorize incl. ret / circ_mv, composites, orthogonalisation,
+    industry merge, t+1 return, rename)."""
+    t0 = time.perf_counter()
+    res = eng.compute(factors)
+    m = eng.master
+    t["descriptors_s"] = t.pop("prep_s", 0.0) + time.perf_counter() - t0
+    t0 = time.perf_counter()
+    dev, nan = eng.device, float("nan")
+    D, N, idx = eng.D, eng.N, eng.grid_idx
+
+    def put(x):
+        g = torch.full((D * N,), nan, dtype=torch.float32, device=dev)
+        g[idx] = x.to(torch.float32)
+        return g.view(D, N)
+
+    def take(g):
+        return g.reshape(-1)[idx]
+
+    col = {"ret": eng.cols["ret"],
+           "circ_mv": eng.cols["circ_mv"] if "circ_mv" in eng.cols else torch.full((eng.R,), nan, device=dev)}
+    col.update(res)
+    for f in list(col):  # winsorize every non-key column (incl. ret, circ_mv: quirk Q23)
+        col[f] = take(XR.winsorize(put(col[f]), cfg.winsor_n_std))
+    for new, cc in cfg.composite.items():
+        xs, ws = [], []
+        for c, w in zip(cc["components"], cc["weights"]):
+            if c in col:
+                xs.append(col[c].to(torch.float32))
+                ws.append(w)
+            else:
+                print(f"Warning: Component '{c}' not found in DataFrame. Skipping.")
+        col[new] = XR.composite(xs, ws) if xs else torch.full((eng.R,), nan, device=dev, dtype=torch.float64)
+    for target, against in cfg.ortho.items():
+        col[target] = take(XR.ols_resid(put(col[target]), [put(col[a]) for a in against],
+                                        min_rows=len(against) + 2))
+    t["postprocess_s"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    sid = eng.stock_id
+    ret = col["ret"].double()
+    nxt = torch.full_like(ret, nan)  # groupby(ts_code).shift(-1) in master (stock-sorted) order
+    if eng.R > 1:
+        nxt[:-1] = torch.where(sid[1:] == sid[:-1], ret[1:], ret.new_tensor(nan))
+    inv = {v: k for k, v in BARRA_RENAME.items()}
+    names, tens = [], []  # numeric export columns in output order
+    for c in BARRA_OUTPUT_COLUMNS:
+        s0 = inv.get(c, c)
+        if s0 == "ret":
+            names.append(c)
+            tens.append(nxt)
+        elif s0 not in ("ts_code", "trade_date", "l1_code") and s0 in col and (s0 == c or c not in col):
+            names.append(c)
+            tens.append(col[s0].double())
+    host = torch.stack(tens).cpu().numpy()  # ONE device->host copy, [columns, rows]
+    codes = m["ts_code"].to_numpy()
+    first = np.r_[0, np.flatnonzero(np.diff(sid.cpu().numpy())) + 1]  # first row of each stock
+    stock_keys = codes[first]
+    pos = pd.Index(sw_industry["ts_code"]).get_indexer(stock_keys)
+    l1 = sw_industry["l1_code"].to_numpy(dtype=object)
+    l1_stock = np.where(pos >= 0, l1[np.maximum(pos, 0)], np.nan).astype(object)
+    counts = np.diff(np.r_[first, eng.R])
+    # the float block is the host array itself (no consolidation copy); key / industry object
+    # columns are inserted at their output positions
+    final = pd.DataFrame(host.T, columns=names, copy=False)
+    for i, c in enumerate(BARRA_OUTPUT_COLUMNS):
+        s0 = inv.get(c, c)
+        at = sum(1 for x in BARRA_OUTPUT_COLUMNS[:i] if x in final.columns)
+        if s0 == "trade_date":
+            final.insert(at, c, m["trade_date"].to_numpy())
+        elif s0 == "ts_code":
+            final.insert(at, c, codes)
+        elif s0 == "l1_code":
+            final.insert(at, c, pd.Series(np.repeat(l1_stock, counts), dtype=object))
+    stk = pd.DataFrame({"ts_code": pd.unique(stock_keys)})
+    cols = [c for c in ["ts_code", "l1_code", "l1_name", "in_date"] if c in sw_industry.columns]
+    info = stk.merge(sw_industry[cols], on="ts_code", how="left")
+    info = info.drop_duplicates(subset=[c for c in ["l1_code", "l1_name"] if c in info.columns]).rename(
+        columns={"l1_code": "code", "l1_name": "industry_names", "in_date": "start_date"})
+    info = info[[c for c in ["code", "industry_names", "start_date"] if c in info.columns]]
+    t["export_s"] = time.perf_counter() - t0
+    return final, info
+
+
 def factor_pipeline(prices_df, index_df, sw_industry_df, factors=None, config: FactorConfig | None = None,
-                    device=None, ctx=None):
+                    device=None, ctx=None, columnar: bool = True):
     """main.py end to end: raw descriptors -> winsorize -> composite -> orthogonalize -> export.
 
+    Single process (the default): :func:`_pipeline_columnar`, device tensors end to end and
+    one export frame; ``columnar=False`` runs the frame-by-frame compat path (same output).
     With an enabled ``ctx`` (torchrun, one rank per GPU) each rank computes its date block
     (``date_shard``: descriptors with a halo, then the per-date post-processing) and rank 0
     gathers the blocks and writes the export; other ranks return ``(None, None, timings)``.
@@ -517,6 +618,11 @@ def factor_pipeline(prices_df, index_df, sw_industry_df, factors=None, config: F
     t = {}
     t0 = time.perf_counter()
     eng = FactorEngine(prices_df, index_df, device=device, config=cfg)
+    if (columnar and not dist_on and eng.R == len(prices_df) and sw_industry_df["ts_code"].is_unique
+            and len(eng.master) == eng.R):
+        t["prep_s"] = time.perf_counter() - t0
+        final, info = _pipeline_columnar(eng, factors or FACTORS_TO_RUN, cfg, sw_industry_df, t)
+        return final, info, dict(t, kernel_ms=getattr(eng, "timings", {}))
     if dist_on:
         eng = eng.date_shard(*pdist.shard_range(eng.D, ctx.rank, ctx.world))
     raw = eng.run(factors or FACTORS_TO_RUN)

@@ -220,6 +220,28 @@ def test_hip_rolling_kernels_large_ragged_panel(cuda):
                                            msg=f"{k} vs mode {ref_mode}")
 
 
+def _pipeline_paths_equal(device):
+    prices, index, sw = FE.synthetic_prices(N=40, T=420, seed=6, suspend_frac=0.03)
+    sw = sw.iloc[1:].reset_index(drop=True)  # one stock without an industry row
+    with contextlib.redirect_stdout(io.StringIO()):
+        f1, i1, t1 = FE.factor_pipeline(prices, index, sw, device=device)
+        f0, i0, _ = FE.factor_pipeline(prices, index, sw, device=device, columnar=False)
+    assert "export_s" in t1
+    pd.testing.assert_frame_equal(f1, f0.reset_index(drop=True))
+    pd.testing.assert_frame_equal(i1, i0)
+
+
+def test_columnar_pipeline_equals_frame_pipeline():
+    """The single-process columnar fast path (device tensors through post-processing, one
+    export frame) gives exactly the frame-by-frame pipeline's output frames."""
+    _pipeline_paths_equal("cpu")
+
+
+@pytest.mark.gpu
+def test_hip_columnar_pipeline_equals_frame_pipeline(cuda):
+    _pipeline_paths_equal(cuda)
+
+
 def test_barra_export_fast_path_equals_merge_path(data):
     """The index-lookup export (unique industry rows) equals the pandas merge / groupby-shift
     path it replaces, including suspended stocks and a stock missing from the industry table."""

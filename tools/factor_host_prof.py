@@ -57,3 +57,19 @@ for name, p in profs.items():
     pstats.Stats(p, stream=s).sort_stats("tottime").print_stats(14)
     print(f"==== {name} ({times[name]:.3f} s)")
     print("\n".join(line[:170] for line in s.getvalue().splitlines()[6:24]))
+
+# the pipeline entry point (single process: columnar fast path) end to end
+for rep in range(2):
+    torch.cuda.synchronize()
+    p = cProfile.Profile()
+    t0 = time.perf_counter()
+    p.enable()
+    with contextlib.redirect_stdout(io.StringIO()):
+        final, info, tt = FE.factor_pipeline(prices, index, sw, device=dev)
+    p.disable()
+    wall = time.perf_counter() - t0
+print("factor_pipeline (columnar)", {k: (round(v, 3) if isinstance(v, float) else v) for k, v in tt.items() if k != "kernel_ms"},
+      "wall", round(wall, 3), "rows", len(final))
+s = io.StringIO()
+pstats.Stats(p, stream=s).sort_stats("tottime").print_stats(20)
+print("\n".join(line[:170] for line in s.getvalue().splitlines()[6:30]))
