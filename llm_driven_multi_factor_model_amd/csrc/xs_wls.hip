@@ -17,6 +17,13 @@ MFA_API void mfa_xs_set_chunks(int S) { g_mfa_xs_chunks = S; }
 // Chunks per date the next mfa_xs_wls / mfa_xs_wls_f64 call on (D, N) will use.
 MFA_API int mfa_xs_chunks(int D, int N) { return xs_chunks(D, N); }
 
+// 1 if the bitwise-deterministic kernel (8 wave-owned segment replicas) fits P industries x Q
+// styles; larger tables run the shared-replica kernel (reproducible to rounding only).
+MFA_API int mfa_xs_det_supported(int P, int Q) {
+  const size_t Pseg = P > 0 ? (size_t)P : 1;
+  return Pseg * ((size_t)(Q + 3) * kRepMax + kXsSegPad) * sizeof(double) <= (size_t)kSegLdsBudget;
+}
+
 // Workspace bytes needed by mfa_xs_wls / mfa_xs_wls_f64 on (D, N, P, Q).
 MFA_API size_t mfa_xs_wls_workspace(int D, int N, int P, int Q) {
   return xs_workspace_bytes(D, N, P, Q);

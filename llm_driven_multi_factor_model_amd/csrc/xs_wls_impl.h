@@ -113,6 +113,7 @@ __device__ __forceinline__ void wave_sync_lds() {
 // (l & 7) + 8 * ((j*NS + ch) & 1): at most 2-way conflicts whatever the industry mix (4
 // lane-strided replicas measured 8.3 conflict cycles per instruction).
 constexpr int kRepMax = MFA_XS_REP;
+constexpr int kXsSegPad = 2;  // doubles of padding per industry segment (LDS bank spread)
 constexpr int kSegLdsBudget = 48 * 1024;  // R = 8 only while the table leaves 2 WGs / CU
 constexpr int kWT = 64;                   // stocks per wave tile (K1: one stock per lane)
 
@@ -139,6 +140,13 @@ struct Layout {
   static constexpr int ROWB = kWT * (int)sizeof(T);            // one field row of a wave tile
   static constexpr int WSLOT = (Q + 2) * ROWB + kWT * 2;       // K1 per-wave ring slot
   __host__ __device__ static constexpr int msize(int Pseg) { return NACC + Pseg * NS; }
+  // replicated segment table [Pseg][NS][R] + SEGPAD doubles per segment: without the pad every
+  // segment starts at the same LDS bank (NS * R * 8 B = 0 mod 128 B), so lanes of one
+  // ds_add_f64 that own the same replica pile onto 2 banks whatever their industries (8-way
+  // conflicts in the 2-replicas-per-wave deterministic mode)
+  static constexpr int SEGPAD = kXsSegPad;
+  __host__ __device__ static constexpr int seg_stride(int R) { return NS * R + SEGPAD; }
+  __host__ __device__ static constexpr int seg_doubles(int R, int Pseg) { return Pseg * seg_stride(R); }
 };
 
 // Reduce a compile-time register array across the workgroup into out[0..CNT) (LDS, zeroed by
@@ -217,8 +225,9 @@ __device__ __forceinline__ void moments_body(
   static_assert(!DET || (R % 4 == 0 && NACC <= 256), "deterministic mode: 4 waves, R/4 replicas each");
   const int rep = DET ? wid * (R / 4) + (lane & (R / 4 - 1)) : (lane & (R - 1));
   const unsigned seg_a = lds_addr(dyn + rep);
-  double* acc = dyn + R * Pseg * NS;
-  for (int i = tid; i < R * Pseg * NS + NACC; i += nthr) dyn[i] = 0.0;
+  constexpr int SJ = L::seg_stride(R);
+  double* acc = dyn + Pseg * SJ;
+  for (int i = tid; i < Pseg * SJ + NACC; i += nthr) dyn[i] = 0.0;
   __syncthreads();
 
   const T* Xd = X + (size_t)d * Q * N;
@@ -303,12 +312,13 @@ __device__ __forceinline__ void moments_body(
       if (VAR & 1) {  // timing-only ablation: skip the segment atomics
         asm volatile("" ::"v"(w), "v"(r));
       } else {
-        const unsigned a = seg_a + (unsigned)(j * NS * R * 8);
+        const unsigned a = seg_a + (unsigned)(j * SJ * 8);
+        const double wr = w * r;
         lds_add_nowait<0>(a, w);
         [&]<int... I>(std::integer_sequence<int, I...>) {
           (lds_add_nowait<8 * R * (1 + I)>(a, wx[I]), ...);
         }(std::make_integer_sequence<int, Q>{});
-        lds_add_nowait<8 * R * (Q + 1)>(a, w * r);
+        lds_add_nowait<8 * R * (Q + 1)>(a, wr);
         lds_add_nowait<8 * R * (Q + 2)>(a, c);
       }
     }
@@ -335,9 +345,10 @@ __device__ __forceinline__ void moments_body(
     }
   }
   for (int i = tid; i < Pseg * NS; i += nthr) {
+    const double* row = dyn + (i / NS) * SJ + (i % NS) * R;
     double t = 0.0;
 #pragma unroll
-    for (int r = 0; r < R; ++r) t += dyn[i * R + r];
+    for (int r = 0; r < R; ++r) t += row[r];
     md[NACC + i] = t;
     if (gout) gout[NACC + i] = t;
   }
@@ -1215,9 +1226,10 @@ __device__ __forceinline__ void moments_body_mf(
     if (gout) gout[tid] = mv;
   }
   for (int i = tid; i < Pseg * NS; i += nthr) {
+    const double* row = dyn + i * R;  // unpadded [Pseg * NS][R] table (MFMA A/B kernels)
     double t = 0.0;
 #pragma unroll
-    for (int r = 0; r < R; ++r) t += dyn[i * R + r];
+    for (int r = 0; r < R; ++r) t += row[r];
     md[NACC + i] = t;
     if (gout) gout[NACC + i] = t;
   }
@@ -1557,9 +1569,9 @@ hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, 
   double* mom = ws;
   double* coef = ws + (size_t)D * S * MS;
   double* sums = coef + (size_t)D * (Q + 1 + P);
-  const size_t seg8 = (size_t)kRepMax * Pseg * L::NS * sizeof(double);
+  const size_t seg8 = (size_t)L::seg_doubles(kRepMax, Pseg) * sizeof(double);
   const bool rep8 = seg8 <= kSegLdsBudget;
-  const size_t lds1 = ((rep8 ? (size_t)kRepMax : 1) * Pseg * L::NS + L::NACC) * sizeof(double);
+  const size_t lds1 = ((size_t)L::seg_doubles(rep8 ? kRepMax : 1, Pseg) + L::NACC) * sizeof(double);
   const size_t lds2 = solve_lds_bytes<Q, T>(Pseg);
   if (lds1 + fused_ring_bytes<Q, T>() > 160 * 1024 || lds2 > 64 * 1024) return hipErrorInvalidValue;
   if (refine && 1 + P + Q > kXsRefineMaxK) return hipErrorInvalidValue;
@@ -1661,9 +1673,9 @@ hipError_t split_q(int what, const T* X, const T* cap, const T* ret, const int16
   const int Pseg = P > 0 ? P : 1;
   const int16_t* indp = P > 0 ? ind : nullptr;
   if (what == 0) {
-    const size_t seg8 = (size_t)kRepMax * Pseg * L::NS * sizeof(double);
+    const size_t seg8 = (size_t)L::seg_doubles(kRepMax, Pseg) * sizeof(double);
     const bool rep8 = seg8 <= kSegLdsBudget;
-    const size_t lds1 = ((rep8 ? (size_t)kRepMax : 1) * Pseg * L::NS + L::NACC) * sizeof(double);
+    const size_t lds1 = ((size_t)L::seg_doubles(rep8 ? kRepMax : 1, Pseg) + L::NACC) * sizeof(double);
     if (lds1 + Ring<Q, T>::BYTES > 160 * 1024) return hipErrorInvalidValue;
     if (rep8)
       hipLaunchKernelGGL((xs_moments_kernel<Q, 0, kRepMax, T>), dim3(D), dim3(256), lds1, s, X,

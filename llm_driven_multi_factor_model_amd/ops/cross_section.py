@@ -79,7 +79,7 @@ def _validate(X, cap, ret, ind, P):
 def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Tensor | None,
            P: int, *, pivot_mode: int = 0, tol: float = 1e-14, want_resid: bool = True,
            refine: bool = True, out: XsResult | None = None,
-           workspace: torch.Tensor | None = None, deterministic: bool = False) -> XsResult:
+           workspace: torch.Tensor | None = None, deterministic: bool | None = None) -> XsResult:
     """Regress every date of the panel in one batched call.
 
     X [D,Q,N] styles, cap/ret [D,N] (all float64 or all float32), ind [D,N] int16 industry ids
@@ -92,9 +92,11 @@ def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Ten
     ``out`` / ``workspace`` let a caller (e.g. a timed loop) reuse preallocated buffers.
     The GPU kernels need N % 8 == 0 (16-byte rows for the LDS-DMA ring); other N are padded
     here with absent stocks (``ind = -1``), which costs a copy — keep panels padded.
-    ``deterministic`` selects the bitwise-reproducible kernel variant (each LDS segment replica
-    owned by one wave, wave partials summed in order); the default shares replicas across waves
-    for fewer bank conflicts and reproduces to rounding only.
+    ``deterministic`` (default: on whenever the kernel supports it, i.e. the 8-replica segment
+    table fits: P <= 53 industries at Q = 10) selects the bitwise-reproducible kernel: each LDS
+    segment replica is owned by one wave and the wave partials are summed in a fixed order.  It
+    costs 0-3 % (profiles/r02_xs_deterministic.md); ``False`` shares the replicas across waves
+    (reproducible to rounding only).
     """
     D, Q, N = _validate(X, cap, ret, ind, P)
     K = 1 + P + Q
@@ -132,6 +134,8 @@ def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Ten
     if workspace is None or workspace.numel() < need:
         workspace = torch.empty(need, dtype=torch.uint8, device=dev)
     dev_refine = refine and K <= REFINE_MAX_K
+    if deterministic is None:
+        deterministic = bool(_native.lib().mfa_xs_det_supported(P, Q))
     flags = (XS_DETERMINISTIC if deterministic else 0) | (XS_REFINE if dev_refine else 0)
     _native.call("mfa_xs_wls_f64" if dt == torch.float64 else "mfa_xs_wls", _native.ptr(X),
                  _native.ptr(cap), _native.ptr(ret),

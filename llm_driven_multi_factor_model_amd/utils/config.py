@@ -28,7 +28,8 @@ class RiskConfig:
     eigen_shard: str = "dates"    # "dates": each rank adjusts its own dates with all M sims;
                                   # "sims": ranks split the M sims of every date + all_reduce (C5)
     eigen_chunk: int = 256        # sims per launch in "sims" mode (bounds the [D, chunk, K] buffer)
-    deterministic: bool = False   # bitwise-reproducible CS-WLS kernel (wave-owned LDS replicas)
+    deterministic: bool | None = None  # bitwise-reproducible CS-WLS kernel (wave-owned LDS
+                                       # replicas); None = whenever supported (P <= 53 at Q = 10)
 
     def __post_init__(self):
         if self.eigen_shard not in ("dates", "sims"):

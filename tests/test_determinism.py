@@ -1,6 +1,7 @@
 """Run-twice bitwise determinism of the whole risk model.
 
-With ``RiskConfig(deterministic=True)`` every stage is order-fixed: the CS-WLS kernel's wave-owned
+With the default ``RiskConfig`` (``deterministic=None``: on whenever the CS-WLS kernel supports
+it, P <= 53 at Q = 10) every stage is order-fixed: the CS-WLS kernel's wave-owned
 LDS replicas, the blocked Newey-West / VRA scans (no atomics), per-(date, sim) Jacobi solves
 with Philox draws keyed by the sim index, and in-order bias sums.  Two runs must agree bit for
 bit, NaN positions included.
@@ -23,9 +24,9 @@ def _bitwise_equal(a, b):
         torch.equal(a.nan_to_num(0.0), b.nan_to_num(0.0))
 
 
-def _check(device, D, N, sims):
+def _check(device, D, N, sims, **kw):
     p = synthetic_panel(D, N, 31, 10, seed=11, device=device, missing_frac=0.02, empty_industries=1)
-    cfg = preset("reference", eigen_sims=sims, deterministic=True)
+    cfg = preset("reference", eigen_sims=sims, **kw)
     a = _outputs(RiskModel(p, cfg).run())
     b = _outputs(RiskModel(p, cfg).run())
     for k in a:
@@ -38,4 +39,21 @@ def test_risk_model_bitwise_deterministic_cpu():
 
 @pytest.mark.gpu
 def test_risk_model_bitwise_deterministic_gpu(cuda):
-    _check(cuda, 300, 2000, 20)
+    _check(cuda, 300, 2000, 20)                      # default config
+    _check(cuda, 300, 2000, 20, deterministic=True)
+
+
+@pytest.mark.gpu
+def test_xs_wls_default_is_bitwise_reproducible(cuda):
+    """The default CS-WLS call (no ``deterministic`` argument) is the deterministic kernel at the
+    reference shape, fp64 and fp32 storage: three runs agree bit for bit."""
+    from llm_driven_multi_factor_model_amd import _native
+    from llm_driven_multi_factor_model_amd.ops import cross_section as X
+    assert _native.lib().mfa_xs_det_supported(31, 10) == 1
+    assert _native.lib().mfa_xs_det_supported(128, 10) == 0
+    for dt in (torch.float64, torch.float32):
+        p = synthetic_panel(512, 3000, 31, 10, seed=5, device=cuda, missing_frac=0.02, dtype=dt)
+        runs = [X.xs_wls(p.styles, p.cap, p.ret, p.ind, 31) for _ in range(3)]
+        for r in runs[1:]:
+            for a, b in ((runs[0].f, r.f), (runs[0].resid, r.resid), (runs[0].r2, r.r2)):
+                assert _bitwise_equal(a, b)
