@@ -11,9 +11,9 @@
 //     v_m[k] = sum_l V[l,k]^2 D0[l] / Lambda[k] where (Lambda, V) = eigh(C_b); no U0 rotation
 //     of the K x T draws is ever formed;
 //   * the reference reseeds with m+1 for EVERY date (quirk Q8), so the draw covariances
-//     C_z,m = cov(z_m) are date-independent: they are computed ONCE per call with Philox
-//     normals and fp32 MFMA (v_mfma_f32_32x32x2_f32, exact-f32 products, fp64 cross-chunk
-//     accumulation) and C_b = S C_z,m S is formed on the fly per (date, sim);
+//     C_z,m = cov(z_m) are date-independent: they are computed ONCE per call from fp64 Philox
+//     normals (53-bit uniforms, fp64 Box-Muller) on the fp64 matrix cores
+//     (v_mfma_f64_16x16x4f64), and C_b = S C_z,m S is formed on the fly per (date, sim);
 //   * eigh (F0): one wave per matrix, pair-block tournament Jacobi (round-robin ordering,
 //     K/2 disjoint rotations per round), packed A + position-space V in LDS, fp64 throughout;
 //   * the (date, sim) bias statistic (252k 42x42 problems at the bench shape) is solved by
@@ -33,7 +33,7 @@ namespace {
 
 using namespace mfa;
 
-// ---------------- Philox4x32-10 + Box-Muller ----------------
+// ---------------- Philox4x32-10 ----------------
 struct U4 { unsigned x, y, z, w; };
 __device__ __forceinline__ U4 philox(U4 c, unsigned k0, unsigned k1) {
 #pragma unroll
@@ -48,20 +48,6 @@ __device__ __forceinline__ U4 philox(U4 c, unsigned k0, unsigned k1) {
   }
   return c;
 }
-__device__ __forceinline__ float u01(unsigned v) {  // (0, 1]
-  return ((float)(v >> 8) + 1.0f) * (1.0f / 16777216.0f);
-}
-// 4 standard normals for counter (a, b, c)
-__device__ __forceinline__ void normal4(unsigned a, unsigned b, unsigned c, unsigned long long seed,
-                                        float& n0, float& n1, float& n2, float& n3) {
-  const U4 r = philox(U4{a, b, c, 0x4D464131u}, (unsigned)seed, (unsigned)(seed >> 32));
-  const float r0 = sqrtf(-2.0f * __logf(u01(r.x))), r1 = sqrtf(-2.0f * __logf(u01(r.z)));
-  float s0, c0, s1, c1;
-  __sincosf(6.283185307179586f * u01(r.y), &s0, &c0);
-  __sincosf(6.283185307179586f * u01(r.w), &s1, &c1);
-  n0 = r0 * c0; n1 = r0 * s0; n2 = r1 * c1; n3 = r1 * s1;
-}
-
 // descending-order rank of lane k's eigenvalue (ties broken by index): perm[rank] = k
 __device__ void sort_desc(const double* A, int K, int lda, int* perm) {
   const int lane = threadIdx.x & 63;
@@ -125,53 +111,54 @@ __global__ __launch_bounds__(64) void eigh_kernel(const double* __restrict__ Ain
   if (lane == 0 && sweeps) sweeps[b] = ns;
 }
 
-// C_z,m = cov(z_m) (ddof 1) for z_m [T x K] standard normals, fp32 MFMA 32x32x2 per 2 rows.
-// Grid (M).  One wave: KP = 64 padded columns -> 2 x 2 output tiles of 32 x 32.
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+// C_z,m = cov(z_m) (ddof 1) for z_m [T x K] standard normals, all fp64 like the reference's
+// numpy draws (MFM.py:113-120 via utils.py:70-76): 53-bit uniforms from Philox4x32-10, fp64
+// Box-Muller, products on the fp64 matrix cores (v_mfma_f64_16x16x4f64) over 64-row LDS
+// blocks, fp64 column sums for the centring.  Grid (M), one wave per simulation; KP = 64
+// padded factors -> the 10 upper 16 x 16 tiles of the symmetric 64 x 64 sum of squares.
+typedef double f64x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ double u01_53(unsigned hi, unsigned lo) {  // (0, 1]
+  return ((double)(((unsigned long long)(hi >> 5) << 26) | (lo >> 6)) + 1.0) * (1.0 / 9007199254740992.0);
+}
 __global__ __launch_bounds__(64) void mc_cov_kernel(int K, int T, unsigned long long seed,
                                                     int m0, double* __restrict__ Cz) {
   // simulation m0 + blockIdx.x: the Philox stream depends only on (seed, global sim index), so
   // any partition of the sims over chunks / ranks draws exactly the single-run covariances
   const int m = m0 + blockIdx.x, lane = threadIdx.x;
-  __shared__ float Z[64][65];   // 64 time rows x 64 (padded) factors
+  __shared__ double Z[64][66];  // 64 time rows x 64 (padded) factors; +2 pad: conflict-free
   __shared__ double colsum[64];
-  const int col = lane & 31, half = lane >> 5;
-  double acc64[3][16];
+  const int r16 = lane & 15, k4 = lane >> 4;
+  constexpr int TI[10] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3};
+  constexpr int TJ[10] = {0, 1, 2, 3, 1, 2, 3, 2, 3, 3};
+  f64x4 acc[10];
 #pragma unroll
-  for (int t = 0; t < 3; ++t)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc64[t][r] = 0.0;
+  for (int t = 0; t < 10; ++t) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
   double cs = 0.0;  // column sum for factor `lane`
   for (int t0 = 0; t0 < T; t0 += 64) {
-    // draw a 64 x 64 block: row = time, col = factor (zero beyond K / T)
+    // draw a 64 x 64 block: row = time, col = factor (zero beyond K / T); one Philox call per
+    // (time, factor pair) -> two 53-bit uniforms -> one Box-Muller pair
+#pragma unroll 4
     for (int r = 0; r < 64; ++r) {
-      // lane handles 1 factor; 4 normals per philox call -> use lane/4 counters
       const int tq = t0 + r;
-      float n0, n1, n2, n3;
-      normal4((unsigned)m, (unsigned)tq, (unsigned)(lane >> 2), seed, n0, n1, n2, n3);
-      const int sub = lane & 3;
-      const float z = sub == 0 ? n0 : (sub == 1 ? n1 : (sub == 2 ? n2 : n3));
-      Z[r][lane] = (tq < T && lane < K) ? z : 0.0f;
+      const U4 u = philox(U4{(unsigned)m, (unsigned)tq, (unsigned)(lane >> 1), 0x4D464131u},
+                          (unsigned)seed, (unsigned)(seed >> 32));
+      const double rr = sqrt(-2.0 * log(u01_53(u.x, u.y)));
+      double sn, cn;
+      sincospi(2.0 * u01_53(u.z, u.w), &sn, &cn);
+      const double z = (lane & 1) ? rr * sn : rr * cn;
+      Z[r][lane] = (tq < T && lane < K) ? z : 0.0;
     }
     wsync();
-    f32x16 acc[3];
+#pragma unroll 2
+    for (int k = 0; k < 64; k += 4) {
+      double a[4];
 #pragma unroll
-    for (int t = 0; t < 3; ++t)
+      for (int i = 0; i < 4; ++i) a[i] = Z[k + k4][16 * i + r16];
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[t][r] = 0.0f;
-#pragma unroll 4
-    for (int k = 0; k < 64; k += 2) {
-      const float a0 = Z[k + half][col];        // tile row/col block 0
-      const float a1 = Z[k + half][32 + col];   // block 1
-      acc[0] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, a0, acc[0], 0, 0, 0);  // (0,0)
-      acc[1] = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, a1, acc[1], 0, 0, 0);  // (0,1)
-      acc[2] = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, a1, acc[2], 0, 0, 0);  // (1,1)
+      for (int t = 0; t < 10; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[TI[t]], a[TJ[t]], acc[t], 0, 0, 0);
     }
-#pragma unroll
-    for (int t = 0; t < 3; ++t)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc64[t][r] += (double)acc[t][r];
-    for (int r = 0; r < 64; ++r) cs += (double)Z[r][lane];
+    for (int r = 0; r < 64; ++r) cs += Z[r][lane];
     wsync();
   }
   colsum[lane] = cs;
@@ -179,14 +166,14 @@ __global__ __launch_bounds__(64) void mc_cov_kernel(int K, int T, unsigned long 
   double* C = Cz + (size_t)blockIdx.x * K * K;
   const double invT1 = 1.0 / (double)(T - 1), invT = 1.0 / (double)T;
 #pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    const int bi = t == 2 ? 1 : 0, bj = t == 0 ? 0 : 1;
+  for (int t = 0; t < 10; ++t) {
 #pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int i = bi * 32 + (r & 3) + 8 * (r >> 2) + 4 * half;
-      const int j = bj * 32 + col;
-      if (i < K && j < K) {
-        const double v = (acc64[t][r] - colsum[i] * colsum[j] * invT) * invT1;
+    for (int e = 0; e < 4; ++e) {
+      // 16x16x4 f64 output layout (tools/probes/mfma64_probe.hip): register e of lane l holds
+      // D[(l >> 4) + 4 e][l & 15]; a diagonal tile writes its upper triangle (both halves)
+      const int i = 16 * TI[t] + k4 + 4 * e, j = 16 * TJ[t] + r16;
+      if (i < K && j < K && (TI[t] != TJ[t] || i <= j)) {
+        const double v = (acc[t][e] - colsum[i] * colsum[j] * invT) * invT1;
         C[i * K + j] = v;
         C[j * K + i] = v;
       }

@@ -115,6 +115,36 @@ def test_hip_bias_solvers_agree_on_pipeline_like_inputs(cuda):
     torch.testing.assert_close(out["tridiag"], out["jacobi"], rtol=1e-10, atol=0)
 
 
+def _philox_normals(m, T, K, seed):
+    """numpy replica of mc_cov_kernel's draws: Philox4x32-10 keyed by (seed), counter
+    (sim, time, factor // 2, 0x4D464131), two 53-bit uniforms, fp64 Box-Muller pair."""
+    M32 = np.uint64(0xFFFFFFFF)
+    t, k = np.meshgrid(np.arange(T, dtype=np.uint64), np.arange(K, dtype=np.uint64) // np.uint64(2), indexing="ij")
+    x = np.full(t.shape, np.uint64(m)); y = t.copy(); z = k.copy(); w = np.full(t.shape, np.uint64(0x4D464131))
+    k0, k1 = np.uint64(seed & 0xFFFFFFFF), np.uint64((seed >> 32) & 0xFFFFFFFF)
+    for _ in range(10):
+        p0 = np.uint64(0xD2511F53) * x
+        p1 = np.uint64(0xCD9E8D57) * z
+        x, y, z, w = ((p1 >> np.uint64(32)) ^ y ^ k0) & M32, p1 & M32, ((p0 >> np.uint64(32)) ^ w ^ k1) & M32, p0 & M32
+        k0, k1 = (k0 + np.uint64(0x9E3779B9)) & M32, (k1 + np.uint64(0xBB67AE85)) & M32
+    u = lambda hi, lo: (((hi >> np.uint64(5)) << np.uint64(26) | (lo >> np.uint64(6))).astype(np.float64) + 1.0) / 2.0 ** 53
+    rr = np.sqrt(-2.0 * np.log(u(x, y)))
+    ang = 2.0 * np.pi * u(z, w)
+    odd = (np.arange(K) & 1)[None, :] == 1
+    return np.where(odd, rr * np.sin(ang), rr * np.cos(ang))
+
+
+@pytest.mark.gpu
+def test_hip_mc_cov_is_fp64_cov_of_its_philox_draws(cuda):
+    """Every entry of the fp64-MFMA draw covariance equals numpy's fp64 cov of the same Philox
+    normals (checks the matrix-core tile layout and the centring)."""
+    K, T, M, seed = 42, 300, 3, 7
+    Cz = eigen.mc_cov(M, K, T, seed=seed, device=cuda).cpu().numpy()
+    for m in range(M):
+        Z = _philox_normals(m, T, K, seed)
+        np.testing.assert_allclose(Cz[m], np.cov(Z.T), rtol=1e-11, atol=1e-13)
+
+
 @pytest.mark.gpu
 def test_hip_mc_cov_range_is_a_slice(cuda):
     full = eigen.mc_cov(12, 42, 300, seed=5, device=cuda)
