@@ -598,101 +598,166 @@ __device__ __forceinline__ double laguerre_toward(double x, double G, double H, 
   return f1 ? c1 : (f2 ? c2 : qnan());
 }
 
-template <int KP>
+// Single-wave workgroups: LDS executes one wave's DS instructions in issue order (they also
+// return in order), so a lane reading what another lane of the SAME wave wrote needs only the
+// compiler to keep program order -- no s_waitcnt / barrier round trip (wsync) per exchange.
+__device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
+
+// ABL: timing-only ablations (bias modes 41..47, KP = 44): 1 = no Laguerre iterations,
+// 2 = no eigenvector / back-transform, 4 = no tridiagonalisation, 8 = setup only (mode 48),
+// 16 = setup + tridiagonalisation only (mode 56); outputs meaningless
+template <int KP, int ABL = 0>
 __global__ __launch_bounds__(64) void mc_bias_tri_kernel(const double* __restrict__ D0, int K, int M,
                                                          const double* __restrict__ Cz,
                                                          const int* __restrict__ dvalid,
                                                          double* __restrict__ vout) {
   extern __shared__ double sm[];
-  constexpr int LD = KP + 1;  // odd row stride: row-per-lane ds_read_b64 is conflict-free
+  constexpr int LD = KP + 1;  // staging stride of C_z (odd: row-per-lane ds_read_b64 conflict-free)
+  constexpr int LU = KP;      // reflector rows (16-B aligned: broadcast ds_read_b128 pairs)
   const int d = blockIdx.x / M, m = blockIdx.x % M, lane = threadIdx.x;
   double* vo = vout + ((size_t)d * M + m) * K;
   if (!dvalid[d]) {
     for (int k = lane; k < K; k += 64) vo[k] = qnan();
     return;
   }
-  double* A = sm;                          // [K][LD]; row s <- u_s after step s
-  double* ub = A + (size_t)K * LD;         // [64] broadcast u
+  double* A = sm;                          // [K][LD]: row s <- reflector u_s (zero-padded)
+  double* ub = A + (((size_t)K * LD + 1) & ~(size_t)1);  // [64] broadcast u (16-B aligned)
   double* wb = ub + 64;                    // [64] broadcast w
   double2* tb = (double2*)(wb + 64);       // [64] {alpha_i, beta_{i-1}^2}
   double* be = (double*)(tb + 64);         // [64] beta_i
   double* ta = be + 64;                    // [64] tau_s
   double* dd = ta + 64;                    // [64] sqrt(D0)
   double* gs = dd + 64;                    // [64] diagonal of A, descending
+  double* rb = gs + 64;                    // [64] row broadcast
+  double* rb2 = rb + 64;                   // [64] second row broadcast (final 2 x 2)
   const double* d0 = D0 + (size_t)d * K;
   dd[lane] = lane < K ? sqrt(fmax(d0[lane], 0.0)) : 0.0;
-  wsync();
+  lds_order();
+  // C_z (shared by every date of sim m, L2-resident) staged coalesced into LDS, then lane i
+  // keeps row i of A = S C_z S in registers (static indices; padding columns zero)
   const double* c = Cz + (size_t)m * K * K;
-  for (int e = lane; e < K * KP; e += 64) {
-    const int i = e / KP, j = e - i * KP;
-    A[i * LD + j] = j < K ? dd[i] * c[i * K + j] * dd[j] : 0.0;
+  for (int e = lane; e < K * K; e += 64) {
+    const int i = e / K;
+    A[i * LD + (e - i * K)] = c[e];
   }
-  wsync();
+  lds_order();
+  double a[KP];
+  {
+    const int i = lane < K ? lane : 0;
+    const double di = lane < K ? dd[i] : 0.0;
+#pragma unroll
+    for (int j = 0; j < KP; ++j) a[j] = j < K ? di * A[i * LD + j] * dd[j] : 0.0;
+  }
   if (lane < K) {  // descending rank of the diagonal (ties by index): initial eigenvalue guesses
-    const double g = A[lane * LD + lane];
+    const double g = dd[lane] * A[lane * LD + lane] * dd[lane];
     int rank = 0;
     for (int j = 0; j < K; ++j) {
-      const double h = A[j * LD + j];
+      const double h = dd[j] * A[j * LD + j] * dd[j];
       rank += (h > g) || (h == g && j < lane);
     }
     gs[rank] = g;
   }
-  // ---- 1. Householder tridiagonalisation ----
-  for (int s = 0; s + 2 < K; ++s) {
-    const bool act = lane > s && lane < K;
-    const double x = act ? A[lane * LD + s] : 0.0;
-    const double x0 = readlane(x, s + 1);
-    const double sig = wave_total(lane > s + 1 && lane < K ? x * x : 0.0);
-    const double alpha = A[s * LD + s];
-    double u = 0.0, tau = 0.0, beta = x0;
-    if (sig != 0.0) {
-      const double nrm = sqrt(fma(x0, x0, sig));
-      beta = x0 >= 0.0 ? -nrm : nrm;
-      tau = 1.0 / (nrm * (nrm + fabs(x0)));
-      u = act ? (lane == s + 1 ? x0 - beta : x) : 0.0;
-    }
-    ub[lane] = u;
-    if (lane == 0) {
-      tb[s] = double2{alpha, s > 0 ? be[s - 1] * be[s - 1] : 0.0};
-      be[s] = beta;
-      ta[s] = tau;
-    }
-    wsync();
-    if (lane < KP) A[s * LD + lane] = u;  // u_s, zero outside (s, K)
-    if (tau != 0.0) {
-      double p0 = 0.0, p1 = 0.0;
-      if (act) {
-        const double* row = A + lane * LD;
-        int j = s + 1;
-        for (; j + 1 < K; j += 2) {
-          p0 = fma(row[j], ub[j], p0);
-          p1 = fma(row[j + 1], ub[j + 1], p1);
+  lds_order();  // the staging area becomes the reflector store (stride LU)
+  if constexpr ((ABL & 8) != 0) {  // timing: setup only
+    if (lane < K) vo[lane] = a[lane % KP] + gs[lane];
+    return;
+  }
+  // ---- 1. Householder tridiagonalisation (rows in registers) ----
+  // Step s reads row s (lane s's registers, published through LDS: x_i = A[s][i] = A[i][s]),
+  // forms u_s, p = tau A u, w = p - (tau/2)(u^T p) u and updates its own row
+  // a -= u_i w + w_i u with u, w broadcast as 16-B LDS pairs.  Columns j < 8 floor(s / 8) are
+  // finished, so each group of 8 steps runs a static column range [J0, KP): ~35 % fewer FMAs.
+  auto steps = [&](auto J0c, int s_begin) {
+    constexpr int J0 = decltype(J0c)::value;
+    for (int s = s_begin; s < s_begin + 8 && s + 2 < K; ++s) {
+      if (lane == s) {
+#pragma unroll
+        for (int j = J0; j < KP; j += 2) *(double2*)(rb + j) = double2{a[j], a[j + 1]};
+      }
+      lds_order();
+      const bool act = lane > s && lane < K;
+      const double x = act ? rb[lane] : 0.0;
+      const double x0 = rb[s + 1];
+      const double sig = wave_total(lane > s + 1 && lane < K ? x * x : 0.0);
+      const double alpha = rb[s];
+      double u = 0.0, tau = 0.0, beta = x0;
+      if (sig != 0.0) {
+        const double nrm = sqrt(fma(x0, x0, sig));
+        beta = x0 >= 0.0 ? -nrm : nrm;
+        tau = 1.0 / (nrm * (nrm + fabs(x0)));
+        u = act ? (lane == s + 1 ? x0 - beta : x) : 0.0;
+      }
+      ub[lane] = u;
+      if (lane < KP) A[s * LU + lane] = u;  // u_s, zero outside (s, K)
+      if (lane == 0) {
+        tb[s] = double2{alpha, s > 0 ? be[s - 1] * be[s - 1] : 0.0};
+        be[s] = beta;
+        ta[s] = tau;
+      }
+      lds_order();
+      if (tau != 0.0) {
+        double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+        for (int j = J0; j < KP; j += 2) {
+          const double2 uu = *(const double2*)(ub + j);
+          p0 = fma(a[j], uu.x, p0);
+          p1 = fma(a[j + 1], uu.y, p1);
         }
-        if (j < K) p0 = fma(row[j], ub[j], p0);
+        const double p = act ? tau * (p0 + p1) : 0.0;
+        const double kk = 0.5 * tau * wave_total(u * p);
+        const double w = p - kk * u;
+        wb[lane] = w;
+        lds_order();
+        if (act) {
+#pragma unroll
+          for (int j = J0; j < KP; j += 2) {
+            const double2 ww = *(const double2*)(wb + j), uu = *(const double2*)(ub + j);
+            a[j] -= fma(u, ww.x, w * uu.x);
+            a[j + 1] -= fma(u, ww.y, w * uu.y);
+          }
+        }
       }
-      const double p = tau * (p0 + p1);
-      const double kk = 0.5 * tau * wave_total(u * p);
-      const double w = p - kk * u;
-      wb[lane] = w;
-      wsync();
-      if (act) {
-        double* row = A + lane * LD;
-        for (int j = s + 1; j < K; ++j) row[j] -= fma(u, wb[j], w * ub[j]);
+      lds_order();
+    }
+  };
+  if constexpr ((ABL & 4) != 0) {
+    if (lane < K) {
+      tb[lane] = double2{gs[lane], 0.0};
+      be[lane] = 0.0;
+      ta[lane] = 0.0;
+    }
+    lds_order();
+  } else {
+    static_assert(KP % 8 == 0 || KP % 4 == 0, "KP: multiple of 4");
+    [&]<int... G>(std::integer_sequence<int, G...>) {
+      (steps(std::integral_constant<int, (8 * G < KP ? 8 * G : 0)>{}, 8 * G), ...);
+    }(std::make_integer_sequence<int, (KP + 7) / 8>{});
+    // final 2 x 2: alpha_{K-2} = A[K-2][K-2], beta_{K-2} = A[K-1][K-2], alpha_{K-1}
+    if (lane == K - 1) {
+#pragma unroll
+      for (int j = 0; j < KP; ++j) rb[j] = a[j];
+    }
+    if (lane == K - 2) {
+#pragma unroll
+      for (int j = 0; j < KP; ++j) rb2[j] = a[j];
+    }
+    lds_order();
+    if (lane == 0) {
+      if (K >= 2) {
+        const double b = rb[K - 2];
+        tb[K - 2] = double2{rb2[K - 2], K > 2 ? be[K - 3] * be[K - 3] : 0.0};
+        be[K - 2] = b;
+        tb[K - 1] = double2{rb[K - 1], b * b};
+      } else {
+        tb[0] = double2{rb[0], 0.0};
       }
     }
-    wsync();
+    lds_order();
   }
-  if (lane == 0) {
-    if (K >= 2) {
-      const double b = A[(K - 1) * LD + (K - 2)];
-      tb[K - 2] = double2{A[(K - 2) * LD + (K - 2)], K > 2 ? be[K - 3] * be[K - 3] : 0.0};
-      be[K - 2] = b;
-      tb[K - 1] = double2{A[(K - 1) * LD + (K - 1)], b * b};
-    } else {
-      tb[0] = double2{A[0], 0.0};
-    }
+  if constexpr ((ABL & 16) != 0) {  // timing: setup + tridiagonalisation only
+    if (lane < K) vo[lane] = tb[lane].x + be[lane];
+    return;
   }
-  wsync();
   // ---- 2. eigenvalue of rank `lane` (descending) ----
   double lo_l = 0.0, hi_l = 0.0, b2max = 0.0;
   if (lane < K) {
@@ -720,14 +785,14 @@ __global__ __launch_bounds__(64) void mc_bias_tri_kernel(const double* __restric
   int* cs = (int*)wb;
   xs[lane] = x;
   cs[lane] = cnt;
-  wsync();
+  lds_order();
   for (int l = 0; l < K; ++l) {
     const double xl = xs[l];
     const int cl = cs[l];
     if (cl <= jt) lo = fmax(lo, xl); else hi = fmin(hi, xl);
   }
-  double lam = 0.0;
-  if (lane < K) {
+  double lam = x;
+  if (lane < K && (ABL & 1) == 0) {
     int prev = -1;
     double sprev = __builtin_inf();
     for (int it = 0; it < 256; ++it) {
@@ -757,6 +822,10 @@ __global__ __launch_bounds__(64) void mc_bias_tri_kernel(const double* __restric
       if (cnt <= jt) lo = x; else hi = x;
     }
     lam = x;
+  }
+  if constexpr ((ABL & 2) != 0) {
+    if (lane < K) vo[lane] = lam;
+    return;
   }
   // ---- 3. eigenvector of T at lam: twisted factorisation ----
   double y[KP];
@@ -810,20 +879,35 @@ __global__ __launch_bounds__(64) void mc_bias_tri_kernel(const double* __restric
     for (int i = 0; i < KP; ++i) y[i] = 0.0;
   }
   // ---- 4. back-transform y = H_0 ... H_{K-3} z and the bias ratio ----
-  for (int s = K - 3; s >= 0; --s) {
-    const double tau = ta[s];
-    if (tau == 0.0) continue;
-    const double* us = A + s * LD;
-    double t0 = 0.0, t1 = 0.0;
+  // u_s is zero in columns <= s, so steps s in [8g, 8g + 8) run the static column range
+  // [8g, KP) (broadcast 16-B pairs of the reflector row)
+  auto back = [&](auto J0c, int s_hi) {
+    constexpr int J0 = decltype(J0c)::value;
+    for (int s = s_hi; s >= J0; --s) {
+      if (s + 2 >= K) continue;
+      const double tau = ta[s];
+      if (tau == 0.0) continue;
+      const double* us = A + s * LU;
+      double t0 = 0.0, t1 = 0.0;
 #pragma unroll
-    for (int j = 0; j < KP; j += 2) {
-      t0 = fma(us[j], y[j], t0);
-      if (j + 1 < KP) t1 = fma(us[j + 1], y[j + 1], t1);
+      for (int j = J0; j < KP; j += 2) {
+        const double2 uu = *(const double2*)(us + j);
+        t0 = fma(uu.x, y[j], t0);
+        t1 = fma(uu.y, y[j + 1], t1);
+      }
+      const double f = tau * (t0 + t1);
+#pragma unroll
+      for (int j = J0; j < KP; j += 2) {
+        const double2 uu = *(const double2*)(us + j);
+        y[j] = fma(-f, uu.x, y[j]);
+        y[j + 1] = fma(-f, uu.y, y[j + 1]);
+      }
     }
-    const double f = tau * (t0 + t1);
-#pragma unroll
-    for (int j = 0; j < KP; ++j) y[j] = fma(-f, us[j], y[j]);
-  }
+  };
+  [&]<int... G>(std::integer_sequence<int, G...>) {
+    constexpr int NG = (KP + 7) / 8;
+    (back(std::integral_constant<int, 8 * (NG - 1 - G)>{}, 8 * (NG - 1 - G) + 7), ...);
+  }(std::make_integer_sequence<int, (KP + 7) / 8>{});
   if (lane < K) {
     double v = 0.0;
 #pragma unroll
@@ -833,7 +917,7 @@ __global__ __launch_bounds__(64) void mc_bias_tri_kernel(const double* __restric
   }
 }
 
-size_t bias_tri_lds(int K, int KP) { return ((size_t)K * (KP + 1) + 7 * 64) * sizeof(double); }
+size_t bias_tri_lds(int K, int KP) { return ((size_t)K * (KP + 1) + 9 * 64 + 2) * sizeof(double); }
 
 // ---------------- pair-block Jacobi WITH eigenvectors (batched eigh of F0) ----------------
 // Same tournament-position scheme as jacobi_pairs, carrying packed A and the full eigenvector
@@ -1080,6 +1164,17 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
                        D0, K, M, Cz, dvalid, ws);                                          \
     return true;                                                                           \
   }
+  if (g_bias_mode > 40 && g_bias_mode < 60 && K <= 44) {  // timing-only ablations
+    const int abl = g_bias_mode - 40;
+#define MFA_TRI_ABL(A_)                                                                      \
+    if (abl == A_)                                                                         \
+      hipLaunchKernelGGL((mc_bias_tri_kernel<44, A_>), dim3(D * M), dim3(64), bias_tri_lds(K, 44), \
+                         s, D0, K, M, Cz, dvalid, ws);
+    MFA_TRI_ABL(1) MFA_TRI_ABL(2) MFA_TRI_ABL(3) MFA_TRI_ABL(4) MFA_TRI_ABL(5) MFA_TRI_ABL(6)
+    MFA_TRI_ABL(7) MFA_TRI_ABL(8) MFA_TRI_ABL(16)
+#undef MFA_TRI_ABL
+    return true;
+  }
   MFA_TRI(8)
   MFA_TRI(16)
   MFA_TRI(24)
@@ -1093,7 +1188,7 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
 
 #define MFA_BIAS_LAUNCH(NBV_)                                                                   \
   {                                                                                            \
-    if (g_bias_mode == 3)                                                                      \
+    if (g_bias_mode == 3 || (g_bias_mode > 40 && g_bias_mode < 60))                            \
       launch_bias_tri(D0, D, K, M, Cz, dvalid, ws, s);                                         \
     else if (g_bias_mode == 1)                                                                 \
       hipLaunchKernelGGL((mc_bias_split_kernel<NBV_, 1, double>), dim3(D * M), dim3(64),       \
