@@ -59,10 +59,14 @@ __device__ void stage_rows(const double* __restrict__ F, const double* __restric
 
 // Advance the (k,l) state over dates [t0, t1).  s[0] = S0 (group 0 only), s[1 + 2g + {0,1}] =
 // A_{i0+g}[k][l], A_{i0+g}[l][k].  EMIT: write (or add) V for dates in [t_lo, t_hi).
+// tab (EMIT only): per date u of the chunk, tab[(u - t0) * (1 + G)] = 1 / Z(n) and
+// tab[(u - t0) * (1 + G) + 1 + g] = l^(n - i0 - g): one pow per (date, lag) per block instead of
+// per (date, lag, k, l) thread
 template <bool EMIT>
 __device__ void nw_run_chunk(const double* Fs, const double* Ms, const double* M0, int t0, int t1,
                              int k, int l, const NwDims& dm, double (&s)[1 + 2 * G],
-                             double* __restrict__ V, int t_lo, int t_hi, bool add) {
+                             double* __restrict__ V, int t_lo, int t_hi, bool add,
+                             const double* tab = nullptr) {
   const int K = dm.K, q = dm.q;
   const int off = dm.i1 - 1;  // LDS row of date t0
   const double lam = dm.lam;
@@ -89,8 +93,8 @@ __device__ void nw_run_chunk(const double* Fs, const double* Ms, const double* M
         if (base) *vo = qnan();
         continue;
       }
-      const double Z = (1.0 - pow(lam, (double)n)) * il;
-      const double iz = 1.0 / Z;
+      const double* tu = tab + (u - t0) * (1 + G);
+      const double iz = tu[0];
       const double mk = Ms[r * K + k] * iz, ml = Ms[r * K + l] * iz;
       double v = base ? s[0] * iz - mk * ml : 0.0;
 #pragma unroll
@@ -98,7 +102,7 @@ __device__ void nw_run_chunk(const double* Fs, const double* Ms, const double* M
         const int i = dm.i0 + g;
         if (i >= dm.i1) break;
         const double ak = Ms[(r - i) * K + k], al = Ms[(r - i) * K + l];  // a_i = M[u-i]
-        const double dec = pow(lam, (double)(n - i));
+        const double dec = tu[1 + g];
         const double bk = Ms[r * K + k] - dec * M0[(i - 1) * K + k];     // b_i
         const double bl = Ms[r * K + l] - dec * M0[(i - 1) * K + l];
         const double zi = (1.0 - dec) * il;                               // z_i = Z(n - i)
@@ -172,7 +176,13 @@ __global__ __launch_bounds__(256) void nw_emit(const double* __restrict__ F,
   const int rows = t1 - t0 + dm.i1 - 1;
   double* Ms = Fs + (size_t)rows * dm.K;
   double* M0 = Ms + (size_t)rows * dm.K;
+  double* tab = M0 + (size_t)(dm.i1 - 1) * dm.K;  // [CH][1 + G]
   stage_rows(F, M, Fs, Ms, M0, t0, t1, dm, true);
+  for (int e = threadIdx.x; e < (t1 - t0) * (1 + G); e += blockDim.x) {
+    const int du = e / (1 + G), g = e % (1 + G);
+    const double n = (double)(t0 + du + 1);
+    tab[e] = g == 0 ? (1.0 - dm.lam) / (1.0 - pow(dm.lam, n)) : pow(dm.lam, n - (dm.i0 + g - 1));
+  }
   __syncthreads();
   const int KK = dm.K * dm.K;
   const int kk = blockIdx.y * blockDim.x + threadIdx.x;
@@ -184,7 +194,8 @@ __global__ __launch_bounds__(256) void nw_emit(const double* __restrict__ F,
 #pragma unroll
   for (int m = 0; m < 1 + 2 * G; ++m)
     if (m < ns) s[slot_of(dm, m)] = C[((size_t)c * ns + m) * KK + kk];
-  nw_run_chunk<true>(Fs, Ms, M0, t0, t1, kk / dm.K, kk % dm.K, dm, s, V, t_lo, t_hi, add != 0);
+  nw_run_chunk<true>(Fs, Ms, M0, t0, t1, kk / dm.K, kk % dm.K, dm, s, V, t_lo, t_hi, add != 0,
+                     tab);
 }
 
 // Decayed running sums of K series: M[t][k] = sum_{s<=t} l^(t-s) x[s][k] (no masking).
@@ -266,7 +277,7 @@ MFA_API size_t mfa_nw_workspace_bytes(int T, int K, int q) {
 
 // Largest lag count the kernels accept for K factors (LDS rows of one chunk).
 MFA_API int mfa_nw_max_lags(int K) {
-  const int rows = (int)(160 * 1024 / (3 * (size_t)K * sizeof(double)));
+  const int rows = (int)((160 * 1024 - CH * (1 + G) * sizeof(double)) / (3 * (size_t)K * sizeof(double)));
   return rows - CH;
 }
 
@@ -291,7 +302,7 @@ MFA_API int mfa_nw_series(const double* F, int T, int K, int q, double tau, int 
     NwDims dm{Tn, K, q, i0, i1, lam};
     const int ns = (i0 == 1 ? 1 : 0) + 2 * (i1 - i0);
     const size_t ldsA = (size_t)(CH + i1 - 1) * K * sizeof(double);
-    const size_t ldsC = (size_t)(2 * (CH + i1 - 1) + (i1 - 1)) * K * sizeof(double);
+    const size_t ldsC = ((size_t)(2 * (CH + i1 - 1) + (i1 - 1)) * K + CH * (1 + G)) * sizeof(double);
     hipLaunchKernelGGL(nw_chunk_sums, dim3(nch, (KK + 255) / 256), blk, ldsA, s, F, dm, C);
     hipLaunchKernelGGL(nw_carry_scan, dim3((ns * KK + 255) / 256), blk, 0, s, dm, nch, C);
     hipLaunchKernelGGL(nw_emit, dim3(nch - c_first, (KK + 255) / 256), blk, ldsC, s, F, M, dm, C,
