@@ -19,7 +19,7 @@ from llm_driven_multi_factor_model_amd.models.panel import synthetic_panel  # no
 
 def main():
     dev = torch.device("cuda:0")
-    D, N, P, Q = 2520, 5000, 31, 10
+    D, N, P, Q = int(os.environ.get("D", 2520)), 5000, 31, 10
     variants = [int(v) for v in os.environ.get("VARIANTS", "0,4,8,12,1,2").split(",")]
     f64 = os.environ.get("DTYPE", "fp32") == "fp64"
     dt = torch.float64 if f64 else torch.float32
@@ -31,7 +31,7 @@ def main():
     sts = torch.empty(D, Q + 2, dtype=torch.float64, device=dev)
     s = torch.empty(D, dtype=torch.int32, device=dev)
     ws = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
-    libs = {} if f64 else {"new": _native.lib()}
+    libs = {"new": _native.lib()}
     for item in os.environ.get("LIBS", "").split(","):  # name=path,...
         if item:
             name, path = item.split("=")
