@@ -644,8 +644,6 @@ __global__ __launch_bounds__(64) void mc_bias_tri_kernel(const double* __restric
   double* ta = be + 64;                    // [64] tau_s
   double* dd = ta + 64;                    // [64] sqrt(D0)
   double* gs = dd + 64;                    // [64] diagonal of A, descending
-  double* rb = gs + 64;                    // [64] row broadcast
-  double* rb2 = rb + 64;                   // [64] second row broadcast (final 2 x 2)
   const double* d0 = D0 + (size_t)d * K;
   dd[lane] = lane < K ? sqrt(fmax(d0[lane], 0.0)) : 0.0;
   lds_order();
@@ -679,23 +677,25 @@ __global__ __launch_bounds__(64) void mc_bias_tri_kernel(const double* __restric
     return;
   }
   // ---- 1. Householder tridiagonalisation (rows in registers) ----
-  // Step s reads row s (lane s's registers, published through LDS: x_i = A[s][i] = A[i][s]),
-  // forms u_s, p = tau A u, w = p - (tau/2)(u^T p) u and updates its own row
+  // Step s takes column s from each lane's own row (x_i = A[i][s], a static select within the
+  // step group), forms u_s, p = tau A u, w = p - (tau/2)(u^T p) u and updates its own row
   // a -= u_i w + w_i u with u, w broadcast as 16-B LDS pairs.  Columns j < 8 floor(s / 8) are
   // finished, so each group of 8 steps runs a static column range [J0, KP): ~35 % fewer FMAs.
   auto steps = [&](auto J0c, int s_begin) {
     constexpr int J0 = decltype(J0c)::value;
     for (int s = s_begin; s < s_begin + 8 && s + 2 < K; ++s) {
-      if (lane == s) {
+      // column s of the (symmetric) matrix is each lane's own a[s]: select it from the group's
+      // 8 static candidates (publishing row s through LDS cost ~22 single-lane 16-B stores per
+      // step, each paying the whole wave's VGPR transfer: the phase's LDS-array time)
+      double xs = a[J0];
 #pragma unroll
-        for (int j = J0; j < KP; j += 2) *(double2*)(rb + j) = double2{a[j], a[j + 1]};
-      }
-      lds_order();
+      for (int k = 1; k < 8; ++k)
+        if (J0 + k < KP) xs = s == J0 + k ? a[J0 + k] : xs;
       const bool act = lane > s && lane < K;
-      const double x = act ? rb[lane] : 0.0;
-      const double x0 = rb[s + 1];
+      const double x = act ? xs : 0.0;
+      const double x0 = readlane(xs, s + 1);
       const double sig = wave_total(lane > s + 1 && lane < K ? x * x : 0.0);
-      const double alpha = rb[s];
+      const double alpha = readlane(xs, s);
       double u = 0.0, tau = 0.0, beta = x0;
       if (sig != 0.0) {
         const double nrm = sqrt(fma(x0, x0, sig));
@@ -749,23 +749,22 @@ __global__ __launch_bounds__(64) void mc_bias_tri_kernel(const double* __restric
       (steps(std::integral_constant<int, (8 * G < KP ? 8 * G : 0)>{}, 8 * G), ...);
     }(std::make_integer_sequence<int, (KP + 7) / 8>{});
     // final 2 x 2: alpha_{K-2} = A[K-2][K-2], beta_{K-2} = A[K-1][K-2], alpha_{K-1}
-    if (lane == K - 1) {
+    double c2 = 0.0, c1 = 0.0;  // each lane's a[K-2], a[K-1] (dynamic index: static select)
 #pragma unroll
-      for (int j = 0; j < KP; ++j) rb[j] = a[j];
+    for (int j = 0; j < KP; ++j) {
+      c2 = j == K - 2 ? a[j] : c2;
+      c1 = j == K - 1 ? a[j] : c1;
     }
-    if (lane == K - 2) {
-#pragma unroll
-      for (int j = 0; j < KP; ++j) rb2[j] = a[j];
-    }
-    lds_order();
+    const double a22 = K >= 2 ? readlane(c2, K - 2) : readlane(c1, 0);
+    const double b21 = K >= 2 ? readlane(c2, K - 1) : 0.0;
+    const double a11 = readlane(c1, K - 1);
     if (lane == 0) {
       if (K >= 2) {
-        const double b = rb[K - 2];
-        tb[K - 2] = double2{rb2[K - 2], K > 2 ? be[K - 3] * be[K - 3] : 0.0};
-        be[K - 2] = b;
-        tb[K - 1] = double2{rb[K - 1], b * b};
+        tb[K - 2] = double2{a22, K > 2 ? be[K - 3] * be[K - 3] : 0.0};
+        be[K - 2] = b21;
+        tb[K - 1] = double2{a11, b21 * b21};
       } else {
-        tb[0] = double2{rb[0], 0.0};
+        tb[0] = double2{a11, 0.0};
       }
     }
     lds_order();
@@ -933,7 +932,7 @@ __global__ __launch_bounds__(64) void mc_bias_tri_kernel(const double* __restric
   }
 }
 
-size_t bias_tri_lds(int K, int KP) { return ((size_t)K * (KP + 1) + 9 * 64 + 2) * sizeof(double); }
+size_t bias_tri_lds(int K, int KP) { return ((size_t)K * (KP + 1) + 7 * 64 + 2) * sizeof(double); }
 
 // ---------------- pair-block Jacobi WITH eigenvectors (batched eigh of F0) ----------------
 // Same tournament-position scheme as jacobi_pairs, carrying packed A and the full eigenvector

@@ -9,10 +9,13 @@ timeout -s KILL 150 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES
 timeout -s KILL 150 rocprofv3 --kernel-trace --pmc SQ_LDS_IDX_ACTIVE SQ_WAVES SQ_WAIT_ANY SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_INST_CYCLES_SALU SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_MUL_F64 -d $O/b -o run --output-format csv -- python3 tools/eigen_tol.py > $O/b.log 2>&1 || exit 1
 python3 - <<'PY'
 import csv, glob, collections
+import os
 agg = collections.defaultdict(list)
+# the tool runs the Jacobi (mode 0) once as its baseline: count only the selected solver
+want = "mc_bias_tri" if os.environ.get("MODES", "0") != "0" else "mc_bias_kernel"
 for f in glob.glob("gpurun_out/pmc_bias/*/**/run_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
-        if "mc_bias" in r["Kernel_Name"]:
+        if want in r["Kernel_Name"]:
             agg[r["Counter_Name"]].append(float(r["Counter_Value"]))
 v = {c: sum(x) / len(x) for c, x in agg.items()}
 print({c: f"{x:.4g}" for c, x in sorted(v.items())})
