@@ -57,7 +57,7 @@ MFA_API int mfa_xs_wls_variant(const float* X, const float* cap, const float* re
     return (int)launch_q<10, vv, float>(X, cap, ret, ind, D, N, P, 0, 1e-14, f, e, r2, stats, \
                                         status, w, s);
     MFA_V(0) MFA_V(1) MFA_V(2) MFA_V(3) MFA_V(4) MFA_V(5) MFA_V(6) MFA_V(7) MFA_V(8)
-    MFA_V(12) MFA_V(15) MFA_V(16) MFA_V(20)
+    MFA_V(12) MFA_V(13) MFA_V(14) MFA_V(15) MFA_V(16) MFA_V(20)
 #undef MFA_V
   }
   return (int)hipErrorInvalidValue;

@@ -73,6 +73,32 @@ __device__ __forceinline__ unsigned lds_addr(const void* p) {
   return (unsigned)(uintptr_t)(__attribute__((address_space(3))) const void*)p;
 }
 
+// LDS reads of an LDS-DMA ring slot from inline asm: a compiler-visible LDS read while any
+// global_load_lds is in flight gets a vmcnt(0) from hipcc's waitcnt pass (it cannot tell the
+// slots apart), which drained the prefetched tiles before every tile's compute.  The caller
+// waits with lgkmcnt(0) before using the values.
+template <int OFF>
+__device__ __forceinline__ double lds_ld(unsigned a, double) {
+  double v;
+  asm volatile("ds_read_b64 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
+  return v;
+}
+template <int OFF>
+__device__ __forceinline__ float lds_ld(unsigned a, float) {
+  float v;
+  asm volatile("ds_read_b32 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
+  return v;
+}
+template <typename V>
+__device__ __forceinline__ void reg_fence(V& v) {
+  asm volatile("" : "+v"(v));
+}
+__device__ __forceinline__ int lds_ld_i16(unsigned a) {
+  int v;
+  asm volatile("ds_read_i16 %0, %1" : "=v"(v) : "v"(a));
+  return v;
+}
+
 // 4-byte async global -> LDS copy (one fp32 per lane: a 64-stock row per wave instruction).
 __device__ __forceinline__ void glds4(const void* src, void* wave_base) {
   __builtin_amdgcn_global_load_lds((gbl_void_t*)src, (lds_void_t*)wave_base, 4, 0, 0);
@@ -196,7 +222,7 @@ struct Ring {
 // LDS-DMA instructions one wave issues per tile (the vmcnt unit of the ring).
 template <int Q, typename T>
 __device__ __forceinline__ constexpr int dma_per_tile(bool has_ind) {
-  return (sizeof(T) == 4 ? Q + 2 : (Q + 3) / 2) + (has_ind ? 1 : 0);
+  return (sizeof(T) == 4 ? (Q + 5) / 4 : (Q + 3) / 2) + (has_ind ? 1 : 0);
 }
 
 // Moments of stocks [nb, ne) of date d (a chunk, or the whole date with nb = 0, ne = N; nb is
@@ -247,12 +273,16 @@ __device__ __forceinline__ void moments_body(
     char* slot = wring + (i % NB) * WSLOT;
     const int s0 = nb + (wid + i * nw) * kWT;
     if constexpr (sizeof(T) == 4) {
-      const bool in = s0 + lane < ne;
-      if (in) glds4(cd + s0 + lane, slot);
-      if (in) glds4(rd + s0 + lane, slot + ROWB);
+      // four 256-B fp32 rows per instruction: lane l -> row rr + l / 16, stocks 4 (l % 16) + 0..3
+      // (16-B pieces: a third of the 4-B DMA instructions for the same image)
+      const int sub = lane >> 4, s = s0 + 4 * (lane & 15);
+      const bool in = s < ne;  // ne is a multiple of 4: all four stocks of the piece exist
 #pragma unroll
-      for (int q = 0; q < Q; ++q)
-        if (in) glds4(Xd + (size_t)q * N + s0 + lane, slot + (2 + q) * ROWB);
+      for (int rr = 0; rr < Q + 2; rr += 4) {
+        const int row = rr + sub;
+        const T* src = row == 0 ? cd : (row == 1 ? rd : Xd + (size_t)(row - 2) * N);
+        if (in && row < Q + 2) glds16(src + s, slot + rr * ROWB);
+      }
     } else {
       // two 512-B fp64 rows per instruction: lanes 0-31 -> row rr, lanes 32-63 -> row rr + 1
       const int half = lane >> 5, s = s0 + 2 * (lane & 31);
@@ -268,18 +298,28 @@ __device__ __forceinline__ void moments_body(
   };
   for (int i = 0; i < NB - 1 && i < ntile; ++i) issue(i);
   for (int i = 0; i < ntile; ++i) {
-    const bool tail = (i + NB - 1 >= ntile);
-    wait_vmcnt(tail ? 0 : (NB - 2) * nrows);
-    __builtin_amdgcn_wave_barrier();
+    // The slot of tile i - 1 is free (its reads completed last iteration): refill it with tile
+    // i + NB - 1 BEFORE waiting for tile i, so NB - 1 tiles stay in flight across the wait.
     if (i + NB - 1 < ntile) issue(i + NB - 1);
+    const int ahead = ntile - 1 - i < NB - 1 ? ntile - 1 - i : NB - 1;  // tiles issued after i
+    wait_vmcnt(__builtin_amdgcn_readfirstlane(ahead * nrows));  // wave-uniform: scalar switch
+    __builtin_amdgcn_wave_barrier();
     const char* slot = wring + (i % NB) * WSLOT;
-    const T* bf = (const T*)slot;
     const int s = nb + (wid + i * nw) * kWT + lane;
-    const T cf = bf[lane], rf = bf[kWT + lane];
-    const int j = id ? (int)((const int16_t*)(slot + (Q + 2) * ROWB))[lane] : 0;
+    const unsigned la = lds_addr(slot) + lane * (unsigned)sizeof(T);
+    T cf = lds_ld<0>(la, T()), rf = lds_ld<ROWB>(la, T());
+    int j = id ? lds_ld_i16(lds_addr(slot) + (Q + 2) * ROWB + lane * 2) : 0;
     T xf[Q];
-#pragma unroll
-    for (int q = 0; q < Q; ++q) xf[q] = bf[(2 + q) * kWT + lane];
+    [&]<int... I>(std::integer_sequence<int, I...>) {
+      ((xf[I] = lds_ld<(2 + I) * ROWB>(la, T())), ...);
+    }(std::make_integer_sequence<int, Q>{});
+    // the wait, then empty asm that "redefines" every loaded register: no consumer of a value
+    // can be scheduled between its read and the wait
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("" : "+v"(cf), "+v"(rf), "+v"(j));
+    [&]<int... I>(std::integer_sequence<int, I...>) {
+      (reg_fence(xf[I]), ...);
+    }(std::make_integer_sequence<int, Q>{});
     bool ok = (s < ne) && (j >= 0) && (j < Pseg) && finite_v(cf) && (cf >= T(0)) && finite_v(rf);
 #pragma unroll
     for (int q = 0; q < Q; ++q) ok = ok && finite_v(xf[q]);
