@@ -239,7 +239,8 @@ template <int Q, int VAR, int R, typename T>
 __device__ __forceinline__ void moments_body(
     const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
     const int16_t* __restrict__ ind, int N, int Pseg, int d, char* ring, double* dyn,
-    double* md, int nb = 0, int ne = -1, double* __restrict__ gout = nullptr) {
+    double* md, int nb = 0, int ne = -1, double* __restrict__ gout = nullptr,
+    unsigned long long* __restrict__ okm = nullptr) {
   using L = Layout<Q, T>;
   if (ne < 0) ne = N;
   constexpr int NS = L::NS, NG = L::NG, NACC = L::NACC;
@@ -302,7 +303,10 @@ __device__ __forceinline__ void moments_body(
     // i + NB - 1 BEFORE waiting for tile i, so NB - 1 tiles stay in flight across the wait.
     if (i + NB - 1 < ntile) issue(i + NB - 1);
     const int ahead = ntile - 1 - i < NB - 1 ? ntile - 1 - i : NB - 1;  // tiles issued after i
-    wait_vmcnt(__builtin_amdgcn_readfirstlane(ahead * nrows));  // wave-uniform: scalar switch
+    // + the validity-mask stores issued after tile i's DMA (iterations i-NB+1 .. i-1): vmcnt
+    // counts stores too, in issue order
+    const int younger = ahead * nrows + (okm ? (i < NB - 1 ? i : NB - 1) : 0);
+    wait_vmcnt(__builtin_amdgcn_readfirstlane(younger));  // wave-uniform: scalar switch
     __builtin_amdgcn_wave_barrier();
     const char* slot = wring + (i % NB) * WSLOT;
     const int s = nb + (wid + i * nw) * kWT + lane;
@@ -323,6 +327,10 @@ __device__ __forceinline__ void moments_body(
     bool ok = (s < ne) && (j >= 0) && (j < Pseg) && finite_v(cf) && (cf >= T(0)) && finite_v(rf);
 #pragma unroll
     for (int q = 0; q < Q; ++q) ok = ok && finite_v(xf[q]);
+    if (okm) {  // validity bits of this 64-stock tile for the residual pass (no cap re-read)
+      const unsigned long long m = __ballot(ok);
+      if (lane == 0) okm[(s - lane) >> 6] = m;
+    }
     if (ok) {
       const double c = cf, r = rf, w = sqrt(c);
       double x[Q], wx[Q];
@@ -876,7 +884,7 @@ __device__ __forceinline__ void resid_body(
     const int16_t* __restrict__ ind, int d, int N, int P, const double* cf_s, bool bad,
     T* __restrict__ eout, double* __restrict__ r2out, double (*red)[5],
     const ResidPre<Q>& pre = ResidPre<Q>{}, double* __restrict__ sums_out = nullptr, int nb = 0,
-    int ne = -1) {
+    int ne = -1, const unsigned long long* __restrict__ okm = nullptr) {
   static_assert(!PRE || sizeof(T) == 4, "residual prefetch is the fp32 path");
   if (ne < 0) ne = N;
   constexpr int V = Stream<T>::VEC, U = UU > 0 ? UU : Stream<T>::U;
@@ -899,14 +907,19 @@ __device__ __forceinline__ void resid_body(
   // V consecutive stocks per thread (16-byte loads; N % 8 == 0 keeps rows aligned) and U
   // iterations' loads issued before any is consumed: the pass is latency-bound otherwise.
   const int step = blockDim.x * V;
-  auto one = [&](T c, T r, int j, const T (&xf)[Q]) -> T {
-    bool ok = (j >= 0) && (j < Pseg) && finite_v(c) && (c >= T(0)) && finite_v(r);
+  // vbit: the moments pass's validity bit of the stock (okm given) or -1 (check here)
+  auto one = [&](T c, T r, int j, const T (&xf)[Q], int vbit) -> T {
+    bool ok;
+    if (vbit >= 0) {
+      ok = vbit != 0;
+    } else {
+      ok = (j >= 0) && (j < Pseg) && finite_v(c) && (c >= T(0)) && finite_v(r);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) ok = ok && finite_v(xf[q]);
+    }
     double e = (double)r - cst;
 #pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      ok = ok && finite_v(xf[q]);
-      e = fma(-beta[q], (double)xf[q], e);
-    }
+    for (int q = 0; q < Q; ++q) e = fma(-beta[q], (double)xf[q], e);
     T eo = (T)qnan();
     if (ok) {
       if (P > 0) e -= fI[j];
@@ -919,10 +932,11 @@ __device__ __forceinline__ void resid_body(
     }
     return eo;
   };
-  auto compute = [&](const vec& cv, const vec& rv, const vec (&xv)[Q], ivec jv) -> vec {
+  // okw: validity bits of the V stocks (okm given: cv is not loaded) or -1
+  auto compute = [&](const vec& cv, const vec& rv, const vec (&xv)[Q], ivec jv, int okw) -> vec {
     T cs[V], rs[V], xs[Q][V], eo[V];
     int js[V];
-    RV::unpack(cv, cs);
+    if (okw < 0) RV::unpack(cv, cs);
     RV::unpack(rv, rs);
     RV::unpack(jv, js);
 #pragma unroll
@@ -932,9 +946,13 @@ __device__ __forceinline__ void resid_body(
       T xf[Q];
 #pragma unroll
       for (int q = 0; q < Q; ++q) xf[q] = xs[q][k];
-      eo[k] = one(cs[k], rs[k], js[k], xf);
+      eo[k] = one(okw < 0 ? cs[k] : T(0), rs[k], js[k], xf, okw < 0 ? -1 : ((okw >> k) & 1));
     }
     return RV::pack(eo);
+  };
+  const unsigned long long* okd = okm;  // this date's tile masks (or null)
+  auto okbits = [&](int n) -> int {
+    return okd ? (int)((okd[n >> 6] >> (n & 63)) & ((1u << V) - 1)) : -1;
   };
   int Nmain = ne;
   if constexpr (PRE) {
@@ -945,7 +963,7 @@ __device__ __forceinline__ void resid_body(
       for (int u = 0; u < kPreU; ++u) {
         const int n = nlo + (tid - 64) * 4 + u * 768;
         if (n < N) {
-          const vec eo = compute(pre.c4[u], pre.r4[u], pre.x4[u], pre.j4[u]);
+          const vec eo = compute(pre.c4[u], pre.r4[u], pre.x4[u], pre.j4[u], okbits(n));
           if (ed) *(vec*)(ed + n) = eo;
         }
       }
@@ -966,7 +984,7 @@ __device__ __forceinline__ void resid_body(
     for (int u = 0; u < U; ++u) {
       const int n = n0 + u * step;
       if (n < Nmain) {
-        cv[u] = *(const vec*)(cd + n);
+        if (!okd) cv[u] = *(const vec*)(cd + n);
         rv[u] = *(const vec*)(rd + n);
 #pragma unroll
         for (int q = 0; q < Q; ++q) xv[u][q] = *(const vec*)(Xd + (size_t)q * N + n);
@@ -981,7 +999,7 @@ __device__ __forceinline__ void resid_body(
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int n = n0 + u * step;
-      if (n < Nmain) eo[u] = compute(cv[u], rv[u], xv[u], jv[u]);
+      if (n < Nmain) eo[u] = compute(cv[u], rv[u], xv[u], jv[u], okbits(n));
     }
     if (b > 0) load_blk(b - 1);
     if (ed) {
@@ -1345,7 +1363,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
     const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
     const int16_t* __restrict__ ind, int N, int P, int Pseg, int pivot_mode, double tol,
     double* __restrict__ fout, T* __restrict__ eout, double* __restrict__ r2out,
-    double* __restrict__ stats, int* __restrict__ status, double* __restrict__ mom_out) {
+    double* __restrict__ stats, int* __restrict__ status, double* __restrict__ mom_out,
+    unsigned long long* __restrict__ okm) {
   __shared__ __attribute__((aligned(16))) char ring[fused_ring_bytes<Q, T>()];
   __shared__ double cf_s[Q + 1 + 128];
   __shared__ double red[4][5];
@@ -1353,13 +1372,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   extern __shared__ double dyn[];
   const int d = blockIdx.x;
   double* sm = (double*)ring;  // moments, then the solve's scratch (ring is idle by then)
+  // per-tile validity bits written by the moments pass and read by the residual pass of the same
+  // workgroup: the residual re-read skips the cap row (8 of 98 bytes per fp64 stock)
+  unsigned long long* okd = okm + (size_t)d * ((N + kWT - 1) / kWT);
   // every date's moments also go to mom_out (from registers, ~9.7 MB per 2520 dates): the
   // device pseudo-inverse pass reads them for near-singular dates.  (Exporting only flagged
   // dates from LDS after the solve cost ~30 us per 2520-date step: the extra LDS read of the
   // DMA ring region made hipcc add conservative vmcnt drains.)
   moments_body<Q, VAR & 35, R, T>(X, cap, ret, ind, N, Pseg, d, ring, dyn, sm, 0, -1,
                                   mom_out ? mom_out + (size_t)d * Layout<Q, T>::msize(Pseg)
-                                          : nullptr);
+                                          : nullptr,
+                                  okd);
   if constexpr ((VAR & 8) != 0) {  // timing-only ablation: no solve
     for (int i = threadIdx.x; i < Q + 1 + P; i += blockDim.x) cf_s[i] = sm[i] * 1e-30;
     if (threadIdx.x == 0) st_s = 0;
@@ -1374,7 +1397,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) voi
   __syncthreads();
   if constexpr ((VAR & 4) == 0)
     resid_body<Q, T, PRE>(X, cap, ret, ind, d, N, P, cf_s, (st_s & XS_BAD) != 0, eout, r2out,
-                          red, pre);
+                          red, pre, nullptr, 0, -1, okd);
   if constexpr ((VAR & 16) != 0) {  // timing-only: a second residual pass (cache-hit cost)
     __syncthreads();
     resid_body<Q, T>(X, cap, ret, ind, d, N, P, cf_s, (st_s & XS_BAD) != 0, eout, r2out, red);
@@ -1584,12 +1607,13 @@ inline int xs_chunks(int D, int N) {
   return (N + C - 1) / C;  // no empty trailing chunk after rounding C up to 64
 }
 
-// Workspace: partial moments [D][S][msize] | coef [D][Q+1+P] | partial R^2 sums [D][S][5].
+// Workspace: partial moments [D][S][msize] | coef [D][Q+1+P] | partial R^2 sums [D][S][5] |
+// per-tile validity bits [D][ceil(N/64)] u64 (fused kernel).
 inline size_t xs_workspace_bytes(int D, int N, int P, int Q) {
   const int Pseg = P > 0 ? P : 1;
   const size_t ms = (size_t)Q * (Q + 1) / 2 + 2 * Q + 4 + (size_t)Pseg * (Q + 3);
   const size_t S = (size_t)xs_chunks(D, N);
-  return (size_t)D * (S * ms + Q + 1 + P + S * 5) * sizeof(double);
+  return (size_t)D * (S * ms + Q + 1 + P + S * 5 + (N + kWT - 1) / kWT) * sizeof(double);
 }
 
 template <int Q, int VAR, typename T>
@@ -1609,6 +1633,7 @@ hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, 
   double* mom = ws;
   double* coef = ws + (size_t)D * S * MS;
   double* sums = coef + (size_t)D * (Q + 1 + P);
+  unsigned long long* okm = (unsigned long long*)(sums + (size_t)D * S * 5);
   const size_t seg8 = (size_t)L::seg_doubles(kRepMax, Pseg) * sizeof(double);
   const bool rep8 = seg8 <= kSegLdsBudget;
   const size_t lds1 = ((size_t)L::seg_doubles(rep8 ? kRepMax : 1, Pseg) + L::NACC) * sizeof(double);
@@ -1658,16 +1683,16 @@ hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, 
     }
   } else if (det) {  // bitwise-reproducible variant of the default path
     hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR | 32, PRE, T>), dim3(D), dim3(256), lds1,
-                       s, X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom);
+                       s, X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom, okm);
   } else if (mode == 0 && rep8) {
     hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR, PRE, T>), dim3(D), dim3(256), lds1, s, X,
-                       cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom);
+                       cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom, okm);
   } else if (rep8) {
     hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR, false, T>), dim3(D), dim3(256), lds1, s,
-                       X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom);
+                       X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom, okm);
   } else {
     hipLaunchKernelGGL((xs_fused_kernel<Q, 1, VAR, false, T>), dim3(D), dim3(256), lds1, s, X,
-                       cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom);
+                       cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom, okm);
   }
   if (refine) {
     const size_t lds3 = refine_lds_doubles<Q>(P) * sizeof(double);
