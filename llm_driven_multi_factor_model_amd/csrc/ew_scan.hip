@@ -35,12 +35,16 @@ struct NwDims {
   int T, K, q;      // series length, factors, total lag count (weights 1 - i/(q+1))
   int i0, i1;       // this launch's lag group [i0, i1), 1-based lags
   double lam;
+  int org;          // first date of the scanned range: chunk c = [org + c CH, org + (c+1) CH)
 };
 
 // LDS image of a chunk: F rows [t0 - i1 + 1, t1) and M rows [t0 - i1 + 1, t1), then M rows
-// [0, i1 - 1) (the b_i boundary terms).  Rows before date 0 are zero.
-__device__ void stage_rows(const double* __restrict__ F, const double* __restrict__ M, double* Fs,
-                           double* Ms, double* M0, int t0, int t1, const NwDims& dm, bool want_m) {
+// [0, i1 - 1) (the b_i boundary terms, from Mg: the GLOBAL series' first rows).  Rows before
+// date 0 are zero.  F and M are indexed by global date (a shard passes base pointers offset so
+// that only its rows [org - q, T) are ever read).
+__device__ void stage_rows(const double* __restrict__ F, const double* __restrict__ M,
+                           const double* __restrict__ Mg, double* Fs, double* Ms, double* M0,
+                           int t0, int t1, const NwDims& dm, bool want_m) {
   const int K = dm.K;
   const int lo = t0 - (dm.i1 - 1);
   const int rows = t1 - lo;
@@ -53,7 +57,7 @@ __device__ void stage_rows(const double* __restrict__ F, const double* __restric
   if (want_m)
     for (int e = threadIdx.x; e < (dm.i1 - 1) * K; e += blockDim.x) {
       const int t = e / K;
-      M0[e] = t < dm.T ? M[e] : 0.0;
+      M0[e] = t < dm.T ? Mg[e] : 0.0;
     }
 }
 
@@ -130,8 +134,8 @@ __global__ __launch_bounds__(256) void nw_chunk_sums(const double* __restrict__ 
                                                      double* __restrict__ C) {
   extern __shared__ double Fs[];
   const int c = blockIdx.x;
-  const int t0 = c * CH, t1 = min(dm.T, t0 + CH);
-  stage_rows(F, nullptr, Fs, nullptr, nullptr, t0, t1, dm, false);
+  const int t0 = dm.org + c * CH, t1 = min(dm.T, t0 + CH);
+  stage_rows(F, nullptr, nullptr, Fs, nullptr, nullptr, t0, t1, dm, false);
   __syncthreads();
   const int KK = dm.K * dm.K;
   const int kk = blockIdx.y * blockDim.x + threadIdx.x;
@@ -147,37 +151,44 @@ __global__ __launch_bounds__(256) void nw_chunk_sums(const double* __restrict__ 
     if (m < ns) C[((size_t)c * ns + m) * KK + kk] = s[slot_of(dm, m)];
 }
 
-// pass B: in-place exclusive scan over chunks: C[c] <- sum_{c'<c} l^(t0_c - t1_c') C[c']
-__global__ __launch_bounds__(256) void nw_carry_scan(NwDims dm, int nchunks, double* __restrict__ C) {
+// pass B: in-place exclusive scan over chunks: C[c] <- Cin + sum_{c'<c} l^(t0_c - t1_c') C[c']
+// (Cin: the state at date org - 1 carried in from earlier shards, decayed along; null = 0).
+// Ctot (optional): the inclusive total at date T - 1 (a shard's contribution to later shards).
+__global__ __launch_bounds__(256) void nw_carry_scan(NwDims dm, int nchunks, double* __restrict__ C,
+                                                     const double* __restrict__ Cin,
+                                                     double* __restrict__ Ctot) {
   const int KK = dm.K * dm.K;
   const int ns = nstate(dm);
   const int e = blockIdx.x * blockDim.x + threadIdx.x;  // (m, kk)
   if (e >= ns * KK) return;
   const double dch = pow(dm.lam, (double)CH);
-  double carry = 0.0;
+  double carry = Cin ? Cin[e] : 0.0;
   for (int c = 0; c < nchunks; ++c) {
-    const int len = min(dm.T, (c + 1) * CH) - c * CH;
+    const int t0 = dm.org + c * CH;
+    const int len = min(dm.T, t0 + CH) - t0;
     double* p = C + (size_t)c * ns * KK + e;
     const double loc = *p;
     *p = carry;
     carry = fma(len == CH ? dch : pow(dm.lam, (double)len), carry, loc);
   }
+  if (Ctot) Ctot[e] = carry;
 }
 
 // pass C: outputs for chunks overlapping [t_lo, t_hi)
 __global__ __launch_bounds__(256) void nw_emit(const double* __restrict__ F,
-                                               const double* __restrict__ M, NwDims dm,
+                                               const double* __restrict__ M,
+                                               const double* __restrict__ Mg, NwDims dm,
                                                const double* __restrict__ C, int c_first,
                                                int t_lo, int t_hi, double* __restrict__ V,
                                                int add) {
   extern __shared__ double Fs[];
   const int c = c_first + blockIdx.x;
-  const int t0 = c * CH, t1 = min(dm.T, t0 + CH);
+  const int t0 = dm.org + c * CH, t1 = min(dm.T, t0 + CH);
   const int rows = t1 - t0 + dm.i1 - 1;
   double* Ms = Fs + (size_t)rows * dm.K;
   double* M0 = Ms + (size_t)rows * dm.K;
   double* tab = M0 + (size_t)(dm.i1 - 1) * dm.K;  // [CH][1 + G]
-  stage_rows(F, M, Fs, Ms, M0, t0, t1, dm, true);
+  stage_rows(F, M, Mg, Fs, Ms, M0, t0, t1, dm, true);
   for (int e = threadIdx.x; e < (t1 - t0) * (1 + G); e += blockDim.x) {
     const int du = e / (1 + G), g = e % (1 + G);
     const double n = (double)(t0 + du + 1);
@@ -198,13 +209,16 @@ __global__ __launch_bounds__(256) void nw_emit(const double* __restrict__ F,
                      tab);
 }
 
-// Decayed running sums of K series: M[t][k] = sum_{s<=t} l^(t-s) x[s][k] (no masking).
+// Decayed running sums of K series over rows [t_s, T): M[t][k] = l^(t-t_s+1) init[k] +
+// sum_{t_s<=s<=t} l^(t-s) x[s][k] (no masking; init null = 0; x, M indexed by global row).
 // One wave per column; lane-chunked two-level scan.
-__global__ __launch_bounds__(64) void ew_cumsum_cols(const double* __restrict__ x, int T, int K,
-                                                    double lam, double* __restrict__ M) {
+__global__ __launch_bounds__(64) void ew_cumsum_cols(const double* __restrict__ x, int t_s, int T,
+                                                    int K, double lam,
+                                                    const double* __restrict__ init,
+                                                    double* __restrict__ M) {
   const int k = blockIdx.x, lane = threadIdx.x;
-  const int per = (T + 63) / 64;
-  const int a = min(T, lane * per), b = min(T, a + per);
+  const int per = (T - t_s + 63) / 64;
+  const int a = min(T, t_s + lane * per), b = min(T, a + per);
   double num = 0.0;
   for (int t = a; t < b; ++t) num = fma(lam, num, x[(size_t)t * K + k]);
   double cn = num, dk = pow(lam, (double)(b - a));
@@ -217,16 +231,29 @@ __global__ __launch_bounds__(64) void ew_cumsum_cols(const double* __restrict__ 
   }
   double en = __shfl_up(cn, 1, 64);
   if (lane == 0) en = 0.0;
+  if (init) en = fma(pow(lam, (double)(a - t_s)), init[k], en);  // carried-in state, decayed
   for (int t = a; t < b; ++t) {
     en = fma(lam, en, x[(size_t)t * K + k]);
     M[(size_t)t * K + k] = en;
   }
 }
 
+// Mtot[k] = sum_{t_s<=s<T} l^(T-1-s) x[s][k]: a shard's own contribution to M[T - 1].
+__global__ __launch_bounds__(64) void ew_cumsum_tail(const double* __restrict__ x, int t_s, int T,
+                                                    int K, double lam, double* __restrict__ Mtot) {
+  const int k = blockIdx.x, lane = threadIdx.x;
+  double acc = 0.0;
+  for (int t = t_s + lane; t < T; t += 64) acc = fma(pow(lam, (double)(T - 1 - t)), x[(size_t)t * K + k], acc);
+  for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+  if (lane == 0) Mtot[k] = acc;
+}
+
 // Decayed prefix mean with validity: out[t] = sum_{s<=t, ok} l^(t-s) x_s / sum_{s<=t, ok} l^(t-s)
 // (VRA factor-volatility multiplier, MFM.py:149-160).  One wave; chunked two-level scan.
 __global__ __launch_bounds__(64) void ew_prefix_mean(const double* __restrict__ x, int T, double lam,
-                                                     double* __restrict__ out) {
+                                                     double* __restrict__ out,
+                                                     const double* __restrict__ init = nullptr,
+                                                     double* __restrict__ tot = nullptr) {
   const int lane = threadIdx.x;
   const int per = (T + 63) / 64;
   const int a = min(T, lane * per), b = min(T, a + per);
@@ -248,16 +275,23 @@ __global__ __launch_bounds__(64) void ew_prefix_mean(const double* __restrict__ 
       dk = dk * pk;
     }
   }
+  if (tot && lane == 63) { tot[0] = cn; tot[1] = cd; }  // own totals at date T - 1
   double en = __shfl_up(cn, 1, 64), ed = __shfl_up(cd, 1, 64);
   if (lane == 0) { en = 0.0; ed = 0.0; }
-  num = en; den = ed;
-  for (int t = a; t < b; ++t) {
-    const double v = x[t];
-    const bool ok = __builtin_isfinite(v);
-    num = fma(lam, num, ok ? v : 0.0);
-    den = fma(lam, den, ok ? 1.0 : 0.0);
-    out[t] = den > 0.0 ? num / den : qnan();
+  if (init) {  // (num, den) carried in at date -1 of this shard, decayed to a - 1
+    const double da = pow(lam, (double)a);
+    en = fma(da, init[0], en);
+    ed = fma(da, init[1], ed);
   }
+  num = en; den = ed;
+  if (out)
+    for (int t = a; t < b; ++t) {
+      const double v = x[t];
+      const bool ok = __builtin_isfinite(v);
+      num = fma(lam, num, ok ? v : 0.0);
+      den = fma(lam, den, ok ? 1.0 : 0.0);
+      out[t] = den > 0.0 ? num / den : qnan();
+    }
 }
 
 size_t nw_carry_bytes(int T, int K, int q) {
@@ -293,21 +327,112 @@ MFA_API int mfa_nw_series(const double* F, int T, int K, int q, double tau, int 
   const int KK = K * K;
   double* C = (double*)ws;
   double* M = (double*)((char*)ws + nw_carry_bytes(Tn, K, q));
-  hipLaunchKernelGGL(ew_cumsum_cols, dim3(K), dim3(64), 0, s, F, Tn, K, lam, M);
+  hipLaunchKernelGGL(ew_cumsum_cols, dim3(K), dim3(64), 0, s, F, 0, Tn, K, lam,
+                     (const double*)nullptr, M);
   const int c_first = t_lo / CH;
   dim3 blk(256);
   // lag groups [i0, i1): group 0 also carries S0 and writes V; later groups add their lags
   for (int i0 = 1, grp = 0; grp == 0 || i0 <= q; i0 += G, ++grp) {
     const int i1 = std::min(q + 1, i0 + G);
-    NwDims dm{Tn, K, q, i0, i1, lam};
+    NwDims dm{Tn, K, q, i0, i1, lam, 0};
     const int ns = (i0 == 1 ? 1 : 0) + 2 * (i1 - i0);
     const size_t ldsA = (size_t)(CH + i1 - 1) * K * sizeof(double);
     const size_t ldsC = ((size_t)(2 * (CH + i1 - 1) + (i1 - 1)) * K + CH * (1 + G)) * sizeof(double);
     hipLaunchKernelGGL(nw_chunk_sums, dim3(nch, (KK + 255) / 256), blk, ldsA, s, F, dm, C);
-    hipLaunchKernelGGL(nw_carry_scan, dim3((ns * KK + 255) / 256), blk, 0, s, dm, nch, C);
-    hipLaunchKernelGGL(nw_emit, dim3(nch - c_first, (KK + 255) / 256), blk, ldsC, s, F, M, dm, C,
-                       c_first, t_lo, t_hi, V, grp > 0 ? 1 : 0);
+    hipLaunchKernelGGL(nw_carry_scan, dim3((ns * KK + 255) / 256), blk, 0, s, dm, nch, C,
+                       (const double*)nullptr, (double*)nullptr);
+    hipLaunchKernelGGL(nw_emit, dim3(nch - c_first, (KK + 255) / 256), blk, ldsC, s, F, M, M, dm,
+                       C, c_first, t_lo, t_hi, V, grp > 0 ? 1 : 0);
   }
+  return (int)hipGetLastError();
+}
+
+// Carried state of the sharded scan: for every lag group g (groups of G lags, [1 + 8g, ...)),
+// nstate(g) x K x K moments (S0 for group 0, then A_i[k][l], A_i[l][k] per lag), concatenated.
+MFA_API size_t mfa_nw_state_doubles(int K, int q) {
+  size_t n = 0;
+  for (int i0 = 1, grp = 0; grp == 0 || i0 <= q; i0 += G, ++grp) {
+    const int i1 = std::min(q + 1, i0 + G);
+    n += (size_t)((i0 == 1 ? 1 : 0) + 2 * (i1 - i0)) * K * K;
+  }
+  return n;
+}
+
+// Shard workspace: chunk carries of [T0, T1) + the M series rows [T0 - q, T1).
+MFA_API size_t mfa_nw_shard_workspace_bytes(int T0, int T1, int K, int q) {
+  const int h = q > 1 ? q : 1;
+  const int lo = T0 - h > 0 ? T0 - h : 0;
+  return nw_carry_bytes(T1 - T0, K, q) + (size_t)(T1 - lo) * K * sizeof(double);
+}
+
+// One date shard [T0, T1) of the expanding-window Newey-West series (SURVEY 2.5 time-axis
+// scan across ranks).  With h = max(q, 1): Fsh = rows [max(0, T0 - h), T1) of F (the halo +
+// the shard); Mh: the GLOBAL decayed sums M[t] = sum_{s<=t} l^(t-s) f_s for rows [max(0, T0 - h), T0)
+// (null when T0 == 0); Mg: global M rows [0, min(q, T1)) (b_i boundary terms).
+// Cin: carried state at date T0 - 1 (mfa_nw_state_doubles layout; null = zero, i.e. T0 == 0).
+// Outputs (each optional): V [T1 - T0][K][K] for the shard's dates; Ctot = the shard's own
+// contribution to the state at date T1 - 1 (chunk sums of [T0, T1) including the halo lag
+// products, NOT including Cin); Mtot = sum_{T0<=s<T1} l^(T1-1-s) f_s.
+MFA_API int mfa_nw_series_shard(const double* Fsh, const double* Mh, const double* Mg, int T0,
+                                int T1, int K, int q, double tau, const double* Cin, double* V,
+                                double* Ctot, double* Mtot, void* ws, void* stream) {
+  if (T1 <= T0) return 0;
+  if (q < 0 || K <= 0 || T0 < 0 || q > mfa_nw_max_lags(K)) return (int)hipErrorInvalidValue;
+  if (V && T0 > 0 && Mh == nullptr) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  const double lam = pow(0.5, 1.0 / tau);
+  const int h = q > 1 ? q : 1;
+  const int lo = T0 - h > 0 ? T0 - h : 0;
+  const int nch = (T1 - T0 - 1) / CH + 1;
+  const int KK = K * K;
+  const double* Fb = Fsh - (size_t)lo * K;  // indexed by global date (rows >= lo only)
+  double* C = (double*)ws;
+  double* Mw = (double*)((char*)ws + nw_carry_bytes(T1 - T0, K, q));
+  double* Mb = Mw - (size_t)lo * K;         // indexed by global date
+  if (V) {
+    if (T0 > lo) {
+      const hipError_t e = hipMemcpyAsync(Mw, Mh, (size_t)(T0 - lo) * K * sizeof(double),
+                                          hipMemcpyDeviceToDevice, s);
+      if (e != hipSuccess) return (int)e;
+    }
+    // own rows of M: carried M[T0 - 1] (the halo's last row) decayed along
+    hipLaunchKernelGGL(ew_cumsum_cols, dim3(K), dim3(64), 0, s, Fb, T0, T1, K, lam,
+                       T0 > 0 ? Mb + (size_t)(T0 - 1) * K : (const double*)nullptr, Mb);
+  }
+  if (Mtot)  // own contribution only: rescan with no carried state
+    hipLaunchKernelGGL(ew_cumsum_tail, dim3(K), dim3(64), 0, s, Fb, T0, T1, K, lam, Mtot);
+  dim3 blk(256);
+  size_t off = 0;
+  for (int i0 = 1, grp = 0; grp == 0 || i0 <= q; i0 += G, ++grp) {
+    const int i1 = std::min(q + 1, i0 + G);
+    NwDims dm{T1, K, q, i0, i1, lam, T0};
+    const int ns = (i0 == 1 ? 1 : 0) + 2 * (i1 - i0);
+    const size_t ldsA = (size_t)(CH + i1 - 1) * K * sizeof(double);
+    const size_t ldsC = ((size_t)(2 * (CH + i1 - 1) + (i1 - 1)) * K + CH * (1 + G)) * sizeof(double);
+    hipLaunchKernelGGL(nw_chunk_sums, dim3(nch, (KK + 255) / 256), blk, ldsA, s, Fb, dm, C);
+    if (Ctot)  // own contribution: scan from zero, keep the total, then rescan from Cin below
+      hipLaunchKernelGGL(nw_carry_scan, dim3((ns * KK + 255) / 256), blk, 0, s, dm, nch, C,
+                         (const double*)nullptr, Ctot + off);
+    if (V) {
+      if (Ctot)
+        hipLaunchKernelGGL(nw_chunk_sums, dim3(nch, (KK + 255) / 256), blk, ldsA, s, Fb, dm, C);
+      hipLaunchKernelGGL(nw_carry_scan, dim3((ns * KK + 255) / 256), blk, 0, s, dm, nch, C,
+                         Cin ? Cin + off : (const double*)nullptr, (double*)nullptr);
+      hipLaunchKernelGGL(nw_emit, dim3(nch, (KK + 255) / 256), blk, ldsC, s, Fb, Mb, Mg, dm, C, 0,
+                         T0, T1, V, grp > 0 ? 1 : 0);
+    }
+    off += (size_t)ns * KK;
+  }
+  return (int)hipGetLastError();
+}
+
+// Shard of the decayed prefix mean: init = (num, den) carried in at date -1 (null = 0), out =
+// the shard's prefix means (nullable), tot = its own (num, den) totals at date T - 1 (nullable).
+MFA_API int mfa_ew_prefix_mean_shard(const double* x, int T, double tau, const double* init,
+                                     double* out, double* tot, void* stream) {
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(ew_prefix_mean, dim3(1), dim3(64), 0, (hipStream_t)stream, x, T,
+                     pow(0.5, 1.0 / tau), out, init, tot);
   return (int)hipGetLastError();
 }
 

@@ -60,7 +60,7 @@ class RiskModel:
         self.factor_ret_global = None
         self.nw_cov = self.eigen_cov = self.vra_cov = self.vra_lambda = None
         self.eigen_bias = None
-        self.B2_global = None
+        self.B2_global = self.B2 = None
         self.nw_params = None     # (q, tau) of the last newey_west() call
 
     def _stage(self, name: str):
@@ -88,24 +88,41 @@ class RiskModel:
                             want_resid=want_resid, deterministic=self.cfg.deterministic)
         self.factor_ret, self.specific_ret, self.r2 = res.f, res.resid, res.r2
         self.status, self.stats = res.status, res.stats
-        with self._stage("allgather_f"):
-            F = pdist.all_gather_rows(self.factor_ret, self.ctx, self.sizes)
-            if self.history is not None:
-                F = torch.cat([self.history["factor_ret"].to(F.device, F.dtype), F])
-            self.factor_ret_global = F
+        self.factor_ret_global = None
+        if self.cfg.time_scan == "gather":
+            self._gather_f()
         return self.factor_ret, self.specific_ret, self.r2
+
+    def _gather_f(self) -> torch.Tensor:
+        """[T, K] factor returns of every date (history first).  Collective."""
+        if self.factor_ret_global is None:
+            with self._stage("allgather_f"):
+                F = pdist.all_gather_rows(self.factor_ret, self.ctx, self.sizes)
+                if self.history is not None:
+                    F = torch.cat([self.history["factor_ret"].to(F.device, F.dtype), F])
+                self.factor_ret_global = F
+        return self.factor_ret_global
+
+    def _hist(self, key: str):
+        if self.history is None:
+            return None
+        return self.history[key].to(self.device, torch.float64)
 
     # --------------------------------------------------------------- stage 2: Newey-West
     def newey_west(self, q: int | None = None, tau: float | None = None):
-        if self.factor_ret_global is None:
+        if self.factor_ret is None:
             raise RuntimeError("please run regress() to get factor returns first")
         q = self.cfg.nw_lags if q is None else q
         tau = self.cfg.nw_half_life if tau is None else tau
         lo = self.t_lo
         self.nw_params = (int(q), float(tau))
         with self._stage("newey_west"):
-            self.nw_cov = ew_scan.newey_west_series(self.factor_ret_global, q, tau, lo,
-                                                    lo + self.panel.D)
+            if self.cfg.time_scan == "carry":  # own dates only, block states carried across ranks
+                self.nw_cov = ew_scan.newey_west_series_sharded(
+                    self.factor_ret, q, tau, self.ctx, self.sizes, history=self._hist("factor_ret"))
+            else:
+                self.nw_cov = ew_scan.newey_west_series(self._gather_f(), q, tau, lo,
+                                                        lo + self.panel.D)
         return self.nw_cov
 
     # --------------------------------------------------------------- stage 3: eigen adjustment
@@ -125,7 +142,7 @@ class RiskModel:
                 # all_reduce of the [T, K] bias sums (C5) completes the mean over M.
                 lo_new = self.T_hist
                 q_nw, tau_nw = self.nw_params  # the (q, tau) newey_west() actually used
-                nw_all = ew_scan.newey_west_series(self.factor_ret_global, q_nw, tau_nw, lo_new,
+                nw_all = ew_scan.newey_west_series(self._gather_f(), q_nw, tau_nw, lo_new,
                                                    self.T)
                 Fh, vb = eigen.eigen_risk_adjust_sharded(
                     nw_all, M=M, scale_coef=scale_coef, T_sim=T_sim, seed=seed,
@@ -162,16 +179,28 @@ class RiskModel:
                 lo = self.panel.date_offset
                 var = prev[lo:lo + self.panel.D]
             B2 = (self.factor_ret ** 2 / var).mean(-1)                    # NaN where ER empty
-            B2_all = pdist.all_gather_rows(B2, self.ctx, self.sizes)
-            if self.history is not None:
-                B2_all = torch.cat([self.history["B2"].to(B2_all.device, B2_all.dtype), B2_all])
-            self.B2_global = B2_all
-            lam2 = ew_scan.ew_prefix_mean(B2_all, tau)[self.t_lo:self.t_lo + self.panel.D]
+            self.B2 = B2
+            self.B2_global = None
+            if self.cfg.time_scan == "carry":
+                lam2 = ew_scan.ew_prefix_mean_sharded(B2, tau, self.ctx, self.sizes,
+                                                      history=self._hist("B2"))
+            else:
+                lam2 = ew_scan.ew_prefix_mean(self._gather_b2(), tau)[
+                    self.t_lo:self.t_lo + self.panel.D]
             # no valid date yet: the reference's sum over an empty selection gives lambda = 0
             lam2 = torch.nan_to_num(lam2, nan=0.0)
             self.vra_lambda = torch.sqrt(lam2)
             self.vra_cov = self.eigen_cov * lam2[:, None, None]
         return self.vra_cov, self.vra_lambda
+
+    def _gather_b2(self) -> torch.Tensor:
+        """[T] VRA bias statistics of every date (history first).  Collective."""
+        if self.B2_global is None:
+            B2_all = pdist.all_gather_rows(self.B2, self.ctx, self.sizes)
+            if self.history is not None:
+                B2_all = torch.cat([self.history["B2"].to(B2_all.device, B2_all.dtype), B2_all])
+            self.B2_global = B2_all
+        return self.B2_global
 
     def run(self):
         self.regress()
@@ -186,8 +215,9 @@ class RiskModel:
 
         Call after :meth:`run`.  Collective in distributed mode (every rank must call it).
         """
-        if self.B2_global is None:
+        if self.vra_cov is None:
             raise RuntimeError("run all four stages before exporting a checkpoint")
+        F_all, B2_all = self._gather_f(), self._gather_b2()
         r2 = pdist.all_gather_rows(self.r2, self.ctx, self.sizes)
         status = pdist.all_gather_rows(self.status, self.ctx, self.sizes)
         var = torch.diagonal(self.eigen_cov, dim1=-2, dim2=-1).contiguous()
@@ -201,10 +231,10 @@ class RiskModel:
             dates = list(self.history["dates"]) + dates
         cfg = self.cfg.to_dict()
         return {
-            "T": int(self.factor_ret_global.shape[0]), "K": int(self.K),
+            "T": int(F_all.shape[0]), "K": int(self.K),
             "factor_names": list(self.panel.factor_names), "dates": dates,
             "config": {k: v for k, v in cfg.items()}, "config_hash": ckpt.config_hash(cfg),
-            "factor_ret": self.factor_ret_global, "B2": self.B2_global,
+            "factor_ret": F_all, "B2": B2_all,
             "r2": r2, "status": status, "last_var": var_all[-1], "last_vra_cov": vra_last,
         }
 

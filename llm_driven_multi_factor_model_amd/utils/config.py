@@ -30,10 +30,17 @@ class RiskConfig:
     eigen_chunk: int = 256        # sims per launch in "sims" mode (bounds the [D, chunk, K] buffer)
     deterministic: bool | None = None  # bitwise-reproducible CS-WLS kernel (wave-owned LDS
                                        # replicas); None = whenever supported (P <= 53 at Q = 10)
+    time_scan: str = "gather"     # time-axis stages (Newey-West, VRA) across date shards:
+                                  # "gather": all-gather the O(T K) series, every rank scans the
+                                  # prefix (bitwise identical to one GPU); "carry": each rank
+                                  # scans only its dates from carried-in block states (SURVEY
+                                  # 2.5 SP design, O(T/world), equal to one GPU to ~1e-13)
 
     def __post_init__(self):
         if self.eigen_shard not in ("dates", "sims"):
             raise ValueError(f"eigen_shard must be 'dates' or 'sims', got {self.eigen_shard!r}")
+        if self.time_scan not in ("gather", "carry"):
+            raise ValueError(f"time_scan must be 'gather' or 'carry', got {self.time_scan!r}")
 
     def to_dict(self) -> dict:
         return asdict(self)

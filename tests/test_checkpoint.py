@@ -14,11 +14,13 @@ def _cfg(**kw):
     return RiskConfig(eigen_sims=6, nw_half_life=20.0, vra_half_life=10.0, **kw)
 
 
-@pytest.mark.parametrize("oos", [False, True])
-def test_resume_equals_full_run(tmp_path, oos):
-    """Run T1 dates, checkpoint, resume on the rest: new-date outputs == one full run."""
+@pytest.mark.parametrize("oos,scan", [(False, "gather"), (True, "gather"), (False, "carry"),
+                                      (True, "carry")])
+def test_resume_equals_full_run(tmp_path, oos, scan):
+    """Run T1 dates, checkpoint, resume on the rest: new-date outputs == one full run (both
+    time-axis scan modes; "carry" starts the new dates' scans from the history's block state)."""
     p = synthetic_panel(40, 64, P=4, Q=3, seed=3, missing_frac=0.02)
-    cfg = _cfg(vra_out_of_sample=oos)
+    cfg = _cfg(vra_out_of_sample=oos, time_scan=scan)
     full = RiskModel(p, cfg).run()
     T1 = 27
     first = RiskModel(p.slice_dates(0, T1), cfg, T_global=T1)
@@ -40,7 +42,7 @@ def test_resume_equals_full_run(tmp_path, oos):
     # chained checkpoint covers all dates
     st2 = m2.state_dict()
     assert st2["T"] == p.D and len(st2["dates"]) == p.D
-    torch.testing.assert_close(st2["factor_ret"], full.factor_ret_global, rtol=0, atol=0)
+    torch.testing.assert_close(st2["factor_ret"], full._gather_f(), rtol=0, atol=0)
 
 
 def test_resume_guards(tmp_path):

@@ -1,0 +1,96 @@
+"""Time-axis scan across date shards (SURVEY 2.5 SP: block carries + exclusive scan + q-row
+halo): ``RiskConfig(time_scan="carry")`` and the sharded Newey-West / VRA scans equal the
+single-process prefix scans (CPU recurrence here; the HIP shard kernel on the GPU)."""
+import os
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+from llm_driven_multi_factor_model_amd.ops import ew_scan
+
+from .test_distributed import _free_port
+
+
+def _series(T, K, seed):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(T, K, generator=g, dtype=torch.float64) * 0.01
+
+
+@pytest.mark.parametrize("q", [0, 1, 2, 5])
+@pytest.mark.parametrize("cut", [1, 4, 33, 69])
+def test_sharded_nw_from_history_matches_prefix_scan(q, cut):
+    F = _series(70, 4, 1)
+    ref = ew_scan.newey_west_series_reference(F, q, 30.0)
+    got = ew_scan.newey_west_series_sharded(F[cut:], q, 30.0, history=F[:cut])
+    torch.testing.assert_close(got, ref[cut:], rtol=1e-12, atol=1e-16, equal_nan=True)
+
+
+def test_sharded_prefix_mean_from_history():
+    x = _series(50, 1, 2)[:, 0]
+    x[[3, 17, 31]] = float("nan")
+    ref = ew_scan.ew_prefix_mean_reference(x, 10.0)
+    got = ew_scan.ew_prefix_mean_sharded(x[20:], 10.0, history=x[:20])
+    torch.testing.assert_close(got, ref[20:], rtol=1e-13, atol=0.0, equal_nan=True)
+
+
+def _worker(rank, world, port, out_path, D, cuts):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from llm_driven_multi_factor_model_amd.models.panel import synthetic_panel
+    from llm_driven_multi_factor_model_amd.models.risk_model import RiskModel
+    from llm_driven_multi_factor_model_amd.parallel import dist as pdist
+    from llm_driven_multi_factor_model_amd.utils.config import preset
+
+    ctx = pdist.init_distributed(device="cpu")
+    full = synthetic_panel(D, 50, 3, 3, seed=7, missing_frac=0.05)
+    a, b = cuts[ctx.rank], cuts[ctx.rank + 1]  # uneven blocks, one shorter than q + 1
+    cfg = preset("use4s", eigen_sims=5, time_scan="carry")
+    m = RiskModel(full.slice_dates(a, b), cfg, T_global=full.D, ctx=ctx)
+    m.run()
+    # the raw series too: every shard's own rows only
+    nw = ew_scan.newey_west_series_sharded(m.factor_ret, 3, 40.0, ctx, m.sizes)
+    out = {k: pdist.gather_to_root(v, ctx) for k, v in
+           dict(nw=m.nw_cov, vr=m.vra_cov, lam=m.vra_lambda, f=m.factor_ret, raw=nw).items()}
+    if ctx.rank == 0:
+        torch.save(out, out_path)
+    pdist.barrier(ctx)
+    torch.distributed.destroy_process_group()
+
+
+@pytest.mark.parametrize("cuts", [[0, 21, 45], [0, 30, 33, 45]])
+def test_carry_mode_ranks_match_single_process(cuts):
+    from llm_driven_multi_factor_model_amd.models.panel import synthetic_panel
+    from llm_driven_multi_factor_model_amd.models.risk_model import RiskModel
+    from llm_driven_multi_factor_model_amd.utils.config import preset
+
+    D, world = cuts[-1], len(cuts) - 1
+    with tempfile.TemporaryDirectory() as td:
+        path = os.path.join(td, "scan.pt")
+        mp.spawn(_worker, args=(world, _free_port(), path, D, cuts), nprocs=world, join=True)
+        got = torch.load(path, weights_only=True)
+    full = synthetic_panel(D, 50, 3, 3, seed=7, missing_frac=0.05)
+    m = RiskModel(full, preset("use4s", eigen_sims=5))  # time_scan="gather", one process
+    m.run()
+    ref = dict(nw=m.nw_cov, vr=m.vra_cov, lam=m.vra_lambda, f=m.factor_ret,
+               raw=ew_scan.newey_west_series_reference(m.factor_ret, 3, 40.0))
+    for k in ref:
+        torch.testing.assert_close(got[k], ref[k], rtol=1e-11, atol=1e-15, equal_nan=True, msg=k)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("q", [0, 2, 5, 10])
+@pytest.mark.parametrize("cut", [1, 37, 64, 333])
+def test_hip_shard_scan_matches_full_scan(cuda, q, cut):
+    """HIP shard kernel (carried state, q-row halo, chunk grid starting at the shard) against
+    the single-launch scan; q = 10 runs two lag groups."""
+    F = (_series(400, 42, 3)).to(cuda)
+    ref = ew_scan.newey_west_series(F, q, 90.0)
+    got = ew_scan.newey_west_series_sharded(F[cut:], q, 90.0, history=F[:cut])
+    torch.testing.assert_close(got, ref[cut:], rtol=1e-10, atol=1e-18, equal_nan=True)
+    x = F[:, 0].clone()
+    x[[5, 50, 200]] = float("nan")
+    pm = ew_scan.ew_prefix_mean_sharded(x[cut:], 40.0, history=x[:cut])
+    torch.testing.assert_close(pm, ew_scan.ew_prefix_mean(x, 40.0)[cut:], rtol=1e-12, atol=0.0,
+                               equal_nan=True)
