@@ -44,6 +44,36 @@ __device__ __forceinline__ double dpp_mov(double v) {
   return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
 }
 
+// 64-bit DPP move where lanes without a source (row_shr past the row start, rows masked off by
+// ROW_MASK) take `ident` instead.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_upd(double v, double ident) {
+  const long long b = __builtin_bit_cast(long long, v), o = __builtin_bit_cast(long long, ident);
+  const int lo = __builtin_amdgcn_update_dpp((int)o, (int)b, CTRL, ROW_MASK, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp((int)(o >> 32), (int)(b >> 32), CTRL, ROW_MASK, 0xF, false);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+// Inclusive scan over the 64 lanes (lane order), OP: 0 = sum, 1 = max, 2 = min, 3 = product.
+// Hillis-Steele
+// inside each 16-lane row (row_shr 1, 2, 4, 8), then row_bcast:15 into rows 1 / 3 and
+// row_bcast:31 into rows 2 / 3: six VALU-only steps, no LDS round trip.
+template <int OP>
+__device__ __forceinline__ double wave_scan_dpp(double v) {
+  constexpr double id = OP == 0 ? 0.0 : (OP == 1 ? -__builtin_huge_val()
+                                                  : (OP == 2 ? __builtin_huge_val() : 1.0));
+  auto op = [](double a, double b) {
+    return OP == 0 ? a + b : (OP == 1 ? fmax(a, b) : (OP == 2 ? fmin(a, b) : a * b));
+  };
+  v = op(v, dpp_upd<0x111, 0xF>(v, id));
+  v = op(v, dpp_upd<0x112, 0xF>(v, id));
+  v = op(v, dpp_upd<0x114, 0xF>(v, id));
+  v = op(v, dpp_upd<0x118, 0xF>(v, id));
+  v = op(v, dpp_upd<0x142, 0xA>(v, id));
+  v = op(v, dpp_upd<0x143, 0xC>(v, id));
+  return v;
+}
+
 // Sum over each row of 16 lanes; every lane of the row gets the same bits.
 __device__ __forceinline__ double row16_sum(double v) {
   v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]  (lane ^ 1)

@@ -887,8 +887,194 @@ __global__ __launch_bounds__(256) void cmra_scan_kernel(const float* __restrict_
   }
 }
 
-int g_roll_mode = 0;  // 0 = default (anchored-prefix / sliding-window kernels), 1 = direct per-row
-                      // kernels (A/B, tests), 2 = round-1 sliding-window BETA / DASTD (A/B)
+// CMRA, full windows (the reference's factor_calculator.py:199-234 path), O(1) per row with the
+// van Herk / Gil-Werman decomposition over 64-row blocks (one row per lane).  With c the running
+// sum of the log returns from the workgroup's first staged row (NaN taps add 0; any NaN in a
+// window makes it NaN), the window [a, r] of W > 64 rows is
+//   [a, end of a's block] U full blocks U [start of r's block, r]
+// so max c = max(suffix-max h[a], block maxima, prefix-max g[r]), likewise min, and CMRA =
+// max - min (ln(1 + max Z) - ln(1 + min Z) with Z = exp(c - c_(a-1)) - 1; the offset cancels).
+// Per 64-row block a wave does a sum scan, prefix / suffix max and min scans (DPP) and one NaN
+// ballot; suffix values and block extrema go to LDS, prefix values stay in registers.  Each workgroup
+// owns kVhRows output rows plus a kVhH-row halo (W - 1 <= kVhH), so HBM sees each row ~once.
+// Replaced the chunked cmra_scan_kernel (O(W / kChunk) taps per row, latency-bound): A/B mode 2.
+constexpr int kVhH = 256;
+constexpr int kVhRows = 2048;
+constexpr int kVhBlk = (kVhRows + kVhH) / 64;  // 36 staged 64-row blocks (37 KB of LDS: 4 WGs / CU)
+constexpr int kVhWaves = 4;
+constexpr int kVhBPW = kVhBlk / kVhWaves;      // 9 blocks per wave
+static_assert(kVhBlk % kVhWaves == 0 && kVhH % 64 == 0, "block split");
+
+__global__ __launch_bounds__(kVhWaves * 64) void cmra_vhgw_kernel(const float* __restrict__ lr,
+                                                                  const int* __restrict__ seg_lo,
+                                                                  int R, int W,
+                                                                  float* __restrict__ out) {
+  __shared__ double hmax[kVhBlk * 64], hmin[kVhBlk * 64];
+  __shared__ double bmax[kVhBlk], bmin[kVhBlk];
+  __shared__ unsigned long long nanm[kVhBlk];
+  __shared__ double wtot[kVhWaves];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int g0 = blockIdx.x * kVhRows - kVhH;
+  // pass 1: this wave's rows (one per lane per block) and its total
+  float v[kVhBPW];
+  double tot = 0.0;
+#pragma unroll
+  for (int k = 0; k < kVhBPW; ++k) {
+    const int g = g0 + (wid * kVhBPW + k) * 64 + lane;
+    v[k] = (g >= 0 && g < R) ? lr[g] : qnanf();
+    tot += fin(v[k]) ? (double)v[k] : 0.0;
+  }
+  tot = wave_sum(tot);
+  if (lane == 0) wtot[wid] = tot;
+  __syncthreads();
+  double carry = 0.0;
+  for (int w = 0; w < wid; ++w) carry += wtot[w];
+  // pass 2: running sum, block prefix (registers) / suffix (LDS) extrema, NaN masks.  All scans
+  // are DPP (VALU-only); the suffix scans run as prefix scans of the lane-reversed sums (one
+  // ds_bpermute) and store to the mirrored LDS slot.
+  double gmax[kVhBPW], gmin[kVhBPW];
+  unsigned long long gnan[kVhBPW];
+#pragma unroll
+  for (int k = 0; k < kVhBPW; ++k) {
+    const int blk = wid * kVhBPW + k;
+    const bool ok = fin(v[k]);
+    const double c = wave_scan_dpp<0>(ok ? (double)v[k] : 0.0) + carry;
+    carry = readlane(c, 63);
+    const double cr = __shfl(c, 63 - lane, kWave);
+    gmax[k] = wave_scan_dpp<1>(c);
+    gmin[k] = wave_scan_dpp<2>(c);
+    hmax[blk * 64 + 63 - lane] = wave_scan_dpp<1>(cr);
+    hmin[blk * 64 + 63 - lane] = wave_scan_dpp<2>(cr);
+    const unsigned long long m = __ballot(!ok);
+    gnan[k] = m;
+    if (lane == 63) { bmax[blk] = gmax[k]; bmin[blk] = gmin[k]; }
+    if (lane == 0) nanm[blk] = m;
+  }
+  __syncthreads();
+  // pass 3: outputs (the first kVhH staged rows are halo)
+#pragma unroll
+  for (int k = 0; k < kVhBPW; ++k) {
+    const int blk = wid * kVhBPW + k;
+    if (blk * 64 < kVhH) continue;
+    const int t = blk * 64 + lane, r = g0 + t;
+    if (r >= R) continue;
+    float o = qnanf();
+    if (r - W + 1 >= seg_lo[r]) {
+      const int at = t - W + 1, ba = at >> 6;  // ba < blk since W > 64
+      double mx = fmax(hmax[at], gmax[k]), mn = fmin(hmin[at], gmin[k]);
+      bool bad = (nanm[ba] >> (at & 63)) != 0 || (gnan[k] & (lane == 63 ? ~0ull : (2ull << lane) - 1)) != 0;
+      for (int j = ba + 1; j < blk; ++j) {
+        mx = fmax(mx, bmax[j]);
+        mn = fmin(mn, bmin[j]);
+        bad = bad || nanm[j] != 0;
+      }
+      if (!bad) o = (float)(mx - mn);
+    }
+    out[r] = o;
+  }
+}
+
+// RSTR (factor_calculator.py:127-153): a NaN-renormalised positional-weight mean over the log
+// returns lr[k], k in [kl, kr] = [max(seg_lo, r - W + 1 - L), r - L], weights lam^(k - kl) (the
+// oldest row weighs 1; the reference's normalisation cancels the common base).  With the
+// BACKWARD-anchored decayed sums U[k] = sum_(j >= k) lam^(j - k) x_j (terms shrink away from k,
+// so no growth), the window sums are U[kl] - lam^(kr + 1 - kl) U[kr + 1] (numerator: x = lr,
+// denominator: x = 1 on valid rows), the valid count a suffix-count difference: O(1) per row.
+// Each wave scans its 64-row blocks last to first with lanes holding the block's rows in reverse
+// (a forward DPP prefix of lam^-m x'), carries U across blocks, and the waves' regions are joined
+// by their carry-ins when read.  Replaced the sliding rstr_scan_kernel (A/B mode 2).
+constexpr int kRsH = 512;                       // halo: W + L - 1 <= kRsH
+constexpr int kRsRows = 2048;                   // output rows per workgroup
+constexpr int kRsBlk = (kRsRows + kRsH) / 64;   // 40 staged 64-row blocks
+constexpr int kRsWaves = 4;
+constexpr int kRsBPW = kRsBlk / kRsWaves;       // 10 blocks per wave
+constexpr int kRsWRows = kRsBPW * 64;           // rows per wave region
+static_assert(kRsBlk % kRsWaves == 0 && kRsH % 64 == 0, "block split");
+
+__global__ __launch_bounds__(kRsWaves * 64) void rstr_ew_kernel(const float* __restrict__ lr,
+                                                                const int* __restrict__ seg_lo,
+                                                                int R, int L, int W, double lam,
+                                                                int minp,
+                                                                float* __restrict__ out) {
+  __shared__ double un[kRsBlk * 64], ud[kRsBlk * 64];
+  __shared__ unsigned short cs[kRsBlk * 64];  // valid-row suffix count in the wave region (<= 640)
+  __shared__ double pw[kRsWRows + 1];
+  __shared__ double tn[kRsWaves], td[kRsWaves], in_n[kRsWaves], in_d[kRsWaves];
+  __shared__ int tc[kRsWaves], in_c[kRsWaves];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int g0 = blockIdx.x * kRsRows - kRsH;
+  // lam^k without pow: lam^lane from a DPP product scan, times (lam^64)^(k / 64)
+  const double lp = wave_scan_dpp<3>(lane == 0 ? 1.0 : lam), lp1 = lp * lam, lpn = 1.0 / lp;
+  {
+    const double l64 = readlane(lp1, 63);
+    double blk = 1.0;
+    for (int b = 0; b * 64 <= kRsWRows; ++b, blk *= l64)
+      if (b % kRsWaves == wid && b * 64 + lane <= kRsWRows) pw[b * 64 + lane] = blk * lp;
+  }
+  // lane m holds block row 63 - m: U_block = lam^m * prefix(lam^-m x') + lam^(m+1) * carry
+  const unsigned long long below = lane == 63 ? ~0ull : (2ull << lane) - 1;
+  double cn = 0.0, cd = 0.0;
+  int cc = 0;
+  for (int k = kRsBPW - 1; k >= 0; --k) {
+    const int t = (wid * kRsBPW + k) * 64 + 63 - lane, g = g0 + t;
+    const float v = (g >= 0 && g < R) ? lr[g] : qnanf();
+    const bool ok = fin(v);
+    const double zn = wave_scan_dpp<0>(ok ? lpn * (double)v : 0.0);
+    const double zd = wave_scan_dpp<0>(ok ? lpn : 0.0);
+    const unsigned long long M = __ballot(ok);
+    const double Un = fma(lp, zn, lp1 * cn), Ud = fma(lp, zd, lp1 * cd);
+    un[t] = Un;
+    ud[t] = Ud;
+    cs[t] = (unsigned short)(cc + __popcll(M & below));
+    cn = readlane(Un, 63);
+    cd = readlane(Ud, 63);
+    cc += __popcll(M);
+  }
+  if (lane == 0) { tn[wid] = cn; td[wid] = cd; tc[wid] = cc; }
+  __syncthreads();
+  if (threadIdx.x == 0) {  // U / count at the first row after each wave's region
+    double a = 0.0, b = 0.0;
+    int c = 0;
+    for (int w = kRsWaves - 1; w >= 0; --w) {
+      in_n[w] = a; in_d[w] = b; in_c[w] = c;
+      a = fma(pw[kRsWRows], a, tn[w]);
+      b = fma(pw[kRsWRows], b, td[w]);
+      c += tc[w];
+    }
+  }
+  __syncthreads();
+  auto full = [&](int t, double& n, double& d, int& c) {
+    const int w = t / kRsWRows;
+    const double f = pw[(w + 1) * kRsWRows - t];
+    n = fma(f, in_n[w], un[t]);
+    d = fma(f, in_d[w], ud[t]);
+    c = cs[t] + in_c[w];
+  };
+  for (int k = 0; k < kRsBPW; ++k) {
+    const int blk = wid * kRsBPW + k;
+    if (blk * 64 < kRsH) continue;
+    const int t = blk * 64 + lane, r = g0 + t;
+    if (r >= R) continue;
+    const int kl = max(seg_lo[r], r - W + 1 - L), kr = r - L;
+    float o = qnanf();
+    if (kr >= kl) {
+      const int tl = kl - g0, tr = kr + 1 - g0;
+      double nl, dl, nr, dr;
+      int cl, cr;
+      full(tl, nl, dl, cl);
+      full(tr, nr, dr, cr);
+      if (cl - cr >= minp) {
+        const double f = pw[tr - tl];
+        o = (float)(fma(-f, nr, nl) / fma(-f, dr, dl));
+      }
+    }
+    out[r] = o;
+  }
+}
+
+int g_roll_mode = 0;  // 0 = default (anchored-prefix / van Herk / sliding-window kernels), 1 = direct
+                      // per-row kernels (A/B, tests), 2 = round-1 sliding-window BETA / DASTD /
+                      // CMRA / RSTR (A/B)
 
 int ew_halo(int W) { return (W + kChunk - 1) / kChunk * kChunk; }
 
@@ -915,7 +1101,10 @@ MFA_API int mfa_beta_hsigma(const float* y, const float* x, const int* seg_lo, i
 MFA_API int mfa_rstr(const float* lr, const int* seg_lo, int R, int L, int W, double lam,
                      int minp, float* out, void* s) {
   if (R <= 0) return 0;
-  if (g_roll_mode != 1 && W + L <= 512 && W + kChunk + 1 <= kPowMax)
+  if (g_roll_mode == 0 && L >= 1 && W >= 1 && W + L - 1 <= kRsH && W <= kRsWRows)
+    hipLaunchKernelGGL(rstr_ew_kernel, dim3((R + kRsRows - 1) / kRsRows), dim3(kRsWaves * 64), 0,
+                       (hipStream_t)s, lr, seg_lo, R, L, W, lam, minp, out);
+  else if (g_roll_mode != 1 && W + L <= 512 && W + kChunk + 1 <= kPowMax)
     hipLaunchKernelGGL(rstr_scan_kernel<512>, MFA_SCAN_GRID(R), 0, (hipStream_t)s, lr, seg_lo, R, L,
                        W, lam, minp, out);
   else
@@ -938,7 +1127,10 @@ MFA_API int mfa_dastd(const float* ret, const float* mret, const int* seg_lo, in
 MFA_API int mfa_cmra(const float* lr, const int* seg_lo, int R, int W, int partial, float* out,
                      void* s) {
   if (R <= 0) return 0;
-  if (g_roll_mode != 1 && W <= 256 && W >= kChunk)
+  if (g_roll_mode == 0 && !partial && W > 64 && W - 1 <= kVhH)
+    hipLaunchKernelGGL(cmra_vhgw_kernel, dim3((R + kVhRows - 1) / kVhRows), dim3(kVhWaves * 64), 0,
+                       (hipStream_t)s, lr, seg_lo, R, W, out);
+  else if (g_roll_mode != 1 && W <= 256 && W >= kChunk)
     hipLaunchKernelGGL(cmra_scan_kernel<256>, MFA_SCAN_GRID(R), 0, (hipStream_t)s, lr, seg_lo, R, W,
                        partial, out);
   else

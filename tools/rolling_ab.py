@@ -1,5 +1,8 @@
-"""A/B of the BETA/HSIGMA and DASTD window kernels on a 5000 x 3780 flat panel (event timing):
-round-1 sliding-window kernels (mode 2) vs the default anchored-prefix pipelined kernel.  Prints ms and effective HBM bandwidth (inputs + outputs, 4 B each)."""
+"""A/B of the BETA/HSIGMA, DASTD, CMRA and RSTR window kernels on a 5000 x 3780 flat panel
+(event timing): round-1 sliding-window kernels (mode 2) vs the defaults (anchored-prefix
+pipelined kernel for BETA/HSIGMA and DASTD, van Herk / Gil-Werman blocks for CMRA, backward-
+anchored decayed sums for RSTR).  Prints ms and
+effective HBM bandwidth (inputs + outputs + seg_lo, 4 B each)."""
 import json
 import os
 import statistics
@@ -23,15 +26,20 @@ mret = mkt[None, :].expand(N, T).reshape(-1).contiguous().float()
 stock = torch.arange(N, device=dev, dtype=torch.int32).repeat_interleave(T)
 seg = RL.seg_lo_from_codes(stock)
 lib = _native.lib()
-beta, hsig, dast = (torch.empty(R, device=dev) for _ in range(3))
+lr = torch.log1p(ret)
+beta, hsig, dast, cmra, rstr = (torch.empty(R, device=dev) for _ in range(5))
 cases = {
     "beta_hsigma": (lambda: _native.call("mfa_beta_hsigma", _native.ptr(ret), _native.ptr(mret),
                                          _native.ptr(seg), R, 252, 0.5 ** (1 / 63), 42,
                                          _native.ptr(beta), _native.ptr(hsig), _native.stream(dev)), 20),
     "dastd": (lambda: _native.call("mfa_dastd", _native.ptr(ret), _native.ptr(mret), _native.ptr(seg),
                                    R, 252, 0.5 ** (1 / 42), 42, _native.ptr(dast), _native.stream(dev)), 16),
+    "cmra": (lambda: _native.call("mfa_cmra", _native.ptr(lr), _native.ptr(seg), R, 252, 0,
+                                  _native.ptr(cmra), _native.stream(dev)), 12),
+    "rstr": (lambda: _native.call("mfa_rstr", _native.ptr(lr), _native.ptr(seg), R, 21, 483,
+                                  0.5 ** (1 / 126), 42, _native.ptr(rstr), _native.stream(dev)), 12),
 }
-variants = [("mode2_r01", 2), ("anchored_prefix", 0)]
+variants = [("mode2_r01", 2), ("default", 0)]
 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 ref = {}
 for name, (fn, bpr) in cases.items():
@@ -40,11 +48,14 @@ for name, (fn, bpr) in cases.items():
         lib.mfa_rolling_set_mode(mode)
         fn()
         torch.cuda.synchronize()
-        out = (beta.clone(), hsig.clone()) if name == "beta_hsigma" else (dast.clone(),)
+        out = {"beta_hsigma": (beta, hsig), "dastd": (dast,), "cmra": (cmra,), "rstr": (rstr,)}[name]
+        out = tuple(o.clone() for o in out)
         if vname == "mode2_r01":
             ref[name] = out
         err = max(((a - b).abs() / b.abs().clamp_min(1e-6)).nan_to_num(0).max().item()
                   for a, b in zip(out, ref[name]))
+        if not all(bool((a.isnan() == b.isnan()).all()) for a, b in zip(out, ref[name])):
+            err = float("inf")  # NaN pattern differs
         ts = []
         for _ in range(5):
             ev0.record()
