@@ -68,12 +68,19 @@ def main() -> int:
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     use_cuda = torch.cuda.is_available()
-    dev = torch.device(f"cuda:{local}" if use_cuda else "cpu")
+    rehearse = bool(os.environ.get("MFA_BENCH_BACKEND"))
+    # a rehearsal may place several ranks on one device (local rank modulo the visible GPUs)
+    gpu = local % max(1, torch.cuda.device_count()) if use_cuda and rehearse else local
+    dev = torch.device(f"cuda:{gpu}" if use_cuda else "cpu")
     if use_cuda:
         torch.cuda.set_device(dev)
+    backend = None
     if world > 1:
-        dist.init_process_group("nccl" if use_cuda else "gloo", rank=rank, world_size=world,
-                                device_id=dev if use_cuda else None)
+        # MFA_BENCH_BACKEND=gloo rehearses the multi-rank flow with several ranks on ONE GPU;
+        # the default on GPUs is nccl (= RCCL).
+        backend = os.environ.get("MFA_BENCH_BACKEND") or ("nccl" if use_cuda else "gloo")
+        dist.init_process_group(backend, rank=rank, world_size=world,
+                                device_id=dev if use_cuda and backend == "nccl" else None)
 
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from llm_driven_multi_factor_model_amd import _native
@@ -207,6 +214,9 @@ def main() -> int:
                 "parallelism": f"dp{world}",
                 "specific_returns": not args.no_resid,
                 "storage": args.storage,
+                "backend": backend,
+                "ranks_per_gpu": (world // max(1, torch.cuda.device_count())
+                                  if use_cuda and rehearse else 1),
             },
         }), flush=True)
     if world > 1:

@@ -289,3 +289,37 @@ def test_cetop_ttm_run_path_equals_merge_path_and_falls_back():
     if b is None:
         b = eng2._ttm_by_merge(eng2.master)
     torch.testing.assert_close(b, eng2._ttm_by_merge(eng2.master), rtol=0, atol=0, equal_nan=True)
+
+
+@pytest.mark.gpu
+def test_hip_cmra_rstr_window_edges(cuda):
+    """The van Herk CMRA and backward-anchored RSTR kernels at the edges of their window ranges
+    (CMRA W = 65 / 257: just above one 64-row block / the 256-row halo; RSTR reach W + L - 1 =
+    512 = the halo, W = 1, L = 1) == the direct per-row kernels, on ragged stocks with NaNs."""
+    from llm_driven_multi_factor_model_amd import _native
+    g = torch.Generator().manual_seed(21)
+    lens = torch.randint(30, 3000, (300,), generator=g)
+    R = int(lens.sum())
+    stock = torch.repeat_interleave(torch.arange(300, dtype=torch.int32), lens)
+    lr = (torch.randn(R, generator=g) * 0.02).float()
+    lr[torch.rand(R, generator=g) < 0.003] = float("nan")
+    seg = RL.seg_lo_from_codes(stock).to(cuda)
+    l_ = lr.to(cuda)
+    fns = {
+        "cmra65": lambda: RL.cmra(l_, seg, 65),
+        "cmra257": lambda: RL.cmra(l_, seg, 257),
+        "rstr_max_reach": lambda: RL.rstr(l_, seg, 512, 21, 126.0, 42),
+        "rstr_w1": lambda: RL.rstr(l_, seg, 2, 1, 5.0, 1),
+        "rstr_short_hl": lambda: RL.rstr(l_, seg, 100, 3, 2.0, 10),
+    }
+    lib = _native.lib()
+    try:
+        lib.mfa_rolling_set_mode(1)
+        direct = {k: f() for k, f in fns.items()}
+        lib.mfa_rolling_set_mode(0)
+        fast = {k: f() for k, f in fns.items()}
+    finally:
+        lib.mfa_rolling_set_mode(0)
+    for k in fns:
+        assert int(torch.isfinite(direct[k]).sum()) > R // 4, k
+        torch.testing.assert_close(fast[k].cpu(), direct[k].cpu(), rtol=2e-5, atol=2e-7, equal_nan=True, msg=k)
