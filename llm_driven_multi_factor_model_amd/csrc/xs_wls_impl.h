@@ -846,6 +846,17 @@ __device__ __forceinline__ void resid_prefetch(const float* __restrict__ X,
 // Residual-pass vector types: HIP's float4 / double2 (16-byte rows) and packed int16 ids.
 // (With clang ext_vector types instead, hipcc scheduled a full vmcnt(0) drain at the top of
 // every residual iteration: +30 us on the fp32 step.)
+// Infinity-Cache (MALL) hygiene of the residual pass (profiles/r02_xs_nt_store_ab.md): the
+// specific returns are stored non-temporally (write-once output: fp64 step 421 -> 412 us), and
+// the fp64 re-read of the panel slice, the last use of those lines, is loaded non-temporally
+// so it does not refresh dead lines over those other dates still have to re-read (412 ->
+// 387 us).  fp32 panels: neutral for the stores, slower at small D for the loads (plain loads).
+#ifndef MFA_XS_NT_E
+#define MFA_XS_NT_E 1
+#endif
+#ifndef MFA_XS_NT_LD64
+#define MFA_XS_NT_LD64 1
+#endif
 template <typename T> struct RVec;
 template <> struct RVec<float> {
   typedef float4 vec;
@@ -860,6 +871,15 @@ template <> struct RVec<float> {
   static __device__ __forceinline__ vec pack(const float (&a)[4]) {
     return make_float4(a[0], a[1], a[2], a[3]);
   }
+  static __device__ __forceinline__ vec load(const float* p) { return *(const vec*)p; }
+  static __device__ __forceinline__ void store(float* p, const vec& v) {
+    if constexpr (MFA_XS_NT_E) {
+      __builtin_nontemporal_store(v.x, p); __builtin_nontemporal_store(v.y, p + 1);
+      __builtin_nontemporal_store(v.z, p + 2); __builtin_nontemporal_store(v.w, p + 3);
+    } else {
+      *(vec*)p = v;
+    }
+  }
   static __device__ __forceinline__ ivec izero() { return make_uint2(0u, 0u); }
 };
 template <> struct RVec<double> {
@@ -870,6 +890,22 @@ template <> struct RVec<double> {
     a[0] = (int)(short)(v & 0xFFFF); a[1] = (int)(short)(v >> 16);
   }
   static __device__ __forceinline__ vec pack(const double (&a)[2]) { return make_double2(a[0], a[1]); }
+  static __device__ __forceinline__ vec load(const double* p) {
+    if constexpr (MFA_XS_NT_LD64) {
+      typedef double d2 __attribute__((ext_vector_type(2)));
+      const d2 t = __builtin_nontemporal_load((const d2*)p);
+      return make_double2(t.x, t.y);
+    } else {
+      return *(const vec*)p;
+    }
+  }
+  static __device__ __forceinline__ void store(double* p, const vec& v) {
+    if constexpr (MFA_XS_NT_E) {
+      __builtin_nontemporal_store(v.x, p); __builtin_nontemporal_store(v.y, p + 1);
+    } else {
+      *(vec*)p = v;
+    }
+  }
   static __device__ __forceinline__ ivec izero() { return 0u; }
 };
 
@@ -964,7 +1000,7 @@ __device__ __forceinline__ void resid_body(
         const int n = nlo + (tid - 64) * 4 + u * 768;
         if (n < N) {
           const vec eo = compute(pre.c4[u], pre.r4[u], pre.x4[u], pre.j4[u], okbits(n));
-          if (ed) *(vec*)(ed + n) = eo;
+          if (ed) RV::store(ed + n, eo);
         }
       }
     }
@@ -984,10 +1020,10 @@ __device__ __forceinline__ void resid_body(
     for (int u = 0; u < U; ++u) {
       const int n = n0 + u * step;
       if (n < Nmain) {
-        if (!okd) cv[u] = *(const vec*)(cd + n);
-        rv[u] = *(const vec*)(rd + n);
+        if (!okd) cv[u] = RV::load(cd + n);
+        rv[u] = RV::load(rd + n);
 #pragma unroll
-        for (int q = 0; q < Q; ++q) xv[u][q] = *(const vec*)(Xd + (size_t)q * N + n);
+        for (int q = 0; q < Q; ++q) xv[u][q] = RV::load(Xd + (size_t)q * N + n);
         jv[u] = id ? *(const ivec*)(id + n) : RV::izero();
       }
     }
@@ -1006,7 +1042,7 @@ __device__ __forceinline__ void resid_body(
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int n = n0 + u * step;
-        if (n < Nmain) *(vec*)(ed + n) = eo[u];
+        if (n < Nmain) RV::store(ed + n, eo[u]);
       }
     }
   }
