@@ -687,10 +687,17 @@ __global__ __launch_bounds__(64) void mc_bias_tri_kernel(const double* __restric
       // column s of the (symmetric) matrix is each lane's own a[s]: select it from the group's
       // 8 static candidates (publishing row s through LDS cost ~22 single-lane 16-B stores per
       // step, each paying the whole wave's VGPR transfer: the phase's LDS-array time)
+      // (each candidate goes through an empty asm: without it the compiler turns the select
+      // chain into a dynamically indexed load, which demotes the whole row to scratch memory
+      // and re-stores it after every step)
       double xs = a[J0];
 #pragma unroll
       for (int k = 1; k < 8; ++k)
-        if (J0 + k < KP) xs = s == J0 + k ? a[J0 + k] : xs;
+        if (J0 + k < KP) {
+          double t = a[J0 + k];
+          asm volatile("" : "+v"(t));
+          xs = s == J0 + k ? t : xs;
+        }
       const bool act = lane > s && lane < K;
       const double x = act ? xs : 0.0;
       const double x0 = readlane(xs, s + 1);
@@ -752,8 +759,10 @@ __global__ __launch_bounds__(64) void mc_bias_tri_kernel(const double* __restric
     double c2 = 0.0, c1 = 0.0;  // each lane's a[K-2], a[K-1] (dynamic index: static select)
 #pragma unroll
     for (int j = 0; j < KP; ++j) {
-      c2 = j == K - 2 ? a[j] : c2;
-      c1 = j == K - 1 ? a[j] : c1;
+      double t = a[j];
+      asm volatile("" : "+v"(t));  // keep `a` in registers (see the step select above)
+      c2 = j == K - 2 ? t : c2;
+      c1 = j == K - 1 ? t : c1;
     }
     const double a22 = K >= 2 ? readlane(c2, K - 2) : readlane(c1, 0);
     const double b21 = K >= 2 ? readlane(c2, K - 1) : 0.0;
