@@ -151,10 +151,13 @@ template <> struct Stream<float> {
   static constexpr int VEC = 4;  // residual pass: stocks per 16-byte load
   static constexpr int U = 3;    // residual iterations in flight
 };
+#ifndef MFA_XS_U64
+#define MFA_XS_U64 2
+#endif
 template <> struct Stream<double> {
   static constexpr int RING = 2;
   static constexpr int VEC = 2;
-  static constexpr int U = 2;
+  static constexpr int U = MFA_XS_U64;
 };
 
 template <int Q, typename T>
