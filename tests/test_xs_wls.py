@@ -167,6 +167,22 @@ def test_device_pinv_refine_matches_oracle(cuda):
 
 
 @pytest.mark.gpu
+def test_device_pinv_refine_more_dates_than_grid(cuda):
+    """Every one of 1100 dates flagged near-singular: the grid-stride refine pass (512
+    workgroups) re-solves dates 0, 511, 512, 1023, 1024 and 1099 like the pinv oracle."""
+    p = _degenerate_panel(D=1100, N=200, P=6, Q=4, seed=9)
+    g = p.to(cuda)
+    out = X.xs_wls(g.styles, g.cap, g.ret, g.ind, p.P)
+    torch.cuda.synchronize()
+    assert ((out.status.cpu() & X.XS_REFINED) != 0).all()
+    idx = [0, 511, 512, 1023, 1024, 1099]
+    ref = X.xs_wls_reference(p.styles[idx], p.cap[idx], p.ret[idx], p.ind[idx], p.P)
+    torch.testing.assert_close(out.f.cpu()[idx], ref.f, rtol=1e-9, atol=1e-12)
+    torch.testing.assert_close(out.r2.cpu()[idx], ref.r2, rtol=1e-9, atol=1e-12)
+    torch.testing.assert_close(out.resid.cpu()[idx], ref.resid, rtol=1e-9, atol=1e-12, equal_nan=True)
+
+
+@pytest.mark.gpu
 def test_kernel_reference_pivot_and_determinism(cuda):
     panel = synthetic_panel(16, 2000, 31, 10, seed=1, missing_frac=0.01).to(cuda)
     ind = panel.ind.clone()
