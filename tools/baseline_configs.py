@@ -38,7 +38,8 @@ def timed(fn, reps=2):
 
 
 def risk_run(D, N, P, Q, cfg, device, attribution=False):
-    p = synthetic_panel(D, N, P, Q, seed=7, device=device, missing_frac=0.01)
+    # fp64 panel: the reference reads float64 exposures / caps / returns (demo.py:21)
+    p = synthetic_panel(D, N, P, Q, seed=7, device=device, missing_frac=0.01, dtype=torch.float64)
 
     def go():
         m = RiskModel(p, cfg).run()

@@ -31,6 +31,8 @@ ap.add_argument("--P", type=int, default=31)
 ap.add_argument("--Q", type=int, default=10)
 ap.add_argument("--sims", type=int, default=None, help="override the preset's eigen sims")
 ap.add_argument("--preset", default="reference")
+ap.add_argument("--storage", choices=["fp64", "fp32"], default="fp64",
+                help="panel storage dtype (fp64 = the reference's input precision)")
 ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--attribution", action="store_true", help="also time an equal-weight attribution")
 a = ap.parse_args()
@@ -39,7 +41,8 @@ dev = ctx.device
 full_D = a.dates
 lo, hi = pdist.shard_range(full_D, ctx.rank, ctx.world)
 # every rank generates the same panel (seeded) and keeps its date block
-p = synthetic_panel(full_D, a.stocks, a.P, a.Q, seed=3, device=dev, missing_frac=0.01).slice_dates(lo, hi)
+p = synthetic_panel(full_D, a.stocks, a.P, a.Q, seed=3, device=dev, missing_frac=0.01,
+                    dtype=torch.float64 if a.storage == "fp64" else torch.float32).slice_dates(lo, hi)
 over = {"eigen_sims": a.sims} if a.sims else {}
 cfg = preset(a.preset, **over)
 stage = {}
