@@ -125,6 +125,17 @@ __device__ __forceinline__ void wait_vmcnt(int n) {
   }
 }
 
+#ifndef MFA_XS_NT_AUX
+#define MFA_XS_NT_AUX 0
+#endif
+// Stores of auxiliary per-date outputs (moment export, validity masks): non-temporal when
+// MFA_XS_NT_AUX, so they do not take Infinity-Cache space from panel lines awaiting re-read.
+template <typename V>
+__device__ __forceinline__ void aux_store(V* p, V v) {
+  if constexpr (MFA_XS_NT_AUX) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
 __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -332,7 +343,7 @@ __device__ __forceinline__ void moments_body(
     for (int q = 0; q < Q; ++q) ok = ok && finite_v(xf[q]);
     if (okm) {  // validity bits of this 64-stock tile for the residual pass (no cap re-read)
       const unsigned long long m = __ballot(ok);
-      if (lane == 0) okm[(s - lane) >> 6] = m;
+      if (lane == 0) aux_store(okm + ((s - lane) >> 6), m);
     }
     if (ok) {
       const double c = cf, r = rf, w = sqrt(c);
@@ -385,14 +396,14 @@ __device__ __forceinline__ void moments_body(
       for (int w = 0; w < nw; ++w) t += ((const double*)(ring + w * RINGW + 8 * 65 * 8))[tid];
     __syncthreads();  // md may alias the ring
     if (tid < NACC) md[tid] = t;
-    if (gout && tid < NACC) gout[tid] = t;
+    if (gout && tid < NACC) aux_store(gout + tid, t);
   } else {
     wg_reduce<NACC>(v, (double*)wring, acc);
     __syncthreads();
     for (int i = tid; i < NACC; i += nthr) {
       const double t = acc[i];
       md[i] = t;
-      if (gout) gout[i] = t;
+      if (gout) aux_store(gout + i, t);
     }
   }
   for (int i = tid; i < Pseg * NS; i += nthr) {
@@ -401,7 +412,7 @@ __device__ __forceinline__ void moments_body(
 #pragma unroll
     for (int r = 0; r < R; ++r) t += row[r];
     md[NACC + i] = t;
-    if (gout) gout[NACC + i] = t;
+    if (gout) aux_store(gout + NACC + i, t);
   }
   __syncthreads();
 }
