@@ -53,14 +53,18 @@ def init_distributed(backend: str | None = None, device: str | None = None) -> D
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     use_cuda = torch.cuda.is_available() and device != "cpu"
-    dev = torch.device(f"cuda:{local}") if use_cuda else torch.device("cpu")
+    # MFA_DIST_BACKEND (e.g. gloo) rehearses a multi-rank run with several ranks per GPU (local
+    # rank modulo the visible devices); RCCL itself refuses two ranks on one device.
+    rehearse = os.environ.get("MFA_DIST_BACKEND")
+    gpu = local % max(1, torch.cuda.device_count()) if use_cuda and rehearse else local
+    dev = torch.device(f"cuda:{gpu}") if use_cuda else torch.device("cpu")
     if use_cuda:
         torch.cuda.set_device(dev)
-    be = backend or ("nccl" if use_cuda else "gloo")
+    be = backend or rehearse or ("nccl" if use_cuda else "gloo")
     if world > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
-        kw = {"device_id": dev} if use_cuda else {}
+        kw = {"device_id": dev} if use_cuda and be == "nccl" else {}
         dist.init_process_group(be, rank=rank, world_size=world, timeout=collective_timeout(), **kw)
     _CTX = DistContext(rank, world, local, dev, be if world > 1 else None)
     return _CTX
