@@ -622,8 +622,11 @@ __device__ __forceinline__ void lds_order() { asm volatile("" ::: "memory"); }
 // ABL: timing-only ablations (bias modes 41..47, KP = 44): 1 = no Laguerre iterations,
 // 2 = no eigenvector / back-transform, 4 = no tridiagonalisation, 8 = setup only (mode 48),
 // 16 = setup + tridiagonalisation only (mode 56); outputs meaningless
+#ifndef MFA_TRI_WPE
+#define MFA_TRI_WPE 1
+#endif
 template <int KP, int ABL = 0>
-__global__ __launch_bounds__(64) void mc_bias_tri_kernel(const double* __restrict__ D0, int K, int M,
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MFA_TRI_WPE))) void mc_bias_tri_kernel(const double* __restrict__ D0, int K, int M,
                                                          const double* __restrict__ Cz,
                                                          const int* __restrict__ dvalid,
                                                          double* __restrict__ vout) {
