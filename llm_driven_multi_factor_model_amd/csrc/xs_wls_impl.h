@@ -233,10 +233,17 @@ struct Ring {
   static constexpr int BYTES = 4 * RINGW;
 };
 
+// A/B knob (fp64 panels): the cap row, which the residual pass never re-reads (it uses the
+// moments pass's validity bits), gets its own non-temporal DMA instruction so it does not take
+// Infinity-Cache space from rows awaiting re-read (one extra DMA instruction per tile).
+#ifndef MFA_XS_CAP_NT
+#define MFA_XS_CAP_NT 0
+#endif
 // LDS-DMA instructions one wave issues per tile (the vmcnt unit of the ring).
 template <int Q, typename T>
 __device__ __forceinline__ constexpr int dma_per_tile(bool has_ind) {
-  return (sizeof(T) == 4 ? (Q + 5) / 4 : (Q + 3) / 2) + (has_ind ? 1 : 0);
+  return (sizeof(T) == 4 ? (Q + 5) / 4 : (MFA_XS_CAP_NT ? 1 + (Q + 2) / 2 : (Q + 3) / 2)) +
+         (has_ind ? 1 : 0);
 }
 
 // Moments of stocks [nb, ne) of date d (a chunk, or the whole date with nb = 0, ne = N; nb is
@@ -302,8 +309,13 @@ __device__ __forceinline__ void moments_body(
       // two 512-B fp64 rows per instruction: lanes 0-31 -> row rr, lanes 32-63 -> row rr + 1
       const int half = lane >> 5, s = s0 + 2 * (lane & 31);
       const bool in = s < ne;  // ne is even: both stocks of the pair exist
+      constexpr int R0 = MFA_XS_CAP_NT ? 1 : 0;
+      if constexpr (MFA_XS_CAP_NT) {  // cap row alone (lanes 0-31), non-temporal
+        if (in && half == 0)
+          __builtin_amdgcn_global_load_lds((gbl_void_t*)(cd + s), (lds_void_t*)slot, 16, 0, 2);
+      }
 #pragma unroll
-      for (int rr = 0; rr < Q + 2; rr += 2) {
+      for (int rr = R0; rr < Q + 2; rr += 2) {
         const int row = rr + half;
         const T* src = row == 0 ? cd : (row == 1 ? rd : Xd + (size_t)(row - 2) * N);
         if (in && row < Q + 2) glds16(src + s, slot + rr * ROWB);
