@@ -1421,7 +1421,10 @@ constexpr int fused_ring_bytes() {
 }
 
 template <int Q, int R, int VAR, bool PRE, typename T>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) void xs_fused_kernel(
+#ifndef MFA_XS_WPE_BIGQ
+#define MFA_XS_WPE_BIGQ 2
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Q <= 10 ? 2 : MFA_XS_WPE_BIGQ, Q <= 10 ? 2 : MFA_XS_WPE_BIGQ))) void xs_fused_kernel(
     const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
     const int16_t* __restrict__ ind, int N, int P, int Pseg, int pivot_mode, double tol,
     double* __restrict__ fout, T* __restrict__ eout, double* __restrict__ r2out,

@@ -24,7 +24,7 @@ from llm_driven_multi_factor_model_amd.ops.cross_section import xs_wls, xs_wls_w
 
 def main():
     dev = torch.device("cuda:0")
-    N, P, Q = 5000, 31, 10
+    N, P, Q = 5000, 31, int(os.environ.get("Q", 10))
     modes = [int(m) for m in os.environ.get("MODES", "0,30").split(",")]
     Ds = [int(d) for d in os.environ.get("DS", "64,256,315,2520").split(",")]
     reps = int(os.environ.get("REPS", "20"))
@@ -74,7 +74,7 @@ def main():
                     ev1.record()
                     ev1.synchronize()
                     res[m].append(ev0.elapsed_time(ev1) / reps * 1e3)
-            print(json.dumps({"storage": dts, "D": D, "us": {f"mode{m}": round(statistics.median(res[m]), 1)
+            print(json.dumps({"storage": dts, "D": D, "Q": Q, "us": {f"mode{m}": round(statistics.median(res[m]), 1)
                                                              for m in modes}}), flush=True)
             lib.mfa_xs_set_mode(0)
 
