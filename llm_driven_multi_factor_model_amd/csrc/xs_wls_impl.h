@@ -1422,7 +1422,7 @@ constexpr int fused_ring_bytes() {
 
 template <int Q, int R, int VAR, bool PRE, typename T>
 #ifndef MFA_XS_WPE_BIGQ
-#define MFA_XS_WPE_BIGQ 2
+#define MFA_XS_WPE_BIGQ 1
 #endif
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Q <= 10 ? 2 : MFA_XS_WPE_BIGQ, Q <= 10 ? 2 : MFA_XS_WPE_BIGQ))) void xs_fused_kernel(
     const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
