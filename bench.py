@@ -10,10 +10,11 @@ WLS on [country | 31 SW-L1 industries | 10 styles] with the industry-neutral con
 A step regresses every date of a rank's shard (weak scaling, the default: ``--dates`` per GPU,
 2520 = 10 years of trading days; ``--scaling strong``: ``--dates`` in total, 2520 / world per
 rank), replayed from a captured HIP graph: the fused moments -> solve -> residual kernel (one
-workgroup per date) for large shards, the stock-chunked kernels (several workgroups per date)
-for small ones, then all-gathers
-the factor-return series across ranks over RCCL (the collective the downstream Newey-West stage
-needs).  Data is a synthetic panel of the named shape with random-init exposures (the reference ships no data).
+workgroup per date), then all-gathers the factor-return series across ranks over RCCL (the
+collective the downstream Newey-West stage needs).  After the headline loop a second loop
+regresses a FIXED global problem (``--strong-dates``, default ``--dates``, split over the ranks)
+and is reported in the JSON's ``"strong"`` record, so one 1 -> N sweep yields both the weak and
+the strong scaling curve.  Data is a synthetic panel of the named shape with random-init exposures (the reference ships no data).
 
 Storage: ``--storage fp64`` (default, the headline) keeps the panel in float64, the precision
 the reference regresses (``demo.py:21`` reads float64 CSV columns into ``CrossSection.reg``);
@@ -49,6 +50,9 @@ def main() -> int:
                     help="dates per GPU (weak scaling) or in total (strong scaling)")
     ap.add_argument("--scaling", choices=["weak", "strong"], default="weak",
                     help="weak: --dates per GPU; strong: --dates in total, sharded over ranks")
+    ap.add_argument("--strong-dates", type=int, default=None,
+                    help="global dates of the extra strong-scaling record (default --dates; "
+                         "0 = skip it)")
     ap.add_argument("--stocks", type=int, default=5000)
     ap.add_argument("--industries", type=int, default=31)
     ap.add_argument("--styles", type=int, default=10)
@@ -100,81 +104,109 @@ def main() -> int:
     sdt = torch.float64 if args.storage == "fp64" else torch.float32
     panel = synthetic_panel(D, N, P, Q, seed=1234 + rank, device=dev, missing_frac=0.01,
                             dtype=sdt)
-    # Two output / gather buffers: step i's RCCL all-gather of the factor-return series runs on
-    # the collective stream underneath step i+1's regression (the write of buffer i%2 at step
-    # i+2 first waits for that gather).  Every collective completes inside the timed region.
-    NB = 2 if world > 1 else 1
-    gathered = [torch.empty(world * D, K, dtype=torch.float64, device=dev) for _ in range(NB)] \
-        if world > 1 else None
-    outs = [None] * NB
-    handles = [None] * NB
-    ws = xs_wls_workspace(D, P, Q, dev, N) if use_cuda else None
-    graphs = [None] * NB
-    it = 0
-
-    def regress(b):
-        outs[b] = xs_wls(panel.styles, panel.cap, panel.ret, panel.ind, P,
-                         want_resid=not args.no_resid, refine=True, out=outs[b], workspace=ws)
-
-    def step():
-        nonlocal it
-        b = it % NB
-        it += 1
-        if handles[b] is not None:
-            handles[b].wait()          # buffer b's previous gather has read outs[b].f
-            handles[b] = None
-        if graphs[b] is not None:
-            graphs[b].replay()
-        else:
-            regress(b)
-        if world > 1:
-            handles[b] = dist.all_gather_into_tensor(gathered[b], outs[b].f, async_op=True)
-
-    def drain():
-        for b in range(NB):
-            if handles[b] is not None:
-                handles[b].wait()
-                handles[b] = None
-
-    for b in range(NB):
-        regress(b)
-    if use_cuda and not args.no_graph:
-        # The kernel of a step is captured once per buffer into a HIP graph and replayed: the
-        # same work, without per-launch host overhead.  The RCCL all-gather stays eager.
-        torch.cuda.synchronize(dev)
-        for b in range(NB):
-            graphs[b] = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(graphs[b]):
-                regress(b)
-    out = outs[0]
 
     def sync():
-        drain()
         if use_cuda:
             torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
 
-    # Setup: bring the GPU to its steady-state clocks (a cold MI355X runs the first ~100 steps
-    # ~10 % slower: 0.308 vs 0.278 ms/step measured).  Same step, same count on every rank (the
-    # all-gathers pair up), all before the W warmup steps and the timed region.
-    for _ in range(args.prewarm):
-        step()
-    sync()
-    for _ in range(args.warmup):
-        step()
-    sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    sync()
-    el = time.perf_counter() - t0
-    if use_cuda:
-        torch.cuda.synchronize(dev)
-    elt = torch.tensor([el], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elt, op=dist.ReduceOp.MAX)
-    el = float(elt.item())
+    def make_runner(Dl):
+        """Step closure over the first ``Dl`` dates of the panel (a contiguous view).
+
+        Two output / gather buffers: step i's RCCL all-gather of the factor-return series runs
+        on the collective stream underneath step i+1's regression (the write of buffer i%2 at
+        step i+2 first waits for that gather).  Every collective completes inside the timed
+        region (``drain``)."""
+        sty, cap, ret = panel.styles[:Dl], panel.cap[:Dl], panel.ret[:Dl]
+        ind = None if panel.ind is None else panel.ind[:Dl]
+        NB = 2 if world > 1 else 1
+        gathered = [torch.empty(world * Dl, K, dtype=torch.float64, device=dev)
+                    for _ in range(NB)] if world > 1 else None
+        outs, handles, graphs = [None] * NB, [None] * NB, [None] * NB
+        ws = xs_wls_workspace(Dl, P, Q, dev, N) if use_cuda else None
+        it = [0]
+
+        def regress(b):
+            outs[b] = xs_wls(sty, cap, ret, ind, P, want_resid=not args.no_resid, refine=True,
+                             out=outs[b], workspace=ws)
+
+        def drain():
+            for b in range(NB):
+                if handles[b] is not None:
+                    handles[b].wait()
+                    handles[b] = None
+
+        def step():
+            b = it[0] % NB
+            it[0] += 1
+            if handles[b] is not None:
+                handles[b].wait()          # buffer b's previous gather has read outs[b].f
+                handles[b] = None
+            if graphs[b] is not None:
+                graphs[b].replay()
+            else:
+                regress(b)
+            if world > 1:
+                handles[b] = dist.all_gather_into_tensor(gathered[b], outs[b].f, async_op=True)
+
+        for b in range(NB):
+            regress(b)
+        if use_cuda and not args.no_graph:
+            # The kernel of a step is captured once per buffer into a HIP graph and replayed:
+            # the same work, without per-launch host overhead.  The RCCL all-gather stays eager.
+            torch.cuda.synchronize(dev)
+            for b in range(NB):
+                graphs[b] = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(graphs[b]):
+                    regress(b)
+        return step, drain, outs
+
+    def timed(step, drain, prewarm, warmup, steps):
+        """W untimed warmup steps, then EXACTLY ``steps`` timed steps between barrier +
+        synchronize fences; returns the max over ranks of the elapsed seconds."""
+        for _ in range(prewarm):
+            step()
+        drain()
+        sync()
+        for _ in range(warmup):
+            step()
+        drain()
+        sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        drain()
+        sync()
+        el = time.perf_counter() - t0
+        elt = torch.tensor([el], dtype=torch.float64, device=dev)
+        if world > 1:
+            dist.all_reduce(elt, op=dist.ReduceOp.MAX)
+        return float(elt.item())
+
+    # Setup (prewarm): bring the GPU to its steady-state clocks (a cold MI355X runs the first
+    # ~100 steps ~10 % slower: 0.308 vs 0.278 ms/step measured).  Same step, same count on every
+    # rank (the all-gathers pair up), all before the W warmup steps and the timed region.
+    step, drain, outs = make_runner(D)
+    el = timed(step, drain, args.prewarm, args.warmup, args.steps)
+    out = outs[0]
+
+    # Second, separately reported record: strong scaling of a FIXED global problem
+    # (--strong-dates in total, split over the ranks), so the driver's 1 -> N runs record both
+    # curves.  The headline fields above stay the weak-scaling (or --scaling) loop.
+    strong = None
+    G = args.strong_dates if args.strong_dates is not None else args.dates
+    if G > 0 and args.scaling == "weak":
+        if G % world:
+            raise SystemExit(f"--strong-dates {G} must be divisible by the world size {world}")
+        Ds = G // world
+        if Ds > D:
+            raise SystemExit(f"--strong-dates {G} needs {Ds} dates per rank, the panel has {D}")
+        s_step, s_drain, _ = make_runner(Ds)
+        s_el = timed(s_step, s_drain, max(1, args.prewarm // 4), args.warmup, args.steps)
+        strong = {"global_dates": G, "dates_per_gpu": Ds, "steps": args.steps,
+                  "ms_per_step": round(s_el / args.steps * 1e3, 4),
+                  "value": round(G * args.steps / s_el, 1), "unit": "regressions/s"}
 
     if args.check and rank == 0:
         sl = slice(0, 8)
@@ -200,8 +232,9 @@ def main() -> int:
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": round(value / BASELINE_REG_PER_S, 1),
-            "dtype": "fp64",
+            "dtype": args.storage,
             "data": "synthetic (random-init exposures, lognormal caps, planted factor returns)",
+            "strong": strong,
             "config": {
                 "model": f"Barra CS-WLS: 1 country + {P} SW-L1 industries + {Q} styles, "
                          "industry-neutral constraint",

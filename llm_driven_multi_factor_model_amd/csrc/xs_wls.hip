@@ -10,8 +10,8 @@ int g_mfa_xs_chunks = 0;
 // fp32 and fp64 entry points.
 MFA_API void mfa_xs_set_mode(int mode) { g_mfa_xs_mode = mode; }
 
-// Stock chunks per date for the next calls: 0 = automatic (default; chunked when a launch has
-// fewer than 1024 dates), > 0 = forced chunk count, < 0 = always one workgroup per date.
+// Stock chunks per date for the next calls: 0 = automatic (default: the fused kernel,
+// kXsChunkMinD = 0), > 0 = forced chunk count, < 0 = always one workgroup per date.
 MFA_API void mfa_xs_set_chunks(int S) { g_mfa_xs_chunks = S; }
 
 // Chunks per date the next mfa_xs_wls / mfa_xs_wls_f64 call on (D, N) will use.
@@ -34,7 +34,8 @@ MFA_API size_t mfa_xs_wls_workspace(int D, int N, int P, int Q) {
 // stocks).  Outputs: f [D][1+P+Q] fp64 (country, industries, styles), e [D][N] fp32 specific
 // returns (nullable), r2 [D] fp64, stats [D][Q+2] fp64 = (mu_q, sigma, n_valid) (nullable),
 // status [D] int32 XsStatus bits.  pivot_mode: 0 = last non-empty industry, 1 = reference;
-// | 0x100 = bitwise-deterministic kernel (needs the 8-replica segment table: P <= 59 at Q = 10).
+// | 0x100 = bitwise-deterministic kernel (needs the 8-replica segment table: mfa_xs_det_supported,
+// P <= 57 at Q = 10).
 MFA_API int mfa_xs_wls(const float* X, const float* cap, const float* ret, const int16_t* ind,
                        int D, int N, int P, int Q, int pivot_mode, double tol, double* f,
                        float* e, double* r2, double* stats, int* status, void* ws,

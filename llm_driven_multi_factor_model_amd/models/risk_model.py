@@ -136,14 +136,21 @@ class RiskModel:
         seed = self.cfg.eigen_seed if seed is None else seed
         with self._stage("eigen_adjust"):
             if self.cfg.eigen_shard == "sims":
-                # Simulations sharded over ranks (10k-bootstrap configuration): every rank
-                # rebuilds the Newey-West series of ALL new dates (an O(T K^2) scan, cheaper
-                # than gathering [T, K, K]), runs its block of sims on all of them, and one
-                # all_reduce of the [T, K] bias sums (C5) completes the mean over M.
+                # Simulations sharded over ranks (10k-bootstrap configuration): every rank needs
+                # the Newey-West covariances of ALL new dates, runs its block of sims on all of
+                # them, and one all_reduce of the [T, K] bias sums (C5) completes the mean over M.
                 lo_new = self.T_hist
-                q_nw, tau_nw = self.nw_params  # the (q, tau) newey_west() actually used
-                nw_all = ew_scan.newey_west_series(self._gather_f(), q_nw, tau_nw, lo_new,
-                                                   self.T)
+                if self.cfg.time_scan == "carry":
+                    # each rank scanned only its own dates: gather those blocks (no rescan, no
+                    # factor-return gather), so the SP scan composes with C5 sharding
+                    nw_all = pdist.all_gather_rows(self.nw_cov.contiguous(), self.ctx,
+                                                   self.sizes)
+                else:
+                    # the gathered series is already on every rank: an O(T K^2) rescan is
+                    # cheaper than gathering [T, K, K]
+                    q_nw, tau_nw = self.nw_params  # the (q, tau) newey_west() actually used
+                    nw_all = ew_scan.newey_west_series(self._gather_f(), q_nw, tau_nw, lo_new,
+                                                       self.T)
                 Fh, vb = eigen.eigen_risk_adjust_sharded(
                     nw_all, M=M, scale_coef=scale_coef, T_sim=T_sim, seed=seed,
                     chunk=self.cfg.eigen_chunk, ctx=self.ctx, psd_tol=self.cfg.psd_tol,
@@ -255,8 +262,16 @@ class RiskModel:
         the total number of dates, quirk Q9, as in a full run)."""
         if not isinstance(state, dict):
             state = ckpt.load_state(state)
-        cfg = config or RiskConfig(**state["config"])
-        if ckpt.config_hash(cfg.to_dict()) != state["config_hash"]:
+        stored = dict(state["config"])
+        fv = int(state.get("format_version", ckpt.FORMAT_VERSION))
+        if ckpt.config_hash(stored, fv) != state["config_hash"]:
+            raise ValueError("checkpoint config does not match its hash (corrupt file?)")
+        # fields a format-1 file predates take their defaults; unknown keys are ignored
+        import dataclasses
+        known = {f.name for f in dataclasses.fields(RiskConfig)}
+        saved = RiskConfig(**{k: v for k, v in stored.items() if k in known})
+        cfg = config or saved
+        if ckpt.model_config(cfg.to_dict()) != ckpt.model_config(saved.to_dict()):
             raise ValueError("checkpoint was produced with a different RiskConfig")
         if int(state["K"]) != panel.K or list(state["factor_names"]) != list(panel.factor_names):
             raise ValueError("factor set of the new panel differs from the checkpoint")
@@ -283,16 +298,67 @@ class RiskModel:
 
     # --------------------------------------------------------------- diagnostics
     def eigenfactor_bias(self, which: str = "eigen", start: int = 0, predlen: int = 1):
+        """Eigenfactor bias statistic (``MFM.py:203-204`` runs it with predlen=21 on dates >=
+        1000) of the chosen covariance series over GLOBAL dates t >= ``start`` with
+        t + predlen < T.  Collective: each rank forms the z-scores of its own dates (the
+        realised returns of later dates come from the gathered factor-return series), the z rows
+        are all-gathered in calendar order and the std runs over all of them, so the result is
+        the same on every rank and for every world size."""
         cov = {"nw": self.nw_cov, "eigen": self.eigen_cov, "vra": self.vra_cov}[which]
-        return eigenfactor_bias_stat(cov[start:], self.factor_ret[start:], predlen)
+        if cov is None:
+            raise RuntimeError(f"covariance series {which!r} not computed yet")
+        F = self._gather_f()                     # [T, K] with history first
+        T, lo, D = self.T, self.t_lo, self.panel.D
+        a, b = max(start, lo), min(lo + D, T - predlen)
+        z = torch.empty(0, self.K, dtype=torch.float64, device=self.device)
+        if b > a:
+            z = eigenfactor_z(cov[a - lo:b - lo], F[a + 1:b + predlen], predlen)
+        Z = pdist.all_gather_rows(z.contiguous(), self.ctx)
+        if Z.shape[0] == 0:
+            return torch.full((self.K,), float("nan"), dtype=torch.float64)
+        Z = Z[torch.isfinite(Z).all(-1)]
+        return Z.std(0, unbiased=False)
 
-    def specific_risk_shrunk(self, window: int = 252, ngroup: int = 10, q: float = 1.0):
-        """Cap-decile Bayesian shrinkage of trailing specific volatility (utils.bayes_shrink)."""
+    def specific_vol_series(self, window: int = 252, min_periods: int = 1) -> torch.Tensor:
+        """[D_loc, N] trailing specific volatility, point in time: for date t the ddof-0 std of
+        each stock's specific returns over the ``window`` dates ENDING at t (dates before t
+        only; no later date enters).  The window crosses rank boundaries through a halo of the
+        preceding window-1 rows (one collective), and every window is summed in the same fixed
+        order whatever the sharding, so the result is bitwise rank-invariant.  Checkpoints keep
+        no specific returns: after a resume the first window-1 new dates see only new dates."""
+        e = self.specific_ret.double()
+        D = e.shape[0]
+        h = window - 1
+        ext = torch.cat([pdist.halo_prev_rows(e, h, self.ctx, self.sizes), e])
+        ok = torch.isfinite(ext)
+        x = torch.where(ok, ext, torch.zeros((), dtype=torch.float64, device=e.device))
+        okd = ok.double()
+        n = torch.zeros_like(e)
+        s1 = torch.zeros_like(e)
+        s2 = torch.zeros_like(e)
+        for j in range(window):  # fixed summation order: newest date first
+            sl = slice(h - j, h - j + D)
+            n += okd[sl]
+            s1 += x[sl]
+            s2 += x[sl] * x[sl]
+        mean = s1 / n
+        var = s2 / n - mean * mean
+        vol = torch.sqrt(torch.clamp(var, min=0.0))
+        return torch.where(n >= max(1, min_periods), vol,
+                           torch.full_like(vol, float("nan")))
+
+    def specific_risk_shrunk(self, window: int = 252, ngroup: int = 10, q: float = 1.0,
+                             per_date: bool = True):
+        """Cap-decile Bayesian shrinkage (``utils.bayes_shrink``, utils.py:153-168) of the
+        point-in-time trailing specific volatility.  ``per_date``: [D_loc, N], date t shrunk
+        with its own window and caps; otherwise [N] of the LAST global date, on every rank
+        (broadcast from the rank that owns it).  Collective in distributed mode."""
         from ..ops.xs_reduce import bayes_shrink
-        e = self.specific_ret[-window:].double()
-        vol = torch.sqrt(torch.nanmean(e * e, 0) - torch.nanmean(e, 0) ** 2)
-        cap = self.panel.cap[-1].double()
-        return bayes_shrink(vol, cap, ngroup, q)
+        vol = self.specific_vol_series(window)
+        s = bayes_shrink(vol, self.panel.cap.double(), ngroup, q).double()
+        if per_date:
+            return s
+        return pdist.broadcast_last_row(s, self.ctx, self.sizes)
 
     def risk_attribution(self, h: torch.Tensor, which: str = "vra",
                          specific_vol: torch.Tensor | str | None = "shrunk"):
@@ -300,7 +366,8 @@ class RiskModel:
         rank's dates against the chosen covariance series (``nw`` / ``eigen`` / ``vra``).
 
         ``specific_vol``: per-stock specific volatility [N] or [D_loc, N]; ``"shrunk"`` uses
-        :meth:`specific_risk_shrunk` (cap-decile Bayesian shrinkage of trailing residual vol);
+        :meth:`specific_risk_shrunk` (cap-decile Bayesian shrinkage of each date's own trailing
+        residual vol: point in time, identical for every world size; collective);
         None ignores specific risk.  Returns :class:`ops.attribution.RiskAttribution`.
         """
         from ..ops import attribution as attr
@@ -338,6 +405,21 @@ class RiskModel:
         return d
 
 
+def eigenfactor_z(cov: torch.Tensor, fwd: torch.Tensor, predlen: int) -> torch.Tensor:
+    """z-scores [n, K] of the eigen-factor portfolios of ``cov`` [n, K, K] (utils.py:103-110):
+    U / colsum(U), sigma = sqrt(predlen diag(U^T cov U)), realised = U^T (prod(1 + f) - 1) over
+    the next predlen dates.  ``fwd`` [n + predlen - 1, K] holds the factor returns of the
+    dates after cov's first date."""
+    cov = cov.double()
+    n = cov.shape[0]
+    w, U = eigen.eigh(cov)
+    U = U / U.sum(-2, keepdim=True)
+    sig = torch.sqrt(predlen * torch.einsum("dki,dkl,dli->di", U, cov, U))
+    growth = (fwd.double()[:n + predlen - 1] + 1.0).unfold(0, predlen, 1).prod(-1) - 1.0  # [n, K]
+    r = torch.einsum("dki,dk->di", U, growth)
+    return r / sig
+
+
 def eigenfactor_bias_stat(cov: torch.Tensor, ret: torch.Tensor, predlen: int = 1) -> torch.Tensor:
     """Bias statistic of eigen-factor portfolios (``utils.eigenfactor_bias_stat``, utils.py:97-117).
 
@@ -351,13 +433,7 @@ def eigenfactor_bias_stat(cov: torch.Tensor, ret: torch.Tensor, predlen: int = 1
     n = cov.shape[0] - predlen
     if n <= 0:
         return torch.full((cov.shape[-1],), float("nan"), dtype=torch.float64)
-    w, U = eigen.eigh(cov[:n])
-    U = U / U.sum(-2, keepdim=True)
-    sig = torch.sqrt(predlen * torch.einsum("dki,dkl,dli->di", U, cov[:n], U))
-    # realised compounded return over the next predlen dates, all n dates at once
-    growth = (ret[1:1 + n + predlen - 1] + 1.0).unfold(0, predlen, 1).prod(-1) - 1.0   # [n, K]
-    r = torch.einsum("dki,dk->di", U, growth)
-    z = r / sig
+    z = eigenfactor_z(cov[:n], ret[1:n + predlen], predlen)
     ok = torch.isfinite(z).all(-1)
     z = z[ok]
     return z.std(0, unbiased=False)

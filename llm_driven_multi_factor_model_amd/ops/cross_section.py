@@ -93,10 +93,10 @@ def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Ten
     The GPU kernels need N % 8 == 0 (16-byte rows for the LDS-DMA ring); other N are padded
     here with absent stocks (``ind = -1``), which costs a copy — keep panels padded.
     ``deterministic`` (default: on whenever the kernel supports it, i.e. the 8-replica segment
-    table fits: P <= 53 industries at Q = 10) selects the bitwise-reproducible kernel: each LDS
-    segment replica is owned by one wave and the wave partials are summed in a fixed order.  It
-    costs 0-3 % (profiles/r02_xs_deterministic.md); ``False`` shares the replicas across waves
-    (reproducible to rounding only).
+    table fits, ``mfa_xs_det_supported``: P <= 57 industries at Q = 10) selects the
+    bitwise-reproducible kernel: each LDS segment replica is owned by one wave and the wave
+    partials are summed in a fixed order.  It costs 0-3 % (profiles/r02_xs_deterministic.md);
+    ``False`` shares the replicas across waves (reproducible to rounding only).
     """
     D, Q, N = _validate(X, cap, ret, ind, P)
     K = 1 + P + Q
@@ -131,8 +131,13 @@ def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Ten
     if resid_buf is not None and Np != N:
         resid_buf = torch.empty(D, Np, dtype=dt, device=dev)
     need = _native.query("mfa_xs_wls_workspace", D, Np, P, Q)
-    if workspace is None or workspace.numel() < need:
+    if workspace is None:
         workspace = torch.empty(need, dtype=torch.uint8, device=dev)
+    elif workspace.numel() < need:
+        # a silently reallocated buffer would defeat reuse and allocate inside captured graphs
+        raise ValueError(f"xs_wls: workspace of {workspace.numel()} B is too small for D={D}, "
+                         f"N={N}, P={P}, Q={Q} ({need} B): size it with xs_wls_workspace(D, P, "
+                         "Q, device, N)")
     dev_refine = refine and K <= REFINE_MAX_K
     if deterministic is None:
         deterministic = bool(_native.lib().mfa_xs_det_supported(P, Q))
@@ -151,9 +156,10 @@ def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Ten
     return out
 
 
-def xs_wls_workspace(D: int, P: int, Q: int, device, N: int = 5000) -> torch.Tensor:
+def xs_wls_workspace(D: int, P: int, Q: int, device, N: int) -> torch.Tensor:
     """Preallocated kernel workspace for repeated :func:`xs_wls` calls on the same shapes
-    (its size depends on the path, i.e. on the stock chunks per date chosen for (D, N))."""
+    (its size depends on N -- per-tile validity bits -- and on the path, i.e. on the stock
+    chunks per date chosen for (D, N)).  :func:`xs_wls` refuses a workspace that is too small."""
     Np = (N + 7) // 8 * 8
     return torch.empty(_native.query("mfa_xs_wls_workspace", D, Np, P, Q), dtype=torch.uint8,
                        device=device)

@@ -131,6 +131,47 @@ def all_gather_rows(x: torch.Tensor, ctx: DistContext | None = None,
     return torch.cat([out[r * mx:r * mx + sizes[r]] for r in range(ctx.world)])
 
 
+def halo_prev_rows(x: torch.Tensor, h: int, ctx: DistContext | None = None,
+                   sizes: list[int] | None = None) -> torch.Tensor:
+    """The ``h`` rows of the GLOBAL series that precede this rank's block (rank order =
+    calendar order), NaN before the first global row: a rolling window's halo across rank
+    boundaries.  One collective: every rank contributes its last min(h, D_r) rows, so a block
+    shorter than the halo is covered by the ranks before it.  Float tensors only."""
+    ctx = ctx or context()
+    shape = (h,) + tuple(x.shape[1:])
+    nan = torch.full(shape, float("nan"), dtype=x.dtype, device=x.device)
+    if h <= 0:
+        return nan[:0]
+    if not ctx.enabled:
+        return nan
+    if sizes is None:
+        sizes = shard_sizes(x.shape[0], ctx)
+    k = min(h, x.shape[0])
+    tail = nan.clone()
+    if k:
+        tail[h - k:] = x[x.shape[0] - k:]
+    out = torch.empty((ctx.world * h,) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.all_gather_into_tensor(out, tail.contiguous())
+    prev = [out[r * h + h - min(h, sizes[r]):(r + 1) * h] for r in range(ctx.rank)]
+    got = torch.cat([nan] + prev)[-h:]
+    return got.contiguous()
+
+
+def broadcast_last_row(x: torch.Tensor, ctx: DistContext | None = None,
+                       sizes: list[int] | None = None) -> torch.Tensor:
+    """Row ``x[-1]`` of the rank that owns the LAST global row, on every rank."""
+    ctx = ctx or context()
+    if not ctx.enabled:
+        return x[-1]
+    if sizes is None:
+        sizes = shard_sizes(x.shape[0], ctx)
+    owner = max(r for r in range(ctx.world) if sizes[r] > 0)
+    row = x[-1].contiguous().clone() if ctx.rank == owner else \
+        torch.empty(tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
+    dist.broadcast(row, src=owner)
+    return row
+
+
 def gather_to_root(x: torch.Tensor, ctx: DistContext | None = None) -> torch.Tensor | None:
     """Rows of every rank concatenated on rank 0 (None elsewhere)."""
     ctx = ctx or context()

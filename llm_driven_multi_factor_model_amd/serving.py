@@ -46,7 +46,7 @@ class RiskService:
         self.X = torch.nan_to_num(self.X, nan=0.0)
         self.F = cov[d].to(torch.float64).contiguous()                  # [K, K]
         if specific_vol is None:
-            specific_vol = model.specific_risk_shrunk()
+            specific_vol = model.specific_risk_shrunk()[d]   # point in time: date d's own
         s = specific_vol.to(self.device, torch.float64)
         self.s2 = torch.nan_to_num(s * s, nan=0.0)                     # [N]
         self.F_ok = bool(torch.isfinite(self.F).all())

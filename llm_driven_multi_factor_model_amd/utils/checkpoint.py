@@ -12,6 +12,13 @@ and :meth:`RiskModel.resume` continues on a panel of NEW dates without re-regres
 re-adjusting the old ones.  Files are written with ``torch.save`` of tensors, strings and
 plain containers only, and read back with ``torch.load(weights_only=True)`` (nothing from the
 file is executed).  A config hash guards against resuming with different parameters.
+
+Only MODEL parameters take part in that guard.  Execution-only settings (how the same numbers
+are computed: the time-axis scan mode, the deterministic kernel, how the eigen sims are sharded
+and chunked) may differ between the saved run and the resumed one, since every mode gives the
+same results (bitwise, or to ~1e-13 for ``time_scan``).  Format 1 (round-2 files) hashed the
+whole config dict; such files still load: their hash is verified the old way, and fields they
+predate take their defaults.
 """
 from __future__ import annotations
 
@@ -21,11 +28,26 @@ from pathlib import Path
 
 import torch
 
-FORMAT_VERSION = 1
+FORMAT_VERSION = 2
+READABLE_FORMATS = (1, 2)
+
+# RiskConfig fields that choose HOW a result is computed, not WHAT is computed
+EXEC_KEYS = frozenset({"time_scan", "deterministic", "eigen_chunk", "eigen_shard"})
 
 
-def config_hash(cfg: dict) -> str:
-    return hashlib.sha256(json.dumps(cfg, sort_keys=True, default=str).encode()).hexdigest()[:16]
+def model_config(cfg: dict) -> dict:
+    """The model-defining part of a config dict (execution-only keys removed)."""
+    return {k: v for k, v in cfg.items() if k not in EXEC_KEYS}
+
+
+def _sha(d: dict) -> str:
+    return hashlib.sha256(json.dumps(d, sort_keys=True, default=str).encode()).hexdigest()[:16]
+
+
+def config_hash(cfg: dict, format_version: int = FORMAT_VERSION) -> str:
+    """Hash of a config dict as written by checkpoint format ``format_version`` (1: the whole
+    dict; 2: its model keys only)."""
+    return _sha(cfg if format_version == 1 else model_config(cfg))
 
 
 def save_state(state: dict, path: str | Path) -> Path:
@@ -41,6 +63,6 @@ def save_state(state: dict, path: str | Path) -> Path:
 
 def load_state(path: str | Path) -> dict:
     state = torch.load(Path(path), map_location="cpu", weights_only=True)
-    if state.get("format_version") != FORMAT_VERSION:
+    if state.get("format_version") not in READABLE_FORMATS:
         raise ValueError(f"unsupported checkpoint format {state.get('format_version')!r}")
     return state

@@ -29,7 +29,8 @@ class RiskConfig:
                                   # "sims": ranks split the M sims of every date + all_reduce (C5)
     eigen_chunk: int = 256        # sims per launch in "sims" mode (bounds the [D, chunk, K] buffer)
     deterministic: bool | None = None  # bitwise-reproducible CS-WLS kernel (wave-owned LDS
-                                       # replicas); None = whenever supported (P <= 53 at Q = 10)
+                                       # replicas); None = whenever supported
+                                       # (mfa_xs_det_supported: P <= 57 at Q = 10)
     time_scan: str = "gather"     # time-axis stages (Newey-West, VRA) across date shards:
                                   # "gather": all-gather the O(T K) series, every rank scans the
                                   # prefix (bitwise identical to one GPU); "carry": each rank

@@ -41,6 +41,15 @@ def test_bench_single_process_json():
     assert r["metric"].startswith("cross-sectional WLS regressions/sec")
     assert r["n_gpus"] == 1 and r["steps"] == 2 and r["scaling"] == "weak"
     assert r["config"]["global_batch"] == 6 and r["value"] > 0
+    assert r["dtype"] == "fp64"
+    s = r["strong"]  # separately reported fixed-global-problem loop
+    assert s["global_dates"] == 6 and s["dates_per_gpu"] == 6 and s["value"] > 0
+    assert abs(s["value"] - 6 * 2 / (s["ms_per_step"] * 2 / 1e3)) / s["value"] < 0.02
+
+
+def test_bench_dtype_follows_storage():
+    r = _run(1, ["--storage", "fp32"])
+    assert r["dtype"] == "fp32" and r["config"]["storage"] == "fp32"
 
 
 def test_bench_two_ranks_aggregate():
@@ -48,6 +57,8 @@ def test_bench_two_ranks_aggregate():
     assert r["n_gpus"] == 2
     assert r["config"]["global_batch"] == 12 and r["config"]["parallelism"] == "dp2"
     assert abs(r["value"] - 12 * 2 / (r["ms_per_step"] * 2 / 1e3)) / r["value"] < 0.02
+    s = r["strong"]  # 6 global dates = 3 per rank; headline fields untouched
+    assert s["global_dates"] == 6 and s["dates_per_gpu"] == 3 and s["value"] > 0
 
 
 def test_bench_strong_scaling_two_ranks():

@@ -45,6 +45,49 @@ def test_resume_equals_full_run(tmp_path, oos, scan):
     torch.testing.assert_close(st2["factor_ret"], full._gather_f(), rtol=0, atol=0)
 
 
+def test_resume_execution_settings_may_change(tmp_path):
+    """time_scan / deterministic / eigen sharding choose HOW, not WHAT: a run saved with one
+    mode resumes under another."""
+    p = synthetic_panel(30, 48, P=3, Q=2, seed=9)
+    T1 = 20
+    m = RiskModel(p.slice_dates(0, T1), _cfg(time_scan="gather")).run()
+    st = m.state_dict()
+    rest = p.slice_dates(T1, p.D)
+    rest = type(rest)(**{**rest.__dict__, "date_offset": 0})
+    for over in (dict(time_scan="carry"), dict(deterministic=False), dict(eigen_chunk=64)):
+        RiskModel.resume(st, rest, config=_cfg(**over))
+
+
+def test_resume_format1_checkpoint(tmp_path):
+    """A checkpoint in the round-2 format (version 1: hash over the WHOLE config dict, no
+    ``time_scan`` key, ``deterministic`` False) still resumes, with the CLI's preset config."""
+    p = synthetic_panel(30, 48, P=3, Q=2, seed=11)
+    T1 = 20
+    m = RiskModel(p.slice_dates(0, T1), _cfg())
+    m.T = p.D  # the eigen simulation length follows the TOTAL number of dates (quirk Q9)
+    m.run()
+    st = m.state_dict()
+    old_cfg = {k: v for k, v in _cfg().to_dict().items() if k != "time_scan"}
+    old_cfg["deterministic"] = False
+    st["config"] = old_cfg
+    st["config_hash"] = ckpt.config_hash(old_cfg, 1)
+    st["format_version"] = 1
+    path = tmp_path / "v1.ckpt"
+    torch.save({k: (v.cpu() if torch.is_tensor(v) else v) for k, v in st.items()}, path)
+    loaded = ckpt.load_state(path)
+    assert loaded["format_version"] == 1
+    rest = p.slice_dates(T1, p.D)
+    rest = type(rest)(**{**rest.__dict__, "date_offset": 0})
+    full = RiskModel(p, _cfg()).run()
+    m2 = RiskModel.resume(loaded, rest, config=_cfg(time_scan="carry")).run()
+    torch.testing.assert_close(m2.vra_cov, full.vra_cov[T1:], rtol=1e-12, atol=1e-18,
+                               equal_nan=True)
+    # a tampered model key is still refused
+    bad = dict(loaded, config=dict(old_cfg, nw_lags=1))
+    with pytest.raises(ValueError, match="hash"):
+        RiskModel.resume(bad, rest)
+
+
 def test_resume_guards(tmp_path):
     p = synthetic_panel(20, 48, P=3, Q=2, seed=5)
     m = RiskModel(p.slice_dates(0, 12), _cfg()).run()

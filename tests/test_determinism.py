@@ -1,7 +1,7 @@
 """Run-twice bitwise determinism of the whole risk model.
 
 With the default ``RiskConfig`` (``deterministic=None``: on whenever the CS-WLS kernel supports
-it, P <= 53 at Q = 10) every stage is order-fixed: the CS-WLS kernel's wave-owned
+it, mfa_xs_det_supported: P <= 57 at Q = 10) every stage is order-fixed: the CS-WLS kernel's wave-owned
 LDS replicas, the blocked Newey-West / VRA scans (no atomics), per-(date, sim) Jacobi solves
 with Philox draws keyed by the sim index, and in-order bias sums.  Two runs must agree bit for
 bit, NaN positions included.

@@ -125,6 +125,9 @@ def test_last_industry_empty_pivot_modes():
     (4, 1000, 28, 16, 0.0, 1),
     (3, 64, 3, 1, 0.0, 0),
     (5, 600, 100, 8, 0.01, 2),
+    # Q > 10 runs the 1-wave-per-SIMD register budget (MFA_XS_WPE_BIGQ)
+    (4, 1500, 31, 11, 0.01, 1),
+    (4, 1500, 31, 12, 0.01, 1),
 ])
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
 def test_kernel_matches_oracle(cuda, D, N, P, Q, miss, empty, dtype):
@@ -168,8 +171,9 @@ def test_device_pinv_refine_matches_oracle(cuda):
 
 @pytest.mark.gpu
 def test_device_pinv_refine_more_dates_than_grid(cuda):
-    """Every one of 1100 dates flagged near-singular: the grid-stride refine pass (512
-    workgroups) re-solves dates 0, 511, 512, 1023, 1024 and 1099 like the pinv oracle."""
+    """Every one of 1100 dates flagged near-singular: the refine pass (one workgroup per date,
+    ``xs_refine_kernel`` launched with dim3(D)) re-solves dates 0, 511, 512, 1023, 1024 and 1099
+    like the pinv oracle."""
     p = _degenerate_panel(D=1100, N=200, P=6, Q=4, seed=9)
     g = p.to(cuda)
     out = X.xs_wls(g.styles, g.cap, g.ret, g.ind, p.P)
