@@ -47,7 +47,7 @@ def register(name: str, argtypes: list) -> None:
     if _lib is not None:
         fn = getattr(_lib, name)
         fn.argtypes = argtypes
-        fn.restype = C.c_size_t if name.endswith("_workspace") or name.endswith("_bytes") else C.c_int
+        fn.restype = C.c_size_t if name.endswith(("_workspace", "_bytes", "_doubles")) else C.c_int
 
 
 def _load() -> C.CDLL:
@@ -66,7 +66,7 @@ def _load() -> C.CDLL:
         for name, argt in _SIGS.items():
             fn = getattr(lib, name)
             fn.argtypes = argt
-            fn.restype = C.c_size_t if name.endswith("_workspace") or name.endswith("_bytes") else C.c_int
+            fn.restype = C.c_size_t if name.endswith(("_workspace", "_bytes", "_doubles")) else C.c_int
         _lib = lib
         return lib
 

@@ -120,21 +120,56 @@ typedef double f64x4 __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ double u01_53(unsigned hi, unsigned lo) {  // (0, 1]
   return ((double)(((unsigned long long)(hi >> 5) << 26) | (lo >> 6)) + 1.0) * (1.0 / 9007199254740992.0);
 }
+// Grid (M sims x C time chunks): wave (m, c) draws the 64-row time blocks [b0, b1) of sim
+// m0 + m.  C == 1 writes C_z directly; C > 1 writes its raw partial sums (the 10 MFMA tiles +
+// the column sums, lane-major) to `part` [M][C][kCovPart] for mc_cov_reduce_kernel, which adds
+// the C chunks in chunk order (deterministic) and centres: the same draws, and with ~20 chunks
+// per sim the 100-sim launch fills the chip instead of 100 of its 256 CUs.
+constexpr int kCovTiles = 10;
+constexpr int kCovPart = kCovTiles * 4 * 64 + 64;  // doubles per (sim, chunk) partial
+constexpr int TI_[kCovTiles] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3};
+constexpr int TJ_[kCovTiles] = {0, 1, 2, 3, 1, 2, 3, 2, 3, 3};
+
+__device__ __forceinline__ void mc_cov_finish(const f64x4 (&acc)[kCovTiles], const double* colsum,
+                                              int K, int T, double* __restrict__ C) {
+  const int lane = threadIdx.x, r16 = lane & 15, k4 = lane >> 4;
+  const double invT1 = 1.0 / (double)(T - 1), invT = 1.0 / (double)T;
+#pragma unroll
+  for (int t = 0; t < kCovTiles; ++t) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      // 16x16x4 f64 output layout (tools/probes/mfma64_probe.hip): register e of lane l holds
+      // D[(l >> 4) + 4 e][l & 15]; a diagonal tile writes its upper triangle (both halves)
+      const int i = 16 * TI_[t] + k4 + 4 * e, j = 16 * TJ_[t] + r16;
+      if (i < K && j < K && (TI_[t] != TJ_[t] || i <= j)) {
+        const double v = (acc[t][e] - colsum[i] * colsum[j] * invT) * invT1;
+        C[i * K + j] = v;
+        C[j * K + i] = v;
+      }
+    }
+  }
+}
+
 __global__ __launch_bounds__(64) void mc_cov_kernel(int K, int T, unsigned long long seed,
-                                                    int m0, double* __restrict__ Cz) {
-  // simulation m0 + blockIdx.x: the Philox stream depends only on (seed, global sim index), so
-  // any partition of the sims over chunks / ranks draws exactly the single-run covariances
-  const int m = m0 + blockIdx.x, lane = threadIdx.x;
+                                                    int m0, int C, double* __restrict__ Cz,
+                                                    double* __restrict__ part) {
+  // simulation m0 + blockIdx.x / C: the Philox stream depends only on (seed, global sim index,
+  // time row), so any partition of the sims over chunks / ranks and of the time axis over
+  // waves draws exactly the single-run normals
+  const int mi = blockIdx.x / C, c = blockIdx.x - mi * C;
+  const int m = m0 + mi, lane = threadIdx.x;
+  const int nblk = (T + 63) / 64;
+  const int per = (nblk + C - 1) / C;
+  const int b0 = c * per, b1 = min(nblk, b0 + per);
   __shared__ double Z[64][66];  // 64 time rows x 64 (padded) factors; +2 pad: conflict-free
   __shared__ double colsum[64];
   const int r16 = lane & 15, k4 = lane >> 4;
-  constexpr int TI[10] = {0, 0, 0, 0, 1, 1, 1, 2, 2, 3};
-  constexpr int TJ[10] = {0, 1, 2, 3, 1, 2, 3, 2, 3, 3};
-  f64x4 acc[10];
+  f64x4 acc[kCovTiles];
 #pragma unroll
-  for (int t = 0; t < 10; ++t) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
+  for (int t = 0; t < kCovTiles; ++t) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
   double cs = 0.0;  // column sum for factor `lane`
-  for (int t0 = 0; t0 < T; t0 += 64) {
+  for (int blk = b0; blk < b1; ++blk) {
+    const int t0 = blk * 64;
     // draw a 64 x 64 block: row = time, col = factor (zero beyond K / T); one Philox call per
     // (time, factor pair) -> two 53-bit uniforms -> one Box-Muller pair
 #pragma unroll 4
@@ -155,30 +190,57 @@ __global__ __launch_bounds__(64) void mc_cov_kernel(int K, int T, unsigned long 
 #pragma unroll
       for (int i = 0; i < 4; ++i) a[i] = Z[k + k4][16 * i + r16];
 #pragma unroll
-      for (int t = 0; t < 10; ++t)
-        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[TI[t]], a[TJ[t]], acc[t], 0, 0, 0);
+      for (int t = 0; t < kCovTiles; ++t)
+        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[TI_[t]], a[TJ_[t]], acc[t], 0, 0, 0);
     }
     for (int r = 0; r < 64; ++r) cs += Z[r][lane];
     wsync();
   }
+  if (C > 1) {  // raw partials, lane-major: [t][e][lane], then the column sums
+    double* pp = part + (size_t)blockIdx.x * kCovPart;
+#pragma unroll
+    for (int t = 0; t < kCovTiles; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pp[(t * 4 + e) * 64 + lane] = acc[t][e];
+    pp[kCovTiles * 4 * 64 + lane] = cs;
+    return;
+  }
   colsum[lane] = cs;
   wsync();
-  double* C = Cz + (size_t)blockIdx.x * K * K;
-  const double invT1 = 1.0 / (double)(T - 1), invT = 1.0 / (double)T;
+  mc_cov_finish(acc, colsum, K, T, Cz + (size_t)mi * K * K);
+}
+
+// Sum of the C time-chunk partials of each sim in chunk order, then the centring.
+__global__ __launch_bounds__(64) void mc_cov_reduce_kernel(int K, int T, int C,
+                                                           const double* __restrict__ part,
+                                                           double* __restrict__ Cz) {
+  const int mi = blockIdx.x, lane = threadIdx.x;
+  __shared__ double colsum[64];
+  f64x4 acc[kCovTiles];
 #pragma unroll
-  for (int t = 0; t < 10; ++t) {
+  for (int t = 0; t < kCovTiles; ++t) acc[t] = f64x4{0.0, 0.0, 0.0, 0.0};
+  double cs = 0.0;
+  for (int c = 0; c < C; ++c) {
+    const double* pp = part + ((size_t)mi * C + c) * kCovPart;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      // 16x16x4 f64 output layout (tools/probes/mfma64_probe.hip): register e of lane l holds
-      // D[(l >> 4) + 4 e][l & 15]; a diagonal tile writes its upper triangle (both halves)
-      const int i = 16 * TI[t] + k4 + 4 * e, j = 16 * TJ[t] + r16;
-      if (i < K && j < K && (TI[t] != TJ[t] || i <= j)) {
-        const double v = (acc[t][e] - colsum[i] * colsum[j] * invT) * invT1;
-        C[i * K + j] = v;
-        C[j * K + i] = v;
-      }
-    }
+    for (int t = 0; t < kCovTiles; ++t)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[t][e] += pp[(t * 4 + e) * 64 + lane];
+    cs += pp[kCovTiles * 4 * 64 + lane];
   }
+  colsum[lane] = cs;
+  wsync();
+  mc_cov_finish(acc, colsum, K, T, Cz + (size_t)mi * K * K);
+}
+
+// time chunks per sim: ~2048 waves in flight, at least 2 time blocks per wave
+inline int mc_cov_chunks(int M, int T) {
+  const int nblk = (T + 63) / 64;
+  int C = (2048 + M - 1) / M;
+  const int cmax = nblk / 2 > 1 ? nblk / 2 : 1;
+  C = C < 1 ? 1 : (C > cmax ? cmax : C);
+  const int per = (nblk + C - 1) / C;
+  return (nblk + per - 1) / per;  // no empty trailing chunk
 }
 
 // ---------------- pair-block Jacobi for the bias statistic ----------------
@@ -1257,7 +1319,8 @@ MFA_API int mfa_eigh_batched(const double* A, int B, int K, int max_sweeps, doub
 MFA_API int mfa_mc_cov(int M, int K, int T, unsigned long long seed, double* Cz, void* stream) {
   if (M <= 0) return 0;
   if (K < 1 || K > 64 || T < 2) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(mc_cov_kernel, dim3(M), dim3(64), 0, (hipStream_t)stream, K, T, seed, 0, Cz);
+  hipLaunchKernelGGL(mc_cov_kernel, dim3(M), dim3(64), 0, (hipStream_t)stream, K, T, seed, 0, 1,
+                     Cz, (double*)nullptr);
   return (int)hipGetLastError();
 }
 
@@ -1266,7 +1329,28 @@ MFA_API int mfa_mc_cov_range(int M, int m0, int K, int T, unsigned long long see
                              void* stream) {
   if (M <= 0) return 0;
   if (K < 1 || K > 64 || T < 2 || m0 < 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(mc_cov_kernel, dim3(M), dim3(64), 0, (hipStream_t)stream, K, T, seed, m0, Cz);
+  hipLaunchKernelGGL(mc_cov_kernel, dim3(M), dim3(64), 0, (hipStream_t)stream, K, T, seed, m0, 1,
+                     Cz, (double*)nullptr);
+  return (int)hipGetLastError();
+}
+
+// Scratch doubles mfa_mc_cov_range_ws needs for (M, T) (0: single-pass launch).
+MFA_API size_t mfa_mc_cov_ws_doubles(int M, int T) {
+  const int C = mc_cov_chunks(M, T);
+  return C > 1 ? (size_t)M * C * kCovPart : 0;
+}
+
+// As mfa_mc_cov_range with the time axis split over ~2048 waves (partials in `ws`, summed in
+// chunk order by a second launch).
+MFA_API int mfa_mc_cov_range_ws(int M, int m0, int K, int T, unsigned long long seed, double* ws,
+                                double* Cz, void* stream) {
+  if (M <= 0) return 0;
+  if (K < 1 || K > 64 || T < 2 || m0 < 0) return (int)hipErrorInvalidValue;
+  const int C = mc_cov_chunks(M, T);
+  hipStream_t s = (hipStream_t)stream;
+  if (C > 1 && ws == nullptr) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(mc_cov_kernel, dim3(M * C), dim3(64), 0, s, K, T, seed, m0, C, Cz, ws);
+  if (C > 1) hipLaunchKernelGGL(mc_cov_reduce_kernel, dim3(M), dim3(64), 0, s, K, T, C, ws, Cz);
   return (int)hipGetLastError();
 }
 

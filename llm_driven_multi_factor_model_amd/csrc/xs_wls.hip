@@ -86,5 +86,14 @@ MFA_API int mfa_xs_resid_sums(const float* X, const float* cap, const float* ret
                                (double*)coef, nullptr, (int*)status, e, sums, stream);
 }
 
+// Device pseudo-inverse of the dates `status` flags near-singular, from their (summed) raw
+// moments: rewrites f [D][1+P+Q], coef [D][Q+1+P] and status in place (stock-sharded path,
+// after the moments all-reduce and mfa_xs_solve; no host synchronisation).  Any K.
+MFA_API int mfa_xs_refine_coef(const double* mom, int D, int P, int Q, int pivot_mode, double* f,
+                               double* coef, int* status, void* stream) {
+  return split_dispatch<float>(3, nullptr, nullptr, nullptr, nullptr, D, 0, P, Q, pivot_mode, 0.0,
+                               (double*)mom, f, coef, nullptr, status, nullptr, nullptr, stream);
+}
+
 // Bytes per date of the raw-moment layout (msize doubles).
 MFA_API size_t mfa_xs_moments_bytes(int P, int Q) { return xs_moments_bytes(P, Q); }

@@ -1480,7 +1480,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Q <= 10 ? 2
 // on the singular values |lambda|).  f = R g, then the whole workgroup redoes the date's
 // specific returns and R^2.
 // ------------------------------------------------------------------------------------------
-constexpr int kXsRefineMaxK = 64;
+constexpr int kXsRefineMaxK = 64;   // full-matrix Jacobi pinv up to here; structured above
 
 template <int Q>
 __host__ __device__ constexpr size_t refine_lds_doubles(int P) {
@@ -1490,36 +1490,339 @@ __host__ __device__ constexpr size_t refine_lds_doubles(int P) {
          4 * (size_t)Kr + (Q + 4);
 }
 
-template <int Q, typename T>
-__global__ __launch_bounds__(256) void xs_refine_kernel(
-    const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
-    const int16_t* __restrict__ ind, int N, int P, int pivot_mode, int S,
-    const double* __restrict__ mom, double* __restrict__ fout, T* __restrict__ eout,
-    double* __restrict__ r2out, int* __restrict__ status) {
+// ------------------------------------------------------------------------------------------
+// Structured pseudo-inverse for ANY K (industries up to 128): pinv semantics of
+// CrossSection.py:76,98 without forming the Kr x Kr matrix.  After the constraint the normal
+// matrix is M = [[A_I, B], [B^T, C]] with the industry block A_I = diag(W) + rho a a^T over the
+// active non-pivot industries (positive definite; exactly-empty industries are zero rows/cols
+// and get f = 0, as pinv gives them), B[j][u] = m_j[u] and the dense block C over
+// [country | z-styles] (ND = Q + 1 columns).  The normal equations are consistent (rhs in
+// range(M)), so every near-null direction of M lies in the dense block's Schur complement S:
+//   null(M) = { [-A_I^{-1} B n ; n] : n in null(S) }.
+// The wave eigen-decomposes S (ND x ND, Jacobi), keeps eigenpair (mu_k, v_k) unless its
+// Rayleigh quotient on M, mu_k / (1 + |A_I^{-1} B v_k|^2), is <= 1e-15 lambda_max(M) (numpy's
+// pinv rcond; lambda_max by power iteration on the structured M), solves the kept part
+// (x2 = sum v v^T b~ / mu, x1 = A_I^{-1}(b1 - B x2)) and projects the result orthogonally to
+// the cut null directions: the minimum-norm solution pinv(M) b.  O(P ND^2) work in one wave.
+// ------------------------------------------------------------------------------------------
+template <int Q>
+__host__ __device__ constexpr size_t refine_struct_lds_doubles(int P) {
+  constexpr int ND = Q + 1, NC = ND + 1;
+  const int Pseg = P > 0 ? P : 1;
+  const int P4 = (Pseg + 63) & ~63;
+  return (size_t)Layout<Q, double>::msize(Pseg) + (size_t)P4 * NC   // moments | m_j rows
+         + 3 * (size_t)P4                                           // a_j/W_j, 1/W_j, x1 / tmp
+         + (size_t)ND * P4                                          // z1_k of cut directions
+         + 2 * (size_t)ND * (ND + 1) + (size_t)ND * NC              // S (Jacobi), V, S | rhs
+         + 4 * 64 + 4 * (size_t)NC + 2 * (size_t)ND * ND + 64;      // rot, vectors, H, misc
+}
+
+// One wave (threadIdx.x < 64).  `md` = the date's raw moments (LDS), `ws` = scratch after them
+// (refine_struct_lds_doubles - msize doubles).  Writes f (global row fo, K entries), the
+// residual coefficients co[Q+1+P] (LDS or global) and returns the status bits to OR in.
+template <int Q>
+__device__ int struct_pinv_wave(const double* md, double* ws, int P, int pivot_mode,
+                                double* __restrict__ fo, double* co) {
+  using L = Layout<Q, double>;
+  constexpr int NS = L::NS, NG = L::NG, NACC = L::NACC, ND = L::ND, NC = ND + 1;
+  const int lane = threadIdx.x & 63;
+  const int Pseg = P > 0 ? P : 1;
+  const int P4 = (Pseg + 63) & ~63;
+  const double* acc = md;
+  const double* seg = md + NACC;
+  double* mrow = ws;                 // [P4][NC]  m_j (0 for inactive)
+  double* aw = mrow + P4 * NC;       // [P4]      a_j / W_j
+  double* iw = aw + P4;              // [P4]      1 / W_j (0 = inactive)
+  double* x1 = iw + P4;              // [P4]      industry unknowns / scratch
+  double* z1 = x1 + P4;              // [ND][P4]  -A_I^{-1} B v_k
+  double* Aj = z1 + ND * P4;         // [ND][ND+1] Jacobi matrix -> eigenvalues
+  double* Vj = Aj + ND * (ND + 1);   // [ND][ND+1] eigenvectors (columns)
+  double* Sx = Vj + ND * (ND + 1);   // [ND][NC]   Schur complement | reduced rhs
+  double* rot = Sx + ND * NC;        // [4*64]
+  double* gp = rot + 4 * 64;         // [NC] standardised pivot row
+  double* at = gp + NC;              // [NC] sum a m / W
+  double* totv = at + NC;            // [NC] column totals
+  double* x2 = totv + NC;            // [NC] dense unknowns
+  double* H = x2 + NC;               // [ND][ND] Gram of the cut null directions
+  double* vk = H + ND * ND;          // [ND][ND] scratch
+  double* misc = vk + ND * ND;       // [64]
+
+  const double Sc = acc[NG + 2 * Q + 0];
+  const double nval = acc[NG + 2 * Q + 3];
+  const double nq = nval * Q;
+  const double mx = acc[NG + 2 * Q + 1] / nq;
+  const double sigma = sqrt(fmax(acc[NG + 2 * Q + 2] / nq - mx * mx, 0.0));
+  const double isig = 1.0 / sigma;
+  int jp = -1;
+  if (P > 0) {
+    if (pivot_mode == 1) {
+      jp = P - 1;
+    } else {
+      for (int jb = 0; jb < P; jb += 64) {
+        const int j = jb + lane;
+        const unsigned long long m = __ballot(j < P && seg[j * NS + Q + 2] > 0.0);
+        if (m) jp = jb + 63 - __builtin_clzll(m);
+      }
+      if (jp < 0) jp = P - 1;
+    }
+  }
+  const int rp = P > 0 ? jp : 0;
+  const double sp = P > 0 ? seg[rp * NS + Q + 2] : 1.0;
+  const double rho = P > 0 ? seg[rp * NS] : 0.0;
+  auto muq = [&](int q) { return acc[NG + Q + q] / Sc; };
+  auto stdz = [&](const double* row, int c) {  // standardised industry channel c of `row`
+    const double raw = row[c];
+    return (c >= 1 && c <= Q) ? (raw - muq(c - 1) * row[0]) * isig : raw;
+  };
+  if (lane < NC) gp[lane] = P > 0 ? stdz(seg + rp * NS, lane) : 0.0;
+  for (int j = lane; j < P4; j += 64) {
+    const double W = j < P ? seg[j * NS] : 0.0;
+    const bool act = (j < P) && (j != jp) && (W > 0.0);
+    const double a = act ? -seg[j * NS + Q + 2] / sp : 0.0;
+    iw[j] = act ? 1.0 / W : 0.0;
+    aw[j] = act ? a / W : 0.0;
+    x1[j] = a;  // a_j, consumed below
+  }
+  wsync();
+  for (int e = lane; e < P4 * NC; e += 64) {
+    const int j = e / NC, c = e - (e / NC) * NC;
+    mrow[e] = iw[j] != 0.0 ? stdz(seg + j * NS, c) + x1[j] * gp[c] : 0.0;
+  }
+  // c0 = sum a^2 / W, sa = sum a (active)
+  double c0 = 0.0, sa = 0.0;
+  for (int j = lane; j < P4; j += 64) { c0 = fma(x1[j], aw[j], c0); sa += x1[j]; }
+  c0 = wave_total(c0);
+  sa = wave_total(sa);
+  const double kappa = P > 0 ? rho / (1.0 + rho * c0) : 0.0;
+  wsync();
+  // column totals and at
+  if (lane < NC) {
+    double t = 0.0, u = 0.0;
+    for (int j = 0; j < P4; ++j) { t += mrow[j * NC + lane]; u = fma(aw[j], mrow[j * NC + lane], u); }
+    // P == 0: the single segment holds the totals
+    totv[lane] = P > 0 ? t + (1.0 - sa) * gp[lane] : stdz(seg, lane);
+    at[lane] = u;
+  }
+  wsync();
+  const double Sw = totv[0];
+  // S = C - B^T A_I^{-1} B (+ rhs column) = M_DD - G + kappa at at^T
+  for (int e = lane; e < ND * NC; e += 64) {
+    const int u = e / NC, w = e - (e / NC) * NC;
+    double m;
+    if (u == 0) m = totv[w];
+    else if (w == 0) m = totv[u];
+    else if (w == ND) m = acc[NG + u - 1] * isig - muq(u - 1) * isig * totv[ND];
+    else {
+      const int q = u - 1, s2 = w - 1;
+      const int hi = q > s2 ? q : s2, lo = q > s2 ? s2 : q;
+      m = (acc[hi * (hi + 1) / 2 + lo] - muq(q) * muq(s2) * Sw) * isig * isig -
+          (muq(q) * totv[w] + muq(s2) * totv[u]) * isig;
+    }
+    double g = 0.0;
+    for (int j = 0; j < P4; ++j) g = fma(mrow[j * NC + u] * iw[j], mrow[j * NC + w], g);
+    Sx[e] = m - g + kappa * at[u] * at[w];
+    if (w < ND) H[u * ND + w] = m;  // the dense block C itself, for the power iteration
+  }
+  wsync();
+  for (int e = lane; e < ND * ND; e += 64) {
+    const int u = e / ND, w = e - (e / ND) * ND;
+    Aj[u * (ND + 1) + w] = Sx[u * NC + w];
+  }
+  wsync();
+  jacobi_wave(Aj, Vj, ND, ND + 1, rot, 60, 1e-17);
+
+  // A_I^{-1} y = y / W - kappa (a/W) ((a/W)^T y), in place on a [P4] LDS vector
+  auto ainv = [&](double* y) {
+    double t = 0.0;
+    for (int j = lane; j < P4; j += 64) t = fma(aw[j], y[j], t);
+    t = wave_total(t);
+    wsync();
+    for (int j = lane; j < P4; j += 64) y[j] = y[j] * iw[j] - kappa * aw[j] * t;
+    wsync();
+  };
+  // lambda_max(M) by power iteration on [x1; x2] (x1 in z1 row 0 as scratch, x2 in misc)
+  double* p1 = z1;  // reused: the cut directions are formed after this
+  for (int j = lane; j < P4; j += 64) p1[j] = iw[j] != 0.0 ? 1.0 : 0.0;
+  if (lane < ND) misc[lane] = 1.0;
+  wsync();
+  double lmax = 0.0;
+  for (int it = 0; it < 60; ++it) {
+    // y1 = W x1 + rho a (a^T x1) + B x2 ; y2 = B^T x1 + C x2  (C = M_DD = S + G - kappa at at^T)
+    double ax = 0.0;
+    for (int j = lane; j < P4; j += 64) ax = fma(aw[j] * (iw[j] != 0.0 ? 1.0 / iw[j] : 0.0), p1[j], ax);
+    ax = wave_total(ax);
+    double y1[2] = {0.0, 0.0};
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = lane + 64 * jj;
+      if (j < P4 && iw[j] != 0.0) {
+        const double W = 1.0 / iw[j], a = aw[j] * W;
+        double t = W * p1[j] + rho * a * ax;
+        for (int u = 0; u < ND; ++u) t = fma(mrow[j * NC + u], misc[u], t);
+        y1[jj] = t;
+      }
+    }
+    double y2 = 0.0;
+    if (lane < ND) {
+      const int u = lane;
+      for (int j = 0; j < P4; ++j) y2 = fma(mrow[j * NC + u], p1[j], y2);
+      for (int w = 0; w < ND; ++w) y2 = fma(H[u * ND + w], misc[w], y2);
+    }
+    double nn = y1[0] * y1[0] + y1[1] * y1[1] + (lane < ND ? y2 * y2 : 0.0);
+    nn = wave_total(nn);
+    const double nrm = sqrt(nn);
+    lmax = nrm;  // |M x| with |x| = 1 after the first step
+    const double inv = nrm > 0.0 ? 1.0 / nrm : 0.0;
+    wsync();
+    for (int jj = 0; jj < 2; ++jj) {
+      const int j = lane + 64 * jj;
+      if (j < P4) p1[j] = y1[jj] * inv;
+    }
+    if (lane < ND) misc[lane] = y2 * inv;
+    wsync();
+  }
+  const double cut = 1e-15 * lmax;
+  // eigenpairs of S: z1_k = -A_I^{-1} B v_k, Rayleigh quotient on M, keep / cut
+  int ncut = 0;
+  unsigned keep_mask = 0;
+  for (int k = 0; k < ND; ++k) {
+    double* zk = z1 + ncut * P4;
+    for (int j = lane; j < P4; j += 64) {
+      double t = 0.0;
+      for (int u = 0; u < ND; ++u) t = fma(mrow[j * NC + u], Vj[u * (ND + 1) + k], t);
+      zk[j] = -t;
+    }
+    wsync();
+    ainv(zk);
+    double zz = 0.0;
+    for (int j = lane; j < P4; j += 64) zz = fma(zk[j], zk[j], zz);
+    zz = wave_total(zz);
+    const double muk = Aj[k * (ND + 1) + k];
+    if (fabs(muk) / (1.0 + zz) > cut) {
+      keep_mask |= 1u << k;
+    } else {
+      if (lane < ND) vk[ncut * ND + lane] = Vj[lane * (ND + 1) + k];
+      ++ncut;  // zk stays: a cut direction
+    }
+    wsync();
+  }
+  // x2 = sum_kept v v^T b~ / mu
+  if (lane < ND) {
+    double t = 0.0;
+    for (int k = 0; k < ND; ++k) {
+      if (!(keep_mask & (1u << k))) continue;
+      double vb = 0.0;
+      for (int u = 0; u < ND; ++u) vb = fma(Vj[u * (ND + 1) + k], Sx[u * NC + ND], vb);
+      t = fma(Vj[lane * (ND + 1) + k], vb / Aj[k * (ND + 1) + k], t);
+    }
+    x2[lane] = t;
+  }
+  wsync();
+  // x1 = A_I^{-1} (b1 - B x2),  b1_j = m_j[ND]
+  for (int j = lane; j < P4; j += 64) {
+    double t = mrow[j * NC + ND];
+    for (int u = 0; u < ND; ++u) t = fma(-mrow[j * NC + u], x2[u], t);
+    x1[j] = iw[j] != 0.0 ? t : 0.0;
+  }
+  wsync();
+  ainv(x1);
+  // minimum norm: x -= Z (Z^T Z)^{-1} Z^T x over the cut directions Z_k = [z1_k ; v_k]
+  if (ncut > 0) {
+    for (int e = 0; e < ncut * ncut; ++e) {
+      const int k = e / ncut, l = e - (e / ncut) * ncut;
+      double t = 0.0;
+      for (int j = lane; j < P4; j += 64) t = fma(z1[k * P4 + j], z1[l * P4 + j], t);
+      t = wave_total(t);
+      double vv = 0.0;
+      for (int u = 0; u < ND; ++u) vv = fma(vk[k * ND + u], vk[l * ND + u], vv);
+      if (lane == 0) H[k * ND + l] = t + vv;
+    }
+    for (int k = 0; k < ncut; ++k) {
+      double t = 0.0;
+      for (int j = lane; j < P4; j += 64) t = fma(z1[k * P4 + j], x1[j], t);
+      t = wave_total(t);
+      double vx = 0.0;
+      for (int u = 0; u < ND; ++u) vx = fma(vk[k * ND + u], x2[u], vx);
+      if (lane == 0) misc[k] = t + vx;
+    }
+    wsync();
+    if (lane == 0) {  // Cholesky solve of the ncut x ncut SPD Gram (ncut <= 17)
+      for (int k = 0; k < ncut; ++k) {
+        double dk = H[k * ND + k];
+        for (int i = 0; i < k; ++i) dk -= H[k * ND + i] * H[k * ND + i];
+        dk = sqrt(fmax(dk, 1e-300));
+        H[k * ND + k] = dk;
+        for (int i = k + 1; i < ncut; ++i) {
+          double t = H[i * ND + k];
+          for (int l = 0; l < k; ++l) t -= H[i * ND + l] * H[k * ND + l];
+          H[i * ND + k] = t / dk;
+        }
+      }
+      for (int k = 0; k < ncut; ++k) {
+        double t = misc[k];
+        for (int l = 0; l < k; ++l) t -= H[k * ND + l] * misc[l];
+        misc[k] = t / H[k * ND + k];
+      }
+      for (int k = ncut - 1; k >= 0; --k) {
+        double t = misc[k];
+        for (int l = k + 1; l < ncut; ++l) t -= H[l * ND + k] * misc[l];
+        misc[k] = t / H[k * ND + k];
+      }
+    }
+    wsync();
+    for (int j = lane; j < P4; j += 64) {
+      double t = x1[j];
+      for (int k = 0; k < ncut; ++k) t = fma(-misc[k], z1[k * P4 + j], t);
+      x1[j] = t;
+    }
+    if (lane < ND) {
+      double t = x2[lane];
+      for (int k = 0; k < ncut; ++k) t = fma(-misc[k], vk[k * ND + lane], t);
+      x2[lane] = t;
+    }
+    wsync();
+  }
+  // outputs: f in the original order, residual coefficients on RAW styles
+  double fpv = 0.0;
+  for (int j = lane; j < P4; j += 64) fpv = fma(aw[j] * (iw[j] != 0.0 ? 1.0 / iw[j] : 0.0), x1[j], fpv);
+  fpv = wave_total(fpv);
+  for (int j = lane; j < P; j += 64) {
+    const double fj = j == jp ? fpv : x1[j];
+    fo[1 + j] = fj;
+    co[Q + 1 + j] = fj;
+  }
+  if (lane == 0) fo[0] = x2[0];
+  if (lane < Q) {
+    fo[1 + P + lane] = x2[1 + lane];
+    co[lane] = x2[1 + lane] * isig;
+  }
+  if (lane == 0) {
+    double cst = x2[0];
+    for (int q = 0; q < Q; ++q) cst -= x2[1 + q] * isig * muq(q);
+    co[Q] = cst;
+  }
+  wsync();
+  return ncut > 0 ? XS_REFINED | XS_ZERO_PIVOT : XS_REFINED;
+}
+
+// Full-matrix Jacobi pinv of the constrained normal matrix, K <= kXsRefineMaxK (the reference's
+// own algebra: eigen-decompose A = R^T X^T W X R, drop |lambda| <= 1e-15 max|lambda|).  The
+// whole workgroup builds A in LDS, wave 0 solves.  Writes f (row fo), co[Q+1+P] and returns
+// the status bits to OR in (threadIdx.x < 64).
+template <int Q>
+__device__ int jacobi_pinv_block(const double* md, double* ws, int P, int pivot_mode,
+                                 double* __restrict__ fo, double* co, double* sc, int* piv_s) {
   using L = Layout<Q, double>;
   constexpr int NS = L::NS, NG = L::NG, NACC = L::NACC;
-  const int d = blockIdx.x;
-  const int st0 = status[d];
-  if (!(st0 & XS_NEAR_SINGULAR) || (st0 & XS_BAD)) return;  // uniform: whole workgroup exits
-  extern __shared__ double sm[];
-  __shared__ double cf_s[Q + 1 + 128];
-  __shared__ double red[4][5];
-  __shared__ double sc[4];   // W_tot, B_tot, sigma, s_pivot
-  __shared__ int piv_s;
   const int tid = threadIdx.x, lane = tid & 63;
   const int Pseg = P > 0 ? P : 1;
-  const int MS = L::msize(Pseg);
   const int K = 1 + P + Q, Kr = P > 0 ? K - 1 : K, lda = Kr + 1;
-  double* md = sm;                 // [MS] raw moments
-  double* A = md + MS;             // [Kr][lda]
+  double* A = ws;                  // [Kr][lda]
   double* V = A + Kr * lda;        // [Kr][lda]
   double* rot = V + Kr * lda;      // [4*64]
   double* rhs = rot + 4 * 64;      // [Kr]
   double* alp = rhs + Kr;          // [Kr]  constraint weights alpha_u
   double* g = alp + Kr;            // [Kr]  eigen-space coefficients
   double* mu = g + Kr;             // [Q]   cap-weighted style means
-  load_moments<Q>(mom, d, S, Pseg, md);
-  __syncthreads();
   const double* acc = md;
   const double* seg = md + NACC;
   if (tid == 0) {
@@ -1535,13 +1838,13 @@ __global__ __launch_bounds__(256) void xs_refine_kernel(
       else for (int j = 0; j < P; ++j) if (seg[j * NS + Q + 2] > 0.0) jp = j;
       if (jp < 0) jp = P - 1;
     }
-    piv_s = jp;
+    *piv_s = jp;
     sc[3] = P > 0 ? seg[jp * NS + Q + 2] : 1.0;
   }
   if (tid < Q) mu[tid] = acc[NG + Q + tid] / acc[NG + 2 * Q];
   __syncthreads();
   const double Wt = sc[0], Bt = sc[1], sig = sc[2], isig = 1.0 / sig, sp = sc[3];
-  const int jp = piv_s;
+  const int jp = *piv_s;
   // Aq_tot[q] = sum_j A_jq
   auto aqt = [&](int q) {
     double t = 0.0;
@@ -1593,48 +1896,102 @@ __global__ __launch_bounds__(256) void xs_refine_kernel(
   for (int u = tid; u < Kr; u += blockDim.x)
     rhs[u] = bfull(orig(u)) + (P > 0 ? alp[u] * bfull(pc) : 0.0);
   __syncthreads();
-  if (tid < 64) {
-    jacobi_wave(A, V, Kr, lda, rot, 40, 1e-17);
-    double lmax = 0.0;
-    for (int k = lane; k < Kr; k += 64) lmax = fmax(lmax, fabs(A[k * lda + k]));
-    lmax = wave_max(lmax);
-    const double cut = 1e-15 * lmax;
-    // c_k = (v_k . rhs) / lambda_k over the kept spectrum
-    for (int k = lane; k < Kr; k += 64) {
-      const double lk = A[k * lda + k];
-      double t = 0.0;
-      for (int i = 0; i < Kr; ++i) t = fma(V[i * lda + k], rhs[i], t);
-      g[k] = fabs(lk) > cut ? t / lk : 0.0;
-    }
-    wsync();
-    for (int i = lane; i < Kr; i += 64) {  // g <- V c
-      double t = 0.0;
-      for (int k = 0; k < Kr; ++k) t = fma(V[i * lda + k], g[k], t);
-      rot[i < 256 ? i : 0] = t;  // rot is free again: stage V c (Kr <= 64)
-    }
-    wsync();
-    // f in original order: f[orig(u)] = g[u], f[pivot] = sum_u alpha_u g[u]
-    double* fo = fout + (size_t)d * K;
-    double fp = 0.0;
-    for (int u = lane; u < Kr; u += 64) fp = fma(alp[u], rot[u], fp);
-    fp = wave_sum(fp);
-    for (int u = lane; u < Kr; u += 64) {
-      const int ou = orig(u);
-      fo[ou] = rot[u];
-      if (ou >= 1 && ou <= P) cf_s[Q + ou] = rot[u];          // industry f_j at Q + 1 + j
-      if (ou > P) cf_s[ou - 1 - P] = rot[u] * isig;           // raw-style coefficient
-    }
-    if (P > 0 && lane == 0) { fo[pc] = fp; cf_s[Q + pc] = fp; }
-    wsync();
-    if (lane == 0) {
-      double cst = rot[0];  // country (column 0 is never the pivot)
-      for (int q = 0; q < Q; ++q) cst -= cf_s[q] * mu[q];
-      cf_s[Q] = cst;
-      status[d] = st0 | XS_REFINED;
-    }
+  if (tid >= 64) return 0;
+  jacobi_wave(A, V, Kr, lda, rot, 40, 1e-17);
+  double lmax = 0.0;
+  for (int k = lane; k < Kr; k += 64) lmax = fmax(lmax, fabs(A[k * lda + k]));
+  lmax = wave_max(lmax);
+  const double cut = 1e-15 * lmax;
+  // c_k = (v_k . rhs) / lambda_k over the kept spectrum
+  for (int k = lane; k < Kr; k += 64) {
+    const double lk = A[k * lda + k];
+    double t = 0.0;
+    for (int i = 0; i < Kr; ++i) t = fma(V[i * lda + k], rhs[i], t);
+    g[k] = fabs(lk) > cut ? t / lk : 0.0;
   }
+  wsync();
+  for (int i = lane; i < Kr; i += 64) {  // g <- V c
+    double t = 0.0;
+    for (int k = 0; k < Kr; ++k) t = fma(V[i * lda + k], g[k], t);
+    rot[i < 256 ? i : 0] = t;  // rot is free again: stage V c (Kr <= 64)
+  }
+  wsync();
+  // f in original order: f[orig(u)] = g[u], f[pivot] = sum_u alpha_u g[u]
+  double fp = 0.0;
+  for (int u = lane; u < Kr; u += 64) fp = fma(alp[u], rot[u], fp);
+  fp = wave_sum(fp);
+  for (int u = lane; u < Kr; u += 64) {
+    const int ou = orig(u);
+    fo[ou] = rot[u];
+    if (ou >= 1 && ou <= P) co[Q + ou] = rot[u];          // industry f_j at Q + 1 + j
+    if (ou > P) co[ou - 1 - P] = rot[u] * isig;           // raw-style coefficient
+  }
+  if (P > 0 && lane == 0) { fo[pc] = fp; co[Q + pc] = fp; }
+  wsync();
+  if (lane == 0) {
+    double cst = rot[0];  // country (column 0 is never the pivot)
+    for (int q = 0; q < Q; ++q) cst -= co[q] * mu[q];
+    co[Q] = cst;
+  }
+  wsync();
+  return XS_REFINED;
+}
+
+template <int Q>
+__host__ __device__ constexpr size_t refine_any_lds_doubles(int P) {
+  return 1 + Q + P > kXsRefineMaxK ? refine_struct_lds_doubles<Q>(P) : refine_lds_doubles<Q>(P);
+}
+
+// ------------------------------------------------------------------------------------------
+// Device pseudo-inverse refinement (pinv semantics of CrossSection.py:76,98) for dates the
+// Cholesky flagged near-singular (e.g. an exactly collinear style pair).  Grid D; a workgroup
+// whose date is not flagged exits at once, so the pass rides in the same stream / HIP graph as
+// the regression with no host synchronisation.  K <= 64: the reference's own algebra (the
+// constrained normal matrix A = R^T X^T W X R in LDS, one-wave Jacobi, pinv(A) = V diag(1 /
+// lambda) V^T over |lambda| > 1e-15 max|lambda|); larger K (SW-L2-sized industry sets): the
+// structured pinv above.  RESID: the whole workgroup then redoes the date's specific returns
+// and R^2; otherwise (stock-sharded path) only f and the residual coefficients coef[d] are
+// rewritten, for the caller's residual pass.
+// ------------------------------------------------------------------------------------------
+template <int Q, typename T, bool RESID>
+__global__ __launch_bounds__(256) void xs_refine_kernel(
+    const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
+    const int16_t* __restrict__ ind, int N, int P, int pivot_mode, int S,
+    const double* __restrict__ mom, double* __restrict__ fout, T* __restrict__ eout,
+    double* __restrict__ r2out, int* __restrict__ status, double* __restrict__ coef) {
+  using L = Layout<Q, double>;
+  const int d = blockIdx.x;
+  const int st0 = status[d];
+  if (!(st0 & XS_NEAR_SINGULAR) || (st0 & XS_BAD)) return;  // uniform: whole workgroup exits
+  extern __shared__ double sm[];
+  __shared__ double cf_s[Q + 1 + 128];
+  __shared__ double red[4][5];
+  __shared__ double sc[4];   // W_tot, B_tot, sigma, s_pivot
+  __shared__ int piv_s;
+  __shared__ int st_s;
+  const int tid = threadIdx.x;
+  const int Pseg = P > 0 ? P : 1;
+  const int MS = L::msize(Pseg);
+  const int K = 1 + P + Q;
+  double* md = sm;                 // [MS] raw moments
+  load_moments<Q>(mom, d, S, Pseg, md);
   __syncthreads();
-  resid_body<Q, T>(X, cap, ret, ind, d, N, P, cf_s, false, eout, r2out, red);
+  double* fo = fout + (size_t)d * K;
+  double* co = RESID ? cf_s : coef + (size_t)d * (Q + 1 + P);
+  int bits;
+  if (K > kXsRefineMaxK) {
+    bits = tid < 64 ? struct_pinv_wave<Q>(md, md + MS, P, pivot_mode, fo, co) : 0;
+  } else {
+    bits = jacobi_pinv_block<Q>(md, md + MS, P, pivot_mode, fo, co, sc, &piv_s);
+  }
+  if (tid == 0) {
+    st_s = st0 | bits;
+    status[d] = st0 | bits;
+  }
+  if constexpr (RESID) {
+    __syncthreads();
+    resid_body<Q, T>(X, cap, ret, ind, d, N, P, cf_s, false, eout, r2out, red);
+  }
 }
 
 constexpr int kXsDeterministic = 0x100;  // pivot_mode flag: bitwise-deterministic kernel
@@ -1704,7 +2061,7 @@ hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, 
   const size_t lds1 = ((size_t)L::seg_doubles(rep8 ? kRepMax : 1, Pseg) + L::NACC) * sizeof(double);
   const size_t lds2 = solve_lds_bytes<Q, T>(Pseg);
   if (lds1 + fused_ring_bytes<Q, T>() > 160 * 1024 || lds2 > 64 * 1024) return hipErrorInvalidValue;
-  if (refine && 1 + P + Q > kXsRefineMaxK) return hipErrorInvalidValue;
+  if (refine && refine_any_lds_doubles<Q>(P) * sizeof(double) > 160 * 1024) return hipErrorInvalidValue;
   if (det && !rep8) return hipErrorNotSupported;
   const int16_t* indp = P > 0 ? ind : nullptr;
   constexpr bool PRE = sizeof(T) == 4;
@@ -1760,9 +2117,9 @@ hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, 
                        cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom, okm);
   }
   if (refine) {
-    const size_t lds3 = refine_lds_doubles<Q>(P) * sizeof(double);
-    hipLaunchKernelGGL((xs_refine_kernel<Q, T>), dim3(D), dim3(256), lds3, s, X, cap, ret, indp,
-                       N, P, pm, S, mom, f, e, r2, status);
+    const size_t lds3 = refine_any_lds_doubles<Q>(P) * sizeof(double);
+    hipLaunchKernelGGL((xs_refine_kernel<Q, T, true>), dim3(D), dim3(256), lds3, s, X, cap, ret,
+                       indp, N, P, pm, S, mom, f, e, r2, status, (double*)nullptr);
   }
   return hipGetLastError();
 }
@@ -1793,7 +2150,8 @@ int xs_wls_dispatch(const T* X, const T* cap, const T* ret, const int16_t* ind, 
 // date into raw moments (additive: the caller all-reduces them), solves redundantly from the
 // summed moments, and forms its stocks' specific returns plus the five R^2 sums
 // [sum e, sum e^2, sum r, sum r^2, n] per date (all-reduced again by the caller).
-// what: 0 = moments, 1 = solve (type independent), 2 = residual sums.
+// what: 0 = moments, 1 = solve (type independent), 2 = residual sums, 3 = device pinv of the
+// dates the solve flagged near-singular (rewrites f and coef in place; no host sync).
 // ------------------------------------------------------------------------------------------
 template <int Q, typename T>
 hipError_t split_q(int what, const T* X, const T* cap, const T* ret, const int16_t* ind, int D,
@@ -1818,6 +2176,13 @@ hipError_t split_q(int what, const T* X, const T* cap, const T* ret, const int16
     if (lds2 > 64 * 1024) return hipErrorInvalidValue;
     hipLaunchKernelGGL(xs_solve_kernel<Q>, dim3(D), dim3(64), lds2, s, mom, 1, P, Pseg, pivot_mode,
                        tol, f, coef, stats, status);
+  } else if (what == 3) {  // device pinv of flagged dates from the (all-reduced) moments
+    const size_t lds3 = refine_any_lds_doubles<Q>(P) * sizeof(double);
+    if (lds3 > 160 * 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((xs_refine_kernel<Q, T, false>), dim3(D), dim3(256), lds3, s,
+                       (const T*)nullptr, (const T*)nullptr, (const T*)nullptr,
+                       (const int16_t*)nullptr, 0, P, pivot_mode, 1, mom, f, (T*)nullptr,
+                       (double*)nullptr, status, coef);
   } else {
     hipLaunchKernelGGL((xs_resid_kernel<Q, T>), dim3(D), dim3(256), 0, s, X, cap, ret, indp, D, N,
                        P, 1, N, coef, status, e, (double*)nullptr, sums);

@@ -40,7 +40,7 @@ XS_BAD_SIGMA = 16
 XS_REFINED = 32          # re-solved by the device pseudo-inverse pass
 XS_DETERMINISTIC = 0x100  # pivot_mode flag of mfa_xs_wls: bitwise-deterministic kernel
 XS_REFINE = 0x200         # pivot_mode flag: device pinv pass for near-singular dates
-REFINE_MAX_K = 64         # largest K the device pinv pass holds in LDS (host fallback above)
+REFINE_MAX_K = 64         # full-matrix Jacobi pinv up to this K; structured device pinv above
 
 
 @dataclass
@@ -88,7 +88,9 @@ def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Ten
     reference's choice is valid); 1 reproduces the reference exactly (always the last column,
     NaN when it is empty, quirk Q3).  ``refine`` re-solves dates the kernel flags as
     near-singular with the pseudo-inverse (pinv semantics, quirk Q4): on the GPU a device pass
-    in the same stream (eigen-pinv of the constrained normal matrix, K <= 64), no host sync.
+    in the same stream, no host sync, for any K (eigen-pinv of the constrained normal matrix for
+    K <= 64; above, the structured pinv that eigen-decomposes only the dense block's Schur
+    complement and projects out the null directions of the full matrix).
     ``out`` / ``workspace`` let a caller (e.g. a timed loop) reuse preallocated buffers.
     The GPU kernels need N % 8 == 0 (16-byte rows for the LDS-DMA ring); other N are padded
     here with absent stocks (``ind = -1``), which costs a copy — keep panels padded.
@@ -138,10 +140,9 @@ def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Ten
         raise ValueError(f"xs_wls: workspace of {workspace.numel()} B is too small for D={D}, "
                          f"N={N}, P={P}, Q={Q} ({need} B): size it with xs_wls_workspace(D, P, "
                          "Q, device, N)")
-    dev_refine = refine and K <= REFINE_MAX_K
     if deterministic is None:
         deterministic = bool(_native.lib().mfa_xs_det_supported(P, Q))
-    flags = (XS_DETERMINISTIC if deterministic else 0) | (XS_REFINE if dev_refine else 0)
+    flags = (XS_DETERMINISTIC if deterministic else 0) | (XS_REFINE if refine else 0)
     _native.call("mfa_xs_wls_f64" if dt == torch.float64 else "mfa_xs_wls", _native.ptr(X),
                  _native.ptr(cap), _native.ptr(ret),
                  _native.ptr(ind if P > 0 else None), D, Np, P, Q, pivot_mode | flags, tol,
@@ -150,9 +151,6 @@ def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Ten
                  _native.stream(dev))
     if resid_buf is not None and Np != N:
         out.resid.copy_(resid_buf[:, :N])
-    if refine and not dev_refine:  # K > 64: host pinv for the flagged dates (syncs)
-        _refine_near_singular(X[..., :N], cap[:, :N], ret[:, :N], ind[:, :N] if P > 0 else None,
-                              P, pivot_mode, out)
     return out
 
 
@@ -163,22 +161,6 @@ def xs_wls_workspace(D: int, P: int, Q: int, device, N: int) -> torch.Tensor:
     Np = (N + 7) // 8 * 8
     return torch.empty(_native.query("mfa_xs_wls_workspace", D, Np, P, Q), dtype=torch.uint8,
                        device=device)
-
-
-def _refine_near_singular(X, cap, ret, ind, P, pivot_mode, out: XsResult) -> None:
-    bad = torch.nonzero((out.status & XS_NEAR_SINGULAR) != 0).flatten()
-    if bad.numel() == 0:
-        return
-    idx = bad.cpu()
-    sub = xs_wls_reference(X[bad].cpu(), cap[bad].cpu(), ret[bad].cpu(),
-                           ind[bad].cpu() if P > 0 else None, P, pivot_mode=pivot_mode,
-                           want_resid=out.resid is not None)
-    out.f[bad] = sub.f.to(out.f.device)
-    out.r2[bad] = sub.r2.to(out.r2.device)
-    out.status[bad] |= XS_REFINED
-    if out.resid is not None:
-        out.resid[bad] = sub.resid.to(out.resid.device, out.resid.dtype)
-    del idx
 
 
 def valid_mask(X, cap, ret, ind, P) -> torch.Tensor:

@@ -32,6 +32,9 @@ _native.register("mfa_eigen_adjust", [C.c_void_p, C.c_void_p, C.c_void_p, C.c_in
                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p])
 _native.register("mfa_mc_cov_range", [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_void_p,
                                        C.c_void_p])
+_native.register("mfa_mc_cov_ws_doubles", [C.c_int, C.c_int])
+_native.register("mfa_mc_cov_range_ws", [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64,
+                                          C.c_void_p, C.c_void_p, C.c_void_p])
 _native.register("mfa_eigen_bias_accumulate", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                                 C.c_void_p, C.c_int, C.c_double, C.c_void_p,
                                                 C.c_void_p, C.c_void_p])
@@ -124,8 +127,11 @@ def mc_cov(M: int, K: int, T: int, seed: int = 1, device="cuda", m0: int = 0) ->
             Cz[i] = torch.cov(z.T)
         return Cz
     Cz = torch.empty(M, K, K, dtype=torch.float64, device=dev)
-    _native.call("mfa_mc_cov_range", M, int(m0), K, T, int(seed) & 0xFFFFFFFFFFFFFFFF,
-                 _native.ptr(Cz), _native.stream(dev))
+    # the time axis is split over ~2048 waves (partial sums added in chunk order)
+    nws = _native.query("mfa_mc_cov_ws_doubles", M, T)
+    ws = torch.empty(max(1, nws), dtype=torch.float64, device=dev)
+    _native.call("mfa_mc_cov_range_ws", M, int(m0), K, T, int(seed) & 0xFFFFFFFFFFFFFFFF,
+                 _native.ptr(ws), _native.ptr(Cz), _native.stream(dev))
     return Cz
 
 

@@ -26,14 +26,15 @@ import ctypes as C
 import torch
 
 from .. import _native
-from .cross_section import (XS_BAD_SIGMA, XS_NEAR_SINGULAR, XS_NO_ROWS, XS_PIVOT_EMPTY, XsResult,
-                            _validate, valid_mask)
+from .cross_section import (XS_BAD_SIGMA, XS_NO_ROWS, XS_PIVOT_EMPTY, XsResult, _validate,
+                            valid_mask)
 
 _vp, _i, _d = C.c_void_p, C.c_int, C.c_double
 _native.register("mfa_xs_moments", [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp])
 _native.register("mfa_xs_solve", [_vp, _i, _i, _i, _i, _d, _vp, _vp, _vp, _vp, _vp])
 _native.register("mfa_xs_resid_sums", [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp])
 _native.register("mfa_xs_moments_bytes", [_i, _i])
+_native.register("mfa_xs_refine_coef", [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp])
 _native.register("mfa_xs_moments_f64", [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp])
 _native.register("mfa_xs_resid_sums_f64", [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp,
                                            _vp])
@@ -171,8 +172,10 @@ def xs_wls_stock_sharded(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor,
     """Regress every date with this rank's STOCKS ``[D, Q, N_local]`` (all ranks hold the same
     dates).  Returns full-universe ``f``, ``r2``, ``stats`` and ``status`` (identical on every
     rank) and this rank's ``resid`` columns.  ``ctx`` = ``parallel.dist`` context (None or world
-    1: plain single-process run).  ``refine`` re-solves near-singular dates with the pinv path
-    from all-reduced CPU moments (pinv semantics, quirk Q4), like ``xs_wls``.
+    1: plain single-process run).  ``refine`` re-solves the dates the solve flags near-singular
+    with the device pseudo-inverse (pinv semantics, quirk Q4) from the all-reduced moments,
+    before the residual pass: no host synchronisation and no extra collective (the flags and
+    the moments are identical on every rank).
     """
     D, Q, N = _validate(X, cap, ret, ind, P)
     if not X.is_cuda:
@@ -208,22 +211,14 @@ def xs_wls_stock_sharded(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor,
     status = torch.empty(D, dtype=torch.int32, device=dev)
     _native.call("mfa_xs_solve", _native.ptr(mom), D, P, Q, pivot_mode, tol, _native.ptr(f),
                  _native.ptr(coef), _native.ptr(stats), _native.ptr(status), st)
+    if refine:  # device pinv of flagged dates: rewrites f / coef / status in place, any K
+        _native.call("mfa_xs_refine_coef", _native.ptr(mom), D, P, Q, pivot_mode, _native.ptr(f),
+                     _native.ptr(coef), _native.ptr(status), st)
     e = torch.empty(D, Np, dtype=dt, device=dev) if want_resid else None
     sums = torch.empty(D, 5, dtype=torch.float64, device=dev)
     _native.call("mfa_xs_resid_sums" + sfx, _native.ptr(Xp), _native.ptr(cp), _native.ptr(rp), iptr, D,
                  Np, P, Q, _native.ptr(coef), _native.ptr(status), _native.ptr(e),
                  _native.ptr(sums), st)
     _all_reduce(sums, ctx)                                     # collective 2: D x 5 fp64
-    out = XsResult(f=f, resid=(e[:, :N] if Np != N else e) if want_resid else None,
-                   r2=_r2_from_sums(sums, status), stats=stats, status=status)
-    if refine:
-        # the flag comes from the summed moments, so every rank picks the same dates
-        bad = torch.nonzero((status & XS_NEAR_SINGULAR) != 0).flatten()
-        if bad.numel():
-            sub = _xs_sharded_cpu(X[bad].cpu(), cap[bad].cpu(), ret[bad].cpu(),
-                                  ind[bad].cpu() if P > 0 else None, P, ctx, pivot_mode, want_resid)
-            out.f[bad] = sub.f.to(dev)
-            out.r2[bad] = sub.r2.to(dev)
-            if want_resid:
-                out.resid[bad] = sub.resid.to(dev, out.resid.dtype)
-    return out
+    return XsResult(f=f, resid=(e[:, :N] if Np != N else e) if want_resid else None,
+                    r2=_r2_from_sums(sums, status), stats=stats, status=status)

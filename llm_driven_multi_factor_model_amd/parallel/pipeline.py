@@ -20,7 +20,7 @@ from __future__ import annotations
 
 import torch
 
-from ..ops.cross_section import XS_NEAR_SINGULAR, XsResult, xs_wls, xs_wls_reference, xs_wls_workspace
+from ..ops.cross_section import XsResult, xs_wls, xs_wls_reference, xs_wls_workspace
 
 
 def _pinned(t: torch.Tensor) -> torch.Tensor:
@@ -98,8 +98,9 @@ def streamed_xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: 
             s_cmp.wait_event(loaded[k])
             view = XsResult(f=o.f[:n], resid=o.resid[:n] if want_resid else None, r2=o.r2[:n],
                             stats=o.stats[:n], status=o.status[:n])
+            # device pinv of near-singular dates inside the chunk's stream (no host sync)
             xs_wls(xi[:n], ci[:n], ri[:n], ii[:n] if ii is not None else None, P,
-                   pivot_mode=pivot_mode, want_resid=want_resid, refine=False, out=view,
+                   pivot_mode=pivot_mode, want_resid=want_resid, refine=refine, out=view,
                    workspace=ws[k])
             computed[k].record(s_cmp)
         with torch.cuda.stream(s_d2h):
@@ -116,15 +117,6 @@ def streamed_xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: 
     s_d2h.synchronize()
     torch.cuda.current_stream(device).wait_stream(s_d2h)
 
-    if refine:
-        bad = torch.nonzero((res.status & XS_NEAR_SINGULAR) != 0).flatten()
-        if bad.numel():
-            sub = xs_wls_reference(X[bad], cap[bad], ret[bad], ind[bad] if P > 0 else None, P,
-                                   pivot_mode=pivot_mode, want_resid=want_resid)
-            res.f[bad] = sub.f
-            res.r2[bad] = sub.r2
-            if want_resid:
-                res.resid[bad] = sub.resid
     return res
 
 

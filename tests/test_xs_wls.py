@@ -169,6 +169,71 @@ def test_device_pinv_refine_matches_oracle(cuda):
     torch.testing.assert_close(o32.f.cpu(), ref32.f, rtol=1e-8, atol=1e-11)
 
 
+def _degenerate_wide(D=4, N=3000, P=123, Q=16, seed=31, empty=(5, 40)):
+    """K = 1 + P + Q wide (SW-L2-sized industries): exactly collinear styles, an industry with
+    a single stock and exactly-empty industries -> near-singular on every date."""
+    p = synthetic_panel(D, N, P, Q, seed=seed, dtype=torch.float64)
+    p.styles[:, 3] = p.styles[:, 1]
+    ind = p.ind.clone()
+    for j in empty:
+        ind[ind == j] = (j + 1) % P
+    ind[ind == 2] = 1
+    ind[:, 0] = 2
+    p.ind = ind
+    return p
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,Q", [(100, 8), (123, 16), (128, 11)])
+def test_device_pinv_refine_any_k(cuda, P, Q):
+    """K > 64 (109 / 140 / 140): the structured device pinv (Schur-complement eigen-solve plus
+    the minimum-norm projection) matches the reference pinv; the whole call is graph-capturable,
+    i.e. it has no host synchronisation (.cpu(), nonzero, ...)."""
+    p = _degenerate_wide(P=P, Q=Q)
+    ref = X.xs_wls_reference(p.styles, p.cap, p.ret, p.ind, p.P)
+    g = p.to(cuda)
+    out = X.xs_wls(g.styles, g.cap, g.ret, g.ind, p.P)
+    torch.cuda.synchronize()
+    st = out.status.cpu()
+    assert ((st & X.XS_REFINED) != 0).all(), st
+    torch.testing.assert_close(out.f.cpu(), ref.f, rtol=1e-9, atol=1e-12)
+    torch.testing.assert_close(out.r2.cpu(), ref.r2, rtol=1e-9, atol=1e-12)
+    torch.testing.assert_close(out.resid.cpu(), ref.resid, rtol=1e-9, atol=1e-12, equal_nan=True)
+    # no host sync anywhere in the refine path: capture it in a HIP graph and replay
+    ws = X.xs_wls_workspace(p.D, p.P, p.Q, cuda, p.N)
+    o2 = X.xs_wls(g.styles, g.cap, g.ret, g.ind, p.P, workspace=ws)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        X.xs_wls(g.styles, g.cap, g.ret, g.ind, p.P, out=o2, workspace=ws)
+    o2.f.zero_()
+    graph.replay()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(o2.f.cpu(), ref.f, rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("P,Q", [(6, 4), (123, 16)])
+def test_stock_sharded_device_refine(cuda, P, Q):
+    """Stock-sharded (TP) path: near-singular dates are re-solved on the device from the
+    all-reduced moments before the residual pass (no host sync: graph-capturable)."""
+    from llm_driven_multi_factor_model_amd.ops import xs_sharded as S
+    p = _degenerate_wide(P=P, Q=Q, empty=(5,) if P > 5 else ())
+    ref = X.xs_wls_reference(p.styles, p.cap, p.ret, p.ind, p.P)
+    g = p.to(cuda)
+    out = S.xs_wls_stock_sharded(g.styles, g.cap, g.ret, g.ind, p.P)
+    torch.cuda.synchronize()
+    assert ((out.status.cpu() & X.XS_REFINED) != 0).all()
+    torch.testing.assert_close(out.f.cpu(), ref.f, rtol=1e-9, atol=1e-12)
+    torch.testing.assert_close(out.r2.cpu(), ref.r2, rtol=1e-9, atol=1e-12)
+    torch.testing.assert_close(out.resid.cpu(), ref.resid, rtol=1e-9, atol=1e-12, equal_nan=True)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        S.xs_wls_stock_sharded(g.styles, g.cap, g.ret, g.ind, p.P)
+    graph.replay()
+    torch.cuda.synchronize()
+
+
 @pytest.mark.gpu
 def test_device_pinv_refine_more_dates_than_grid(cuda):
     """Every one of 1100 dates flagged near-singular: the refine pass (one workgroup per date,
