@@ -8,6 +8,8 @@
     torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m llm_driven_multi_factor_model_amd.cli risk ...
     python -m llm_driven_multi_factor_model_amd.cli factors --prices prices.csv --index index.csv \
         --industry sw_industry.csv --out data/
+    python -m llm_driven_multi_factor_model_amd.cli pipeline --prices prices.csv --index index.csv \
+        --industry sw_industry.csv --out results/ [--write-barra data/]   # main.py + demo.py in HBM
     python -m llm_driven_multi_factor_model_amd.cli serve --data barra_data_csi.csv \
         --industry industry_info.csv --port 8000      # POST /risk {"portfolios": [...]}
 
@@ -187,6 +189,47 @@ def cmd_serve(a):
     uvicorn.run(make_app(svc), host=a.host, port=a.port, log_level="info")
 
 
+def cmd_pipeline(a):
+    """The whole job in HBM: loader CSVs -> descriptors -> exposures -> risk model -> the five
+    results CSVs (main.py then demo.py without the barra_data_csi.csv round trip)."""
+    from .models import e2e
+    from .utils.config import preset
+    from .utils.io import write_risk_results
+    _setup_logging()
+    t0 = time.perf_counter()
+    prices, index = e2e.read_price_columns(a.prices, a.index)
+    if prices is None:
+        prices = pd.read_csv(a.prices)
+        index = pd.read_csv(a.index)
+    sw = pd.read_csv(a.industry, dtype={"ts_code": str, "l1_code": str})
+    t_read = time.perf_counter() - t0
+    over = {k: v for k, v in dict(eigen_sims=a.sims, vra_half_life=a.vra_tau, nw_lags=a.nw_q,
+                                  nw_half_life=a.nw_tau).items() if v is not None}
+    cfg = preset(a.preset, **over)
+    model, info, frame, t = e2e.run_pipeline(prices, index, sw, risk_cfg=cfg, device=a.device,
+                                             want_barra=bool(a.write_barra))
+    t0 = time.perf_counter()
+    paths = write_risk_results(model, a.out, long_specific=a.long_specific)
+    if a.write_barra:
+        os.makedirs(a.write_barra, exist_ok=True)
+        frame.to_csv(os.path.join(a.write_barra, "barra_data_csi.csv"), index=False)
+        info.to_csv(os.path.join(a.write_barra, "industry_info.csv"), index=False)
+    t_write = time.perf_counter() - t0
+    compute = {k: round(v, 4) for k, v in t.items() if k.endswith("_s")}
+    log.info("pipeline: panel %d dates x %d stocks x K=%d; read %.3fs, compute %s (%.3fs), "
+             "write %.3fs", model.panel.D, model.panel.N, model.K, t_read, json.dumps(compute),
+             sum(compute.values()), t_write)
+    if a.timings:
+        with open(a.timings, "w") as fh:
+            json.dump({"read_s": t_read, "write_s": t_write, **compute,
+                       "non_io_s": sum(compute.values()), "D": model.panel.D,
+                       "N": model.panel.N, "K": model.K,
+                       "rows": int(model.panel.valid().sum()) if hasattr(model.panel, "valid") else None},
+                      fh)
+    for k, v in paths.items():
+        log.info("wrote %s -> %s", k, v)
+
+
 def cmd_factors(a):
     from .models.factor_engine import run_factor_pipeline
     from .parallel import dist as pdist
@@ -256,6 +299,22 @@ def main(argv=None):
     v.add_argument("--host", default="127.0.0.1")
     v.add_argument("--port", type=int, default=8000)
     v.set_defaults(fn=cmd_serve)
+    q = sub.add_parser("pipeline", help="main.py + demo.py in HBM: loader CSVs -> results/*.csv")
+    q.add_argument("--prices", required=True)
+    q.add_argument("--index", required=True)
+    q.add_argument("--industry", required=True)
+    q.add_argument("--out", default="results")
+    q.add_argument("--write-barra", default=None, metavar="DIR",
+                   help="also write barra_data_csi.csv + industry_info.csv here")
+    q.add_argument("--preset", default="reference")
+    q.add_argument("--sims", type=int, default=None)
+    q.add_argument("--nw-q", type=int, default=None)
+    q.add_argument("--nw-tau", type=float, default=None)
+    q.add_argument("--vra-tau", type=float, default=None)
+    q.add_argument("--long-specific", action="store_true")
+    q.add_argument("--device", default=None)
+    q.add_argument("--timings", default=None, help="write stage timings (JSON) here")
+    q.set_defaults(fn=cmd_pipeline)
     f = sub.add_parser("factors", help="main.py equivalent: descriptors -> Barra exposures")
     f.add_argument("--prices", required=True)
     f.add_argument("--index", required=True)

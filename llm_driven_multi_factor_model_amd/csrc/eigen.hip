@@ -676,6 +676,49 @@ __device__ __forceinline__ double laguerre_toward(double x, double G, double H, 
   return f1 ? c1 : (f2 ? c2 : qnan());
 }
 
+// Division-free Sturm evaluation (bias mode 5): the determinant recurrence of the leading
+// minors f_i(x) = det(T_i - x I) = (a_{i-1} - x) f_{i-1} - b_{i-2}^2 f_{i-2}, with f' and f''
+// carried by the differentiated recurrences.  Same outputs as sturm_gh (Sturm count = sign
+// changes of f_0 .. f_K = #eigenvalues < x, G = f'/f, H = G^2 - f''/f), but every step is
+// fmas off the previous two values (no reciprocal in the dependent chain: ~1/4 of the q-form's
+// chain latency).  The three sequences are rescaled together by a power of two every 4 steps
+// (exact), so they stay in range; they are homogeneous, so G and H are unaffected.
+__device__ __forceinline__ int sturm_gh_p(const double2* tb, int K, double x, double& G,
+                                          double& H) {
+  double f2 = 1.0, f1 = tb[0].x - x;   // f_0, f_1
+  double g2 = 0.0, g1 = -1.0;          // f'_0, f'_1
+  double h2 = 0.0, h1 = 0.0;           // f''_0, f''_1
+  int cnt = f1 < 0.0;
+  auto step = [&](const double2 t) {
+    const double d = t.x - x, b2 = t.y;
+    const double f0 = fma(d, f1, -b2 * f2);
+    const double g0 = fma(d, g1, -fma(b2, g2, f1));
+    const double h0 = fma(d, h1, -fma(b2, h2, 2.0 * g1));
+    cnt += (f0 < 0.0) != (f1 < 0.0);
+    f2 = f1; f1 = f0; g2 = g1; g1 = g0; h2 = h1; h1 = h0;
+  };
+  auto rescale = [&]() {
+    int e;
+    frexp(fmax(fabs(f1), fabs(f2)), &e);
+    const double sc = ldexp(1.0, -e);
+    f1 *= sc; f2 *= sc; g1 *= sc; g2 *= sc; h1 *= sc; h2 *= sc;
+  };
+  int i = 1;
+  for (; i + 3 < K; i += 4) {
+    const double2 t0 = tb[i], t1 = tb[i + 1], t2 = tb[i + 2], t3 = tb[i + 3];
+    step(t0);
+    step(t1);
+    step(t2);
+    step(t3);
+    rescale();
+  }
+  for (; i < K; ++i) step(tb[i]);
+  const double r = 1.0 / f1;
+  G = g1 * r;
+  H = fma(G, G, -h1 * r);
+  return cnt;
+}
+
 // Single-wave workgroups: LDS executes one wave's DS instructions in issue order (they also
 // return in order), so a lane reading what another lane of the SAME wave wrote needs only the
 // compiler to keep program order -- no s_waitcnt / barrier round trip (wsync) per exchange.
@@ -1008,6 +1051,319 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MFA_TRI_WPE)
 
 size_t bias_tri_lds(int K, int KP) { return ((size_t)K * (KP + 1) + 7 * 64 + 2) * sizeof(double); }
 
+// ---------------- lean tridiagonal bias solver (bias mode 4, the default) ----------------
+// The same four phases and the same arithmetic as mc_bias_tri_kernel, re-laid-out for
+// occupancy (the old kernel ran 2 waves / SIMD, bound by 217 VGPRs and 18.7 KB of LDS):
+//   * C_z is symmetric, so lane i's row C_z[i][:] is read as the column C_z[:][i]: K coalesced
+//     global loads (L2-resident, shared by every date of sim m), no LDS staging area;
+//   * the reflector u_s is stored only over the live column range [8 floor(s/8), KP) of its
+//     8-step group (packed rows, 16-B aligned) and the tridiagonalisation broadcasts u from that
+//     row (no separate broadcast buffer): 12.3 KB of LDS at K = 42;
+//   * the twisted factorisation keeps ONLY the eigenvector registers: the forward pivots are
+//     written into y, the backward pivots are recomputed in a second pass for the part below
+//     the twist instead of being stored (one extra K-step recurrence, 2 x KP fewer VGPRs).
+// waves_per_eu(3) caps the registers at 168 -> 3 waves / SIMD (LDS allows 12 workgroups / CU).
+#ifndef MFA_TRI2_WPE
+#define MFA_TRI2_WPE 3
+#endif
+// LDS reads of an unrolled broadcast loop are issued in batches of 4 x 16 B: without the fence
+// hipcc hoists all ~22 of them (88 VGPRs) above the FMAs, which set the kernel's register peak
+__device__ __forceinline__ void lds_batch() { asm volatile("" ::: "memory"); }
+
+template <int KP>
+__host__ __device__ constexpr int tri2_rows_doubles(int K) {
+  // rows s = 0 .. K-3, row s holds columns [8 floor(s/8), KP)
+  int n = 0;
+  for (int s = 0; s + 2 < K; ++s) n += KP - 8 * (s / 8);
+  return n;
+}
+template <int KP>
+__device__ __forceinline__ int tri2_row_off(int s) {
+  // sum over earlier full groups g' < g of 8 (KP - 8 g') + (s - 8 g)(KP - 8 g)
+  const int g = s >> 3;
+  return 8 * (g * KP - 4 * g * (g - 1)) + (s - 8 * g) * (KP - 8 * g);
+}
+
+template <int KP, bool PF = false>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MFA_TRI2_WPE))) void
+mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* __restrict__ Cz,
+                    const int* __restrict__ dvalid, double* __restrict__ vout) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int d = blockIdx.x / M, m = blockIdx.x % M, lane = threadIdx.x;
+  double* vo = vout + ((size_t)d * M + m) * K;
+  if (!dvalid[d]) {
+    for (int k = lane; k < K; k += 64) vo[k] = qnan();
+    return;
+  }
+  const int nrow = (tri2_rows_doubles<KP>(K) + 1) & ~1;
+  double* R = sm;                          // packed reflector rows
+  double* wb = R + nrow;                   // [64] broadcast w; Sturm counts later
+  double2* tb = (double2*)(wb + 64);       // [64] {alpha_i, beta_{i-1}^2}
+  double* be = (double*)(tb + 64);         // [64] beta_i
+  double* ta = be + 64;                    // [64] tau_s
+  double* dd = ta + 64;                    // [64] sqrt(D0)
+  double* gs = dd + 64;                    // [64] diagonal of A, descending; Laguerre x later
+  const double* d0 = D0 + (size_t)d * K;
+  const double di = lane < K ? sqrt(fmax(d0[lane], 0.0)) : 0.0;
+  dd[lane] = di;
+  lds_order();
+  // lane i's row of A = S C_z S from the coalesced columns of the symmetric C_z
+  const double* c = Cz + (size_t)m * K * K;
+  const int li = lane < K ? lane : 0;
+  double a[KP];
+#pragma unroll
+  for (int j = 0; j < KP; ++j) {
+    a[j] = j < K ? di * c[j * K + li] * dd[j] : 0.0;
+    if ((j & 7) == 7) lds_batch();  // 8 loads in flight, not all 44 (register peak)
+  }
+  {
+    const double g = lane < K ? di * c[li * K + li] * di : 0.0;
+    wb[lane] = g;
+    lds_order();
+    if (lane < K) {  // descending rank of the diagonal (ties by index): initial guesses
+      int rank = 0;
+      for (int j = 0; j < K; ++j) {
+        const double h = wb[j];
+        rank += (h > g) || (h == g && j < lane);
+      }
+      gs[rank] = g;
+    }
+    lds_order();
+  }
+  // ---- 1. Householder tridiagonalisation (rows in registers, u broadcast from its row) ----
+  // Step s < K (runtime trip count); for s >= K - 2 the column below the subdiagonal is zero,
+  // so tau = 0 and the step only records alpha_s / beta_s: s = K-2, K-1 are the final 2 x 2.
+  auto steps = [&](auto J0c) {
+    constexpr int J0 = decltype(J0c)::value;
+    for (int s = J0; s < J0 + 8 && s < K; ++s) {
+      double xs = a[J0];
+#pragma unroll
+      for (int k = 1; k < 8; ++k)
+        if (J0 + k < KP) {
+          double t = a[J0 + k];
+          asm volatile("" : "+v"(t));
+          xs = s == J0 + k ? t : xs;
+        }
+      const bool act = lane > s && lane < K;
+      const double x = act ? xs : 0.0;
+      const double x0 = s + 1 < 64 ? readlane(xs, s + 1) : 0.0;
+      const double sig = wave_total(lane > s + 1 && lane < K ? x * x : 0.0);
+      const double alpha = readlane(xs, s);
+      double u = 0.0, tau = 0.0, beta = x0;
+      if (sig != 0.0) {
+        const double nrm = sqrt(fma(x0, x0, sig));
+        beta = x0 >= 0.0 ? -nrm : nrm;
+        tau = 1.0 / (nrm * (nrm + fabs(x0)));
+        u = act ? (lane == s + 1 ? x0 - beta : x) : 0.0;
+      }
+      double* us = R + tri2_row_off<KP>(s) - J0;  // us[j], j in [J0, KP)
+      if (s + 2 < K && lane >= J0 && lane < KP) us[lane] = u;  // u_s, zero outside (s, K)
+      if (lane == 0) {
+        tb[s] = double2{alpha, s > 0 ? be[s - 1] * be[s - 1] : 0.0};
+        be[s] = beta;
+        ta[s] = tau;
+      }
+      lds_order();
+      // branch-free: tau = 0 (nothing to reflect) gives u = p = w = 0, and lanes <= s have
+      // u = p = w = 0, so the update is a no-op there (no divergent copies of the row)
+      double p0 = 0.0, p1 = 0.0;
+      // rows s >= K - 2 are not stored (tau = 0 there): read the group's first row instead,
+      // finite values times u = w = p = 0
+      if (s + 2 >= K) us = R + tri2_row_off<KP>(J0) - J0;
+#pragma unroll
+      for (int j = J0; j < KP; j += 2) {
+        const double2 uu = *(const double2*)(us + j);
+        p0 = fma(a[j], uu.x, p0);
+        p1 = fma(a[j + 1], uu.y, p1);
+        if (((j - J0) & 7) == 6) lds_batch();
+      }
+      const double p = act ? tau * (p0 + p1) : 0.0;
+      const double kk = 0.5 * tau * wave_total(u * p);
+      const double w = p - kk * u;
+      wb[lane] = w;
+      lds_order();
+#pragma unroll
+      for (int j = J0; j < KP; j += 2) {
+        const double2 ww = *(const double2*)(wb + j), uu = *(const double2*)(us + j);
+        a[j] -= fma(u, ww.x, w * uu.x);
+        a[j + 1] -= fma(u, ww.y, w * uu.y);
+        if (((j - J0) & 7) == 6) lds_batch();
+      }
+      lds_order();
+    }
+  };
+  static_assert(KP % 4 == 0, "KP: multiple of 4");
+  [&]<int... G>(std::integer_sequence<int, G...>) {
+    (steps(std::integral_constant<int, 8 * G>{}), ...);
+  }(std::make_integer_sequence<int, (KP + 7) / 8>{});
+  lds_order();
+  // ---- 2. eigenvalue of rank `lane` (descending): as mc_bias_tri_kernel ----
+  double lo_l = 0.0, hi_l = 0.0, b2max = 0.0;
+  if (lane < K) {
+    const double ad = tb[lane].x;
+    const double r = (lane > 0 ? fabs(be[lane - 1]) : 0.0) + (lane + 1 < K ? fabs(be[lane]) : 0.0);
+    lo_l = ad - r;
+    hi_l = ad + r;
+    b2max = tb[lane].y;
+  } else {
+    lo_l = tb[0].x;
+    hi_l = tb[0].x;
+  }
+  const double gl = wave_min(lo_l), gu = wave_max(hi_l);
+  const double tnorm = fmax(fabs(gl), fabs(gu));
+  const double pivmin = 2.2250738585072014e-308 * fmax(1.0, wave_max(b2max));
+  constexpr double kEps = 2.220446049250313e-16;
+  const double abstol = 1e-22 * tnorm + pivmin;
+  const int jt = K - 1 - lane;
+  double lo = gl - 2.0 * kEps * tnorm - pivmin, hi = gu + 2.0 * kEps * tnorm + pivmin;
+  double x = lane < K ? fmin(fmax(gs[lane], lo), hi) : 0.5 * (lo + hi);
+  double G = 0.0, H = 0.0;
+  auto sturm = [&](double xx) {
+    if constexpr (PF) return sturm_gh_p(tb, K, xx, G, H);
+    else return sturm_gh(tb, K, xx, pivmin, G, H);
+  };
+  int cnt = sturm(x);
+  double* xsv = gs;  // each lane read its own gs slot above
+  int* csv = (int*)wb;
+  xsv[lane] = x;
+  csv[lane] = cnt;
+  lds_order();
+  for (int l = 0; l < K; ++l) {
+    const double xl = xsv[l];
+    const int cl = csv[l];
+    if (cl <= jt) lo = fmax(lo, xl); else hi = fmin(hi, xl);
+  }
+  double lam = x;
+  if (lane < K) {
+    int prev = -1;
+    double sprev = __builtin_inf();
+    for (int it = 0; it < 256; ++it) {
+      bool lag = false;
+      double xn = 0.0;
+      if (cnt == jt || cnt == jt + 1) {
+        xn = laguerre_toward(x, G, H, K, cnt == jt);
+        double st = fabs(xn - x);
+        if (prev == cnt && st >= 1.5 * sprev) {
+          xn = fma(8.0, xn - x, x);
+          st *= 8.0;
+        }
+        lag = __builtin_isfinite(xn) && xn >= lo && xn <= hi;
+        if (lag && prev == cnt && st <= 1e-9 * fabs(x) && st <= 0.25 * sprev) { x = xn; break; }
+        sprev = lag ? st : __builtin_inf();
+      }
+      if (!lag) { xn = 0.5 * (lo + hi); sprev = __builtin_inf(); }
+      if (hi - lo <= 2.0 * kEps * (fabs(lo) + fabs(hi)) + abstol) { x = 0.5 * (lo + hi); break; }
+      prev = lag ? cnt : -1;
+      x = xn;
+      cnt = sturm(x);
+      if (cnt <= jt) lo = x; else hi = x;
+    }
+    lam = x;
+  }
+  // ---- 3. eigenvector of T at lam: twisted factorisation in the y registers only ----
+  double y[KP];
+  if (lane < K) {
+    double dp = 0.0;
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {  // forward pivots -> y
+      if (i < K) {
+        const double2 t = tb[i];
+        dp = guard_pivot(i == 0 ? t.x - lam : (t.x - lam) - t.y * rcp_nr(dp), pivmin);
+      }
+      y[i] = i < K ? dp : 0.0;
+    }
+    double dm = 0.0, gmin = 0.0;
+    int r = K - 1;
+#pragma unroll
+    for (int i = KP - 1; i >= 0; --i) {  // backward pivots on the fly: the twist index r
+      if (i < K) {
+        const double ai = tb[i].x - lam;
+        dm = guard_pivot(i == K - 1 ? ai : ai - tb[i + 1].y * rcp_nr(dm), pivmin);
+        const double g = fabs(y[i] + dm - ai);
+        if (i == K - 1 || g < gmin) { gmin = g; r = i; }
+      }
+    }
+    double cz = 1.0, nrm = 1.0;
+#pragma unroll
+    for (int i = KP - 1; i >= 0; --i) {  // below the twist: y_i = -beta_i y_{i+1} / P_i
+      if (i < r) {
+        cz = -be[i] * cz * rcp_nr(y[i]);
+        nrm = fma(cz, cz, nrm);
+        y[i] = cz;
+      }
+    }
+    dm = 0.0;
+#pragma unroll
+    for (int i = KP - 1; i >= 0; --i) {  // above the twist: recompute Q_i into y_i
+      if (i < K && i > r) {
+        const double ai = tb[i].x - lam;
+        dm = guard_pivot(i == K - 1 ? ai : ai - tb[i + 1].y * rcp_nr(dm), pivmin);
+        y[i] = dm;
+      }
+    }
+    cz = 1.0;
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {
+      if (i == r) y[i] = 1.0;
+      if (i > r && i < K) {
+        cz = -be[i - 1] * cz * rcp_nr(y[i]);
+        nrm = fma(cz, cz, nrm);
+        y[i] = cz;
+      }
+      if (i >= K) y[i] = 0.0;
+    }
+    const double sc = rsq_nr(nrm);
+#pragma unroll
+    for (int i = 0; i < KP; ++i) y[i] *= sc;
+  } else {
+#pragma unroll
+    for (int i = 0; i < KP; ++i) y[i] = 0.0;
+  }
+  // ---- 4. back-transform with the packed reflector rows and the bias ratio ----
+  auto back = [&](auto J0c, int s_hi) {
+    constexpr int J0 = decltype(J0c)::value;
+    for (int s = s_hi; s >= J0; --s) {
+      if (s + 2 >= K) continue;
+      const double tau = ta[s];
+      if (tau == 0.0) continue;
+      const double* us = R + tri2_row_off<KP>(s) - J0;
+      double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+      for (int j = J0; j < KP; j += 2) {
+        const double2 uu = *(const double2*)(us + j);
+        t0 = fma(uu.x, y[j], t0);
+        t1 = fma(uu.y, y[j + 1], t1);
+        if (((j - J0) & 7) == 6) lds_batch();
+      }
+      const double f = tau * (t0 + t1);
+#pragma unroll
+      for (int j = J0; j < KP; j += 2) {
+        const double2 uu = *(const double2*)(us + j);
+        y[j] = fma(-f, uu.x, y[j]);
+        y[j + 1] = fma(-f, uu.y, y[j + 1]);
+        if (((j - J0) & 7) == 6) lds_batch();
+      }
+    }
+  };
+  [&]<int... G>(std::integer_sequence<int, G...>) {
+    constexpr int NG = (KP + 7) / 8;
+    (back(std::integral_constant<int, 8 * (NG - 1 - G)>{}, 8 * (NG - 1 - G) + 7), ...);
+  }(std::make_integer_sequence<int, (KP + 7) / 8>{});
+  if (lane < K) {
+    double v = 0.0;
+#pragma unroll
+    for (int j = 0; j < KP; ++j)
+      if (j < K) v = fma(dd[j] * dd[j], y[j] * y[j], v);
+    vo[lane] = v / lam;
+  }
+}
+
+size_t bias_tri2_lds(int K, int KP) {
+  int n = 0;
+  for (int s = 0; s + 2 < K; ++s) n += KP - 8 * (s / 8);
+  return ((size_t)((n + 1) & ~1) + 64 + 128 + 4 * 64) * sizeof(double);
+}
+
 // ---------------- pair-block Jacobi WITH eigenvectors (batched eigh of F0) ----------------
 // Same tournament-position scheme as jacobi_pairs, carrying packed A and the full eigenvector
 // matrix V [K][Ke] whose COLUMNS are positions: a round's column rotation of V uses the same
@@ -1247,6 +1603,27 @@ MFA_API void mfa_eigen_set_bias_mode(int mode) { g_bias_mode = mode; }
 // Householder-tridiagonal solver: KP = K rounded up to an instantiated register width.
 bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, const int* dvalid,
                      double* ws, hipStream_t s) {
+  if (g_bias_mode == 4 || g_bias_mode == 5) {
+#define MFA_TRI2(KP_)                                                                        \
+    if (K <= KP_) {                                                                        \
+      if (g_bias_mode == 5)                                                                \
+        hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, true>), dim3(D * M), dim3(64),        \
+                           bias_tri2_lds(K, KP_), s, D0, K, M, Cz, dvalid, ws);            \
+      else                                                                                 \
+        hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, false>), dim3(D * M), dim3(64),       \
+                           bias_tri2_lds(K, KP_), s, D0, K, M, Cz, dvalid, ws);            \
+      return true;                                                                         \
+    }
+    MFA_TRI2(8)
+    MFA_TRI2(16)
+    MFA_TRI2(24)
+    MFA_TRI2(32)
+    MFA_TRI2(44)
+    MFA_TRI2(48)
+    MFA_TRI2(64)
+#undef MFA_TRI2
+    return false;
+  }
 #define MFA_TRI(KP_)                                                                         \
   if (K <= KP_) {                                                                          \
     hipLaunchKernelGGL((mc_bias_tri_kernel<KP_>), dim3(D * M), dim3(64), bias_tri_lds(K, KP_), s, \
@@ -1277,7 +1654,7 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
 
 #define MFA_BIAS_LAUNCH(NBV_)                                                                   \
   {                                                                                            \
-    if (g_bias_mode == 3 || (g_bias_mode > 40 && g_bias_mode < 60))                            \
+    if ((g_bias_mode >= 3 && g_bias_mode <= 5) || (g_bias_mode > 40 && g_bias_mode < 60))      \
       launch_bias_tri(D0, D, K, M, Cz, dvalid, ws, s);                                         \
     else if (g_bias_mode == 1)                                                                 \
       hipLaunchKernelGGL((mc_bias_split_kernel<NBV_, 1, double>), dim3(D * M), dim3(64),       \

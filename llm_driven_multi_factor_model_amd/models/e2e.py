@@ -1,0 +1,352 @@
+"""In-HBM end-to-end job: prices -> descriptors -> Barra exposures -> risk model -> results.
+
+The reference runs two programs joined by a CSV file: ``Barra_factor_cal/main.py:42-158``
+writes ``barra_data_csi.csv`` and ``Barra-master/demo.py:22-96`` reads it back, one-hot encodes
+the industries, drops NaN rows and runs ``MFM``.  Here the whole job stays on the device:
+
+1. :class:`DeviceFactorEngine` builds the master panel (sorted by stock, then date) from the
+   native CSV reader's columnar buffers with device sorts: stock codes are fixed-width bytes
+   compared as big-endian integers (lexicographic = the reference's string order), dates are
+   YYYYMMDD integers, and no per-row Python object is ever created (the pandas master frame
+   of :class:`FactorEngine` cost ~70 % of the factor pipeline's host time);
+2. descriptors and post-processing run on device tensors (``factor_engine.postprocess_columns``);
+3. :func:`risk_panel` turns the exported columns into a :class:`RiskPanel` with the demo.py
+   semantics (t+1 return, industry id against ``industry_info``, rows with any NaN dropped,
+   dates / stocks that keep at least one row) by scattering rows into the [D, Q, N] grid;
+4. :class:`RiskModel` runs its four stages and ``write_risk_results`` writes the five CSVs.
+
+The panel equals the one ``panel_from_barra_csv`` builds from the exported CSV bit for bit
+(every value is a float32 descriptor widened to float64, which the CSV round trip preserves),
+so results equal the two-step path.  ``barra_data_csi.csv`` is written only on request.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import time
+
+import numpy as np
+import pandas as pd
+import torch
+
+from ..ops import rolling as RL
+from ..utils.config import FactorConfig, RiskConfig
+from .factor_engine import (BARRA_OUTPUT_COLUMNS, BARRA_RENAME, FACTORS_TO_RUN, FactorEngine,
+                            next_return, postprocess_columns)
+from .panel import RiskPanel
+
+log = logging.getLogger("mfa.e2e")
+
+PRICE_STRING_COLS = ("ts_code",)
+PRICE_DATE_COLS = ("trade_date", "end_date")
+STYLE_COLUMNS = BARRA_OUTPUT_COLUMNS[5:]  # size ... leverage (demo.py's Q = 10 styles)
+
+
+class NeedsPandasPath(Exception):
+    """Input the device path does not model (duplicate (stock, date) rows, a stock whose
+    statement runs break the point-in-time order): use :class:`FactorEngine`."""
+
+
+def _s16_keys(a: np.ndarray):
+    """(hi, lo) int64 keys of fixed-width byte strings whose numeric order is the strings'
+    lexicographic order (big-endian words; ASCII keeps the sign bit clear)."""
+    a = np.ascontiguousarray(a, dtype="S16")
+    w = a.view(">u8").reshape(-1, 2)
+    return w[:, 0].astype(np.int64), w[:, 1].astype(np.int64)
+
+
+def _unique_pairs(hi: torch.Tensor, lo: torch.Tensor):
+    """Sorted unique (hi, lo) pairs on the device: (codes per row, index of one row per
+    unique key, in key order)."""
+    o1 = torch.argsort(lo, stable=True)
+    perm = o1[torch.argsort(hi[o1], stable=True)]
+    hs, ls = hi[perm], lo[perm]
+    new = torch.ones(hs.numel(), dtype=torch.bool, device=hs.device)
+    if hs.numel() > 1:
+        new[1:] = (hs[1:] != hs[:-1]) | (ls[1:] != ls[:-1])
+    rank = torch.cumsum(new.to(torch.int64), 0) - 1
+    codes = torch.empty_like(rank)
+    codes[perm] = rank
+    return codes, perm[new]
+
+
+def _ymd_to_datetime64(v: np.ndarray) -> np.ndarray:
+    return pd.to_datetime(pd.Series(v.astype(np.int64)).astype(str), format="%Y%m%d").to_numpy(
+        dtype="datetime64[ns]")
+
+
+class DeviceFactorEngine(FactorEngine):
+    """:class:`FactorEngine` whose master panel is built on the device from columnar arrays.
+
+    ``prices``: {column: ndarray} with ``ts_code`` as ``S16`` bytes, ``trade_date`` (and
+    ``end_date``) as int YYYYMMDD (-1 = missing), numeric columns float64 — the layout of
+    ``utils.native_io.read_columns``.  ``index``: {``trade_date``: int YYYYMMDD, ``close``}.
+    Same descriptors as ``FactorEngine(prices_df, index_df)`` on the equivalent frames (test:
+    ``tests/test_e2e.py``); ``master`` is None (no pandas frame).
+    """
+
+    def __init__(self, prices: dict, index: dict, device=None, config: FactorConfig | None = None):
+        self.cfg = config or FactorConfig()
+        self.device = torch.device(device) if device is not None else torch.device(
+            os.environ.get("MFA_DEVICE") or ("cuda:0" if torch.cuda.is_available() else "cpu"))
+        t0 = time.perf_counter()
+        self.master = None
+        self._prepare_arrays(prices, index)
+        self.prep_s = time.perf_counter() - t0
+        self.own = None
+
+    def _prepare_arrays(self, prices: dict, index: dict) -> None:
+        dev = self.device
+        hi, lo = (torch.from_numpy(x).to(dev) for x in _s16_keys(prices["ts_code"]))
+        scodes, srep = _unique_pairs(hi, lo)
+        td = torch.from_numpy(np.asarray(prices["trade_date"], dtype=np.int64)).to(dev)
+        if bool((td < 0).any()):
+            raise NeedsPandasPath("missing trade_date")
+        dvals, dcodes = torch.unique(td, sorted=True, return_inverse=True)
+        D = int(dvals.numel())
+        key = scodes * D + dcodes
+        R = int(key.numel())
+        if R > 1 and not bool((key[1:] >= key[:-1]).all()):
+            order = torch.argsort(key, stable=True)      # _prepare_data's (ts_code, trade_date) sort
+            key = key[order]
+        else:
+            order = None
+        if R > 1 and bool((key[1:] == key[:-1]).any()):
+            raise NeedsPandasPath("duplicate (ts_code, trade_date) rows")
+        perm = (lambda x: x[order]) if order is not None else (lambda x: x)
+        self.R, self.D = R, D
+        names = np.asarray(prices["ts_code"], dtype="S16")[srep.cpu().numpy()]
+        self.N = int(names.size)
+        self.stock_names = pd.Index(names.astype("U16").astype(object))
+        dv = dvals.cpu().numpy()
+        self.date_ints = dv
+        self.date_names = pd.Index(np.array([f"{d // 10000:04d}/{d // 100 % 100:02d}/{d % 100:02d}"
+                                             for d in dv], dtype=object))
+        self.stock_id = perm(scodes).to(torch.int32)
+        self.date_id = perm(dcodes).to(torch.int32)
+        self.seg_lo = RL.seg_lo_from_codes(self.stock_id)
+        self.grid_idx = self.date_id.long() * self.N + self.stock_id.long()
+        # market_ret: the index close's pct_change (float64), looked up by date, then float32 as
+        # every loaded column (load_data.py:18-21, Q27)
+        it = np.asarray(index["trade_date"], dtype=np.int64)
+        ic = np.asarray(index["close"], dtype=np.float64)
+        if len(np.unique(it)) != len(it):
+            raise NeedsPandasPath("duplicate index dates")
+        io = np.argsort(it, kind="stable")
+        it, ic = it[io], ic[io]
+        mr_idx = np.full(len(ic), np.nan)
+        if len(ic) > 1:
+            mr_idx[1:] = ic[1:] / ic[:-1] - 1.0
+        pos = np.searchsorted(it, dv)
+        hit = (pos < len(it)) & (it[np.minimum(pos, len(it) - 1)] == dv)
+        mr_date = np.where(hit, mr_idx[np.minimum(pos, len(it) - 1)], np.nan)
+        mr = torch.from_numpy(mr_date).to(dev)[self.date_id.long()]
+        self.cols = {}
+        for c in self.NUMERIC:
+            if c in prices:
+                x = torch.from_numpy(np.asarray(prices[c], dtype=np.float64)).to(dev)
+                self.cols[c] = perm(x).to(torch.float32)
+        self.cols["market_ret"] = mr.to(torch.float32)
+        self.cols["ret"], self.cols["log_ret"] = RL.returns(self.cols["close"], self.seg_lo)
+        self.end_date = None
+        if "end_date" in prices:
+            e = torch.from_numpy(np.asarray(prices["end_date"], dtype=np.int64)).to(dev)
+            self.end_date = perm(e)
+
+    # statement-row TTM (factor_calculator.py:392-410) with integer end dates on the device
+    def compute_earnings_yield(self):
+        if not (self._need("n_cashflow_act", "total_mv", "pe_ttm") and self.end_date is not None):
+            return None
+        dev = self.device
+        e = torch.where(self.end_date < 0, torch.full_like(self.end_date, 2 ** 62), self.end_date)
+        sc = self.stock_id.to(torch.int64)
+        v = self.cols["n_cashflow_act"].double()  # float32-loaded like every column
+        ds, de = sc[1:] - sc[:-1], e[1:] - e[:-1]
+        start = torch.ones(self.R, dtype=torch.bool, device=dev)
+        start[1:] = (ds != 0) | (de != 0)
+        if bool(((ds == 0) & (de < 0)).any()):
+            # a restatement moved end_date backwards: distinct (stock, end_date) rows by sort
+            key = sc * (2 ** 40) + torch.clamp(e, max=2 ** 40 - 1)
+            uk, inv = torch.unique(key, sorted=True, return_inverse=True)
+            first = torch.full((uk.numel(),), self.R, dtype=torch.int64, device=dev)
+            first = first.scatter_reduce(0, inv, torch.arange(self.R, device=dev), reduce="amin")
+            seg_codes = (uk // (2 ** 40)).to(torch.int32)
+        else:
+            inv = torch.cumsum(start.to(torch.int64), 0) - 1
+            first = torch.nonzero(start).flatten()
+            seg_codes = sc[first].to(torch.int32)
+        vf = v[first]
+        vb = vf[inv]
+        if not bool(((v == vb) | (v.isnan() & vb.isnan())).all()):
+            raise NeedsPandasPath("several cash-flow values for one (stock, end_date)")
+        ttm = RL.rolling_sum(vf.float(), RL.seg_lo_from_codes(seg_codes), 4, 4).double()[inv]
+        mv = self.cols["total_mv"].double()
+        nan = torch.full_like(mv, float("nan"))
+        cetop = torch.where((mv > 0) & (ttm > 0), ttm / mv, nan)  # unit mix-up kept (quirk Q17)
+        pe = self.cols["pe_ttm"].double()
+        etop = torch.where(pe > 0, 1.0 / pe, nan)
+        return {"CETOP": cetop.float(), "ETOP": etop.float()}
+
+
+def industry_info(eng: FactorEngine, sw_industry: pd.DataFrame) -> tuple[pd.DataFrame, np.ndarray]:
+    """main.py:129-137 ``industry_info`` (first-seen stock order, one row per industry) and
+    each engine stock's SW-L1 code (object array, NaN without membership)."""
+    keys = np.asarray(eng.stock_names, dtype=object)
+    pos = pd.Index(sw_industry["ts_code"].astype(str)).get_indexer(keys)
+    l1 = sw_industry["l1_code"].to_numpy(dtype=object)
+    l1_stock = np.where(pos >= 0, l1[np.maximum(pos, 0)], np.nan).astype(object)
+    stk = pd.DataFrame({"ts_code": pd.unique(keys)})
+    cols = [c for c in ["ts_code", "l1_code", "l1_name", "in_date"] if c in sw_industry.columns]
+    sw = sw_industry[cols].copy()
+    sw["ts_code"] = sw["ts_code"].astype(str)
+    info = stk.merge(sw, on="ts_code", how="left")
+    info = info.drop_duplicates(subset=[c for c in ["l1_code", "l1_name"] if c in info.columns]).rename(
+        columns={"l1_code": "code", "l1_name": "industry_names", "in_date": "start_date"})
+    info = info[[c for c in ["code", "industry_names", "start_date"] if c in info.columns]]
+    return info.reset_index(drop=True), l1_stock
+
+
+def export_columns(col: dict, nxt: torch.Tensor) -> dict:
+    """The numeric barra_data_csi.csv columns (main.py:98-112 rename) as float64 device
+    tensors: capital, ret (t+1) and the ten styles."""
+    inv = {v: k for k, v in BARRA_RENAME.items()}
+    out = {}
+    for c in BARRA_OUTPUT_COLUMNS:
+        s0 = inv.get(c, c)
+        if s0 == "ret":
+            out[c] = nxt
+        elif s0 not in ("ts_code", "trade_date", "l1_code") and s0 in col and (s0 == c or c not in col):
+            out[c] = col[s0].double()
+    return out
+
+
+def risk_panel(eng: FactorEngine, cols: dict, l1_stock: np.ndarray, info: pd.DataFrame,
+               dtype=torch.float64) -> RiskPanel:
+    """demo.py:22-35 on device tensors: rows with any NaN (or no industry in ``info``) are
+    dropped, industries become ids into ``info``'s rows, and the rows are scattered into the
+    [D, Q, N] panel over the dates / stocks that keep at least one row (the panel
+    ``panel_from_barra_csv`` builds from the exported CSV)."""
+    dev = eng.device
+    missing = [c for c in ["capital", "ret", *STYLE_COLUMNS] if c not in cols]
+    if missing:
+        raise ValueError(f"exposure columns missing for the risk panel: {missing}")
+    codes = info["code"].astype(str).to_numpy()
+    cpos = {c: i for i, c in enumerate(codes)}
+    ind_stock = np.array([cpos.get(str(x), -1) if isinstance(x, str) else -1 for x in l1_stock],
+                         dtype=np.int64)
+    ind_row = torch.from_numpy(ind_stock).to(dev)[eng.stock_id.long()]
+    keep = ind_row >= 0
+    for c in ["capital", "ret", *STYLE_COLUMNS]:
+        keep &= torch.isfinite(cols[c])
+    sid, did = eng.stock_id.long(), eng.date_id.long()
+    dk = torch.zeros(eng.D, dtype=torch.bool, device=dev)
+    sk = torch.zeros(eng.N, dtype=torch.bool, device=dev)
+    dk[did[keep]] = True
+    sk[sid[keep]] = True
+    dnew = torch.cumsum(dk.to(torch.int64), 0) - 1
+    snew = torch.cumsum(sk.to(torch.int64), 0) - 1
+    Dp, Np = int(dk.sum()), int(sk.sum())
+    rows = torch.nonzero(keep).flatten()
+    d_r, s_r = dnew[did[rows]], snew[sid[rows]]
+    flat = d_r * Np + s_r
+    Q = len(STYLE_COLUMNS)
+    nan = float("nan")
+    cap = torch.full((Dp * Np,), nan, dtype=dtype, device=dev)
+    ret = torch.full((Dp * Np,), nan, dtype=dtype, device=dev)
+    cap[flat] = cols["capital"][rows].to(dtype)
+    ret[flat] = cols["ret"][rows].to(dtype)
+    sty = torch.full((Dp, Q, Np), nan, dtype=dtype, device=dev)
+    sflat = d_r * (Q * Np) + s_r
+    sv = sty.view(-1)
+    for q, c in enumerate(STYLE_COLUMNS):
+        sv[sflat + q * Np] = cols[c][rows].to(dtype)
+    ind = torch.full((Dp * Np,), -1, dtype=torch.int16, device=dev)
+    ind[flat] = ind_row[rows].to(torch.int16)
+    dmask, smask = dk.cpu().numpy(), sk.cpu().numpy()
+    dates = _ymd_to_datetime64(eng.date_ints[dmask]) if hasattr(eng, "date_ints") else \
+        pd.to_datetime(pd.Index(np.asarray(eng.date_names)[dmask]), format="%Y/%m/%d").to_numpy(
+            dtype="datetime64[ns]")
+    return RiskPanel(styles=sty, cap=cap.view(Dp, Np), ret=ret.view(Dp, Np),
+                     ind=ind.view(Dp, Np) if len(info) else None, P=len(info), dates=dates,
+                     stocks=np.asarray(eng.stock_names, dtype=object)[smask],
+                     style_names=list(STYLE_COLUMNS),
+                     industry_names=list(info["industry_names"].astype(str).to_numpy()))
+
+
+def barra_frame(eng: FactorEngine, cols: dict, l1_stock: np.ndarray) -> pd.DataFrame:
+    """The barra_data_csi.csv frame (only built when requested: it is I/O, not compute)."""
+    names = [c for c in BARRA_OUTPUT_COLUMNS if c in cols]
+    host = torch.stack([cols[c] for c in names]).cpu().numpy()
+    final = pd.DataFrame(host.T, columns=names, copy=False)
+    sid = eng.stock_id.cpu().numpy()
+    did = eng.date_id.cpu().numpy()
+    final.insert(0, "date", np.asarray(eng.date_names, dtype=object)[did])
+    final.insert(1, "stocknames", np.asarray(eng.stock_names, dtype=object)[sid])
+    final.insert(4, "industry", pd.Series(l1_stock[sid], dtype=object))
+    return final[[c for c in BARRA_OUTPUT_COLUMNS if c in final.columns]]
+
+
+def read_price_columns(prices_csv: str, index_csv: str):
+    """Columnar parse of the loader's CSVs by the native reader: codes as S16 bytes, dates as
+    YYYYMMDD ints, everything else float64.  None if the native reader is unavailable."""
+    from ..utils import native_io
+    types = {c: 1 for c in PRICE_STRING_COLS}
+    types.update({c: 2 for c in PRICE_DATE_COLS})
+    p = native_io.read_columns(prices_csv, types)
+    i = native_io.read_columns(index_csv, {"ts_code": 1, "trade_date": 2})
+    return p, i
+
+
+def _columns_from_frames(prices_df: pd.DataFrame, index_df: pd.DataFrame):
+    """The columnar layout of :class:`DeviceFactorEngine` from pandas frames (tests, API)."""
+    def ymd(s):
+        d = pd.to_datetime(s)
+        out = (d.dt.year * 10000 + d.dt.month * 100 + d.dt.day).to_numpy(dtype=np.float64)
+        return np.where(np.isnan(out), -1, out).astype(np.int64)
+    p = {}
+    for c in prices_df.columns:
+        if c == "ts_code":
+            p[c] = prices_df[c].astype(str).to_numpy().astype("S16")
+        elif c in PRICE_DATE_COLS:
+            p[c] = ymd(prices_df[c])
+        else:
+            try:
+                p[c] = prices_df[c].to_numpy(dtype=np.float64, na_value=np.nan)
+            except (TypeError, ValueError):
+                continue
+    i = {"trade_date": ymd(index_df["trade_date"]),
+         "close": index_df["close"].to_numpy(dtype=np.float64)}
+    return p, i
+
+
+def run_pipeline(prices, index, sw_industry: pd.DataFrame, risk_cfg: RiskConfig | None = None,
+                 factor_cfg: FactorConfig | None = None, factors=None, device=None,
+                 want_barra: bool = False, sync: bool = True):
+    """The whole job in HBM.  ``prices`` / ``index``: columnar dicts (``read_price_columns``)
+    or pandas frames.  Returns ``(model, info, barra_frame or None, timings)``; the model has
+    run all four stages."""
+    from .risk_model import RiskModel
+    t = {}
+    t0 = time.perf_counter()
+    if isinstance(prices, pd.DataFrame):
+        prices, index = _columns_from_frames(prices, index)
+    eng = DeviceFactorEngine(prices, index, device=device, config=factor_cfg)
+    res = eng.compute(factors or FACTORS_TO_RUN)
+    t["descriptors_s"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    col = postprocess_columns(eng, res, eng.cfg)
+    nxt = next_return(eng, col["ret"])
+    cols = export_columns(col, nxt)
+    info, l1_stock = industry_info(eng, sw_industry)
+    panel = risk_panel(eng, cols, l1_stock, info)
+    if sync and eng.device.type == "cuda":
+        torch.cuda.synchronize(eng.device)
+    t["exposures_to_panel_s"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    model = RiskModel(panel, risk_cfg or RiskConfig()).run()
+    if sync and eng.device.type == "cuda":
+        torch.cuda.synchronize(eng.device)
+    t["risk_model_s"] = time.perf_counter() - t0
+    t["kernel_ms"] = getattr(eng, "timings", {})
+    frame = barra_frame(eng, cols, l1_stock) if want_barra else None
+    return model, info, frame, t

@@ -513,18 +513,10 @@ def barra_export(processed: pd.DataFrame, sw_industry: pd.DataFrame, _merge_path
     return final, info
 
 
-def _pipeline_columnar(eng: "FactorEngine", factors, cfg: FactorConfig, sw_industry: pd.DataFrame, t: dict):
-    """Single-process fast path of :func:`factor_pipeline` (same output frames, bit for bit):
-    the descriptors stay device tensors through winsorize / composite / orthogonalize on the
-    engine's own (date, stock) grid index (no re-factorisation of string keys), the t+1 return
-    is a shift on stock ids, and the export frame is built once from ONE device->host copy.
-    Mirrors main.py:42-137 (winsorize incl. ret / circ_mv, composites, orthogonalisation,
-    industry merge, t+1 return, rename)."""
-    t0 = time.perf_counter()
-    res = eng.compute(factors)
-    m = eng.master
-    t["descriptors_s"] = t.pop("prep_s", 0.0) + time.perf_counter() - t0
-    t0 = time.perf_counter()
+def postprocess_columns(eng: "FactorEngine", res: dict, cfg: FactorConfig) -> dict:
+    """main.py:71-86 on device tensors in master order: winsorize every non-key column (incl.
+    ret and circ_mv, quirk Q23), the composites, then the orthogonalisation, on the engine's
+    own (date, stock) grid index.  Returns {column: flat tensor}."""
     dev, nan = eng.device, float("nan")
     D, N, idx = eng.D, eng.N, eng.grid_idx
 
@@ -553,13 +545,36 @@ def _pipeline_columnar(eng: "FactorEngine", factors, cfg: FactorConfig, sw_indus
     for target, against in cfg.ortho.items():
         col[target] = take(XR.ols_resid(put(col[target]), [put(col[a]) for a in against],
                                         min_rows=len(against) + 2))
+    return col
+
+
+def next_return(eng: "FactorEngine", ret: torch.Tensor) -> torch.Tensor:
+    """``groupby(ts_code).ret.shift(-1)`` (main.py:99, the t+1 return) in master order."""
+    ret = ret.double()
+    sid = eng.stock_id
+    nxt = torch.full_like(ret, float("nan"))
+    if eng.R > 1:
+        nxt[:-1] = torch.where(sid[1:] == sid[:-1], ret[1:], ret.new_tensor(float("nan")))
+    return nxt
+
+
+def _pipeline_columnar(eng: "FactorEngine", factors, cfg: FactorConfig, sw_industry: pd.DataFrame, t: dict):
+    """Single-process fast path of :func:`factor_pipeline` (same output frames, bit for bit):
+    the descriptors stay device tensors through winsorize / composite / orthogonalize on the
+    engine's own (date, stock) grid index (no re-factorisation of string keys), the t+1 return
+    is a shift on stock ids, and the export frame is built once from ONE device->host copy.
+    Mirrors main.py:42-137 (winsorize incl. ret / circ_mv, composites, orthogonalisation,
+    industry merge, t+1 return, rename)."""
+    t0 = time.perf_counter()
+    res = eng.compute(factors)
+    m = eng.master
+    t["descriptors_s"] = t.pop("prep_s", 0.0) + time.perf_counter() - t0
+    t0 = time.perf_counter()
+    col = postprocess_columns(eng, res, cfg)
     t["postprocess_s"] = time.perf_counter() - t0
     t0 = time.perf_counter()
     sid = eng.stock_id
-    ret = col["ret"].double()
-    nxt = torch.full_like(ret, nan)  # groupby(ts_code).shift(-1) in master (stock-sorted) order
-    if eng.R > 1:
-        nxt[:-1] = torch.where(sid[1:] == sid[:-1], ret[1:], ret.new_tensor(nan))
+    nxt = next_return(eng, col["ret"])
     inv = {v: k for k, v in BARRA_RENAME.items()}
     names, tens = [], []  # numeric export columns in output order
     for c in BARRA_OUTPUT_COLUMNS:

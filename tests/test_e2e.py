@@ -1,0 +1,126 @@
+"""In-HBM end-to-end job: prices -> descriptors -> exposures -> risk model.
+
+* the device-built master panel (``DeviceFactorEngine``: native columnar buffers, device sorts)
+  gives the same descriptors as the pandas-built ``FactorEngine``;
+* the risk panel handed over in HBM equals the one ``panel_from_barra_csv`` reads back from the
+  exported ``barra_data_csi.csv``, and the risk model's outputs match the two-step path;
+* ``cli pipeline`` writes the five demo.py result files equal to ``cli factors`` + ``cli risk``.
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from llm_driven_multi_factor_model_amd.models import e2e
+from llm_driven_multi_factor_model_amd.models.factor_engine import (FACTORS_TO_RUN, FactorEngine,
+                                                                    factor_pipeline,
+                                                                    synthetic_prices)
+from llm_driven_multi_factor_model_amd.models.risk_model import RiskModel
+from llm_driven_multi_factor_model_amd.utils.config import preset
+from llm_driven_multi_factor_model_amd.utils.io import panel_from_barra_csv
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _data(N=40, T=330, seed=3):
+    prices, index, sw = synthetic_prices(N=N, T=T, seed=seed, n_ind=6, suspend_frac=0.03)
+    # shuffle the rows: the device path must sort like _prepare_data
+    prices = prices.sample(frac=1.0, random_state=1).reset_index(drop=True)
+    sw.loc[sw.index[-1], "l1_code"] = None  # one stock without membership (dropped by demo.py)
+    return prices, index, sw
+
+
+def test_device_master_matches_pandas_master():
+    prices, index, _ = _data()
+    ref = FactorEngine(prices, index, device="cpu")
+    p, i = e2e._columns_from_frames(prices, index)
+    dev = e2e.DeviceFactorEngine(p, i, device="cpu")
+    assert (dev.R, dev.D, dev.N) == (ref.R, ref.D, ref.N)
+    assert list(dev.stock_names) == list(ref.stock_names)
+    assert list(dev.date_names) == list(ref.date_names)
+    torch.testing.assert_close(dev.stock_id, ref.stock_id.to(dev.stock_id.dtype), rtol=0, atol=0)
+    torch.testing.assert_close(dev.date_id, ref.date_id.to(dev.date_id.dtype), rtol=0, atol=0)
+    a, b = ref.compute(FACTORS_TO_RUN), dev.compute(FACTORS_TO_RUN)
+    assert list(a) == list(b)
+    for k in a:
+        torch.testing.assert_close(b[k].double(), a[k].double(), rtol=0, atol=0, equal_nan=True,
+                                   msg=k)
+
+
+def _two_step(prices, index, sw, tmp_path, cfg):
+    final, info, _ = factor_pipeline(prices, index, sw, device="cpu")
+    final.to_csv(tmp_path / "barra_data_csi.csv", index=False)
+    info.to_csv(tmp_path / "industry_info.csv", index=False)
+    panel = panel_from_barra_csv(str(tmp_path / "barra_data_csi.csv"),
+                                 str(tmp_path / "industry_info.csv"))
+    return RiskModel(panel, cfg).run(), final, info
+
+
+def test_hbm_handoff_equals_csv_round_trip(tmp_path):
+    prices, index, sw = _data()
+    cfg = preset("reference", eigen_sims=4)
+    ref, final_ref, info_ref = _two_step(prices, index, sw, tmp_path, cfg)
+    model, info, frame, t = e2e.run_pipeline(prices, index, sw, risk_cfg=cfg, device="cpu",
+                                             want_barra=True)
+    pd.testing.assert_frame_equal(info.reset_index(drop=True), info_ref.reset_index(drop=True))
+    # the exported frame equals main.py's (the columnar export)
+    pd.testing.assert_frame_equal(frame.reset_index(drop=True),
+                                  final_ref.reset_index(drop=True), check_dtype=False)
+    p, q = model.panel, ref.panel
+    assert list(p.stocks) == list(q.stocks) and (p.dates == q.dates).all()
+    for name in ("styles", "cap", "ret"):
+        torch.testing.assert_close(getattr(p, name), getattr(q, name), rtol=0, atol=0,
+                                   equal_nan=True, msg=name)
+    assert torch.equal(p.ind, q.ind) and p.P == q.P
+    assert p.industry_names == q.industry_names and p.style_names == q.style_names
+    for k in ("factor_ret", "r2", "specific_ret", "nw_cov", "eigen_cov", "vra_cov", "vra_lambda"):
+        torch.testing.assert_close(getattr(model, k), getattr(ref, k), rtol=1e-12, atol=1e-15,
+                                   equal_nan=True, msg=k)
+    assert {"descriptors_s", "exposures_to_panel_s", "risk_model_s"} <= set(t)
+
+
+def _cli(*args):
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1")
+    return subprocess.run([sys.executable, "-m", "llm_driven_multi_factor_model_amd.cli", *args],
+                          cwd=ROOT, capture_output=True, text=True, timeout=600, env=env)
+
+
+def test_cli_pipeline_equals_factors_then_risk(tmp_path):
+    prices, index, sw = _data(N=30, T=300, seed=5)
+    d = tmp_path
+    prices.to_csv(d / "prices.csv", index=False)
+    index.to_csv(d / "index.csv", index=False)
+    sw.to_csv(d / "sw.csv", index=False)
+    r = _cli("factors", "--prices", str(d / "prices.csv"), "--index", str(d / "index.csv"),
+             "--industry", str(d / "sw.csv"), "--out", str(d / "data"), "--device", "cpu")
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = _cli("risk", "--data", str(d / "data/barra_data_csi.csv"), "--industry",
+             str(d / "data/industry_info.csv"), "--out", str(d / "res2"), "--sims", "3",
+             "--device", "cpu")
+    assert r.returncode == 0, r.stderr[-3000:]
+    r = _cli("pipeline", "--prices", str(d / "prices.csv"), "--index", str(d / "index.csv"),
+             "--industry", str(d / "sw.csv"), "--out", str(d / "res1"), "--sims", "3",
+             "--device", "cpu", "--timings", str(d / "t.json"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    for f in ("factor_returns.csv", "r_squared.csv", "specific_returns.csv",
+              "final_vol_regime_adj_covariance.csv", "volatility_multiplier_lambda.csv"):
+        a = pd.read_csv(d / "res1" / f, index_col=0)
+        b = pd.read_csv(d / "res2" / f, index_col=0)
+        assert list(a.columns) == list(b.columns) and list(a.index) == list(b.index), f
+        np.testing.assert_allclose(a.to_numpy(np.float64), b.to_numpy(np.float64), rtol=1e-12,
+                                   atol=1e-15, err_msg=f)
+    import json
+    t = json.loads((d / "t.json").read_text())
+    assert t["non_io_s"] > 0 and t["D"] > 0
+
+
+def test_duplicate_rows_need_pandas_path():
+    prices, index, _ = _data(N=5, T=60)
+    prices = pd.concat([prices, prices.iloc[:1]], ignore_index=True)
+    p, i = e2e._columns_from_frames(prices, index)
+    with pytest.raises(e2e.NeedsPandasPath):
+        e2e.DeviceFactorEngine(p, i, device="cpu")
