@@ -15,6 +15,7 @@ from __future__ import annotations
 import argparse
 import concurrent.futures as cf
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -52,11 +53,23 @@ def sources() -> list[Path]:
     return sorted(CSRC.glob("*.hip"))
 
 
+def _local_includes(src: Path, seen: set[Path] | None = None) -> set[Path]:
+    """Headers of csrc/ that `src` includes, transitively (#include "x.h")."""
+    seen = set() if seen is None else seen
+    for m in re.finditer(r'^\s*#\s*include\s+"([^"]+)"', src.read_text(), re.M):
+        h = CSRC / m.group(1)
+        if h.exists() and h not in seen:
+            seen.add(h)
+            _local_includes(h, seen)
+    return seen
+
+
 def _stale(src: Path, obj: Path, headers: list[Path]) -> bool:
     if not obj.exists():
         return True
     t = obj.stat().st_mtime
-    return src.stat().st_mtime > t or any(h.stat().st_mtime > t for h in headers)
+    deps = _local_includes(src) & set(headers)
+    return src.stat().st_mtime > t or any(h.stat().st_mtime > t for h in deps)
 
 
 def _compile(src: Path, obj: Path) -> tuple[Path, str]:

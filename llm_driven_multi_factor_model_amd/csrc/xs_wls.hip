@@ -2,8 +2,11 @@
 // Kernels and algebra: xs_wls_impl.h (reference: Barra-master/mfm/CrossSection.py:12-108).
 #include "xs_wls_impl.h"
 
+MFA_XS_DECLARE_ALL(float)
+
 int g_mfa_xs_mode = 0;
 int g_mfa_xs_chunks = 0;
+int g_mfa_xs_coop = 0;
 
 // Ablation: 0 = fused single-kernel path with the residual prefetch during the wave-0 solve
 // (default), 1 = three separate kernels, 7 = fused without the prefetch.  Applies to both the
@@ -13,6 +16,11 @@ MFA_API void mfa_xs_set_mode(int mode) { g_mfa_xs_mode = mode; }
 // Stock chunks per date for the next calls: 0 = automatic (default: the fused kernel,
 // kXsChunkMinD = 0), > 0 = forced chunk count, < 0 = always one workgroup per date.
 MFA_API void mfa_xs_set_chunks(int S) { g_mfa_xs_chunks = S; }
+
+// Team (cooperative) CS-WLS kernel for the next calls: 0 = off, C > 0 = C chunks per date,
+// < 0 = automatic chunk count (xs_coop_chunks).
+MFA_API void mfa_xs_set_coop(int C) { g_mfa_xs_coop = C; }
+MFA_API int mfa_xs_coop_chunks(int D, int N) { return xs_coop_chunks(D, N); }
 
 // Chunks per date the next mfa_xs_wls / mfa_xs_wls_f64 call on (D, N) will use.
 MFA_API int mfa_xs_chunks(int D, int N) { return xs_chunks(D, N); }
@@ -42,26 +50,6 @@ MFA_API int mfa_xs_wls(const float* X, const float* cap, const float* ret, const
                        void* stream) {
   return xs_wls_dispatch<float>(X, cap, ret, ind, D, N, P, Q, pivot_mode, tol, f, e, r2, stats,
                                 status, ws, stream);
-}
-
-// Timing-only ablation entry (fp32, Q = 10): bit 1 = no segment atomics, bit 2 = no style-Gram
-// FMAs, bit 4 = no residual pass, bit 8 = no solve (fused mode only), 16 = second residual pass.
-MFA_API int mfa_xs_wls_variant(const float* X, const float* cap, const float* ret,
-                               const int16_t* ind, int D, int N, int P, int variant, double* f,
-                               float* e, double* r2, double* stats, int* status, void* ws,
-                               void* stream) {
-  hipStream_t s = (hipStream_t)stream;
-  double* w = (double*)ws;
-  switch (variant) {
-#define MFA_V(vv)                                                                              \
-  case vv:                                                                                     \
-    return (int)launch_q<10, vv, float>(X, cap, ret, ind, D, N, P, 0, 1e-14, f, e, r2, stats, \
-                                        status, w, s);
-    MFA_V(0) MFA_V(1) MFA_V(2) MFA_V(3) MFA_V(4) MFA_V(5) MFA_V(6) MFA_V(7) MFA_V(8)
-    MFA_V(12) MFA_V(13) MFA_V(14) MFA_V(15) MFA_V(16) MFA_V(20)
-#undef MFA_V
-  }
-  return (int)hipErrorInvalidValue;
 }
 
 // Raw moments [D][msize] of this rank's stocks (layout: Layout<Q>, see K1).

@@ -36,8 +36,10 @@
 extern int g_mfa_xs_mode;
 // Stock chunks per date: 0 = automatic (chunked below kXsChunkMinD dates), > 0 forced, < 0 never.
 extern int g_mfa_xs_chunks;
+// Team (cooperative) CS-WLS kernel: 0 = off, > 0 = forced chunks per date, < 0 = automatic.
+extern int g_mfa_xs_coop;
 
-namespace {
+namespace mfa_xs {
 
 using namespace mfa;
 
@@ -753,7 +755,7 @@ __device__ __forceinline__ void solve_body(double* sm, int d, int P, int Pseg, i
     gph = fma(-gpv[u], b[u], gph);
   }
   const bool bad = (st & XS_BAD) != 0;
-  double* fo = fout + (size_t)d * K;
+  double* fo = fout ? fout + (size_t)d * K : nullptr;  // null: coefficients only
   for (int j = lane; j < P; j += 64) {
     const double* p = seg + j * NS;
     const double W = p[0];
@@ -768,14 +770,14 @@ __device__ __forceinline__ void solve_body(double* sm, int d, int P, int Pseg, i
       for (int q = 0; q < Q; ++q) mh = fma(-(p[1 + q] - muv[q] * W) * isig, b[1 + q], mh);
       fj = (mh + aj * gph - kappa * aj * z) * iwv[j];
     }
-    fo[1 + j] = bad ? qnan() : fj;
+    if (fout) fo[1 + j] = bad ? qnan() : fj;
     co[Q + 1 + j] = bad ? qnan() : fj;
   }
-  if (lane == 0) fo[0] = bad ? qnan() : b[0];
+  if (fout && lane == 0) fo[0] = bad ? qnan() : b[0];
 #pragma unroll
   for (int q = 0; q < Q; ++q)
     if (lane == q) {
-      fo[1 + P + q] = bad ? qnan() : b[1 + q];
+      if (fout) fo[1 + P + q] = bad ? qnan() : b[1 + q];
       co[q] = bad ? qnan() : b[1 + q] * isig;  // residual coefficients on RAW styles
     }
   if (lane == 0) {
@@ -783,7 +785,7 @@ __device__ __forceinline__ void solve_body(double* sm, int d, int P, int Pseg, i
 #pragma unroll
     for (int q = 0; q < Q; ++q) cst -= b[1 + q] * isig * muv[q];
     co[Q] = bad ? qnan() : cst;
-    status[d] = st;
+    if (status) status[d] = st;
     if (st_lds) *st_lds = st;
   }
   if (stats) {
@@ -1114,6 +1116,7 @@ __global__ __launch_bounds__(256) void xs_resid_kernel(
 }
 
 // R^2 of every date from its S chunk sums [sum e, sum e^2, sum r, sum r^2, n], in chunk order.
+template <int = 0>
 __global__ __launch_bounds__(256) void xs_r2_combine_kernel(const double* __restrict__ sums, int D,
                                                             int S, const int* __restrict__ status,
                                                             double* __restrict__ r2out) {
@@ -1466,6 +1469,152 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Q <= 10 ? 2
   if constexpr ((VAR & 16) != 0) {  // timing-only: a second residual pass (cache-hit cost)
     __syncthreads();
     resid_body<Q, T>(X, cap, ret, ind, d, N, P, cf_s, (st_s & XS_BAD) != 0, eout, r2out, red);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// Team (cooperative) CS-WLS: C workgroups per date, one stock chunk each, ONE launch.
+//
+// The fused kernel's residual pass re-reads the date's panel slice from HBM: one workgroup
+// streams a whole 490 KB fp64 date, so ~512 dates (~250 MB) are in flight and the slice has
+// mostly left the 256 MB Infinity Cache by the time it is re-read (2.46 GB moved per 1.34 GB
+// compulsory, profiles/r02_xs_cluster_ab.md).  Here a date is split into C chunks on C
+// workgroups that run at the same time; each streams its chunk once into partial raw moments,
+// publishes them, and -- once the whole team has published -- sums the C partials in chunk
+// order (bitwise identical in every member), solves redundantly in wave 0 and re-reads ONLY
+// ITS chunk for the residuals, a few microseconds after streaming it: the re-read is served by
+// the XCD's L2 / the Infinity Cache instead of HBM.  A date also occupies C CUs instead of one,
+// so a 315-date shard (8-GPU strong scaling) fills the chip.
+//
+// Progress guarantee (no co-residency assumption): a workgroup takes a ticket from a global
+// counter when it STARTS, and ticket t is chunk t % C of date t / C.  A workgroup publishes its
+// partial before it waits on anything, and waits only for tickets of its own date.  Tickets are
+// taken in start order, so every date except the one holding the next untaken ticket is fully
+// ticketed; if every resident workgroup were waiting, all would hold tickets of that one date,
+// i.e. at most C - 1 of them -- so any device that can hold C of these workgroups (C <= 8)
+// always has a running one.  Each poll loop is also bounded (XS_COOP_TIMEOUT): the grid drains.
+//
+// Hand-offs (MI355X_MICROARCH.md, inter-workgroup visibility): partial moments and R^2 sums
+// are stored write-through (relaxed agent-scope atomic stores, `sc1`), every storing wave waits
+// vmcnt(0) before the workgroup barrier behind which ONE lane adds to the date's counter; the
+// readers poll that counter with `sc1` loads from one lane and load the payload with `sc1` loads
+// after a workgroup barrier.  No fence (a __threadfence per workgroup measured 4x slower).
+// sync = [ticket | arrive[D] | done[D]] ints, zeroed before every launch (memset node).
+// ------------------------------------------------------------------------------------------
+constexpr int XS_COOP_TIMEOUT = 64;  // status bit: a team wait gave up (results invalid)
+constexpr int kCoopSpin = 1 << 21;
+constexpr int kCoopMaxC = 8;         // chunks (workgroups) per date at most   // poll iterations (s_sleep 4 each, ~0.2 s) before giving up
+
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// one lane: wait until *ctr >= target; false on timeout
+__device__ __forceinline__ bool coop_wait(int* ctr, int target) {
+  for (int it = 0; it < kCoopSpin; ++it) {
+    if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
+    __builtin_amdgcn_s_sleep(4);
+  }
+  return false;
+}
+
+template <int Q, int R, int VAR, typename T>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Q <= 10 ? 2 : MFA_XS_WPE_BIGQ, Q <= 10 ? 2 : MFA_XS_WPE_BIGQ))) void xs_coop_kernel(
+    const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
+    const int16_t* __restrict__ ind, int N, int P, int Pseg, int C, int Cs, int pivot_mode,
+    double tol, double* __restrict__ fout, T* __restrict__ eout, double* __restrict__ r2out,
+    double* __restrict__ stats, int* __restrict__ status, double* __restrict__ mom,
+    double* __restrict__ sums, unsigned long long* __restrict__ okm, int* __restrict__ sync) {
+  __shared__ __attribute__((aligned(16))) char ring[fused_ring_bytes<Q, T>()];
+  __shared__ double cf_s[Q + 1 + 128];
+  __shared__ double red[4][5];
+  __shared__ double rs[5];
+  __shared__ int st_s, tk_s, to_s;
+  extern __shared__ double dyn[];
+  const int tid = threadIdx.x;
+  const int D = (int)gridDim.x / C;
+  if (tid == 0) {
+    tk_s = __hip_atomic_fetch_add(sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    to_s = 0;
+  }
+  __syncthreads();
+  const int t = tk_s, d = t / C, c = t - d * C;
+  const int nb = c * Cs, ne = min(N, nb + Cs);
+  const int MS = Layout<Q, T>::msize(Pseg);
+  double* sm = (double*)ring;
+  unsigned long long* okd = okm + (size_t)d * ((N + kWT - 1) / kWT);
+  moments_body<Q, VAR & 35, R, T>(X, cap, ret, ind, N, Pseg, d, ring, dyn, sm, nb, ne, nullptr, okd);
+  // publish this chunk's partial (write-through), then arrive
+  double* mp = mom + ((size_t)d * C + c) * MS;
+  for (int i = tid; i < MS; i += blockDim.x) st_sc1(mp + i, sm[i]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* arrive = sync + 1 + d;
+  if (tid == 0) {
+    __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (!coop_wait(arrive, C)) to_s = XS_COOP_TIMEOUT;
+  }
+  __syncthreads();
+  // the date's moments: the C partials summed in chunk order (identical bits in every member)
+  // (every load of a thread is issued before the first add: a load -> add chain would pay the
+  // cross-XCD round trip C times per element)
+  const double* md = mom + (size_t)d * C * MS;
+  for (int i0 = tid; i0 < MS; i0 += 2 * blockDim.x) {
+    double v[2][kCoopMaxC];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = i0 + u * (int)blockDim.x;
+#pragma unroll
+      for (int k = 0; k < kCoopMaxC; ++k)
+        v[u][k] = (k < C && i < MS) ? ld_sc1(md + (size_t)k * MS + i) : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = i0 + u * (int)blockDim.x;
+      double s = v[u][0];
+#pragma unroll
+      for (int k = 1; k < kCoopMaxC; ++k)
+        if (k < C) s += v[u][k];
+      if (i < MS) sm[i] = s;
+    }
+  }
+  __syncthreads();
+  if (tid < 64) {
+    // every member solves (same bits); f / stats / status rows are written by chunk 0 only
+    solve_body<Q>(sm, d, P, Pseg, pivot_mode, tol, c == 0 ? fout : nullptr, cf_s,
+                  c == 0 ? stats : nullptr, c == 0 ? status : nullptr, &st_s);
+    if (tid == 0 && to_s) {
+      st_s |= to_s;
+      if (c == 0) status[d] = st_s;
+    }
+  }
+  __syncthreads();
+  resid_body<Q, T>(X, cap, ret, ind, d, N, P, cf_s, (st_s & (XS_BAD | XS_COOP_TIMEOUT)) != 0, eout,
+                   nullptr, red, ResidPre<Q>{}, rs, nb, ne, okd);
+  // R^2: the last member of the team to finish combines the C chunk sums in chunk order
+  if (tid == 0) {
+    double* so = sums + ((size_t)d * C + c) * 5;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) st_sc1(so + k, rs[k]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    int* done = sync + 1 + D + d;
+    if (__hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == C - 1) {
+      const double* sd = sums + (size_t)d * C * 5;
+      double v[kCoopMaxC][5];
+#pragma unroll
+      for (int k = 0; k < kCoopMaxC; ++k)
+#pragma unroll
+        for (int j = 0; j < 5; ++j) v[k][j] = k < C ? ld_sc1(sd + k * 5 + j) : 0.0;
+      double a = v[0][0], b = v[0][1], cr = v[0][2], e2 = v[0][3], n = v[0][4];
+#pragma unroll
+      for (int k = 1; k < kCoopMaxC; ++k)
+        if (k < C) { a += v[k][0]; b += v[k][1]; cr += v[k][2]; e2 += v[k][3]; n += v[k][4]; }
+      const double ve = b / n - (a / n) * (a / n);
+      const double vr = e2 / n - (cr / n) * (cr / n);
+      r2out[d] = (st_s & (XS_BAD | XS_COOP_TIMEOUT)) ? qnan() : 1.0 - ve / vr;
+    }
   }
 }
 
@@ -1976,7 +2125,7 @@ __global__ __launch_bounds__(256) void xs_refine_kernel(
   double* md = sm;                 // [MS] raw moments
   load_moments<Q>(mom, d, S, Pseg, md);
   __syncthreads();
-  double* fo = fout + (size_t)d * K;
+  double* fo = fout ? fout + (size_t)d * K : nullptr;  // null: coefficients only
   double* co = RESID ? cf_s : coef + (size_t)d * (Q + 1 + P);
   int bits;
   if (K > kXsRefineMaxK) {
@@ -2029,13 +2178,33 @@ inline int xs_chunks(int D, int N) {
   return (N + C - 1) / C;  // no empty trailing chunk after rounding C up to 64
 }
 
+// Team (cooperative) path: chunks per date (g_mfa_xs_coop: 0 = off, > 0 = forced, < 0 = auto).
+// Auto: enough chunks for ~kCoopTargetWG workgroups, at least kCoopMinChunk stocks per chunk.
+constexpr int kCoopTargetWG = 4096;
+constexpr int kCoopMinChunk = 512;
+inline int xs_coop_chunks(int D, int N) {
+  const int g = g_mfa_xs_coop;
+  if (g == 0 || g_mfa_xs_mode != 0) return 1;
+  int C = g > 0 ? g : (kCoopTargetWG + D - 1) / D;
+  const int minChunk = g > 0 ? kWT : kCoopMinChunk;  // forced counts: one tile per chunk at least
+  const int maxC = N / minChunk > 1 ? N / minChunk : 1;
+  C = C < 1 ? 1 : (C > maxC ? maxC : C);
+  C = C > kCoopMaxC ? kCoopMaxC : C;
+  if (C <= 1) return 1;
+  const int Cs = xs_chunk_size(N, C);
+  return (N + Cs - 1) / Cs;
+}
+
 // Workspace: partial moments [D][S][msize] | coef [D][Q+1+P] | partial R^2 sums [D][S][5] |
-// per-tile validity bits [D][ceil(N/64)] u64 (fused kernel).
+// per-tile validity bits [D][ceil(N/64)] u64 (fused kernel) | team counters (1 + 2 D) ints.
+// S = max(chunked-path chunks, team chunks).
 inline size_t xs_workspace_bytes(int D, int N, int P, int Q) {
   const int Pseg = P > 0 ? P : 1;
   const size_t ms = (size_t)Q * (Q + 1) / 2 + 2 * Q + 4 + (size_t)Pseg * (Q + 3);
-  const size_t S = (size_t)xs_chunks(D, N);
-  return (size_t)D * (S * ms + Q + 1 + P + S * 5 + (N + kWT - 1) / kWT) * sizeof(double);
+  const size_t S1 = (size_t)xs_chunks(D, N), S2 = (size_t)xs_coop_chunks(D, N);
+  const size_t S = S1 > S2 ? S1 : S2;
+  return (size_t)D * (S * ms + Q + 1 + P + S * 5 + (N + kWT - 1) / kWT) * sizeof(double) +
+         (1 + 2 * (size_t)D) * sizeof(int);
 }
 
 template <int Q, int VAR, typename T>
@@ -2049,13 +2218,17 @@ hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, 
   const bool refine = (pivot_mode & kXsRefine) != 0;
   const int pm = pivot_mode & 0xff;
   const int mode = g_mfa_xs_mode;
-  const int S = xs_chunks(D, N);
+  const int Sc = xs_chunks(D, N), Ct = xs_coop_chunks(D, N);
+  const bool team = Ct > 1 && Sc == 1;
+  const int S = team ? Ct : Sc;  // partial-moment rows per date (read by the refine pass)
+  const int Sw = Sc > Ct ? Sc : Ct;  // workspace layout stride (xs_workspace_bytes)
   const int C = xs_chunk_size(N, S);
-  const bool chunked = S > 1 || mode == 1;
+  const bool chunked = !team && (S > 1 || mode == 1);
   double* mom = ws;
-  double* coef = ws + (size_t)D * S * MS;
+  double* coef = ws + (size_t)D * Sw * MS;
   double* sums = coef + (size_t)D * (Q + 1 + P);
-  unsigned long long* okm = (unsigned long long*)(sums + (size_t)D * S * 5);
+  unsigned long long* okm = (unsigned long long*)(sums + (size_t)D * Sw * 5);
+  int* sync = (int*)(okm + (size_t)D * ((N + kWT - 1) / kWT));
   const size_t seg8 = (size_t)L::seg_doubles(kRepMax, Pseg) * sizeof(double);
   const bool rep8 = seg8 <= kSegLdsBudget;
   const size_t lds1 = ((size_t)L::seg_doubles(rep8 ? kRepMax : 1, Pseg) + L::NACC) * sizeof(double);
@@ -2065,7 +2238,21 @@ hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, 
   if (det && !rep8) return hipErrorNotSupported;
   const int16_t* indp = P > 0 ? ind : nullptr;
   constexpr bool PRE = sizeof(T) == 4;
-  if (chunked) {
+  if (team) {
+    if (hipError_t err = hipMemsetAsync(sync, 0, (1 + 2 * (size_t)D) * sizeof(int), s)) return err;
+    const dim3 g(D * S);
+    if (det)
+      hipLaunchKernelGGL((xs_coop_kernel<Q, kRepMax, VAR | 32, T>), g, dim3(256), lds1, s, X, cap,
+                         ret, indp, N, P, Pseg, S, C, pm, tol, f, e, r2, stats, status, mom, sums,
+                         okm, sync);
+    else if (rep8)
+      hipLaunchKernelGGL((xs_coop_kernel<Q, kRepMax, VAR, T>), g, dim3(256), lds1, s, X, cap, ret,
+                         indp, N, P, Pseg, S, C, pm, tol, f, e, r2, stats, status, mom, sums, okm,
+                         sync);
+    else
+      hipLaunchKernelGGL((xs_coop_kernel<Q, 1, VAR, T>), g, dim3(256), lds1, s, X, cap, ret, indp,
+                         N, P, Pseg, S, C, pm, tol, f, e, r2, stats, status, mom, sums, okm, sync);
+  } else if (chunked) {
     const dim3 g(D * S);
     if (det)
       hipLaunchKernelGGL((xs_moments_kernel<Q, VAR | 32, kRepMax, T>), g, dim3(256), lds1, s, X,
@@ -2082,7 +2269,7 @@ hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, 
       hipLaunchKernelGGL((xs_resid_kernel<Q, T>), g, dim3(256), 0, s, X, cap, ret, indp, D, N, P,
                          S, C, coef, status, e, r2, S > 1 ? sums : nullptr);
       if (S > 1)
-        hipLaunchKernelGGL(xs_r2_combine_kernel, dim3((D + 255) / 256), dim3(256), 0, s, sums, D,
+        hipLaunchKernelGGL(xs_r2_combine_kernel<0>, dim3((D + 255) / 256), dim3(256), 0, s, sums, D,
                            S, status, r2);
     }
   } else if (Q == 10 && (mode == 10 || mode == 11 || mode == 12)) {
@@ -2215,4 +2402,24 @@ inline size_t xs_moments_bytes(int P, int Q) {
   return ((size_t)Q * (Q + 1) / 2 + 2 * Q + 4 + (size_t)Pseg * (Q + 3)) * sizeof(double);
 }
 
-}  // namespace
+}  // namespace mfa_xs
+
+using namespace mfa_xs;
+
+// The per-Q instantiations are split over several translation units (xs_inst_*.hip) so the
+// build compiles them in parallel; the entry-point TUs see only these declarations.
+#define MFA_XS_LAUNCH_SIG(qq, vv, T)                                                            \
+  hipError_t mfa_xs::launch_q<qq, vv, T>(const T*, const T*, const T*, const int16_t*, int, int,  \
+                                         int, int, double, double*, T*, double*, double*, int*,  \
+                                         double*, hipStream_t)
+#define MFA_XS_SPLIT_SIG(qq, T)                                                                 \
+  hipError_t mfa_xs::split_q<qq, T>(int, const T*, const T*, const T*, const int16_t*, int, int,  \
+                                    int, int, double, double*, double*, double*, double*, int*,  \
+                                    T*, double*, hipStream_t)
+#define MFA_XS_INSTANTIATE(qq, T) template MFA_XS_LAUNCH_SIG(qq, 0, T); template MFA_XS_SPLIT_SIG(qq, T);
+#define MFA_XS_DECLARE(qq, T) extern template MFA_XS_LAUNCH_SIG(qq, 0, T); extern template MFA_XS_SPLIT_SIG(qq, T);
+#define MFA_XS_DECLARE_ALL(T)                                                                   \
+  MFA_XS_DECLARE(1, T) MFA_XS_DECLARE(2, T) MFA_XS_DECLARE(3, T) MFA_XS_DECLARE(4, T)           \
+  MFA_XS_DECLARE(5, T) MFA_XS_DECLARE(6, T) MFA_XS_DECLARE(7, T) MFA_XS_DECLARE(8, T)           \
+  MFA_XS_DECLARE(9, T) MFA_XS_DECLARE(10, T) MFA_XS_DECLARE(11, T) MFA_XS_DECLARE(12, T)        \
+  MFA_XS_DECLARE(13, T) MFA_XS_DECLARE(14, T) MFA_XS_DECLARE(15, T) MFA_XS_DECLARE(16, T)

@@ -1,51 +1,126 @@
-"""Perf regression guards on 1x MI355X, at fixed shapes.
+"""Perf regression guards on 1x MI355X, at the production shapes and calls.
 
-Thresholds are ~2.5-3x the measured steady-state numbers in profiles/ (bench: 0.275 ms per 2520
-dates at N = 5000; MC eigen adjust 37 ms per 2520 x 100; as-of search 0.10 ms at 6.7 M rows),
-so clock ramp or a noisy neighbour does not fail them, while a fallback to a slow path (e.g. the
-split K1/K2/K3 kernels, an eager PyTorch path or a per-date loop) does."""
+Each guard times the call the framework runs in production and fails below 0.8x the rate
+measured on a fresh MI355X (``MEASURED`` below; sources in profiles/), so a regression of more
+than ~20 % -- a fallback to a slow path, a lost fusion, a register spill -- fails, while run-to-run
+noise (< 3 % measured on fresh boxes) does not.  The GPU is brought to its steady clocks first
+(a cold MI355X runs the first ~100 steps ~10 % slower)."""
 import pytest
 import torch
 
 pytestmark = pytest.mark.gpu
 
+# measured on 1x MI355X (ROCm 7.2), round 3 (profiles/r03_start/, profiles/r02_*):
+MEASURED = {
+    # bench.py: fp64 storage, refine on, deterministic, graph replay: 0.392 ms / 2520 dates
+    "xs_wls_fp64_reg_per_s": 6.43e6,
+    # RiskModel eigen stage at 2520 dates x M = 100 (profiles/r02_risk_stages_final_fp64.json)
+    "eigen_adjust_2520x100_ms": 20.65,
+    # Newey-West expanding series, T = 2520, K = 42, q = 2 (profiles/r02_nw_bench.jsonl)
+    "newey_west_2520_ms": 0.103,
+    # BETA/HSIGMA anchored-prefix kernel, 5000 x 3780 (profiles/r02_rolling_ab.jsonl)
+    "beta_hsigma_5000x3780_ms": 0.214,
+}
+SLACK = 0.8
 
-def _time_ms(fn, reps=10, warm=5):
+
+def _warm_clocks():
+    a = torch.randn(4096, 4096, device="cuda:0")
+    for _ in range(30):
+        a = a @ a
+        a = a / a.norm()
+    torch.cuda.synchronize()
+
+
+def _time_ms(fn, reps=20, warm=5, rounds=3):
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(reps):
-        fn()
-    e1.record()
-    torch.cuda.synchronize()
-    return e0.elapsed_time(e1) / reps
+    best = float("inf")
+    for _ in range(rounds):
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        best = min(best, e0.elapsed_time(e1) / reps)
+    return best
 
 
-def test_xs_wls_headline_shape_throughput():
+def test_xs_wls_production_call_throughput():
+    """bench.py's step: fp64 panel, refine=True, deterministic default, one HIP graph replay."""
     from llm_driven_multi_factor_model_amd.models.panel import synthetic_panel
     from llm_driven_multi_factor_model_amd.ops.cross_section import xs_wls, xs_wls_workspace
-    D, N, P, Q = 1000, 5000, 31, 10
-    g = synthetic_panel(D, N, P, Q, seed=0, missing_frac=0.02).to("cuda:0")
+    D, N, P, Q = 2520, 5000, 31, 10
+    g = synthetic_panel(D, N, P, Q, seed=1234, device="cuda:0", missing_frac=0.01,
+                        dtype=torch.float64)
     ws = xs_wls_workspace(D, P, Q, "cuda:0", N)
-    out = xs_wls(g.styles, g.cap, g.ret, g.ind, P, workspace=ws, refine=False)
-    ms = _time_ms(lambda: xs_wls(g.styles, g.cap, g.ret, g.ind, P, out=out, workspace=ws, refine=False))
-    reg_per_s = D / (ms * 1e-3)
-    print(f"xs_wls {D}x{N}: {ms:.3f} ms, {reg_per_s / 1e6:.2f} M reg/s")
-    assert reg_per_s > 3.0e6, f"{reg_per_s:.3g} reg/s"
+    out = xs_wls(g.styles, g.cap, g.ret, g.ind, P, refine=True, workspace=ws)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        xs_wls(g.styles, g.cap, g.ret, g.ind, P, refine=True, out=out, workspace=ws)
+    _warm_clocks()
+    for _ in range(100):
+        graph.replay()
+    ms = _time_ms(graph.replay, reps=30)
+    rate = D / (ms * 1e-3)
+    floor = SLACK * MEASURED["xs_wls_fp64_reg_per_s"]
+    print(f"xs_wls fp64 {D}x{N} graph: {ms:.4f} ms, {rate / 1e6:.2f} M reg/s (floor {floor / 1e6:.2f})")
+    assert int((out.status & 64).ne(0).sum()) == 0
+    assert rate > floor, f"{rate:.3g} reg/s < {floor:.3g}"
 
 
-def test_mc_eigen_adjust_throughput():
+def test_eigen_adjust_2520x100():
+    """The eigen stage of RiskModel.run at the BASELINE shape (tridiagonal bias solver)."""
     from llm_driven_multi_factor_model_amd.ops import eigen
-    D, K, M = 252, 42, 100
+    D, K, M = 2520, 42, 100
     gen = torch.Generator().manual_seed(0)
-    X = torch.randn(D, 300, K, generator=gen, dtype=torch.float64) * torch.logspace(-1, -3, K, dtype=torch.float64)
-    F0 = (X.transpose(1, 2) @ X / 300).to("cuda:0")
+    Xr = torch.randn(D, 300, K, generator=gen, dtype=torch.float64) * torch.logspace(-1, -3, K, dtype=torch.float64)
+    F0 = (Xr.transpose(1, 2) @ Xr / 300).to("cuda:0")
     Cz = eigen.mc_cov(M, K, D, 1, "cuda:0")
-    ms = _time_ms(lambda: eigen.eigen_risk_adjust(F0, M=M, Cz=Cz), reps=3, warm=1)
-    print(f"eigen_risk_adjust {D}x{M}: {ms:.2f} ms")
-    assert ms < 15.0, f"{ms:.2f} ms"
+    _warm_clocks()
+    ms = _time_ms(lambda: eigen.eigen_risk_adjust(F0, M=M, Cz=Cz), reps=3, warm=1, rounds=2)
+    ceil = MEASURED["eigen_adjust_2520x100_ms"] / SLACK
+    print(f"eigen_risk_adjust {D}x{M}: {ms:.2f} ms (ceiling {ceil:.2f})")
+    assert ms < ceil, f"{ms:.2f} ms"
+
+
+def test_newey_west_scan_2520():
+    from llm_driven_multi_factor_model_amd.ops.ew_scan import newey_west_series
+    T, K = 2520, 42
+    F = torch.randn(T, K, dtype=torch.float64, device="cuda:0", generator=torch.Generator(
+        device="cuda:0").manual_seed(0)) * 0.01
+    _warm_clocks()
+    ms = _time_ms(lambda: newey_west_series(F, q=2, tau=252.0))
+    ceil = MEASURED["newey_west_2520_ms"] / SLACK
+    print(f"newey_west_series T={T} K={K}: {ms:.4f} ms (ceiling {ceil:.4f})")
+    assert ms < ceil, f"{ms:.4f} ms"
+
+
+def test_beta_hsigma_5000x3780():
+    from llm_driven_multi_factor_model_amd import _native
+    from llm_driven_multi_factor_model_amd.ops import rolling as RL
+    N, T = 5000, 3780
+    R = N * T
+    dev = torch.device("cuda:0")
+    g = torch.Generator(device=dev).manual_seed(0)
+    mkt = torch.randn(T, device=dev, generator=g) * 0.012
+    ret = (mkt[None, :] * 1.1 + torch.randn(N, T, device=dev, generator=g) * 0.02).reshape(-1).float()
+    ret[torch.rand(R, device=dev, generator=g) < 0.02] = float("nan")
+    mret = mkt[None, :].expand(N, T).reshape(-1).contiguous().float()
+    seg = RL.seg_lo_from_codes(torch.arange(N, device=dev, dtype=torch.int32).repeat_interleave(T))
+    beta, hsig = torch.empty(R, device=dev), torch.empty(R, device=dev)
+    fn = lambda: _native.call("mfa_beta_hsigma", _native.ptr(ret), _native.ptr(mret),  # noqa: E731
+                              _native.ptr(seg), R, 252, 0.5 ** (1 / 63), 42, _native.ptr(beta),
+                              _native.ptr(hsig), _native.stream(dev))
+    _warm_clocks()
+    ms = _time_ms(fn)
+    ceil = MEASURED["beta_hsigma_5000x3780_ms"] / SLACK
+    print(f"beta_hsigma {N}x{T}: {ms:.4f} ms (ceiling {ceil:.4f})")
+    assert torch.isfinite(beta).any()
+    assert ms < ceil, f"{ms:.4f} ms"
 
 
 def test_asof_search_throughput():

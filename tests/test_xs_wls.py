@@ -318,6 +318,61 @@ def test_chunked_path_matches_oracle(cuda, dtype, S, D, N, P, Q, empty):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("C,D,N,P,Q,empty", [(2, 9, 1000, 31, 10, 1), (4, 37, 5000, 31, 10, 2),
+                                             (8, 4, 4096, 12, 3, 0), (3, 5, 1544, 0, 4, 0),
+                                             (7, 3, 4000, 28, 16, 1), (4, 300, 5000, 31, 10, 1)])
+def test_team_path_matches_oracle(cuda, dtype, C, D, N, P, Q, empty):
+    """Team (cooperative) kernel: C workgroups per date publish partial moments, wait for the
+    team, solve redundantly and re-read only their chunk == the float64 oracle; deterministic
+    mode is bitwise reproducible and equal to the chunked path's combine order."""
+    from llm_driven_multi_factor_model_amd import _native
+    panel = synthetic_panel(D, N, P, Q, seed=C * 11 + D, missing_frac=0.02,
+                            empty_industries=empty, dtype=dtype)
+    ref = X.xs_wls_reference(panel.styles, panel.cap, panel.ret, panel.ind, P)
+    g = panel.to(cuda)
+    lib = _native.lib()
+    lib.mfa_xs_set_coop(C)
+    try:
+        assert _native.query("mfa_xs_coop_chunks", D, N) == C
+        out = X.xs_wls(g.styles, g.cap, g.ret, g.ind, P)
+        det = [X.xs_wls(g.styles, g.cap, g.ret, g.ind, P, deterministic=True) for _ in range(2)]
+        torch.cuda.synchronize()
+    finally:
+        lib.mfa_xs_set_coop(0)
+    assert not bool((out.status & 64).any()), "team wait timed out"
+    torch.testing.assert_close(out.f.cpu(), ref.f, rtol=1e-9, atol=1e-12)
+    torch.testing.assert_close(out.r2.cpu(), ref.r2, rtol=1e-9, atol=1e-11)
+    tol = dict(rtol=1e-9, atol=1e-13) if dtype == torch.float64 else dict(rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(out.resid.cpu(), ref.resid, equal_nan=True, **tol)
+    torch.testing.assert_close(out.stats.cpu(), ref.stats, rtol=1e-10, atol=1e-12)
+    assert torch.equal(det[0].f, det[1].f) and torch.equal(det[0].r2, det[1].r2)
+    assert torch.equal(det[0].resid.nan_to_num(7.0), det[1].resid.nan_to_num(7.0))
+    torch.testing.assert_close(det[0].f.cpu(), ref.f, rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_team_path_refines_singular_dates(cuda):
+    """A date with an exactly collinear style pair: the team kernel flags it and the device
+    pinv pass (reading the team's partial-moment rows in chunk order) matches numpy's pinv."""
+    from llm_driven_multi_factor_model_amd import _native
+    p = synthetic_panel(6, 3000, 31, 10, seed=3, missing_frac=0.01, dtype=torch.float64)
+    p.styles[2, 4] = 2.0 * p.styles[2, 1]
+    ref = X.xs_wls_reference(p.styles, p.cap, p.ret, p.ind, 31)
+    g = p.to(cuda)
+    lib = _native.lib()
+    lib.mfa_xs_set_coop(4)
+    try:
+        out = X.xs_wls(g.styles, g.cap, g.ret, g.ind, 31)
+        torch.cuda.synchronize()
+    finally:
+        lib.mfa_xs_set_coop(0)
+    assert int(out.status[2]) & 32, "date 2 should be refined on the device"
+    torch.testing.assert_close(out.f.cpu(), ref.f, rtol=1e-8, atol=1e-11)
+    torch.testing.assert_close(out.resid.cpu(), ref.resid, rtol=1e-8, atol=1e-12, equal_nan=True)
+
+
+@pytest.mark.gpu
 def test_path_selection_and_small_shards(cuda):
     """The fused kernel is the automatic path at every shard size (the chunked path measured
     slower from 315 to 2520 dates); forced chunk counts are honoured and clamped."""
