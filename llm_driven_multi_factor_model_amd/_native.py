@@ -33,6 +33,7 @@ _SIGS: dict[str, list] = {
     "mfa_xs_set_chunks": [_i],
     "mfa_xs_set_mode": [_i],
     "mfa_xs_set_coop": [_i],
+    "mfa_xs_set_pipe": [_i, _i],
     "mfa_xs_coop_chunks": [_i, _i],
     "mfa_xs_det_supported": [_i, _i],
     "mfa_xs_wls_variant": [_vp, _vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp],

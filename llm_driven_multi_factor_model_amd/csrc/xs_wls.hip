@@ -7,6 +7,8 @@ MFA_XS_DECLARE_ALL(float)
 int g_mfa_xs_mode = 0;
 int g_mfa_xs_chunks = 0;
 int g_mfa_xs_coop = 0;
+int g_mfa_xs_lag = 1;
+int g_mfa_xs_pipe_wpc = 0;
 
 // Ablation: 0 = fused single-kernel path with the residual prefetch during the wave-0 solve
 // (default), 1 = three separate kernels, 7 = fused without the prefetch.  Applies to both the
@@ -17,9 +19,14 @@ MFA_API void mfa_xs_set_mode(int mode) { g_mfa_xs_mode = mode; }
 // kXsChunkMinD = 0), > 0 = forced chunk count, < 0 = always one workgroup per date.
 MFA_API void mfa_xs_set_chunks(int S) { g_mfa_xs_chunks = S; }
 
-// Team (cooperative) CS-WLS kernel for the next calls: 0 = off, C > 0 = C chunks per date,
+// Pipelined team CS-WLS kernel for the next calls: 0 = off, C > 0 = C chunks per date,
 // < 0 = automatic chunk count (xs_coop_chunks).
 MFA_API void mfa_xs_set_coop(int C) { g_mfa_xs_coop = C; }
+// Pipelined team kernel: residual-pass lag in tickets (1..3) and workgroups per CU (0 = max).
+MFA_API void mfa_xs_set_pipe(int lag, int wpc) {
+  g_mfa_xs_lag = lag;
+  g_mfa_xs_pipe_wpc = wpc;
+}
 MFA_API int mfa_xs_coop_chunks(int D, int N) { return xs_coop_chunks(D, N); }
 
 // Chunks per date the next mfa_xs_wls / mfa_xs_wls_f64 call on (D, N) will use.

@@ -36,8 +36,12 @@
 extern int g_mfa_xs_mode;
 // Stock chunks per date: 0 = automatic (chunked below kXsChunkMinD dates), > 0 forced, < 0 never.
 extern int g_mfa_xs_chunks;
-// Team (cooperative) CS-WLS kernel: 0 = off, > 0 = forced chunks per date, < 0 = automatic.
+// Team (pipelined) CS-WLS kernel: 0 = off, > 0 = forced chunks per date, < 0 = automatic.
 extern int g_mfa_xs_coop;
+// Pipelined team kernel: residual pass `lag` tickets behind the moments (1..kPipeMaxLag), and
+// the persistent grid's workgroups per CU (0 = the occupancy limit).
+extern int g_mfa_xs_lag;
+extern int g_mfa_xs_pipe_wpc;
 
 namespace mfa_xs {
 
@@ -1473,37 +1477,46 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Q <= 10 ? 2
 }
 
 // ------------------------------------------------------------------------------------------
-// Team (cooperative) CS-WLS: C workgroups per date, one stock chunk each, ONE launch.
+// Pipelined team CS-WLS (persistent grid, deferred residuals): C stock chunks per date, each
+// chunk's moments and residuals done by the same workgroup, dates solved by their team's last
+// arriver, and no workgroup ever idles while its team catches up.
 //
-// The fused kernel's residual pass re-reads the date's panel slice from HBM: one workgroup
-// streams a whole 490 KB fp64 date, so ~512 dates (~250 MB) are in flight and the slice has
-// mostly left the 256 MB Infinity Cache by the time it is re-read (2.46 GB moved per 1.34 GB
-// compulsory, profiles/r02_xs_cluster_ab.md).  Here a date is split into C chunks on C
-// workgroups that run at the same time; each streams its chunk once into partial raw moments,
-// publishes them, and -- once the whole team has published -- sums the C partials in chunk
-// order (bitwise identical in every member), solves redundantly in wave 0 and re-reads ONLY
-// ITS chunk for the residuals, a few microseconds after streaming it: the re-read is served by
-// the XCD's L2 / the Infinity Cache instead of HBM.  A date also occupies C CUs instead of one,
-// so a 315-date shard (8-GPU strong scaling) fills the chip.
-//
-// Progress guarantee (no co-residency assumption): a workgroup takes a ticket from a global
-// counter when it STARTS, and ticket t is chunk t % C of date t / C.  A workgroup publishes its
-// partial before it waits on anything, and waits only for tickets of its own date.  Tickets are
-// taken in start order, so every date except the one holding the next untaken ticket is fully
-// ticketed; if every resident workgroup were waiting, all would hold tickets of that one date,
-// i.e. at most C - 1 of them -- so any device that can hold C of these workgroups (C <= 8)
-// always has a running one.  Each poll loop is also bounded (XS_COOP_TIMEOUT): the grid drains.
-//
-// Hand-offs (MI355X_MICROARCH.md, inter-workgroup visibility): partial moments and R^2 sums
-// are stored write-through (relaxed agent-scope atomic stores, `sc1`), every storing wave waits
-// vmcnt(0) before the workgroup barrier behind which ONE lane adds to the date's counter; the
-// readers poll that counter with `sc1` loads from one lane and load the payload with `sc1` loads
-// after a workgroup barrier.  No fence (a __threadfence per workgroup measured 4x slower).
-// sync = [ticket | arrive[D] | done[D]] ints, zeroed before every launch (memset node).
+// The fused kernel's residual pass re-reads the date's panel slice: one workgroup streams a
+// whole 490 KB fp64 date in ~35 us, ~512 dates are in flight, so ~250 MB of other dates pass
+// through the 256 MB Infinity Cache between a line's first read and its re-read and most
+// re-reads go to HBM (2.46 GB moved per 1.34 GB compulsory, profiles/r02_xs_cluster_ab.md).  A
+// one-wave-per-date team that WAITS for its partners (round-3 first try, r03_team_ab.md) pays
+// the wait and a redundant solve per member on the 2 workgroup slots of a CU and lost 25-260 %.
+// Here a persistent workgroup loops over tickets:
+//   1. take a ticket t of its group (blockIdx & 7: the blocks of one XCD), t -> chunk c = t % C
+//      of date d = group + 8 (t / C); stream the chunk once (LDS-DMA ring) into raw moments;
+//   2. publish the partial row (write-through sc1 stores), arrive on the date's counter; the
+//      LAST arriver sums the C partials in chunk order (bitwise-deterministic), solves in wave 0
+//      and publishes the residual coefficients + a ready flag carrying the status word;
+//   3. `lag` tickets later (the chunk's date has been solved by then), the same workgroup
+//      re-reads ITS chunk for the residual pass: ~10-20 us after the first read instead of
+//      ~40, so the re-read is an Infinity-Cache hit; partial R^2 sums are combined in chunk
+//      order by the last member to finish.
+// Progress (no co-residency assumption): tickets are taken in order by running workgroups, and a
+// workgroup always finishes step 2 of a ticket it took before it waits on anything, so every
+// fully ticketed date gets solved.  A workgroup waits (step 3) only for a date whose ticket it
+// took `lag` or more tickets ago; if that date is not fully ticketed, every ticket taken since
+// belongs to it, so a waiting workgroup holds lag + 1 of its C tickets: with lag >= 1 and
+// C <= 16, all resident workgroups of a group can be waiting at once only if fewer than
+// (C - 1) / (lag + 1) + 1 <= 8 of them are resident.  Every poll is bounded anyway
+// (XS_COOP_TIMEOUT status bit): the grid always drains.
+// Hand-offs (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the sc1 table):
+// payloads stored sc1, every storing wave waits vmcnt(0), a workgroup barrier, then ONE lane
+// adds / stores the counter or flag; readers poll with sc1 loads from one lane, barrier, and
+// load the payload with sc1 loads.
+// sync = [tickets 8 | arrive[D] | done[D] | ready[D]] ints, zeroed before every launch.
 // ------------------------------------------------------------------------------------------
 constexpr int XS_COOP_TIMEOUT = 64;  // status bit: a team wait gave up (results invalid)
-constexpr int kCoopSpin = 1 << 21;
-constexpr int kCoopMaxC = 8;         // chunks (workgroups) per date at most   // poll iterations (s_sleep 4 each, ~0.2 s) before giving up
+constexpr int kCoopSpin = 1 << 21;   // poll iterations (s_sleep 4 each, ~0.2 s) before giving up
+constexpr int kCoopMaxC = 16;        // chunks per date at most
+constexpr int kPipeGroups = 8;       // ticket groups: blockIdx & 7 (the blocks sharing an XCD)
+constexpr int kPipeMaxLag = 3;       // residual pass at most 3 tickets behind the moments
+constexpr int kReadyBit = 1 << 30;   // ready flag = status | kReadyBit
 
 __device__ __forceinline__ double ld_sc1(const double* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1511,109 +1524,140 @@ __device__ __forceinline__ double ld_sc1(const double* p) {
 __device__ __forceinline__ void st_sc1(double* p, double v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// one lane: wait until *ctr >= target; false on timeout
-__device__ __forceinline__ bool coop_wait(int* ctr, int target) {
-  for (int it = 0; it < kCoopSpin; ++it) {
-    if (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= target) return true;
-    __builtin_amdgcn_s_sleep(4);
-  }
-  return false;
-}
 
 template <int Q, int R, int VAR, typename T>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Q <= 10 ? 2 : MFA_XS_WPE_BIGQ, Q <= 10 ? 2 : MFA_XS_WPE_BIGQ))) void xs_coop_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Q <= 10 ? 2 : MFA_XS_WPE_BIGQ, Q <= 10 ? 2 : MFA_XS_WPE_BIGQ))) void xs_pipe_kernel(
     const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
-    const int16_t* __restrict__ ind, int N, int P, int Pseg, int C, int Cs, int pivot_mode,
-    double tol, double* __restrict__ fout, T* __restrict__ eout, double* __restrict__ r2out,
-    double* __restrict__ stats, int* __restrict__ status, double* __restrict__ mom,
-    double* __restrict__ sums, unsigned long long* __restrict__ okm, int* __restrict__ sync) {
+    const int16_t* __restrict__ ind, int D, int N, int P, int Pseg, int C, int Cs, int lag,
+    int pivot_mode, double tol, double* __restrict__ fout, T* __restrict__ eout,
+    double* __restrict__ r2out, double* __restrict__ stats, int* __restrict__ status,
+    double* __restrict__ mom, double* __restrict__ coef, double* __restrict__ sums,
+    unsigned long long* __restrict__ okm, int* __restrict__ sync) {
   __shared__ __attribute__((aligned(16))) char ring[fused_ring_bytes<Q, T>()];
   __shared__ double cf_s[Q + 1 + 128];
   __shared__ double red[4][5];
   __shared__ double rs[5];
-  __shared__ int st_s, tk_s, to_s;
+  __shared__ int tk_s, last_s, st_s, flag_s;
   extern __shared__ double dyn[];
   const int tid = threadIdx.x;
-  const int D = (int)gridDim.x / C;
-  if (tid == 0) {
-    tk_s = __hip_atomic_fetch_add(sync, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    to_s = 0;
-  }
-  __syncthreads();
-  const int t = tk_s, d = t / C, c = t - d * C;
-  const int nb = c * Cs, ne = min(N, nb + Cs);
+  const int grp = (int)blockIdx.x & (kPipeGroups - 1);
+  const int ndg = D > grp ? (D - grp + kPipeGroups - 1) / kPipeGroups : 0;
+  const int ntk = ndg * C;  // this group's tickets
   const int MS = Layout<Q, T>::msize(Pseg);
-  double* sm = (double*)ring;
-  unsigned long long* okd = okm + (size_t)d * ((N + kWT - 1) / kWT);
-  moments_body<Q, VAR & 35, R, T>(X, cap, ret, ind, N, Pseg, d, ring, dyn, sm, nb, ne, nullptr, okd);
-  // publish this chunk's partial (write-through), then arrive
-  double* mp = mom + ((size_t)d * C + c) * MS;
-  for (int i = tid; i < MS; i += blockDim.x) st_sc1(mp + i, sm[i]);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  int* arrive = sync + 1 + d;
-  if (tid == 0) {
-    __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (!coop_wait(arrive, C)) to_s = XS_COOP_TIMEOUT;
-  }
-  __syncthreads();
-  // the date's moments: the C partials summed in chunk order (identical bits in every member)
-  // (every load of a thread is issued before the first add: a load -> add chain would pay the
-  // cross-XCD round trip C times per element)
-  const double* md = mom + (size_t)d * C * MS;
-  for (int i0 = tid; i0 < MS; i0 += 2 * blockDim.x) {
-    double v[2][kCoopMaxC];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int i = i0 + u * (int)blockDim.x;
-#pragma unroll
-      for (int k = 0; k < kCoopMaxC; ++k)
-        v[u][k] = (k < C && i < MS) ? ld_sc1(md + (size_t)k * MS + i) : 0.0;
+  const int NT = (N + kWT - 1) / kWT;
+  const int KC = Q + 1 + P;
+  int* tick = sync;
+  int* arrive = sync + kPipeGroups;
+  int* done = arrive + D;
+  int* ready = done + D;
+  double* sm = (double*)ring;  // the chunk's moments, then the solve's scratch
+  int pend[kPipeMaxLag + 1];   // tickets whose residual pass is pending (oldest first)
+  int np = 0;
+  bool more = true;
+  for (;;) {
+    int t = ntk;
+    if (more) {
+      __syncthreads();  // tk_s of the previous iteration has been read by every thread
+      if (tid == 0) tk_s = __hip_atomic_fetch_add(tick + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __syncthreads();
+      t = tk_s;
+      more = t < ntk;
     }
+    if (t < ntk) {
+      // ---- 1 + 2: moments of the chunk, publish, arrive; the last arriver solves the date ----
+      const int k = t / C, c = t - k * C, d = grp + kPipeGroups * k;
+      const int nb = c * Cs, ne = min(N, nb + Cs);
+      moments_body<Q, VAR & 35, R, T>(X, cap, ret, ind, N, Pseg, d, ring, dyn, sm, nb, ne, nullptr,
+                                      okm + (size_t)d * NT);
+      double* mp = mom + ((size_t)d * C + c) * MS;
+      for (int i = tid; i < MS; i += blockDim.x) st_sc1(mp + i, sm[i]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0)
+        last_s = __hip_atomic_fetch_add(arrive + d, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == C - 1;
+      __syncthreads();
+      if (last_s) {
+        // the date's moments: the C partials summed in chunk order (all loads of a thread are
+        // issued before its first add: a load -> add chain pays the round trip C times)
+        const double* md = mom + (size_t)d * C * MS;
+        for (int i = tid; i < MS; i += blockDim.x) {
+          double v[kCoopMaxC];
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int i = i0 + u * (int)blockDim.x;
-      double s = v[u][0];
+          for (int kk = 0; kk < kCoopMaxC; ++kk) v[kk] = kk < C ? ld_sc1(md + (size_t)kk * MS + i) : 0.0;
+          double s = v[0];
 #pragma unroll
-      for (int k = 1; k < kCoopMaxC; ++k)
-        if (k < C) s += v[u][k];
-      if (i < MS) sm[i] = s;
+          for (int kk = 1; kk < kCoopMaxC; ++kk)
+            if (kk < C) s += v[kk];
+          sm[i] = s;
+        }
+        __syncthreads();
+        if (tid < 64) solve_body<Q>(sm, d, P, Pseg, pivot_mode, tol, fout, cf_s, stats, status, &st_s);
+        __syncthreads();
+        double* co = coef + (size_t)d * KC;
+        for (int i = tid; i < KC; i += blockDim.x) st_sc1(co + i, cf_s[i]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) __hip_atomic_store(ready + d, st_s | kReadyBit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+#pragma unroll
+      for (int i = 0; i <= kPipeMaxLag; ++i)
+        if (i == np) pend[i] = t;
+      ++np;
     }
-  }
-  __syncthreads();
-  if (tid < 64) {
-    // every member solves (same bits); f / stats / status rows are written by chunk 0 only
-    solve_body<Q>(sm, d, P, Pseg, pivot_mode, tol, c == 0 ? fout : nullptr, cf_s,
-                  c == 0 ? stats : nullptr, c == 0 ? status : nullptr, &st_s);
-    if (tid == 0 && to_s) {
-      st_s |= to_s;
-      if (c == 0) status[d] = st_s;
-    }
-  }
-  __syncthreads();
-  resid_body<Q, T>(X, cap, ret, ind, d, N, P, cf_s, (st_s & (XS_BAD | XS_COOP_TIMEOUT)) != 0, eout,
-                   nullptr, red, ResidPre<Q>{}, rs, nb, ne, okd);
-  // R^2: the last member of the team to finish combines the C chunk sums in chunk order
-  if (tid == 0) {
-    double* so = sums + ((size_t)d * C + c) * 5;
+    if (np > 0 && (np > lag || !more)) {
+      // ---- 3: residual pass of the oldest pending chunk ----
+      const int t2 = pend[0];
 #pragma unroll
-    for (int k = 0; k < 5; ++k) st_sc1(so + k, rs[k]);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    int* done = sync + 1 + D + d;
-    if (__hip_atomic_fetch_add(done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == C - 1) {
-      const double* sd = sums + (size_t)d * C * 5;
-      double v[kCoopMaxC][5];
+      for (int i = 0; i < kPipeMaxLag; ++i) pend[i] = pend[i + 1];
+      --np;
+      const int k2 = t2 / C, c2 = t2 - k2 * C, d2 = grp + kPipeGroups * k2;
+      const int nb2 = c2 * Cs, ne2 = min(N, nb2 + Cs);
+      if (tid == 0) {
+        int v = 0;
+        for (int it = 0; it < kCoopSpin; ++it) {
+          v = __hip_atomic_load(ready + d2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (v) break;
+          __builtin_amdgcn_s_sleep(4);
+        }
+        flag_s = v ? v : (kReadyBit | XS_COOP_TIMEOUT);
+      }
+      __syncthreads();
+      const int st2 = flag_s & ~kReadyBit;
+      const double* co2 = coef + (size_t)d2 * KC;
+      for (int i = tid; i < KC; i += blockDim.x) cf_s[i] = ld_sc1(co2 + i);
+      __syncthreads();
+      const bool bad = (st2 & (XS_BAD | XS_COOP_TIMEOUT)) != 0;
+      resid_body<Q, T>(X, cap, ret, ind, d2, N, P, cf_s, bad, eout, nullptr, red, ResidPre<Q>{}, rs,
+                       nb2, ne2, okm + (size_t)d2 * NT);
+      // R^2: the last member of the team to finish combines the C chunk sums in chunk order
+      if (tid < 64) {
+        double* sd = sums + (size_t)d2 * C * 5;
+        int lastd = 0;
+        if (tid == 0) {
 #pragma unroll
-      for (int k = 0; k < kCoopMaxC; ++k)
+          for (int j = 0; j < 5; ++j) st_sc1(sd + c2 * 5 + j, rs[j]);
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          lastd = __hip_atomic_fetch_add(done + d2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == C - 1;
+          if ((st2 & XS_COOP_TIMEOUT) != 0) atomicOr(status + d2, XS_COOP_TIMEOUT);
+        }
+        if (__builtin_amdgcn_readfirstlane(lastd)) {
+          double v[5];
 #pragma unroll
-        for (int j = 0; j < 5; ++j) v[k][j] = k < C ? ld_sc1(sd + k * 5 + j) : 0.0;
-      double a = v[0][0], b = v[0][1], cr = v[0][2], e2 = v[0][3], n = v[0][4];
+          for (int j = 0; j < 5; ++j) v[j] = tid < C ? ld_sc1(sd + tid * 5 + j) : 0.0;
+          double a[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+          for (int kk = 0; kk < C; ++kk)  // chunk order, wave-uniform
 #pragma unroll
-      for (int k = 1; k < kCoopMaxC; ++k)
-        if (k < C) { a += v[k][0]; b += v[k][1]; cr += v[k][2]; e2 += v[k][3]; n += v[k][4]; }
-      const double ve = b / n - (a / n) * (a / n);
-      const double vr = e2 / n - (cr / n) * (cr / n);
-      r2out[d] = (st_s & (XS_BAD | XS_COOP_TIMEOUT)) ? qnan() : 1.0 - ve / vr;
+            for (int j = 0; j < 5; ++j) a[j] += readlane(v[j], kk);
+          if (tid == 0) {
+            const double n = a[4];
+            const double ve = a[1] / n - (a[0] / n) * (a[0] / n);
+            const double vr = a[3] / n - (a[2] / n) * (a[2] / n);
+            r2out[d2] = bad ? qnan() : 1.0 - ve / vr;
+          }
+        }
+      }
+    } else if (!more) {
+      break;
     }
   }
 }
@@ -2178,14 +2222,14 @@ inline int xs_chunks(int D, int N) {
   return (N + C - 1) / C;  // no empty trailing chunk after rounding C up to 64
 }
 
-// Team (cooperative) path: chunks per date (g_mfa_xs_coop: 0 = off, > 0 = forced, < 0 = auto).
-// Auto: enough chunks for ~kCoopTargetWG workgroups, at least kCoopMinChunk stocks per chunk.
-constexpr int kCoopTargetWG = 4096;
+// Team (pipelined) path: chunks per date (g_mfa_xs_coop: 0 = off, > 0 = forced, < 0 = auto).
+// Auto: enough chunks for ~kCoopTargetChunks chunks, at least kCoopMinChunk stocks per chunk.
+constexpr int kCoopTargetChunks = 8192;
 constexpr int kCoopMinChunk = 512;
 inline int xs_coop_chunks(int D, int N) {
   const int g = g_mfa_xs_coop;
   if (g == 0 || g_mfa_xs_mode != 0) return 1;
-  int C = g > 0 ? g : (kCoopTargetWG + D - 1) / D;
+  int C = g > 0 ? g : (kCoopTargetChunks + D - 1) / D;
   const int minChunk = g > 0 ? kWT : kCoopMinChunk;  // forced counts: one tile per chunk at least
   const int maxC = N / minChunk > 1 ? N / minChunk : 1;
   C = C < 1 ? 1 : (C > maxC ? maxC : C);
@@ -2194,9 +2238,13 @@ inline int xs_coop_chunks(int D, int N) {
   const int Cs = xs_chunk_size(N, C);
   return (N + Cs - 1) / Cs;
 }
+inline int xs_pipe_lag() {
+  const int l = g_mfa_xs_lag;
+  return l < 1 ? 1 : (l > kPipeMaxLag ? kPipeMaxLag : l);
+}
 
 // Workspace: partial moments [D][S][msize] | coef [D][Q+1+P] | partial R^2 sums [D][S][5] |
-// per-tile validity bits [D][ceil(N/64)] u64 (fused kernel) | team counters (1 + 2 D) ints.
+// per-tile validity bits [D][ceil(N/64)] u64 (fused kernel) | team counters (8 + 3 D) ints.
 // S = max(chunked-path chunks, team chunks).
 inline size_t xs_workspace_bytes(int D, int N, int P, int Q) {
   const int Pseg = P > 0 ? P : 1;
@@ -2204,7 +2252,39 @@ inline size_t xs_workspace_bytes(int D, int N, int P, int Q) {
   const size_t S1 = (size_t)xs_chunks(D, N), S2 = (size_t)xs_coop_chunks(D, N);
   const size_t S = S1 > S2 ? S1 : S2;
   return (size_t)D * (S * ms + Q + 1 + P + S * 5 + (N + kWT - 1) / kWT) * sizeof(double) +
-         (1 + 2 * (size_t)D) * sizeof(int);
+         (kPipeGroups + 3 * (size_t)D) * sizeof(int);
+}
+
+// Persistent grid of the pipelined team kernel: resident workgroups (occupancy query, cached per
+// kernel), a multiple of the 8 ticket groups, no more than the busiest group's tickets need.
+template <typename K>
+int pipe_grid(K kern, size_t lds, int D, int C) {
+  // (kernel, LDS bytes) -> resident workgroups per CU; kernels of one signature share a type,
+  // so the cache is keyed by the kernel's address
+  static const void* keys[64];
+  static size_t klds[64];
+  static int vals[64], nkeys = 0, cus = 0;
+  int per = -1;
+  for (int i = 0; i < nkeys; ++i)
+    if (keys[i] == (const void*)kern && klds[i] == lds) per = vals[i];
+  if (per < 0) {
+    int dev = 0;
+    if (cus <= 0 && (hipGetDevice(&dev) != hipSuccess ||
+                     hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess))
+      cus = 256;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, 256, lds) != hipSuccess || per < 1) per = 1;
+    if (nkeys < 64) {
+      keys[nkeys] = (const void*)kern;
+      klds[nkeys] = lds;
+      vals[nkeys++] = per;
+    }
+  }
+  int w = g_mfa_xs_pipe_wpc > 0 && g_mfa_xs_pipe_wpc < per ? g_mfa_xs_pipe_wpc : per;
+  int G = w * cus;
+  G -= G % kPipeGroups;
+  const int need = kPipeGroups * ((D + kPipeGroups - 1) / kPipeGroups) * C;
+  G = G < need ? G : need;
+  return G < kPipeGroups ? kPipeGroups : G;
 }
 
 template <int Q, int VAR, typename T>
@@ -2239,19 +2319,19 @@ hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, 
   const int16_t* indp = P > 0 ? ind : nullptr;
   constexpr bool PRE = sizeof(T) == 4;
   if (team) {
-    if (hipError_t err = hipMemsetAsync(sync, 0, (1 + 2 * (size_t)D) * sizeof(int), s)) return err;
-    const dim3 g(D * S);
-    if (det)
-      hipLaunchKernelGGL((xs_coop_kernel<Q, kRepMax, VAR | 32, T>), g, dim3(256), lds1, s, X, cap,
-                         ret, indp, N, P, Pseg, S, C, pm, tol, f, e, r2, stats, status, mom, sums,
-                         okm, sync);
-    else if (rep8)
-      hipLaunchKernelGGL((xs_coop_kernel<Q, kRepMax, VAR, T>), g, dim3(256), lds1, s, X, cap, ret,
-                         indp, N, P, Pseg, S, C, pm, tol, f, e, r2, stats, status, mom, sums, okm,
-                         sync);
-    else
-      hipLaunchKernelGGL((xs_coop_kernel<Q, 1, VAR, T>), g, dim3(256), lds1, s, X, cap, ret, indp,
-                         N, P, Pseg, S, C, pm, tol, f, e, r2, stats, status, mom, sums, okm, sync);
+    if (hipError_t err = hipMemsetAsync(sync, 0, (kPipeGroups + 3 * (size_t)D) * sizeof(int), s)) return err;
+    const int lag = xs_pipe_lag();
+#define MFA_XS_PIPE(RR, VV)                                                                     \
+  {                                                                                             \
+    auto kern = xs_pipe_kernel<Q, RR, VV, T>;                                                   \
+    const int G = pipe_grid(kern, lds1, D, S);                                                  \
+    hipLaunchKernelGGL(kern, dim3(G), dim3(256), lds1, s, X, cap, ret, indp, D, N, P, Pseg, S,  \
+                       C, lag, pm, tol, f, e, r2, stats, status, mom, coef, sums, okm, sync);   \
+  }
+    if (det) MFA_XS_PIPE(kRepMax, VAR | 32)
+    else if (rep8) MFA_XS_PIPE(kRepMax, VAR)
+    else MFA_XS_PIPE(1, VAR)
+#undef MFA_XS_PIPE
   } else if (chunked) {
     const dim3 g(D * S);
     if (det)

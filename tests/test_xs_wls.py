@@ -319,13 +319,17 @@ def test_chunked_path_matches_oracle(cuda, dtype, S, D, N, P, Q, empty):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
-@pytest.mark.parametrize("C,D,N,P,Q,empty", [(2, 9, 1000, 31, 10, 1), (4, 37, 5000, 31, 10, 2),
-                                             (8, 4, 4096, 12, 3, 0), (3, 5, 1544, 0, 4, 0),
-                                             (7, 3, 4000, 28, 16, 1), (4, 300, 5000, 31, 10, 1)])
-def test_team_path_matches_oracle(cuda, dtype, C, D, N, P, Q, empty):
-    """Team (cooperative) kernel: C workgroups per date publish partial moments, wait for the
-    team, solve redundantly and re-read only their chunk == the float64 oracle; deterministic
-    mode is bitwise reproducible and equal to the chunked path's combine order."""
+@pytest.mark.parametrize("C,D,N,P,Q,empty,lag", [(2, 9, 1000, 31, 10, 1, 1),
+                                                 (4, 37, 5000, 31, 10, 2, 1),
+                                                 (8, 4, 4096, 12, 3, 0, 2), (3, 5, 1544, 0, 4, 0, 1),
+                                                 (7, 3, 4000, 28, 16, 1, 3),
+                                                 (4, 300, 5000, 31, 10, 1, 2),
+                                                 (16, 61, 5000, 31, 10, 1, 1)])
+def test_team_path_matches_oracle(cuda, dtype, C, D, N, P, Q, empty, lag):
+    """Pipelined team kernel (persistent grid): C chunks per date, partial moments published
+    and solved by the date's last arriver, each chunk's residual pass `lag` tickets later by
+    the workgroup that streamed it == the float64 oracle; deterministic mode is bitwise
+    reproducible."""
     from llm_driven_multi_factor_model_amd import _native
     panel = synthetic_panel(D, N, P, Q, seed=C * 11 + D, missing_frac=0.02,
                             empty_industries=empty, dtype=dtype)
@@ -333,6 +337,7 @@ def test_team_path_matches_oracle(cuda, dtype, C, D, N, P, Q, empty):
     g = panel.to(cuda)
     lib = _native.lib()
     lib.mfa_xs_set_coop(C)
+    lib.mfa_xs_set_pipe(lag, 0)
     try:
         assert _native.query("mfa_xs_coop_chunks", D, N) == C
         out = X.xs_wls(g.styles, g.cap, g.ret, g.ind, P)
@@ -340,6 +345,7 @@ def test_team_path_matches_oracle(cuda, dtype, C, D, N, P, Q, empty):
         torch.cuda.synchronize()
     finally:
         lib.mfa_xs_set_coop(0)
+        lib.mfa_xs_set_pipe(1, 0)
     assert not bool((out.status & 64).any()), "team wait timed out"
     torch.testing.assert_close(out.f.cpu(), ref.f, rtol=1e-9, atol=1e-12)
     torch.testing.assert_close(out.r2.cpu(), ref.r2, rtol=1e-9, atol=1e-11)

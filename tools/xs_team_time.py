@@ -41,6 +41,7 @@ def main():
     dates = [int(x) for x in os.environ.get("DATES", "315,2520").split(",")]
     chunks = [int(x) for x in os.environ.get("CHUNKS", "2,3,4,6,8").split(",") if x]
     dtypes = os.environ.get("DTYPES", "fp64,fp32").split(",")
+    lags = [int(x) for x in os.environ.get("LAGS", "1").split(",")]
     lib = _native.lib()
     for dt in dtypes:
         base = synthetic_panel(max(dates), N, P, Q, seed=1, device=dev, missing_frac=0.01,
@@ -52,8 +53,9 @@ def main():
             p = base.slice_dates(0, D)
             st, cp, rt, ind = (t.contiguous() for t in (p.styles, p.cap, p.ret, p.ind))
             ref = None
-            for C in [0] + chunks:
+            for C, lag in [(0, 0)] + [(c, l) for c in chunks for l in lags]:
                 lib.mfa_xs_set_coop(C)
+                lib.mfa_xs_set_pipe(max(lag, 1), 0)
                 try:
                     ws = X.xs_wls_workspace(D, P, Q, dev, N)
                     out = X.xs_wls(st, cp, rt, ind, P, workspace=ws)
@@ -62,7 +64,8 @@ def main():
                     cc = _native.query("mfa_xs_coop_chunks", D, N)
                 finally:
                     lib.mfa_xs_set_coop(0)
-                rec = {"storage": dt, "D": D, "coop": C, "chunks": cc, "us_med": round(med, 1),
+                    lib.mfa_xs_set_pipe(1, 0)
+                rec = {"storage": dt, "D": D, "coop": C, "lag": lag, "chunks": cc, "us_med": round(med, 1),
                        "us_min": round(mn, 1), "Mreg_s": round(D / med, 3),
                        "timeouts": int((out.status & 64).ne(0).sum())}
                 if ref is None:
