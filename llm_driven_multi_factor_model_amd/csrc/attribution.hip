@@ -96,6 +96,79 @@ int portfolio_exposure_dispatch(const T* X, const T* cap, const T* ret, const in
   return (int)hipGetLastError();
 }
 
+// Point-in-time trailing specific volatility (RiskModel.specific_vol_series): for every stock
+// n and local date t, the ddof-0 std of the finite values among the W rows ENDING at t of
+// ext = [halo (h rows) ; e (D rows)], summed NEWEST FIRST with one rounding per operation
+// (count += ok, s1 += x, s2 += fl(x * x); mean = s1 / n, var = fl(s2 / n) - fl(mean * mean)),
+// i.e. bitwise the order of the tensor loop it replaces (risk_model.py) -- and so bitwise
+// rank-invariant, the property that loop was written for.  One thread per (stock, TD-date
+// tile): the W-row window slides through a register array (one load per step, unrolled by TD
+// so the slide is a register renaming); stocks are the contiguous axis, so every load of a
+// wave is one 512-byte row segment.  The tensor loop moved 3 x W full [D, N] temporaries
+// (~50 ms at 2520 x 5000); this reads each ext row ~(W + TD) / TD times from L2.
+template <int TD>
+__global__ __launch_bounds__(256) void trailing_vol_kernel(const double* __restrict__ halo, int h,
+                                                           const double* __restrict__ e, int D,
+                                                           int N, int W, int minp,
+                                                           double* __restrict__ vol) {
+  // one rounding per operation, as the tensor loop: the library builds with
+  // -ffp-contract=fast (which ignores `#pragma clang fp contract`), and HIP's __dadd_rn /
+  // __dmul_rn are plain + / * that it would fuse -- an empty asm on each product blocks that
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  const int t0 = blockIdx.y * TD;
+  const int nt = D - t0 < TD ? D - t0 : TD;
+  auto ld = [&](int i) -> double {  // ext row i (0 outside, never summed)
+    if (i < 0 || i >= h + D) return 0.0;
+    return i < h ? halo[(size_t)i * N + n] : e[(size_t)(i - h) * N + n];
+  };
+  double c[TD], s1[TD], s2[TD], win[TD];
+#pragma unroll
+  for (int k = 0; k < TD; ++k) {
+    c[k] = 0.0;
+    s1[k] = 0.0;
+    s2[k] = 0.0;
+    win[k] = k < nt ? ld(t0 + k + h) : 0.0;  // step j = 0: row t itself
+  }
+  int j = 0;
+  auto step = [&]() {
+#pragma unroll
+    for (int k = 0; k < TD; ++k) {
+      const double x = win[k];
+      const bool ok = __builtin_isfinite(x);
+      const double xz = ok ? x : 0.0;
+      c[k] = __dadd_rn(c[k], ok ? 1.0 : 0.0);
+      s1[k] = __dadd_rn(s1[k], xz);
+      double sq = __dmul_rn(xz, xz);
+      asm volatile("" : "+v"(sq));
+      s2[k] = __dadd_rn(s2[k], sq);
+    }
+    // next step: win[k] <- row t0 + k + h - (j + 1) = the current win[k - 1]
+#pragma unroll
+    for (int k = TD - 1; k > 0; --k) win[k] = win[k - 1];
+    ++j;
+    win[0] = j < W ? ld(t0 + h - j) : 0.0;
+  };
+  int w = 0;
+  for (; w + TD <= W; w += TD) {
+#pragma unroll
+    for (int u = 0; u < TD; ++u) step();
+  }
+  for (; w < W; ++w) step();
+  const double thr = minp > 1 ? (double)minp : 1.0;
+#pragma unroll
+  for (int k = 0; k < TD; ++k) {
+    if (k < nt) {
+      const double mean = __ddiv_rn(s1[k], c[k]);
+      double m2 = __dmul_rn(mean, mean);
+      asm volatile("" : "+v"(m2));
+      const double var = __dsub_rn(__ddiv_rn(s2[k], c[k]), m2);
+      const double v = __dsqrt_rn(var > 0.0 ? var : 0.0);
+      vol[(size_t)(t0 + k) * N + n] = c[k] >= thr ? v : qnan();
+    }
+  }
+}
+
 }  // namespace
 
 // X [D][Q][N] f32, cap/ret [D][N] f32 (validity only), ind [D][N] int16 (nullable when P == 0),
@@ -112,4 +185,17 @@ MFA_API int mfa_portfolio_exposure_f64(const double* X, const double* cap, const
                                        const int16_t* ind, const double* h, const double* stats,
                                        int D, int N, int P, int Q, double* out, void* stream) {
   return portfolio_exposure_dispatch<double>(X, cap, ret, ind, h, stats, D, N, P, Q, out, stream);
+}
+
+// vol [D][N] = trailing point-in-time specific volatility of e [D][N] over W rows ending at each
+// date, with halo [h][N] (h = W - 1 rows preceding e; NaN where none).  Bitwise equal to the
+// newest-first tensor loop of RiskModel.specific_vol_series.
+MFA_API int mfa_trailing_vol(const double* halo, int h, const double* e, int D, int N, int W,
+                             int min_periods, double* vol, void* stream) {
+  if (D <= 0 || N <= 0) return 0;
+  if (W < 1 || h < 0 || (h > 0 && !halo)) return (int)hipErrorInvalidValue;
+  constexpr int TD = 16;
+  hipLaunchKernelGGL(trailing_vol_kernel<TD>, dim3((N + 255) / 256, (D + TD - 1) / TD), dim3(256),
+                     0, (hipStream_t)stream, halo, h, e, D, N, W, min_periods, vol);
+  return (int)hipGetLastError();
 }

@@ -1084,14 +1084,33 @@ __device__ __forceinline__ int tri2_row_off(int s) {
   return 8 * (g * KP - 4 * g * (g - 1)) + (s - 8 * g) * (KP - 8 * g);
 }
 
-template <int KP, bool PF = false>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MFA_TRI2_WPE))) void
+// ABL: timing-only ablations (bias modes 61..67 = 60 + ABL, division-free Sturm, KP = 44):
+// 1 = no Laguerre iterations, 2 = no eigenvector / back-transform, 4 = no tridiagonalisation;
+// outputs meaningless.
+// EIG: batched symmetric eigendecomposition with the same machinery (eigh of F0): D0 = the input
+// matrices [B][K][K] (symmetrised), M = 1, vout = w [B][K] descending, Uout [B][K][K] with
+// U[:, k] = eigenvector k; flag[b] = 1 when the twisted-factorisation eigenvectors of a
+// clustered spectrum are not orthogonal to 1e-12 (the caller re-solves those matrices with the
+// Jacobi), 0 otherwise.  Non-finite matrices give NaN.
+template <int KP, bool PF = false, int ABL = 0, int WPE = MFA_TRI2_WPE, bool EIG = false>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void
 mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* __restrict__ Cz,
-                    const int* __restrict__ dvalid, double* __restrict__ vout) {
+                    const int* __restrict__ dvalid, double* __restrict__ vout,
+                    double* __restrict__ Uout, int* __restrict__ flag) {
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int d = blockIdx.x / M, m = blockIdx.x % M, lane = threadIdx.x;
   double* vo = vout + ((size_t)d * M + m) * K;
-  if (!dvalid[d]) {
+  const double* Ain = D0 + (size_t)d * K * K;  // EIG input matrix
+  if constexpr (EIG) {
+    bool fin = true;
+    for (int e = lane; e < K * K; e += 64) fin = fin && __builtin_isfinite(Ain[e]);
+    if (!__all(fin)) {
+      for (int k = lane; k < K; k += 64) vo[k] = qnan();
+      for (int e = lane; e < K * K; e += 64) Uout[(size_t)d * K * K + e] = qnan();
+      if (lane == 0) flag[d] = 0;
+      return;
+    }
+  } else if (!dvalid[d]) {
     for (int k = lane; k < K; k += 64) vo[k] = qnan();
     return;
   }
@@ -1103,21 +1122,30 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
   double* ta = be + 64;                    // [64] tau_s
   double* dd = ta + 64;                    // [64] sqrt(D0)
   double* gs = dd + 64;                    // [64] diagonal of A, descending; Laguerre x later
-  const double* d0 = D0 + (size_t)d * K;
-  const double di = lane < K ? sqrt(fmax(d0[lane], 0.0)) : 0.0;
-  dd[lane] = di;
-  lds_order();
-  // lane i's row of A = S C_z S from the coalesced columns of the symmetric C_z
-  const double* c = Cz + (size_t)m * K * K;
   const int li = lane < K ? lane : 0;
   double a[KP];
+  double di = 0.0;
+  const double* c = Cz + (size_t)m * K * K;
+  if constexpr (EIG) {  // lane i's row of the symmetrised input
 #pragma unroll
-  for (int j = 0; j < KP; ++j) {
-    a[j] = j < K ? di * c[j * K + li] * dd[j] : 0.0;
-    if ((j & 7) == 7) lds_batch();  // 8 loads in flight, not all 44 (register peak)
+    for (int j = 0; j < KP; ++j) {
+      a[j] = j < K ? 0.5 * (Ain[j * K + li] + Ain[li * K + j]) : 0.0;
+      if ((j & 7) == 7) lds_batch();
+    }
+  } else {
+    const double* d0 = D0 + (size_t)d * K;
+    di = lane < K ? sqrt(fmax(d0[lane], 0.0)) : 0.0;
+    dd[lane] = di;
+    lds_order();
+    // lane i's row of A = S C_z S from the coalesced columns of the symmetric C_z
+#pragma unroll
+    for (int j = 0; j < KP; ++j) {
+      a[j] = j < K ? di * c[j * K + li] * dd[j] : 0.0;
+      if ((j & 7) == 7) lds_batch();  // 8 loads in flight, not all 44 (register peak)
+    }
   }
   {
-    const double g = lane < K ? di * c[li * K + li] * di : 0.0;
+    const double g = lane < K ? (EIG ? Ain[li * K + li] : di * c[li * K + li] * di) : 0.0;
     wb[lane] = g;
     lds_order();
     if (lane < K) {  // descending rank of the diagonal (ties by index): initial guesses
@@ -1193,9 +1221,16 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
     }
   };
   static_assert(KP % 4 == 0, "KP: multiple of 4");
-  [&]<int... G>(std::integer_sequence<int, G...>) {
-    (steps(std::integral_constant<int, 8 * G>{}), ...);
-  }(std::make_integer_sequence<int, (KP + 7) / 8>{});
+  if constexpr ((ABL & 4) == 0) {
+    [&]<int... G>(std::integer_sequence<int, G...>) {
+      (steps(std::integral_constant<int, 8 * G>{}), ...);
+    }(std::make_integer_sequence<int, (KP + 7) / 8>{});
+  } else {  // ablation: T = the sorted diagonal with a weak coupling, no reflectors
+    const double g = gs[lane];
+    tb[lane] = double2{g, lane > 0 ? 1e-12 * g * g : 0.0};
+    be[lane] = 1e-6 * g;
+    ta[lane] = 0.0;
+  }
   lds_order();
   // ---- 2. eigenvalue of rank `lane` (descending): as mc_bias_tri_kernel ----
   double lo_l = 0.0, hi_l = 0.0, b2max = 0.0;
@@ -1234,7 +1269,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
     if (cl <= jt) lo = fmax(lo, xl); else hi = fmin(hi, xl);
   }
   double lam = x;
-  if (lane < K) {
+  if (lane < K && (ABL & 1) == 0) {
     int prev = -1;
     double sprev = __builtin_inf();
     for (int it = 0; it < 256; ++it) {
@@ -1259,6 +1294,10 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
       if (cnt <= jt) lo = x; else hi = x;
     }
     lam = x;
+  }
+  if constexpr ((ABL & 2) != 0) {  // ablation: no eigenvectors / back-transform
+    if (lane < K) vo[lane] = lam;
+    return;
   }
   // ---- 3. eigenvector of T at lam: twisted factorisation in the y registers only ----
   double y[KP];
@@ -1349,6 +1388,37 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
     constexpr int NG = (KP + 7) / 8;
     (back(std::integral_constant<int, 8 * (NG - 1 - G)>{}, 8 * (NG - 1 - G) + 7), ...);
   }(std::make_integer_sequence<int, (KP + 7) / 8>{});
+  if constexpr (EIG) {
+    // w (descending by lane rank), U[:, k] = y of lane k, and the orthogonality check of the
+    // eigenvectors through the rows of Y in LDS (after the tables, which are still live here)
+    double* Ys = gs + 64;
+    double* Ub = Uout + (size_t)d * K * K;
+    if (lane < K) {
+      vo[lane] = lam;
+#pragma unroll
+      for (int j = 0; j < KP; ++j) {
+        if (j < K) Ub[j * K + lane] = y[j];
+        Ys[lane * KP + j] = y[j];
+      }
+    }
+    lds_order();
+    double err = 0.0;
+    if (lane < K) {
+      for (int l = 0; l < K; ++l) {
+        const double* yl = Ys + l * KP;
+        double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+        for (int j = 0; j < KP; j += 2) {
+          t0 = fma(y[j], yl[j], t0);
+          t1 = fma(y[j + 1], yl[j + 1], t1);
+        }
+        err = fmax(err, fabs(t0 + t1 - (l == lane ? 1.0 : 0.0)));
+      }
+    }
+    err = wave_max(err);
+    if (lane == 0) flag[d] = (err > 1e-12 || !(err == err)) ? 1 : 0;
+    return;
+  }
   if (lane < K) {
     double v = 0.0;
 #pragma unroll
@@ -1363,6 +1433,7 @@ size_t bias_tri2_lds(int K, int KP) {
   for (int s = 0; s + 2 < K; ++s) n += KP - 8 * (s / 8);
   return ((size_t)((n + 1) & ~1) + 64 + 128 + 4 * 64) * sizeof(double);
 }
+size_t eigh_tri2_lds(int K, int KP) { return bias_tri2_lds(K, KP) + (size_t)K * KP * sizeof(double); }
 
 // ---------------- pair-block Jacobi WITH eigenvectors (batched eigh of F0) ----------------
 // Same tournament-position scheme as jacobi_pairs, carrying packed A and the full eigenvector
@@ -1475,14 +1546,17 @@ size_t eigh_pairs_lds(int K) {
          32 * sizeof(double2) + 64 * sizeof(int);
 }
 
+// only != nullptr: re-solve only the matrices with only[b] != 0 (the tridiagonal eigh's flags)
 template <int NB, int NBV, int FAST = 0>
 __global__ __launch_bounds__(64) void eigh_pairs_kernel(const double* __restrict__ Ain, int K,
                                                         int max_sweeps, double tol,
                                                         double* __restrict__ w,
                                                         double* __restrict__ U,
-                                                        int* __restrict__ sweeps) {
+                                                        int* __restrict__ sweeps,
+                                                        const int* __restrict__ only) {
   extern __shared__ double sm[];
   const int b = blockIdx.x, lane = threadIdx.x;
+  if (only && !only[b]) return;
   const int Ke = K + (K & 1);
   const int np = pk_size(Ke);
   double* A = sm;
@@ -1587,10 +1661,14 @@ __global__ __launch_bounds__(256) void eigen_finalize_kernel(const double* __res
   }
 }
 
-int g_eigh_mode = 0;  // 0 = pair-block tournament Jacobi, 1 = row/column cyclic Jacobi (A/B)
+int g_eigh_mode = 2;  // 0 = pair-block tournament Jacobi, 1 = row/column cyclic Jacobi (A/B),
+                      // 2 = Householder tridiagonal (mc_bias_tri2_kernel<EIG>) + the pair-block
+                      //     Jacobi for the matrices it flags (non-orthogonal eigenvectors)
 int g_fast_rot = 1;   // 1 = rcp/rsq + Newton rotation parameters (jacobi_cs<1>); 0 = IEEE div/sqrt
-int g_bias_mode = 3;  // 0 = packed (A, M) double2; 1 = split fp64 A / fp64 M; 2 = split, fp32 M;
-                      // 3 = Householder tridiagonal + Newton / twisted factorisation
+int g_bias_mode = 5;  // 0 = packed (A, M) double2; 1 = split fp64 A / fp64 M; 2 = split, fp32 M;
+                      // 3 = Householder tridiagonal + Laguerre / twisted factorisation;
+                      // 4 = its lean-layout kernel; 5 = lean layout + division-free Sturm
+                      // (default: 13.1 vs 17.5 ms for mode 3, profiles/r03_team/)
 
 size_t eigh_lds(int K) { return ((size_t)2 * K * (K + 1) + 4 * 64 + 64) * sizeof(double) + 64 * sizeof(int); }
 
@@ -1608,10 +1686,10 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
     if (K <= KP_) {                                                                        \
       if (g_bias_mode == 5)                                                                \
         hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, true>), dim3(D * M), dim3(64),        \
-                           bias_tri2_lds(K, KP_), s, D0, K, M, Cz, dvalid, ws);            \
+                           bias_tri2_lds(K, KP_), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr);            \
       else                                                                                 \
         hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, false>), dim3(D * M), dim3(64),       \
-                           bias_tri2_lds(K, KP_), s, D0, K, M, Cz, dvalid, ws);            \
+                           bias_tri2_lds(K, KP_), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr);            \
       return true;                                                                         \
     }
     MFA_TRI2(8)
@@ -1623,6 +1701,26 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
     MFA_TRI2(64)
 #undef MFA_TRI2
     return false;
+  }
+  if ((g_bias_mode == 6 || g_bias_mode == 7) && K <= 44) {  // A/B: mode 5 at 4 / 5 waves per SIMD
+    if (g_bias_mode == 6)
+      hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, 4>), dim3(D * M), dim3(64),
+                         bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr);
+    else
+      hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, 5>), dim3(D * M), dim3(64),
+                         bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr);
+    return true;
+  }
+  if (g_bias_mode > 60 && g_bias_mode < 68 && K <= 44) {  // timing-only ablations of mode 5
+    const int abl = g_bias_mode - 60;
+#define MFA_TRI2_ABL(A_)                                                                     \
+    if (abl == A_)                                                                         \
+      hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, A_>), dim3(D * M), dim3(64),       \
+                         bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr);
+    MFA_TRI2_ABL(1) MFA_TRI2_ABL(2) MFA_TRI2_ABL(3) MFA_TRI2_ABL(4) MFA_TRI2_ABL(5)
+    MFA_TRI2_ABL(6) MFA_TRI2_ABL(7)
+#undef MFA_TRI2_ABL
+    return true;
   }
 #define MFA_TRI(KP_)                                                                         \
   if (K <= KP_) {                                                                          \
@@ -1654,7 +1752,7 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
 
 #define MFA_BIAS_LAUNCH(NBV_)                                                                   \
   {                                                                                            \
-    if ((g_bias_mode >= 3 && g_bias_mode <= 5) || (g_bias_mode > 40 && g_bias_mode < 60))      \
+    if ((g_bias_mode >= 3 && g_bias_mode <= 7) || (g_bias_mode > 40 && g_bias_mode < 68))      \
       launch_bias_tri(D0, D, K, M, Cz, dvalid, ws, s);                                         \
     else if (g_bias_mode == 1)                                                                 \
       hipLaunchKernelGGL((mc_bias_split_kernel<NBV_, 1, double>), dim3(D * M), dim3(64),       \
@@ -1678,15 +1776,31 @@ MFA_API int mfa_eigh_batched(const double* A, int B, int K, int max_sweeps, doub
   hipStream_t s = (hipStream_t)stream;
   const int lpp = 64 / npair, rows_per_lane = (K + lpp - 1) / lpp;
   (void)nv;
-  if (g_eigh_mode == 0 && nb <= 4 * 64 && rows_per_lane <= 14 && g_fast_rot)
+  // mode 2: `sweeps` receives the tridiagonal solver's per-matrix fallback flags (required)
+  const int* only = nullptr;
+  if (g_eigh_mode == 2 && sweeps) {
+    bool done = false;
+#define MFA_EIGT(KP_)                                                                          \
+    if (!done && K <= KP_) {                                                                 \
+      hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, true, 0, MFA_TRI2_WPE, true>), dim3(B),   \
+                         dim3(64), eigh_tri2_lds(K, KP_), s, A, K, 1, (const double*)nullptr, \
+                         (const int*)nullptr, w, U, sweeps);                                 \
+      done = true;                                                                           \
+    }
+    MFA_EIGT(8) MFA_EIGT(16) MFA_EIGT(24) MFA_EIGT(32) MFA_EIGT(44) MFA_EIGT(48) MFA_EIGT(64)
+#undef MFA_EIGT
+    only = sweeps;  // the Jacobi below re-solves the flagged matrices only
+    sweeps = nullptr;
+  }
+  if (g_eigh_mode != 1 && nb <= 4 * 64 && rows_per_lane <= 14 && g_fast_rot)
     hipLaunchKernelGGL((eigh_pairs_kernel<4, 14, 1>), dim3(B), dim3(64), eigh_pairs_lds(K), s, A,
-                       K, max_sweeps, tol, w, U, sweeps);
-  else if (g_eigh_mode == 0 && nb <= 4 * 64 && rows_per_lane <= 14)
+                       K, max_sweeps, tol, w, U, sweeps, only);
+  else if (g_eigh_mode != 1 && nb <= 4 * 64 && rows_per_lane <= 14)
     hipLaunchKernelGGL((eigh_pairs_kernel<4, 14>), dim3(B), dim3(64), eigh_pairs_lds(K), s, A, K,
-                       max_sweeps, tol, w, U, sweeps);
-  else if (g_eigh_mode == 0)
+                       max_sweeps, tol, w, U, sweeps, only);
+  else if (g_eigh_mode != 1)
     hipLaunchKernelGGL((eigh_pairs_kernel<9, 32>), dim3(B), dim3(64), eigh_pairs_lds(K), s, A, K,
-                       max_sweeps, tol, w, U, sweeps);
+                       max_sweeps, tol, w, U, sweeps, only);
   else
     hipLaunchKernelGGL(eigh_kernel, dim3(B), dim3(64), eigh_lds(K), s, A, K, max_sweeps, tol, w, U,
                        sweeps);

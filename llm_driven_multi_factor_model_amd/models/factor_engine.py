@@ -722,3 +722,46 @@ def synthetic_prices(N: int = 50, T: int = 300, seed: int = 0, n_ind: int = 8, s
                        "l1_name": [f"industry_{j % n_ind}" for j in range(len(codes))],
                        "in_date": "20000101", "out_date": None, "is_new": "Y"})
     return prices, index, sw
+
+
+def synthetic_prices_fast(N: int = 5000, T: int = 2520, seed: int = 0, n_ind: int = 31,
+                          suspend_frac: float = 0.0, start: str = "2019-01-02"):
+    """Vectorised :func:`synthetic_prices` for benchmark-sized panels (5000 x 2520 in seconds
+    instead of minutes): same schema and the same generating model, a different random stream
+    (per-field arrays instead of per-row draws), so it does not reproduce the fixtures that
+    :func:`synthetic_prices` feeds."""
+    rng = np.random.default_rng(seed)
+    dates = pd.bdate_range(start, periods=T)
+    mkt = rng.normal(0.0003, 0.012, T)
+    idx_close = 3000 * np.exp(np.cumsum(mkt))
+    qends = pd.date_range(dates[0] - pd.Timedelta(days=400), dates[-1], freq="QE")
+    nq = len(qends)
+    kq = np.maximum(np.searchsorted(qends.values, (dates - pd.Timedelta(days=45)).values) - 1, 0)
+    beta = rng.uniform(0.5, 1.5, N)
+    close = 10 * np.exp(np.cumsum(beta[:, None] * mkt[None, :] + rng.normal(0, 0.02, (N, T)), axis=1))
+    shares = rng.lognormal(10, 1, N)
+    keep = (rng.random((N, T)) >= suspend_frac).ravel()
+    q = {name: gen for name, gen in (("n_cashflow_act", rng.normal(1e8, 5e7, (N, nq))),
+                                     ("total_ncl", rng.lognormal(20, 1, (N, nq))),
+                                     ("total_hldr_eqy_inc_min_int", rng.lognormal(21, 1, (N, nq))),
+                                     ("debt_to_assets", rng.uniform(20, 80, (N, nq))),
+                                     ("q_profit_yoy", rng.normal(10, 30, (N, nq))),
+                                     ("q_sales_yoy", rng.normal(8, 20, (N, nq))))}
+    codes = np.array([f"{600000 + i:06d}.SH" if i % 2 else f"{i:06d}.SZ" for i in range(N)])
+    mv = close * shares[:, None]
+    cols = {"ts_code": np.repeat(codes, T), "trade_date": np.tile(dates.values, N),
+            "close": close.ravel(), "total_mv": mv.ravel(), "circ_mv": (mv * 0.7).ravel(),
+            "pb": rng.uniform(0.5, 8, N * T), "turnover_rate": rng.uniform(0.1, 5, N * T),
+            "pe_ttm": rng.uniform(5, 60, N * T), "n_cashflow_act": q["n_cashflow_act"][:, kq].ravel(),
+            "end_date": np.tile(qends.values[kq], N)}
+    for name in ("total_ncl", "total_hldr_eqy_inc_min_int", "debt_to_assets", "q_profit_yoy",
+                 "q_sales_yoy"):
+        cols[name] = q[name][:, kq].ravel()
+    prices = pd.DataFrame({k: v[keep] for k, v in cols.items()})
+    for c in ["close", "total_mv", "circ_mv", "pb", "turnover_rate", "pe_ttm"]:
+        prices[c] = prices[c].astype(np.float32).astype(np.float64)  # reference downcasts (Q27)
+    index = pd.DataFrame({"ts_code": "000300.SH", "trade_date": dates, "close": idx_close})
+    sw = pd.DataFrame({"ts_code": codes, "l1_code": [f"80{j % n_ind:04d}.SI" for j in range(N)],
+                       "l1_name": [f"industry_{j % n_ind}" for j in range(N)],
+                       "in_date": "20000101", "out_date": None, "is_new": "Y"})
+    return prices, index, sw

@@ -329,7 +329,11 @@ class RiskModel:
         e = self.specific_ret.double()
         D = e.shape[0]
         h = window - 1
-        ext = torch.cat([pdist.halo_prev_rows(e, h, self.ctx, self.sizes), e])
+        halo = pdist.halo_prev_rows(e, h, self.ctx, self.sizes)
+        if e.is_cuda:  # HIP kernel, bitwise the loop below (csrc/attribution.hip)
+            from ..ops.attribution import trailing_vol
+            return trailing_vol(halo, e, window, min_periods)
+        ext = torch.cat([halo, e])
         ok = torch.isfinite(ext)
         x = torch.where(ok, ext, torch.zeros((), dtype=torch.float64, device=e.device))
         okd = ok.double()

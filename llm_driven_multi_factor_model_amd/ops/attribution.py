@@ -28,6 +28,27 @@ _native.register("mfa_portfolio_exposure_f64", [C.c_void_p] * 6 + [C.c_int] * 4 
                  [C.c_void_p, C.c_void_p])
 
 
+_native.register("mfa_trailing_vol", [C.c_void_p, C.c_int, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                       C.c_int, C.c_void_p, C.c_void_p])
+
+
+def trailing_vol(halo: torch.Tensor, e: torch.Tensor, window: int, min_periods: int = 1) -> torch.Tensor:
+    """[D, N] point-in-time trailing ddof-0 std over the ``window`` rows ending at each date of
+    ``cat([halo, e])`` (``halo`` = the window - 1 preceding rows, NaN where none), finite values
+    only; NaN below ``min_periods`` values.  GPU: one HIP kernel, bitwise equal to the
+    newest-first loop of :meth:`RiskModel.specific_vol_series` (its CPU path)."""
+    D, N = e.shape
+    h = window - 1
+    if halo.shape != (h, N):
+        raise ValueError(f"halo must be [{h}, {N}], got {tuple(halo.shape)}")
+    e = _native.check_device_tensor(e, torch.float64, "e")
+    halo = halo.to(torch.float64).contiguous()
+    vol = torch.empty(D, N, dtype=torch.float64, device=e.device)
+    _native.call("mfa_trailing_vol", _native.ptr(halo) if h > 0 else None, h, _native.ptr(e), D, N,
+                 window, min_periods, _native.ptr(vol), _native.stream(e.device))
+    return vol
+
+
 def portfolio_exposure(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor,
                        ind: torch.Tensor | None, h: torch.Tensor, stats: torch.Tensor,
                        P: int) -> torch.Tensor:

@@ -47,8 +47,11 @@ TOL = 1e-15
 
 # Per-(date, sim) solver of the bias statistic (csrc/eigen.hip): "jacobi" = pair-block
 # tournament Jacobi carrying M = V^T D0 V; "tridiag" = Householder tridiagonalisation,
-# count-guided Laguerre eigenvalues, twisted-factorisation eigenvectors, back-transform.
-BIAS_SOLVERS = {"jacobi": 0, "tridiag": 3}
+# count-guided Laguerre eigenvalues (division-free Sturm recurrence), twisted-factorisation
+# eigenvectors, back-transform, lean register / LDS layout (mode 5, the default);
+# "tridiag_v1" / "tridiag_lean" = the round-2 kernel (mode 3) / lean layout with the pivot-form
+# Sturm recurrence (mode 4), kept for A/B.
+BIAS_SOLVERS = {"jacobi": 0, "tridiag": 5, "tridiag_v1": 3, "tridiag_lean": 4}
 _bias_solver = "tridiag"
 
 
@@ -92,8 +95,11 @@ def eigh(A: torch.Tensor, max_sweeps: int = MAX_SWEEPS, tol: float = TOL):
     B = Ab.shape[0]
     w = torch.empty(B, K, dtype=torch.float64, device=A.device)
     U = torch.empty(B, K, K, dtype=torch.float64, device=A.device)
+    # Householder-tridiagonal eigh; `flags` marks matrices whose eigenvectors came out
+    # non-orthogonal (clustered spectra), re-solved by the Jacobi in the same call (no sync)
+    flags = torch.empty(B, dtype=torch.int32, device=A.device)
     _native.call("mfa_eigh_batched", _native.ptr(Ab), B, K, max_sweeps, tol, _native.ptr(w),
-                 _native.ptr(U), _native.ptr(None), _native.stream(A.device))
+                 _native.ptr(U), _native.ptr(flags), _native.stream(A.device))
     return w.reshape(shp[:-1]), U.reshape(shp)
 
 

@@ -73,3 +73,43 @@ def test_hip_portfolio_exposure_matches_oracle(cuda):
     gp = p.to(cuda)
     got = attr.portfolio_exposure(gp.styles, gp.cap, gp.ret, gp.ind, h.to(cuda), out.stats.to(cuda), p.P)
     torch.testing.assert_close(got.cpu(), ref, rtol=1e-11, atol=1e-14)
+
+
+def _trailing_vol_loop(halo, e, window, min_periods=1):
+    """The newest-first tensor loop of RiskModel.specific_vol_series (its CPU path)."""
+    D = e.shape[0]
+    h = window - 1
+    ext = torch.cat([halo, e])
+    ok = torch.isfinite(ext)
+    okd = ok.double()
+    n, s1, s2 = torch.zeros_like(e), torch.zeros_like(e), torch.zeros_like(e)
+    x = torch.where(ok, ext, torch.zeros((), dtype=torch.float64, device=e.device))
+    for j in range(window):
+        sl = slice(h - j, h - j + D)
+        n += okd[sl]
+        s1 += x[sl]
+        s2 += x[sl] * x[sl]
+    mean = s1 / n
+    vol = torch.sqrt(torch.clamp(s2 / n - mean * mean, min=0.0))
+    return torch.where(n >= max(1, min_periods), vol, torch.full_like(vol, float("nan")))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("D,N,window,minp", [(300, 777, 252, 1), (37, 300, 10, 4), (5, 64, 1, 1),
+                                             (2520, 520, 252, 20)])
+def test_trailing_vol_kernel_is_bitwise_the_loop(cuda, D, N, window, minp):
+    """The HIP trailing-vol kernel equals the newest-first tensor loop on the GPU bit for bit
+    (NaN rows, NaN halo, partial windows, a tile tail): rank-invariance of the point-in-time
+    specific vol rests on that fixed order.  (Against the CPU loop only to 1 ulp: torch's CPU
+    sqrt is SLEEF's 0.5001-ulp vector sqrt, not the correctly rounded one.)"""
+    g = torch.Generator().manual_seed(D + N)
+    e = torch.randn(D, N, generator=g, dtype=torch.float64) * 0.02
+    e[torch.rand(D, N, generator=g) < 0.05] = float("nan")
+    halo = torch.randn(window - 1, N, generator=g, dtype=torch.float64) * 0.02
+    halo[: (window - 1) // 2] = float("nan")
+    ref = _trailing_vol_loop(halo.to(cuda), e.to(cuda), window, minp).cpu()
+    got = attr.trailing_vol(halo.to(cuda), e.to(cuda), window, minp).cpu()
+    assert torch.equal(got.isnan(), ref.isnan())
+    assert torch.equal(got.nan_to_num(-1.0), ref.nan_to_num(-1.0))
+    cpu = _trailing_vol_loop(halo, e, window, minp)
+    torch.testing.assert_close(got, cpu, rtol=4e-16, atol=0, equal_nan=True)
