@@ -102,10 +102,11 @@ int portfolio_exposure_dispatch(const T* X, const T* cap, const T* ret, const in
 // (count += ok, s1 += x, s2 += fl(x * x); mean = s1 / n, var = fl(s2 / n) - fl(mean * mean)),
 // i.e. bitwise the order of the tensor loop it replaces (risk_model.py) -- and so bitwise
 // rank-invariant, the property that loop was written for.  One thread per (stock, TD-date
-// tile): the W-row window slides through a register array (one load per step, unrolled by TD
-// so the slide is a register renaming); stocks are the contiguous axis, so every load of a
-// wave is one 512-byte row segment.  The tensor loop moved 3 x W full [D, N] temporaries
-// (~50 ms at 2520 x 5000); this reads each ext row ~(W + TD) / TD times from L2.
+// tile): the tile's TD + W - 1 rows are walked newest to oldest in blocks of 16, the next block's
+// loads issued before the current block is summed (the loads are the latency); each row is
+// added to the outputs whose window holds it and +0.0 to the others (exact: the sums are never
+// -0.0).  Stocks are the contiguous axis, so every load of a wave is one 512-byte row segment.
+// The tensor loop moved 3 x W full [D, N] temporaries (~50 ms at 2520 x 5000).
 template <int TD>
 __global__ __launch_bounds__(256) void trailing_vol_kernel(const double* __restrict__ halo, int h,
                                                            const double* __restrict__ e, int D,
@@ -114,47 +115,51 @@ __global__ __launch_bounds__(256) void trailing_vol_kernel(const double* __restr
   // one rounding per operation, as the tensor loop: the library builds with
   // -ffp-contract=fast (which ignores `#pragma clang fp contract`), and HIP's __dadd_rn /
   // __dmul_rn are plain + / * that it would fuse -- an empty asm on each product blocks that
+  constexpr int RB = 16;  // rows per block
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
   const int t0 = blockIdx.y * TD;
   const int nt = D - t0 < TD ? D - t0 : TD;
-  auto ld = [&](int i) -> double {  // ext row i (0 outside, never summed)
+  auto ld = [&](int i) -> double {  // ext row i (0 outside; such rows are never active)
     if (i < 0 || i >= h + D) return 0.0;
     return i < h ? halo[(size_t)i * N + n] : e[(size_t)(i - h) * N + n];
   };
-  double c[TD], s1[TD], s2[TD], win[TD];
+  double c[TD], s1[TD], s2[TD];
 #pragma unroll
   for (int k = 0; k < TD; ++k) {
     c[k] = 0.0;
     s1[k] = 0.0;
     s2[k] = 0.0;
-    win[k] = k < nt ? ld(t0 + k + h) : 0.0;  // step j = 0: row t itself
   }
-  int j = 0;
-  auto step = [&]() {
+  // row offset o = row - (t0 + h): output k holds it iff k - W < o <= k; rows o = TD-1 .. -(W-1)
+  const int o_hi = TD - 1, nrows = TD + W - 1;
+  const int nblk = (nrows + RB - 1) / RB;
+  double xb[RB], nb[RB];
 #pragma unroll
-    for (int k = 0; k < TD; ++k) {
-      const double x = win[k];
-      const bool ok = __builtin_isfinite(x);
-      const double xz = ok ? x : 0.0;
-      c[k] = __dadd_rn(c[k], ok ? 1.0 : 0.0);
-      s1[k] = __dadd_rn(s1[k], xz);
+  for (int u = 0; u < RB; ++u) xb[u] = ld(t0 + h + o_hi - u);
+  for (int b = 0; b < nblk; ++b) {
+    const int ob = o_hi - b * RB;  // offset of the block's first (newest) row
+#pragma unroll
+    for (int u = 0; u < RB; ++u) nb[u] = b + 1 < nblk ? ld(t0 + h + ob - RB - u) : 0.0;
+#pragma unroll
+    for (int u = 0; u < RB; ++u) {
+      const int o = ob - u;
+      const double x = xb[u];
+      const bool fin = __builtin_isfinite(x);
+      const double xz = fin ? x : 0.0;
       double sq = __dmul_rn(xz, xz);
       asm volatile("" : "+v"(sq));
-      s2[k] = __dadd_rn(s2[k], sq);
+#pragma unroll
+      for (int k = 0; k < TD; ++k) {
+        const bool act = (k >= o) && (k - W < o) && (o > -W);
+        c[k] = __dadd_rn(c[k], act && fin ? 1.0 : 0.0);
+        s1[k] = __dadd_rn(s1[k], act ? xz : 0.0);
+        s2[k] = __dadd_rn(s2[k], act ? sq : 0.0);
+      }
     }
-    // next step: win[k] <- row t0 + k + h - (j + 1) = the current win[k - 1]
 #pragma unroll
-    for (int k = TD - 1; k > 0; --k) win[k] = win[k - 1];
-    ++j;
-    win[0] = j < W ? ld(t0 + h - j) : 0.0;
-  };
-  int w = 0;
-  for (; w + TD <= W; w += TD) {
-#pragma unroll
-    for (int u = 0; u < TD; ++u) step();
+    for (int u = 0; u < RB; ++u) xb[u] = nb[u];
   }
-  for (; w < W; ++w) step();
   const double thr = minp > 1 ? (double)minp : 1.0;
 #pragma unroll
   for (int k = 0; k < TD; ++k) {

@@ -451,6 +451,20 @@ __device__ __forceinline__ EwMap<NS> ew_shfl_up(const EwMap<NS>& m, int d) {
   return p;
 }
 
+// fp32-output finishers: v_rcp_f64 / v_rsq_f64 seeds + one Newton step (~2e-15 relative, far
+// below the fp32 rounding of the outputs) instead of the IEEE fp64 division / square-root
+// sequences (~12 / ~15 dependent instructions each), which dominated the per-row VALU count.
+__device__ __forceinline__ double frcp(double x) {
+  const double r = __builtin_amdgcn_rcp(x);
+  return fma(r, fma(-x, r, 1.0), r);
+}
+__device__ __forceinline__ double fsqrt(double x) {  // x >= 0
+  if (!(x > 0.0)) return 0.0;
+  double y = __builtin_amdgcn_rsq(x);
+  y = fma(0.5 * y, fma(-x * y, y, 1.0), y);
+  return x * y;
+}
+
 struct BetaOp {  // y ~ 1 + x (ret ~ mret): sums of 1, x, y, xx, xy, yy
   static constexpr int NS = 6;
   // v = 0 for an invalid row (NaN in either series); returns validity
@@ -463,15 +477,15 @@ struct BetaOp {  // y ~ 1 + x (ret ~ mret): sums of 1, x, y, xx, xy, yy
   __device__ static void emit(const double (&S)[NS], int n, int minp, int r, float* o0, float* o1) {
     float b = qnanf(), h = qnanf();
     if (n >= minp && n > 2) {
-      const double iw = 1.0 / S[0];
+      const double iw = frcp(S[0]);
       const double mx = S[1] * iw, my = S[2] * iw;
       const double vxx = S[3] * iw - mx * mx;
       const double cxy = S[4] * iw - mx * my;
       const double vyy = S[5] * iw - my * my;
-      const double bb = cxy / vxx;
+      const double bb = cxy * frcp(vxx);
       const double ssr = fmax(S[0] * (vyy - bb * cxy), 0.0);
       b = (float)bb;
-      h = (float)sqrt(ssr / (double)(n - 2));
+      h = (float)fsqrt(ssr * frcp((double)(n - 2)));
     }
     o0[r] = b;
     o1[r] = h;
@@ -489,8 +503,9 @@ struct DastdOp {  // e = ret - mret: sums of 1, e, ee; weighted population std
   __device__ static void emit(const double (&S)[NS], int n, int minp, int r, float* o0, float*) {
     float o = qnanf();
     if (n >= minp) {
-      const double m = S[1] / S[0];
-      o = (float)sqrt(fmax(S[2] / S[0] - m * m, 0.0));
+      const double iw = frcp(S[0]);
+      const double m = S[1] * iw;
+      o = (float)fsqrt(fmax(S[2] * iw - m * m, 0.0));
     }
     o0[r] = o;
   }
@@ -673,10 +688,19 @@ void launch_ew_pipe(const float* a, const float* b, const int* seg, int R, int W
                      s, a, b, seg, R, W, H, lam, minp, o0, o1, ntiles);
 }
 
+// A/B geometry of the anchored-prefix kernel (mfa_rolling_set_ew_variant): 0 = 8-row chunks x
+// 256 threads (2048-row tiles, default), 1 = 8 x 512 (4096-row tiles: half the halo re-read),
+// 2 = 16 x 256 (4096-row tiles, half the scan steps per row).
+int g_ew_variant = 0;
 template <class Op>
 void launch_ew(const float* a, const float* b, const int* seg, int R, int W, int H, double lam,
                int minp, float* o0, float* o1, hipStream_t s) {
-  launch_ew_pipe<Op, 8, 2048>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
+  if (g_ew_variant == 1)
+    launch_ew_pipe<Op, 8, 4096>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
+  else if (g_ew_variant == 2)
+    launch_ew_pipe<Op, 16, 4096>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
+  else
+    launch_ew_pipe<Op, 8, 2048>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
 }
 
 template <int H>
@@ -1084,6 +1108,7 @@ int ew_halo(int W) { return (W + kChunk - 1) / kChunk * kChunk; }
 #define MFA_SCAN_GRID(R) dim3(((R) + kBlockRows - 1) / kBlockRows), dim3(256)
 
 MFA_API void mfa_rolling_set_mode(int mode) { g_roll_mode = mode; }
+MFA_API void mfa_rolling_set_ew_variant(int v) { g_ew_variant = v; }
 
 MFA_API int mfa_beta_hsigma(const float* y, const float* x, const int* seg_lo, int R, int W,
                             double lam, int minp, float* beta, float* hsig, void* s) {

@@ -39,13 +39,17 @@ cases = {
     "rstr": (lambda: _native.call("mfa_rstr", _native.ptr(lr), _native.ptr(seg), R, 21, 483,
                                   0.5 ** (1 / 126), 42, _native.ptr(rstr), _native.stream(dev)), 12),
 }
-variants = [("mode2_r01", 2), ("default", 0)]
+variants = [("mode2_r01", 2, 0), ("default", 0, 0), ("ew_8x512", 0, 1), ("ew_16x256", 0, 2)]
+_native.register("mfa_rolling_set_ew_variant", [__import__("ctypes").c_int])
 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 ref = {}
 for name, (fn, bpr) in cases.items():
     res = {}
-    for vname, mode in variants:
+    for vname, mode, ewv in variants:
+        if ewv and name not in ("beta_hsigma", "dastd"):
+            continue
         lib.mfa_rolling_set_mode(mode)
+        lib.mfa_rolling_set_ew_variant(ewv)
         fn()
         torch.cuda.synchronize()
         out = {"beta_hsigma": (beta, hsig), "dastd": (dast,), "cmra": (cmra,), "rstr": (rstr,)}[name]
@@ -68,3 +72,4 @@ for name, (fn, bpr) in cases.items():
         res[vname] = {"ms": round(ms, 4), "TB_s": round(R * bpr / ms / 1e9, 3), "max_rel_vs_r01": err}
     print(json.dumps({"kernel": name, "N": N, "T": T, **res}), flush=True)
 lib.mfa_rolling_set_mode(0)
+lib.mfa_rolling_set_ew_variant(0)
