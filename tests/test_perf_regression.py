@@ -10,16 +10,19 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-# measured on 1x MI355X (ROCm 7.2), round 3 (profiles/r03_start/, profiles/r02_*):
+# measured on 1x MI355X (ROCm 7.2), round 3 (profiles/r03_risk/perf_guards.log, r03_start/):
 MEASURED = {
-    # bench.py: fp64 storage, refine on, deterministic, graph replay: 0.392 ms / 2520 dates
-    "xs_wls_fp64_reg_per_s": 6.43e6,
-    # RiskModel eigen stage at 2520 dates x M = 100 (profiles/r02_risk_stages_final_fp64.json)
-    "eigen_adjust_2520x100_ms": 20.65,
-    # Newey-West expanding series, T = 2520, K = 42, q = 2 (profiles/r02_nw_bench.jsonl)
-    "newey_west_2520_ms": 0.103,
-    # BETA/HSIGMA anchored-prefix kernel, 5000 x 3780 (profiles/r02_rolling_ab.jsonl)
-    "beta_hsigma_5000x3780_ms": 0.214,
+    # bench.py: fp64 storage, refine on, deterministic, graph replay: 0.388 ms / 2520 dates
+    "xs_wls_fp64_reg_per_s": 6.50e6,
+    # eigen_risk_adjust at 2520 dates x M = 100: tridiagonal eigh of F0 + bias solver mode 5
+    # + finalize (draw covariances given)
+    "eigen_adjust_2520x100_ms": 14.45,
+    # Newey-West expanding series, T = 2520, K = 42, q = 2
+    "newey_west_2520_ms": 0.100,
+    # BETA/HSIGMA anchored-prefix kernel, 5000 x 3780 (Newton-reciprocal finishers)
+    "beta_hsigma_5000x3780_ms": 0.194,
+    # point-in-time trailing specific vol, 2520 x 5000, W = 252 (profiles/r03_risk/)
+    "trailing_vol_2520x5000_ms": 1.075,
 }
 SLACK = 0.8
 
@@ -134,3 +137,17 @@ def test_asof_search_throughput():
     ms = _time_ms(lambda: asof.asof_search(lg, lk, rg, rk, check_sorted=False))
     print(f"asof_search {lg.numel()} x {rg.numel()}: {ms:.3f} ms")
     assert ms < 0.5, f"{ms:.3f} ms"
+
+
+def test_trailing_vol_2520x5000():
+    """The specific-vol window of the attribution stage (bitwise the tensor loop)."""
+    from llm_driven_multi_factor_model_amd.ops import attribution as attr
+    D, N, W = 2520, 5000, 252
+    g = torch.Generator(device="cuda:0").manual_seed(0)
+    e = torch.randn(D, N, device="cuda:0", generator=g, dtype=torch.float64) * 0.02
+    halo = torch.full((W - 1, N), float("nan"), device="cuda:0", dtype=torch.float64)
+    _warm_clocks()
+    ms = _time_ms(lambda: attr.trailing_vol(halo, e, W, 1), reps=5)
+    ceil = MEASURED["trailing_vol_2520x5000_ms"] / SLACK
+    print(f"trailing_vol {D}x{N} W={W}: {ms:.3f} ms (ceiling {ceil:.3f})")
+    assert ms < ceil, f"{ms:.3f} ms"
