@@ -940,14 +940,18 @@ __global__ __launch_bounds__(kVhWaves * 64) void cmra_vhgw_kernel(const float* _
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g0 = blockIdx.x * kVhRows - kVhH;
   // pass 1: this wave's rows (one per lane per block) and its total
+  // (seg_lo of the output rows is loaded here too: pass 3 then waits on no global load)
   float v[kVhBPW];
+  int sl[kVhBPW];
   double tot = 0.0;
 #pragma unroll
   for (int k = 0; k < kVhBPW; ++k) {
     const int g = g0 + (wid * kVhBPW + k) * 64 + lane;
     v[k] = (g >= 0 && g < R) ? lr[g] : qnanf();
-    tot += fin(v[k]) ? (double)v[k] : 0.0;
+    sl[k] = ((wid * kVhBPW + k) * 64 >= kVhH && g < R) ? seg_lo[g] : 0;
   }
+#pragma unroll
+  for (int k = 0; k < kVhBPW; ++k) tot += fin(v[k]) ? (double)v[k] : 0.0;
   tot = wave_sum(tot);
   if (lane == 0) wtot[wid] = tot;
   __syncthreads();
@@ -983,7 +987,7 @@ __global__ __launch_bounds__(kVhWaves * 64) void cmra_vhgw_kernel(const float* _
     const int t = blk * 64 + lane, r = g0 + t;
     if (r >= R) continue;
     float o = qnanf();
-    if (r - W + 1 >= seg_lo[r]) {
+    if (r - W + 1 >= sl[k]) {
       const int at = t - W + 1, ba = at >> 6;  // ba < blk since W > 64
       double mx = fmax(hmax[at], gmax[k]), mn = fmin(hmin[at], gmin[k]);
       bool bad = (nanm[ba] >> (at & 63)) != 0 || (gnan[k] & (lane == 63 ? ~0ull : (2ull << lane) - 1)) != 0;
@@ -1037,11 +1041,23 @@ __global__ __launch_bounds__(kRsWaves * 64) void rstr_ew_kernel(const float* __r
   }
   // lane m holds block row 63 - m: U_block = lam^m * prefix(lam^-m x') + lam^(m+1) * carry
   const unsigned long long below = lane == 63 ? ~0ull : (2ull << lane) - 1;
+  // every load of the workgroup issued up front (the block scans below are a serial chain):
+  // this wave's log returns, lane-reversed per block, and seg_lo of its output rows
+  float vv[kRsBPW];
+  int sl[kRsBPW];
+#pragma unroll
+  for (int k = 0; k < kRsBPW; ++k) {
+    const int g = g0 + (wid * kRsBPW + k) * 64 + 63 - lane;
+    vv[k] = (g >= 0 && g < R) ? lr[g] : qnanf();
+    const int go = g0 + (wid * kRsBPW + k) * 64 + lane;
+    sl[k] = ((wid * kRsBPW + k) * 64 >= kRsH && go < R) ? seg_lo[go] : 0;
+  }
   double cn = 0.0, cd = 0.0;
   int cc = 0;
+#pragma unroll
   for (int k = kRsBPW - 1; k >= 0; --k) {
-    const int t = (wid * kRsBPW + k) * 64 + 63 - lane, g = g0 + t;
-    const float v = (g >= 0 && g < R) ? lr[g] : qnanf();
+    const int t = (wid * kRsBPW + k) * 64 + 63 - lane;
+    const float v = vv[k];
     const bool ok = fin(v);
     const double zn = wave_scan_dpp<0>(ok ? lpn * (double)v : 0.0);
     const double zd = wave_scan_dpp<0>(ok ? lpn : 0.0);
@@ -1074,12 +1090,13 @@ __global__ __launch_bounds__(kRsWaves * 64) void rstr_ew_kernel(const float* __r
     d = fma(f, in_d[w], ud[t]);
     c = cs[t] + in_c[w];
   };
+#pragma unroll
   for (int k = 0; k < kRsBPW; ++k) {
     const int blk = wid * kRsBPW + k;
     if (blk * 64 < kRsH) continue;
     const int t = blk * 64 + lane, r = g0 + t;
     if (r >= R) continue;
-    const int kl = max(seg_lo[r], r - W + 1 - L), kr = r - L;
+    const int kl = max(sl[k], r - W + 1 - L), kr = r - L;
     float o = qnanf();
     if (kr >= kl) {
       const int tl = kl - g0, tr = kr + 1 - g0;
@@ -1089,7 +1106,7 @@ __global__ __launch_bounds__(kRsWaves * 64) void rstr_ew_kernel(const float* __r
       full(tr, nr, dr, cr);
       if (cl - cr >= minp) {
         const double f = pw[tr - tl];
-        o = (float)(fma(-f, nr, nl) / fma(-f, dr, dl));
+        o = (float)(fma(-f, nr, nl) * frcp(fma(-f, dr, dl)));
       }
     }
     out[r] = o;
