@@ -16,8 +16,8 @@ agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob("gpurun_out/pmc_roll/a/**/run_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         kn = r["Kernel_Name"]
-        if "scan_kernel" in kn or "ew_window" in kn:
-            key = kn[kn.find("::") + 2:kn.find("_kernel") + 7] + ("<" + kn.split("::")[2][:8] + ">" if "ew_window" in kn else "")
+        if any(t in kn for t in ("scan_kernel", "ew_window", "vhgw", "rstr_ew")):
+            key = kn.split("(")[0][-70:]
             agg[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in agg.items():
     v = {c: sum(x) / len(x) for c, x in d.items()}
