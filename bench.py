@@ -155,10 +155,13 @@ def main() -> int:
         if use_cuda and not args.no_graph:
             # The kernel of a step is captured once per buffer into a HIP graph and replayed:
             # the same work, without per-launch host overhead.  The RCCL all-gather stays eager.
+            # thread_local capture: the process group's watchdog thread keeps polling the events
+            # of earlier collectives (the barrier before the strong-scaling loop) while this
+            # thread captures, which a global-mode capture forbids.
             torch.cuda.synchronize(dev)
             for b in range(NB):
                 graphs[b] = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(graphs[b]):
+                with torch.cuda.graph(graphs[b], capture_error_mode="thread_local"):
                     regress(b)
         return step, drain, outs
 
