@@ -276,6 +276,7 @@ __device__ __forceinline__ void moments_body(
   const int tid = threadIdx.x, nthr = blockDim.x;
   const int lane = tid & 63, wid = tid >> 6, nw = nthr >> 6;
   constexpr bool DET = (VAR & 32) != 0;
+  constexpr bool PLAIN = (VAR & 64) != 0;
   static_assert(!DET || (R % 4 == 0 && NACC <= 256), "deterministic mode: 4 waves, R/4 replicas each");
   const int rep = DET ? wid * (R / 4) + (lane & (R / 4 - 1)) : (lane & (R - 1));
   const unsigned seg_a = lds_addr(dyn + rep);
@@ -329,6 +330,90 @@ __device__ __forceinline__ void moments_body(
     }
     if (id && lane < kWT / 2 && s0 + 2 * lane < ne) glds4(id + s0 + 2 * lane, slot + (Q + 2) * ROWB);
   };
+  // the per-stock accumulation of one loaded tile (shared by the LDS-DMA ring and the
+  // plain-load paths): s = this lane's stock, okm bits, moments FMAs, segment atomics
+  auto consume = [&](int s, T cf, T rf, int j, const T (&xf)[Q]) {
+      bool ok = (s < ne) && (j >= 0) && (j < Pseg) && finite_v(cf) && (cf >= T(0)) && finite_v(rf);
+  #pragma unroll
+      for (int q = 0; q < Q; ++q) ok = ok && finite_v(xf[q]);
+      if (okm) {  // validity bits of this 64-stock tile for the residual pass (no cap re-read)
+        const unsigned long long m = __ballot(ok);
+        if (lane == 0) aux_store(okm + ((s - lane) >> 6), m);
+      }
+      if (ok) {
+        const double c = cf, r = rf, w = sqrt(c);
+        double x[Q], wx[Q];
+  #pragma unroll
+        for (int q = 0; q < Q; ++q) { x[q] = xf[q]; wx[q] = w * x[q]; }
+        if constexpr ((VAR & 2) != 0) {  // timing-only ablation: skip the moment FMAs
+  #pragma unroll
+          for (int q = 0; q < Q; ++q) asm volatile("" ::"v"(wx[q]));
+        } else {
+  #pragma unroll
+        for (int q = 0; q < Q; ++q)
+  #pragma unroll
+          for (int t = 0; t <= q; ++t) v[q * (q + 1) / 2 + t] = fma(wx[q], x[t], v[q * (q + 1) / 2 + t]);
+        }
+        double sx = 0.0, sxx = 0.0;
+  #pragma unroll
+        for (int q = 0; q < Q; ++q) {
+          v[NG + q] = fma(wx[q], r, v[NG + q]);
+          v[NG + Q + q] = fma(c, x[q], v[NG + Q + q]);
+          sx += x[q];
+          sxx = fma(x[q], x[q], sxx);
+        }
+        v[NG + 2 * Q + 0] += c;
+        v[NG + 2 * Q + 1] += sx;
+        v[NG + 2 * Q + 2] += sxx;
+        v[NG + 2 * Q + 3] += 1.0;
+        if (VAR & 1) {  // timing-only ablation: skip the segment atomics
+          asm volatile("" ::"v"(w), "v"(r));
+        } else {
+          const unsigned a = seg_a + (unsigned)(j * SJ * 8);
+          const double wr = w * r;
+          lds_add_nowait<0>(a, w);
+          [&]<int... I>(std::integer_sequence<int, I...>) {
+            (lds_add_nowait<8 * R * (1 + I)>(a, wx[I]), ...);
+          }(std::make_integer_sequence<int, Q>{});
+          lds_add_nowait<8 * R * (Q + 1)>(a, wr);
+          lds_add_nowait<8 * R * (Q + 2)>(a, c);
+        }
+      }
+  };
+  if constexpr (PLAIN) {
+    // VAR & 64: plain vector loads straight into registers (one stock per lane, each field row
+    // a coalesced 64-lane load), the next tile's loads in flight while this one is consumed --
+    // no LDS-DMA ring (whose per-CU issue path caps a lone workgroup near 25 GB/s)
+    // VAR & 128: two tiles in flight (fp32 panels have the registers for it)
+    constexpr bool DEEP = (VAR & 128) != 0;
+    struct Tile {
+      T c, r, x[Q];
+      int j;
+    };
+    Tile n1{}, n2{};
+    auto ldt = [&](int i, Tile& t) {
+      const int s = nb + (wid + i * nw) * kWT + lane;
+      const bool in = s < ne;
+      t.c = in ? cd[s] : T(0);
+      t.r = in ? rd[s] : T(0);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) t.x[q] = in ? Xd[(size_t)q * N + s] : T(0);
+      t.j = (in && id) ? (int)id[s] : 0;
+    };
+    if (ntile > 0) ldt(0, n1);
+    if (DEEP && ntile > 1) ldt(1, n2);
+    for (int i = 0; i < ntile; ++i) {
+      const int s = nb + (wid + i * nw) * kWT + lane;
+      const Tile cur = n1;
+      if constexpr (DEEP) {
+        n1 = n2;
+        if (i + 2 < ntile) ldt(i + 2, n2);
+      } else {
+        if (i + 1 < ntile) ldt(i + 1, n1);
+      }
+      consume(s, cur.c, cur.r, cur.j, cur.x);
+    }
+  } else {
   for (int i = 0; i < NB - 1 && i < ntile; ++i) issue(i);
   for (int i = 0; i < ntile; ++i) {
     // The slot of tile i - 1 is free (its reads completed last iteration): refill it with tile
@@ -356,52 +441,8 @@ __device__ __forceinline__ void moments_body(
     [&]<int... I>(std::integer_sequence<int, I...>) {
       (reg_fence(xf[I]), ...);
     }(std::make_integer_sequence<int, Q>{});
-    bool ok = (s < ne) && (j >= 0) && (j < Pseg) && finite_v(cf) && (cf >= T(0)) && finite_v(rf);
-#pragma unroll
-    for (int q = 0; q < Q; ++q) ok = ok && finite_v(xf[q]);
-    if (okm) {  // validity bits of this 64-stock tile for the residual pass (no cap re-read)
-      const unsigned long long m = __ballot(ok);
-      if (lane == 0) aux_store(okm + ((s - lane) >> 6), m);
-    }
-    if (ok) {
-      const double c = cf, r = rf, w = sqrt(c);
-      double x[Q], wx[Q];
-#pragma unroll
-      for (int q = 0; q < Q; ++q) { x[q] = xf[q]; wx[q] = w * x[q]; }
-      if constexpr ((VAR & 2) != 0) {  // timing-only ablation: skip the moment FMAs
-#pragma unroll
-        for (int q = 0; q < Q; ++q) asm volatile("" ::"v"(wx[q]));
-      } else {
-#pragma unroll
-      for (int q = 0; q < Q; ++q)
-#pragma unroll
-        for (int t = 0; t <= q; ++t) v[q * (q + 1) / 2 + t] = fma(wx[q], x[t], v[q * (q + 1) / 2 + t]);
-      }
-      double sx = 0.0, sxx = 0.0;
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        v[NG + q] = fma(wx[q], r, v[NG + q]);
-        v[NG + Q + q] = fma(c, x[q], v[NG + Q + q]);
-        sx += x[q];
-        sxx = fma(x[q], x[q], sxx);
-      }
-      v[NG + 2 * Q + 0] += c;
-      v[NG + 2 * Q + 1] += sx;
-      v[NG + 2 * Q + 2] += sxx;
-      v[NG + 2 * Q + 3] += 1.0;
-      if (VAR & 1) {  // timing-only ablation: skip the segment atomics
-        asm volatile("" ::"v"(w), "v"(r));
-      } else {
-        const unsigned a = seg_a + (unsigned)(j * SJ * 8);
-        const double wr = w * r;
-        lds_add_nowait<0>(a, w);
-        [&]<int... I>(std::integer_sequence<int, I...>) {
-          (lds_add_nowait<8 * R * (1 + I)>(a, wx[I]), ...);
-        }(std::make_integer_sequence<int, Q>{});
-        lds_add_nowait<8 * R * (Q + 1)>(a, wr);
-        lds_add_nowait<8 * R * (Q + 2)>(a, c);
-      }
-    }
+    consume(s, cf, rf, j, xf);
+  }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1451,7 +1492,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Q <= 10 ? 2
   // device pseudo-inverse pass reads them for near-singular dates.  (Exporting only flagged
   // dates from LDS after the solve cost ~30 us per 2520-date step: the extra LDS read of the
   // DMA ring region made hipcc add conservative vmcnt drains.)
-  moments_body<Q, VAR & 35, R, T>(X, cap, ret, ind, N, Pseg, d, ring, dyn, sm, 0, -1,
+  moments_body<Q, VAR & 227, R, T>(X, cap, ret, ind, N, Pseg, d, ring, dyn, sm, 0, -1,
                                   mom_out ? mom_out + (size_t)d * Layout<Q, T>::msize(Pseg)
                                           : nullptr,
                                   okd);
@@ -2287,6 +2328,17 @@ int pipe_grid(K kern, size_t lds, int D, int C) {
   return G < kPipeGroups ? kPipeGroups : G;
 }
 
+// Moments source of the fused kernel: plain vector loads straight into registers, or the
+// LDS-DMA ring.  Measured (tools/xs_mode_time.py, profiles/r03_xs_plain_loads.jsonl): plain loads
+// win for fp32 panels at every D (2520 dates: 298 -> 273 us) and for fp64 shards up to ~2
+// dates per CU (315: 72 -> 66 us; a lone workgroup's LDS-DMA issue path caps near 25 GB/s per
+// CU), the ring for larger fp64 steps (2520: 386 vs 395 us).  Bitwise-identical results.
+constexpr int kXsPlainMaxD64 = 512;
+template <typename T>
+inline bool xs_plain_moments(int D) {
+  return sizeof(T) == 4 || D <= kXsPlainMaxD64;
+}
+
 template <int Q, int VAR, typename T>
 hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, int D, int N,
                     int P, int pivot_mode, double tol, double* f, T* e, double* r2, double* stats,
@@ -2370,8 +2422,21 @@ hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, 
         hipLaunchKernelGGL((xs_fused_mf_kernel<Q, 2, VAR, T, 4>), dim3(D), dim3(256), ldsm, s, X,
                            cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom);
     }
+  } else if ((mode == 20 || mode == 21 || (mode == 0 && xs_plain_moments<T>(D))) && det) {
+    // moments from plain vector loads (default for fp32 panels and small fp64 shards)
+    if (mode == 21)  // two tiles in flight
+      hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR | 32 | 64 | 128, PRE, T>), dim3(D),
+                         dim3(256), lds1, s, X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2,
+                         stats, status, mom, okm);
+    else
+      hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR | 32 | 64, PRE, T>), dim3(D),
+                         dim3(256), lds1, s, X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2,
+                         stats, status, mom, okm);
   } else if (det) {  // bitwise-reproducible variant of the default path
     hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR | 32, PRE, T>), dim3(D), dim3(256), lds1,
+                       s, X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom, okm);
+  } else if (mode == 0 && rep8 && xs_plain_moments<T>(D)) {
+    hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR | 64, PRE, T>), dim3(D), dim3(256), lds1,
                        s, X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom, okm);
   } else if (mode == 0 && rep8) {
     hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR, PRE, T>), dim3(D), dim3(256), lds1, s, X,

@@ -15,3 +15,5 @@ timeout -k 10 300 python __graft_entry__.py smoke > $O/smoke.log 2>&1 && tail -1
  && for d in 315 630 1260; do timeout -k 10 120 python bench.py --steps 30 --warmup 5 --dates $d > $O/bench_fp64_d$d.log 2>&1 && tail -1 $O/bench_fp64_d$d.log || exit 1; done \
  && timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $O/prof -o run --output-format csv -- python3 bench.py --steps 10 --warmup 2 --prewarm 20 > $O/prof.log 2>&1 \
  && find $O/prof -name '*kernel_stats.csv' | head -1 | xargs head -6 | cut -c1-160
+echo "== 2-rank gloo rehearsal (two ranks share the GPU)" \
+ && MFA_BENCH_BACKEND=gloo timeout -k 10 240 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 --prewarm 5 > $O/bench_gloo2.log 2>&1 && tail -1 $O/bench_gloo2.log
