@@ -1092,7 +1092,13 @@ __device__ __forceinline__ int tri2_row_off(int s) {
 // U[:, k] = eigenvector k; flag[b] = 1 when the twisted-factorisation eigenvectors of a
 // clustered spectrum are not orthogonal to 1e-12 (the caller re-solves those matrices with the
 // Jacobi), 0 otherwise.  Non-finite matrices give NaN.
-template <int KP, bool PF = false, int ABL = 0, int WPE = MFA_TRI2_WPE, bool EIG = false>
+// ACC: a Laguerre step of relative size <= 10^-ACC (and shrinking, same Sturm count) is the
+// last one; cubic convergence leaves far less than fp64 resolution after it.  A/B on the
+// pipeline's inputs (profiles/r03_risk/bias_laguerre_stop_ab.jsonl): 1e-9 13.26 ms, 1e-8
+// 12.40 ms (bias ratios within 3e-14 of the Jacobi, 1.9e-14 of LAPACK), 1e-7 11.65 ms but
+// 1.4e-11 off: 1e-8 is the default; modes 8 / 9 select 1e-9 / 1e-7.
+template <int KP, bool PF = false, int ABL = 0, int WPE = MFA_TRI2_WPE, bool EIG = false,
+          int ACC = 8>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void
 mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* __restrict__ Cz,
                     const int* __restrict__ dvalid, double* __restrict__ vout,
@@ -1179,9 +1185,12 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
       const double alpha = readlane(xs, s);
       double u = 0.0, tau = 0.0, beta = x0;
       if (sig != 0.0) {
-        const double nrm = sqrt(fma(x0, x0, sig));
+        // v_rsq / v_rcp seeds + two Newton steps (~1 ulp) instead of the IEEE sequences: they
+        // sit on the per-step critical path of every problem
+        const double n2 = fma(x0, x0, sig);
+        const double nrm = n2 * rsq_nr(n2);
         beta = x0 >= 0.0 ? -nrm : nrm;
-        tau = 1.0 / (nrm * (nrm + fabs(x0)));
+        tau = rcp_nr(nrm * (nrm + fabs(x0)));
         u = act ? (lane == s + 1 ? x0 - beta : x) : 0.0;
       }
       double* us = R + tri2_row_off<KP>(s) - J0;  // us[j], j in [J0, KP)
@@ -1269,6 +1278,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
     if (cl <= jt) lo = fmax(lo, xl); else hi = fmin(hi, xl);
   }
   double lam = x;
+  constexpr double kAccTol = ACC == 9 ? 1e-9 : (ACC == 8 ? 1e-8 : (ACC == 7 ? 1e-7 : 1e-5));
   if (lane < K && (ABL & 1) == 0) {
     int prev = -1;
     double sprev = __builtin_inf();
@@ -1283,7 +1293,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
           st *= 8.0;
         }
         lag = __builtin_isfinite(xn) && xn >= lo && xn <= hi;
-        if (lag && prev == cnt && st <= 1e-9 * fabs(x) && st <= 0.25 * sprev) { x = xn; break; }
+        if (lag && prev == cnt && st <= kAccTol * fabs(x) && st <= 0.25 * sprev) { x = xn; break; }
         sprev = lag ? st : __builtin_inf();
       }
       if (!lag) { xn = 0.5 * (lo + hi); sprev = __builtin_inf(); }
@@ -1702,6 +1712,15 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
 #undef MFA_TRI2
     return false;
   }
+  if ((g_bias_mode == 8 || g_bias_mode == 9) && K <= 44) {  // A/B: Laguerre stop at 1e-9 / 1e-7
+    if (g_bias_mode == 8)
+      hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 9>), dim3(D * M),
+                         dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr);
+    else
+      hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 7>), dim3(D * M),
+                         dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr);
+    return true;
+  }
   if ((g_bias_mode == 6 || g_bias_mode == 7) && K <= 44) {  // A/B: mode 5 at 4 / 5 waves per SIMD
     if (g_bias_mode == 6)
       hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, 4>), dim3(D * M), dim3(64),
@@ -1752,7 +1771,7 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
 
 #define MFA_BIAS_LAUNCH(NBV_)                                                                   \
   {                                                                                            \
-    if ((g_bias_mode >= 3 && g_bias_mode <= 7) || (g_bias_mode > 40 && g_bias_mode < 68))      \
+    if ((g_bias_mode >= 3 && g_bias_mode <= 9) || (g_bias_mode > 40 && g_bias_mode < 68))      \
       launch_bias_tri(D0, D, K, M, Cz, dvalid, ws, s);                                         \
     else if (g_bias_mode == 1)                                                                 \
       hipLaunchKernelGGL((mc_bias_split_kernel<NBV_, 1, double>), dim3(D * M), dim3(64),       \
