@@ -1317,7 +1317,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
     for (int i = 0; i < KP; ++i) {  // forward pivots -> y
       if (i < K) {
         const double2 t = tb[i];
-        dp = guard_pivot(i == 0 ? t.x - lam : (t.x - lam) - t.y * rcp_nr(dp), pivmin);
+        dp = guard_pivot(i == 0 ? t.x - lam : (t.x - lam) - t.y * rcp_nr1(dp), pivmin);
       }
       y[i] = i < K ? dp : 0.0;
     }
@@ -1327,7 +1327,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
     for (int i = KP - 1; i >= 0; --i) {  // backward pivots on the fly: the twist index r
       if (i < K) {
         const double ai = tb[i].x - lam;
-        dm = guard_pivot(i == K - 1 ? ai : ai - tb[i + 1].y * rcp_nr(dm), pivmin);
+        dm = guard_pivot(i == K - 1 ? ai : ai - tb[i + 1].y * rcp_nr1(dm), pivmin);
         const double g = fabs(y[i] + dm - ai);
         if (i == K - 1 || g < gmin) { gmin = g; r = i; }
       }
@@ -1336,7 +1336,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
 #pragma unroll
     for (int i = KP - 1; i >= 0; --i) {  // below the twist: y_i = -beta_i y_{i+1} / P_i
       if (i < r) {
-        cz = -be[i] * cz * rcp_nr(y[i]);
+        cz = -be[i] * cz * rcp_nr1(y[i]);
         nrm = fma(cz, cz, nrm);
         y[i] = cz;
       }
@@ -1346,7 +1346,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
     for (int i = KP - 1; i >= 0; --i) {  // above the twist: recompute Q_i into y_i
       if (i < K && i > r) {
         const double ai = tb[i].x - lam;
-        dm = guard_pivot(i == K - 1 ? ai : ai - tb[i + 1].y * rcp_nr(dm), pivmin);
+        dm = guard_pivot(i == K - 1 ? ai : ai - tb[i + 1].y * rcp_nr1(dm), pivmin);
         y[i] = dm;
       }
     }
@@ -1355,7 +1355,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
     for (int i = 0; i < KP; ++i) {
       if (i == r) y[i] = 1.0;
       if (i > r && i < K) {
-        cz = -be[i - 1] * cz * rcp_nr(y[i]);
+        cz = -be[i - 1] * cz * rcp_nr1(y[i]);
         nrm = fma(cz, cz, nrm);
         y[i] = cz;
       }
@@ -1400,8 +1400,11 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
   }(std::make_integer_sequence<int, (KP + 7) / 8>{});
   if constexpr (EIG) {
     // w (descending by lane rank), U[:, k] = y of lane k, and the orthogonality check of the
-    // eigenvectors through the rows of Y in LDS (after the tables, which are still live here)
-    double* Ys = gs + 64;
+    // eigenvectors through the rows of Y in LDS, over the reflector rows and tables (all dead
+    // now; one wave's DS instructions execute in order): 14.8 KB per workgroup at K = 42 instead
+    // of 27 KB keeps ~2.5 waves per SIMD resident (0.93 -> ~0.2 ms for 2520 matrices)
+    double* Ys = sm;
+    lds_order();
     double* Ub = Uout + (size_t)d * K * K;
     if (lane < K) {
       vo[lane] = lam;
@@ -1443,7 +1446,10 @@ size_t bias_tri2_lds(int K, int KP) {
   for (int s = 0; s + 2 < K; ++s) n += KP - 8 * (s / 8);
   return ((size_t)((n + 1) & ~1) + 64 + 128 + 4 * 64) * sizeof(double);
 }
-size_t eigh_tri2_lds(int K, int KP) { return bias_tri2_lds(K, KP) + (size_t)K * KP * sizeof(double); }
+size_t eigh_tri2_lds(int K, int KP) {
+  const size_t b = bias_tri2_lds(K, KP), y = (size_t)K * KP * sizeof(double);
+  return b > y ? b : y;
+}
 
 // ---------------- pair-block Jacobi WITH eigenvectors (batched eigh of F0) ----------------
 // Same tournament-position scheme as jacobi_pairs, carrying packed A and the full eigenvector
