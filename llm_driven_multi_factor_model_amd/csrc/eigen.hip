@@ -1098,7 +1098,7 @@ __device__ __forceinline__ int tri2_row_off(int s) {
 // 12.40 ms (bias ratios within 3e-14 of the Jacobi, 1.9e-14 of LAPACK), 1e-7 11.65 ms but
 // 1.4e-11 off: 1e-8 is the default; modes 8 / 9 select 1e-9 / 1e-7.
 template <int KP, bool PF = false, int ABL = 0, int WPE = MFA_TRI2_WPE, bool EIG = false,
-          int ACC = 8>
+          int ACC = 8, int LB = 8>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void
 mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* __restrict__ Cz,
                     const int* __restrict__ dvalid, double* __restrict__ vout,
@@ -1212,7 +1212,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
         const double2 uu = *(const double2*)(us + j);
         p0 = fma(a[j], uu.x, p0);
         p1 = fma(a[j + 1], uu.y, p1);
-        if (((j - J0) & 7) == 6) lds_batch();
+        if (((j - J0) & (LB - 1)) == LB - 2) lds_batch();
       }
       const double p = act ? tau * (p0 + p1) : 0.0;
       const double kk = 0.5 * tau * wave_total(u * p);
@@ -1224,7 +1224,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
         const double2 ww = *(const double2*)(wb + j), uu = *(const double2*)(us + j);
         a[j] -= fma(u, ww.x, w * uu.x);
         a[j + 1] -= fma(u, ww.y, w * uu.y);
-        if (((j - J0) & 7) == 6) lds_batch();
+        if (((j - J0) & (LB - 1)) == LB - 2) lds_batch();
       }
       lds_order();
     }
@@ -1382,7 +1382,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
         const double2 uu = *(const double2*)(us + j);
         t0 = fma(uu.x, y[j], t0);
         t1 = fma(uu.y, y[j + 1], t1);
-        if (((j - J0) & 7) == 6) lds_batch();
+        if (((j - J0) & (LB - 1)) == LB - 2) lds_batch();
       }
       const double f = tau * (t0 + t1);
 #pragma unroll
@@ -1390,7 +1390,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
         const double2 uu = *(const double2*)(us + j);
         y[j] = fma(-f, uu.x, y[j]);
         y[j + 1] = fma(-f, uu.y, y[j + 1]);
-        if (((j - J0) & 7) == 6) lds_batch();
+        if (((j - J0) & (LB - 1)) == LB - 2) lds_batch();
       }
     }
   };
@@ -1718,6 +1718,11 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
 #undef MFA_TRI2
     return false;
   }
+  if (g_bias_mode == 10 && K <= 44) {  // A/B: LDS broadcast reads fenced in batches of 8 x 16 B
+    hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 16>), dim3(D * M),
+                       dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr);
+    return true;
+  }
   if ((g_bias_mode == 8 || g_bias_mode == 9) && K <= 44) {  // A/B: Laguerre stop at 1e-9 / 1e-7
     if (g_bias_mode == 8)
       hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 9>), dim3(D * M),
@@ -1777,7 +1782,7 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
 
 #define MFA_BIAS_LAUNCH(NBV_)                                                                   \
   {                                                                                            \
-    if ((g_bias_mode >= 3 && g_bias_mode <= 9) || (g_bias_mode > 40 && g_bias_mode < 68))      \
+    if ((g_bias_mode >= 3 && g_bias_mode <= 10) || (g_bias_mode > 40 && g_bias_mode < 68))     \
       launch_bias_tri(D0, D, K, M, Cz, dvalid, ws, s);                                         \
     else if (g_bias_mode == 1)                                                                 \
       hipLaunchKernelGGL((mc_bias_split_kernel<NBV_, 1, double>), dim3(D * M), dim3(64),       \
