@@ -418,3 +418,28 @@ def test_mfma_moments_ablation_matches_default(cuda):
                 lib.mfa_xs_set_mode(0)
             torch.testing.assert_close(o.f, base.f, rtol=1e-12, atol=1e-15)
             torch.testing.assert_close(o.r2, base.r2, rtol=1e-12, atol=1e-14)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_plain_load_and_lds_dma_moments_are_bitwise_equal(cuda, dtype):
+    """The fused kernel's two moment sources -- plain vector loads (default for fp32 panels and
+    fp64 shards up to 512 dates) and the LDS-DMA ring (larger fp64 steps) -- feed the same
+    per-wave accumulation in the same order: bitwise-identical f, R^2 and specific returns."""
+    import ctypes as C
+    from llm_driven_multi_factor_model_amd import _native
+    _native.register("mfa_xs_set_mode", [C.c_int])
+    panel = synthetic_panel(37, 5000, 31, 10, seed=77, missing_frac=0.02, empty_industries=1,
+                            dtype=dtype).to(cuda)
+    lib = _native.lib()
+    outs = {}
+    try:
+        for mode in (20, 7):  # 20 = plain loads, 7 = LDS-DMA ring (both deterministic)
+            lib.mfa_xs_set_mode(mode)
+            outs[mode] = X.xs_wls(panel.styles, panel.cap, panel.ret, panel.ind, 31)
+        torch.cuda.synchronize()
+    finally:
+        lib.mfa_xs_set_mode(0)
+    a, b = outs[20], outs[7]
+    assert torch.equal(a.f, b.f) and torch.equal(a.r2, b.r2)
+    assert torch.equal(a.resid.nan_to_num(7.0), b.resid.nan_to_num(7.0))
