@@ -1222,8 +1222,10 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
 #pragma unroll
       for (int j = J0; j < KP; j += 2) {
         const double2 ww = *(const double2*)(wb + j), uu = *(const double2*)(us + j);
-        a[j] -= fma(u, ww.x, w * uu.x);
-        a[j + 1] -= fma(u, ww.y, w * uu.y);
+        // two fmas per element (the rank-2 update a - u w^T - w u^T): fma(u, w, w * u) then
+        // a subtraction cost three VALU ops, and the kernel is VALU-issue bound
+        a[j] = fma(-u, ww.x, fma(-w, uu.x, a[j]));
+        a[j + 1] = fma(-u, ww.y, fma(-w, uu.y, a[j + 1]));
         if (((j - J0) & (LB - 1)) == LB - 2) lds_batch();
       }
       lds_order();
