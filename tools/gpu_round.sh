@@ -18,3 +18,7 @@ timeout -k 10 300 python __graft_entry__.py smoke > $O/smoke.log 2>&1 && tail -1
 echo "== 2-rank gloo rehearsal (two ranks share the GPU)" \
  && MFA_BENCH_BACKEND=gloo timeout -k 10 240 python -m torch.distributed.run --nnodes 1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 10 --warmup 2 --prewarm 5 > $O/bench_gloo2.log 2>&1 && tail -1 $O/bench_gloo2.log
 bash tools/prof_kernels.sh risk_run python3 tools/risk_stages.py --reps 1 > /dev/null 2>&1 && cp gpurun_out/risk_run_stats.txt $O/risk_run_kernel_stats.txt && head -8 $O/risk_run_kernel_stats.txt
+echo "== stage timings / BASELINE configs / end-to-end job" \
+ && timeout -k 10 300 python tools/risk_stages.py > $O/risk_stages.log 2>&1 && tail -2 $O/risk_stages.log \
+ && timeout -k 10 400 python tools/baseline_configs.py > $O/baseline_configs.log 2>&1 && tail -6 $O/baseline_configs.log \
+ && timeout -k 10 300 python tools/pipeline_e2e.py > $O/pipeline_e2e.log 2>&1 && tail -2 $O/pipeline_e2e.log
