@@ -31,8 +31,10 @@
 #include <utility>
 
 // CS-WLS execution mode shared by the fp32 and fp64 translation units (mfa_xs_set_mode):
-// 0 = fused single kernel (fp32: with the residual prefetch during the solve), 1 = three
-// separate kernels (ablation / large-P fallback), 7 = fused without the prefetch.
+// 0 = fused single kernel (with the residual prefetch during the solve: fp32 panels, and fp64
+// panels on the LDS-DMA moments path), 1 = three separate kernels (ablation / large-P
+// fallback), 7 = fused without the prefetch, 23 / 24 = prefetch forced on the plain-load /
+// LDS-DMA path (A/B).
 extern int g_mfa_xs_mode;
 // Stock chunks per date: 0 = automatic (chunked below kXsChunkMinD dates), > 0 forced, < 0 never.
 extern int g_mfa_xs_chunks;
@@ -880,42 +882,7 @@ __global__ __launch_bounds__(64) void xs_solve_kernel(const double* __restrict__
 
 // ------------------------------------------------------------------------------------------
 // K3: specific returns and R^2.
-// Residual-pass data of the last stocks, loaded by waves 1..3 while wave 0 solves (fused fp32
-// kernel, PRE): the pass then starts with 1536 stocks already in registers.
 // ------------------------------------------------------------------------------------------
-#ifndef MFA_XS_PREU
-#define MFA_XS_PREU 2
-#endif
-constexpr int kPreU = MFA_XS_PREU;
-constexpr int kPreStocks = 3 * 64 * 4 * kPreU;
-template <int Q>
-struct ResidPre {
-  float4 c4[kPreU], r4[kPreU], x4[kPreU][Q];
-  uint2 j4[kPreU];
-};
-
-template <int Q>
-__device__ __forceinline__ void resid_prefetch(const float* __restrict__ X,
-                                               const float* __restrict__ cap,
-                                               const float* __restrict__ ret,
-                                               const int16_t* __restrict__ ind, int d, int N,
-                                               ResidPre<Q>& pr) {
-  const int nlo = N > kPreStocks ? N - kPreStocks : 0;
-  const int t = threadIdx.x - 64;  // waves 1..3
-  const float* Xd = X + (size_t)d * Q * N;
-#pragma unroll
-  for (int u = 0; u < kPreU; ++u) {
-    const int n = nlo + t * 4 + u * 768;
-    if (n < N) {
-      pr.c4[u] = *(const float4*)(cap + (size_t)d * N + n);
-      pr.r4[u] = *(const float4*)(ret + (size_t)d * N + n);
-#pragma unroll
-      for (int q = 0; q < Q; ++q) pr.x4[u][q] = *(const float4*)(Xd + (size_t)q * N + n);
-      pr.j4[u] = ind ? *(const uint2*)(ind + (size_t)d * N + n) : make_uint2(0u, 0u);
-    }
-  }
-}
-
 // Residual-pass vector types: HIP's float4 / double2 (16-byte rows) and packed int16 ids.
 // (With clang ext_vector types instead, hipcc scheduled a full vmcnt(0) drain at the top of
 // every residual iteration: +30 us on the fp32 step.)
@@ -982,19 +949,56 @@ template <> struct RVec<double> {
   static __device__ __forceinline__ ivec izero() { return 0u; }
 };
 
+// Residual-pass data of the last stocks, loaded by waves 1..3 while wave 0 solves (fused kernel,
+// PRE): the pass then starts with 3 x 64 x VEC x kPreU stocks already in registers (1536 fp32 /
+// 768 fp64 stocks).  The cap row is not loaded when the moments pass left validity bits (okm).
+#ifndef MFA_XS_PREU
+#define MFA_XS_PREU 2
+#endif
+constexpr int kPreU = MFA_XS_PREU;
+template <typename T>
+constexpr int pre_stocks() { return 3 * 64 * Stream<T>::VEC * kPreU; }
+template <int Q, typename T>
+struct ResidPre {
+  typename RVec<T>::vec c4[kPreU], r4[kPreU], x4[kPreU][Q];
+  typename RVec<T>::ivec j4[kPreU];
+};
+
+template <int Q, typename T>
+__device__ __forceinline__ void resid_prefetch(const T* __restrict__ X, const T* __restrict__ cap,
+                                               const T* __restrict__ ret,
+                                               const int16_t* __restrict__ ind, int d, int N,
+                                               bool need_cap, ResidPre<Q, T>& pr) {
+  using RV = RVec<T>;
+  constexpr int V = Stream<T>::VEC;
+  const int nlo = N > pre_stocks<T>() ? N - pre_stocks<T>() : 0;
+  const int t = threadIdx.x - 64;  // waves 1..3
+  const T* Xd = X + (size_t)d * Q * N;
+#pragma unroll
+  for (int u = 0; u < kPreU; ++u) {
+    const int n = nlo + t * V + u * 192 * V;
+    if (n < N) {
+      if (need_cap) pr.c4[u] = RV::load(cap + (size_t)d * N + n);
+      pr.r4[u] = RV::load(ret + (size_t)d * N + n);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) pr.x4[u][q] = RV::load(Xd + (size_t)q * N + n);
+      pr.j4[u] = ind ? *(const typename RV::ivec*)(ind + (size_t)d * N + n) : RV::izero();
+    }
+  }
+}
+
 // Specific returns + R^2 of date d from the coefficients `cf_s` [Q+1+P] (LDS) by the whole
 // workgroup (<= 16 waves); `red` = 16 x 5 doubles of LDS.
-// PRE (fp32 only): waves 1..3 hold the last kPreStocks stocks in `pre` (resid_prefetch) and the
-// main loop covers [0, N - kPreStocks) only.
+// PRE: waves 1..3 hold the last pre_stocks<T>() stocks in `pre` (resid_prefetch) and the main
+// loop covers [0, N - pre_stocks<T>()) only.
 // sums_out != nullptr: stock-sharded regression: write the 5 R^2 sums instead of R^2.
 template <int Q, typename T, bool PRE = false, int UU = 0>
 __device__ __forceinline__ void resid_body(
     const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
     const int16_t* __restrict__ ind, int d, int N, int P, const double* cf_s, bool bad,
     T* __restrict__ eout, double* __restrict__ r2out, double (*red)[5],
-    const ResidPre<Q>& pre = ResidPre<Q>{}, double* __restrict__ sums_out = nullptr, int nb = 0,
+    const ResidPre<Q, T>& pre = ResidPre<Q, T>{}, double* __restrict__ sums_out = nullptr, int nb = 0,
     int ne = -1, const unsigned long long* __restrict__ okm = nullptr) {
-  static_assert(!PRE || sizeof(T) == 4, "residual prefetch is the fp32 path");
   if (ne < 0) ne = N;
   constexpr int V = Stream<T>::VEC, U = UU > 0 ? UU : Stream<T>::U;
   using RV = RVec<T>;
@@ -1065,12 +1069,12 @@ __device__ __forceinline__ void resid_body(
   };
   int Nmain = ne;
   if constexpr (PRE) {
-    const int nlo = N > kPreStocks ? N - kPreStocks : 0;
+    const int nlo = N > pre_stocks<T>() ? N - pre_stocks<T>() : 0;
     Nmain = nlo;
     if (tid >= 64) {
 #pragma unroll
       for (int u = 0; u < kPreU; ++u) {
-        const int n = nlo + (tid - 64) * 4 + u * 768;
+        const int n = nlo + (tid - 64) * V + u * 192 * V;
         if (n < N) {
           const vec eo = compute(pre.c4[u], pre.r4[u], pre.x4[u], pre.j4[u], okbits(n));
           if (ed) RV::store(ed + n, eo);
@@ -1157,7 +1161,7 @@ __global__ __launch_bounds__(256) void xs_resid_kernel(
   for (int i = threadIdx.x; i < Q + 1 + P; i += blockDim.x) cf_s[i] = co[i];
   __syncthreads();
   resid_body<Q, T>(X, cap, ret, ind, d, N, P, cf_s, (status[d] & XS_BAD) != 0, eout, r2out, red,
-                   ResidPre<Q>{}, sums_out ? sums_out + (size_t)b * 5 : nullptr, nb, ne);
+                   ResidPre<Q, T>{}, sums_out ? sums_out + (size_t)b * 5 : nullptr, nb, ne);
 }
 
 // R^2 of every date from its S chunk sums [sum e, sum e^2, sum r, sum r^2, n], in chunk order.
@@ -1502,10 +1506,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Q <= 10 ? 2
   } else if (threadIdx.x < 64) {
     solve_body<Q>(sm, d, P, Pseg, pivot_mode, tol, fout, cf_s, stats, status, &st_s);
   }
-  ResidPre<Q> pre;
+  ResidPre<Q, T> pre;
   if constexpr (PRE) {
     if (__builtin_amdgcn_readfirstlane(threadIdx.x >> 6) != 0)
-      resid_prefetch<Q>(X, cap, ret, ind, d, N, pre);
+      resid_prefetch<Q, T>(X, cap, ret, ind, d, N, okd == nullptr, pre);
   }
   __syncthreads();
   if constexpr ((VAR & 4) == 0)
@@ -1668,7 +1672,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Q <= 10 ? 2
       for (int i = tid; i < KC; i += blockDim.x) cf_s[i] = ld_sc1(co2 + i);
       __syncthreads();
       const bool bad = (st2 & (XS_BAD | XS_COOP_TIMEOUT)) != 0;
-      resid_body<Q, T>(X, cap, ret, ind, d2, N, P, cf_s, bad, eout, nullptr, red, ResidPre<Q>{}, rs,
+      resid_body<Q, T>(X, cap, ret, ind, d2, N, P, cf_s, bad, eout, nullptr, red, ResidPre<Q, T>{}, rs,
                        nb2, ne2, okm + (size_t)d2 * NT);
       // R^2: the last member of the team to finish combines the C chunk sums in chunk order
       if (tid < 64) {
@@ -2422,6 +2426,16 @@ hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, 
         hipLaunchKernelGGL((xs_fused_mf_kernel<Q, 2, VAR, T, 4>), dim3(D), dim3(256), ldsm, s, X,
                            cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom);
     }
+  } else if ((mode == 23 || mode == 24) && det) {
+    // A/B: residual prefetch during the solve on every storage type (plain-load / LDS-DMA moments)
+    if (mode == 23)
+      hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR | 32 | 64, true, T>), dim3(D), dim3(256),
+                         lds1, s, X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status,
+                         mom, okm);
+    else
+      hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR | 32, true, T>), dim3(D), dim3(256),
+                         lds1, s, X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status,
+                         mom, okm);
   } else if ((mode == 20 || mode == 21 || (mode == 0 && xs_plain_moments<T>(D))) && det) {
     // moments from plain vector loads (default for fp32 panels and small fp64 shards)
     if (mode == 21)  // two tiles in flight
@@ -2433,7 +2447,9 @@ hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, 
                          dim3(256), lds1, s, X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2,
                          stats, status, mom, okm);
   } else if (det) {  // bitwise-reproducible variant of the default path
-    hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR | 32, PRE, T>), dim3(D), dim3(256), lds1,
+    // residual prefetch during the solve on every storage type here (fp64 panels, D > 512:
+    // 2520 dates 382 -> 370 us, profiles/r03_xs_pre64_ab.jsonl; no gain on the plain-load path)
+    hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR | 32, true, T>), dim3(D), dim3(256), lds1,
                        s, X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status, mom, okm);
   } else if (mode == 0 && rep8 && xs_plain_moments<T>(D)) {
     hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR | 64, PRE, T>), dim3(D), dim3(256), lds1,

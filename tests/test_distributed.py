@@ -94,7 +94,11 @@ def _hang_worker(rank, world, port, out_path):
     from llm_driven_multi_factor_model_amd.parallel import dist as pdist
     ctx = pdist.init_distributed(device="cpu")
     if ctx.rank == 1:      # a rank that stops participating (hung / dead)
-        time.sleep(8)
+        # stay alive (connections open) until rank 0 has reported, so rank 0 sees the timeout
+        # rather than a closed peer even on a loaded machine
+        t_end = time.time() + 30
+        while not os.path.exists(out_path) and time.time() < t_end:
+            time.sleep(0.2)
         return
     t0 = time.time()
     try:

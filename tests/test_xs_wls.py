@@ -425,7 +425,10 @@ def test_mfma_moments_ablation_matches_default(cuda):
 def test_plain_load_and_lds_dma_moments_are_bitwise_equal(cuda, dtype):
     """The fused kernel's two moment sources -- plain vector loads (default for fp32 panels and
     fp64 shards up to 512 dates) and the LDS-DMA ring (larger fp64 steps) -- feed the same
-    per-wave accumulation in the same order: bitwise-identical f, R^2 and specific returns."""
+    per-wave accumulation in the same order: bitwise-identical f, R^2 and specific returns when
+    both run the residual pass with the prefetch during the solve (modes 23 / 7).  The fp64
+    plain-load default (mode 20) runs the residual pass without it: same f and specific returns,
+    R^2 summed in another stock order."""
     import ctypes as C
     from llm_driven_multi_factor_model_amd import _native
     _native.register("mfa_xs_set_mode", [C.c_int])
@@ -434,12 +437,15 @@ def test_plain_load_and_lds_dma_moments_are_bitwise_equal(cuda, dtype):
     lib = _native.lib()
     outs = {}
     try:
-        for mode in (20, 7):  # 20 = plain loads, 7 = LDS-DMA ring (both deterministic)
+        # 23 = plain loads + prefetch, 7 = LDS-DMA ring (+ prefetch), 20 = plain-load default
+        for mode in (23, 7, 20):
             lib.mfa_xs_set_mode(mode)
             outs[mode] = X.xs_wls(panel.styles, panel.cap, panel.ret, panel.ind, 31)
         torch.cuda.synchronize()
     finally:
         lib.mfa_xs_set_mode(0)
-    a, b = outs[20], outs[7]
+    a, b, c = outs[23], outs[7], outs[20]
     assert torch.equal(a.f, b.f) and torch.equal(a.r2, b.r2)
     assert torch.equal(a.resid.nan_to_num(7.0), b.resid.nan_to_num(7.0))
+    assert torch.equal(c.f, b.f) and torch.equal(c.resid.nan_to_num(7.0), b.resid.nan_to_num(7.0))
+    torch.testing.assert_close(c.r2, b.r2, rtol=0, atol=1e-14)
