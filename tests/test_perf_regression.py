@@ -12,8 +12,8 @@ pytestmark = pytest.mark.gpu
 
 # measured on 1x MI355X (ROCm 7.2), round 3 (profiles/r03_risk/perf_guards.log, r03_start/):
 MEASURED = {
-    # bench.py: fp64 storage, refine on, deterministic, graph replay: 0.388 ms / 2520 dates
-    "xs_wls_fp64_reg_per_s": 6.50e6,
+    # bench.py: fp64 storage, refine on, deterministic, graph replay: 0.384 ms / 2520 dates
+    "xs_wls_fp64_reg_per_s": 6.55e6,
     # eigen_risk_adjust at 2520 dates x M = 100: tridiagonal eigh of F0 + bias solver mode 5
     # + finalize (draw covariances given)
     "eigen_adjust_2520x100_ms": 14.45,
