@@ -531,8 +531,11 @@ __device__ __forceinline__ double ipow(double lam, int k) {
 // thread keeps its own C rows in registers (phase A and its own-row steps read them there, the
 // LDS copy only serves other threads' lagged rows) and issues the NEXT tile's loads before
 // computing the current one, so HBM latency hides behind the scan / window math.
-template <class Op, int C, int TR>
-__global__ __launch_bounds__(TR / C) void ew_window_pipe_kernel(
+// PF = false (A/B, ew variant 3): no software prefetch of the next tile -- ~20 fewer VGPRs for
+// occupancy instead.
+template <class Op, int C, int TR, bool PF = true>
+__global__ __launch_bounds__(TR / C) __attribute__((amdgpu_waves_per_eu(PF ? 1 : 4))) void
+ew_window_pipe_kernel(
     const float* __restrict__ in_a, const float* __restrict__ in_b,
     const int* __restrict__ seg_lo, int R, int W, int H, double lam, int minp,
     float* __restrict__ o0, float* __restrict__ o1, int ntiles) {
@@ -588,8 +591,9 @@ __global__ __launch_bounds__(TR / C) void ew_window_pipe_kernel(
   if (tile >= ntiles) return;
   float ra[C], rb[C];
   short rd[C];
-  load(tile, ra, rb, rd);
+  if constexpr (PF) load(tile, ra, rb, rd);
   for (; tile < ntiles; tile += gridDim.x) {
+    if constexpr (!PF) load(tile, ra, rb, rd);
     const int g0 = tile * (TR - H) - H;
 #pragma unroll
     for (int i = 0; i < C; ++i) {
@@ -601,7 +605,8 @@ __global__ __launch_bounds__(TR / C) void ew_window_pipe_kernel(
     float na[C], nb[C];
     short nd[C];
     const int nxt = tile + gridDim.x;
-    if (nxt < ntiles) load(nxt, na, nb, nd);
+    if constexpr (PF)
+      if (nxt < ntiles) load(nxt, na, nb, nd);
     // A. chunk map from registers
     EwMap<NS> m;
     m.A = 1.0;
@@ -663,16 +668,18 @@ __global__ __launch_bounds__(TR / C) void ew_window_pipe_kernel(
       }
     }
     __syncthreads();  // LDS tile / carries are rewritten by the next iteration
+    if constexpr (PF) {
 #pragma unroll
-    for (int i = 0; i < C; ++i) {
-      ra[i] = na[i];
-      rb[i] = nb[i];
-      rd[i] = nd[i];
+      for (int i = 0; i < C; ++i) {
+        ra[i] = na[i];
+        rb[i] = nb[i];
+        rd[i] = nd[i];
+      }
     }
   }
 }
 
-template <class Op, int C, int TR>
+template <class Op, int C, int TR, bool PF = true>
 void launch_ew_pipe(const float* a, const float* b, const int* seg, int R, int W, int H,
                     double lam, int minp, float* o0, float* o1, hipStream_t s) {
   static int blocks = 0;
@@ -680,11 +687,11 @@ void launch_ew_pipe(const float* a, const float* b, const int* seg, int R, int W
     int dev = 0, cus = 0, per = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, ew_window_pipe_kernel<Op, C, TR>, TR / C, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, ew_window_pipe_kernel<Op, C, TR, PF>, TR / C, 0);
     blocks = max(1, cus * max(per, 1));
   }
   const int ntiles = (R + TR - H - 1) / (TR - H);
-  hipLaunchKernelGGL((ew_window_pipe_kernel<Op, C, TR>), dim3(min(ntiles, blocks)), dim3(TR / C), 0,
+  hipLaunchKernelGGL((ew_window_pipe_kernel<Op, C, TR, PF>), dim3(min(ntiles, blocks)), dim3(TR / C), 0,
                      s, a, b, seg, R, W, H, lam, minp, o0, o1, ntiles);
 }
 
@@ -699,6 +706,8 @@ void launch_ew(const float* a, const float* b, const int* seg, int R, int W, int
     launch_ew_pipe<Op, 8, 4096>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
   else if (g_ew_variant == 2)
     launch_ew_pipe<Op, 16, 4096>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
+  else if (g_ew_variant == 3)
+    launch_ew_pipe<Op, 8, 2048, false>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
   else
     launch_ew_pipe<Op, 8, 2048>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
 }
