@@ -531,8 +531,10 @@ __device__ __forceinline__ double ipow(double lam, int k) {
 // thread keeps its own C rows in registers (phase A and its own-row steps read them there, the
 // LDS copy only serves other threads' lagged rows) and issues the NEXT tile's loads before
 // computing the current one, so HBM latency hides behind the scan / window math.
-// PF = false (A/B, ew variant 3): no software prefetch of the next tile -- ~20 fewer VGPRs for
-// occupancy instead.
+// PF = false (default): no software prefetch of the next tile -- BETA 148 -> 128 VGPRs, 3 -> 4
+// waves / SIMD, and the extra waves hide the tile loads better than the prefetch did (5000 x
+// 3780: BETA/HSIGMA 0.196 -> 0.173 ms, DASTD 0.131 -> 0.122 ms, bitwise the same outputs,
+// profiles/r03_rolling_nopf_ab.jsonl).  PF = true = ew variant 3.
 template <class Op, int C, int TR, bool PF = true>
 __global__ __launch_bounds__(TR / C) __attribute__((amdgpu_waves_per_eu(PF ? 1 : 4))) void
 ew_window_pipe_kernel(
@@ -697,7 +699,8 @@ void launch_ew_pipe(const float* a, const float* b, const int* seg, int R, int W
 
 // A/B geometry of the anchored-prefix kernel (mfa_rolling_set_ew_variant): 0 = 8-row chunks x
 // 256 threads (2048-row tiles, default), 1 = 8 x 512 (4096-row tiles: half the halo re-read),
-// 2 = 16 x 256 (4096-row tiles, half the scan steps per row).
+// 2 = 16 x 256 (4096-row tiles, half the scan steps per row), 3 = the default geometry with the
+// software prefetch of the next tile (3 waves / SIMD).
 int g_ew_variant = 0;
 template <class Op>
 void launch_ew(const float* a, const float* b, const int* seg, int R, int W, int H, double lam,
@@ -706,10 +709,10 @@ void launch_ew(const float* a, const float* b, const int* seg, int R, int W, int
     launch_ew_pipe<Op, 8, 4096>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
   else if (g_ew_variant == 2)
     launch_ew_pipe<Op, 16, 4096>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
-  else if (g_ew_variant == 3)
-    launch_ew_pipe<Op, 8, 2048, false>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
+  else if (g_ew_variant == 3)  // round-3 default until the 4-wave variant measured faster
+    launch_ew_pipe<Op, 8, 2048, true>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
   else
-    launch_ew_pipe<Op, 8, 2048>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
+    launch_ew_pipe<Op, 8, 2048, false>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
 }
 
 template <int H>

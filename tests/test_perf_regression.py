@@ -19,8 +19,8 @@ MEASURED = {
     "eigen_adjust_2520x100_ms": 14.45,
     # Newey-West expanding series, T = 2520, K = 42, q = 2
     "newey_west_2520_ms": 0.100,
-    # BETA/HSIGMA anchored-prefix kernel, 5000 x 3780 (Newton-reciprocal finishers)
-    "beta_hsigma_5000x3780_ms": 0.194,
+    # BETA/HSIGMA anchored-prefix kernel, 5000 x 3780 (Newton-reciprocal finishers, 4 waves / SIMD)
+    "beta_hsigma_5000x3780_ms": 0.173,
     # point-in-time trailing specific vol, 2520 x 5000, W = 252 (profiles/r03_risk/)
     "trailing_vol_2520x5000_ms": 1.075,
 }
