@@ -709,6 +709,8 @@ void launch_ew(const float* a, const float* b, const int* seg, int R, int W, int
     launch_ew_pipe<Op, 8, 4096>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
   else if (g_ew_variant == 2)
     launch_ew_pipe<Op, 16, 4096>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
+  else if (g_ew_variant == 4)  // A/B: 4096-row tiles without the prefetch (half the halo)
+    launch_ew_pipe<Op, 8, 4096, false>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
   else if (g_ew_variant == 3)  // round-3 default until the 4-wave variant measured faster
     launch_ew_pipe<Op, 8, 2048, true>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
   else

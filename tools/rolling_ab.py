@@ -39,7 +39,7 @@ cases = {
     "rstr": (lambda: _native.call("mfa_rstr", _native.ptr(lr), _native.ptr(seg), R, 21, 483,
                                   0.5 ** (1 / 126), 42, _native.ptr(rstr), _native.stream(dev)), 12),
 }
-variants = [("mode2_r01", 2, 0), ("default", 0, 0), ("ew_8x512", 0, 1), ("ew_16x256", 0, 2), ("ew_8x256_prefetch", 0, 3)]
+variants = [("mode2_r01", 2, 0), ("default", 0, 0), ("ew_8x512", 0, 1), ("ew_16x256", 0, 2), ("ew_8x256_prefetch", 0, 3), ("ew_8x512_nopf", 0, 4)]
 _native.register("mfa_rolling_set_ew_variant", [__import__("ctypes").c_int])
 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 ref = {}
