@@ -10,6 +10,8 @@
         --industry sw_industry.csv --out data/
     python -m llm_driven_multi_factor_model_amd.cli pipeline --prices prices.csv --index index.csv \
         --industry sw_industry.csv --out results/ [--write-barra data/]   # main.py + demo.py in HBM
+    torchrun --nproc-per-node 8 --master-addr 127.0.0.1 -m llm_driven_multi_factor_model_amd.cli \
+        pipeline ...          # date-sharded end to end: each rank its date block + halo
     python -m llm_driven_multi_factor_model_amd.cli serve --data barra_data_csi.csv \
         --industry industry_info.csv --port 8000      # POST /risk {"portfolios": [...]}
 
@@ -193,9 +195,13 @@ def cmd_pipeline(a):
     """The whole job in HBM: loader CSVs -> descriptors -> exposures -> risk model -> the five
     results CSVs (main.py then demo.py without the barra_data_csi.csv round trip)."""
     from .models import e2e
+    from .parallel import dist as pdist
     from .utils.config import preset
     from .utils.io import write_risk_results
-    _setup_logging()
+    # torchrun: date-sharded end to end (each rank reads the loader columns, computes its date
+    # block + halo, and the risk model runs over the ranks' blocks); rank 0 writes the CSVs
+    ctx = pdist.init_distributed(device=a.device)
+    _setup_logging(ctx.rank)
     t0 = time.perf_counter()
     prices, index = e2e.read_price_columns(a.prices, a.index)
     if prices is None:
@@ -204,30 +210,37 @@ def cmd_pipeline(a):
     sw = pd.read_csv(a.industry, dtype={"ts_code": str, "l1_code": str})
     t_read = time.perf_counter() - t0
     over = {k: v for k, v in dict(eigen_sims=a.sims, vra_half_life=a.vra_tau, nw_lags=a.nw_q,
-                                  nw_half_life=a.nw_tau).items() if v is not None}
+                                  nw_half_life=a.nw_tau, time_scan=a.time_scan).items()
+            if v is not None}
     cfg = preset(a.preset, **over)
-    model, info, frame, t = e2e.run_pipeline(prices, index, sw, risk_cfg=cfg, device=a.device,
-                                             want_barra=bool(a.write_barra))
+    pdist.barrier(ctx)
+    model, info, frame, t = e2e.run_pipeline(prices, index, sw, risk_cfg=cfg,
+                                             device=None if ctx.enabled else a.device,
+                                             want_barra=bool(a.write_barra), ctx=ctx)
     t0 = time.perf_counter()
     paths = write_risk_results(model, a.out, long_specific=a.long_specific)
-    if a.write_barra:
+    if a.write_barra and frame is not None:
         os.makedirs(a.write_barra, exist_ok=True)
         frame.to_csv(os.path.join(a.write_barra, "barra_data_csi.csv"), index=False)
         info.to_csv(os.path.join(a.write_barra, "industry_info.csv"), index=False)
     t_write = time.perf_counter() - t0
-    compute = {k: round(v, 4) for k, v in t.items() if k.endswith("_s")}
-    log.info("pipeline: panel %d dates x %d stocks x K=%d; read %.3fs, compute %s (%.3fs), "
-             "write %.3fs", model.panel.D, model.panel.N, model.K, t_read, json.dumps(compute),
-             sum(compute.values()), t_write)
-    if a.timings:
-        with open(a.timings, "w") as fh:
-            json.dump({"read_s": t_read, "write_s": t_write, **compute,
-                       "non_io_s": sum(compute.values()), "D": model.panel.D,
-                       "N": model.panel.N, "K": model.K,
-                       "rows": int(model.panel.valid().sum()) if hasattr(model.panel, "valid") else None},
-                      fh)
-    for k, v in paths.items():
-        log.info("wrote %s -> %s", k, v)
+    compute = {k: v for k, v in t.items() if k.endswith("_s")}
+    if ctx.enabled:  # the job's time is the slowest rank's
+        compute = {k: pdist.all_reduce_max(v, ctx) for k, v in compute.items()}
+    compute = {k: round(v, 4) for k, v in compute.items()}
+    T = sum(model.sizes)
+    if ctx.rank == 0:
+        log.info("pipeline: %d rank(s), panel %d dates x %d stocks x K=%d; read %.3fs, compute "
+                 "%s (%.3fs), write %.3fs", ctx.world, T, model.panel.N, model.K, t_read,
+                 json.dumps(compute), sum(compute.values()), t_write)
+        if a.timings:
+            with open(a.timings, "w") as fh:
+                json.dump({"read_s": t_read, "write_s": t_write, **compute,
+                           "non_io_s": sum(compute.values()), "D": T, "N": model.panel.N,
+                           "K": model.K, "world": ctx.world}, fh)
+        for k, v in paths.items():
+            log.info("wrote %s -> %s", k, v)
+    pdist.barrier(ctx)
 
 
 def cmd_factors(a):
@@ -311,6 +324,9 @@ def main(argv=None):
     q.add_argument("--nw-q", type=int, default=None)
     q.add_argument("--nw-tau", type=float, default=None)
     q.add_argument("--vra-tau", type=float, default=None)
+    q.add_argument("--time-scan", choices=["gather", "carry"], default=None,
+                   help="time-axis stages across ranks: gather the factor-return series "
+                        "(default, equal to one process) or carry block states")
     q.add_argument("--long-specific", action="store_true")
     q.add_argument("--device", default=None)
     q.add_argument("--timings", default=None, help="write stage timings (JSON) here")
@@ -323,7 +339,7 @@ def main(argv=None):
     f.add_argument("--device", default=None)
     f.set_defaults(fn=cmd_factors)
     a = ap.parse_args(argv)
-    if a.cmd not in ("risk", "factors", "serve"):
+    if a.cmd not in ("risk", "factors", "serve", "pipeline"):
         _setup_logging()
     a.fn(a)
     return 0

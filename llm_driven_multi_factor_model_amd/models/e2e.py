@@ -153,10 +153,19 @@ class DeviceFactorEngine(FactorEngine):
             e = torch.from_numpy(np.asarray(prices["end_date"], dtype=np.int64)).to(dev)
             self.end_date = perm(e)
 
+    def _has_statements(self) -> bool:
+        return "n_cashflow_act" in self.cols and self.end_date is not None
+
+    def _take(self, idx, d_lo=0, d_hi=None):
+        sub = super()._take(idx, d_lo, d_hi)
+        sub.end_date = None if self.end_date is None else self.end_date[idx]
+        sub.date_ints = self.date_ints[d_lo:sub.D + d_lo]
+        return sub
+
     # statement-row TTM (factor_calculator.py:392-410) with integer end dates on the device
-    def compute_earnings_yield(self):
-        if not (self._need("n_cashflow_act", "total_mv", "pe_ttm") and self.end_date is not None):
-            return None
+    def cashflow_ttm(self) -> torch.Tensor:
+        if getattr(self, "_ttm", None) is not None:
+            return self._ttm
         dev = self.device
         e = torch.where(self.end_date < 0, torch.full_like(self.end_date, 2 ** 62), self.end_date)
         sc = self.stock_id.to(torch.int64)
@@ -179,7 +188,13 @@ class DeviceFactorEngine(FactorEngine):
         vb = vf[inv]
         if not bool(((v == vb) | (v.isnan() & vb.isnan())).all()):
             raise NeedsPandasPath("several cash-flow values for one (stock, end_date)")
-        ttm = RL.rolling_sum(vf.float(), RL.seg_lo_from_codes(seg_codes), 4, 4).double()[inv]
+        self._ttm = RL.rolling_sum(vf.float(), RL.seg_lo_from_codes(seg_codes), 4, 4).double()[inv]
+        return self._ttm
+
+    def compute_earnings_yield(self):
+        if not (self._need("n_cashflow_act", "total_mv", "pe_ttm") and self._has_statements()):
+            return None
+        ttm = self.cashflow_ttm()
         mv = self.cols["total_mv"].double()
         nan = torch.full_like(mv, float("nan"))
         cetop = torch.where((mv > 0) & (ttm > 0), ttm / mv, nan)  # unit mix-up kept (quirk Q17)
@@ -220,12 +235,51 @@ def export_columns(col: dict, nxt: torch.Tensor) -> dict:
     return out
 
 
+def next_return_global(eng: FactorEngine, ret: torch.Tensor, ctx=None) -> torch.Tensor:
+    """``groupby(ts_code).ret.shift(-1)`` (main.py:99) on a rank's owned rows of a date-sharded
+    run.  Inside the block it is the in-rank shift; the last owned row of a stock takes the
+    stock's FIRST row on the next rank that has one (a stock may skip a whole block).  One
+    collective: every rank contributes [first-row value, has-a-row] per stock ([2, N] fp64)."""
+    from ..parallel import dist as pdist
+    nxt = next_return(eng, ret)
+    if ctx is None or not ctx.enabled:
+        return nxt
+    dev, N, R = eng.device, eng.N, eng.R
+    sid = eng.stock_id.long()
+    mine = torch.zeros(2, N, dtype=torch.float64, device=dev)
+    mine[0].fill_(float("nan"))
+    if R:
+        first = torch.ones(R, dtype=torch.bool, device=dev)
+        last = torch.ones(R, dtype=torch.bool, device=dev)
+        first[1:] = sid[1:] != sid[:-1]
+        last[:-1] = sid[1:] != sid[:-1]
+        fr = torch.nonzero(first).flatten()
+        mine[0, sid[fr]] = ret.double()[fr]
+        mine[1, sid[fr]] = 1.0
+    allr = pdist.all_gather_rows(mine[None], ctx, [1] * ctx.world)   # [world, 2, N]
+    later = allr[ctx.rank + 1:]
+    if later.shape[0] and R:
+        has = later[:, 1] > 0                                            # [w', N]
+        which = torch.argmax(has.to(torch.int8), 0)                      # first later rank
+        val = later[:, 0].gather(0, which[None]).squeeze(0)
+        val = torch.where(has.any(0), val, torch.full_like(val, float("nan")))
+        lr = torch.nonzero(last).flatten()
+        nxt[lr] = val[sid[lr]]
+    return nxt
+
+
 def risk_panel(eng: FactorEngine, cols: dict, l1_stock: np.ndarray, info: pd.DataFrame,
-               dtype=torch.float64) -> RiskPanel:
+               dtype=torch.float64, ctx=None) -> RiskPanel:
     """demo.py:22-35 on device tensors: rows with any NaN (or no industry in ``info``) are
     dropped, industries become ids into ``info``'s rows, and the rows are scattered into the
     [D, Q, N] panel over the dates / stocks that keep at least one row (the panel
-    ``panel_from_barra_csv`` builds from the exported CSV)."""
+    ``panel_from_barra_csv`` builds from the exported CSV).
+
+    Date-sharded (``ctx`` enabled, ``eng`` = a rank's owned rows on its local date axis): the
+    stock axis is GLOBAL -- the keep masks are max-reduced over ranks (one [N] all_reduce) so
+    every rank scatters into the same columns -- and the panel's ``date_offset`` counts the
+    kept dates of the ranks before (one [world] all_gather)."""
+    from ..parallel import dist as pdist
     dev = eng.device
     missing = [c for c in ["capital", "ret", *STYLE_COLUMNS] if c not in cols]
     if missing:
@@ -243,6 +297,13 @@ def risk_panel(eng: FactorEngine, cols: dict, l1_stock: np.ndarray, info: pd.Dat
     sk = torch.zeros(eng.N, dtype=torch.bool, device=dev)
     dk[did[keep]] = True
     sk[sid[keep]] = True
+    offset = 0
+    if ctx is not None and ctx.enabled:
+        ski = sk.to(torch.int32)
+        pdist.all_reduce_max_(ski, ctx)
+        sk = ski > 0
+        kept = pdist.shard_sizes(int(dk.sum()), ctx)
+        offset = sum(kept[:ctx.rank])
     dnew = torch.cumsum(dk.to(torch.int64), 0) - 1
     snew = torch.cumsum(sk.to(torch.int64), 0) - 1
     Dp, Np = int(dk.sum()), int(sk.sum())
@@ -270,17 +331,40 @@ def risk_panel(eng: FactorEngine, cols: dict, l1_stock: np.ndarray, info: pd.Dat
                      ind=ind.view(Dp, Np) if len(info) else None, P=len(info), dates=dates,
                      stocks=np.asarray(eng.stock_names, dtype=object)[smask],
                      style_names=list(STYLE_COLUMNS),
-                     industry_names=list(info["industry_names"].astype(str).to_numpy()))
+                     industry_names=list(info["industry_names"].astype(str).to_numpy()),
+                     date_offset=offset)
 
 
-def barra_frame(eng: FactorEngine, cols: dict, l1_stock: np.ndarray) -> pd.DataFrame:
-    """The barra_data_csi.csv frame (only built when requested: it is I/O, not compute)."""
+def barra_frame(eng: FactorEngine, cols: dict, l1_stock: np.ndarray, ctx=None,
+                date_names=None) -> pd.DataFrame | None:
+    """The barra_data_csi.csv frame (only built when requested: it is I/O, not compute).
+
+    Date-sharded: every rank's owned rows go to rank 0 in ONE collective ([R_r, C + 2] fp64:
+    the numeric columns, stock id and global date id) and are put back in master order
+    (stock, date) by one device sort; other ranks return None.  ``date_names``: the GLOBAL
+    date strings (the full engine's)."""
+    from ..parallel import dist as pdist
     names = [c for c in BARRA_OUTPUT_COLUMNS if c in cols]
-    host = torch.stack([cols[c] for c in names]).cpu().numpy()
+    sid_t, did_t = eng.stock_id.long(), eng.date_id.long()
+    if ctx is not None and ctx.enabled:
+        did_t = did_t + getattr(eng, "date_lo", 0)
+        block = torch.stack([cols[c].double() for c in names]
+                            + [sid_t.double(), did_t.double()], 1)
+        full = pdist.gather_to_root(block.contiguous(), ctx)
+        if full is None:
+            return None
+        sid_t, did_t = full[:, -2].long(), full[:, -1].long()
+        order = torch.argsort(sid_t * (1 << 32) + did_t)
+        full = full[order]
+        sid_t, did_t = sid_t[order], did_t[order]
+        host = full[:, :len(names)].T.cpu().numpy()
+    else:
+        host = torch.stack([cols[c] for c in names]).cpu().numpy()
     final = pd.DataFrame(host.T, columns=names, copy=False)
-    sid = eng.stock_id.cpu().numpy()
-    did = eng.date_id.cpu().numpy()
-    final.insert(0, "date", np.asarray(eng.date_names, dtype=object)[did])
+    sid = sid_t.cpu().numpy()
+    did = did_t.cpu().numpy()
+    dn = eng.date_names if date_names is None else date_names
+    final.insert(0, "date", np.asarray(dn, dtype=object)[did])
     final.insert(1, "stocknames", np.asarray(eng.stock_names, dtype=object)[sid])
     final.insert(4, "industry", pd.Series(l1_stock[sid], dtype=object))
     return final[[c for c in BARRA_OUTPUT_COLUMNS if c in final.columns]]
@@ -319,34 +403,96 @@ def _columns_from_frames(prices_df: pd.DataFrame, index_df: pd.DataFrame):
     return p, i
 
 
-def run_pipeline(prices, index, sw_industry: pd.DataFrame, risk_cfg: RiskConfig | None = None,
-                 factor_cfg: FactorConfig | None = None, factors=None, device=None,
-                 want_barra: bool = False, sync: bool = True):
-    """The whole job in HBM.  ``prices`` / ``index``: columnar dicts (``read_price_columns``)
-    or pandas frames.  Returns ``(model, info, barra_frame or None, timings)``; the model has
-    run all four stages."""
-    from .risk_model import RiskModel
+def exposures(prices, index, sw_industry: pd.DataFrame, factor_cfg: FactorConfig | None = None,
+              factors=None, device=None, ctx=None, sync: bool = True):
+    """``main.py:42-137`` on device tensors: descriptors -> winsorize -> composites ->
+    orthogonalisation -> t+1 return -> export columns.
+
+    Single process: every row.  Date-sharded (``ctx`` enabled, torchrun one rank per GPU):
+    every rank builds the device master from the same loader columns (no collective, C2),
+    keeps its balanced date block plus each stock's ``halo_rows()`` preceding rows
+    (``date_shard``: the RSTR window reaches 504 rows back), runs the descriptors on that
+    slice, and the per-date post-processing on its owned dates only (local [D_r, N] grid);
+    the t+1 return crosses the block boundary with one [2, N] collective.
+
+    Returns ``(eng, cols, info, l1_stock, full_eng, timings)``: ``eng`` = the rows this rank
+    owns, ``cols`` = {barra column: float64 tensor over those rows}."""
     t = {}
     t0 = time.perf_counter()
     if isinstance(prices, pd.DataFrame):
         prices, index = _columns_from_frames(prices, index)
-    eng = DeviceFactorEngine(prices, index, device=device, config=factor_cfg)
-    res = eng.compute(factors or FACTORS_TO_RUN)
+    if ctx is not None and ctx.enabled and device is None:
+        device = ctx.device
+    full = DeviceFactorEngine(prices, index, device=device, config=factor_cfg)
+    if ctx is not None and ctx.enabled:
+        from ..parallel import dist as pdist
+        sh = full.date_shard(*pdist.shard_range(full.D, ctx.rank, ctx.world))
+        res = sh.compute(factors or FACTORS_TO_RUN)
+        own = torch.nonzero(sh.own).flatten()
+        res = {k: v[own] for k, v in res.items()}
+        eng = sh.owned()
+        eng.timings = sh.timings
+    else:
+        eng = full
+        res = eng.compute(factors or FACTORS_TO_RUN)
     t["descriptors_s"] = time.perf_counter() - t0
     t0 = time.perf_counter()
     col = postprocess_columns(eng, res, eng.cfg)
-    nxt = next_return(eng, col["ret"])
+    nxt = next_return_global(eng, col["ret"], ctx)
     cols = export_columns(col, nxt)
     info, l1_stock = industry_info(eng, sw_industry)
-    panel = risk_panel(eng, cols, l1_stock, info)
     if sync and eng.device.type == "cuda":
         torch.cuda.synchronize(eng.device)
-    t["exposures_to_panel_s"] = time.perf_counter() - t0
+    t["postprocess_s"] = time.perf_counter() - t0
+    return eng, cols, info, l1_stock, full, t
+
+
+def run_factors(prices, index, sw_industry: pd.DataFrame, factor_cfg: FactorConfig | None = None,
+                factors=None, device=None, ctx=None):
+    """``cli factors`` (main.py) on the device path: ``(barra frame, industry_info, timings)``
+    on rank 0 (``(None, None, timings)`` on the other ranks of a date-sharded run)."""
+    eng, cols, info, l1_stock, full, t = exposures(prices, index, sw_industry, factor_cfg,
+                                                   factors, device, ctx)
     t0 = time.perf_counter()
-    model = RiskModel(panel, risk_cfg or RiskConfig()).run()
+    frame = barra_frame(eng, cols, l1_stock, ctx, full.date_names)
+    t["export_s"] = time.perf_counter() - t0
+    t["kernel_ms"] = getattr(eng, "timings", {})
+    if frame is None:
+        return None, None, t
+    return frame, info, t
+
+
+def run_pipeline(prices, index, sw_industry: pd.DataFrame, risk_cfg: RiskConfig | None = None,
+                 factor_cfg: FactorConfig | None = None, factors=None, device=None,
+                 want_barra: bool = False, sync: bool = True, ctx=None):
+    """The whole job in HBM.  ``prices`` / ``index``: columnar dicts (``read_price_columns``)
+    or pandas frames.  Returns ``(model, info, barra_frame or None, timings)``; the model has
+    run all four stages.
+
+    With an enabled ``ctx`` (torchrun, one rank per GPU) the job is date-sharded end to end
+    (BASELINE config 3): :func:`exposures` on the rank's block, a :class:`RiskPanel` on the
+    global stock axis, and :class:`RiskModel` over the ranks' date blocks.  With the default
+    ``time_scan="gather"`` every output equals the single-process run to rounding-free
+    equality of the regression and 1e-12 of the scans (tests/test_e2e_dist.py); "carry" scans
+    only the rank's own dates and carries block states across ranks (the Newey-West series
+    then differs from one process at ~1e-11 relative, which the eigen adjustment can amplify
+    where eigenvalues nearly coincide).  Nothing leaves HBM until the CSV writers gather to
+    rank 0; the barra frame (``want_barra``) is returned on rank 0 only."""
+    from .risk_model import RiskModel
+    dist_on = ctx is not None and ctx.enabled
+    eng, cols, info, l1_stock, full, t = exposures(prices, index, sw_industry, factor_cfg,
+                                                   factors, device, ctx, sync)
+    t0 = time.perf_counter()
+    panel = risk_panel(eng, cols, l1_stock, info, ctx=ctx)
+    if sync and eng.device.type == "cuda":
+        torch.cuda.synchronize(eng.device)
+    t["exposures_to_panel_s"] = t.pop("postprocess_s") + time.perf_counter() - t0
+    t0 = time.perf_counter()
+    cfg = risk_cfg or RiskConfig()
+    model = RiskModel(panel, cfg, ctx=ctx if dist_on else None).run()
     if sync and eng.device.type == "cuda":
         torch.cuda.synchronize(eng.device)
     t["risk_model_s"] = time.perf_counter() - t0
     t["kernel_ms"] = getattr(eng, "timings", {})
-    frame = barra_frame(eng, cols, l1_stock) if want_barra else None
+    frame = barra_frame(eng, cols, l1_stock, ctx, full.date_names) if want_barra else None
     return model, info, frame, t

@@ -161,7 +161,9 @@ class FactorEngine:
         Every window of an owned row then lies inside the slice, or starts at the stock's true
         first row, so the rolling descriptors of owned rows equal the full-panel ones (up to the
         summation order of the sliding kernels); per-date steps only see owned dates whole.
-        Rows outside [lo, hi) are dropped again by :meth:`run`.
+        The statement-row TTM (whose 4 distinct statements can reach further back than any
+        row window) is formed on the full rows first and sliced.  Rows outside [lo, hi) are
+        dropped again by :meth:`run` (or :meth:`owned`).
         """
         H = self.halo_rows() if halo is None else int(halo)
         dev = self.device
@@ -173,17 +175,42 @@ class FactorEngine:
         f = first[sid]
         keep = own | ((f < self.R) & (row < f) & (row >= f - H))
         idx = torch.nonzero(keep).flatten()
+        if self._has_statements():
+            self.cashflow_ttm()
+        sub = self._take(idx)
+        sub.own = own[idx]
+        sub.lo, sub.hi = lo, hi
+        return sub
+
+    def owned(self) -> "FactorEngine":
+        """The owned rows of a :meth:`date_shard` as an engine of its own, on the LOCAL date
+        axis [0, hi - lo) (``date_lo`` = global index of local date 0): the per-date
+        post-processing then works on a [hi - lo, N] grid instead of the global one."""
+        if self.own is None:
+            return self
+        sub = self._take(torch.nonzero(self.own).flatten(), self.lo, self.hi)
+        sub.date_lo = self.lo
+        return sub
+
+    def _take(self, idx: torch.Tensor, d_lo: int = 0, d_hi: int | None = None) -> "FactorEngine":
+        """Rows ``idx`` (increasing, so still sorted by stock then date) as a new engine; dates
+        renumbered to [0, d_hi - d_lo)."""
+        d_hi = self.D if d_hi is None else d_hi
         sub = object.__new__(type(self))
-        sub.cfg, sub.device, sub.prep_s = self.cfg, dev, 0.0
-        sub.stock_names, sub.date_names = self.stock_names, self.date_names
-        sub.D, sub.N, sub.R = self.D, self.N, int(idx.numel())
-        sub.master = self.master.iloc[idx.cpu().numpy()].reset_index(drop=True)
-        sub.stock_id, sub.date_id = self.stock_id[idx], self.date_id[idx]
+        sub.cfg, sub.device, sub.prep_s = self.cfg, self.device, 0.0
+        sub.stock_names, sub.date_names = self.stock_names, self.date_names[d_lo:d_hi]
+        sub.D, sub.N, sub.R = d_hi - d_lo, self.N, int(idx.numel())
+        sub.master = None if self.master is None else \
+            self.master.iloc[idx.cpu().numpy()].reset_index(drop=True)
+        sub.stock_id = self.stock_id[idx]
+        sub.date_id = self.date_id[idx] - d_lo if d_lo else self.date_id[idx]
         sub.seg_lo = RL.seg_lo_from_codes(sub.stock_id)
         sub.grid_idx = sub.date_id.long() * sub.N + sub.stock_id.long()
         sub.cols = {k: v[idx] for k, v in self.cols.items()}
-        sub.own = own[idx]
-        sub.lo, sub.hi = lo, hi
+        ttm = getattr(self, "_ttm", None)
+        sub._ttm = None if ttm is None else ttm[idx]
+        sub.own = None
+        sub.date_lo = getattr(self, "date_lo", 0) + d_lo
         return sub
 
     # ---------------------------------------------------------------- grid helpers
@@ -248,13 +275,22 @@ class FactorEngine:
             out[name] = RL.rolling_sum(tr, self.seg_lo, w, mp, scale=0.01, log=True)
         return out
 
+    def _has_statements(self) -> bool:
+        return "n_cashflow_act" in self.cols and "end_date" in self.master.columns
+
+    def cashflow_ttm(self) -> torch.Tensor:
+        """[R] float64 statement-row TTM of ``n_cashflow_act`` (factor_calculator.py:392-410),
+        computed once and kept (date shards slice the full-row result)."""
+        if getattr(self, "_ttm", None) is None:
+            m = self.master
+            cf = self._ttm_by_codes(m)
+            self._ttm = cf if cf is not None else self._ttm_by_merge(m)
+        return self._ttm
+
     def compute_earnings_yield(self):
-        if not (self._need("n_cashflow_act", "total_mv", "pe_ttm") and "end_date" in self.master.columns):
+        if not (self._need("n_cashflow_act", "total_mv", "pe_ttm") and self._has_statements()):
             return None
-        m = self.master
-        cf = self._ttm_by_codes(m)
-        if cf is None:
-            cf = self._ttm_by_merge(m)
+        cf = self.cashflow_ttm()
         mv = self.cols["total_mv"].double()
         nan = torch.full_like(mv, float("nan"))
         cetop = torch.where((mv > 0) & (cf > 0), cf / mv, nan)  # unit mix-up kept (quirk Q17)
@@ -621,25 +657,32 @@ def factor_pipeline(prices_df, index_df, sw_industry_df, factors=None, config: F
 
     Single process (the default): :func:`_pipeline_columnar`, device tensors end to end and
     one export frame; ``columnar=False`` runs the frame-by-frame compat path (same output).
-    With an enabled ``ctx`` (torchrun, one rank per GPU) each rank computes its date block
-    (``date_shard``: descriptors with a halo, then the per-date post-processing) and rank 0
-    gathers the blocks and writes the export; other ranks return ``(None, None, timings)``.
+    With an enabled ``ctx`` (torchrun, one rank per GPU) the job is date-sharded on device
+    tensors end to end (``e2e.run_factors``: each rank's block plus a halo, per-date steps on
+    owned dates, the t+1 return across blocks by one collective, the owned rows gathered to
+    rank 0 as one fp64 block); other ranks return ``(None, None, timings)``.  Input the device
+    path does not model (duplicate (stock, date) rows, ...) runs on rank 0 alone.
     """
-    from ..parallel import dist as pdist
     cfg = config or FactorConfig()
     dist_on = ctx is not None and ctx.enabled
-    if dist_on and device is None:
-        device = ctx.device
+    if dist_on:
+        from . import e2e
+        if device is None:
+            device = ctx.device
+        try:
+            return e2e.run_factors(prices_df, index_df, sw_industry_df, cfg, factors, device, ctx)
+        except e2e.NeedsPandasPath as exc:
+            log.warning("date-sharded factor pipeline: %s; rank 0 runs the whole panel", exc)
+            if ctx.rank != 0:
+                return None, None, {}
     t = {}
     t0 = time.perf_counter()
     eng = FactorEngine(prices_df, index_df, device=device, config=cfg)
-    if (columnar and not dist_on and eng.R == len(prices_df) and sw_industry_df["ts_code"].is_unique
+    if (columnar and eng.R == len(prices_df) and sw_industry_df["ts_code"].is_unique
             and len(eng.master) == eng.R):
         t["prep_s"] = time.perf_counter() - t0
         final, info = _pipeline_columnar(eng, factors or FACTORS_TO_RUN, cfg, sw_industry_df, t)
         return final, info, dict(t, kernel_ms=getattr(eng, "timings", {}))
-    if dist_on:
-        eng = eng.date_shard(*pdist.shard_range(eng.D, ctx.rank, ctx.world))
     raw = eng.run(factors or FACTORS_TO_RUN)
     t["descriptors_s"] = time.perf_counter() - t0
     t0 = time.perf_counter()
@@ -650,23 +693,31 @@ def factor_pipeline(prices_df, index_df, sw_industry_df, factors=None, config: F
     c = composite_frame(w, cfg.composite, device=eng.device, copy=False)
     o = orthogonalize_frame(c, cfg.ortho, device=eng.device, grid=grid, copy=False)
     t["postprocess_s"] = time.perf_counter() - t0
-    if dist_on:  # C7: date blocks to rank 0, back in master order (ts_code, trade_date)
-        parts = pdist.gather_objects(o, ctx)
-        if ctx.rank != 0:
-            return None, None, dict(t, kernel_ms=getattr(eng, "timings", {}))
-        o = pd.concat(parts, ignore_index=True).sort_values(["ts_code", "trade_date"], kind="stable")
-        o = o.reset_index(drop=True)
     final, info = barra_export(o, sw_industry_df)
     return final, info, dict(t, kernel_ms=getattr(eng, "timings", {}))
 
 
 def run_factor_pipeline(prices_csv, index_csv, industry_csv, out_dir, device=None, ctx=None):
-    prices = pd.read_csv(prices_csv)
-    index = pd.read_csv(index_csv)
-    sw = pd.read_csv(industry_csv)
-    for df in (prices, index):
-        df["trade_date"] = pd.to_datetime(df["trade_date"].astype(str), format="mixed")
-    final, info, t = factor_pipeline(prices, index, sw, device=device, ctx=ctx)
+    """``cli factors``: loader CSVs -> barra_data_csi.csv + industry_info.csv.  The native
+    columnar reader feeds the device path (``e2e.run_factors``; date-sharded under torchrun);
+    pandas frames only when the reader is unavailable or the input needs the pandas path."""
+    from . import e2e
+    sw = pd.read_csv(industry_csv, dtype={"ts_code": str, "l1_code": str})
+    final = info = None
+    done = False
+    p, i = e2e.read_price_columns(prices_csv, index_csv)
+    if p is not None:
+        try:
+            final, info, t = e2e.run_factors(p, i, sw, device=device, ctx=ctx)
+            done = True
+        except e2e.NeedsPandasPath as exc:
+            log.info("factors: %s; pandas path", exc)
+    if not done:
+        prices = pd.read_csv(prices_csv)
+        index = pd.read_csv(index_csv)
+        for df in (prices, index):
+            df["trade_date"] = pd.to_datetime(df["trade_date"].astype(str), format="mixed")
+        final, info, t = factor_pipeline(prices, index, sw, device=device, ctx=ctx)
     if final is None:  # non-root rank of a sharded run
         return None, None
     os.makedirs(out_dir, exist_ok=True)

@@ -9,7 +9,10 @@ Collective call sites:
   C3 factor-return series      all_gather   (D_local x K fp64)
   C5 MC bias accumulators      all_reduce   (D x K fp64, sims-sharded eigen adjustment)
   C6 VRA bias series           all_gather   (D_local fp64)
-  C7 outputs to rank 0         gather       (only when writing CSVs; factor-pipeline frames)
+  C7 outputs to rank 0         gather       (only when writing CSVs: result series, the
+                                             barra frame's owned rows as one fp64 block)
+  C10 t+1 return across blocks all_gather   ([2, N] first-row value / presence per stock)
+  C11 global stock axis        all_reduce   ([N] keep mask, MAX) + [world] kept-date counts
   C8 benchmark fences          barrier
   C9 stock-sharded (TP) CS-WLS all_reduce   (D x msize moments, then D x 5 R^2 sums;
                                              ops/xs_sharded.py)
@@ -181,17 +184,6 @@ def gather_to_root(x: torch.Tensor, ctx: DistContext | None = None) -> torch.Ten
     return full if ctx.rank == 0 else None
 
 
-def gather_objects(obj, ctx: DistContext | None = None) -> list | None:
-    """Every rank's picklable ``obj`` in rank order on rank 0 (None elsewhere); C7 for
-    host-side frames (the sharded factor pipeline's per-rank date blocks)."""
-    ctx = ctx or context()
-    if not ctx.enabled:
-        return [obj]
-    out = [None] * ctx.world if ctx.rank == 0 else None
-    dist.gather_object(obj, out, dst=0)
-    return out
-
-
 def all_reduce_max(x: float, ctx: DistContext | None = None, device=None) -> float:
     ctx = ctx or context()
     if not ctx.enabled:
@@ -199,6 +191,15 @@ def all_reduce_max(x: float, ctx: DistContext | None = None, device=None) -> flo
     t = torch.tensor([x], dtype=torch.float64, device=device or ctx.device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def all_reduce_max_(x: torch.Tensor, ctx: DistContext | None = None) -> torch.Tensor:
+    """In-place elementwise MAX over ranks (e.g. the global stock-axis keep mask of a
+    date-sharded risk panel)."""
+    ctx = ctx or context()
+    if ctx.enabled:
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+    return x
 
 
 def all_reduce_sum(x: torch.Tensor, ctx: DistContext | None = None) -> torch.Tensor:
