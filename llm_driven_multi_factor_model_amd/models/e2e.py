@@ -489,7 +489,10 @@ def run_pipeline(prices, index, sw_industry: pd.DataFrame, risk_cfg: RiskConfig 
     t["exposures_to_panel_s"] = t.pop("postprocess_s") + time.perf_counter() - t0
     t0 = time.perf_counter()
     cfg = risk_cfg or RiskConfig()
-    model = RiskModel(panel, cfg, ctx=ctx if dist_on else None).run()
+    from ..parallel import dist as pdist
+    # one process: an explicit single-rank context (a torchrun job's rank may also run a
+    # whole-panel pipeline of its own, e.g. tools/pipeline_dist.py's comparison)
+    model = RiskModel(panel, cfg, ctx=ctx if dist_on else pdist.DistContext(device=eng.device)).run()
     if sync and eng.device.type == "cuda":
         torch.cuda.synchronize(eng.device)
     t["risk_model_s"] = time.perf_counter() - t0
