@@ -233,13 +233,14 @@ __global__ __launch_bounds__(64) void mc_cov_reduce_kernel(int K, int T, int C,
   mc_cov_finish(acc, colsum, K, T, Cz + (size_t)mi * K * K);
 }
 
-// time chunks per sim: ~2048 waves in flight, at least 2 time blocks per wave
-inline int mc_cov_chunks(int M, int T) {
+// time chunks per sim: a function of T ONLY (at most 8 chunks of >= 2 64-row blocks), so the
+// partial sums of a sim are added in the same order whatever the number of sims in the launch:
+// any partition of the sims over chunks / ranks (eigen_chunk, the short last chunk, world size)
+// reproduces one unsplit call bit for bit.  (Sizing C by M -- ~2048 waves per launch -- gave a
+// 256-sim launch 8 chunks but a 16-sim tail 20 at T = 2520.)  M is unused.
+inline int mc_cov_chunks(int /*M*/, int T) {
   const int nblk = (T + 63) / 64;
-  int C = (2048 + M - 1) / M;
-  const int cmax = nblk / 2 > 1 ? nblk / 2 : 1;
-  C = C < 1 ? 1 : (C > cmax ? cmax : C);
-  const int per = (nblk + C - 1) / C;
+  const int per = max(2, (nblk + 7) / 8);
   return (nblk + per - 1) / per;  // no empty trailing chunk
 }
 
@@ -1863,8 +1864,8 @@ MFA_API size_t mfa_mc_cov_ws_doubles(int M, int T) {
   return C > 1 ? (size_t)M * C * kCovPart : 0;
 }
 
-// As mfa_mc_cov_range with the time axis split over ~2048 waves (partials in `ws`, summed in
-// chunk order by a second launch).
+// As mfa_mc_cov_range with the time axis split into mc_cov_chunks(T) chunks (partials in `ws`,
+// summed in chunk order by a second launch).
 MFA_API int mfa_mc_cov_range_ws(int M, int m0, int K, int T, unsigned long long seed, double* ws,
                                 double* Cz, void* stream) {
   if (M <= 0) return 0;

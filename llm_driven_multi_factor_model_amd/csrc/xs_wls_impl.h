@@ -2141,12 +2141,15 @@ __device__ int jacobi_pinv_block(const double* md, double* ws, int P, int pivot_
   lmax = wave_max(lmax);
   const double cut = 1e-15 * lmax;
   // c_k = (v_k . rhs) / lambda_k over the kept spectrum
+  double ncut = 0.0;
   for (int k = lane; k < Kr; k += 64) {
     const double lk = A[k * lda + k];
     double t = 0.0;
     for (int i = 0; i < Kr; ++i) t = fma(V[i * lda + k], rhs[i], t);
     g[k] = fabs(lk) > cut ? t / lk : 0.0;
+    ncut += fabs(lk) > cut ? 0.0 : 1.0;
   }
+  ncut = wave_sum(ncut);
   wsync();
   for (int i = lane; i < Kr; i += 64) {  // g <- V c
     double t = 0.0;
@@ -2172,7 +2175,8 @@ __device__ int jacobi_pinv_block(const double* md, double* ws, int P, int pivot_
     co[Q] = cst;
   }
   wsync();
-  return XS_REFINED;
+  // same status semantics as the structured pinv (K > 64): ZERO_PIVOT iff a direction was cut
+  return ncut > 0.0 ? XS_REFINED | XS_ZERO_PIVOT : XS_REFINED;
 }
 
 template <int Q>

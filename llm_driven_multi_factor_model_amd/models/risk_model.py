@@ -303,12 +303,20 @@ class RiskModel:
         t + predlen < T.  Collective: each rank forms the z-scores of its own dates (the
         realised returns of later dates come from the gathered factor-return series), the z rows
         are all-gathered in calendar order and the std runs over all of them, so the result is
-        the same on every rank and for every world size."""
+        the same on every rank and for every world size.  After :meth:`resume` only dates
+        computed in this run have covariances: dates before the checkpoint's end are skipped
+        with a RuntimeWarning."""
         cov = {"nw": self.nw_cov, "eigen": self.eigen_cov, "vra": self.vra_cov}[which]
         if cov is None:
             raise RuntimeError(f"covariance series {which!r} not computed yet")
         F = self._gather_f()                     # [T, K] with history first
         T, lo, D = self.T, self.t_lo, self.panel.D
+        if self.T_hist > start and self.ctx.rank == 0:
+            # a checkpoint keeps no covariance series: resumed runs cover their own dates only
+            import warnings
+            warnings.warn(f"eigenfactor_bias: dates [{start}, {self.T_hist}) precede this resumed "
+                          f"run (no stored covariances); the statistic covers dates >= "
+                          f"{self.T_hist} only", RuntimeWarning, stacklevel=2)
         a, b = max(start, lo), min(lo + D, T - predlen)
         z = torch.empty(0, self.K, dtype=torch.float64, device=self.device)
         if b > a:

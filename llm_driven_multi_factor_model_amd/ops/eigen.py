@@ -133,7 +133,8 @@ def mc_cov(M: int, K: int, T: int, seed: int = 1, device="cuda", m0: int = 0) ->
             Cz[i] = torch.cov(z.T)
         return Cz
     Cz = torch.empty(M, K, K, dtype=torch.float64, device=dev)
-    # the time axis is split over ~2048 waves (partial sums added in chunk order)
+    # the time axis is split into chunks that depend on T only (partials added in chunk order),
+    # so a sim's covariance is bitwise the same in any launch that contains it
     nws = _native.query("mfa_mc_cov_ws_doubles", M, T)
     ws = torch.empty(max(1, nws), dtype=torch.float64, device=dev)
     _native.call("mfa_mc_cov_range_ws", M, int(m0), K, T, int(seed) & 0xFFFFFFFFFFFFFFFF,

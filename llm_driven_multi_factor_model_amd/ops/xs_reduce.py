@@ -184,6 +184,8 @@ def _bayes_ref(v, c, G, q):
     for d in range(D):
         vd, cd = v[d].double().numpy(), c[d].double().numpy()
         ok = np.isfinite(vd) & np.isfinite(cd)
+        if not ok.any():  # no (vol, cap) pair on this date (e.g. an all-NaN halo date): NaN row
+            continue
         cs = cd[ok]
         edges = np.quantile(cs, np.linspace(0, 1, G + 1))
         g = np.zeros(len(cs), dtype=np.int64)

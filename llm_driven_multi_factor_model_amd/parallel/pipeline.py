@@ -67,7 +67,10 @@ def streamed_xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: 
             r2=torch.empty(chunk, dtype=torch.float64, device=device),
             stats=torch.empty(chunk, Q + 2, dtype=torch.float64, device=device),
             status=torch.empty(chunk, dtype=torch.int32, device=device)))
-        ws.append(xs_wls_workspace(chunk, P, Q, device, N))
+        # the kernel's workspace is not monotone in D (auto stock chunking picks more chunks
+        # per date for fewer dates), so size the slot for every chunk length it will see
+        lens = {chunk} | ({D % chunk} if D % chunk else set())
+        ws.append(max((xs_wls_workspace(n, P, Q, device, N) for n in lens), key=lambda t: t.numel()))
 
     s_h2d, s_cmp, s_d2h = (torch.cuda.Stream(device) for _ in range(3))
     loaded = [torch.cuda.Event() for _ in range(nslot)]

@@ -45,6 +45,21 @@ def test_resume_equals_full_run(tmp_path, oos, scan):
     torch.testing.assert_close(st2["factor_ret"], full._gather_f(), rtol=0, atol=0)
 
 
+def test_resumed_bias_stat_warns_about_skipped_dates():
+    """a resumed run has no covariances for checkpointed dates, so a bias statistic
+    asked from an earlier start covers only the new dates -- and says so."""
+    p = synthetic_panel(30, 48, P=3, Q=2, seed=9)
+    T1 = 20
+    st = RiskModel(p.slice_dates(0, T1), _cfg()).run().state_dict()
+    rest = p.slice_dates(T1, p.D)
+    rest = type(rest)(**{**rest.__dict__, "date_offset": 0})
+    m2 = RiskModel.resume(st, rest).run()
+    with pytest.warns(RuntimeWarning, match="precede this resumed run"):
+        a = m2.eigenfactor_bias("nw", start=5, predlen=2)
+    b = m2.eigenfactor_bias("nw", start=T1, predlen=2)  # no warning: same dates
+    torch.testing.assert_close(a, b, rtol=0, atol=0, equal_nan=True)
+
+
 def test_resume_execution_settings_may_change(tmp_path):
     """time_scan / deterministic / eigen sharding choose HOW, not WHAT: a run saved with one
     mode resumes under another."""

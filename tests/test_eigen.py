@@ -169,11 +169,18 @@ def test_hip_mc_cov_is_fp64_cov_of_its_philox_draws(cuda):
 
 
 @pytest.mark.gpu
-def test_hip_mc_cov_range_is_a_slice(cuda):
-    full = eigen.mc_cov(12, 42, 300, seed=5, device=cuda)
-    parts = torch.cat([eigen.mc_cov(5, 42, 300, seed=5, device=cuda),
-                       eigen.mc_cov(7, 42, 300, seed=5, device=cuda, m0=5)])
-    assert torch.equal(full, parts)
+@pytest.mark.parametrize("T,splits", [(300, (5, 7)), (2520, (256, 16)), (2520, (1, 100, 171))])
+def test_hip_mc_cov_range_is_a_slice(cuda, T, splits):
+    """Any partition of the sims over launches (eigen_chunk, the short last chunk, world size)
+    draws the covariances of one unsplit call bit for bit: the time-axis chunking depends on T
+    only (at T = 2520 a 256-sim and a 16-sim launch used to sum in different orders)."""
+    M = sum(splits)
+    full = eigen.mc_cov(M, 42, T, seed=5, device=cuda)
+    parts, m0 = [], 0
+    for s in splits:
+        parts.append(eigen.mc_cov(s, 42, T, seed=5, device=cuda, m0=m0))
+        m0 += s
+    assert torch.equal(full, torch.cat(parts))
 
 
 @pytest.mark.gpu

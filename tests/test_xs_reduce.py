@@ -92,3 +92,24 @@ def test_hip_reductions_match_cpu(cuda):
     cap2 = torch.exp(torch.randn(4, 3000))
     torch.testing.assert_close(R.bayes_shrink(vol.to(cuda), cap2.to(cuda)).cpu(),
                                R.bayes_shrink(vol, cap2), rtol=1e-5, atol=1e-6)
+
+
+def test_bayes_shrink_all_nan_date_cpu():
+    """A date without any finite (vol, cap) pair (the first date of a resumed panel: its
+    trailing-vol halo is all NaN) stays a NaN row instead of failing np.quantile."""
+    vol = torch.rand(3, 200) * 0.05 + 0.01
+    cap = torch.exp(torch.randn(3, 200))
+    vol[0] = float("nan")
+    out, g = R.bayes_shrink(vol, cap, 10, 1.0, return_groups=True)
+    assert torch.isnan(out[0]).all() and (g[0] == -1).all()
+    torch.testing.assert_close(out[1:], R.bayes_shrink(vol[1:], cap[1:], 10, 1.0))
+
+
+@pytest.mark.gpu
+def test_hip_bayes_shrink_all_nan_date(cuda):
+    vol = torch.rand(3, 500) * 0.05 + 0.01
+    cap = torch.exp(torch.randn(3, 500))
+    vol[0] = float("nan")
+    got = R.bayes_shrink(vol.to(cuda), cap.to(cuda)).cpu()
+    assert torch.isnan(got[0]).all()
+    torch.testing.assert_close(got[1:], R.bayes_shrink(vol, cap)[1:], rtol=1e-5, atol=1e-6)
