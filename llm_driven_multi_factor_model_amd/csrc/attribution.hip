@@ -9,70 +9,82 @@
 // non-finite inputs (the regression's validity rule) contribute nothing.
 //
 // One 256-thread workgroup per date: fp64 register accumulators for the Q + 1 dense sums, LDS
-// atomics for the (<= 128) industry sums, a fixed-order workgroup reduction.
+// atomics for the industry sums (dynamic LDS), a fixed-order workgroup reduction; style sets
+// wider than 16 run in blocks of 16 styles.
 #include "common.h"
 
 namespace {
 
 using namespace mfa;
 
-template <int Q, typename T>
+// QB styles per launch (template), starting at style q0 of Q; the validity rule still checks all
+// Q styles.  The launch with q0 == 0 also writes the country and industry exposures.  Industry
+// sums live in dynamic LDS (P doubles), so any P fits (64 K industries = 512 KB would not; the
+// host caps P at 8192).
+template <int QB, typename T>
 __global__ __launch_bounds__(256) void portfolio_exposure_kernel(
     const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
     const int16_t* __restrict__ ind, const double* __restrict__ h, const double* __restrict__ stats,
-    int N, int P, int K, double* __restrict__ out) {
-  __shared__ double segs[128];
-  __shared__ double red[4][Q + 1];
+    int N, int P, int Q, int q0, int K, double* __restrict__ out) {
+  extern __shared__ double segs[];
+  __shared__ double red[4][QB + 1];
   const int d = blockIdx.x, tid = threadIdx.x;
   const int Pseg = P > 0 ? P : 1;
-  for (int j = tid; j < 128; j += blockDim.x) segs[j] = 0.0;
+  const bool lead = q0 == 0;
+  if (lead)
+    for (int j = tid; j < Pseg; j += blockDim.x) segs[j] = 0.0;
   __syncthreads();
   const T* Xd = X + (size_t)d * Q * N;
   const T* cd = cap + (size_t)d * N;
   const T* rd = ret + (size_t)d * N;
   const int16_t* id = ind ? ind + (size_t)d * N : nullptr;
   const double* hd = h + (size_t)d * N;
-  double acc[Q + 1];
+  double acc[QB + 1];
 #pragma unroll
-  for (int q = 0; q <= Q; ++q) acc[q] = 0.0;
+  for (int q = 0; q <= QB; ++q) acc[q] = 0.0;
   for (int n = tid; n < N; n += blockDim.x) {
     const T c = cd[n], r = rd[n];
     const int j = id ? (int)id[n] : 0;
     const double w = hd[n];
     bool ok = (j >= 0) && (j < Pseg) && __builtin_isfinite(c) && (c >= T(0)) &&
               __builtin_isfinite(r) && __builtin_isfinite(w);
-    T xf[Q];
+    T xf[QB];
 #pragma unroll
-    for (int q = 0; q < Q; ++q) {
-      xf[q] = Xd[(size_t)q * N + n];
+    for (int q = 0; q < QB; ++q) {
+      xf[q] = q0 + q < Q ? Xd[(size_t)(q0 + q) * N + n] : T(0);
       ok = ok && __builtin_isfinite(xf[q]);
     }
+    if (Q > QB)  // styles outside this launch's block still decide validity
+      for (int q = 0; q < Q; ++q)
+        if (q < q0 || q >= q0 + QB) ok = ok && __builtin_isfinite(Xd[(size_t)q * N + n]);
     if (!ok || w == 0.0) continue;
-    acc[Q] += w;
+    acc[QB] += w;
 #pragma unroll
-    for (int q = 0; q < Q; ++q) acc[q] = fma(w, (double)xf[q], acc[q]);
-    if (P > 0) atomicAdd(&segs[j], w);
+    for (int q = 0; q < QB; ++q) acc[q] = fma(w, (double)xf[q], acc[q]);
+    if (P > 0 && lead) atomicAdd(&segs[j], w);
   }
   const int lane = tid & 63, wid = tid >> 6;
 #pragma unroll
-  for (int q = 0; q <= Q; ++q) {
+  for (int q = 0; q <= QB; ++q) {
     const double v = wave_sum(acc[q]);
     if (lane == 0) red[wid][q] = v;
   }
   __syncthreads();
   double* o = out + (size_t)d * K;
   const double* st = stats + (size_t)d * (Q + 2);
-  if (tid <= Q) {
+  if (tid <= QB) {
     double s = 0.0;
     for (int w = 0; w < (int)(blockDim.x >> 6); ++w) s += red[w][tid];
     red[0][tid] = s;  // each entry is read back only by its own thread below
   }
   __syncthreads();
-  const double hs = red[0][Q];
+  const double hs = red[0][QB];
   const double isig = 1.0 / st[Q];
-  if (tid == 0) o[0] = hs;
-  for (int j = tid; j < P; j += blockDim.x) o[1 + j] = segs[j];
-  if (tid < Q) o[1 + P + tid] = (red[0][tid] - st[tid] * hs) * isig;
+  if (lead) {
+    if (tid == 0) o[0] = hs;
+    for (int j = tid; j < P; j += blockDim.x) o[1 + j] = segs[j];
+  }
+  if (tid < QB && q0 + tid < Q) o[1 + P + q0 + tid] = (red[0][tid] - st[q0 + tid] * hs) * isig;
 }
 
 template <typename T>
@@ -80,14 +92,22 @@ int portfolio_exposure_dispatch(const T* X, const T* cap, const T* ret, const in
                                 const double* h, const double* stats, int D, int N, int P, int Q,
                                 double* out, void* stream) {
   if (D <= 0) return 0;
-  if (Q < 1 || Q > 16 || P < 0 || P > 128 || N <= 0) return (int)hipErrorInvalidValue;
+  if (Q < 1 || P < 0 || P > 8192 || N <= 0) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   const int K = 1 + P + Q;
+  const size_t lds = (size_t)(P > 0 ? P : 1) * sizeof(double);
+  if (Q > 16) {  // wide style sets: blocks of 16 styles, one launch each (the first adds the
+                 // country / industry sums)
+    for (int q0 = 0; q0 < Q; q0 += 16)
+      hipLaunchKernelGGL((portfolio_exposure_kernel<16, T>), dim3(D), dim3(256), lds, s, X, cap,
+                         ret, P > 0 ? ind : nullptr, h, stats, N, P, Q, q0, K, out);
+    return (int)hipGetLastError();
+  }
   switch (Q) {
 #define MFA_Q(qq)                                                                              \
   case qq:                                                                                     \
-    hipLaunchKernelGGL((portfolio_exposure_kernel<qq, T>), dim3(D), dim3(256), 0, s, X, cap,   \
-                       ret, P > 0 ? ind : nullptr, h, stats, N, P, K, out);                    \
+    hipLaunchKernelGGL((portfolio_exposure_kernel<qq, T>), dim3(D), dim3(256), lds, s, X, cap, \
+                       ret, P > 0 ? ind : nullptr, h, stats, N, P, Q, 0, K, out);              \
     break;
     MFA_Q(1) MFA_Q(2) MFA_Q(3) MFA_Q(4) MFA_Q(5) MFA_Q(6) MFA_Q(7) MFA_Q(8)
     MFA_Q(9) MFA_Q(10) MFA_Q(11) MFA_Q(12) MFA_Q(13) MFA_Q(14) MFA_Q(15) MFA_Q(16)

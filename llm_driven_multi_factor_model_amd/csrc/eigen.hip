@@ -233,6 +233,31 @@ __global__ __launch_bounds__(64) void mc_cov_reduce_kernel(int K, int T, int C,
   mc_cov_finish(acc, colsum, K, T, Cz + (size_t)mi * K * K);
 }
 
+// Wide factor sets (K > 64): the standard normals of sims [m0, m0 + M) as Z [M][T][Kp]
+// (Kp = K rounded up to even, the padding column is a real draw the caller ignores), keyed
+// exactly like mc_cov_kernel (Philox counter {sim, time row, factor pair, tag}, one Box-Muller
+// pair per counter), so factor k < 64 of a sim draws the same numbers at any K.  The covariance
+// is then one batched fp64 GEMM (rocBLAS) on the caller's side: the draw is the only custom step.
+// One thread per (sim, row, factor pair): consecutive threads write consecutive 16-B pairs.
+__global__ __launch_bounds__(256) void philox_normals_kernel(int M, int m0, int T, int Kp,
+                                                             unsigned long long seed,
+                                                             double* __restrict__ Z) {
+  const int npair = Kp >> 1;
+  const size_t n = (size_t)M * T * npair;
+  for (size_t e = (size_t)blockIdx.x * blockDim.x + threadIdx.x; e < n;
+       e += (size_t)gridDim.x * blockDim.x) {
+    const int pr = (int)(e % npair);
+    const size_t mt = e / npair;
+    const int tq = (int)(mt % T), mi = (int)(mt / T);
+    const U4 u = philox(U4{(unsigned)(m0 + mi), (unsigned)tq, (unsigned)pr, 0x4D464131u},
+                        (unsigned)seed, (unsigned)(seed >> 32));
+    const double rr = sqrt(-2.0 * log(u01_53(u.x, u.y)));
+    double sn, cn;
+    sincospi(2.0 * u01_53(u.z, u.w), &sn, &cn);
+    *(double2*)(Z + mt * Kp + 2 * pr) = double2{rr * cn, rr * sn};
+  }
+}
+
 // time chunks per sim: a function of T ONLY (at most 8 chunks of >= 2 64-row blocks), so the
 // partial sums of a sim are added in the same order whatever the number of sims in the launch:
 // any partition of the sims over chunks / ranks (eigen_chunk, the short last chunk, world size)
@@ -1855,6 +1880,20 @@ MFA_API int mfa_mc_cov_range(int M, int m0, int K, int T, unsigned long long see
   if (K < 1 || K > 64 || T < 2 || m0 < 0) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(mc_cov_kernel, dim3(M), dim3(64), 0, (hipStream_t)stream, K, T, seed, m0, 1,
                      Cz, (double*)nullptr);
+  return (int)hipGetLastError();
+}
+
+// Normals of sims [m0, m0 + M) for any K (Z: [M][T][K + (K & 1)] doubles); see
+// philox_normals_kernel.
+MFA_API int mfa_philox_normals(int M, int m0, int K, int T, unsigned long long seed, double* Z,
+                               void* stream) {
+  if (M <= 0) return 0;
+  if (K < 1 || T < 1 || m0 < 0) return (int)hipErrorInvalidValue;
+  const int Kp = K + (K & 1);
+  const size_t n = (size_t)M * T * (Kp >> 1);
+  const int blocks = (int)((n + 255) / 256 < 65536 ? (n + 255) / 256 : 65536);
+  hipLaunchKernelGGL(philox_normals_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, M,
+                     m0, T, Kp, seed, Z);
   return (int)hipGetLastError();
 }
 

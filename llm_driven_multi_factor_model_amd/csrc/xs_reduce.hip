@@ -213,37 +213,44 @@ __global__ __launch_bounds__(256) void style_norm_kernel(float* __restrict__ X, 
 // groups: pd.qcut(cap, G).codes (linear-interpolated quantile edges, right-closed bins, the
 // first bin includes the minimum); per group m = sum(vol*cap)/sum(cap), s = sqrt(mean((vol-m)^2));
 // out = v*m + (1-v)*|vol| with v = q|vol-m| / (q|vol-m| + s).
+// presorted != nullptr (wide universes, N > kBayesLdsN): the caller sorted each date's masked
+// caps (+inf = invalid) on the device and the edges are read from there instead of the LDS sort.
 __global__ __launch_bounds__(1024) void bayes_shrink_kernel(const float* __restrict__ vol,
                                                             const float* __restrict__ cap, int N,
                                                             int G, double qq, float* __restrict__ out,
-                                                            int* __restrict__ group_out) {
-  extern __shared__ float keys[];  // [NP] sorted caps
+                                                            int* __restrict__ group_out,
+                                                            const float* __restrict__ presorted) {
+  extern __shared__ float lkeys[];  // [NP] sorted caps
   __shared__ double gs[64][4];
   const int d = blockIdx.x, tid = threadIdx.x, nt = blockDim.x;
   const float* vd = vol + (size_t)d * N;
   const float* cd = cap + (size_t)d * N;
-  int NP = 1;
-  while (NP < N) NP <<= 1;
+  const float* keys = presorted ? presorted + (size_t)d * N : lkeys;
   int nvalid = 0;
-  for (int i = tid; i < NP; i += nt) {
-    const bool ok = i < N && fin(cd[i]) && fin(vd[i]);
-    keys[i] = ok ? cd[i] : __builtin_inff();
-  }
   for (int g = tid; g < G * 4; g += nt) gs[g / 4][g % 4] = 0.0;
-  __syncthreads();
-  // bitonic sort ascending
-  for (int k = 2; k <= NP; k <<= 1)
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < NP; i += nt) {
-        const int ij = i ^ j;
-        if (ij > i) {
-          const bool up = (i & k) == 0;
-          const float a = keys[i], b = keys[ij];
-          if ((a > b) == up) { keys[i] = b; keys[ij] = a; }
-        }
-      }
-      __syncthreads();
+  if (!presorted) {
+    int NP = 1;
+    while (NP < N) NP <<= 1;
+    for (int i = tid; i < NP; i += nt) {
+      const bool ok = i < N && fin(cd[i]) && fin(vd[i]);
+      lkeys[i] = ok ? cd[i] : __builtin_inff();
     }
+    __syncthreads();
+    // bitonic sort ascending
+    for (int k = 2; k <= NP; k <<= 1)
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = tid; i < NP; i += nt) {
+          const int ij = i ^ j;
+          if (ij > i) {
+            const bool up = (i & k) == 0;
+            const float a = lkeys[i], b = lkeys[ij];
+            if ((a > b) == up) { lkeys[i] = b; lkeys[ij] = a; }
+          }
+        }
+        __syncthreads();
+      }
+  }
+  __syncthreads();
   {
     int c = 0;
     for (int i = tid; i < N; i += nt) c += fin(keys[i]) ? 1 : 0;
@@ -353,6 +360,18 @@ MFA_API int mfa_bayes_shrink(const float* vol, const float* cap, int D, int N, i
   int NP = 1;
   while (NP < N) NP <<= 1;
   hipLaunchKernelGGL(bayes_shrink_kernel, dim3(D), dim3(1024), NP * sizeof(float), (hipStream_t)stream,
-                     vol, cap, N, G, q, out, groups);
+                     vol, cap, N, G, q, out, groups, (const float*)nullptr);
+  return (int)hipGetLastError();
+}
+
+// Any N: `sorted` [D][N] = each date's caps with invalid (vol, cap) pairs set to +inf, sorted
+// ascending (the caller's device sort); the kernel takes the decile edges from it.
+MFA_API int mfa_bayes_shrink_presorted(const float* vol, const float* cap, const float* sorted,
+                                       int D, int N, int G, double q, float* out, int* groups,
+                                       void* stream) {
+  if (D <= 0) return 0;
+  if (N <= 0 || G < 1 || G > 64 || sorted == nullptr) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(bayes_shrink_kernel, dim3(D), dim3(1024), 0, (hipStream_t)stream, vol, cap,
+                     N, G, q, out, groups, sorted);
   return (int)hipGetLastError();
 }

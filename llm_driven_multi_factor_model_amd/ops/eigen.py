@@ -38,12 +38,20 @@ _native.register("mfa_mc_cov_range_ws", [C.c_int, C.c_int, C.c_int, C.c_int, C.c
 _native.register("mfa_eigen_bias_accumulate", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                                 C.c_void_p, C.c_int, C.c_double, C.c_void_p,
                                                 C.c_void_p, C.c_void_p])
+_native.register("mfa_philox_normals", [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_void_p,
+                                         C.c_void_p])
 _native.register("mfa_eigen_finalize_sum", [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                              C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p,
                                              C.c_void_p, C.c_void_p])
 
 MAX_SWEEPS = 30
 TOL = 1e-15
+# Factor sets wider than one wave (K > 64, e.g. SW-L2 industries: K = 140) leave the
+# register-resident one-wave kernels: the draws are the same Philox stream (factor k < 64 of a
+# sim is the same number at any K) with the covariance as one batched rocBLAS GEMM, and the
+# eigen-decompositions go through rocSOLVER's batched symmetric solver in bounded chunks.
+WIDE_K = 64
+WIDE_CHUNK_DOUBLES = 1 << 27     # ~1 GB of fp64 per batched eigh / draw chunk
 
 # Per-(date, sim) solver of the bias statistic (csrc/eigen.hip): "jacobi" = pair-block
 # tournament Jacobi carrying M = V^T D0 V; "tridiag" = Householder tridiagonalisation,
@@ -82,7 +90,7 @@ def using_bias_solver(name: str):
 def eigh(A: torch.Tensor, max_sweeps: int = MAX_SWEEPS, tol: float = TOL):
     """Batched symmetric eigendecomposition, eigenvalues DESCENDING.
 
-    ``A`` [..., K, K] float64 (K <= 64 on the GPU).  Returns ``(w [..., K], U [..., K, K])``
+    ``A`` [..., K, K] float64 (any K; K > 64 on the GPU goes through :func:`_eigh_wide`).  Returns ``(w [..., K], U [..., K, K])``
     with ``A = U diag(w) U^T`` and ``U[..., :, k]`` the k-th eigenvector.  Non-finite input
     matrices give NaN outputs.
     """
@@ -92,6 +100,8 @@ def eigh(A: torch.Tensor, max_sweeps: int = MAX_SWEEPS, tol: float = TOL):
     Ab = A.reshape(-1, K, K).contiguous()
     if not A.is_cuda:
         return _eigh_reference(Ab, shp)
+    if K > WIDE_K:
+        return _eigh_wide(Ab, shp)
     B = Ab.shape[0]
     w = torch.empty(B, K, dtype=torch.float64, device=A.device)
     U = torch.empty(B, K, K, dtype=torch.float64, device=A.device)
@@ -100,6 +110,24 @@ def eigh(A: torch.Tensor, max_sweeps: int = MAX_SWEEPS, tol: float = TOL):
     flags = torch.empty(B, dtype=torch.int32, device=A.device)
     _native.call("mfa_eigh_batched", _native.ptr(Ab), B, K, max_sweeps, tol, _native.ptr(w),
                  _native.ptr(U), _native.ptr(flags), _native.stream(A.device))
+    return w.reshape(shp[:-1]), U.reshape(shp)
+
+
+def _eigh_wide(Ab, shp):
+    """K > 64 on the device: rocSOLVER batched eigh of the finite (symmetrised) matrices, in
+    chunks of ~WIDE_CHUNK_DOUBLES; NaN for non-finite inputs.  Eigenvalues descending."""
+    B, K = Ab.shape[0], Ab.shape[-1]
+    w = torch.full((B, K), float("nan"), dtype=torch.float64, device=Ab.device)
+    U = torch.full((B, K, K), float("nan"), dtype=torch.float64, device=Ab.device)
+    ok = torch.isfinite(Ab).all(-1).all(-1)
+    idx = torch.nonzero(ok).flatten()
+    step = max(1, WIDE_CHUNK_DOUBLES // (K * K))
+    for a in range(0, idx.numel(), step):
+        sel = idx[a:a + step]
+        S = Ab[sel]
+        ww, UU = torch.linalg.eigh(0.5 * (S + S.transpose(-1, -2)))
+        w[sel] = ww.flip(-1)
+        U[sel] = UU.flip(-1)
     return w.reshape(shp[:-1]), U.reshape(shp)
 
 
@@ -132,6 +160,8 @@ def mc_cov(M: int, K: int, T: int, seed: int = 1, device="cuda", m0: int = 0) ->
             z = torch.randn(T, K, generator=g, dtype=torch.float64)
             Cz[i] = torch.cov(z.T)
         return Cz
+    if K > WIDE_K:
+        return _mc_cov_wide(M, K, T, seed, dev, m0)
     Cz = torch.empty(M, K, K, dtype=torch.float64, device=dev)
     # the time axis is split into chunks that depend on T only (partials added in chunk order),
     # so a sim's covariance is bitwise the same in any launch that contains it
@@ -140,6 +170,63 @@ def mc_cov(M: int, K: int, T: int, seed: int = 1, device="cuda", m0: int = 0) ->
     _native.call("mfa_mc_cov_range_ws", M, int(m0), K, T, int(seed) & 0xFFFFFFFFFFFFFFFF,
                  _native.ptr(ws), _native.ptr(Cz), _native.stream(dev))
     return Cz
+
+
+def _mc_cov_wide(M: int, K: int, T: int, seed: int, dev, m0: int) -> torch.Tensor:
+    """K > 64: Philox normals Z [sims, T, K] (HIP kernel, same stream keys as the one-wave
+    draw kernel), then cov = (Z^T Z - s s^T / T) / (T - 1) with s the column sums: one batched
+    fp64 GEMM per chunk of sims (rocBLAS).  Each sim's covariance depends on that sim only, so
+    any partition of the sims gives the same matrices."""
+    Kp = K + (K & 1)
+    Cz = torch.empty(M, K, K, dtype=torch.float64, device=dev)
+    step = max(1, WIDE_CHUNK_DOUBLES // (T * Kp))
+    for a in range(0, M, step):
+        mc = min(step, M - a)
+        Z = torch.empty(mc, T, Kp, dtype=torch.float64, device=dev)
+        _native.call("mfa_philox_normals", mc, int(m0 + a), K, T, int(seed) & 0xFFFFFFFFFFFFFFFF,
+                     _native.ptr(Z), _native.stream(dev))
+        Zk = Z[:, :, :K]
+        cs = Zk.sum(1)
+        G = torch.bmm(Zk.transpose(1, 2), Zk)
+        Cz[a:a + mc] = (G - cs[:, :, None] * cs[:, None, :] / T) / (T - 1)
+    return Cz
+
+
+def _bias_sum_wide(w, valid, Cz):
+    """K > 64 on the device: S[d, k] = sum_m v_m[d, k] with v_m = diag(V^T D0 V) / lambda of
+    A = sqrt(D0) C_z sqrt(D0) (the identity of SURVEY.md §2.3.4), eigen-decomposed by rocSOLVER
+    in chunks of (dates x sims); invalid dates give NaN."""
+    D, K = w.shape
+    M = Cz.shape[0]
+    dev = w.device
+    S = torch.zeros(D, K, dtype=torch.float64, device=dev)
+    dd = torch.nonzero(valid).flatten()
+    sq = torch.sqrt(w.clamp_min(0.0))
+    nm = max(1, min(M, WIDE_CHUNK_DOUBLES // (K * K)))
+    nd = max(1, WIDE_CHUNK_DOUBLES // (nm * K * K))
+    for a in range(0, dd.numel(), nd):
+        ds = dd[a:a + nd]
+        s = sq[ds]                                                     # [nd, K]
+        acc = torch.zeros(ds.numel(), K, dtype=torch.float64, device=dev)
+        for b in range(0, M, nm):
+            cz = Cz[b:b + nm]
+            A = s[:, None, :, None] * cz[None] * s[:, None, None, :]   # [nd, nm, K, K]
+            lam, V = torch.linalg.eigh(A.reshape(-1, K, K))
+            lam, V = lam.flip(-1), V.flip(-1)
+            wv = w[ds][:, None, :, None].expand(-1, cz.shape[0], -1, -1).reshape(-1, K, 1)
+            v = ((V * V) * wv).sum(1) / lam                            # [nd * nm, K]
+            acc += v.view(ds.numel(), cz.shape[0], K).sum(1)
+        S[ds] = acc
+    S[~valid] = float("nan")
+    return S
+
+
+def _finalize_torch(S, M, w, U, valid, scale_coef):
+    v = scale_coef * (torch.sqrt(S / M) - 1.0) + 1.0
+    vb = torch.where(valid[:, None], v, torch.full_like(v, float("nan")))
+    Fh = (U * (vb * vb * w)[:, None, :]) @ U.transpose(-1, -2)
+    Fh[~valid] = float("nan")
+    return Fh, vb
 
 
 def sim_shard(M: int, rank: int, world: int) -> tuple[int, int]:
@@ -173,7 +260,12 @@ def eigen_risk_adjust_sharded(F0: torch.Tensor, *, M: int = 10_000, scale_coef: 
     rank, world = (ctx.rank, ctx.world) if ctx.enabled else (0, 1)
     m0, m1 = sim_shard(M, rank, world)
     S = torch.zeros(D, K, dtype=torch.float64, device=dev)
-    if dev.type == "cuda":
+    wide = dev.type == "cuda" and K > WIDE_K
+    if wide:
+        for a in range(m0, m1, chunk):
+            mc = min(chunk, m1 - a)
+            S += _bias_sum_wide(w, valid, mc_cov(mc, K, max(T_sim, 2), seed, dev, m0=a))
+    elif dev.type == "cuda":
         dv = valid.to(torch.int32).contiguous()
         ws = torch.empty(D * min(chunk, max(1, m1 - m0)) * K, dtype=torch.float64, device=dev)
         for a in range(m0, m1, chunk):
@@ -189,7 +281,9 @@ def eigen_risk_adjust_sharded(F0: torch.Tensor, *, M: int = 10_000, scale_coef: 
             S += _bias_sum_reference(w, valid, Cz)
     if ctx.enabled:
         pdist.all_reduce_sum(S, ctx)
-    if dev.type == "cuda":
+    if wide:
+        Fh, vb = _finalize_torch(S, M, w, U, valid, scale_coef)
+    elif dev.type == "cuda":
         Fh = torch.empty(D, K, K, dtype=torch.float64, device=dev)
         vb = torch.empty(D, K, dtype=torch.float64, device=dev)
         _native.call("mfa_eigen_finalize_sum", _native.ptr(S), int(M), _native.ptr(w),
@@ -239,6 +333,9 @@ def eigen_risk_adjust(F0: torch.Tensor, *, M: int = 100, scale_coef: float = 1.4
     M = Cz.shape[0]
     if dev.type != "cuda":
         return _eigen_adjust_reference(w, U, valid, Cz, scale_coef, return_bias)
+    if K > WIDE_K:
+        Fh, vb = _finalize_torch(_bias_sum_wide(w, valid, Cz), M, w, U, valid, scale_coef)
+        return (Fh, vb) if return_bias else Fh
     Fh = torch.empty(D, K, K, dtype=torch.float64, device=dev)
     vb = torch.empty(D, K, dtype=torch.float64, device=dev)
     ws = torch.empty(D * M * K, dtype=torch.float64, device=dev)

@@ -29,6 +29,9 @@ _native.register("mfa_style_norm", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.
                                      C.c_void_p, C.c_void_p])
 _native.register("mfa_bayes_shrink", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_double,
                                        C.c_void_p, C.c_void_p, C.c_void_p])
+_native.register("mfa_bayes_shrink_presorted", [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
+                                                 C.c_int, C.c_double, C.c_void_p, C.c_void_p,
+                                                 C.c_void_p])
 
 
 def _f32(t: torch.Tensor) -> torch.Tensor:
@@ -154,6 +157,9 @@ def style_norm(X: torch.Tensor, cap: torch.Tensor):
 
 
 # ------------------------------------------------------------------ Bayesian shrinkage
+BAYES_LDS_N = 16384  # universes up to this size sort their caps in LDS
+
+
 def bayes_shrink(volatility: torch.Tensor, capital: torch.Tensor, ngroup: int = 10, q: float = 1.0,
                  return_groups: bool = False):
     """Cap-decile Bayesian shrinkage of specific volatility (``utils.bayes_shrink``).
@@ -169,8 +175,16 @@ def bayes_shrink(volatility: torch.Tensor, capital: torch.Tensor, ngroup: int = 
     else:
         out = torch.empty_like(v)
         g = torch.empty(D, N, dtype=torch.int32, device=v.device)
-        _native.call("mfa_bayes_shrink", _native.ptr(v), _native.ptr(c), D, N, ngroup, float(q),
-                     _native.ptr(out), _native.ptr(g), _native.stream(v.device))
+        if N <= BAYES_LDS_N:  # bitonic sort of the caps in LDS
+            _native.call("mfa_bayes_shrink", _native.ptr(v), _native.ptr(c), D, N, ngroup,
+                         float(q), _native.ptr(out), _native.ptr(g), _native.stream(v.device))
+        else:  # wide universe: device segmented sort (rocPRIM) feeds the same kernel
+            keys = torch.where(torch.isfinite(v) & torch.isfinite(c), c,
+                               torch.full_like(c, float("inf")))
+            srt = torch.sort(keys, dim=1).values.contiguous()
+            _native.call("mfa_bayes_shrink_presorted", _native.ptr(v), _native.ptr(c),
+                         _native.ptr(srt), D, N, ngroup, float(q), _native.ptr(out),
+                         _native.ptr(g), _native.stream(v.device))
     if squeeze:
         out, g = out[0], g[0]
     return (out, g) if return_groups else out

@@ -1,0 +1,124 @@
+"""Risk model beyond one wave of factors (K > 64).
+
+SW-L2-sized factor sets (P = 123 industries, Q = 16 styles: K = 140) run every stage on the
+device: the CS-WLS regression (structured device pinv), the Newey-West scan, the eigen adjustment
+(Philox draws + rocBLAS GEMM covariances, rocSOLVER batched eigen-decompositions), VRA, the
+eigenfactor bias statistic, and the attribution kernels (portfolio exposures for any P / Q,
+cap-decile shrinkage for any N).  Each is compared with the CPU fp64 path on shared draws.
+"""
+import numpy as np
+import pytest
+import torch
+
+from llm_driven_multi_factor_model_amd.models.panel import synthetic_panel
+from llm_driven_multi_factor_model_amd.models.risk_model import RiskModel
+from llm_driven_multi_factor_model_amd.ops import attribution as A
+from llm_driven_multi_factor_model_amd.ops import eigen
+from llm_driven_multi_factor_model_amd.ops import xs_reduce as R
+from llm_driven_multi_factor_model_amd.utils.config import preset
+
+
+def _spd(B, K, seed=0, spread=3.0):
+    g = torch.Generator().manual_seed(seed)
+    Q, _ = torch.linalg.qr(torch.randn(B, K, K, generator=g, dtype=torch.float64))
+    lam = torch.exp(torch.linspace(0, -spread * 2.3, K, dtype=torch.float64))[None] * \
+        (1 + 0.1 * torch.rand(B, K, generator=g, dtype=torch.float64))
+    return (Q * lam[:, None, :]) @ Q.transpose(1, 2)
+
+
+def test_wide_eigen_adjust_cpu_runs():
+    """The CPU fp64 path (oracle) handles any K."""
+    F = _spd(3, 70, seed=1) * 1e-4
+    F[1] = float("nan")
+    Cz = eigen.mc_cov(5, 70, 120, seed=2, device="cpu")
+    Fh, v = eigen.eigen_risk_adjust(F, Cz=Cz, return_bias=True)
+    assert torch.isnan(Fh[1]).all() and torch.isfinite(Fh[[0, 2]]).all()
+
+
+@pytest.mark.gpu
+def test_hip_wide_mc_cov_same_draws(cuda):
+    """K = 140 draws: factor k < 64 of a sim is the same Philox number as in the one-wave
+    kernel (the leading block of the covariance agrees to summation order), and any partition
+    of the sims gives the same matrices."""
+    T = 600
+    wide = eigen.mc_cov(6, 140, T, seed=3, device=cuda)
+    narrow = eigen.mc_cov(6, 42, T, seed=3, device=cuda)
+    torch.testing.assert_close(wide[:, :42, :42], narrow, rtol=1e-11, atol=1e-13)
+    assert torch.allclose(wide, wide.transpose(1, 2))
+    d = torch.diagonal(wide, dim1=1, dim2=2)
+    assert abs(d.mean().item() - 1.0) < 0.02
+    parts = torch.cat([eigen.mc_cov(2, 140, T, seed=3, device=cuda),
+                       eigen.mc_cov(4, 140, T, seed=3, device=cuda, m0=2)])
+    assert torch.equal(parts, wide)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [65, 140])
+def test_hip_wide_eigh_and_adjust_match_cpu(cuda, K):
+    D, M = 6, 5
+    F = _spd(D, K, seed=K, spread=2.0) * 1e-4
+    F[2] = float("nan")
+    w, U = eigen.eigh(F.to(cuda))
+    wr = torch.linalg.eigvalsh(F[[0, 1, 3, 4, 5]]).flip(-1)
+    torch.testing.assert_close(w.cpu()[[0, 1, 3, 4, 5]], wr, rtol=1e-10, atol=1e-18)
+    assert torch.isnan(w[2]).all()
+    Cz = eigen.mc_cov(M, K, 400, seed=2, device=cuda)
+    Fg, vg = eigen.eigen_risk_adjust(F.to(cuda), Cz=Cz, return_bias=True)
+    Fc, vc = eigen.eigen_risk_adjust(F, Cz=Cz.cpu(), return_bias=True)
+    torch.testing.assert_close(vg.cpu(), vc, rtol=1e-8, atol=1e-10, equal_nan=True)
+    torch.testing.assert_close(Fg.cpu(), Fc, rtol=1e-8, atol=1e-16, equal_nan=True)
+    # sims-sharded accumulation == one shot
+    Fs, vs = eigen.eigen_risk_adjust_sharded(F.to(cuda), M=M, T_sim=400, seed=2, chunk=2,
+                                             return_bias=True)
+    torch.testing.assert_close(vs.cpu(), vc, rtol=1e-10, atol=1e-12, equal_nan=True)
+
+
+@pytest.mark.gpu
+def test_hip_risk_model_k140_matches_cpu(cuda):
+    """RiskModel.run + eigenfactor_bias at P = 123, Q = 16 (K = 140) on the GPU; every stage
+    matches the CPU fp64 path (the eigen stage on the GPU's own draw covariances)."""
+    D, N, P, Q, M = 40, 2000, 123, 16, 6
+    p = synthetic_panel(D, N, P, Q, seed=13, missing_frac=0.01, dtype=torch.float64)
+    cfg = preset("reference", eigen_sims=M, nw_half_life=30.0, vra_half_life=10.0,
+                 eigen_sim_length=300)   # T_sim > K: full-rank draw covariances
+    g = RiskModel(p.to(cuda), cfg).run()
+    assert g.K == 140
+    c = RiskModel(p, cfg)
+    c.regress()
+    c.newey_west()
+    torch.testing.assert_close(g.factor_ret.cpu(), c.factor_ret, rtol=1e-9, atol=1e-12)
+    torch.testing.assert_close(g.nw_cov.cpu(), c.nw_cov, rtol=1e-8, atol=1e-15, equal_nan=True)
+    Cz = eigen.mc_cov(M, 140, 300, seed=cfg.eigen_seed, device=cuda).cpu()
+    Fh, vb = eigen.eigen_risk_adjust(g.nw_cov.cpu(), Cz=Cz, scale_coef=cfg.eigen_scale,
+                                     return_bias=True)
+    torch.testing.assert_close(g.eigen_bias.cpu(), vb, rtol=1e-8, atol=1e-10, equal_nan=True)
+    torch.testing.assert_close(g.eigen_cov.cpu(), Fh, rtol=1e-8, atol=1e-16, equal_nan=True)
+    assert torch.isfinite(g.vra_cov[-1]).all()
+    bias = g.eigenfactor_bias("eigen", start=5, predlen=2)
+    assert bias.shape == (140,) and torch.isfinite(bias).all()
+
+
+@pytest.mark.gpu
+def test_hip_portfolio_exposure_wide(cuda):
+    """P = 150 industries (> 128) and Q = 20 styles (> 16): block launches and dynamic LDS."""
+    p = synthetic_panel(5, 1500, 150, 20, seed=3, missing_frac=0.02, dtype=torch.float64)
+    from llm_driven_multi_factor_model_amd.ops import cross_section as X
+    g = p.to(cuda)
+    res = X.xs_wls(g.styles, g.cap, g.ret, g.ind, p.P)
+    h = torch.rand(p.D, p.N, dtype=torch.float64)
+    got = A.portfolio_exposure(g.styles, g.cap, g.ret, g.ind, h.to(cuda), res.stats, p.P)
+    ref = A.portfolio_exposure(p.styles, p.cap, p.ret, p.ind, h, res.stats.cpu(), p.P)
+    torch.testing.assert_close(got.cpu(), ref, rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_hip_bayes_shrink_wide_universe(cuda):
+    """N = 20000 stocks (> the 16384 LDS sort): device sort + the same shrink kernel."""
+    g = torch.Generator().manual_seed(5)
+    vol = torch.rand(3, 20000, generator=g) * 0.05 + 0.01
+    cap = torch.exp(torch.randn(3, 20000, generator=g))
+    vol[1, ::7] = float("nan")
+    got = R.bayes_shrink(vol.to(cuda), cap.to(cuda)).cpu()
+    ref = R.bayes_shrink(vol, cap)
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6, equal_nan=True)
+    assert np.isnan(got[1, ::7].numpy()).all()
