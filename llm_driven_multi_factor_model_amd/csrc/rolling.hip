@@ -1127,6 +1127,88 @@ __global__ __launch_bounds__(kRsWaves * 64) void rstr_ew_kernel(const float* __r
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// Statement-row TTM (factor_calculator.py:392-410, quirk Q18): the rows of a stock form runs of
+// one (ts_code, end_date) statement (a point-in-time as-of join keeps end_date non-decreasing),
+// the TTM of a run is the NaN-skipping sum of the last 4 runs' values (min_periods 4), and every
+// row takes its run's TTM.  Three row-parallel kernels around one int32 prefix sum, no host sync:
+//   ttm_flags: run starts (stock change or end_date change) and two error bits (1 = end_date
+//              moved backwards inside a stock: a restatement, the caller takes the sort path;
+//              2 = one statement with two different values: the pandas path);
+//   ttm_runs:  per run its value and stock (written by the run's first row);
+//   ttm_rows:  the 4-run window of the row's run, summed newest first in fp64, rounded to fp32
+//              like the rolling-sum kernel's output, widened back to fp64.
+// Missing end dates (-1) sort last within a stock, as in the pandas path.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ long long ttm_key(long long e) { return e < 0 ? (1LL << 62) : e; }
+
+__global__ __launch_bounds__(256) void ttm_flags_kernel(const int* __restrict__ sid,
+                                                        const long long* __restrict__ end_date,
+                                                        const float* __restrict__ v, int R,
+                                                        int* __restrict__ start,
+                                                        int* __restrict__ flags) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  int st = 1, bad = 0;
+  if (r > 0) {
+    const bool same = sid[r] == sid[r - 1];
+    const long long e0 = ttm_key(end_date[r - 1]), e1 = ttm_key(end_date[r]);
+    st = !(same && e0 == e1);
+    if (same && e1 < e0) bad |= 1;
+    if (!st) {
+      const float a = v[r], b = v[r - 1];
+      if (!(a == b || (a != a && b != b))) bad |= 2;
+    }
+  }
+  start[r] = st;
+  if (bad) atomicOr(flags, bad);
+}
+
+__global__ __launch_bounds__(256) void ttm_runs_kernel(const int* __restrict__ sid,
+                                                       const float* __restrict__ v,
+                                                       const int* __restrict__ start,
+                                                       const int* __restrict__ run_incl, int R,
+                                                       float* __restrict__ vf,
+                                                       int* __restrict__ rsid) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R || !start[r]) return;
+  const int q = run_incl[r] - 1;
+  vf[q] = v[r];
+  rsid[q] = sid[r];
+}
+
+__global__ __launch_bounds__(256) void ttm_rows_kernel(const int* __restrict__ run_incl,
+                                                       const float* __restrict__ vf,
+                                                       const int* __restrict__ rsid, int R,
+                                                       double* __restrict__ out) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const int q = run_incl[r] - 1, s0 = rsid[q];
+  double s = 0.0;
+  int n = 0;
+  for (int k = q; k >= 0 && k > q - 4 && rsid[k] == s0; --k) {
+    const float x = vf[k];
+    if (fin(x)) { s += (double)x; ++n; }
+  }
+  out[r] = n >= 4 ? (double)(float)s : (double)qnanf();
+}
+
+// MLEV = (total_mv + total_ncl) / total_mv (+-inf -> NaN), BLEV = (BE + total_ncl) / BE for BE > 0,
+// in fp64 from the fp32 columns, rounded to fp32 (factor_calculator.py:464-509): one pass instead
+// of ~12 elementwise tensor launches.
+__global__ __launch_bounds__(256) void leverage_kernel(const float* __restrict__ mv,
+                                                       const float* __restrict__ ncl,
+                                                       const float* __restrict__ be, int R,
+                                                       float* __restrict__ mlev,
+                                                       float* __restrict__ blev) {
+  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= R) return;
+  const double m = mv[r], n = ncl[r], b = be[r];
+  const double ml = (m + n) / m;
+  mlev[r] = __builtin_isinf(ml) ? qnanf() : (float)ml;
+  blev[r] = b > 0.0 ? (float)((b + n) / b) : qnanf();
+}
+
 int g_roll_mode = 0;  // 0 = default (anchored-prefix / van Herk / sliding-window kernels), 1 = direct
                       // per-row kernels (A/B, tests), 2 = round-1 sliding-window BETA / DASTD /
                       // CMRA / RSTR (A/B)
@@ -1202,6 +1284,28 @@ MFA_API int mfa_rolling_sum(const float* x, const int* seg_lo, int R, int W, int
   else
     hipLaunchKernelGGL(rolling_sum_kernel, MFA_GRID(R), 0, (hipStream_t)s, x, seg_lo, R, W, minp,
                        scale, mode, out);
+  return (int)hipGetLastError();
+}
+MFA_API int mfa_ttm_flags(const int* sid, const long long* end_date, const float* v, int R,
+                          int* start, int* flags, void* s) {
+  if (R <= 0) return 0;
+  hipLaunchKernelGGL(ttm_flags_kernel, MFA_GRID(R), 0, (hipStream_t)s, sid, end_date, v, R, start,
+                     flags);
+  return (int)hipGetLastError();
+}
+// run_incl: inclusive prefix sum of `start` (the caller's device scan); vf / rsid: R scratch.
+MFA_API int mfa_ttm_finish(const int* sid, const float* v, const int* start, const int* run_incl,
+                           int R, float* vf, int* rsid, double* out, void* s) {
+  if (R <= 0) return 0;
+  hipLaunchKernelGGL(ttm_runs_kernel, MFA_GRID(R), 0, (hipStream_t)s, sid, v, start, run_incl, R,
+                     vf, rsid);
+  hipLaunchKernelGGL(ttm_rows_kernel, MFA_GRID(R), 0, (hipStream_t)s, run_incl, vf, rsid, R, out);
+  return (int)hipGetLastError();
+}
+MFA_API int mfa_leverage(const float* mv, const float* ncl, const float* be, int R, float* mlev,
+                         float* blev, void* s) {
+  if (R <= 0) return 0;
+  hipLaunchKernelGGL(leverage_kernel, MFA_GRID(R), 0, (hipStream_t)s, mv, ncl, be, R, mlev, blev);
   return (int)hipGetLastError();
 }
 MFA_API int mfa_returns(const float* close, const int* seg_lo, int R, float* ret, float* logret,

@@ -5,7 +5,10 @@
 // runtime component memory-maps the file, splits it into line-aligned chunks, and parses every
 // chunk on its own std::thread straight into caller-allocated columnar buffers:
 //   type 0 = float64 (empty / "nan" -> NaN), 1 = fixed-width string (16 bytes, NUL padded),
-//   type 2 = date -> int32 YYYYMMDD (accepts YYYY/MM/DD, YYYY-MM-DD, YYYYMMDD).
+//   type 2 = date -> int32 YYYYMMDD (accepts YYYY/MM/DD, YYYY-MM-DD, YYYYMMDD),
+//   type 3 = float32: parsed as float64, then rounded to float32 -- the reference's load-time
+//            downcast (Barra_factor_cal/load_data.py:13-25, quirk Q27), done while parsing so the
+//            device upload moves half the bytes (and, into pinned buffers, by DMA).
 // C ABI for ctypes; no Python objects are touched.
 #include <fcntl.h>
 #include <sys/mman.h>
@@ -99,6 +102,7 @@ void parse_range(const char* s, const char* e, int64_t row0, int ncol, const int
           break;
         }
         case 2: ((int32_t*)outs[c])[r] = parse_date(f, fe); break;
+        case 3: ((float*)outs[c])[r] = (float)parse_double(f, fe); break;
         default: break;
       }
       f = fe < line_end ? fe + 1 : line_end;

@@ -55,6 +55,30 @@ def _s16_keys(a: np.ndarray):
     return w[:, 0].astype(np.int64), w[:, 1].astype(np.int64)
 
 
+def _upload(x: np.ndarray, dev) -> torch.Tensor:
+    """Host array -> device tensor; asynchronous when the array lives in pinned memory (the
+    native reader's staging buffers)."""
+    t = torch.from_numpy(np.ascontiguousarray(x))
+    if dev.type != "cuda":
+        return t
+    return t.to(dev, non_blocking=t.is_pinned())
+
+
+_BE_SHIFTS = {}
+
+
+def _s16_keys_device(code_u8: torch.Tensor):
+    """(hi, lo) int64 keys of [R * 16] code bytes (NUL padded), formed on the device: each 8-byte
+    half read big-endian, so integer order is the strings' lexicographic order (ASCII keeps the
+    sign bit clear).  Same keys as :func:`_s16_keys`."""
+    b = code_u8.view(-1, 2, 8).to(torch.int64)
+    sh = _BE_SHIFTS.get(b.device)
+    if sh is None:
+        sh = _BE_SHIFTS[b.device] = torch.arange(56, -8, -8, dtype=torch.int64, device=b.device)
+    k = (b << sh).sum(-1)            # disjoint byte fields: the sum is the bitwise OR
+    return k[:, 0].contiguous(), k[:, 1].contiguous()
+
+
 def _unique_pairs(hi: torch.Tensor, lo: torch.Tensor):
     """Sorted unique (hi, lo) pairs on the device: (codes per row, index of one row per
     unique key, in key order)."""
@@ -97,21 +121,36 @@ class DeviceFactorEngine(FactorEngine):
 
     def _prepare_arrays(self, prices: dict, index: dict) -> None:
         dev = self.device
-        hi, lo = (torch.from_numpy(x).to(dev) for x in _s16_keys(prices["ts_code"]))
-        scodes, srep = _unique_pairs(hi, lo)
-        td = torch.from_numpy(np.asarray(prices["trade_date"], dtype=np.int64)).to(dev)
-        if bool((td < 0).any()):
-            raise NeedsPandasPath("missing trade_date")
-        dvals, dcodes = torch.unique(td, sorted=True, return_inverse=True)
+        # every host -> device copy is issued first (asynchronous from the reader's pinned
+        # buffers), in the dtype the reader produced: float32 loader columns (the reference's
+        # load downcast, Q27) move half the bytes of float64; codes go up as raw S16 bytes and
+        # dates as int32, and their keys are formed on the device
+        code = _upload(np.ascontiguousarray(prices["ts_code"], dtype="S16").view(np.uint8), dev)
+        td32 = _upload(np.asarray(prices["trade_date"]), dev)
+        up = {c: _upload(np.asarray(prices[c]), dev) for c in self.NUMERIC if c in prices}
+        ed = _upload(np.asarray(prices["end_date"]), dev) if "end_date" in prices else None
+        hi, lo = _s16_keys_device(code)
+        scodes, srep = _unique_pairs(hi, lo)                 # one sync (N)
+        td = td32.long()
+        dvals, dcodes = torch.unique(td, sorted=True, return_inverse=True)  # one sync (D)
         D = int(dvals.numel())
         key = scodes * D + dcodes
         R = int(key.numel())
-        if R > 1 and not bool((key[1:] >= key[:-1]).all()):
+        # input checks gathered into ONE host read: missing dates, sortedness, duplicates
+        chk = torch.zeros(3, dtype=torch.bool, device=dev)
+        chk[0] = (td < 0).any() if R else False
+        if R > 1:
+            chk[1] = (key[1:] < key[:-1]).any()
+            chk[2] = (key[1:] == key[:-1]).any()
+        missing, unsorted, dup = chk.tolist()
+        if missing:
+            raise NeedsPandasPath("missing trade_date")
+        order = None
+        if unsorted:
             order = torch.argsort(key, stable=True)      # _prepare_data's (ts_code, trade_date) sort
             key = key[order]
-        else:
-            order = None
-        if R > 1 and bool((key[1:] == key[:-1]).any()):
+            dup = bool((key[1:] == key[:-1]).any())
+        if dup:
             raise NeedsPandasPath("duplicate (ts_code, trade_date) rows")
         perm = (lambda x: x[order]) if order is not None else (lambda x: x)
         self.R, self.D = R, D
@@ -120,8 +159,10 @@ class DeviceFactorEngine(FactorEngine):
         self.stock_names = pd.Index(names.astype("U16").astype(object))
         dv = dvals.cpu().numpy()
         self.date_ints = dv
-        self.date_names = pd.Index(np.array([f"{d // 10000:04d}/{d // 100 % 100:02d}/{d % 100:02d}"
-                                             for d in dv], dtype=object))
+        y, m, d = dv // 10000, dv // 100 % 100, dv % 100
+        self.date_names = pd.Index(np.char.add(np.char.add(np.char.add(
+            np.char.zfill(y.astype(str), 4), "/"), np.char.add(np.char.zfill(m.astype(str), 2), "/")),
+            np.char.zfill(d.astype(str), 2)).astype(object))
         self.stock_id = perm(scodes).to(torch.int32)
         self.date_id = perm(dcodes).to(torch.int32)
         self.seg_lo = RL.seg_lo_from_codes(self.stock_id)
@@ -141,17 +182,10 @@ class DeviceFactorEngine(FactorEngine):
         hit = (pos < len(it)) & (it[np.minimum(pos, len(it) - 1)] == dv)
         mr_date = np.where(hit, mr_idx[np.minimum(pos, len(it) - 1)], np.nan)
         mr = torch.from_numpy(mr_date).to(dev)[self.date_id.long()]
-        self.cols = {}
-        for c in self.NUMERIC:
-            if c in prices:
-                x = torch.from_numpy(np.asarray(prices[c], dtype=np.float64)).to(dev)
-                self.cols[c] = perm(x).to(torch.float32)
+        self.cols = {c: perm(x).to(torch.float32) for c, x in up.items()}
         self.cols["market_ret"] = mr.to(torch.float32)
         self.cols["ret"], self.cols["log_ret"] = RL.returns(self.cols["close"], self.seg_lo)
-        self.end_date = None
-        if "end_date" in prices:
-            e = torch.from_numpy(np.asarray(prices["end_date"], dtype=np.int64)).to(dev)
-            self.end_date = perm(e)
+        self.end_date = None if ed is None else perm(ed.long())
 
     def _has_statements(self) -> bool:
         return "n_cashflow_act" in self.cols and self.end_date is not None
@@ -166,6 +200,15 @@ class DeviceFactorEngine(FactorEngine):
     def cashflow_ttm(self) -> torch.Tensor:
         if getattr(self, "_ttm", None) is not None:
             return self._ttm
+        if self.device.type == "cuda":
+            # run-based kernels, one host read (the error flags) instead of three syncs
+            ttm, flags = RL.ttm_runs(self.stock_id, self.end_date, self.cols["n_cashflow_act"])
+            f = int(flags.item())
+            if f & RL.TTM_MULTIVALUE:
+                raise NeedsPandasPath("several cash-flow values for one (stock, end_date)")
+            if not f & RL.TTM_RESTATED:
+                self._ttm = ttm
+                return ttm
         dev = self.device
         e = torch.where(self.end_date < 0, torch.full_like(self.end_date, 2 ** 62), self.end_date)
         sc = self.stock_id.to(torch.int64)
@@ -372,13 +415,42 @@ def barra_frame(eng: FactorEngine, cols: dict, l1_stock: np.ndarray, ctx=None,
 
 def read_price_columns(prices_csv: str, index_csv: str):
     """Columnar parse of the loader's CSVs by the native reader: codes as S16 bytes, dates as
-    YYYYMMDD ints, everything else float64.  None if the native reader is unavailable."""
+    YYYYMMDD ints, the engine's numeric columns float32, anything else float64.  None if the
+    native reader is unavailable."""
     from ..utils import native_io
-    types = {c: 1 for c in PRICE_STRING_COLS}
+    # numeric loader columns parse straight to float32 (the reference's load downcast, Q27)
+    # into pinned staging buffers when a GPU is present
+    types = {c: 3 for c in FactorEngine.NUMERIC}
+    types.update({c: 1 for c in PRICE_STRING_COLS})
     types.update({c: 2 for c in PRICE_DATE_COLS})
-    p = native_io.read_columns(prices_csv, types)
+    p = native_io.read_columns(prices_csv, types, pinned=torch.cuda.is_available())
     i = native_io.read_columns(index_csv, {"ts_code": 1, "trade_date": 2})
     return p, i
+
+
+def stage_host_columns(prices: dict, pinned: bool | None = None) -> dict:
+    """The layout :func:`read_price_columns` produces, from float64 columnar arrays (e.g.
+    :func:`_columns_from_frames`): the engine's numeric columns rounded to float32 (Q27), codes /
+    dates / numerics in pinned host memory when a GPU is present.  This is the native reader's
+    parse-time work; benchmarks count it as I/O."""
+    from ..utils.native_io import _host_buffer
+    pinned = torch.cuda.is_available() if pinned is None else pinned
+    out = {}
+    for c, x in prices.items():
+        x = np.asarray(x)
+        if c in FactorEngine.NUMERIC:
+            dt = np.float32
+        elif x.dtype.kind == "S":
+            dt = "S16"
+        elif c in PRICE_DATE_COLS:
+            dt = np.int32
+        else:
+            out[c] = x
+            continue
+        buf = _host_buffer(len(x), dt, pinned)
+        buf[...] = x
+        out[c] = buf
+    return out
 
 
 def _columns_from_frames(prices_df: pd.DataFrame, index_df: pd.DataFrame):

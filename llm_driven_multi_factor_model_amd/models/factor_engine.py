@@ -373,6 +373,10 @@ class FactorEngine:
     def compute_leverage(self):
         if not self._need("total_mv", "total_ncl", "total_hldr_eqy_inc_min_int", "debt_to_assets"):
             return None
+        if self.device.type == "cuda":  # one fused pass (csrc/rolling.hip leverage_kernel)
+            mlev, blev = RL.leverage(self.cols["total_mv"], self.cols["total_ncl"],
+                                     self.cols["total_hldr_eqy_inc_min_int"])
+            return {"MLEV": mlev, "DTOA": self.cols["debt_to_assets"], "BLEV": blev}
         mv = self.cols["total_mv"].double()
         ncl = self.cols["total_ncl"].double()
         be = self.cols["total_hldr_eqy_inc_min_int"].double()

@@ -22,6 +22,9 @@ _native.register("mfa_dastd", [_vp, _vp, _vp, _i, _i, _d, _i, _vp, _vp])
 _native.register("mfa_cmra", [_vp, _vp, _i, _i, _i, _vp, _vp])
 _native.register("mfa_rolling_sum", [_vp, _vp, _i, _i, _i, _d, _i, _vp, _vp])
 _native.register("mfa_returns", [_vp, _vp, _i, _vp, _vp, _vp])
+_native.register("mfa_ttm_flags", [_vp, _vp, _vp, _i, _vp, _vp, _vp])
+_native.register("mfa_ttm_finish", [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp])
+_native.register("mfa_leverage", [_vp, _vp, _vp, _i, _vp, _vp, _vp])
 
 
 def _f(t):
@@ -203,3 +206,44 @@ def rolling_sum(x, seg_lo, window, min_periods, scale=1.0, log=False):
             t = w.sum()
             out[r] = (np.nan if t == 0 else math.log(t)) if log else t
     return torch.from_numpy(out).float()
+
+
+# ---------------------------------------------------------------- statement-row TTM, leverage
+TTM_RESTATED, TTM_MULTIVALUE = 1, 2
+
+
+def ttm_runs(stock_id, end_date, v):
+    """Statement-row TTM on the device (``csrc/rolling.hip`` ttm_* kernels): rows sorted by
+    (stock, date); a run = consecutive rows of one (stock, end_date); each row gets the
+    NaN-skipping sum of its run's and the 3 previous runs' values (min 4), fp32-rounded like the
+    rolling-sum path, as float64.  Returns ``(ttm [R] float64, flags int32 [1] device tensor)``:
+    flag ``TTM_RESTATED`` = end_date moved backwards within a stock (the result is then not
+    valid: use the sort-based path), ``TTM_MULTIVALUE`` = one statement carries two values."""
+    sid = _i32(stock_id)
+    e = end_date.to(torch.int64).contiguous()
+    x = _f(v)
+    R = x.numel()
+    dev = x.device
+    start = torch.empty(R, dtype=torch.int32, device=dev)
+    flags = torch.zeros(1, dtype=torch.int32, device=dev)
+    out = torch.empty(R, dtype=torch.float64, device=dev)
+    if R == 0:
+        return out, flags
+    st = _native.stream(dev)
+    _native.call("mfa_ttm_flags", _native.ptr(sid), _native.ptr(e), _native.ptr(x), R,
+                 _native.ptr(start), _native.ptr(flags), st)
+    run_incl = torch.cumsum(start, 0, dtype=torch.int32)
+    vf = torch.empty(R, dtype=torch.float32, device=dev)
+    rsid = torch.empty(R, dtype=torch.int32, device=dev)
+    _native.call("mfa_ttm_finish", _native.ptr(sid), _native.ptr(x), _native.ptr(start),
+                 _native.ptr(run_incl), R, _native.ptr(vf), _native.ptr(rsid), _native.ptr(out), st)
+    return out, flags
+
+
+def leverage(mv, ncl, be):
+    """(MLEV, BLEV) float32 (factor_calculator.py:464-509) in one device pass."""
+    mv, ncl, be = _f(mv), _f(ncl), _f(be)
+    mlev, blev = torch.empty_like(mv), torch.empty_like(mv)
+    _native.call("mfa_leverage", _native.ptr(mv), _native.ptr(ncl), _native.ptr(be), mv.numel(),
+                 _native.ptr(mlev), _native.ptr(blev), _native.stream(mv.device))
+    return mlev, blev

@@ -94,10 +94,26 @@ def read_barra_csv(path: str) -> pd.DataFrame | None:
     return read_csv(path)
 
 
-def read_columns(path: str, types: dict, nthreads: int = 0):
-    """Raw columnar parse: ``types`` maps column name -> 0 float64 / 1 bytes16 / 2 int YYYYMMDD.
+def _host_buffer(rows: int, dtype, pinned: bool) -> np.ndarray:
+    """A numpy array of ``rows`` elements, in page-locked (pinned) host memory when ``pinned``:
+    the parser writes straight into DMA-able staging buffers (no extra host copy before the
+    device upload)."""
+    if pinned:
+        import torch
+        tdt = {np.float32: torch.float32, np.float64: torch.float64, np.int32: torch.int32}.get(dtype)
+        if tdt is not None:
+            return torch.empty(rows, dtype=tdt, pin_memory=True).numpy()
+        if dtype == "S16":
+            return torch.zeros(rows * 16, dtype=torch.uint8, pin_memory=True).numpy().view("S16")
+    return np.zeros(rows, dtype=dtype) if dtype == "S16" else np.empty(rows, dtype=dtype)
 
-    Returns ``{name: ndarray}`` (bytes columns stay ``S16``), or None if unavailable.
+
+def read_columns(path: str, types: dict, nthreads: int = 0, pinned: bool = False):
+    """Raw columnar parse: ``types`` maps column name -> 0 float64 / 1 bytes16 / 2 int YYYYMMDD /
+    3 float32 (float64 parse rounded to float32, the reference's load downcast).
+
+    Returns ``{name: ndarray}`` (bytes columns stay ``S16``), or None if unavailable.  With
+    ``pinned`` (a GPU is present) the buffers are page-locked host memory.
     """
     lib = _load_or_none()
     if lib is None:
@@ -112,8 +128,8 @@ def read_columns(path: str, types: dict, nthreads: int = 0):
     for name in header:
         t = types.get(name, 0)
         tl.append(t)
-        bufs.append(np.zeros(rows, dtype="S16") if t == 1 else
-                    (np.empty(rows, dtype=np.int32) if t == 2 else np.empty(rows, dtype=np.float64)))
+        dt = {1: "S16", 2: np.int32, 3: np.float32}.get(t, np.float64)
+        bufs.append(_host_buffer(rows, dt, pinned))
     got = lib.mfa_csv_parse(path.encode(), len(header), (C.c_int * len(tl))(*tl),
                             (C.c_void_p * len(bufs))(*[b.ctypes.data for b in bufs]), nthreads)
     return {n: b[:got] for n, b in zip(header, bufs)}

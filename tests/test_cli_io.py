@@ -70,6 +70,28 @@ def test_native_csv_reader_matches_pandas(tmp_path):
     pd.testing.assert_frame_equal(got, pd.read_csv(p), check_dtype=False)
 
 
+def test_native_reader_float32_columns(tmp_path):
+    """Type 3 columns parse to float64 and round to float32 -- exactly pandas' float64 read
+    followed by the reference's astype(float32) load downcast (load_data.py:13-25, Q27)."""
+    from llm_driven_multi_factor_model_amd.utils import native_io
+    rng = np.random.default_rng(3)
+    n = 4000
+    df = pd.DataFrame({"ts_code": [f"{i % 900:06d}.SZ" for i in range(n)],
+                       "trade_date": np.repeat(["2020-01-02", "2020-01-03"], n // 2),
+                       "close": rng.lognormal(2, 1, n), "total_mv": rng.lognormal(14, 2, n) * 1e3,
+                       "pe_ttm": rng.normal(20, 30, n)})
+    df.loc[7, "close"] = np.nan
+    p = str(tmp_path / "prices.csv")
+    df.to_csv(p, index=False)
+    got = native_io.read_columns(p, {"ts_code": 1, "trade_date": 2, "close": 3, "total_mv": 3,
+                                     "pe_ttm": 3})
+    ref = pd.read_csv(p)
+    for c in ("close", "total_mv", "pe_ttm"):
+        assert got[c].dtype == np.float32
+        np.testing.assert_array_equal(got[c], ref[c].to_numpy().astype(np.float32), err_msg=c)
+    assert (got["trade_date"][:2] == 20200102).all() and got["ts_code"][0] == b"000000.SZ"
+
+
 def test_panel_from_barra_csv_native_equals_pandas(tmp_path, monkeypatch):
     from llm_driven_multi_factor_model_amd.utils.io import panel_from_barra_csv
     d = str(tmp_path)

@@ -124,3 +124,28 @@ def test_duplicate_rows_need_pandas_path():
     p, i = e2e._columns_from_frames(prices, index)
     with pytest.raises(e2e.NeedsPandasPath):
         e2e.DeviceFactorEngine(p, i, device="cpu")
+
+
+@pytest.mark.gpu
+def test_hip_device_engine_matches_cpu_engine(cuda):
+    """The device-built master on the GPU (async uploads, device code keys, run-based TTM and
+    fused leverage kernels) against the CPU engine: statement / leverage descriptors exactly,
+    rolling ones to fp32 rounding; also with a restated statement (end_date moving backwards:
+    the TTM kernel flags it and the sort-based path runs)."""
+    prices, index, _ = _data()
+    for restate in (False, True):
+        pr = prices.copy()
+        if restate:
+            s0 = pr["ts_code"] == pr["ts_code"].iloc[0]
+            late = s0 & (pr["trade_date"] > pr["trade_date"].quantile(0.6))
+            pr.loc[late, "end_date"] = pr.loc[late, "end_date"] - pd.Timedelta(days=400)
+        p, i = e2e._columns_from_frames(pr, index)
+        ref = e2e.DeviceFactorEngine(p, i, device="cpu").compute(FACTORS_TO_RUN)
+        got = e2e.DeviceFactorEngine(e2e.stage_host_columns(p), i, device=cuda).compute(FACTORS_TO_RUN)
+        assert list(got) == list(ref)
+        for k in ref:
+            exact = k in ("BP", "CETOP", "ETOP", "YOYProfit", "YOYSales", "MLEV", "DTOA",
+                          "BLEV")
+            torch.testing.assert_close(got[k].cpu().double(), ref[k].double(),
+                                       rtol=0 if exact else 2e-4, atol=0 if exact else 2e-6,
+                                       equal_nan=True, msg=f"{k} restate={restate}")

@@ -32,6 +32,7 @@ def main():
     ctx = pdist.init_distributed()
     prices, index, sw = FE.synthetic_prices_fast(N=N, T=T, seed=0, n_ind=31, suspend_frac=0.01)
     cols = e2e._columns_from_frames(prices, index)
+    cols = (e2e.stage_host_columns(cols[0]), cols[1])   # the native reader's layout (I/O)
     del prices
     cfg = preset("reference")
     small = FE.synthetic_prices(N=60, T=300, seed=1, n_ind=31)

@@ -25,6 +25,9 @@ prices, index, sw = FE.synthetic_prices_fast(N=N, T=T, seed=0, n_ind=31, suspend
 gen_s = time.perf_counter() - t0
 print(json.dumps({"rows": len(prices), "gen_s": round(gen_s, 2)}), flush=True)
 cols = e2e._columns_from_frames(prices, index)
+t0 = time.perf_counter()
+cols = (e2e.stage_host_columns(cols[0]), cols[1])   # the native reader's output layout (I/O)
+print(json.dumps({"stage_host_s": round(time.perf_counter() - t0, 3)}), flush=True)
 small_p, small_i, small_sw = FE.synthetic_prices(N=60, T=300, seed=1, n_ind=31)
 e2e.run_pipeline(small_p, small_i, small_sw, device=dev)  # warm-up: kernel load, allocator
 for rep in range(2):
