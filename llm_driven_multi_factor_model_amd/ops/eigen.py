@@ -58,8 +58,10 @@ WIDE_CHUNK_DOUBLES = 1 << 27     # ~1 GB of fp64 per batched eigh / draw chunk
 # count-guided Laguerre eigenvalues (division-free Sturm recurrence), twisted-factorisation
 # eigenvectors, back-transform, lean register / LDS layout (mode 5, the default);
 # "tridiag_v1" / "tridiag_lean" = the round-2 kernel (mode 3) / lean layout with the pivot-form
-# Sturm recurrence (mode 4), kept for A/B.
-BIAS_SOLVERS = {"jacobi": 0, "tridiag": 5, "tridiag_v1": 3, "tridiag_lean": 4}
+# Sturm recurrence (mode 4), kept for A/B; "tridiag_dense" = mode 5's arithmetic with three
+# problems on the 126 lanes of a 2-wave workgroup (mode 11, K <= 42; wider K falls back to the
+# one-problem-per-wave kernel).
+BIAS_SOLVERS = {"jacobi": 0, "tridiag": 5, "tridiag_v1": 3, "tridiag_lean": 4, "tridiag_dense": 11}
 _bias_solver = "tridiag"
 
 

@@ -138,6 +138,25 @@ def test_hip_bias_solvers_agree_on_pipeline_like_inputs(cuda):
         torch.testing.assert_close(out[solver], out["jacobi"], rtol=1e-10, atol=0)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("K,D,M", [(42, 7, 5), (30, 5, 4), (42, 1, 1)])
+def test_hip_dense_bias_solver_tail_and_invalid_dates(cuda, K, D, M):
+    """Lane-dense solver (3 problems per 2-wave workgroup): a last workgroup with empty slots
+    (D * M not a multiple of 3), a NaN date in the middle of a workgroup, K < 42 (inactive
+    rows in every slot) -- same bias ratios as the one-problem-per-wave mode-5 kernel."""
+    F = _spd(D, K, seed=K + D, spread=2.5) * 1e-4
+    if D > 2:
+        F[2] = float("nan")
+    Cz = eigen.mc_cov(M, K, 2520, seed=4, device=cuda)
+    with eigen.using_bias_solver("tridiag"):
+        Fa, va = eigen.eigen_risk_adjust(F.to(cuda), Cz=Cz, return_bias=True)
+    with eigen.using_bias_solver("tridiag_dense"):
+        Fb, vb = eigen.eigen_risk_adjust(F.to(cuda), Cz=Cz, return_bias=True)
+    assert torch.equal(va.isnan(), vb.isnan())
+    torch.testing.assert_close(vb.cpu(), va.cpu(), rtol=1e-11, atol=0, equal_nan=True)
+    torch.testing.assert_close(Fb.cpu(), Fa.cpu(), rtol=1e-10, atol=1e-20, equal_nan=True)
+
+
 def _philox_normals(m, T, K, seed):
     """numpy replica of mc_cov_kernel's draws: Philox4x32-10 keyed by (seed), counter
     (sim, time, factor // 2, 0x4D464131), two 53-bit uniforms, fp64 Box-Muller pair."""

@@ -1,0 +1,50 @@
+"""RiskModel.run alone, for a kernel trace that holds only the model's kernels.
+
+    python tools/risk_run_only.py --make gpurun_out/panel.pt     # generate + save (not traced)
+    rocprofv3 --kernel-trace --stats -d OUT -- python tools/risk_run_only.py --load gpurun_out/panel.pt
+
+The traced process loads the saved fp64 panel from host memory (host -> device copies only, no
+generator kernels), runs one warm-up ``RiskModel.run`` and ``--reps`` timed ones, and prints the
+per-stage milliseconds of the last one.  Divide the kernel counts of the trace by reps + 1.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from llm_driven_multi_factor_model_amd.models.panel import RiskPanel, synthetic_panel  # noqa: E402
+from llm_driven_multi_factor_model_amd.models.risk_model import RiskModel  # noqa: E402
+from llm_driven_multi_factor_model_amd.utils.config import preset  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--make", default=None)
+ap.add_argument("--load", default=None)
+ap.add_argument("--dates", type=int, default=2520)
+ap.add_argument("--stocks", type=int, default=5000)
+ap.add_argument("--reps", type=int, default=2)
+a = ap.parse_args()
+if a.make:
+    p = synthetic_panel(a.dates, a.stocks, 31, 10, seed=3, missing_frac=0.01, dtype=torch.float64)
+    torch.save({"styles": p.styles, "cap": p.cap, "ret": p.ret, "ind": p.ind,
+                "dates": torch.from_numpy(p.dates.astype("int64"))}, a.make)
+    sys.exit(0)
+d = torch.load(a.load, weights_only=True)
+import numpy as np  # noqa: E402
+p = RiskPanel(styles=d["styles"], cap=d["cap"], ret=d["ret"], ind=d["ind"], P=31,
+              dates=d["dates"].numpy().astype("datetime64[ns]"),
+              stocks=np.array([f"{i:06d}.SZ" for i in range(d["cap"].shape[1])], dtype=object)
+              ).to("cuda:0")
+cfg = preset("reference")
+for rep in range(a.reps + 1):
+    m = RiskModel(p, cfg)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    m.run()
+    torch.cuda.synchronize()
+    tot = (time.perf_counter() - t0) * 1e3
+print(json.dumps({"total_ms": round(tot, 3),
+                  "stage_ms": {k: round(v, 3) for k, v in m.times.ms.items()}}))
