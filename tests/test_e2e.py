@@ -144,8 +144,10 @@ def test_hip_device_engine_matches_cpu_engine(cuda):
         got = e2e.DeviceFactorEngine(e2e.stage_host_columns(p), i, device=cuda).compute(FACTORS_TO_RUN)
         assert list(got) == list(ref)
         for k in ref:
-            exact = k in ("BP", "CETOP", "ETOP", "YOYProfit", "YOYSales", "MLEV", "DTOA",
-                          "BLEV")
-            torch.testing.assert_close(got[k].cpu().double(), ref[k].double(),
-                                       rtol=0 if exact else 2e-4, atol=0 if exact else 2e-6,
-                                       equal_nan=True, msg=f"{k} restate={restate}")
+            # statement / leverage descriptors in fp64 then rounded: exact; x / 100 in fp32 may
+            # be a reciprocal multiply on the GPU (1 ulp); rolling ones: fp32 rounding
+            exact = k in ("BP", "CETOP", "ETOP", "MLEV", "DTOA", "BLEV")
+            ulp = k in ("YOYProfit", "YOYSales", "SIZE")
+            tol = (0, 0) if exact else ((2.4e-7, 0) if ulp else (2e-4, 2e-6))
+            torch.testing.assert_close(got[k].cpu().double(), ref[k].double(), rtol=tol[0],
+                                       atol=tol[1], equal_nan=True, msg=f"{k} restate={restate}")

@@ -76,8 +76,10 @@ def test_hip_wide_eigh_and_adjust_match_cpu(cuda, K):
 @pytest.mark.gpu
 def test_hip_risk_model_k140_matches_cpu(cuda):
     """RiskModel.run + eigenfactor_bias at P = 123, Q = 16 (K = 140) on the GPU; every stage
-    matches the CPU fp64 path (the eigen stage on the GPU's own draw covariances)."""
-    D, N, P, Q, M = 40, 2000, 123, 16, 6
+    matches the CPU fp64 path (the eigen stage on the GPU's own draw covariances).  200 dates:
+    the Newey-West covariance needs more dates than factors (utils.py:29-30), so dates >= 140
+    carry finite covariances."""
+    D, N, P, Q, M = 200, 1200, 123, 16, 6
     p = synthetic_panel(D, N, P, Q, seed=13, missing_frac=0.01, dtype=torch.float64)
     cfg = preset("reference", eigen_sims=M, nw_half_life=30.0, vra_half_life=10.0,
                  eigen_sim_length=300)   # T_sim > K: full-rank draw covariances
@@ -88,13 +90,15 @@ def test_hip_risk_model_k140_matches_cpu(cuda):
     c.newey_west()
     torch.testing.assert_close(g.factor_ret.cpu(), c.factor_ret, rtol=1e-9, atol=1e-12)
     torch.testing.assert_close(g.nw_cov.cpu(), c.nw_cov, rtol=1e-8, atol=1e-15, equal_nan=True)
+    fin = torch.isfinite(g.nw_cov.reshape(D, -1)).all(-1).cpu()
+    assert fin[150:].all() and not fin[:100].any()
     Cz = eigen.mc_cov(M, 140, 300, seed=cfg.eigen_seed, device=cuda).cpu()
     Fh, vb = eigen.eigen_risk_adjust(g.nw_cov.cpu(), Cz=Cz, scale_coef=cfg.eigen_scale,
                                      return_bias=True)
     torch.testing.assert_close(g.eigen_bias.cpu(), vb, rtol=1e-8, atol=1e-10, equal_nan=True)
     torch.testing.assert_close(g.eigen_cov.cpu(), Fh, rtol=1e-8, atol=1e-16, equal_nan=True)
     assert torch.isfinite(g.vra_cov[-1]).all()
-    bias = g.eigenfactor_bias("eigen", start=5, predlen=2)
+    bias = g.eigenfactor_bias("eigen", start=150, predlen=2)
     assert bias.shape == (140,) and torch.isfinite(bias).all()
 
 
@@ -102,12 +106,14 @@ def test_hip_risk_model_k140_matches_cpu(cuda):
 def test_hip_portfolio_exposure_wide(cuda):
     """P = 150 industries (> 128) and Q = 20 styles (> 16): block launches and dynamic LDS."""
     p = synthetic_panel(5, 1500, 150, 20, seed=3, missing_frac=0.02, dtype=torch.float64)
-    from llm_driven_multi_factor_model_amd.ops import cross_section as X
     g = p.to(cuda)
-    res = X.xs_wls(g.styles, g.cap, g.ret, g.ind, p.P)
+    # stats [D, Q + 2] (cap-weighted style means, pooled sigma, n) are inputs of the kernel;
+    # the regression's own are not needed to compare the two paths
+    st = torch.rand(p.D, p.Q + 2, dtype=torch.float64)
+    st[:, p.Q] += 0.5
     h = torch.rand(p.D, p.N, dtype=torch.float64)
-    got = A.portfolio_exposure(g.styles, g.cap, g.ret, g.ind, h.to(cuda), res.stats, p.P)
-    ref = A.portfolio_exposure(p.styles, p.cap, p.ret, p.ind, h, res.stats.cpu(), p.P)
+    got = A.portfolio_exposure(g.styles, g.cap, g.ret, g.ind, h.to(cuda), st.to(cuda), p.P)
+    ref = A.portfolio_exposure(p.styles, p.cap, p.ret, p.ind, h, st, p.P)
     torch.testing.assert_close(got.cpu(), ref, rtol=1e-10, atol=1e-12)
 
 

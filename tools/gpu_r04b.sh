@@ -17,3 +17,4 @@ step $O/risk_run_only.log timeout -k 10 240 rocprofv3 --kernel-trace --stats -d 
 step $O/xs_chunk_ab.jsonl timeout -k 10 300 python tools/xs_chunk_ab.py
 step $O/risk_stages_k140.log timeout -k 10 300 python tools/risk_stages.py --P 123 --Q 16 --stocks 5000 --dates 252 --reps 2
 step $O/bias_dense_ab.jsonl timeout -k 10 300 env MODES=5,11,61,62,111,112,5,11 SETTINGS=1e-15:30 python tools/eigen_tol.py
+MFA_DIST_BACKEND=gloo step $O/pipeline_dist4_gloo.log timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29533 tools/pipeline_dist.py

@@ -30,13 +30,21 @@ def main():
     N = int(sys.argv[1]) if len(sys.argv) > 1 else 5000
     T = int(sys.argv[2]) if len(sys.argv) > 2 else 2520
     ctx = pdist.init_distributed()
+    t0 = time.perf_counter()
+
+    def note(msg):  # progress on stderr (a long silent phase looks hung to the GPU harness)
+        print(f"[rank {ctx.rank} +{time.perf_counter() - t0:.1f}s] {msg}", file=sys.stderr,
+              flush=True)
     prices, index, sw = FE.synthetic_prices_fast(N=N, T=T, seed=0, n_ind=31, suspend_frac=0.01)
+    note("synthetic loader frames ready")
     cols = e2e._columns_from_frames(prices, index)
     cols = (e2e.stage_host_columns(cols[0]), cols[1])   # the native reader's layout (I/O)
     del prices
+    note("columns staged")
     cfg = preset("reference")
     small = FE.synthetic_prices(N=60, T=300, seed=1, n_ind=31)
     e2e.run_pipeline(*small, risk_cfg=cfg, ctx=ctx)  # warm-up: kernel load, allocator, comms
+    note("warm-up done")
     for rep in range(2):
         pdist.barrier(ctx)
         t0 = time.perf_counter()
@@ -46,6 +54,7 @@ def main():
         rec = {k: pdist.all_reduce_max(v, ctx) for k, v in t.items() if k.endswith("_s")}
         rec["wall_s"] = pdist.all_reduce_max(wall, ctx)
         rec["non_io_s"] = sum(v for k, v in rec.items() if k.endswith("_s") and k != "wall_s")
+        note(f"rep {rep} done")
         if ctx.rank == 0:
             print(json.dumps({"world": ctx.world, "backend": ctx.backend, "N": N, "T": T,
                               "D_panel": sum(model.sizes), "K": model.K, "rep": rep,
@@ -53,6 +62,7 @@ def main():
                               "kernel_ms_rank0": {k: round(v, 3) for k, v in
                                                   t.get("kernel_ms", {}).items()}}), flush=True)
     got = {k: pdist.gather_to_root(getattr(model, k).contiguous(), ctx) for k in KEYS}
+    note("gathered")
     if ctx.rank == 0:
         one, _, _, t1 = e2e.run_pipeline(dict(cols[0]), dict(cols[1]), sw, risk_cfg=cfg,
                                          device=ctx.device)
