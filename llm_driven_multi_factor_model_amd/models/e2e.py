@@ -423,9 +423,14 @@ def read_price_columns(prices_csv: str, index_csv: str):
     types = {c: 3 for c in FactorEngine.NUMERIC}
     types.update({c: 1 for c in PRICE_STRING_COLS})
     types.update({c: 2 for c in PRICE_DATE_COLS})
-    p = native_io.read_columns(prices_csv, types, pinned=torch.cuda.is_available())
+    p = native_io.read_columns(prices_csv, types, pinned=_pin_default())
     i = native_io.read_columns(index_csv, {"ts_code": 1, "trade_date": 2})
     return p, i
+
+
+def _pin_default() -> bool:
+    """Pinned staging when a GPU is present (``MFA_PINNED=0`` turns it off)."""
+    return torch.cuda.is_available() and os.environ.get("MFA_PINNED", "1") != "0"
 
 
 def stage_host_columns(prices: dict, pinned: bool | None = None) -> dict:
@@ -434,7 +439,7 @@ def stage_host_columns(prices: dict, pinned: bool | None = None) -> dict:
     dates / numerics in pinned host memory when a GPU is present.  This is the native reader's
     parse-time work; benchmarks count it as I/O."""
     from ..utils.native_io import _host_buffer
-    pinned = torch.cuda.is_available() if pinned is None else pinned
+    pinned = _pin_default() if pinned is None else pinned
     out = {}
     for c, x in prices.items():
         x = np.asarray(x)

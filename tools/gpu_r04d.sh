@@ -3,14 +3,13 @@
 # the single-process sharded-exposures profile (no collectives), then a 2-rank rehearsal.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; O=gpurun_out/r04d; mkdir -p $O; export TMPDIR=/tmp
+PIN=${PIN:-0}
 pids=""
 for r in 0 1 2 3; do
-  timeout -k 10 300 python -u tools/shard_prof.py 5000 2520 4 $r > $O/shard_prof_4proc_r$r.jsonl 2>&1 &
+  MFA_PINNED=$PIN timeout -k 10 300 python -u tools/shard_prof.py 5000 2520 4 $r > $O/shard_prof_4proc_pin${PIN}_r$r.jsonl 2>&1 &
   pids="$pids $!"
 done
 rc=0
 for p in $pids; do wait $p || rc=$?; done
-tail -2 $O/shard_prof_4proc_r*.jsonl
+for f in $O/shard_prof_4proc_pin${PIN}_r*.jsonl; do tail -n 1 $f | cut -c1-200; done
 case $rc in 124|137|134|139) echo "stopping rc=$rc"; exit $rc;; esac
-MFA_DIST_BACKEND=gloo timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 tools/pipeline_dist.py > $O/pipeline_dist2_gloo.log 2>&1
-tail -5 $O/pipeline_dist2_gloo.log
