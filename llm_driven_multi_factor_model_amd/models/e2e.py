@@ -429,8 +429,13 @@ def read_price_columns(prices_csv: str, index_csv: str):
 
 
 def _pin_default() -> bool:
-    """Pinned staging when a GPU is present (``MFA_PINNED=0`` turns it off)."""
-    return torch.cuda.is_available() and os.environ.get("MFA_PINNED", "1") != "0"
+    """Pinned staging when a GPU is present (``MFA_PINNED=0`` turns it off).  Off by default
+    when several ranks share one device (``MFA_DIST_BACKEND`` rehearsals): four processes
+    copying from pinned buffers into ONE MI355X at once measured 65 s for what takes 0.05 s
+    alone, pageable copies 0.57 s (profiles/r04/README.md)."""
+    if os.environ.get("MFA_PINNED"):
+        return torch.cuda.is_available() and os.environ["MFA_PINNED"] != "0"
+    return torch.cuda.is_available() and not os.environ.get("MFA_DIST_BACKEND")
 
 
 def stage_host_columns(prices: dict, pinned: bool | None = None) -> dict:
