@@ -322,7 +322,10 @@ MFA_API int mfa_nw_series(const double* F, int T, int K, int q, double tau, int 
     return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   const double lam = pow(0.5, 1.0 / tau);
-  const int Tn = t_hi;  // only dates up to t_hi - 1 are needed
+  // the scan always covers all T dates (the caller passes the series length), so a rank that
+  // emits only its own window [t_lo, t_hi) computes every date bitwise like the one-process
+  // run (same chunking and carries); the extra scan is ~0.1 ms at T = 2520
+  const int Tn = T;
   const int nch = (Tn - 1) / CH + 1;
   const int KK = K * K;
   double* C = (double*)ws;

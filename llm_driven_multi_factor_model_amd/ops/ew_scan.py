@@ -55,8 +55,10 @@ def newey_west_series(F: torch.Tensor, q: int = 2, tau: float = 252.0, t_lo: int
     V = torch.empty(t_hi - t_lo, K, K, dtype=torch.float64, device=F.device)
     if t_hi == t_lo:
         return V
-    ws = torch.empty(max(8, _ws_bytes(t_hi, K, q)), dtype=torch.uint8, device=F.device)
-    _native.call("mfa_nw_series", _native.ptr(F), t_hi, K, q, float(tau), t_lo, t_hi,
+    # the scan runs over all T dates whatever the window, so every window is bitwise the slice
+    # of the full series (rank-invariant gather mode)
+    ws = torch.empty(max(8, _ws_bytes(T, K, q)), dtype=torch.uint8, device=F.device)
+    _native.call("mfa_nw_series", _native.ptr(F), T, K, q, float(tau), t_lo, t_hi,
                  _native.ptr(V), _native.ptr(ws), _native.stream(F.device))
     return V
 

@@ -76,6 +76,18 @@ def test_hip_scan_any_lag_count(cuda, T, K, q, tau, lo, hi):
 
 
 @pytest.mark.gpu
+def test_hip_scan_windows_are_bitwise_slices(cuda):
+    """A rank's own window (gather mode) is bitwise the slice of the one-process series: the
+    scan always spans all T dates, whatever the emitted window (rank-invariant NW)."""
+    F = _series(2520, 42, seed=11).to(cuda)
+    full = ew_scan.newey_west_series(F, 2, 252.0)
+    for lo, hi in ((0, 315), (315, 630), (1890, 2205), (2205, 2520), (7, 1300)):
+        part = ew_scan.newey_west_series(F, 2, 252.0, lo, hi)
+        assert torch.equal(part.isnan(), full[lo:hi].isnan())
+        assert torch.equal(torch.nan_to_num(part), torch.nan_to_num(full[lo:hi])), (lo, hi)
+
+
+@pytest.mark.gpu
 @pytest.mark.reference
 def test_hip_scan_use4s_lags_match_reference(cuda, ref):
     """USE4-S 5-lag Newey-West on the GPU against the reference utils.Newey_West itself."""
