@@ -5,4 +5,5 @@ timeout -k 10 300 python -u -m pytest tests/test_newey_west.py tests/test_time_s
 tail -3 $O/pytest.log
 case $rc in 124|137|134|139) exit $rc;; esac
 MFA_DIST_BACKEND=gloo timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 tools/pipeline_dist.py > $O/pipeline_dist2_gloo.log 2>&1
-rc=$?; grep -v "socket.cpp\|amdgpu.ids" $O/pipeline_dist2_gloo.log | tail -2 | cut -c1-700; exit $rc
+rc=$?; grep -v "socket.cpp\|amdgpu.ids" $O/pipeline_dist2_gloo.log | tail -2 | cut -c1-700; case $rc in 124|137|134|139) exit $rc;; esac
+timeout -k 10 300 python tools/wide_eigh_probe.py > $O/wide_eigh_probe.jsonl 2>&1; rc=$?; tail -3 $O/wide_eigh_probe.jsonl; exit $rc
