@@ -60,7 +60,7 @@ def _upload(x: np.ndarray, dev) -> torch.Tensor:
     native reader's staging buffers)."""
     t = torch.from_numpy(np.ascontiguousarray(x))
     if dev.type != "cuda":
-        return t
+        return t.clone()  # never alias the caller's buffers
     return t.to(dev, non_blocking=t.is_pinned())
 
 
