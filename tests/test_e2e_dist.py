@@ -174,3 +174,51 @@ def test_sharded_pipeline_gloo_rehearsal_on_one_gpu(cuda):
     model, frame, info = _reference("cuda:0")
     got = _run(3, "cuda")
     _compare(got, model, frame, info, rtol=5e-3, atol=1e-6, frame_rtol=2e-4, frame_atol=2e-6)
+
+
+def _torchrun_cli(nproc, *args, port=None):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="", OMP_NUM_THREADS="1",
+               PYTHONPATH=root)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={nproc}", "--master-addr", "127.0.0.1",
+           f"--master-port={port or _free_port()}", "-m", "llm_driven_multi_factor_model_amd.cli",
+           *args]
+    return subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=900, env=env)
+
+
+def test_cli_pipeline_and_factors_under_torchrun(tmp_path):
+    """`cli pipeline` / `cli factors` under torchrun (2 gloo ranks, date-sharded end to end)
+    write the same files as one process: the five demo.py results and barra_data_csi.csv."""
+    prices, index, sw = _data()
+    d = tmp_path
+    prices.to_csv(d / "prices.csv", index=False)
+    index.to_csv(d / "index.csv", index=False)
+    sw.to_csv(d / "sw.csv", index=False)
+    common = ["--prices", str(d / "prices.csv"), "--index", str(d / "index.csv"),
+              "--industry", str(d / "sw.csv")]
+    for n in (1, 2):
+        r = _torchrun_cli(n, "pipeline", *common, "--out", str(d / f"res{n}"), "--sims", "3",
+                          "--device", "cpu", "--write-barra", str(d / f"barra{n}"))
+        assert r.returncode == 0, r.stderr[-3000:]
+        r = _torchrun_cli(n, "factors", *common, "--out", str(d / f"fac{n}"), "--device", "cpu")
+        assert r.returncode == 0, r.stderr[-3000:]
+    for f in ("factor_returns.csv", "r_squared.csv", "specific_returns.csv",
+              "final_vol_regime_adj_covariance.csv", "volatility_multiplier_lambda.csv"):
+        a = pd.read_csv(d / "res1" / f, index_col=0)
+        b = pd.read_csv(d / "res2" / f, index_col=0)
+        assert list(a.columns) == list(b.columns) and list(a.index) == list(b.index), f
+        np.testing.assert_allclose(b.to_numpy(np.float64), a.to_numpy(np.float64), rtol=1e-12,
+                                   atol=1e-15, err_msg=f)
+    for one, two in (("barra1", "barra2"), ("fac1", "fac2"), ("barra1", "fac2")):
+        for f in ("barra_data_csi.csv", "industry_info.csv"):
+            a, b = pd.read_csv(d / one / f), pd.read_csv(d / two / f)
+            assert list(a.columns) == list(b.columns) and len(a) == len(b), (one, two, f)
+            for c in a.columns:
+                if a[c].dtype.kind == "f":
+                    np.testing.assert_allclose(b[c].values, a[c].values, rtol=1e-12, atol=0,
+                                               equal_nan=True, err_msg=f"{one} {two} {f} {c}")
+                else:
+                    assert (a[c].astype(str).values == b[c].astype(str).values).all(), c
