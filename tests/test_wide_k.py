@@ -76,12 +76,13 @@ def test_hip_wide_eigh_and_adjust_match_cpu(cuda, K):
 @pytest.mark.gpu
 def test_hip_risk_model_k140_matches_cpu(cuda):
     """RiskModel.run + eigenfactor_bias at P = 123, Q = 16 (K = 140) on the GPU; every stage
-    matches the CPU fp64 path (the eigen stage on the GPU's own draw covariances).  200 dates:
+    matches the CPU fp64 path (the eigen stage on the GPU's own draw covariances).  300 dates:
     the Newey-West covariance needs more dates than factors (utils.py:29-30), so dates >= 140
-    carry finite covariances."""
-    D, N, P, Q, M = 200, 1200, 123, 16, 6
+    carry finite covariances; a long half-life keeps them positive definite (a 30-day half-life
+    leaves < 140 effective dates: negative eigenvalues, an all-NaN eigen stage)."""
+    D, N, P, Q, M = 300, 1200, 123, 16, 6
     p = synthetic_panel(D, N, P, Q, seed=13, missing_frac=0.01, dtype=torch.float64)
-    cfg = preset("reference", eigen_sims=M, nw_half_life=30.0, vra_half_life=10.0,
+    cfg = preset("reference", eigen_sims=M, nw_half_life=1000.0, vra_half_life=10.0,
                  eigen_sim_length=300)   # T_sim > K: full-rank draw covariances
     g = RiskModel(p.to(cuda), cfg).run()
     assert g.K == 140
@@ -91,12 +92,13 @@ def test_hip_risk_model_k140_matches_cpu(cuda):
     torch.testing.assert_close(g.factor_ret.cpu(), c.factor_ret, rtol=1e-9, atol=1e-12)
     torch.testing.assert_close(g.nw_cov.cpu(), c.nw_cov, rtol=1e-8, atol=1e-15, equal_nan=True)
     fin = torch.isfinite(g.nw_cov.reshape(D, -1)).all(-1).cpu()
-    assert fin[150:].all() and not fin[:100].any()
+    assert fin[140:].all() and not fin[:139].any()
     Cz = eigen.mc_cov(M, 140, 300, seed=cfg.eigen_seed, device=cuda).cpu()
     Fh, vb = eigen.eigen_risk_adjust(g.nw_cov.cpu(), Cz=Cz, scale_coef=cfg.eigen_scale,
                                      return_bias=True)
     torch.testing.assert_close(g.eigen_bias.cpu(), vb, rtol=1e-8, atol=1e-10, equal_nan=True)
     torch.testing.assert_close(g.eigen_cov.cpu(), Fh, rtol=1e-8, atol=1e-16, equal_nan=True)
+    assert torch.isfinite(g.eigen_cov.reshape(D, -1)[140:]).all()   # not vacuously NaN
     assert torch.isfinite(g.vra_cov[-1]).all()
     bias = g.eigenfactor_bias("eigen", start=150, predlen=2)
     assert bias.shape == (140,) and torch.isfinite(bias).all()
