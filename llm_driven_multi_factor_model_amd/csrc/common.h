@@ -58,6 +58,53 @@ __device__ __forceinline__ double dpp_upd(double v, double ident) {
 // Hillis-Steele
 // inside each 16-lane row (row_shr 1, 2, 4, 8), then row_bcast:15 into rows 1 / 3 and
 // row_bcast:31 into rows 2 / 3: six VALU-only steps, no LDS round trip.
+// 64-bit DPP move, bound_ctrl: lanes whose source is outside the row read 0 (no identity copy)
+template <int CTRL>
+__device__ __forceinline__ double dpp_zf(double v) {
+  const long long b = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_mov_dpp((int)b, CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp((int)(b >> 32), CTRL, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, ((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+// max / min of finite or infinite (never signalling-NaN) operands: one instruction (fmax / fmin
+// first canonicalise an operand that comes out of a DPP move, a second v_max_f64 per step)
+__device__ __forceinline__ double vmax64(double a, double b) {
+  double r;
+  asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+__device__ __forceinline__ double vmin64(double a, double b) {
+  double r;
+  asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+  return r;
+}
+
+// Instruction-lean scans (round 4; same results as wave_scan_dpp): the sum's row_shr steps
+// zero-fill through bound_ctrl instead of copying the identity into the DPP destination, and
+// max / min (idempotent) keep the lane's own value where the source is invalid (old = v, one
+// 64-bit copy) and skip the canonicalisation: 4 / 4 instructions per step instead of 5 / 6.
+__device__ __forceinline__ double wave_scan_sum(double v) {
+  v += dpp_zf<0x111>(v);
+  v += dpp_zf<0x112>(v);
+  v += dpp_zf<0x114>(v);
+  v += dpp_zf<0x118>(v);
+  v += dpp_upd<0x142, 0xA>(v, 0.0);
+  v += dpp_upd<0x143, 0xC>(v, 0.0);
+  return v;
+}
+template <bool MAX>
+__device__ __forceinline__ double wave_scan_ext(double v) {
+  auto op = [](double a, double b) { return MAX ? vmax64(a, b) : vmin64(a, b); };
+  v = op(v, dpp_upd<0x111, 0xF>(v, v));
+  v = op(v, dpp_upd<0x112, 0xF>(v, v));
+  v = op(v, dpp_upd<0x114, 0xF>(v, v));
+  v = op(v, dpp_upd<0x118, 0xF>(v, v));
+  v = op(v, dpp_upd<0x142, 0xA>(v, v));
+  v = op(v, dpp_upd<0x143, 0xC>(v, v));
+  return v;
+}
+
 template <int OP>
 __device__ __forceinline__ double wave_scan_dpp(double v) {
   constexpr double id = OP == 0 ? 0.0 : (OP == 1 ? -__builtin_huge_val()

@@ -474,6 +474,11 @@ struct BetaOp {  // y ~ 1 + x (ret ~ mret): sums of 1, x, y, xx, xy, yy
     v[0] = ok ? 1.0 : 0.0; v[1] = x; v[2] = y; v[3] = x * x; v[4] = x * y; v[5] = y * y;
     return ok;
   }
+  // sanitised rows (inputs already 0 on an invalid row): no per-step selects
+  __device__ static void vals(float yv, float xv, double okd, double (&v)[NS]) {
+    const double x = xv, y = yv;
+    v[0] = okd; v[1] = x; v[2] = y; v[3] = x * x; v[4] = x * y; v[5] = y * y;
+  }
   __device__ static void emit(const double (&S)[NS], int n, int minp, int r, float* o0, float* o1) {
     float b = qnanf(), h = qnanf();
     if (n >= minp && n > 2) {
@@ -485,7 +490,9 @@ struct BetaOp {  // y ~ 1 + x (ret ~ mret): sums of 1, x, y, xx, xy, yy
       const double bb = cxy * frcp(vxx);
       const double ssr = fmax(S[0] * (vyy - bb * cxy), 0.0);
       b = (float)bb;
-      h = (float)fsqrt(ssr * frcp((double)(n - 2)));
+      // past the cancellation the tail is fp32: ~2 ulp vs the fp64 sqrt (the window
+      // subtraction already costs up to 2 bits), 3 instructions instead of 13
+      h = __builtin_amdgcn_sqrtf((float)ssr * __builtin_amdgcn_rcpf((float)(n - 2)));
     }
     o0[r] = b;
     o1[r] = h;
@@ -500,12 +507,16 @@ struct DastdOp {  // e = ret - mret: sums of 1, e, ee; weighted population std
     v[0] = ok ? 1.0 : 0.0; v[1] = e; v[2] = e * e;
     return ok;
   }
+  __device__ static void vals(float a, float bm, double okd, double (&v)[NS]) {
+    const double e = (double)a - (double)bm;
+    v[0] = okd; v[1] = e; v[2] = e * e;
+  }
   __device__ static void emit(const double (&S)[NS], int n, int minp, int r, float* o0, float*) {
     float o = qnanf();
     if (n >= minp) {
       const double iw = frcp(S[0]);
       const double m = S[1] * iw;
-      o = (float)fsqrt(fmax(S[2] * iw - m * m, 0.0));
+      o = __builtin_amdgcn_sqrtf((float)fmax(S[2] * iw - m * m, 0.0));
     }
     o0[r] = o;
   }
@@ -697,15 +708,276 @@ void launch_ew_pipe(const float* a, const float* b, const int* seg, int R, int W
                      s, a, b, seg, R, W, H, lam, minp, o0, o1, ntiles);
 }
 
-// A/B geometry of the anchored-prefix kernel (mfa_rolling_set_ew_variant): 0 = 8-row chunks x
-// 256 threads (2048-row tiles, default), 1 = 8 x 512 (4096-row tiles: half the halo re-read),
-// 2 = 16 x 256 (4096-row tiles, half the scan steps per row), 3 = the default geometry with the
-// software prefetch of the next tile (3 waves / SIMD).
+// ------------------------------------------------------------------------------------------
+// Sanitised-row variant of the anchored-prefix kernel (default since round 4).  The round-3
+// kernel spent ~40 VALU instructions per recurrence step, three steps per output row (chunk map,
+// own row, lagged row): the finiteness tests, zero selects of both fp64 inputs and the merge
+// copies of an exec-masked update (`if (d < 0) return`) were repeated at every step
+// (`profiles/r03_pmc_rolling.txt`: 237 VALU / row).  Here the load stage tests each row ONCE:
+// an invalid row's inputs become 0 and its validity / stock-start / outside state goes into a
+// 16-bit code, so a step is branch-free -- 2 conversions, the value products, 2 selects of the
+// decay factor and the NS fmas -- and an outside row is simply "invalid, no reset" (decay 1,
+// value 0).  The chunk-map scan composes branch-free (a zero multiplier instead of a masked
+// compose) and the window subtraction selects its lag factor instead of branching.
+// Same recurrence and summation order as ew_window_pipe_kernel.
+// ------------------------------------------------------------------------------------------
+// row code: bits 0-13 rows since the stock start (clamped), bit 14 both inputs finite, bit 15
+// outside [0, R) (its distance bits all set: neither a stock start nor valid)
+constexpr unsigned kCdD = 0x3FFFu, kCdOk = 0x4000u, kCdOut = 0xBFFFu;
+
+template <class Op, int C, int TR, bool PF = false, bool SL = true>
+__global__ __launch_bounds__(TR / C) __attribute__((amdgpu_waves_per_eu(4))) void
+ew_window_san_kernel(
+    const float* __restrict__ in_a, const float* __restrict__ in_b,
+    const int* __restrict__ seg_lo, int R, int W, int H, double lam, int minp,
+    float* __restrict__ o0, float* __restrict__ o1, int ntiles) {
+  constexpr int NS = Op::NS, NT = TR / C, LEN = TR + TR / C;
+  __shared__ float sa[LEN], sb[LEN];
+  __shared__ unsigned short sd[LEN];
+  __shared__ double carry[NT][NS];
+  __shared__ int ccnt[NT];
+  __shared__ EwMap<NS> wtot[NT / 64];
+  __shared__ double pw[257];
+  const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
+  for (int k = t; k <= W; k += NT) pw[k] = ipow(lam, k);
+  const int p0 = t * C;
+  auto code = [](float& a, float& b, int d) -> unsigned {
+    const bool ok = fin(a) && fin(b);
+    a = ok ? a : 0.f;
+    b = ok ? b : 0.f;
+    return (unsigned)min(d, (int)kCdD) | (ok ? kCdOk : 0u);
+  };
+  auto load = [&](int tile, float (&xa)[C], float (&xb)[C], unsigned (&xd)[C]) {
+    const int g = tile * (TR - H) - H + p0;
+    if (g >= 0 && g + C <= R) {
+#pragma unroll
+      for (int i = 0; i < C; i += 4) {
+        const float4 va = *(const float4*)(in_a + g + i), vb = *(const float4*)(in_b + g + i);
+        const int4 vs = *(const int4*)(seg_lo + g + i);
+        xa[i] = va.x; xa[i + 1] = va.y; xa[i + 2] = va.z; xa[i + 3] = va.w;
+        xb[i] = vb.x; xb[i + 1] = vb.y; xb[i + 2] = vb.z; xb[i + 3] = vb.w;
+        xd[i] = code(xa[i], xb[i], g + i - vs.x);
+        xd[i + 1] = code(xa[i + 1], xb[i + 1], g + i + 1 - vs.y);
+        xd[i + 2] = code(xa[i + 2], xb[i + 2], g + i + 2 - vs.z);
+        xd[i + 3] = code(xa[i + 3], xb[i + 3], g + i + 3 - vs.w);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < C; ++i) {
+        const int gi = g + i;
+        if (gi >= 0 && gi < R) {
+          xa[i] = in_a[gi];
+          xb[i] = in_b[gi];
+          xd[i] = code(xa[i], xb[i], gi - seg_lo[gi]);
+        } else {
+          xa[i] = 0.f;
+          xb[i] = 0.f;
+          xd[i] = kCdOut;
+        }
+      }
+    }
+  };
+  // one recurrence step E <- f E + v: f = 0 at a stock start, lam on a valid row, 1 otherwise
+  auto row = [&](float av, float bv, unsigned cd, double (&S)[NS], int& c) {
+    const bool st = (cd & kCdD) == 0u, ok = (cd & kCdOk) != 0u;
+    double v[NS];
+    Op::vals(av, bv, ok ? 1.0 : 0.0, v);
+    const double f = st ? 0.0 : (ok ? lam : 1.0);
+#pragma unroll
+    for (int k = 0; k < NS; ++k) S[k] = fma(f, S[k], v[k]);
+    c = (st ? 0 : c) + (ok ? 1 : 0);
+  };
+  int tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  float ra[C], rb[C];
+  unsigned rd[C];
+  if constexpr (PF) load(tile, ra, rb, rd);
+  for (; tile < ntiles; tile += gridDim.x) {
+    if constexpr (!PF) load(tile, ra, rb, rd);
+    const int g0 = tile * (TR - H) - H;
+#pragma unroll
+    for (int i = 0; i < C; ++i) {
+      const int q = ew_idx<C>(p0 + i);
+      sa[q] = ra[i];
+      sb[q] = rb[i];
+      sd[q] = (unsigned short)rd[i];
+    }
+    // PF: the next tile's loads are in flight through the whole tile (raw values: the
+    // sanitising code runs when they are consumed, so only 3 x C registers stay live)
+    float na[C], nb[C];
+    int ns[C];
+    const int nxt = tile + gridDim.x, gn = nxt * (TR - H) - H + p0;
+    const bool nfast = PF && nxt < ntiles && gn >= 0 && gn + C <= R;
+    if constexpr (PF) {
+      if (nfast) {
+#pragma unroll
+        for (int i = 0; i < C; i += 4) {
+          const float4 va = *(const float4*)(in_a + gn + i), vb = *(const float4*)(in_b + gn + i);
+          const int4 vs = *(const int4*)(seg_lo + gn + i);
+          na[i] = va.x; na[i + 1] = va.y; na[i + 2] = va.z; na[i + 3] = va.w;
+          nb[i] = vb.x; nb[i + 1] = vb.y; nb[i + 2] = vb.z; nb[i + 3] = vb.w;
+          ns[i] = vs.x; ns[i + 1] = vs.y; ns[i + 2] = vs.z; ns[i + 3] = vs.w;
+        }
+      }
+    }
+    // A. chunk map from registers (A = lam^valid rows since the last reset / chunk start)
+    EwMap<NS> m;
+    m.A = 1.0;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) m.B[k] = 0.0;
+    m.cnt = 0;
+    m.reset = 0;
+#pragma unroll
+    for (int i = 0; i < C; ++i) {
+      const unsigned cd = rd[i];
+      const bool st = (cd & kCdD) == 0u, ok = (cd & kCdOk) != 0u;
+      row(ra[i], rb[i], cd, m.B, m.cnt);
+      m.A = (st ? 1.0 : m.A) * (ok ? lam : 1.0);
+      m.reset |= st ? 1 : 0;
+    }
+    // B. inclusive scan over the NT chunks
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const EwMap<NS> pm = ew_shfl_up(m, d);
+      if (lane >= d) ew_compose(m, pm);
+    }
+    if (lane == 63) wtot[wid] = m;
+    __syncthreads();
+    for (int w = wid - 1; w >= 0; --w) ew_compose(m, wtot[w]);
+#pragma unroll
+    for (int k = 0; k < NS; ++k) carry[t][k] = m.B[k];
+    ccnt[t] = m.cnt;
+    __syncthreads();
+    // C. outputs: own rows (registers) and lagged rows r - W (LDS).  The empty asm hides the
+    // own rows' identity from the optimiser: otherwise it keeps phase A's fp64 values of all C
+    // rows alive across the scan for reuse (241 VGPRs, 2 waves / SIMD) instead of re-deriving
+    // them (~5 instructions per row, 4 waves / SIMD).
+#pragma unroll
+    for (int i = 0; i < C; ++i) asm volatile("" : "+v"(ra[i]), "+v"(rb[i]), "+v"(rd[i]));
+    if (p0 >= H) {
+      int lp = p0 - W;
+      asm volatile("" : "+v"(lp));  // per-tile address math: not 24 hoisted LDS addresses
+      const int lc = lp / C;
+      double E[NS], L[NS];
+#pragma unroll
+      for (int k = 0; k < NS; ++k) {
+        E[k] = t > 0 ? carry[t - 1][k] : 0.0;
+        L[k] = lc > 0 ? carry[lc - 1][k] : 0.0;
+      }
+      int ce = t > 0 ? ccnt[t - 1] : 0, cl = lc > 0 ? ccnt[lc - 1] : 0;
+      for (int p = lc * C; p < lp; ++p) {
+        const int q = ew_idx<C>(p);
+        row(sa[q], sb[q], sd[q], L, cl);
+      }
+      if constexpr (SL) {
+        // Sliding form: the window sum of row p0 - 1 from the prefixes (as below), then per row
+        // S <- f S + v_r - lam^nv v_(r-W): the lagged row costs its value and one fma per sum,
+        // not a second recurrence plus the prefix subtraction (~10 fewer VALU per row).  8 steps
+        // of drift: ~1e-15 relative, far below the fp32 outputs.
+        double S[NS];
+        {
+          const unsigned dp = sd[ew_idx<C>(p0 - 1)];
+          const bool in = (int)(dp & kCdD) >= W;
+          const double f = in ? pw[ce - cl] : 0.0;
+#pragma unroll
+          for (int k = 0; k < NS; ++k) S[k] = fma(-f, L[k], E[k]);
+        }
+#pragma unroll
+        for (int i = 0; i < C; ++i) {
+          const int r = g0 + p0 + i;
+          if (rd[i] & 0x8000u) break;  // past the end of the panel
+          row(ra[i], rb[i], rd[i], S, ce);
+          const int q = ew_idx<C>(lp + i);
+          const unsigned cq = sd[q];
+          const bool stq = (cq & kCdD) == 0u, okq = (cq & kCdOk) != 0u;
+          cl = (stq ? 0 : cl) + (okq ? 1 : 0);
+          // whole window inside the stock: row r - W leaves it; else the window started with
+          // the stock and S already is its sum
+          const bool in = (int)(rd[i] & kCdD) >= W;
+          const int nv = in ? ce - cl : ce;
+          const double w = in ? pw[nv] : 0.0;
+          double vq[NS];
+          Op::vals(sa[q], sb[q], okq ? 1.0 : 0.0, vq);
+#pragma unroll
+          for (int k = 0; k < NS; ++k) S[k] = fma(-w, vq[k], S[k]);
+          Op::emit(S, nv, minp, r, o0, o1);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < C; ++i) {
+          const int r = g0 + p0 + i;
+          if (rd[i] & 0x8000u) break;  // past the end of the panel
+          const int q = ew_idx<C>(lp + i);
+          row(sa[q], sb[q], sd[q], L, cl);
+          row(ra[i], rb[i], rd[i], E, ce);
+          // whole window inside the stock: subtract the lagged prefix; else the window is E
+          const bool in = (int)(rd[i] & kCdD) >= W;
+          const int nv = in ? ce - cl : ce;
+          const double f = in ? pw[nv] : 0.0;
+          double S[NS];
+#pragma unroll
+          for (int k = 0; k < NS; ++k) S[k] = fma(-f, L[k], E[k]);
+          Op::emit(S, nv, minp, r, o0, o1);
+        }
+      }
+    }
+    __syncthreads();  // LDS tile / carries are rewritten by the next iteration
+    if constexpr (PF) {
+      if (nfast) {
+#pragma unroll
+        for (int i = 0; i < C; ++i) {
+          ra[i] = na[i];
+          rb[i] = nb[i];
+          rd[i] = code(ra[i], rb[i], gn + i - ns[i]);
+        }
+      } else if (nxt < ntiles) {
+        load(nxt, ra, rb, rd);
+      }
+    }
+  }
+}
+
+template <class Op, int C, int TR, bool PF = false, bool SL = true>
+void launch_ew_san(const float* a, const float* b, const int* seg, int R, int W, int H,
+                   double lam, int minp, float* o0, float* o1, hipStream_t s) {
+  static int blocks = 0;
+  if (blocks == 0) {
+    int dev = 0, cus = 0, per = 0;
+    (void)hipGetDevice(&dev);
+    (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, ew_window_san_kernel<Op, C, TR, PF, SL>,
+                                                       TR / C, 0);
+    blocks = max(1, cus * max(per, 1));
+  }
+  const int ntiles = (R + TR - H - 1) / (TR - H);
+  hipLaunchKernelGGL((ew_window_san_kernel<Op, C, TR, PF, SL>), dim3(min(ntiles, blocks)), dim3(TR / C),
+                     0, s, a, b, seg, R, W, H, lam, minp, o0, o1, ntiles);
+}
+
+// A/B geometry of the anchored-prefix kernel (mfa_rolling_set_ew_variant): 0 = sanitised rows,
+// 8-row chunks x 256 threads (2048-row tiles; default: BETA 0.146, DASTD 0.106 ms at 5000 x
+// 3780, profiles/r04/rolling_ab.jsonl), 7 = the same with the next tile's loads in flight (no
+// faster: 128 VGPRs + a small spill), 5 = the round-3 kernel at the same geometry (and the
+// round-3 CMRA kernel), 1 = 8 x 512 (4096-row tiles: half the halo re-read), 2 = 16 x 256 (4096-row tiles,
+// half the scan steps per row), 3 = round-3 geometry with the software prefetch of the next
+// tile (3 waves / SIMD), 4 = 4096-row tiles without the prefetch, 6 = sanitised rows, 4096-row
+// tiles, 8 = sanitised rows, 4096-row tiles with the prefetch, 9 = variant 0 with the per-row
+// prefix subtraction instead of the sliding window update.
 int g_ew_variant = 0;
 template <class Op>
 void launch_ew(const float* a, const float* b, const int* seg, int R, int W, int H, double lam,
                int minp, float* o0, float* o1, hipStream_t s) {
-  if (g_ew_variant == 1)
+  if (g_ew_variant == 0)
+    launch_ew_san<Op, 8, 2048>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
+  else if (g_ew_variant == 6)
+    launch_ew_san<Op, 8, 4096>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
+  else if (g_ew_variant == 7)
+    launch_ew_san<Op, 8, 2048, true>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
+  else if (g_ew_variant == 8)
+    launch_ew_san<Op, 8, 4096, true>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
+  else if (g_ew_variant == 9)  // per-row prefix subtraction instead of the sliding form
+    launch_ew_san<Op, 8, 2048, false, false>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
+  else if (g_ew_variant == 1)
     launch_ew_pipe<Op, 8, 4096>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
   else if (g_ew_variant == 2)
     launch_ew_pipe<Op, 16, 4096>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
@@ -1016,6 +1288,123 @@ __global__ __launch_bounds__(kVhWaves * 64) void cmra_vhgw_kernel(const float* _
   }
 }
 
+// CMRA van Herk / Gil-Werman with TWO rows per lane (128-row blocks; default for W > 128).
+// cmra_vhgw_kernel spends ~5 fp64 DPP scans (sum, prefix max / min, suffix max / min) per
+// 64-row block, i.e. per row of each lane: 288 VALU instructions per row, VALU pipe ~97 % busy
+// (profiles/r03_pmc_rolling.txt).  Here a lane owns rows 2L, 2L+1 of a 128-row block: the pair is
+// combined in registers (sum, max / min of its two running sums) and the same five wave scans
+// run over the 64 pair aggregates, so each scan serves two rows; the scans are the lean
+// variants (common.h wave_scan_sum / wave_scan_ext: 4 instead of 5-6 VALU per step).  Prefix extrema of row 2L take
+// the exclusive scan (shifted one lane), suffix extrema of row 2L+1 the exclusive suffix; the NaN
+// masks are two ballots per block (even / odd rows).  A window of W >= 129 rows always starts in
+// an earlier block than it ends, so [a, r] = suffix(a's block) U full blocks U prefix(r's block).
+constexpr int kV2H = 256;
+constexpr int kV2Blk = 16;                      // staged 128-row blocks: 2048 rows, 32 KB of LDS
+constexpr int kV2Waves = 4;
+constexpr int kV2BPW = kV2Blk / kV2Waves;       // 4 blocks per wave
+constexpr int kV2Rows = kV2Blk * 128 - kV2H;    // 1792 output rows per workgroup
+static_assert(kV2Blk % kV2Waves == 0 && kV2H % 128 == 0, "block split");
+
+__device__ __forceinline__ unsigned long long shr64(unsigned long long m, int s) {
+  return s >= 64 ? 0ull : m >> s;
+}
+
+__global__ __launch_bounds__(kV2Waves * 64) void cmra_vh2_kernel(const float* __restrict__ lr,
+                                                                 const int* __restrict__ seg_lo,
+                                                                 int R, int W,
+                                                                 float* __restrict__ out) {
+  __shared__ double hmax[kV2Blk * 128], hmin[kV2Blk * 128];
+  __shared__ double bmax[kV2Blk], bmin[kV2Blk];
+  __shared__ unsigned long long nan0[kV2Blk], nan1[kV2Blk];
+  __shared__ double wtot[kV2Waves];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int g0 = blockIdx.x * kV2Rows - kV2H;
+  constexpr double kInf = __builtin_huge_val();
+  // pass 1: loads (the wave's rows and seg_lo of its output rows) and the wave total
+  float v[kV2BPW][2];
+  int sl[kV2BPW][2];
+  double tot = 0.0;
+#pragma unroll
+  for (int k = 0; k < kV2BPW; ++k) {
+    const int blk = wid * kV2BPW + k;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int g = g0 + blk * 128 + 2 * lane + i;
+      const bool in = g >= 0 && g < R;
+      v[k][i] = in ? lr[g] : qnanf();
+      sl[k][i] = (blk * 128 >= kV2H && in) ? seg_lo[g] : 0;
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kV2BPW; ++k)
+    tot += (fin(v[k][0]) ? (double)v[k][0] : 0.0) + (fin(v[k][1]) ? (double)v[k][1] : 0.0);
+  tot = wave_sum(tot);
+  if (lane == 0) wtot[wid] = tot;
+  __syncthreads();
+  double carry = 0.0;
+  for (int w = 0; w < wid; ++w) carry += wtot[w];
+  // pass 2: running sums, prefix extrema (registers), suffix extrema (LDS), NaN masks
+  const unsigned long long lt = (1ull << lane) - 1, le = lane == 63 ? ~0ull : (2ull << lane) - 1;
+  double gmax[kV2BPW][2], gmin[kV2BPW][2];
+  unsigned long long gn0[kV2BPW], gn1[kV2BPW];
+#pragma unroll
+  for (int k = 0; k < kV2BPW; ++k) {
+    const int blk = wid * kV2BPW + k;
+    const bool ok0 = fin(v[k][0]), ok1 = fin(v[k][1]);
+    const double d0 = ok0 ? (double)v[k][0] : 0.0, d1 = ok1 ? (double)v[k][1] : 0.0;
+    const double c1 = wave_scan_sum(d0 + d1) + carry, c0 = c1 - d1;
+    carry = readlane(c1, 63);
+    const double phi = vmax64(c0, c1), plo = vmin64(c0, c1);
+    const double Mx = wave_scan_ext<true>(phi), Mn = wave_scan_ext<false>(plo);
+    // every cross-lane read is executed by ALL lanes, the select comes after (a shuffle inside
+    // `lane ? ... : ...` runs with the lanes that skip it disabled, and a disabled lane is not a
+    // valid source)
+    const double Mxu = __shfl_up(Mx, 1, kWave), Mnu = __shfl_up(Mn, 1, kWave);
+    const double Mxe = lane ? Mxu : -kInf, Mne = lane ? Mnu : kInf;
+    gmax[k][0] = vmax64(Mxe, c0); gmax[k][1] = Mx;
+    gmin[k][0] = vmin64(Mne, c0); gmin[k][1] = Mn;
+    // suffix scans as prefix scans of the lane-reversed pair extrema
+    const double Rx = wave_scan_ext<true>(__shfl(phi, 63 - lane, kWave));
+    const double Rn = wave_scan_ext<false>(__shfl(plo, 63 - lane, kWave));
+    const double Sxi = __shfl(Rx, 63 - lane, kWave), Sni = __shfl(Rn, 63 - lane, kWave);
+    const double Sxu = __shfl(Rx, (62 - lane) & 63, kWave), Snu = __shfl(Rn, (62 - lane) & 63, kWave);
+    const double Sxe = lane < 63 ? Sxu : -kInf, Sne = lane < 63 ? Snu : kInf;
+    const int t0 = blk * 128 + 2 * lane;
+    hmax[t0] = Sxi; hmax[t0 + 1] = vmax64(c1, Sxe);
+    hmin[t0] = Sni; hmin[t0 + 1] = vmin64(c1, Sne);
+    const unsigned long long m0 = __ballot(!ok0), m1 = __ballot(!ok1);
+    gn0[k] = m0; gn1[k] = m1;
+    if (lane == 63) { bmax[blk] = Mx; bmin[blk] = Mn; }
+    if (lane == 0) { nan0[blk] = m0; nan1[blk] = m1; }
+  }
+  __syncthreads();
+  // pass 3: outputs (the first kV2H staged rows are halo)
+#pragma unroll
+  for (int k = 0; k < kV2BPW; ++k) {
+    const int blk = wid * kV2BPW + k;
+    if (blk * 128 < kV2H) continue;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int t = blk * 128 + 2 * lane + i, r = g0 + t;
+      if (r >= R) continue;
+      float o = qnanf();
+      if (r - W + 1 >= sl[k][i]) {
+        const int at = t - W + 1, ba = at >> 7, ain = at & 127;  // ba < blk since W > 128
+        double mx = vmax64(hmax[at], gmax[k][i]), mn = vmin64(hmin[at], gmin[k][i]);
+        bool bad = (shr64(nan0[ba], (ain + 1) >> 1) | shr64(nan1[ba], ain >> 1)) != 0 ||
+                   (gn0[k] & le) != 0 || (gn1[k] & (i ? le : lt)) != 0;
+        for (int j = ba + 1; j < blk; ++j) {
+          mx = vmax64(mx, bmax[j]);
+          mn = vmin64(mn, bmin[j]);
+          bad = bad || (nan0[j] | nan1[j]) != 0;
+        }
+        if (!bad) o = (float)(mx - mn);
+      }
+      out[r] = o;
+    }
+  }
+}
+
 // RSTR (factor_calculator.py:127-153): a NaN-renormalised positional-weight mean over the log
 // returns lr[k], k in [kl, kr] = [max(seg_lo, r - W + 1 - L), r - L], weights lam^(k - kl) (the
 // oldest row weighs 1; the reference's normalisation cancels the common base).  With the
@@ -1039,7 +1428,7 @@ __global__ __launch_bounds__(kRsWaves * 64) void rstr_ew_kernel(const float* __r
                                                                 int minp,
                                                                 float* __restrict__ out) {
   __shared__ double un[kRsBlk * 64], ud[kRsBlk * 64];
-  __shared__ unsigned short cs[kRsBlk * 64];  // valid-row suffix count in the wave region (<= 640)
+  __shared__ unsigned short cs[kRsBlk * 64];  // valid-row suffix count (region, then tile: <= 2560)
   __shared__ double pw[kRsWRows + 1];
   __shared__ double tn[kRsWaves], td[kRsWaves], in_n[kRsWaves], in_d[kRsWaves];
   __shared__ int tc[kRsWaves], in_c[kRsWaves];
@@ -1073,8 +1462,8 @@ __global__ __launch_bounds__(kRsWaves * 64) void rstr_ew_kernel(const float* __r
     const int t = (wid * kRsBPW + k) * 64 + 63 - lane;
     const float v = vv[k];
     const bool ok = fin(v);
-    const double zn = wave_scan_dpp<0>(ok ? lpn * (double)v : 0.0);
-    const double zd = wave_scan_dpp<0>(ok ? lpn : 0.0);
+    const double zn = wave_scan_sum(ok ? lpn * (double)v : 0.0);
+    const double zd = wave_scan_sum(ok ? lpn : 0.0);
     const unsigned long long M = __ballot(ok);
     const double Un = fma(lp, zn, lp1 * cn), Ud = fma(lp, zd, lp1 * cd);
     un[t] = Un;
@@ -1097,12 +1486,26 @@ __global__ __launch_bounds__(kRsWaves * 64) void rstr_ew_kernel(const float* __r
     }
   }
   __syncthreads();
+  // region-relative U / counts -> tile-absolute, once per row (the two window ends below then
+  // need no region lookup / integer division): the same fma as a per-read lookup, so the outputs
+  // are bitwise unchanged
+  {
+    const double fn = in_n[wid], fd = in_d[wid];
+    const int fc = in_c[wid];
+#pragma unroll
+    for (int k = 0; k < kRsBPW; ++k) {
+      const int t = (wid * kRsBPW + k) * 64 + lane;
+      const double f = pw[(wid + 1) * kRsWRows - t];
+      un[t] = fma(f, fn, un[t]);
+      ud[t] = fma(f, fd, ud[t]);
+      cs[t] = (unsigned short)(cs[t] + fc);
+    }
+  }
+  __syncthreads();
   auto full = [&](int t, double& n, double& d, int& c) {
-    const int w = t / kRsWRows;
-    const double f = pw[(w + 1) * kRsWRows - t];
-    n = fma(f, in_n[w], un[t]);
-    d = fma(f, in_d[w], ud[t]);
-    c = cs[t] + in_c[w];
+    n = un[t];
+    d = ud[t];
+    c = cs[t];
   };
 #pragma unroll
   for (int k = 0; k < kRsBPW; ++k) {
@@ -1265,7 +1668,10 @@ MFA_API int mfa_dastd(const float* ret, const float* mret, const int* seg_lo, in
 MFA_API int mfa_cmra(const float* lr, const int* seg_lo, int R, int W, int partial, float* out,
                      void* s) {
   if (R <= 0) return 0;
-  if (g_roll_mode == 0 && !partial && W > 64 && W - 1 <= kVhH)
+  if (g_roll_mode == 0 && !partial && W > 128 && W - 1 <= kV2H && g_ew_variant != 5)
+    hipLaunchKernelGGL(cmra_vh2_kernel, dim3((R + kV2Rows - 1) / kV2Rows), dim3(kV2Waves * 64), 0,
+                       (hipStream_t)s, lr, seg_lo, R, W, out);
+  else if (g_roll_mode == 0 && !partial && W > 64 && W - 1 <= kVhH)
     hipLaunchKernelGGL(cmra_vhgw_kernel, dim3((R + kVhRows - 1) / kVhRows), dim3(kVhWaves * 64), 0,
                        (hipStream_t)s, lr, seg_lo, R, W, out);
   else if (g_roll_mode != 1 && W <= 256 && W >= kChunk)

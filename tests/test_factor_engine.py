@@ -294,7 +294,9 @@ def test_cetop_ttm_run_path_equals_merge_path_and_falls_back():
 @pytest.mark.gpu
 def test_hip_cmra_rstr_window_edges(cuda):
     """The van Herk CMRA and backward-anchored RSTR kernels at the edges of their window ranges
-    (CMRA W = 65 / 257: just above one 64-row block / the 256-row halo; RSTR reach W + L - 1 =
+    (CMRA W = 65 / 128 / 129 / 257: just above one 64-row block, the last window of the one-row-
+    per-lane kernel, the first of the two-rows-per-lane kernel (a window spanning exactly two
+    128-row blocks), the 256-row halo; RSTR reach W + L - 1 =
     512 = the halo, W = 1, L = 1) == the direct per-row kernels, on ragged stocks with NaNs."""
     from llm_driven_multi_factor_model_amd import _native
     g = torch.Generator().manual_seed(21)
@@ -307,6 +309,9 @@ def test_hip_cmra_rstr_window_edges(cuda):
     l_ = lr.to(cuda)
     fns = {
         "cmra65": lambda: RL.cmra(l_, seg, 65),
+        "cmra128": lambda: RL.cmra(l_, seg, 128),
+        "cmra129": lambda: RL.cmra(l_, seg, 129),
+        "cmra200": lambda: RL.cmra(l_, seg, 200),
         "cmra257": lambda: RL.cmra(l_, seg, 257),
         "rstr_max_reach": lambda: RL.rstr(l_, seg, 512, 21, 126.0, 42),
         "rstr_w1": lambda: RL.rstr(l_, seg, 2, 1, 5.0, 1),

@@ -2,16 +2,16 @@
 # PMC of the default rolling kernels (tools/rolling_ab.py, 5000 x 3780): VALU / LDS activity.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"; export TMPDIR=/tmp
-O=gpurun_out/pmc_roll2; rm -rf $O; mkdir -p $O
+O=${O:-gpurun_out/pmc_roll2}; rm -rf $O; mkdir -p $O
 timeout -s KILL 150 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_WAIT_INST_ANY SQ_WAVES -d $O/a -o run --output-format csv -- python3 tools/rolling_ab.py > $O/a.log 2>&1 || exit 1
-python3 - <<'PY'
+O=$O python3 - <<'PY'
 import csv, glob, collections
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
-for f in glob.glob("gpurun_out/pmc_roll2/a/**/run_counter_collection.csv", recursive=True):
+for f in glob.glob(__import__("os").environ.get("O", "gpurun_out/pmc_roll2") + "/a/**/run_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         kn = r["Kernel_Name"]
-        if any(t in kn for t in ("ew_window_pipe", "vhgw", "rstr_ew")):
-            agg[kn.split("(")[0][-60:]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+        if any(t in kn for t in ("ew_window", "vhgw", "rstr_ew")):
+            agg[kn[:kn.rfind("(")].replace("(anonymous namespace)::", "")[-70:]][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in agg.items():
     v = {c: sum(x) / len(x) for c, x in d.items()}
     wc = v.get("SQ_WAVE_CYCLES", 1)
