@@ -10,7 +10,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
-# measured on 1x MI355X (ROCm 7.2), round 3 (profiles/r03_risk/perf_guards.log, r03_start/):
+# measured on 1x MI355X (ROCm 7.2), rounds 3-4 (profiles/r03_risk/, r04/):
 MEASURED = {
     # bench.py: fp64 storage, refine on, deterministic, graph replay: 0.384 ms / 2520 dates
     "xs_wls_fp64_reg_per_s": 6.55e6,
@@ -19,8 +19,13 @@ MEASURED = {
     "eigen_adjust_2520x100_ms": 14.45,
     # Newey-West expanding series, T = 2520, K = 42, q = 2
     "newey_west_2520_ms": 0.100,
-    # BETA/HSIGMA anchored-prefix kernel, 5000 x 3780 (Newton-reciprocal finishers, 4 waves / SIMD)
-    "beta_hsigma_5000x3780_ms": 0.173,
+    # window-descriptor kernels, 5000 x 3780, round 4 (profiles/r04/rolling_ab.jsonl): BETA/HSIGMA
+    # and DASTD sanitised-row sliding kernel, CMRA two-rows-per-lane van Herk, RSTR backward-
+    # anchored sums with tile-absolute prefixes
+    "beta_hsigma_5000x3780_ms": 0.146,
+    "dastd_5000x3780_ms": 0.106,
+    "cmra_5000x3780_ms": 0.098,
+    "rstr_5000x3780_ms": 0.101,
     # point-in-time trailing specific vol, 2520 x 5000, W = 252 (profiles/r03_risk/)
     "trailing_vol_2520x5000_ms": 1.075,
 }
@@ -102,7 +107,21 @@ def test_newey_west_scan_2520():
     assert ms < ceil, f"{ms:.4f} ms"
 
 
-def test_beta_hsigma_5000x3780():
+_ROLL_CALLS = {
+    # the factor engine's calls (factor_calculator.py:79-234 windows and half-lives)
+    "beta_hsigma": lambda P: ("mfa_beta_hsigma", P["ret"], P["mret"], P["seg"], P["R"], 252,
+                              0.5 ** (1 / 63), 42, P["o0"], P["o1"]),
+    "dastd": lambda P: ("mfa_dastd", P["ret"], P["mret"], P["seg"], P["R"], 252, 0.5 ** (1 / 42),
+                        42, P["o0"]),
+    "cmra": lambda P: ("mfa_cmra", P["lr"], P["seg"], P["R"], 252, 0, P["o0"]),
+    "rstr": lambda P: ("mfa_rstr", P["lr"], P["seg"], P["R"], 21, 483, 0.5 ** (1 / 126), 42,
+                       P["o0"]),
+}
+
+
+@pytest.mark.parametrize("kernel", list(_ROLL_CALLS))
+def test_rolling_kernels_5000x3780(kernel):
+    """The four window-descriptor kernels at 5000 stocks x 3780 days (flat rows, 2 % NaN)."""
     from llm_driven_multi_factor_model_amd import _native
     from llm_driven_multi_factor_model_amd.ops import rolling as RL
     N, T = 5000, 3780
@@ -114,15 +133,17 @@ def test_beta_hsigma_5000x3780():
     ret[torch.rand(R, device=dev, generator=g) < 0.02] = float("nan")
     mret = mkt[None, :].expand(N, T).reshape(-1).contiguous().float()
     seg = RL.seg_lo_from_codes(torch.arange(N, device=dev, dtype=torch.int32).repeat_interleave(T))
-    beta, hsig = torch.empty(R, device=dev), torch.empty(R, device=dev)
-    fn = lambda: _native.call("mfa_beta_hsigma", _native.ptr(ret), _native.ptr(mret),  # noqa: E731
-                              _native.ptr(seg), R, 252, 0.5 ** (1 / 63), 42, _native.ptr(beta),
-                              _native.ptr(hsig), _native.stream(dev))
+    lr = torch.log1p(ret)
+    o0, o1 = torch.empty(R, device=dev), torch.empty(R, device=dev)
+    P = {"ret": _native.ptr(ret), "mret": _native.ptr(mret), "seg": _native.ptr(seg),
+         "lr": _native.ptr(lr), "o0": _native.ptr(o0), "o1": _native.ptr(o1), "R": R}
+    args = _ROLL_CALLS[kernel](P)
+    fn = lambda: _native.call(*args, _native.stream(dev))  # noqa: E731
     _warm_clocks()
     ms = _time_ms(fn)
-    ceil = MEASURED["beta_hsigma_5000x3780_ms"] / SLACK
-    print(f"beta_hsigma {N}x{T}: {ms:.4f} ms (ceiling {ceil:.4f})")
-    assert torch.isfinite(beta).any()
+    ceil = MEASURED[f"{kernel}_5000x3780_ms"] / SLACK
+    print(f"{kernel} {N}x{T}: {ms:.4f} ms (ceiling {ceil:.4f})")
+    assert torch.isfinite(o0).any()
     assert ms < ceil, f"{ms:.4f} ms"
 
 
