@@ -79,7 +79,10 @@ def main() -> int:
     if use_cuda:
         torch.cuda.set_device(dev)
     backend = None
-    if world > 1:
+    # MFA_FORCE_PG=1 keeps the process group and the collectives at world size 1 (one rank over
+    # RCCL on one GPU: the all-gather next to the graph replays, the barrier, the MAX reduce)
+    coll = world > 1 or os.environ.get("MFA_FORCE_PG") == "1"
+    if coll:
         # MFA_BENCH_BACKEND=gloo rehearses the multi-rank flow with several ranks on ONE GPU;
         # the default on GPUs is nccl (= RCCL).
         backend = os.environ.get("MFA_BENCH_BACKEND") or ("nccl" if use_cuda else "gloo")
@@ -108,7 +111,7 @@ def main() -> int:
     def sync():
         if use_cuda:
             torch.cuda.synchronize(dev)
-        if world > 1:
+        if coll:
             dist.barrier()
 
     def make_runner(Dl):
@@ -120,9 +123,9 @@ def main() -> int:
         region (``drain``)."""
         sty, cap, ret = panel.styles[:Dl], panel.cap[:Dl], panel.ret[:Dl]
         ind = None if panel.ind is None else panel.ind[:Dl]
-        NB = 2 if world > 1 else 1
+        NB = 2 if coll else 1
         gathered = [torch.empty(world * Dl, K, dtype=torch.float64, device=dev)
-                    for _ in range(NB)] if world > 1 else None
+                    for _ in range(NB)] if coll else None
         outs, handles, graphs = [None] * NB, [None] * NB, [None] * NB
         ws = xs_wls_workspace(Dl, P, Q, dev, N) if use_cuda else None
         it = [0]
@@ -147,7 +150,7 @@ def main() -> int:
                 graphs[b].replay()
             else:
                 regress(b)
-            if world > 1:
+            if coll:
                 handles[b] = dist.all_gather_into_tensor(gathered[b], outs[b].f, async_op=True)
 
         for b in range(NB):
@@ -183,7 +186,7 @@ def main() -> int:
         sync()
         el = time.perf_counter() - t0
         elt = torch.tensor([el], dtype=torch.float64, device=dev)
-        if world > 1:
+        if coll:
             dist.all_reduce(elt, op=dist.ReduceOp.MAX)
         return float(elt.item())
 
@@ -255,7 +258,7 @@ def main() -> int:
                                   if use_cuda and rehearse else 1),
             },
         }), flush=True)
-    if world > 1:
+    if coll:
         dist.destroy_process_group()
     return 0
 

@@ -40,10 +40,11 @@ class DistContext:
     local_rank: int = 0
     device: torch.device = torch.device("cpu")
     backend: str | None = None
+    force: bool = False  # MFA_FORCE_PG=1: a one-rank process group still runs the collectives
 
     @property
     def enabled(self) -> bool:
-        return self.world > 1 and dist.is_available() and dist.is_initialized()
+        return (self.world > 1 or self.force) and dist.is_available() and dist.is_initialized()
 
 
 _CTX: DistContext | None = None
@@ -64,12 +65,16 @@ def init_distributed(backend: str | None = None, device: str | None = None) -> D
     if use_cuda:
         torch.cuda.set_device(dev)
     be = backend or rehearse or ("nccl" if use_cuda else "gloo")
-    if world > 1 and not dist.is_initialized():
+    # MFA_FORCE_PG=1 (under torchrun): a process group and every collective even at world size
+    # 1 -- on one GPU that runs the RCCL paths themselves (communicator init with device_id, the
+    # collectives on RCCL's stream next to captured graphs), which several ranks cannot do there
+    force = os.environ.get("MFA_FORCE_PG") == "1"
+    if (world > 1 or force) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
         kw = {"device_id": dev} if use_cuda and be == "nccl" else {}
         dist.init_process_group(be, rank=rank, world_size=world, timeout=collective_timeout(), **kw)
-    _CTX = DistContext(rank, world, local, dev, be if world > 1 else None)
+    _CTX = DistContext(rank, world, local, dev, be if (world > 1 or force) else None, force)
     return _CTX
 
 
