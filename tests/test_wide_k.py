@@ -130,3 +130,26 @@ def test_hip_bayes_shrink_wide_universe(cuda):
     ref = R.bayes_shrink(vol, cap)
     torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6, equal_nan=True)
     assert np.isnan(got[1, ::7].numpy()).all()
+
+
+def test_rocsolver_wrapper_rejects_host_tensors():
+    from llm_driven_multi_factor_model_amd.ops import rocsolver
+    with pytest.raises(TypeError):
+        rocsolver.syev_batched(torch.eye(3, dtype=torch.float64)[None])
+
+
+@pytest.mark.gpu
+def test_rocsolver_strided_batched_eigh(cuda):
+    """ops/rocsolver.py (the K > 64 probe utility): rocSOLVER's strided-batched syevd / syevj on
+    140 x 140 sample covariances == LAPACK eigenvalues, A V = V diag(w)."""
+    from llm_driven_multi_factor_model_amd.ops import rocsolver
+    g = torch.Generator().manual_seed(5)
+    X = torch.randn(6, 300, 140, generator=g, dtype=torch.float64)
+    A = (X.transpose(1, 2) @ X / 300).to(cuda)
+    wr = torch.linalg.eigvalsh(A.cpu())
+    for method, tol in (("syevd", 1e-11), ("syevj", 1e-9)):
+        w, V, info = rocsolver.syev_batched(A, method)
+        assert int(info.abs().sum()) == 0, method
+        torch.testing.assert_close(w.cpu(), wr, rtol=tol, atol=1e-13, msg=method)
+        R = A @ V - V * w[:, None, :]
+        assert float(R.abs().max()) < 1e-9, method
