@@ -878,7 +878,7 @@ ew_window_san_kernel(
         {
           const unsigned dp = sd[ew_idx<C>(p0 - 1)];
           const bool in = (int)(dp & kCdD) >= W;
-          const double f = in ? pw[ce - cl] : 0.0;
+          const double f = in ? pw[in ? ce - cl : 0] : 0.0;  // index in [0, W] even if not taken
 #pragma unroll
           for (int k = 0; k < NS; ++k) S[k] = fma(-f, L[k], E[k]);
         }
