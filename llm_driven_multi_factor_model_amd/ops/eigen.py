@@ -18,6 +18,7 @@ the normals come from Philox rather than MT19937 (bitwise parity with numpy is i
 from __future__ import annotations
 
 import contextlib
+import os
 import ctypes as C
 
 import torch
@@ -40,6 +41,8 @@ _native.register("mfa_eigen_bias_accumulate", [C.c_void_p, C.c_void_p, C.c_int, 
                                                 C.c_void_p, C.c_void_p])
 _native.register("mfa_philox_normals", [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_void_p,
                                          C.c_void_p])
+_native.register("mfa_eigen_bias_accumulate_wide", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                                     C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p])
 _native.register("mfa_eigen_finalize_sum", [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                              C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p,
                                              C.c_void_p, C.c_void_p])
@@ -52,6 +55,31 @@ TOL = 1e-15
 # eigen-decompositions go through rocSOLVER's batched symmetric solver in bounded chunks.
 WIDE_K = 64
 WIDE_CHUNK_DOUBLES = 1 << 27     # ~1 GB of fp64 per batched eigh / draw chunk
+# Bias statistic for 64 < K <= WIDE_HIP_MAX_K: "rocsolver" (batched syevd through torch, the
+# default) or "hip" (csrc/eigen_wide.hip: mode 5's tridiagonal solver on one 2-3-wave workgroup
+# per (date, sim); opt-in until measured on the GPU).  MFA_WIDE_BIAS selects it at import.
+WIDE_HIP_MAX_K = 144
+WIDE_BIAS_SOLVERS = ("rocsolver", "hip")
+_wide_solver = os.environ.get("MFA_WIDE_BIAS", "rocsolver")
+
+
+def set_wide_bias_solver(name: str) -> None:
+    """Select the bias-statistic solver for factor sets wider than one wave (process-wide)."""
+    global _wide_solver
+    if name not in WIDE_BIAS_SOLVERS:
+        raise ValueError(f"wide bias solver must be one of {WIDE_BIAS_SOLVERS}, got {name!r}")
+    _wide_solver = name
+
+
+@contextlib.contextmanager
+def using_wide_bias_solver(name: str):
+    global _wide_solver
+    old = _wide_solver
+    set_wide_bias_solver(name)
+    try:
+        yield
+    finally:
+        _wide_solver = old
 
 # Per-(date, sim) solver of the bias statistic (csrc/eigen.hip): "jacobi" = pair-block
 # tournament Jacobi carrying M = V^T D0 V; "tridiag" = Householder tridiagonalisation,
@@ -197,10 +225,13 @@ def _mc_cov_wide(M: int, K: int, T: int, seed: int, dev, m0: int) -> torch.Tenso
 def _bias_sum_wide(w, valid, Cz):
     """K > 64 on the device: S[d, k] = sum_m v_m[d, k] with v_m = diag(V^T D0 V) / lambda of
     A = sqrt(D0) C_z sqrt(D0) (the identity of SURVEY.md §2.3.4), eigen-decomposed by rocSOLVER
-    in chunks of (dates x sims); invalid dates give NaN."""
+    in chunks of (dates x sims), or by the multi-wave HIP solver (``set_wide_bias_solver``);
+    invalid dates give NaN."""
     D, K = w.shape
     M = Cz.shape[0]
     dev = w.device
+    if _wide_solver == "hip" and K <= WIDE_HIP_MAX_K:
+        return _bias_sum_wide_hip(w, valid, Cz)
     S = torch.zeros(D, K, dtype=torch.float64, device=dev)
     dd = torch.nonzero(valid).flatten()
     sq = torch.sqrt(w.clamp_min(0.0))
@@ -220,6 +251,25 @@ def _bias_sum_wide(w, valid, Cz):
             acc += v.view(ds.numel(), cz.shape[0], K).sum(1)
         S[ds] = acc
     S[~valid] = float("nan")
+    return S
+
+
+def _bias_sum_wide_hip(w, valid, Cz):
+    """The multi-wave HIP solver over chunks of sims (per-(date, sim) values: D x chunk x K
+    doubles at a time), each chunk summed into S in sim order."""
+    D, K = w.shape
+    M = Cz.shape[0]
+    dev = w.device
+    S = torch.zeros(D, K, dtype=torch.float64, device=dev)
+    wc = w.contiguous()
+    dv = valid.to(torch.int32).contiguous()
+    mc = max(1, min(M, WIDE_CHUNK_DOUBLES // max(1, D * K)))
+    ws = torch.empty(D * mc * K, dtype=torch.float64, device=dev)
+    for a in range(0, M, mc):
+        n = min(mc, M - a)
+        cz = Cz[a:a + n].contiguous()
+        _native.call("mfa_eigen_bias_accumulate_wide", _native.ptr(wc), _native.ptr(dv), D, K, n,
+                     _native.ptr(cz), _native.ptr(ws), _native.ptr(S), _native.stream(dev))
     return S
 
 

@@ -153,3 +153,54 @@ def test_rocsolver_strided_batched_eigh(cuda):
         torch.testing.assert_close(w.cpu(), wr, rtol=tol, atol=1e-13, msg=method)
         R = A @ V - V * w[:, None, :]
         assert float(R.abs().max()) < 1e-9, method
+
+
+@pytest.mark.gpu
+def test_hip_wide_bias_solver_matches_oracle(cuda):
+    """csrc/eigen_wide.hip (the opt-in "hip" wide solver): K = 42 on the 2-wave kernel equals the
+    one-wave mode-5 kernel, K = 140 on the 3-wave kernel equals the CPU fp64 oracle; an invalid
+    date gives NaN."""
+    from llm_driven_multi_factor_model_amd import _native
+    g = torch.Generator().manual_seed(9)
+    for K, D, M in ((42, 12, 8), (140, 6, 5)):
+        X = torch.randn(D, 400, K, generator=g, dtype=torch.float64)
+        F = X.transpose(1, 2) @ X / 400
+        F[2] = float("nan")
+        w, _ = eigen.eigh(F.to(cuda))
+        valid = torch.isfinite(w).all(-1)
+        w = torch.where(valid[:, None], w.clamp_min(0.0), w).contiguous()
+        Cz = eigen.mc_cov(M, K, 300, seed=3, device=cuda)
+        S = eigen._bias_sum_wide_hip(w, valid, Cz)
+        ref = eigen._bias_sum_reference(w.cpu(), valid.cpu(), Cz.cpu())
+        torch.testing.assert_close(S.cpu(), ref, rtol=1e-9, atol=1e-12, equal_nan=True, msg=str(K))
+        assert torch.isnan(S[2]).all() and torch.isfinite(S[valid]).all()
+        if K <= 64:
+            S5 = torch.zeros_like(S)
+            ws = torch.empty(D * M * K, dtype=torch.float64, device=cuda)
+            _native.call("mfa_eigen_bias_accumulate", _native.ptr(w),
+                         _native.ptr(valid.to(torch.int32).contiguous()), D, K, M, _native.ptr(Cz),
+                         eigen.MAX_SWEEPS, eigen.TOL, _native.ptr(ws), _native.ptr(S5),
+                         _native.stream(cuda))
+            torch.testing.assert_close(S, S5, rtol=1e-12, atol=1e-14, equal_nan=True)
+
+
+@pytest.mark.gpu
+def test_hip_wide_bias_solver_in_risk_model(cuda):
+    """RiskModel at K = 140 with the "hip" wide solver == the rocSOLVER path."""
+    D, N, P, Q, M = 200, 1000, 123, 16, 4
+    p = synthetic_panel(D, N, P, Q, seed=17, missing_frac=0.01, dtype=torch.float64)
+    cfg = preset("reference", eigen_sims=M, nw_half_life=1000.0, eigen_sim_length=300)
+    a = RiskModel(p.to(cuda), cfg).run()
+    with eigen.using_wide_bias_solver("hip"):
+        b = RiskModel(p.to(cuda), cfg).run()
+    assert torch.isfinite(a.eigen_bias[-1]).all()
+    torch.testing.assert_close(b.eigen_bias, a.eigen_bias, rtol=1e-9, atol=1e-12, equal_nan=True)
+    torch.testing.assert_close(b.eigen_cov, a.eigen_cov, rtol=1e-8, atol=1e-16, equal_nan=True)
+
+
+def test_wide_bias_solver_selection():
+    with pytest.raises(ValueError):
+        eigen.set_wide_bias_solver("lapack")
+    with eigen.using_wide_bias_solver("hip"):
+        assert eigen._wide_solver == "hip"
+    assert eigen._wide_solver in eigen.WIDE_BIAS_SOLVERS
