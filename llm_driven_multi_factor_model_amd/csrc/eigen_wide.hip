@@ -47,7 +47,7 @@ __host__ __device__ constexpr int wide_rows_doubles(int K) { return tri2_rows_do
 template <int KP, int NW>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1))) void
 mc_bias_wide_kernel(const double* __restrict__ D0, int K, int M, const double* __restrict__ Cz,
-                    const int* __restrict__ dvalid, double* __restrict__ vout) {
+                    const int* __restrict__ dvalid, double* __restrict__ vout, int abl) {
   static_assert(KP % 8 == 0 && KP <= NW * 64, "KP: multiple of 8, at most one row per lane");
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int d = blockIdx.x / M, m = blockIdx.x % M, t = threadIdx.x;
@@ -150,9 +150,19 @@ mc_bias_wide_kernel(const double* __restrict__ D0, int K, int M, const double* _
       __syncthreads();  // wb / red[1] / bc reused by the next step
     }
   };
-  [&]<int... G>(std::integer_sequence<int, G...>) {
-    (steps(std::integral_constant<int, 8 * G>{}), ...);
-  }(std::make_integer_sequence<int, KP / 8>{});
+  if ((abl & 4) == 0) {
+    [&]<int... G>(std::integer_sequence<int, G...>) {
+      (steps(std::integral_constant<int, 8 * G>{}), ...);
+    }(std::make_integer_sequence<int, KP / 8>{});
+  } else {  // timing ablation: T = the sorted diagonal with a weak coupling, no reflectors
+    const double g = gs[t];
+    if (t < KP) {
+      tb[t] = double2{g, t > 0 ? 1e-12 * g * g : 0.0};
+      be[t] = 1e-6 * g;
+      ta[t] = 0.0;
+    }
+    __syncthreads();
+  }
   // ---- 2. eigenvalue of rank t (descending), as mode 5 ----
   double lo_l = 0.0, hi_l = 0.0, b2max = 0.0;
   if (t < K) {
@@ -190,7 +200,7 @@ mc_bias_wide_kernel(const double* __restrict__ D0, int K, int M, const double* _
     if (cl <= jt) lo = fmax(lo, xl); else hi = fmin(hi, xl);
   }
   double lam = x;
-  if (t < K) {
+  if (t < K && (abl & 1) == 0) {
     int prev = -1;
     double sprev = __builtin_inf();
     for (int it = 0; it < 512; ++it) {
@@ -215,6 +225,10 @@ mc_bias_wide_kernel(const double* __restrict__ D0, int K, int M, const double* _
       if (cnt <= jt) lo = x; else hi = x;
     }
     lam = x;
+  }
+  if (abl & 2) {  // timing ablation: no eigenvectors / back-transform
+    if (t < K) vo[t] = lam;
+    return;
   }
   // ---- 3. eigenvector of T at lam: twisted factorisation in the y registers only ----
   double y[KP];
@@ -337,6 +351,9 @@ __global__ __launch_bounds__(64) void wide_bias_sum_kernel(const double* __restr
 // Wide factor sets: S[d][k] += sum over this call's M sims of v_m[d][k] for 2 < K <= 144 with the
 // multi-wave solver (one workgroup of 2 / 3 waves per (date, sim) for K <= 96 / 144); ws: D*M*K
 // doubles.  Invalid dates (dvalid[d] = 0) accumulate NaN.
+int g_wide_abl = 0;  // timing-only phase ablations (bits: 1 Laguerre, 2 eigenvectors, 4 Householder)
+MFA_API void mfa_eigen_wide_set_ablation(int abl) { g_wide_abl = abl; }
+
 MFA_API int mfa_eigen_bias_accumulate_wide(const double* D0, const int* dvalid, int D, int K,
                                            int M, const double* Cz, double* ws, double* S,
                                            void* stream) {
@@ -349,7 +366,7 @@ MFA_API int mfa_eigen_bias_accumulate_wide(const double* D0, const int* dvalid, 
     (void)hipFuncSetAttribute((const void*)mc_bias_wide_kernel<KP_, NW_>,                    \
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);         \
     hipLaunchKernelGGL((mc_bias_wide_kernel<KP_, NW_>), dim3(D * M), dim3(NW_ * 64), lds, s, \
-                       D0, K, M, Cz, dvalid, ws);                                            \
+                       D0, K, M, Cz, dvalid, ws, g_wide_abl);                                \
   } else
   MFA_WIDE(96, 2) MFA_WIDE(144, 3) {}
 #undef MFA_WIDE

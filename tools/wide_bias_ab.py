@@ -1,6 +1,6 @@
 """A/B of the wide-K (K = 140) bias statistic: rocSOLVER batched syevd (through torch) vs the
 multi-wave HIP solver (csrc/eigen_wide.hip), D dates x M sims, plus the max relative difference
-of the per-date sums.  Prints one JSON line per solver."""
+of the per-date sums and the HIP solver's phase ablations.  Prints JSON lines."""
 import json
 import os
 import sys
@@ -36,3 +36,22 @@ for name in ("hip", "rocsolver"):
                       "us_per_problem": round(ms * 1e3 / (D * M), 3)}), flush=True)
 rel = ((out["hip"] - out["rocsolver"]).abs() / out["rocsolver"].abs()).max().item()
 print(json.dumps({"max_rel_hip_vs_rocsolver": rel}), flush=True)
+# phase ablations of the HIP solver (timing only, outputs meaningless): 1 = no Laguerre,
+# 2 = no eigenvectors / back-transform, 3 = tridiagonalisation + setup, 4 = no Householder
+import ctypes  # noqa: E402
+from llm_driven_multi_factor_model_amd import _native  # noqa: E402
+_native.register("mfa_eigen_wide_set_ablation", [ctypes.c_int])
+abl_ms = {}
+try:
+    with eigen.using_wide_bias_solver("hip"):
+        for abl in (0, 1, 2, 3, 4, 6):
+            _native.lib().mfa_eigen_wide_set_ablation(abl)
+            eigen._bias_sum_wide(w, valid, Cz)
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            eigen._bias_sum_wide(w, valid, Cz)
+            torch.cuda.synchronize()
+            abl_ms[abl] = round((time.perf_counter() - t0) * 1e3, 2)
+finally:
+    _native.lib().mfa_eigen_wide_set_ablation(0)
+print(json.dumps({"hip_ablation_ms": abl_ms}), flush=True)
