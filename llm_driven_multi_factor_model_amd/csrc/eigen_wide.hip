@@ -328,6 +328,392 @@ mc_bias_wide_kernel(const double* __restrict__ D0, int K, int M, const double* _
   }
 }
 
+// ---------------- two lanes per row (wide variant 1) ----------------
+// The row-per-lane kernel needs 2 x KP registers for a 144-column row (a, then y): 32+ of them
+// live in AGPRs and the eigenvector phase spills to scratch, at one 3-wave workgroup per CU.
+// Here lanes 2i and 2i+1 share row i: lane half h holds columns [h HP, h HP + HP) (HP = KP / 2)
+// of the row in phase 1 and entries [h HP, h HP + HP) of the eigenvector in phases 3-4, so a lane
+// keeps HP = 72 doubles.  Row-level scalars (x, u, p, w, the eigenvalue) are computed by both
+// lanes of a pair with identical arithmetic; partial dot products over the two halves are
+// summed with one DPP lane swap (a + b == b + a bitwise); sequential recurrences that cross
+// the halves (the eigenvector below / above the twist) run over the upper / lower half in turn
+// and hand their carry to the partner lane.  Same operations in the same order as the
+// row-per-lane kernel except the two-half split of each dot product.
+__device__ __forceinline__ double pair_swap(double v) { return dpp_mov<0xB1>(v); }  // lane ^ 1
+__device__ __forceinline__ int pair_swap_i(int v) {
+  return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);
+}
+
+template <int KP, int NW>
+__global__ __launch_bounds__(NW * 64) void mc_bias_wide2_kernel(
+    const double* __restrict__ D0, int K, int M, const double* __restrict__ Cz,
+    const int* __restrict__ dvalid, double* __restrict__ vout, int abl) {
+  constexpr int HP = KP / 2;
+  static_assert(KP % 16 == 0 && KP <= NW * 32, "KP: multiple of 16, two lanes per row");
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int d = blockIdx.x / M, m = blockIdx.x % M, t = threadIdx.x;
+  const int i = t >> 1, h = t & 1;  // row, half
+  double* vo = vout + ((size_t)d * M + m) * K;
+  if (!dvalid[d]) {
+    for (int k = t; k < K; k += NW * 64) vo[k] = qnan();
+    return;
+  }
+  const int nrow = (tri2_rows_doubles<KP>(K) + 1) & ~1;
+  double* R = sm;                          // packed reflector rows
+  double* wb = R + nrow;                   // [KP] broadcast w; Sturm counts later
+  double2* tb = (double2*)(wb + KP);       // [KP] {alpha_i, beta_{i-1}^2}
+  double* be = (double*)(tb + KP);         // [KP] beta_i
+  double* ta = be + KP;                    // [KP] tau_s
+  double* dd = ta + KP;                    // [KP] sqrt(D0)
+  double* gs = dd + KP;                    // [KP] diagonal of A, descending; Laguerre x later
+  double* red = gs + KP;                   // [2][NW] block-reduction partials
+  double* bc = red + 2 * NW;               // [2] pivot-row broadcasts
+  const bool row_ok = i < K;
+  const int li = row_ok ? i : 0;
+  const bool lead = h == 0 && i < KP;      // the lane that writes row-indexed LDS slots
+  double a[HP];
+  const double* c = Cz + (size_t)m * K * K;
+  const double* d0 = D0 + (size_t)d * K;
+  const double di = row_ok ? sqrt(fmax(d0[li], 0.0)) : 0.0;
+  if (lead) dd[i] = di;
+  __syncthreads();
+#pragma unroll
+  for (int jj = 0; jj < HP; ++jj) {
+    const int j = h * HP + jj;
+    a[jj] = (j < K && row_ok) ? di * c[j * K + li] * dd[j] : 0.0;
+    if ((jj & 7) == 7) lds_batch();
+  }
+  {
+    const double g = row_ok ? di * c[li * K + li] * di : 0.0;
+    if (lead) wb[i] = g;
+    __syncthreads();
+    if (lead && row_ok) {
+      int rank = 0;
+      for (int j = 0; j < K; ++j) {
+        const double q = wb[j];
+        rank += (q > g) || (q == g && j < i);
+      }
+      gs[rank] = g;
+    }
+    __syncthreads();
+  }
+  // ---- 1. Householder tridiagonalisation ----
+  auto steps = [&](auto J0c) {
+    constexpr int J0 = decltype(J0c)::value;
+    constexpr int HS = J0 / HP;              // half holding columns J0 .. J0 + 7
+    constexpr int JL = J0 > HP ? J0 - HP : 0;  // first register of the static column range
+    for (int s = J0; s < J0 + 8 && s < K; ++s) {
+      double xo = a[J0 - HS * HP];
+#pragma unroll
+      for (int k = 1; k < 8; ++k) {
+        double tt = a[J0 - HS * HP + k];
+        asm volatile("" : "+v"(tt));
+        xo = s == J0 + k ? tt : xo;
+      }
+      const double xp = pair_swap(xo);
+      const double xs = h == HS ? xo : xp;   // column s of row i, on both lanes of the pair
+      const bool act = i > s && row_ok;
+      const double x = act ? xs : 0.0;
+      if (t == 2 * s) bc[0] = xs;
+      if (t == 2 * s + 2) bc[1] = xs;
+      const double sig = block_total<NW>(h == 0 && i > s + 1 && row_ok ? x * x : 0.0, red, t);
+      const double alpha = bc[0], x0 = s + 1 < K ? bc[1] : 0.0;
+      double u = 0.0, tau = 0.0, beta = x0;
+      if (sig != 0.0) {
+        const double n2 = fma(x0, x0, sig);
+        const double nrm = n2 * rsq_nr(n2);
+        beta = x0 >= 0.0 ? -nrm : nrm;
+        tau = rcp_nr(nrm * (nrm + fabs(x0)));
+        u = act ? (i == s + 1 ? x0 - beta : x) : 0.0;
+      }
+      double* us = R + tri2_row_off<KP>(s) - J0;  // us[j], j in [J0, KP)
+      if (s + 2 < K && lead && i >= J0) us[i] = u;
+      if (t == 0) {
+        tb[s] = double2{alpha, s > 0 ? be[s - 1] * be[s - 1] : 0.0};
+        be[s] = beta;
+        ta[s] = tau;
+      }
+      __syncthreads();
+      if (s + 2 >= K) us = R + tri2_row_off<KP>(J0) - J0;
+      const double* uh = us + h * HP;
+      double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+      for (int jj = JL; jj < HP; jj += 2) {
+        double2 uu = *(const double2*)(uh + jj);
+        if (jj < J0) uu = h ? uu : double2{0.0, 0.0};  // lower half left of the row: u = 0
+        p0 = fma(a[jj], uu.x, p0);
+        p1 = fma(a[jj + 1], uu.y, p1);
+        if (((jj - JL) & 7) == 6) lds_batch();
+      }
+      const double pl = p0 + p1, pr = pair_swap(pl);
+      const double p = act ? tau * (h ? pr + pl : pl + pr) : 0.0;
+      const double kk = 0.5 * tau * block_total<NW>(h == 0 ? u * p : 0.0, red + NW, t);
+      const double w = p - kk * u;
+      if (lead) wb[i] = w;
+      __syncthreads();
+      const double* wh = wb + h * HP;
+#pragma unroll
+      for (int jj = JL; jj < HP; jj += 2) {
+        const double2 ww = *(const double2*)(wh + jj);
+        double2 uu = *(const double2*)(uh + jj);
+        if (jj < J0) uu = h ? uu : double2{0.0, 0.0};
+        a[jj] = fma(-u, ww.x, fma(-w, uu.x, a[jj]));
+        a[jj + 1] = fma(-u, ww.y, fma(-w, uu.y, a[jj + 1]));
+        if (((jj - JL) & 7) == 6) lds_batch();
+      }
+      __syncthreads();
+    }
+  };
+  if ((abl & 4) == 0) {
+    [&]<int... G>(std::integer_sequence<int, G...>) {
+      (steps(std::integral_constant<int, 8 * G>{}), ...);
+    }(std::make_integer_sequence<int, KP / 8>{});
+  } else {
+    if (lead) {
+      const double g = gs[i];
+      tb[i] = double2{g, i > 0 ? 1e-12 * g * g : 0.0};
+      be[i] = 1e-6 * g;
+      ta[i] = 0.0;
+    }
+    __syncthreads();
+  }
+  // T padded to KP with decoupled rows (alpha = 1e300, beta = 0): the eigenvector recurrences
+  // below run over all KP entries without per-entry K tests (their unrolled K masks otherwise
+  // overflow the scalar registers); the padded pivots are ~1e300, their twist candidates never
+  // win and their eigenvector entries come out 0 (beta = 0).  Sturm counts still use K.
+  if (lead && i >= K) {
+    tb[i] = double2{1e300, 0.0};
+    be[i] = 0.0;
+  }
+  if (t == 0) be[K - 1] = 0.0;
+  // ---- 2. eigenvalue of rank i (descending), both lanes of the pair ----
+  double lo_l = 0.0, hi_l = 0.0, b2max = 0.0;
+  if (row_ok) {
+    const double ad = tb[i].x;
+    const double r = (i > 0 ? fabs(be[i - 1]) : 0.0) + (i + 1 < K ? fabs(be[i]) : 0.0);
+    lo_l = ad - r;
+    hi_l = ad + r;
+    b2max = tb[i].y;
+  } else {
+    lo_l = tb[0].x;
+    hi_l = tb[0].x;
+  }
+  const double gl = block_ext<NW, false>(lo_l, red, t);
+  const double gu = block_ext<NW, true>(hi_l, red + NW, t);
+  __syncthreads();
+  const double b2 = block_ext<NW, true>(b2max, red, t);
+  const double tnorm = fmax(fabs(gl), fabs(gu));
+  const double pivmin = 2.2250738585072014e-308 * fmax(1.0, b2);
+  constexpr double kEps = 2.220446049250313e-16;
+  const double abstol = 1e-22 * tnorm + pivmin;
+  const int jt = K - 1 - i;
+  double lo = gl - 2.0 * kEps * tnorm - pivmin, hi = gu + 2.0 * kEps * tnorm + pivmin;
+  double x = row_ok ? fmin(fmax(gs[li], lo), hi) : 0.5 * (lo + hi);
+  double G = 0.0, H = 0.0;
+  int cnt = sturm_gh_p(tb, K, x, G, H);
+  __syncthreads();
+  double* xsv = gs;
+  int* csv = (int*)wb;
+  if (lead) {
+    xsv[i] = x;
+    csv[i] = cnt;
+  }
+  __syncthreads();
+  for (int l = 0; l < K; ++l) {
+    const double xl = xsv[l];
+    const int cl = csv[l];
+    if (cl <= jt) lo = fmax(lo, xl); else hi = fmin(hi, xl);
+  }
+  double lam = x;
+  if (row_ok && (abl & 1) == 0) {
+    int prev = -1;
+    double sprev = __builtin_inf();
+    for (int it = 0; it < 512; ++it) {
+      bool lag = false;
+      double xn = 0.0;
+      if (cnt == jt || cnt == jt + 1) {
+        xn = laguerre_toward(x, G, H, K, cnt == jt);
+        double st = fabs(xn - x);
+        if (prev == cnt && st >= 1.5 * sprev) {
+          xn = fma(8.0, xn - x, x);
+          st *= 8.0;
+        }
+        lag = __builtin_isfinite(xn) && xn >= lo && xn <= hi;
+        if (lag && prev == cnt && st <= 1e-8 * fabs(x) && st <= 0.25 * sprev) { x = xn; break; }
+        sprev = lag ? st : __builtin_inf();
+      }
+      if (!lag) { xn = 0.5 * (lo + hi); sprev = __builtin_inf(); }
+      if (hi - lo <= 2.0 * kEps * (fabs(lo) + fabs(hi)) + abstol) { x = 0.5 * (lo + hi); break; }
+      prev = lag ? cnt : -1;
+      x = xn;
+      cnt = sturm_gh_p(tb, K, x, G, H);
+      if (cnt <= jt) lo = x; else hi = x;
+    }
+    lam = x;
+  }
+  if (abl & 2) {
+    if (lead && row_ok) vo[i] = lam;
+    return;
+  }
+  // ---- 3. eigenvector of T at lam, entries [h HP, h HP + HP) in this lane ----
+  double y[HP];
+  double nrm = 0.0;  // this half's sum of squares, the twist entry's 1 added at the end
+  {
+    // forward pivots of the whole recurrence, kept for this half
+    double dp = 0.0;
+#pragma unroll
+    for (int q = 0; q < KP; ++q) {
+      const double2 tt = tb[q];
+      dp = guard_pivot(q == 0 ? tt.x - lam : (tt.x - lam) - tt.y * rcp_nr1(dp), pivmin);
+      if (q < HP) y[q] = h == 0 ? dp : y[q];
+      else y[q - HP] = h == 1 ? dp : y[q - HP];
+      if ((q & 3) == 3) lds_batch();  // the table loads stay 4 steps ahead, not 144
+    }
+    // backward pivots of the whole recurrence; the twist candidates of this half
+    double dm = 0.0, gmin = __builtin_inf();
+    int r = -1;
+#pragma unroll
+    for (int q = KP - 1; q >= 0; --q) {
+      const double ai = tb[q].x - lam;
+      dm = guard_pivot(q == KP - 1 ? ai : ai - tb[q + 1].y * rcp_nr1(dm), pivmin);
+      const bool mine = (q < HP) == (h == 0);
+      const double yq = q < HP ? y[q] : y[q - HP];
+      const double g = fabs(yq + dm - ai);
+      if (mine && (r < 0 || g < gmin)) { gmin = g; r = q; }
+      if ((q & 3) == 0) lds_batch();
+    }
+    // the pair's twist: the upper half's candidate wins ties (the descending scan meets it first)
+    const double go = pair_swap(gmin);
+    const int ro = pair_swap_i(r);
+    const double gu2 = h ? gmin : go, gl2 = h ? go : gmin;
+    const int ru2 = h ? r : ro, rl2 = h ? ro : r;
+    r = (ru2 >= 0 && !(gl2 < gu2)) || rl2 < 0 ? ru2 : rl2;
+    // below the twist, descending: the upper half first, its carry handed to the lower half
+    double cz = 1.0;
+#pragma unroll
+    for (int q = KP - 1; q >= HP; --q) {
+      if (h == 1 && q < r) {
+        cz = -be[q] * cz * rcp_nr1(y[q - HP]);
+        nrm = fma(cz, cz, nrm);
+        y[q - HP] = cz;
+      }
+      if ((q & 3) == 0) lds_batch();
+    }
+    {
+      const double cu = pair_swap(cz);
+      if (h == 0) cz = r > HP ? cu : 1.0;
+    }
+#pragma unroll
+    for (int q = HP - 1; q >= 0; --q) {
+      if (h == 0 && q < r) {
+        cz = -be[q] * cz * rcp_nr1(y[q]);
+        nrm = fma(cz, cz, nrm);
+        y[q] = cz;
+      }
+      if ((q & 3) == 0) lds_batch();
+    }
+    // above the twist: backward pivots into this half's slots
+    dm = 0.0;
+#pragma unroll
+    for (int q = KP - 1; q >= 0; --q) {
+      if (q > r) {
+        const double ai = tb[q].x - lam;
+        dm = guard_pivot(q == KP - 1 ? ai : ai - tb[q + 1].y * rcp_nr1(dm), pivmin);
+        if (q < HP) y[q] = h == 0 ? dm : y[q];
+        else y[q - HP] = h == 1 ? dm : y[q - HP];
+      }
+      if ((q & 3) == 0) lds_batch();
+    }
+    // ascending from the twist: the lower half first, its carry handed to the upper half
+    cz = 1.0;
+#pragma unroll
+    for (int q = 0; q < HP; ++q) {
+      if (h == 0) {
+        if (q == r) y[q] = 1.0;
+        if (q > r) {
+          cz = -be[q - 1] * cz * rcp_nr1(y[q]);
+          nrm = fma(cz, cz, nrm);
+          y[q] = cz;
+        }
+      }
+      if ((q & 3) == 3) lds_batch();
+    }
+    {
+      const double cl = pair_swap(cz);
+      if (h == 1) cz = r < HP ? cl : 1.0;
+    }
+#pragma unroll
+    for (int q = HP; q < KP; ++q) {
+      if (h == 1) {
+        if (q == r) y[q - HP] = 1.0;
+        if (q > r) {
+          cz = -be[q - 1] * cz * rcp_nr1(y[q - HP]);
+          nrm = fma(cz, cz, nrm);
+          y[q - HP] = cz;
+        }
+      }
+      if ((q & 3) == 3) lds_batch();
+    }
+    const double no = pair_swap(nrm);
+    const double sc = rsq_nr(1.0 + (h ? no + nrm : nrm + no));
+#pragma unroll
+    for (int q = 0; q < HP; ++q) y[q] *= sc;
+    if (!row_ok) {
+#pragma unroll
+      for (int q = 0; q < HP; ++q) y[q] = 0.0;
+    }
+  }
+  // ---- 4. back-transform and the bias ratio ----
+  auto back = [&](auto J0c, int s_hi) {
+    constexpr int J0 = decltype(J0c)::value;
+    constexpr int JL = J0 > HP ? J0 - HP : 0;
+    for (int s = s_hi; s >= J0; --s) {
+      if (s + 2 >= K) continue;
+      const double tau = ta[s];
+      if (tau == 0.0) continue;
+      const double* uh = R + tri2_row_off<KP>(s) - J0 + h * HP;
+      double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+      for (int jj = JL; jj < HP; jj += 2) {
+        double2 uu = *(const double2*)(uh + jj);
+        if (jj < J0) uu = h ? uu : double2{0.0, 0.0};
+        t0 = fma(uu.x, y[jj], t0);
+        t1 = fma(uu.y, y[jj + 1], t1);
+        if (((jj - JL) & 7) == 6) lds_batch();
+      }
+      const double tl = t0 + t1, tr = pair_swap(tl);
+      const double f = tau * (h ? tr + tl : tl + tr);
+#pragma unroll
+      for (int jj = JL; jj < HP; jj += 2) {
+        double2 uu = *(const double2*)(uh + jj);
+        if (jj < J0) uu = h ? uu : double2{0.0, 0.0};
+        y[jj] = fma(-f, uu.x, y[jj]);
+        y[jj + 1] = fma(-f, uu.y, y[jj + 1]);
+        if (((jj - JL) & 7) == 6) lds_batch();
+      }
+    }
+  };
+  [&]<int... G>(std::integer_sequence<int, G...>) {
+    constexpr int NG = KP / 8;
+    (back(std::integral_constant<int, 8 * (NG - 1 - G)>{}, 8 * (NG - 1 - G) + 7), ...);
+  }(std::make_integer_sequence<int, KP / 8>{});
+  double v = 0.0;
+#pragma unroll
+  for (int jj = 0; jj < HP; ++jj) {
+    const double dj = dd[h * HP + jj];  // 0 for the padded entries
+    v = fma(dj * dj, y[jj] * y[jj], v);
+    if ((jj & 7) == 7) lds_batch();
+  }
+  const double vo2 = pair_swap(v);
+  if (lead && row_ok) vo[i] = (v + vo2) / lam;
+}
+
+size_t bias_wide2_lds(int K, int KP, int NW) {
+  int n = 0;
+  for (int s = 0; s + 2 < K; ++s) n += KP - 8 * (s / 8);
+  return ((size_t)((n + 1) & ~1) + 7 * KP + 2 * NW + 2) * sizeof(double);
+}
+
 size_t bias_wide_lds(int K, int KP, int NW) {
   int n = 0;
   for (int s = 0; s + 2 < K; ++s) n += KP - 8 * (s / 8);
@@ -352,7 +738,9 @@ __global__ __launch_bounds__(64) void wide_bias_sum_kernel(const double* __restr
 // multi-wave solver (one workgroup of 2 / 3 waves per (date, sim) for K <= 96 / 144); ws: D*M*K
 // doubles.  Invalid dates (dvalid[d] = 0) accumulate NaN.
 int g_wide_abl = 0;  // timing-only phase ablations (bits: 1 Laguerre, 2 eigenvectors, 4 Householder)
+int g_wide_variant = 0;  // 0 = one lane per row, 1 = two lanes per row (K > 96; A/B until measured)
 MFA_API void mfa_eigen_wide_set_ablation(int abl) { g_wide_abl = abl; }
+MFA_API void mfa_eigen_wide_set_variant(int v) { g_wide_variant = v; }
 
 MFA_API int mfa_eigen_bias_accumulate_wide(const double* D0, const int* dvalid, int D, int K,
                                            int M, const double* Cz, double* ws, double* S,
@@ -360,6 +748,15 @@ MFA_API int mfa_eigen_bias_accumulate_wide(const double* D0, const int* dvalid, 
   if (D <= 0 || M <= 0) return 0;
   if (K < 3 || K > 144) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
+  if (g_wide_variant == 1 && K > 96) {
+    const size_t lds = bias_wide2_lds(K, 144, 5);
+    (void)hipFuncSetAttribute((const void*)mc_bias_wide2_kernel<144, 5>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((mc_bias_wide2_kernel<144, 5>), dim3(D * M), dim3(5 * 64), lds, s, D0, K, M,
+                       Cz, dvalid, ws, g_wide_abl);
+    hipLaunchKernelGGL(wide_bias_sum_kernel, dim3(D), dim3(64), 0, s, ws, K, M, S);
+    return (int)hipGetLastError();
+  }
 #define MFA_WIDE(KP_, NW_)                                                                     \
   if (K <= KP_) {                                                                            \
     const size_t lds = bias_wide_lds(K, KP_, NW_);                                           \

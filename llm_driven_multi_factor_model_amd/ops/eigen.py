@@ -43,6 +43,7 @@ _native.register("mfa_philox_normals", [C.c_int, C.c_int, C.c_int, C.c_int, C.c_
                                          C.c_void_p])
 _native.register("mfa_eigen_bias_accumulate_wide", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p])
+_native.register("mfa_eigen_wide_set_variant", [C.c_int])
 _native.register("mfa_eigen_finalize_sum", [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                              C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p,
                                              C.c_void_p, C.c_void_p])
@@ -71,6 +72,17 @@ def set_wide_bias_solver(name: str) -> None:
     if name not in WIDE_BIAS_SOLVERS:
         raise ValueError(f"wide bias solver must be one of {WIDE_BIAS_SOLVERS}, got {name!r}")
     _wide_solver = name
+
+
+# Layout of the "hip" wide solver: "row" = one lane per matrix row (default), "pair" = two
+# lanes per row (half the registers per lane: no spills, 5 waves per problem; A/B).
+WIDE_LAYOUTS = {"row": 0, "pair": 1}
+
+
+def set_wide_kernel_layout(name: str) -> None:
+    if name not in WIDE_LAYOUTS:
+        raise ValueError(f"wide kernel layout must be one of {sorted(WIDE_LAYOUTS)}, got {name!r}")
+    _native.lib().mfa_eigen_wide_set_variant(WIDE_LAYOUTS[name])
 
 
 @contextlib.contextmanager

@@ -156,13 +156,22 @@ def test_rocsolver_strided_batched_eigh(cuda):
 
 
 @pytest.mark.gpu
-def test_hip_wide_bias_solver_matches_oracle(cuda):
-    """csrc/eigen_wide.hip (the opt-in "hip" wide solver): K = 42 on the 2-wave kernel equals the
-    one-wave mode-5 kernel, K = 140 on the 3-wave kernel equals the CPU fp64 oracle; an invalid
-    date gives NaN."""
+@pytest.mark.parametrize("layout", ["row", "pair"])
+def test_hip_wide_bias_solver_matches_oracle(cuda, layout):
+    """csrc/eigen_wide.hip (the "hip" wide solver): K = 42 on the 2-wave kernel equals the
+    one-wave mode-5 kernel, K = 100 / 140 equal the CPU fp64 oracle, with one lane per row and
+    with two lanes per row (K > 96); an invalid date gives NaN."""
     from llm_driven_multi_factor_model_amd import _native
     g = torch.Generator().manual_seed(9)
-    for K, D, M in ((42, 12, 8), (140, 6, 5)):
+    eigen.set_wide_kernel_layout(layout)
+    try:
+        _wide_oracle_cases(cuda, g, _native)
+    finally:
+        eigen.set_wide_kernel_layout("row")
+
+
+def _wide_oracle_cases(cuda, g, _native):
+    for K, D, M in ((42, 12, 8), (100, 5, 4), (140, 6, 5)):
         X = torch.randn(D, 400, K, generator=g, dtype=torch.float64)
         F = X.transpose(1, 2) @ X / 400
         F[2] = float("nan")

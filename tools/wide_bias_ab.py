@@ -23,8 +23,9 @@ valid = torch.isfinite(w).all(-1)
 w = w.clamp_min(0.0).contiguous()
 Cz = eigen.mc_cov(M, K, 300, seed=2, device=dev)
 out = {}
-for name in ("hip", "rocsolver"):
-    with eigen.using_wide_bias_solver(name):
+for name in ("hip", "hip_pair", "rocsolver"):
+    eigen.set_wide_kernel_layout("pair" if name == "hip_pair" else "row")
+    with eigen.using_wide_bias_solver("hip" if name.startswith("hip") else name):
         S = eigen._bias_sum_wide(w, valid, Cz)  # warm-up (kernel load, workspace)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
@@ -34,8 +35,10 @@ for name in ("hip", "rocsolver"):
     out[name] = S
     print(json.dumps({"solver": name, "K": K, "D": D, "M": M, "ms": round(ms, 2),
                       "us_per_problem": round(ms * 1e3 / (D * M), 3)}), flush=True)
-rel = ((out["hip"] - out["rocsolver"]).abs() / out["rocsolver"].abs()).max().item()
-print(json.dumps({"max_rel_hip_vs_rocsolver": rel}), flush=True)
+eigen.set_wide_kernel_layout("row")
+for name in ("hip", "hip_pair"):
+    rel = ((out[name] - out["rocsolver"]).abs() / out["rocsolver"].abs()).max().item()
+    print(json.dumps({f"max_rel_{name}_vs_rocsolver": rel}), flush=True)
 # phase ablations of the HIP solver (timing only, outputs meaningless): 1 = no Laguerre,
 # 2 = no eigenvectors / back-transform, 3 = tridiagonalisation + setup, 4 = no Householder
 import ctypes  # noqa: E402
@@ -44,14 +47,17 @@ _native.register("mfa_eigen_wide_set_ablation", [ctypes.c_int])
 abl_ms = {}
 try:
     with eigen.using_wide_bias_solver("hip"):
-        for abl in (0, 1, 2, 3, 4, 6):
-            _native.lib().mfa_eigen_wide_set_ablation(abl)
-            eigen._bias_sum_wide(w, valid, Cz)
-            torch.cuda.synchronize()
-            t0 = time.perf_counter()
-            eigen._bias_sum_wide(w, valid, Cz)
-            torch.cuda.synchronize()
-            abl_ms[abl] = round((time.perf_counter() - t0) * 1e3, 2)
+        for layout in ("row", "pair"):
+            eigen.set_wide_kernel_layout(layout)
+            for abl in (0, 1, 2, 3, 4, 6):
+                _native.lib().mfa_eigen_wide_set_ablation(abl)
+                eigen._bias_sum_wide(w, valid, Cz)
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                eigen._bias_sum_wide(w, valid, Cz)
+                torch.cuda.synchronize()
+                abl_ms[f"{layout}_{abl}"] = round((time.perf_counter() - t0) * 1e3, 2)
 finally:
     _native.lib().mfa_eigen_wide_set_ablation(0)
+    eigen.set_wide_kernel_layout("row")
 print(json.dumps({"hip_ablation_ms": abl_ms}), flush=True)
