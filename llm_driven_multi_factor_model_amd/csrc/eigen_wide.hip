@@ -20,6 +20,13 @@ using namespace mfa;
 // every cross-wave LDS exchange is behind a barrier (4 per Householder step).  Replaces
 // rocSOLVER's batched syevd (~27 us per 140 x 140 problem at the GPU's throughput) for the bias
 // statistic; eigenvalues, eigenvectors and back-transform are per lane as before.
+#ifndef MFA_WIDE_ROUNDS
+#define MFA_WIDE_ROUNDS 0
+#endif
+// multisection rounds before the Laguerre loop (0 = off: not yet measured on the GPU; the
+// Laguerre phase is ~1/3 of the K = 140 solver, profiles/r04/wide_bias_ab.jsonl)
+constexpr int kWideRounds = MFA_WIDE_ROUNDS;
+
 template <int NW>
 __device__ __forceinline__ double block_total(double v, double* red, int t) {
   v = wave_total(v);
@@ -198,6 +205,27 @@ mc_bias_wide_kernel(const double* __restrict__ D0, int K, int M, const double* _
     const double xl = xsv[l];
     const int cl = csv[l];
     if (cl <= jt) lo = fmax(lo, xl); else hi = fmin(hi, xl);
+  }
+  // multisection: every lane samples the count at its bracket's midpoint and every lane
+  // tightens its bracket with all K samples (the diagonal is a poor guess when C_z is far from
+  // the identity, e.g. T_sim ~ 2 K: the Laguerre loop otherwise starts with long bisections)
+  for (int rd = 0; rd < kWideRounds; ++rd) {
+    const double xm = 0.5 * (lo + hi);
+    double Gm, Hm;
+    const int cm = sturm_gh_p(tb, K, xm, Gm, Hm);
+    __syncthreads();
+    xsv[t] = xm;
+    csv[t] = cm;
+    __syncthreads();
+    for (int l = 0; l < K; ++l) {
+      const double xl = xsv[l];
+      const int cl = csv[l];
+      if (cl <= jt) lo = fmax(lo, xl); else hi = fmin(hi, xl);
+    }
+  }
+  if (kWideRounds > 0 && !(x > lo && x < hi)) {  // the guess fell out: restart mid-bracket
+    x = 0.5 * (lo + hi);
+    cnt = sturm_gh_p(tb, K, x, G, H);
   }
   double lam = x;
   if (t < K && (abl & 1) == 0) {
@@ -524,6 +552,26 @@ __global__ __launch_bounds__(NW * 64) void mc_bias_wide2_kernel(
     const int cl = csv[l];
     if (cl <= jt) lo = fmax(lo, xl); else hi = fmin(hi, xl);
   }
+  for (int rd = 0; rd < kWideRounds; ++rd) {  // multisection, as in the row kernel
+    const double xm = 0.5 * (lo + hi);
+    double Gm, Hm;
+    const int cm = sturm_gh_p(tb, K, xm, Gm, Hm);
+    __syncthreads();
+    if (lead) {
+      xsv[i] = xm;
+      csv[i] = cm;
+    }
+    __syncthreads();
+    for (int l = 0; l < K; ++l) {
+      const double xl = xsv[l];
+      const int cl = csv[l];
+      if (cl <= jt) lo = fmax(lo, xl); else hi = fmin(hi, xl);
+    }
+  }
+  if (kWideRounds > 0 && !(x > lo && x < hi)) {
+    x = 0.5 * (lo + hi);
+    cnt = sturm_gh_p(tb, K, x, G, H);
+  }
   double lam = x;
   if (row_ok && (abl & 1) == 0) {
     int prev = -1;
@@ -738,7 +786,8 @@ __global__ __launch_bounds__(64) void wide_bias_sum_kernel(const double* __restr
 // multi-wave solver (one workgroup of 2 / 3 waves per (date, sim) for K <= 96 / 144); ws: D*M*K
 // doubles.  Invalid dates (dvalid[d] = 0) accumulate NaN.
 int g_wide_abl = 0;  // timing-only phase ablations (bits: 1 Laguerre, 2 eigenvectors, 4 Householder)
-int g_wide_variant = 0;  // 0 = one lane per row, 1 = two lanes per row (K > 96; A/B until measured)
+int g_wide_variant = 1;  // 1 = two lanes per row for K > 96 (default: 26.9 vs 28.3 ms at K = 140,
+                         // 60 x 100 problems, no spills), 0 = one lane per row
 MFA_API void mfa_eigen_wide_set_ablation(int abl) { g_wide_abl = abl; }
 MFA_API void mfa_eigen_wide_set_variant(int v) { g_wide_variant = v; }
 

@@ -167,7 +167,7 @@ def test_hip_wide_bias_solver_matches_oracle(cuda, layout):
     try:
         _wide_oracle_cases(cuda, g, _native)
     finally:
-        eigen.set_wide_kernel_layout("row")
+        eigen.set_wide_kernel_layout("pair")
 
 
 def _wide_oracle_cases(cuda, g, _native):

@@ -35,7 +35,7 @@ for name in ("hip", "hip_pair", "rocsolver"):
     out[name] = S
     print(json.dumps({"solver": name, "K": K, "D": D, "M": M, "ms": round(ms, 2),
                       "us_per_problem": round(ms * 1e3 / (D * M), 3)}), flush=True)
-eigen.set_wide_kernel_layout("row")
+eigen.set_wide_kernel_layout("pair")
 for name in ("hip", "hip_pair"):
     rel = ((out[name] - out["rocsolver"]).abs() / out["rocsolver"].abs()).max().item()
     print(json.dumps({f"max_rel_{name}_vs_rocsolver": rel}), flush=True)
@@ -59,5 +59,5 @@ try:
                 abl_ms[f"{layout}_{abl}"] = round((time.perf_counter() - t0) * 1e3, 2)
 finally:
     _native.lib().mfa_eigen_wide_set_ablation(0)
-    eigen.set_wide_kernel_layout("row")
+    eigen.set_wide_kernel_layout("pair")
 print(json.dumps({"hip_ablation_ms": abl_ms}), flush=True)
