@@ -481,6 +481,29 @@ struct BetaOp {  // y ~ 1 + x (ret ~ mret): sums of 1, x, y, xx, xy, yy
     const double x = xv, y = yv;
     v[0] = okd; v[1] = x; v[2] = y; v[3] = x * x; v[4] = x * y; v[5] = y * y;
   }
+  // ew_window_san_kernel: the weight sum of a window is implied by its valid count n
+  // (sum_(k<n) lam^k, a table), so only the 5 data sums x, y, xx, xy, yy are carried
+  static constexpr int NSX = 5;
+  __device__ static void vals_x(float yv, float xv, double (&v)[NSX]) {
+    const double x = xv, y = yv;
+    v[0] = x; v[1] = y; v[2] = x * x; v[3] = x * y; v[4] = y * y;
+  }
+  __device__ static void emit_x(const double (&S)[NSX], double iw, int n, int minp, int r,
+                                float* o0, float* o1) {
+    float b = qnanf(), h = qnanf();
+    if (n >= minp && n > 2) {
+      const double mx = S[0] * iw, my = S[1] * iw;
+      const double vxx = S[2] * iw - mx * mx;
+      const double cxy = S[3] * iw - mx * my;
+      const double bb = cxy * frcp(vxx);
+      // Sw (vyy - b cxy) with Sw vyy = Syy - Sy my and Sw cxy = Sxy - Sx my
+      const double ssr = fmax((S[4] - S[1] * my) - bb * (S[3] - S[0] * my), 0.0);
+      b = (float)bb;
+      h = __builtin_amdgcn_sqrtf((float)ssr * __builtin_amdgcn_rcpf((float)(n - 2)));
+    }
+    o0[r] = b;
+    o1[r] = h;
+  }
   __device__ static void emit(const double (&S)[NS], int n, int minp, int r, float* o0, float* o1) {
     float b = qnanf(), h = qnanf();
     if (n >= minp && n > 2) {
@@ -512,6 +535,20 @@ struct DastdOp {  // e = ret - mret: sums of 1, e, ee; weighted population std
   __device__ static void vals(float a, float bm, double okd, double (&v)[NS]) {
     const double e = (double)a - (double)bm;
     v[0] = okd; v[1] = e; v[2] = e * e;
+  }
+  static constexpr int NSX = 2;  // ew_window_san_kernel: the weight sum comes from the count
+  __device__ static void vals_x(float a, float bm, double (&v)[NSX]) {
+    const double e = (double)a - (double)bm;
+    v[0] = e; v[1] = e * e;
+  }
+  __device__ static void emit_x(const double (&S)[NSX], double iw, int n, int minp, int r,
+                                float* o0, float*) {
+    float o = qnanf();
+    if (n >= minp) {
+      const double m = S[0] * iw;
+      o = __builtin_amdgcn_sqrtf((float)fmax(S[1] * iw - m * m, 0.0));
+    }
+    o0[r] = o;
   }
   __device__ static void emit(const double (&S)[NS], int n, int minp, int r, float* o0, float*) {
     float o = qnanf();
@@ -720,8 +757,9 @@ void launch_ew_pipe(const float* a, const float* b, const int* seg, int R, int W
 // 16-bit code, so a step is branch-free -- 2 conversions, the value products, 2 selects of the
 // decay factor and the NS fmas -- and an outside row is simply "invalid, no reset" (decay 1,
 // value 0).  The chunk-map scan composes branch-free (a zero multiplier instead of a masked
-// compose) and the window subtraction selects its lag factor instead of branching.
-// Same recurrence and summation order as ew_window_pipe_kernel.
+// compose) and the window subtraction selects its lag factor instead of branching.  The
+// window's weight sum is implied by its valid count (a table), so BETA carries 5 sums (not 6)
+// and DASTD 2 (not 3) through the recurrences, the scan and the carries.
 // ------------------------------------------------------------------------------------------
 // row code: bits 0-13 rows since the stock start (clamped), bit 14 both inputs finite, bit 15
 // outside [0, R) (its distance bits all set: neither a stock start nor valid)
@@ -733,15 +771,24 @@ ew_window_san_kernel(
     const float* __restrict__ in_a, const float* __restrict__ in_b,
     const int* __restrict__ seg_lo, int R, int W, int H, double lam, int minp,
     float* __restrict__ o0, float* __restrict__ o1, int ntiles) {
-  constexpr int NS = Op::NS, NT = TR / C, LEN = TR + TR / C;
+  constexpr int NS = Op::NSX, NT = TR / C, LEN = TR + TR / C;
   __shared__ float sa[LEN], sb[LEN];
   __shared__ unsigned short sd[LEN];
   __shared__ double carry[NT][NS];
   __shared__ int ccnt[NT];
   __shared__ EwMap<NS> wtot[NT / 64];
   __shared__ double pw[257];
+  __shared__ double isw[257];  // 1 / sum_(k<n) lam^k: the weight sum of a window with n valid rows
   const int t = threadIdx.x, lane = t & 63, wid = t >> 6;
   for (int k = t; k <= W; k += NT) pw[k] = ipow(lam, k);
+  if (t == 0) {  // read after the tile loop's first barriers
+    double sw = 0.0, p = 1.0;
+    for (int k = 0; k <= W; ++k) {
+      isw[k] = k ? 1.0 / sw : 0.0;
+      sw += p;
+      p *= lam;
+    }
+  }
   const int p0 = t * C;
   auto code = [](float& a, float& b, int d) -> unsigned {
     const bool ok = fin(a) && fin(b);
@@ -783,7 +830,7 @@ ew_window_san_kernel(
   auto row = [&](float av, float bv, unsigned cd, double (&S)[NS], int& c) {
     const bool st = (cd & kCdD) == 0u, ok = (cd & kCdOk) != 0u;
     double v[NS];
-    Op::vals(av, bv, ok ? 1.0 : 0.0, v);
+    Op::vals_x(av, bv, v);
     const double f = st ? 0.0 : (ok ? lam : 1.0);
 #pragma unroll
     for (int k = 0; k < NS; ++k) S[k] = fma(f, S[k], v[k]);
@@ -899,10 +946,10 @@ ew_window_san_kernel(
           const int nv = in ? ce - cl : ce;
           const double w = in ? pw[nv] : 0.0;
           double vq[NS];
-          Op::vals(sa[q], sb[q], okq ? 1.0 : 0.0, vq);
+          Op::vals_x(sa[q], sb[q], vq);
 #pragma unroll
           for (int k = 0; k < NS; ++k) S[k] = fma(-w, vq[k], S[k]);
-          Op::emit(S, nv, minp, r, o0, o1);
+          Op::emit_x(S, isw[nv], nv, minp, r, o0, o1);
         }
       } else {
 #pragma unroll
@@ -919,7 +966,7 @@ ew_window_san_kernel(
           double S[NS];
 #pragma unroll
           for (int k = 0; k < NS; ++k) S[k] = fma(-f, L[k], E[k]);
-          Op::emit(S, nv, minp, r, o0, o1);
+          Op::emit_x(S, isw[nv], nv, minp, r, o0, o1);
         }
       }
     }
