@@ -20,7 +20,6 @@
 // 256-byte wave load that mostly hits L1/L2.  fp64 accumulation throughout.
 #include "common.h"
 
-#include <type_traits>
 
 namespace {
 
@@ -1004,10 +1003,10 @@ void launch_ew_san(const float* a, const float* b, const int* seg, int R, int W,
 }
 
 // A/B geometry of the anchored-prefix kernel (mfa_rolling_set_ew_variant): 0 = sanitised rows,
-// 8-row chunks x 256 threads (2048-row tiles), the sliding window update; DASTD with the next
-// tile's loads in flight, BETA without (its 6 sums leave no registers for them: 0.1457 vs 0.1455
-// ms; DASTD 0.1043 vs 0.1069 ms at 5000 x 3780, profiles/r04/rolling_ab.jsonl), 7 = always
-// with the prefetch, 5 = the round-3 kernel at the same geometry (and the round-3 CMRA kernel), 1 = 8 x 512 (4096-row tiles: half the halo re-read), 2 = 16 x 256 (4096-row tiles,
+// 8-row chunks x 256 threads (2048-row tiles), the sliding window update, count-implied weight
+// sums and the next tile's loads in flight (BETA 0.142, DASTD 0.096 ms at 5000 x 3780,
+// profiles/r04/rolling_ab.jsonl), 7 = the same (kept for the A/B tables), 5 = the round-3
+// kernel at the same geometry (and the round-3 CMRA kernel), 1 = 8 x 512 (4096-row tiles: half the halo re-read), 2 = 16 x 256 (4096-row tiles,
 // half the scan steps per row), 3 = round-3 geometry with the software prefetch of the next
 // tile (3 waves / SIMD), 4 = 4096-row tiles without the prefetch, 6 = sanitised rows, 4096-row
 // tiles, 8 = sanitised rows, 4096-row tiles with the prefetch, 9 = variant 0 with the per-row
@@ -1016,9 +1015,8 @@ int g_ew_variant = 0;
 template <class Op>
 void launch_ew(const float* a, const float* b, const int* seg, int R, int W, int H, double lam,
                int minp, float* o0, float* o1, hipStream_t s) {
-  if (g_ew_variant == 0)  // DASTD (3 sums, 108 VGPRs) keeps the next tile's loads in flight
-    launch_ew_san<Op, 8, 2048, std::is_same_v<Op, DastdOp>>(a, b, seg, R, W, H, lam, minp, o0,
-                                                             o1, s);
+  if (g_ew_variant == 0)  // the next tile's loads in flight (BETA 119, DASTD 102 VGPRs)
+    launch_ew_san<Op, 8, 2048, true>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
   else if (g_ew_variant == 6)
     launch_ew_san<Op, 8, 4096>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
   else if (g_ew_variant == 7)
