@@ -20,12 +20,9 @@ using namespace mfa;
 // every cross-wave LDS exchange is behind a barrier (4 per Householder step).  Replaces
 // rocSOLVER's batched syevd (~27 us per 140 x 140 problem at the GPU's throughput) for the bias
 // statistic; eigenvalues, eigenvectors and back-transform are per lane as before.
-#ifndef MFA_WIDE_ROUNDS
-#define MFA_WIDE_ROUNDS 0
-#endif
-// multisection rounds before the Laguerre loop (0 = off: not yet measured on the GPU; the
-// Laguerre phase is ~1/3 of the K = 140 solver, profiles/r04/wide_bias_ab.jsonl)
-constexpr int kWideRounds = MFA_WIDE_ROUNDS;
+// Multisection rounds before the Laguerre loop: bits 4-6 of the kernels' `abl` argument
+// (mfa_eigen_wide_set_ablation(r << 4)); 0 = off until measured (the Laguerre phase is ~1/3 of
+// the K = 140 solver, profiles/r04/wide_bias_ab.jsonl).
 
 template <int NW>
 __device__ __forceinline__ double block_total(double v, double* red, int t) {
@@ -209,7 +206,7 @@ mc_bias_wide_kernel(const double* __restrict__ D0, int K, int M, const double* _
   // multisection: every lane samples the count at its bracket's midpoint and every lane
   // tightens its bracket with all K samples (the diagonal is a poor guess when C_z is far from
   // the identity, e.g. T_sim ~ 2 K: the Laguerre loop otherwise starts with long bisections)
-  for (int rd = 0; rd < kWideRounds; ++rd) {
+  for (int rd = 0; rd < ((abl >> 4) & 7); ++rd) {
     const double xm = 0.5 * (lo + hi);
     double Gm, Hm;
     const int cm = sturm_gh_p(tb, K, xm, Gm, Hm);
@@ -223,7 +220,7 @@ mc_bias_wide_kernel(const double* __restrict__ D0, int K, int M, const double* _
       if (cl <= jt) lo = fmax(lo, xl); else hi = fmin(hi, xl);
     }
   }
-  if (kWideRounds > 0 && !(x > lo && x < hi)) {  // the guess fell out: restart mid-bracket
+  if ((abl >> 4) != 0 && !(x > lo && x < hi)) {  // the guess fell out: restart mid-bracket
     x = 0.5 * (lo + hi);
     cnt = sturm_gh_p(tb, K, x, G, H);
   }
@@ -552,7 +549,7 @@ __global__ __launch_bounds__(NW * 64) void mc_bias_wide2_kernel(
     const int cl = csv[l];
     if (cl <= jt) lo = fmax(lo, xl); else hi = fmin(hi, xl);
   }
-  for (int rd = 0; rd < kWideRounds; ++rd) {  // multisection, as in the row kernel
+  for (int rd = 0; rd < ((abl >> 4) & 7); ++rd) {  // multisection, as in the row kernel
     const double xm = 0.5 * (lo + hi);
     double Gm, Hm;
     const int cm = sturm_gh_p(tb, K, xm, Gm, Hm);
@@ -568,7 +565,7 @@ __global__ __launch_bounds__(NW * 64) void mc_bias_wide2_kernel(
       if (cl <= jt) lo = fmax(lo, xl); else hi = fmin(hi, xl);
     }
   }
-  if (kWideRounds > 0 && !(x > lo && x < hi)) {
+  if ((abl >> 4) != 0 && !(x > lo && x < hi)) {
     x = 0.5 * (lo + hi);
     cnt = sturm_gh_p(tb, K, x, G, H);
   }

@@ -49,7 +49,7 @@ try:
     with eigen.using_wide_bias_solver("hip"):
         for layout in ("row", "pair"):
             eigen.set_wide_kernel_layout(layout)
-            for abl in (0, 1, 2, 3, 4, 6):
+            for abl in (0, 1, 2, 3, 4, 6, 1 << 4, 2 << 4, 3 << 4, 5 << 4):  # + multisection rounds
                 _native.lib().mfa_eigen_wide_set_ablation(abl)
                 eigen._bias_sum_wide(w, valid, Cz)
                 torch.cuda.synchronize()
@@ -61,3 +61,12 @@ finally:
     _native.lib().mfa_eigen_wide_set_ablation(0)
     eigen.set_wide_kernel_layout("pair")
 print(json.dumps({"hip_ablation_ms": abl_ms}), flush=True)
+# multisection rounds must not change the results beyond rounding
+with eigen.using_wide_bias_solver("hip"):
+    try:
+        _native.lib().mfa_eigen_wide_set_ablation(3 << 4)
+        S3 = eigen._bias_sum_wide(w, valid, Cz)
+    finally:
+        _native.lib().mfa_eigen_wide_set_ablation(0)
+rel3 = ((S3 - out["rocsolver"]).abs() / out["rocsolver"].abs()).max().item()
+print(json.dumps({"max_rel_hip_pair_3rounds_vs_rocsolver": rel3}), flush=True)
