@@ -11,9 +11,10 @@ using namespace mfa;
 
 // ---------------- multi-wave tridiagonal bias solver (64 < K <= 144) ----------------
 // Wide factor sets (e.g. SW-L2 industries, K = 140) with mode 5's four phases and arithmetic on
-// ONE workgroup of NW waves per (date, sim): lane t owns row t of A = S C_z S in registers (KP
-// doubles), the packed reflector rows and the tridiagonal tables live in LDS (~87 KB at K = 140:
-// one workgroup per CU, one wave per SIMD, every register the row and the eigenvector need).
+// ONE workgroup of NW waves per (date, sim).  Layout 0 (mc_bias_wide_kernel, default for
+// K <= 96): lane t owns row t of A = S C_z S in registers (KP doubles); layout 1
+// (mc_bias_wide2_kernel below, default for K > 96): two lanes per row.  The packed reflector
+// rows and the tridiagonal tables live in LDS (~87 KB at K = 140: one workgroup per CU).
 // What changes against the one-wave kernel is only where lanes meet: the Householder column
 // norm, u^T p and the Gershgorin / pivot bounds are block reductions (per-wave DPP totals, then
 // the NW partials in wave order: deterministic), the pivot row's entries are LDS broadcasts, and
@@ -44,9 +45,6 @@ __device__ __forceinline__ double block_ext(double v, double* red, int t) {
   for (int w = 1; w < NW; ++w) s = MAX ? fmax(s, red[w]) : fmin(s, red[w]);
   return s;
 }
-
-template <int KP>
-__host__ __device__ constexpr int wide_rows_doubles(int K) { return tri2_rows_doubles<KP>(K); }
 
 template <int KP, int NW>
 __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(1))) void
