@@ -367,17 +367,33 @@ __device__ __forceinline__ int pair_swap_i(int v) {
   return __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, false);
 }
 
-template <int KP, int NW>
+// EIG: batched symmetric eigendecomposition with the same machinery (eigh of wide F0): D0 = the
+// input matrices [B][K][K] (symmetrised), M = 1, vout = w [B][K] descending, Uout [B][K][K]
+// with U[:, k] = eigenvector k; a matrix with a non-finite entry gives NaN.  The caller checks
+// U^T U = I (clustered spectra) and re-solves what fails.
+template <int KP, int NW, bool EIG = false>
 __global__ __launch_bounds__(NW * 64) void mc_bias_wide2_kernel(
     const double* __restrict__ D0, int K, int M, const double* __restrict__ Cz,
-    const int* __restrict__ dvalid, double* __restrict__ vout, int abl) {
+    const int* __restrict__ dvalid, double* __restrict__ vout, int abl,
+    double* __restrict__ Uout = nullptr) {
   constexpr int HP = KP / 2;
   static_assert(KP % 16 == 0 && KP <= NW * 32, "KP: multiple of 16, two lanes per row");
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int d = blockIdx.x / M, m = blockIdx.x % M, t = threadIdx.x;
   const int i = t >> 1, h = t & 1;  // row, half
   double* vo = vout + ((size_t)d * M + m) * K;
-  if (!dvalid[d]) {
+  const double* Ain = D0 + (size_t)d * K * K;  // EIG input matrix
+  if constexpr (EIG) {
+    bool fin = true;
+    for (int e = t; e < K * K; e += NW * 64) fin = fin && __builtin_isfinite(Ain[e]);
+    double* redx = sm;  // before any other use of the LDS
+    if (block_total<NW>(fin ? 0.0 : 1.0, redx, t) != 0.0) {
+      for (int k = t; k < K; k += NW * 64) vo[k] = qnan();
+      for (int e = t; e < K * K; e += NW * 64) Uout[(size_t)d * K * K + e] = qnan();
+      return;
+    }
+    __syncthreads();  // the partials slot is reused as reflector storage below
+  } else if (!dvalid[d]) {
     for (int k = t; k < K; k += NW * 64) vo[k] = qnan();
     return;
   }
@@ -397,17 +413,20 @@ __global__ __launch_bounds__(NW * 64) void mc_bias_wide2_kernel(
   double a[HP];
   const double* c = Cz + (size_t)m * K * K;
   const double* d0 = D0 + (size_t)d * K;
-  const double di = row_ok ? sqrt(fmax(d0[li], 0.0)) : 0.0;
+  const double di = (row_ok && !EIG) ? sqrt(fmax(d0[li], 0.0)) : 0.0;
   if (lead) dd[i] = di;
   __syncthreads();
 #pragma unroll
   for (int jj = 0; jj < HP; ++jj) {
     const int j = h * HP + jj;
-    a[jj] = (j < K && row_ok) ? di * c[j * K + li] * dd[j] : 0.0;
+    if constexpr (EIG)  // this lane's half of row i of the symmetrised input
+      a[jj] = (j < K && row_ok) ? 0.5 * (Ain[li * K + j] + Ain[j * K + li]) : 0.0;
+    else
+      a[jj] = (j < K && row_ok) ? di * c[j * K + li] * dd[j] : 0.0;
     if ((jj & 7) == 7) lds_batch();
   }
   {
-    const double g = row_ok ? di * c[li * K + li] * di : 0.0;
+    const double g = row_ok ? (EIG ? Ain[li * K + li] : di * c[li * K + li] * di) : 0.0;
     if (lead) wb[i] = g;
     __syncthreads();
     if (lead && row_ok) {
@@ -594,7 +613,7 @@ __global__ __launch_bounds__(NW * 64) void mc_bias_wide2_kernel(
     }
     lam = x;
   }
-  if (abl & 2) {
+  if (!EIG && (abl & 2)) {
     if (lead && row_ok) vo[i] = lam;
     return;
   }
@@ -740,6 +759,18 @@ __global__ __launch_bounds__(NW * 64) void mc_bias_wide2_kernel(
     constexpr int NG = KP / 8;
     (back(std::integral_constant<int, 8 * (NG - 1 - G)>{}, 8 * (NG - 1 - G) + 7), ...);
   }(std::make_integer_sequence<int, KP / 8>{});
+  if constexpr (EIG) {  // w (descending by row rank) and U[:, i] = eigenvector i
+    if (row_ok) {
+      if (h == 0) vo[i] = lam;
+      double* Ub = Uout + (size_t)d * K * K;
+#pragma unroll
+      for (int jj = 0; jj < HP; ++jj) {
+        const int j = h * HP + jj;
+        if (j < K) Ub[(size_t)j * K + i] = y[jj];
+      }
+    }
+    return;
+  }
   double v = 0.0;
 #pragma unroll
   for (int jj = 0; jj < HP; ++jj) {
@@ -780,6 +811,20 @@ __global__ __launch_bounds__(64) void wide_bias_sum_kernel(const double* __restr
 // Wide factor sets: S[d][k] += sum over this call's M sims of v_m[d][k] for 2 < K <= 144 with the
 // multi-wave solver (one workgroup of 2 / 3 waves per (date, sim) for K <= 96 / 144); ws: D*M*K
 // doubles.  Invalid dates (dvalid[d] = 0) accumulate NaN.
+// Batched eigendecomposition of symmetric [B][K][K] matrices, 96 < K <= 144 (two lanes per row):
+// w [B][K] descending, U [B][K][K] with U[:, k] = eigenvector k (NaN for non-finite inputs).
+MFA_API int mfa_eigh_wide(const double* A, int B, int K, double* w, double* U, void* stream) {
+  if (B <= 0) return 0;
+  if (K <= 96 || K > 144) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  const size_t lds = bias_wide2_lds(K, 144, 5);
+  (void)hipFuncSetAttribute((const void*)mc_bias_wide2_kernel<144, 5, true>,
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL((mc_bias_wide2_kernel<144, 5, true>), dim3(B), dim3(5 * 64), lds, s, A, K, 1,
+                     (const double*)nullptr, (const int*)nullptr, w, 0, U);
+  return (int)hipGetLastError();
+}
+
 int g_wide_abl = 0;  // timing-only phase ablations (bits: 1 Laguerre, 2 eigenvectors, 4 Householder)
 int g_wide_variant = 1;  // 1 = two lanes per row for K > 96 (default: 26.9 vs 28.3 ms at K = 140,
                          // 60 x 100 problems, no spills), 0 = one lane per row

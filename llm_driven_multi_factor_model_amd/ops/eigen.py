@@ -44,6 +44,8 @@ _native.register("mfa_philox_normals", [C.c_int, C.c_int, C.c_int, C.c_int, C.c_
 _native.register("mfa_eigen_bias_accumulate_wide", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p])
 _native.register("mfa_eigen_wide_set_variant", [C.c_int])
+_native.register("mfa_eigh_wide", [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                   C.c_void_p])
 _native.register("mfa_eigen_finalize_sum", [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                              C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p,
                                              C.c_void_p, C.c_void_p])
@@ -159,9 +161,26 @@ def eigh(A: torch.Tensor, max_sweeps: int = MAX_SWEEPS, tol: float = TOL):
 
 
 def _eigh_wide(Ab, shp):
-    """K > 64 on the device: rocSOLVER batched eigh of the finite (symmetrised) matrices, in
-    chunks of ~WIDE_CHUNK_DOUBLES; NaN for non-finite inputs.  Eigenvalues descending."""
+    """K > 64 on the device: for 96 < K <= WIDE_HIP_MAX_K the multi-wave HIP solver
+    (``mfa_eigh_wide``; matrices whose eigenvectors come out non-orthogonal to 1e-10, i.e.
+    clustered spectra, are re-solved by rocSOLVER), otherwise rocSOLVER's batched eigh of the
+    finite (symmetrised) matrices in chunks of ~WIDE_CHUNK_DOUBLES; NaN for non-finite inputs.
+    Eigenvalues descending."""
     B, K = Ab.shape[0], Ab.shape[-1]
+    if _wide_solver == "hip" and 96 < K <= WIDE_HIP_MAX_K:
+        w = torch.empty(B, K, dtype=torch.float64, device=Ab.device)
+        U = torch.empty(B, K, K, dtype=torch.float64, device=Ab.device)
+        _native.call("mfa_eigh_wide", _native.ptr(Ab), B, K, _native.ptr(w), _native.ptr(U),
+                     _native.stream(Ab.device))
+        eye = torch.eye(K, dtype=torch.float64, device=Ab.device)
+        err = (U.transpose(-1, -2) @ U - eye).abs().amax((-1, -2))
+        redo = torch.nonzero(err > 1e-10).flatten()       # NaN matrices: err is NaN, not > tol
+        if redo.numel():
+            S = Ab[redo]
+            ww, UU = torch.linalg.eigh(0.5 * (S + S.transpose(-1, -2)))
+            w[redo] = ww.flip(-1)
+            U[redo] = UU.flip(-1)
+        return w.reshape(shp[:-1]), U.reshape(shp)
     w = torch.full((B, K), float("nan"), dtype=torch.float64, device=Ab.device)
     U = torch.full((B, K, K), float("nan"), dtype=torch.float64, device=Ab.device)
     ok = torch.isfinite(Ab).all(-1).all(-1)

@@ -216,3 +216,27 @@ def test_wide_bias_solver_selection():
     with eigen.using_wide_bias_solver("hip"):
         assert eigen._wide_solver == "hip"
     assert eigen._wide_solver in eigen.WIDE_BIAS_SOLVERS
+
+
+@pytest.mark.gpu
+def test_hip_wide_eigh_native(cuda):
+    """eigen.eigh at 96 < K <= 144 on the multi-wave HIP solver == LAPACK (values 1e-10 relative,
+    A U = U diag(w), U orthonormal); a NaN matrix gives NaN; the rocSOLVER path agrees."""
+    g = torch.Generator().manual_seed(12)
+    K, B = 140, 7
+    X = torch.randn(B, 400, K, generator=g, dtype=torch.float64)
+    F = X.transpose(1, 2) @ X / 400
+    F[3] = float("nan")
+    w, U = eigen.eigh(F.to(cuda))
+    ok = [b for b in range(B) if b != 3]
+    wr = torch.linalg.eigvalsh(F[ok]).flip(-1)
+    torch.testing.assert_close(w.cpu()[ok], wr, rtol=1e-10, atol=1e-13)
+    Fg = F.to(cuda)[ok]
+    R = Fg @ U[ok] - U[ok] * w[ok][:, None, :]
+    assert float(R.abs().max()) < 1e-10
+    G = U[ok].transpose(-1, -2) @ U[ok] - torch.eye(K, dtype=torch.float64, device=cuda)
+    assert float(G.abs().max()) < 1e-10
+    assert torch.isnan(w[3]).all() and torch.isnan(U[3]).all()
+    with eigen.using_wide_bias_solver("rocsolver"):
+        w2, _ = eigen.eigh(F.to(cuda))
+    torch.testing.assert_close(w2.cpu()[ok], w.cpu()[ok], rtol=1e-10, atol=1e-13)

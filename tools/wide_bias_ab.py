@@ -70,3 +70,15 @@ with eigen.using_wide_bias_solver("hip"):
         _native.lib().mfa_eigen_wide_set_ablation(0)
 rel3 = ((S3 - out["rocsolver"]).abs() / out["rocsolver"].abs()).max().item()
 print(json.dumps({"max_rel_hip_pair_3rounds_vs_rocsolver": rel3}), flush=True)
+
+# eigh of the F0 batch itself (D matrices, K x K): multi-wave HIP solver vs rocSOLVER
+Fb = F.repeat((2520 + D - 1) // D, 1, 1)[:2520].contiguous()
+for name in ("hip", "rocsolver"):
+    with eigen.using_wide_bias_solver(name):
+        eigen.eigh(Fb)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        wq, Uq = eigen.eigh(Fb)
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) * 1e3
+    print(json.dumps({"eigh": name, "B": Fb.shape[0], "K": K, "ms": round(ms, 2)}), flush=True)
