@@ -10,7 +10,7 @@ agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in glob.glob(__import__("os").environ.get("O", "gpurun_out/pmc_roll2") + "/a/**/run_counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         kn = r["Kernel_Name"]
-        if any(t in kn for t in ("ew_window", "vhgw", "rstr_ew")):
+        if any(t in kn for t in ("ew_window", "vhgw", "vh2", "rstr_ew")):
             agg[kn[:kn.rfind("(")].replace("(anonymous namespace)::", "")[-70:]][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in agg.items():
     v = {c: sum(x) / len(x) for c, x in d.items()}
