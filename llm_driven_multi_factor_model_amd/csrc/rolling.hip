@@ -1470,6 +1470,11 @@ constexpr int kRsBPW = kRsBlk / kRsWaves;       // 10 blocks per wave
 constexpr int kRsWRows = kRsBPW * 64;           // rows per wave region
 static_assert(kRsBlk % kRsWaves == 0 && kRsH % 64 == 0, "block split");
 
+// TWO (default since round 4): pass 2 on 128-row blocks with two rows per lane -- the pair's
+// local decayed sum, then ONE DPP scan per block for each of the numerator / denominator serves
+// both rows (the exclusive prefix for the first row of the pair is one lane shift): ~half the
+// scan instructions per row.
+template <bool TWO>
 __global__ __launch_bounds__(kRsWaves * 64) void rstr_ew_kernel(const float* __restrict__ lr,
                                                                 const int* __restrict__ seg_lo,
                                                                 int R, int L, int W, double lam,
@@ -1505,21 +1510,63 @@ __global__ __launch_bounds__(kRsWaves * 64) void rstr_ew_kernel(const float* __r
   }
   double cn = 0.0, cd = 0.0;
   int cc = 0;
+  if constexpr (!TWO) {
 #pragma unroll
-  for (int k = kRsBPW - 1; k >= 0; --k) {
-    const int t = (wid * kRsBPW + k) * 64 + 63 - lane;
-    const float v = vv[k];
-    const bool ok = fin(v);
-    const double zn = wave_scan_sum(ok ? lpn * (double)v : 0.0);
-    const double zd = wave_scan_sum(ok ? lpn : 0.0);
-    const unsigned long long M = __ballot(ok);
-    const double Un = fma(lp, zn, lp1 * cn), Ud = fma(lp, zd, lp1 * cd);
-    un[t] = Un;
-    ud[t] = Ud;
-    cs[t] = (unsigned short)(cc + __popcll(M & below));
-    cn = readlane(Un, 63);
-    cd = readlane(Ud, 63);
-    cc += __popcll(M);
+    for (int k = kRsBPW - 1; k >= 0; --k) {
+      const int t = (wid * kRsBPW + k) * 64 + 63 - lane;
+      const float v = vv[k];
+      const bool ok = fin(v);
+      const double zn = wave_scan_sum(ok ? lpn * (double)v : 0.0);
+      const double zd = wave_scan_sum(ok ? lpn : 0.0);
+      const unsigned long long M = __ballot(ok);
+      const double Un = fma(lp, zn, lp1 * cn), Ud = fma(lp, zd, lp1 * cd);
+      un[t] = Un;
+      ud[t] = Ud;
+      cs[t] = (unsigned short)(cc + __popcll(M & below));
+      cn = readlane(Un, 63);
+      cd = readlane(Ud, 63);
+      cc += __popcll(M);
+    }
+  } else {
+    // 128-row blocks, lane m holds the block's reversed positions q = 2m, 2m + 1 (rows 127 - 2m,
+    // 126 - 2m); the same row values as vv, re-read pairwise (L1 / L2 hits)
+    constexpr int BPW2 = kRsBPW / 2;
+    static_assert(kRsBPW % 2 == 0, "pairs of 64-row blocks");
+    const double l2 = lam * lam;
+    const double lq = wave_scan_dpp<3>(lane == 0 ? 1.0 : l2);  // lam^(2m)
+    const double lqn = 1.0 / lq, lq1 = lq * lam, lq2 = lq * l2;
+    const unsigned long long lt = (1ull << lane) - 1;
+    float x0v[BPW2], x1v[BPW2];
+#pragma unroll
+    for (int k = 0; k < BPW2; ++k) {
+      const int g = g0 + (wid * BPW2 + k) * 128 + 127 - 2 * lane;
+      x0v[k] = (g >= 0 && g < R) ? lr[g] : qnanf();
+      x1v[k] = (g - 1 >= 0 && g - 1 < R) ? lr[g - 1] : qnanf();
+    }
+#pragma unroll
+    for (int k = BPW2 - 1; k >= 0; --k) {
+      const int t0 = (wid * BPW2 + k) * 128 + 127 - 2 * lane, t1 = t0 - 1;
+      const bool ok0 = fin(x0v[k]), ok1 = fin(x1v[k]);
+      const double xn0 = ok0 ? (double)x0v[k] : 0.0, xn1 = ok1 ? (double)x1v[k] : 0.0;
+      const double xd0 = ok0 ? 1.0 : 0.0, xd1 = ok1 ? 1.0 : 0.0;
+      // prefix over q at the pair's second position: P_m = lam^2 P_(m-1) + (lam x_q0 + x_q1)
+      const double Pn = lq * wave_scan_sum(lqn * fma(lam, xn0, xn1));
+      const double Pd = lq * wave_scan_sum(lqn * fma(lam, xd0, xd1));
+      const double Pnu = __shfl_up(Pn, 1, kWave), Pdu = __shfl_up(Pd, 1, kWave);
+      const double Pne = lane ? Pnu : 0.0, Pde = lane ? Pdu : 0.0;
+      // U at position q = prefix(q) + lam^(q+1) U(row after the block)
+      const double Un0 = fma(lam, Pne, xn0) + lq1 * cn, Un1 = fma(lq2, cn, Pn);
+      const double Ud0 = fma(lam, Pde, xd0) + lq1 * cd, Ud1 = fma(lq2, cd, Pd);
+      un[t0] = Un0; un[t1] = Un1;
+      ud[t0] = Ud0; ud[t1] = Ud1;
+      const unsigned long long M0 = __ballot(ok0), M1 = __ballot(ok1);
+      const int c01 = cc + __popcll(M0 & below);
+      cs[t0] = (unsigned short)(c01 + __popcll(M1 & lt));
+      cs[t1] = (unsigned short)(c01 + __popcll(M1 & below));
+      cn = readlane(Un1, 63);
+      cd = readlane(Ud1, 63);
+      cc += __popcll(M0) + __popcll(M1);
+    }
   }
   if (lane == 0) { tn[wid] = cn; td[wid] = cd; tc[wid] = cc; }
   __syncthreads();
@@ -1690,9 +1737,16 @@ MFA_API int mfa_beta_hsigma(const float* y, const float* x, const int* seg_lo, i
 MFA_API int mfa_rstr(const float* lr, const int* seg_lo, int R, int L, int W, double lam,
                      int minp, float* out, void* s) {
   if (R <= 0) return 0;
-  if (g_roll_mode == 0 && L >= 1 && W >= 1 && W + L - 1 <= kRsH && W <= kRsWRows)
-    hipLaunchKernelGGL(rstr_ew_kernel, dim3((R + kRsRows - 1) / kRsRows), dim3(kRsWaves * 64), 0,
-                       (hipStream_t)s, lr, seg_lo, R, L, W, lam, minp, out);
+  if (g_roll_mode == 0 && L >= 1 && W >= 1 && W + L - 1 <= kRsH && W <= kRsWRows) {
+    if (g_ew_variant == 5)  // A/B: the round-3 pass 2 (one row per lane)
+      hipLaunchKernelGGL(rstr_ew_kernel<false>, dim3((R + kRsRows - 1) / kRsRows),
+                         dim3(kRsWaves * 64), 0, (hipStream_t)s, lr, seg_lo, R, L, W, lam, minp,
+                         out);
+    else
+      hipLaunchKernelGGL(rstr_ew_kernel<true>, dim3((R + kRsRows - 1) / kRsRows),
+                         dim3(kRsWaves * 64), 0, (hipStream_t)s, lr, seg_lo, R, L, W, lam, minp,
+                         out);
+  }
   else if (g_roll_mode != 1 && W + L <= 512 && W + kChunk + 1 <= kPowMax)
     hipLaunchKernelGGL(rstr_scan_kernel<512>, MFA_SCAN_GRID(R), 0, (hipStream_t)s, lr, seg_lo, R, L,
                        W, lam, minp, out);
