@@ -52,9 +52,9 @@ ROUNDS = int(os.environ.get("ROUNDS", 3))   # variants interleaved per round: no
 for name, (fn, bpr) in cases.items():
     res = {}
     todo = [(v, m, e) for v, m, e in variants
-            if not (e and name not in ("beta_hsigma", "dastd") and not (name == "cmra" and e == 5))]
+            if not (e and name not in ("beta_hsigma", "dastd") and not (name in ("cmra", "rstr") and e == 5))]
     for rnd in range(ROUNDS):
-        for vname, mode, ewv in todo:  # ew variant 5 also selects the round-3 CMRA kernel
+        for vname, mode, ewv in todo:  # ew variant 5 also selects the round-3 CMRA / RSTR kernels
             lib.mfa_rolling_set_mode(mode)
             lib.mfa_rolling_set_ew_variant(ewv)
             fn()
