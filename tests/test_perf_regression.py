@@ -19,13 +19,13 @@ MEASURED = {
     "eigen_adjust_2520x100_ms": 14.45,
     # Newey-West expanding series, T = 2520, K = 42, q = 2
     "newey_west_2520_ms": 0.100,
-    # window-descriptor kernels, 5000 x 3780, round 4 (profiles/r04/rolling_ab.jsonl, r04l/): BETA/
+    # window-descriptor kernels, 5000 x 3780, round 4 (profiles/r04/rolling_ab.jsonl, r04q/): BETA/
     # HSIGMA and DASTD sanitised-row sliding kernel with count-implied weight sums, CMRA two-rows-
     # per-lane van Herk, RSTR backward-anchored sums with tile-absolute prefixes
-    "beta_hsigma_5000x3780_ms": 0.144,
+    "beta_hsigma_5000x3780_ms": 0.141,
     "dastd_5000x3780_ms": 0.095,
     "cmra_5000x3780_ms": 0.089,
-    "rstr_5000x3780_ms": 0.092,
+    "rstr_5000x3780_ms": 0.089,
     # point-in-time trailing specific vol, 2520 x 5000, W = 252 (profiles/r03_risk/)
     "trailing_vol_2520x5000_ms": 1.075,
 }
