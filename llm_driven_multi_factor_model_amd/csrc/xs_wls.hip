@@ -14,6 +14,8 @@ int g_mfa_xs_pipe_wpc = 0;
 // (default), 1 = three separate kernels, 7 = fused without the prefetch.  Applies to both the
 // fp32 and fp64 entry points.
 MFA_API void mfa_xs_set_mode(int mode) { g_mfa_xs_mode = mode; }
+unsigned long long* g_mfa_xs_prof = nullptr;
+MFA_API void mfa_xs_set_prof(void* p) { g_mfa_xs_prof = (unsigned long long*)p; }
 
 // Stock chunks per date for the next calls: 0 = automatic (default: the fused kernel,
 // kXsChunkMinD = 0), > 0 = forced chunk count, < 0 = always one workgroup per date.
