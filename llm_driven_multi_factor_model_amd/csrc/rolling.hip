@@ -1025,6 +1025,10 @@ void launch_ew(const float* a, const float* b, const int* seg, int R, int W, int
     launch_ew_san<Op, 8, 4096, true>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
   else if (g_ew_variant == 9)  // per-row prefix subtraction instead of the sliding form
     launch_ew_san<Op, 8, 2048, false, false>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
+  else if (g_ew_variant == 10)  // 16-row chunks, 4096-row tiles: half the scan steps and halo
+    launch_ew_san<Op, 16, 4096, true>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
+  else if (g_ew_variant == 11)  // 16-row chunks, 2048-row tiles on 2-wave workgroups
+    launch_ew_san<Op, 16, 2048, true>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
   else if (g_ew_variant == 1)
     launch_ew_pipe<Op, 8, 4096>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
   else if (g_ew_variant == 2)
