@@ -66,6 +66,8 @@ WIDE_CHUNK_DOUBLES = 1 << 27     # ~1 GB of fp64 per batched eigh / draw chunk
 WIDE_HIP_MAX_K = 144
 WIDE_BIAS_SOLVERS = ("rocsolver", "hip")
 _wide_solver = os.environ.get("MFA_WIDE_BIAS", "hip")
+if _wide_solver not in WIDE_BIAS_SOLVERS:  # a typo must not silently select rocSOLVER
+    raise ValueError(f"MFA_WIDE_BIAS must be one of {WIDE_BIAS_SOLVERS}, got {_wide_solver!r}")
 
 
 def set_wide_bias_solver(name: str) -> None:

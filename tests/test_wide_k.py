@@ -218,6 +218,18 @@ def test_wide_bias_solver_selection():
     assert eigen._wide_solver in eigen.WIDE_BIAS_SOLVERS
 
 
+def test_wide_bias_env_is_validated():
+    """A misspelt MFA_WIDE_BIAS fails the import instead of silently selecting rocSOLVER."""
+    import os
+    import subprocess
+    import sys
+    env = dict(os.environ, MFA_WIDE_BIAS="hipp", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", "import llm_driven_multi_factor_model_amd.ops.eigen"],
+                       capture_output=True, text=True, env=env, timeout=300, cwd=root)
+    assert r.returncode != 0 and "MFA_WIDE_BIAS" in r.stderr
+
+
 @pytest.mark.gpu
 def test_hip_wide_eigh_native(cuda):
     """eigen.eigh at 96 < K <= 144 on the multi-wave HIP solver == LAPACK (values 1e-10 relative,
