@@ -993,8 +993,10 @@ size_t bias_tri_lds(int K, int KP) { return ((size_t)K * (KP + 1) + 7 * 64 + 2) 
 // pipeline's inputs (profiles/r03_risk/bias_laguerre_stop_ab.jsonl): 1e-9 13.26 ms, 1e-8
 // 12.40 ms (bias ratios within 3e-14 of the Jacobi, 1.9e-14 of LAPACK), 1e-7 11.65 ms but
 // 1.4e-11 off: 1e-8 is the default; modes 8 / 9 select 1e-9 / 1e-7.
+// NA: independent accumulators of the Householder matvec and the back-transform dot products
+// (2, or 4: half the dependent fma chain per step, A/B bias mode 13).
 template <int KP, bool PF = false, int ABL = 0, int WPE = MFA_TRI2_WPE, bool EIG = false,
-          int ACC = 8, int LB = 8>
+          int ACC = 8, int LB = 8, int NA = 2>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void
 mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* __restrict__ Cz,
                     const int* __restrict__ dvalid, double* __restrict__ vout,
@@ -1099,18 +1101,23 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
       lds_order();
       // branch-free: tau = 0 (nothing to reflect) gives u = p = w = 0, and lanes <= s have
       // u = p = w = 0, so the update is a no-op there (no divergent copies of the row)
-      double p0 = 0.0, p1 = 0.0;
+      double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
       // rows s >= K - 2 are not stored (tau = 0 there): read the group's first row instead,
       // finite values times u = w = p = 0
       if (s + 2 >= K) us = R + tri2_row_off<KP>(J0) - J0;
 #pragma unroll
       for (int j = J0; j < KP; j += 2) {
         const double2 uu = *(const double2*)(us + j);
-        p0 = fma(a[j], uu.x, p0);
-        p1 = fma(a[j + 1], uu.y, p1);
+        if (NA == 4 && ((j - J0) & 2) != 0) {
+          p2 = fma(a[j], uu.x, p2);
+          p3 = fma(a[j + 1], uu.y, p3);
+        } else {
+          p0 = fma(a[j], uu.x, p0);
+          p1 = fma(a[j + 1], uu.y, p1);
+        }
         if (((j - J0) & (LB - 1)) == LB - 2) lds_batch();
       }
-      const double p = act ? tau * (p0 + p1) : 0.0;
+      const double p = act ? tau * (NA == 4 ? (p0 + p1) + (p2 + p3) : p0 + p1) : 0.0;
       const double kk = 0.5 * tau * wave_total(u * p);
       const double w = p - kk * u;
       wb[lane] = w;
@@ -1274,15 +1281,20 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
       const double tau = ta[s];
       if (tau == 0.0) continue;
       const double* us = R + tri2_row_off<KP>(s) - J0;
-      double t0 = 0.0, t1 = 0.0;
+      double t0 = 0.0, t1 = 0.0, t2 = 0.0, t3 = 0.0;
 #pragma unroll
       for (int j = J0; j < KP; j += 2) {
         const double2 uu = *(const double2*)(us + j);
-        t0 = fma(uu.x, y[j], t0);
-        t1 = fma(uu.y, y[j + 1], t1);
+        if (NA == 4 && ((j - J0) & 2) != 0) {
+          t2 = fma(uu.x, y[j], t2);
+          t3 = fma(uu.y, y[j + 1], t3);
+        } else {
+          t0 = fma(uu.x, y[j], t0);
+          t1 = fma(uu.y, y[j + 1], t1);
+        }
         if (((j - J0) & (LB - 1)) == LB - 2) lds_batch();
       }
-      const double f = tau * (t0 + t1);
+      const double f = tau * (NA == 4 ? (t0 + t1) + (t2 + t3) : t0 + t1);
 #pragma unroll
       for (int j = J0; j < KP; j += 2) {
         const double2 uu = *(const double2*)(us + j);
@@ -1937,6 +1949,11 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
     else  // timing: no eigenvectors / back-transform
       hipLaunchKernelGGL((mc_bias_tri3_kernel<2>), dim3(blocks), dim3(128), bias_tri3_lds(), s, D0,
                          K, M, DM, Cz, dvalid, ws);
+    return true;
+  }
+  if (g_bias_mode == 13 && K <= 44) {  // A/B: four accumulators per matvec / dot product
+    hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 4>), dim3(D * M),
+                       dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr);
     return true;
   }
   if (g_bias_mode == 10 && K <= 44) {  // A/B: LDS broadcast reads fenced in batches of 8 x 16 B
