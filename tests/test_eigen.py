@@ -139,6 +139,28 @@ def test_hip_bias_solvers_agree_on_pipeline_like_inputs(cuda):
 
 
 @pytest.mark.gpu
+def test_bias_mode13_four_accumulators_matches_mode5(cuda):
+    """A/B mode 13 (mode 5 with four accumulators per matvec / back-transform dot product): the
+    same bias ratios as mode 5 to rounding, on graded draw covariances and with a NaN date."""
+    import ctypes as C
+    from llm_driven_multi_factor_model_amd import _native
+    _native.register("mfa_eigen_set_bias_mode", [C.c_int])
+    F = _spd(9, 42, seed=11, spread=2.5) * 1e-4
+    F[4] = float("nan")
+    Cz = eigen.mc_cov(16, 42, 2520, seed=5, device=cuda)
+    lib = _native.lib()
+    out = {}
+    try:
+        for mode in (5, 13):
+            lib.mfa_eigen_set_bias_mode(mode)
+            out[mode] = eigen.eigen_risk_adjust(F.to(cuda), Cz=Cz, return_bias=True)[1].cpu()
+    finally:
+        lib.mfa_eigen_set_bias_mode(5)
+    assert torch.equal(out[5].isnan(), out[13].isnan())
+    torch.testing.assert_close(out[13], out[5], rtol=1e-12, atol=0, equal_nan=True)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("K,D,M", [(42, 7, 5), (30, 5, 4), (42, 1, 1)])
 def test_hip_dense_bias_solver_tail_and_invalid_dates(cuda, K, D, M):
     """Lane-dense solver (3 problems per 2-wave workgroup): a last workgroup with empty slots
