@@ -2020,8 +2020,8 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
 
 #define MFA_BIAS_LAUNCH(NBV_)                                                                   \
   {                                                                                            \
-    if ((g_bias_mode >= 3 && g_bias_mode <= 11) || (g_bias_mode > 40 && g_bias_mode < 68) ||   \
-        g_bias_mode == 111 || g_bias_mode == 112)                                              \
+    if ((g_bias_mode >= 3 && g_bias_mode <= 11) || g_bias_mode == 13 ||                        \
+        (g_bias_mode > 40 && g_bias_mode < 68) || g_bias_mode == 111 || g_bias_mode == 112)    \
       launch_bias_tri(D0, D, K, M, Cz, dvalid, ws, s);                                         \
     else if (g_bias_mode == 1)                                                                 \
       hipLaunchKernelGGL((mc_bias_split_kernel<NBV_, 1, double>), dim3(D * M), dim3(64),       \

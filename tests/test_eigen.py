@@ -151,13 +151,15 @@ def test_bias_mode13_four_accumulators_matches_mode5(cuda):
     lib = _native.lib()
     out = {}
     try:
-        for mode in (5, 13):
+        for mode in (0, 5, 13):
             lib.mfa_eigen_set_bias_mode(mode)
             out[mode] = eigen.eigen_risk_adjust(F.to(cuda), Cz=Cz, return_bias=True)[1].cpu()
     finally:
         lib.mfa_eigen_set_bias_mode(5)
     assert torch.equal(out[5].isnan(), out[13].isnan())
     torch.testing.assert_close(out[13], out[5], rtol=1e-12, atol=0, equal_nan=True)
+    # a different kernel ran (not a fallback to the Jacobi, mode 0): different rounding
+    assert not torch.equal(out[13].nan_to_num(0), out[0].nan_to_num(0))
 
 
 @pytest.mark.gpu
