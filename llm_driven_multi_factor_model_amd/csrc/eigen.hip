@@ -995,8 +995,12 @@ size_t bias_tri_lds(int K, int KP) { return ((size_t)K * (KP + 1) + 7 * 64 + 2) 
 // 1.4e-11 off: 1e-8 is the default; modes 8 / 9 select 1e-9 / 1e-7.
 // NA: independent accumulators of the Householder matvec and the back-transform dot products
 // (2, or 4: half the dependent fma chain per step, A/B bias mode 13).
+// PAD: the tridiagonal is padded to KP with decoupled rows (alpha = 1e300, beta = 0) before the
+// eigenvector phase, so its unrolled recurrences need no `i < K` tests: with a runtime K each
+// test was a 64-bit scalar mask, ~100 of them spilled to VGPR lanes and reloaded (v_readlane +
+// hazard nops + a branch) on every step of the dependent pivot chains (A/B bias mode 14).
 template <int KP, bool PF = false, int ABL = 0, int WPE = MFA_TRI2_WPE, bool EIG = false,
-          int ACC = 8, int LB = 8, int NA = 2>
+          int ACC = 8, int LB = 8, int NA = 2, bool PAD = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void
 mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* __restrict__ Cz,
                     const int* __restrict__ dvalid, double* __restrict__ vout,
@@ -1216,7 +1220,77 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
   }
   // ---- 3. eigenvector of T at lam: twisted factorisation in the y registers only ----
   double y[KP];
-  if (lane < K) {
+  if constexpr (PAD) {
+    // rows K .. 63 decoupled: alpha huge (never an eigenvalue rank a lane targets, pivots finite),
+    // beta = 0 (be[K-1] is 0 already: column K of the reduced matrix is zero)
+    lds_order();
+    if (lane >= K) {
+      tb[lane] = double2{1e300, 0.0};
+      be[lane] = 0.0;
+    }
+    lds_order();
+  }
+  if (PAD && lane < K) {
+    double dp = 0.0;
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {  // forward pivots -> y
+      const double2 t = tb[i];
+      // the laundered copy keeps hipcc from keeping these 44 reciprocals alive for the
+      // rcp_nr1(y[i]) of the below-the-twist loop (it spilled them to scratch)
+      double q = dp;
+      asm volatile("" : "+v"(q));
+      dp = guard_pivot(i == 0 ? t.x - lam : (t.x - lam) - t.y * rcp_nr1(q), pivmin);
+      y[i] = dp;
+      if ((i & 3) == 3) lds_batch();  // not all 44 coefficient reads hoisted (register peak)
+    }
+    // backward pivots on the fly: the twist index r (padded rows: |gamma| ~ 1e300, never chosen)
+    double dm = 1.0, gmin = 1e308;
+    int r = K - 1;
+#pragma unroll
+    for (int i = KP - 1; i >= 0; --i) {
+      const double ai = tb[i].x - lam;
+      double q = dm;  // laundered: the above-the-twist pass recomputes, not keeps, these
+      asm volatile("" : "+v"(q));
+      dm = guard_pivot(ai - tb[i + 1].y * rcp_nr1(q), pivmin);
+      const double g = fabs(y[i] + dm - ai);
+      if (g < gmin) { gmin = g; r = i; }
+      if ((i & 3) == 0) lds_batch();
+    }
+    double cz = 1.0, nrm = 1.0;
+#pragma unroll
+    for (int i = KP - 1; i >= 0; --i) {  // below the twist: y_i = -beta_i y_{i+1} / P_i
+      if (i < r) {
+        cz = -be[i] * cz * rcp_nr1(y[i]);
+        nrm = fma(cz, cz, nrm);
+        y[i] = cz;
+      }
+      if ((i & 3) == 0) lds_batch();
+    }
+    dm = 1.0;
+#pragma unroll
+    for (int i = KP - 1; i >= 0; --i) {  // above the twist: recompute Q_i into y_i
+      if (i > r) {
+        const double ai = tb[i].x - lam;
+        dm = guard_pivot(ai - tb[i + 1].y * rcp_nr1(dm), pivmin);
+        y[i] = dm;
+      }
+      if ((i & 3) == 0) lds_batch();
+    }
+    cz = 1.0;
+#pragma unroll
+    for (int i = 0; i < KP; ++i) {  // padded rows: be[i-1] = 0 -> y_i = -0
+      if (i == r) y[i] = 1.0;
+      if (i > r) {
+        cz = -be[i - 1] * cz * rcp_nr1(y[i]);
+        nrm = fma(cz, cz, nrm);
+        y[i] = cz;
+      }
+      if ((i & 3) == 3) lds_batch();
+    }
+    const double sc = rsq_nr(nrm);
+#pragma unroll
+    for (int i = 0; i < KP; ++i) y[i] *= sc;
+  } else if (!PAD && lane < K) {
     double dp = 0.0;
 #pragma unroll
     for (int i = 0; i < KP; ++i) {  // forward pivots -> y
@@ -1345,8 +1419,8 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
   if (lane < K) {
     double v = 0.0;
 #pragma unroll
-    for (int j = 0; j < KP; ++j)
-      if (j < K) v = fma(dd[j] * dd[j], y[j] * y[j], v);
+    for (int j = 0; j < KP; ++j)  // dd[j] = 0 past K (and y[j] = 0 there)
+      if (PAD || j < K) v = fma(dd[j] * dd[j], y[j] * y[j], v);
     vo[lane] = v / lam;
   }
 }
@@ -1951,6 +2025,12 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
                          K, M, DM, Cz, dvalid, ws);
     return true;
   }
+  if (g_bias_mode == 14 && K <= 44) {  // A/B: mask-free padded eigenvector phase
+    hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, true>),
+                       dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws,
+                       nullptr, nullptr);
+    return true;
+  }
   if (g_bias_mode == 13 && K <= 44) {  // A/B: four accumulators per matvec / dot product
     hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 4>), dim3(D * M),
                        dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr);
@@ -2020,7 +2100,7 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
 
 #define MFA_BIAS_LAUNCH(NBV_)                                                                   \
   {                                                                                            \
-    if ((g_bias_mode >= 3 && g_bias_mode <= 11) || g_bias_mode == 13 ||                        \
+    if ((g_bias_mode >= 3 && g_bias_mode <= 11) || g_bias_mode == 13 || g_bias_mode == 14 ||   \
         (g_bias_mode > 40 && g_bias_mode < 68) || g_bias_mode == 111 || g_bias_mode == 112)    \
       launch_bias_tri(D0, D, K, M, Cz, dvalid, ws, s);                                         \
     else if (g_bias_mode == 1)                                                                 \

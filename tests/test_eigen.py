@@ -163,6 +163,30 @@ def test_bias_mode13_four_accumulators_matches_mode5(cuda):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("K", [42, 30, 44])
+def test_bias_mode14_padded_eigenvectors_bitwise_mode5(cuda, K):
+    """A/B mode 14 (mode 5 with the tridiagonal padded to 44 rows by decoupled rows, so the
+    eigenvector recurrences carry no `i < K` tests): the same arithmetic on every real row and
+    the same twist index, so bitwise the mode-5 bias ratios; NaN dates stay NaN."""
+    import ctypes as C
+    from llm_driven_multi_factor_model_amd import _native
+    _native.register("mfa_eigen_set_bias_mode", [C.c_int])
+    F = _spd(7, K, seed=K, spread=2.5) * 1e-4
+    F[3] = float("nan")
+    Cz = eigen.mc_cov(12, K, 2520, seed=6, device=cuda)
+    lib = _native.lib()
+    out = {}
+    try:
+        for mode in (5, 14):
+            lib.mfa_eigen_set_bias_mode(mode)
+            out[mode] = eigen.eigen_risk_adjust(F.to(cuda), Cz=Cz, return_bias=True)[1].cpu()
+    finally:
+        lib.mfa_eigen_set_bias_mode(5)
+    assert torch.equal(out[5].isnan(), out[14].isnan())
+    assert torch.equal(out[14].nan_to_num(7.0), out[5].nan_to_num(7.0))
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("K,D,M", [(42, 7, 5), (30, 5, 4), (42, 1, 1)])
 def test_hip_dense_bias_solver_tail_and_invalid_dates(cuda, K, D, M):
     """Lane-dense solver (3 problems per 2-wave workgroup): a last workgroup with empty slots
