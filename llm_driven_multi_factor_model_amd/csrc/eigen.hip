@@ -998,7 +998,8 @@ size_t bias_tri_lds(int K, int KP) { return ((size_t)K * (KP + 1) + 7 * 64 + 2) 
 // PAD: the tridiagonal is padded to KP with decoupled rows (alpha = 1e300, beta = 0) before the
 // eigenvector phase, so its unrolled recurrences need no `i < K` tests: with a runtime K each
 // test was a 64-bit scalar mask, ~100 of them spilled to VGPR lanes and reloaded (v_readlane +
-// hazard nops + a branch) on every step of the dependent pivot chains (A/B bias mode 14).
+// hazard nops + a branch) on every step of the dependent pivot chains.  Default for mode 5 at
+// KP = 44 (12.0 -> 11.4-11.5 ms, bitwise the same ratios; mode 14 = unpadded, r04z/).
 template <int KP, bool PF = false, int ABL = 0, int WPE = MFA_TRI2_WPE, bool EIG = false,
           int ACC = 8, int LB = 8, int NA = 2, bool PAD = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void
@@ -1976,8 +1977,9 @@ int g_eigh_mode = 2;  // 0 = pair-block tournament Jacobi, 1 = row/column cyclic
 int g_fast_rot = 1;   // 1 = rcp/rsq + Newton rotation parameters (jacobi_cs<1>); 0 = IEEE div/sqrt
 int g_bias_mode = 5;  // 0 = packed (A, M) double2; 1 = split fp64 A / fp64 M; 2 = split, fp32 M;
                       // 3 = Householder tridiagonal + Laguerre / twisted factorisation;
-                      // 4 = its lean-layout kernel; 5 = lean layout + division-free Sturm
-                      // (default: 13.1 vs 17.5 ms for mode 3, profiles/r03_team/)
+                      // 4 = its lean-layout kernel; 5 = lean layout + division-free Sturm +
+                      // padded eigenvector phase (default: 11.4-11.5 ms; 17.5 for mode 3);
+                      // 14 = mode 5 without the padding (12.0 ms, profiles/r04/r04z/)
 
 size_t eigh_lds(int K) { return ((size_t)2 * K * (K + 1) + 4 * 64 + 64) * sizeof(double) + 64 * sizeof(int); }
 
@@ -1993,8 +1995,10 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
   if (g_bias_mode == 4 || g_bias_mode == 5) {
 #define MFA_TRI2(KP_)                                                                        \
     if (K <= KP_) {                                                                        \
-      if (g_bias_mode == 5)                                                                \
-        hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, true>), dim3(D * M), dim3(64),        \
+      if (g_bias_mode == 5) /* padded eigenvector phase at the measured width (K <= 44) */ \
+        hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, true, 0, MFA_TRI2_WPE, false, 8, 8, 2,  \
+                                                (KP_ == 44)>),                             \
+                           dim3(D * M), dim3(64),                                          \
                            bias_tri2_lds(K, KP_), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr);            \
       else                                                                                 \
         hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, false>), dim3(D * M), dim3(64),       \
@@ -2025,8 +2029,8 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
                          K, M, DM, Cz, dvalid, ws);
     return true;
   }
-  if (g_bias_mode == 14 && K <= 44) {  // A/B: mask-free padded eigenvector phase
-    hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, true>),
+  if (g_bias_mode == 14 && K <= 44) {  // A/B: mode 5 with the unpadded eigenvector phase
+    hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, false>),
                        dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws,
                        nullptr, nullptr);
     return true;

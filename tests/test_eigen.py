@@ -164,10 +164,10 @@ def test_bias_mode13_four_accumulators_matches_mode5(cuda):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("K", [42, 30, 44])
-def test_bias_mode14_padded_eigenvectors_bitwise_mode5(cuda, K):
-    """A/B mode 14 (mode 5 with the tridiagonal padded to 44 rows by decoupled rows, so the
-    eigenvector recurrences carry no `i < K` tests): the same arithmetic on every real row and
-    the same twist index, so bitwise the mode-5 bias ratios; NaN dates stay NaN."""
+def test_bias_padded_eigenvectors_bitwise_unpadded(cuda, K):
+    """Mode 5 pads the tridiagonal to 44 rows with decoupled rows, so its eigenvector
+    recurrences carry no `i < K` tests; mode 14 is the unpadded kernel.  Same arithmetic on every
+    real row and the same twist index: bitwise the same bias ratios; NaN dates stay NaN."""
     import ctypes as C
     from llm_driven_multi_factor_model_amd import _native
     _native.register("mfa_eigen_set_bias_mode", [C.c_int])
