@@ -1000,8 +1000,11 @@ size_t bias_tri_lds(int K, int KP) { return ((size_t)K * (KP + 1) + 7 * 64 + 2) 
 // test was a 64-bit scalar mask, ~100 of them spilled to VGPR lanes and reloaded (v_readlane +
 // hazard nops + a branch) on every step of the dependent pivot chains.  Default for mode 5 at
 // KP = 44 (12.0 -> 11.4-11.5 ms, bitwise the same ratios; mode 14 = unpadded, r04z/).
+// ZR: reflector rows are stored for every step s < K (rows K-2, K-1 hold u = 0), so the
+// Householder matvec always reads its own row: no per-read select of a fallback row (three
+// SALU + one VALU per LDS read in the ISA) and constant row offsets (A/B bias modes 15 / 16).
 template <int KP, bool PF = false, int ABL = 0, int WPE = MFA_TRI2_WPE, bool EIG = false,
-          int ACC = 8, int LB = 8, int NA = 2, bool PAD = false>
+          int ACC = 8, int LB = 8, int NA = 2, bool PAD = false, bool ZR = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void
 mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* __restrict__ Cz,
                     const int* __restrict__ dvalid, double* __restrict__ vout,
@@ -1023,7 +1026,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
     for (int k = lane; k < K; k += 64) vo[k] = qnan();
     return;
   }
-  const int nrow = (tri2_rows_doubles<KP>(K) + 1) & ~1;
+  const int nrow = (tri2_rows_doubles<KP>(ZR ? K + 2 : K) + 1) & ~1;
   double* R = sm;                          // packed reflector rows
   double* wb = R + nrow;                   // [64] broadcast w; Sturm counts later
   double2* tb = (double2*)(wb + 64);       // [64] {alpha_i, beta_{i-1}^2}
@@ -1097,7 +1100,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
         u = act ? (lane == s + 1 ? x0 - beta : x) : 0.0;
       }
       double* us = R + tri2_row_off<KP>(s) - J0;  // us[j], j in [J0, KP)
-      if (s + 2 < K && lane >= J0 && lane < KP) us[lane] = u;  // u_s, zero outside (s, K)
+      if ((ZR || s + 2 < K) && lane >= J0 && lane < KP) us[lane] = u;  // u_s, zero outside (s, K)
       if (lane == 0) {
         tb[s] = double2{alpha, s > 0 ? be[s - 1] * be[s - 1] : 0.0};
         be[s] = beta;
@@ -1109,7 +1112,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
       double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
       // rows s >= K - 2 are not stored (tau = 0 there): read the group's first row instead,
       // finite values times u = w = p = 0
-      if (s + 2 >= K) us = R + tri2_row_off<KP>(J0) - J0;
+      if (!ZR && s + 2 >= K) us = R + tri2_row_off<KP>(J0) - J0;
 #pragma unroll
       for (int j = J0; j < KP; j += 2) {
         const double2 uu = *(const double2*)(us + j);
@@ -2029,6 +2032,18 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
                          K, M, DM, Cz, dvalid, ws);
     return true;
   }
+  if ((g_bias_mode == 15 || g_bias_mode == 16) && K <= 44) {  // A/B: padded + every reflector
+    // row stored, LDS reads fenced every 2 (15) / 1 (16) double2 steps (LB 4 / 2: fewer spills)
+    if (g_bias_mode == 15)
+      hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 4, 2, true, true>),
+                         dim3(D * M), dim3(64), bias_tri2_lds(K + 2, 44), s, D0, K, M, Cz, dvalid,
+                         ws, nullptr, nullptr);
+    else
+      hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 2, 2, true, true>),
+                         dim3(D * M), dim3(64), bias_tri2_lds(K + 2, 44), s, D0, K, M, Cz, dvalid,
+                         ws, nullptr, nullptr);
+    return true;
+  }
   if (g_bias_mode == 14 && K <= 44) {  // A/B: mode 5 with the unpadded eigenvector phase
     hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, false>),
                        dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws,
@@ -2104,7 +2119,7 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
 
 #define MFA_BIAS_LAUNCH(NBV_)                                                                   \
   {                                                                                            \
-    if ((g_bias_mode >= 3 && g_bias_mode <= 11) || g_bias_mode == 13 || g_bias_mode == 14 ||   \
+    if ((g_bias_mode >= 3 && g_bias_mode <= 11) || (g_bias_mode >= 13 && g_bias_mode <= 16) || \
         (g_bias_mode > 40 && g_bias_mode < 68) || g_bias_mode == 111 || g_bias_mode == 112)    \
       launch_bias_tri(D0, D, K, M, Cz, dvalid, ws, s);                                         \
     else if (g_bias_mode == 1)                                                                 \

@@ -177,13 +177,14 @@ def test_bias_padded_eigenvectors_bitwise_unpadded(cuda, K):
     lib = _native.lib()
     out = {}
     try:
-        for mode in (5, 14):
+        for mode in (5, 14, 15, 16):  # 15 / 16: every reflector row stored (A/B)
             lib.mfa_eigen_set_bias_mode(mode)
             out[mode] = eigen.eigen_risk_adjust(F.to(cuda), Cz=Cz, return_bias=True)[1].cpu()
     finally:
         lib.mfa_eigen_set_bias_mode(5)
-    assert torch.equal(out[5].isnan(), out[14].isnan())
-    assert torch.equal(out[14].nan_to_num(7.0), out[5].nan_to_num(7.0))
+    for mode in (14, 15, 16):
+        assert torch.equal(out[5].isnan(), out[mode].isnan())
+        assert torch.equal(out[mode].nan_to_num(7.0), out[5].nan_to_num(7.0)), mode
 
 
 @pytest.mark.gpu
