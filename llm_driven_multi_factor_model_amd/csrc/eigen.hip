@@ -1003,8 +1003,10 @@ size_t bias_tri_lds(int K, int KP) { return ((size_t)K * (KP + 1) + 7 * 64 + 2) 
 // ZR: reflector rows are stored for every step s < K (rows K-2, K-1 hold u = 0), so the
 // Householder matvec always reads its own row: no per-read select of a fallback row (three
 // SALU + one VALU per LDS read in the ISA) and constant row offsets (A/B bias modes 15 / 16).
+// SK: the steps s >= K - 2 (tau = 0) skip the matvec and the update with a uniform branch, so
+// the matvec never needs the fallback row either, without storing extra rows (A/B mode 18).
 template <int KP, bool PF = false, int ABL = 0, int WPE = MFA_TRI2_WPE, bool EIG = false,
-          int ACC = 8, int LB = 8, int NA = 2, bool PAD = false, bool ZR = false>
+          int ACC = 8, int LB = 8, int NA = 2, bool PAD = false, bool ZR = false, bool SK = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void
 mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* __restrict__ Cz,
                     const int* __restrict__ dvalid, double* __restrict__ vout,
@@ -1112,7 +1114,11 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
       double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
       // rows s >= K - 2 are not stored (tau = 0 there): read the group's first row instead,
       // finite values times u = w = p = 0
-      if (!ZR && s + 2 >= K) us = R + tri2_row_off<KP>(J0) - J0;
+      if constexpr (SK) {
+        if (s + 2 >= K) continue;  // tau = 0: u = p = w = 0, nothing to update
+      } else if (!ZR && s + 2 >= K) {
+        us = R + tri2_row_off<KP>(J0) - J0;
+      }
 #pragma unroll
       for (int j = J0; j < KP; j += 2) {
         const double2 uu = *(const double2*)(us + j);
@@ -2044,6 +2050,12 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
                          ws, nullptr, nullptr);
     return true;
   }
+  if (g_bias_mode == 18 && K <= 44) {  // A/B: padded, steps s >= K-2 skip the update
+    hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, true, false, true>),
+                       dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws,
+                       nullptr, nullptr);
+    return true;
+  }
   if (g_bias_mode == 14 && K <= 44) {  // A/B: mode 5 with the unpadded eigenvector phase
     hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, false>),
                        dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws,
@@ -2119,7 +2131,7 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
 
 #define MFA_BIAS_LAUNCH(NBV_)                                                                   \
   {                                                                                            \
-    if ((g_bias_mode >= 3 && g_bias_mode <= 11) || (g_bias_mode >= 13 && g_bias_mode <= 16) || \
+    if ((g_bias_mode >= 3 && g_bias_mode <= 11) || (g_bias_mode >= 13 && g_bias_mode <= 18) || \
         (g_bias_mode > 40 && g_bias_mode < 68) || g_bias_mode == 111 || g_bias_mode == 112)    \
       launch_bias_tri(D0, D, K, M, Cz, dvalid, ws, s);                                         \
     else if (g_bias_mode == 1)                                                                 \
