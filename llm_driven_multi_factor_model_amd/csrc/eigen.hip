@@ -1004,7 +1004,8 @@ size_t bias_tri_lds(int K, int KP) { return ((size_t)K * (KP + 1) + 7 * 64 + 2) 
 // Householder matvec always reads its own row: no per-read select of a fallback row (three
 // SALU + one VALU per LDS read in the ISA) and constant row offsets (A/B bias modes 15 / 16).
 // SK: the steps s >= K - 2 (tau = 0) skip the matvec and the update with a uniform branch, so
-// the matvec never needs the fallback row either, without storing extra rows (A/B mode 18).
+// the matvec never needs the fallback row either, without storing extra rows.  Default with PAD
+// at KP = 44 (11.42-11.48 -> 11.36-11.38 ms, bitwise; `r04zc/`); mode 18 = the same kernel.
 template <int KP, bool PF = false, int ABL = 0, int WPE = MFA_TRI2_WPE, bool EIG = false,
           int ACC = 8, int LB = 8, int NA = 2, bool PAD = false, bool ZR = false, bool SK = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void
@@ -1987,7 +1988,8 @@ int g_fast_rot = 1;   // 1 = rcp/rsq + Newton rotation parameters (jacobi_cs<1>)
 int g_bias_mode = 5;  // 0 = packed (A, M) double2; 1 = split fp64 A / fp64 M; 2 = split, fp32 M;
                       // 3 = Householder tridiagonal + Laguerre / twisted factorisation;
                       // 4 = its lean-layout kernel; 5 = lean layout + division-free Sturm +
-                      // padded eigenvector phase (default: 11.4-11.5 ms; 17.5 for mode 3);
+                      // padded eigenvector phase + skipped no-op Householder steps (default:
+                      // 11.36-11.38 ms; 17.5 for mode 3);
                       // 14 = mode 5 without the padding (12.0 ms, profiles/r04/r04z/)
 
 size_t eigh_lds(int K) { return ((size_t)2 * K * (K + 1) + 4 * 64 + 64) * sizeof(double) + 64 * sizeof(int); }
@@ -2006,7 +2008,7 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
     if (K <= KP_) {                                                                        \
       if (g_bias_mode == 5) /* padded eigenvector phase at the measured width (K <= 44) */ \
         hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, true, 0, MFA_TRI2_WPE, false, 8, 8, 2,  \
-                                                (KP_ == 44)>),                             \
+                                                (KP_ == 44), false, (KP_ == 44)>),         \
                            dim3(D * M), dim3(64),                                          \
                            bias_tri2_lds(K, KP_), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr);            \
       else                                                                                 \
