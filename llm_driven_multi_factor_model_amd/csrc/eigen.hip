@@ -1006,8 +1006,11 @@ size_t bias_tri_lds(int K, int KP) { return ((size_t)K * (KP + 1) + 7 * 64 + 2) 
 // SK: the steps s >= K - 2 (tau = 0) skip the matvec and the update with a uniform branch, so
 // the matvec never needs the fallback row either, without storing extra rows.  Default with PAD
 // at KP = 44 (11.42-11.48 -> 11.36-11.38 ms, bitwise; `r04zc/`); mode 18 = the same kernel.
+// FL: the Laguerre loop's square root and divisions (laguerre_toward, sturm_gh_p's 1 / f) as
+// Newton-refined v_rsq / v_rcp (A/B bias mode 19).
 template <int KP, bool PF = false, int ABL = 0, int WPE = MFA_TRI2_WPE, bool EIG = false,
-          int ACC = 8, int LB = 8, int NA = 2, bool PAD = false, bool ZR = false, bool SK = false>
+          int ACC = 8, int LB = 8, int NA = 2, bool PAD = false, bool ZR = false, bool SK = false,
+          bool FL = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void
 mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* __restrict__ Cz,
                     const int* __restrict__ dvalid, double* __restrict__ vout,
@@ -1183,7 +1186,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
   double x = lane < K ? fmin(fmax(gs[lane], lo), hi) : 0.5 * (lo + hi);
   double G = 0.0, H = 0.0;
   auto sturm = [&](double xx) {
-    if constexpr (PF) return sturm_gh_p(tb, K, xx, G, H);
+    if constexpr (PF) return sturm_gh_p<FL>(tb, K, xx, G, H);
     else return sturm_gh(tb, K, xx, pivmin, G, H);
   };
   int cnt = sturm(x);
@@ -1206,7 +1209,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
       bool lag = false;
       double xn = 0.0;
       if (cnt == jt || cnt == jt + 1) {
-        xn = laguerre_toward(x, G, H, K, cnt == jt);
+        xn = laguerre_toward<FL>(x, G, H, K, cnt == jt);
         double st = fabs(xn - x);
         if (prev == cnt && st >= 1.5 * sprev) {
           xn = fma(8.0, xn - x, x);
@@ -2052,6 +2055,12 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
                          ws, nullptr, nullptr);
     return true;
   }
+  if (g_bias_mode == 19 && K <= 44) {  // A/B: the default + Newton-refined Laguerre arithmetic
+    hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, true, false, true, true>),
+                       dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws,
+                       nullptr, nullptr);
+    return true;
+  }
   if (g_bias_mode == 18 && K <= 44) {  // A/B: padded, steps s >= K-2 skip the update
     hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, true, false, true>),
                        dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws,
@@ -2133,7 +2142,7 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
 
 #define MFA_BIAS_LAUNCH(NBV_)                                                                   \
   {                                                                                            \
-    if ((g_bias_mode >= 3 && g_bias_mode <= 11) || (g_bias_mode >= 13 && g_bias_mode <= 18) || \
+    if ((g_bias_mode >= 3 && g_bias_mode <= 11) || (g_bias_mode >= 13 && g_bias_mode <= 19) || \
         (g_bias_mode > 40 && g_bias_mode < 68) || g_bias_mode == 111 || g_bias_mode == 112)    \
       launch_bias_tri(D0, D, K, M, Cz, dvalid, ws, s);                                         \
     else if (g_bias_mode == 1)                                                                 \

@@ -66,9 +66,15 @@ __device__ __forceinline__ int sturm_gh(const double2* tb, int K, double x, doub
 
 // Laguerre step for a degree-n real-rooted polynomial: the two candidates lie between x and
 // its adjacent roots; returns the one on the requested side (NaN if neither is finite).
+// FAST: Newton-refined v_rsq / v_rcp instead of the IEEE square root and divisions (~10
+// dependent instructions each on the iteration's critical path); the iteration is guarded by
+// Sturm counts, so ~1-ulp steps only move where it lands within the stopping tolerance.
+template <bool FAST = false>
 __device__ __forceinline__ double laguerre_toward(double x, double G, double H, int n, bool right) {
-  const double rad = sqrt(fmax(0.0, (double)(n - 1) * fma((double)n, H, -G * G)));
-  const double c1 = x - (double)n / (G + rad), c2 = x - (double)n / (G - rad);
+  const double q = (double)(n - 1) * fma((double)n, H, -G * G);
+  const double rad = FAST ? (q > 0.0 ? q * rsq_nr(q) : 0.0) : sqrt(fmax(0.0, q));
+  const double c1 = FAST ? x - (double)n * rcp_nr(G + rad) : x - (double)n / (G + rad);
+  const double c2 = FAST ? x - (double)n * rcp_nr(G - rad) : x - (double)n / (G - rad);
   const bool f1 = __builtin_isfinite(c1), f2 = __builtin_isfinite(c2);
   if (f1 && f2) return right ? fmax(c1, c2) : fmin(c1, c2);
   return f1 ? c1 : (f2 ? c2 : qnan());
@@ -81,6 +87,7 @@ __device__ __forceinline__ double laguerre_toward(double x, double G, double H, 
 // fmas off the previous two values (no reciprocal in the dependent chain: ~1/4 of the q-form's
 // chain latency).  The three sequences are rescaled together by a power of two every 4 steps
 // (exact), so they stay in range; they are homogeneous, so G and H are unaffected.
+template <bool FAST = false>
 __device__ __forceinline__ int sturm_gh_p(const double2* tb, int K, double x, double& G,
                                           double& H) {
   double f2 = 1.0, f1 = tb[0].x - x;   // f_0, f_1
@@ -111,7 +118,7 @@ __device__ __forceinline__ int sturm_gh_p(const double2* tb, int K, double x, do
     rescale();
   }
   for (; i < K; ++i) step(tb[i]);
-  const double r = 1.0 / f1;
+  const double r = FAST ? rcp_nr(f1) : 1.0 / f1;
   G = g1 * r;
   H = fma(G, G, -h1 * r);
   return cnt;

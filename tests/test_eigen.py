@@ -188,6 +188,30 @@ def test_bias_padded_eigenvectors_bitwise_unpadded(cuda, K):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("K", [42, 37])
+def test_bias_mode19_newton_laguerre_matches_default(cuda, K):
+    """A/B mode 19 (the default with Newton-refined reciprocal / square root in the Laguerre
+    loop): the Sturm-guarded iteration lands within its stopping tolerance of the same roots, so
+    the bias ratios agree with the default to rounding; NaN dates stay NaN."""
+    import ctypes as C
+    from llm_driven_multi_factor_model_amd import _native
+    _native.register("mfa_eigen_set_bias_mode", [C.c_int])
+    F = _spd(7, K, seed=K + 1, spread=2.5) * 1e-4
+    F[2] = float("nan")
+    Cz = eigen.mc_cov(12, K, 2520, seed=8, device=cuda)
+    lib = _native.lib()
+    out = {}
+    try:
+        for mode in (5, 19):
+            lib.mfa_eigen_set_bias_mode(mode)
+            out[mode] = eigen.eigen_risk_adjust(F.to(cuda), Cz=Cz, return_bias=True)[1].cpu()
+    finally:
+        lib.mfa_eigen_set_bias_mode(5)
+    assert torch.equal(out[5].isnan(), out[19].isnan())
+    torch.testing.assert_close(out[19], out[5], rtol=1e-12, atol=0, equal_nan=True)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("K,D,M", [(42, 7, 5), (30, 5, 4), (42, 1, 1)])
 def test_hip_dense_bias_solver_tail_and_invalid_dates(cuda, K, D, M):
     """Lane-dense solver (3 problems per 2-wave workgroup): a last workgroup with empty slots
