@@ -15,8 +15,9 @@ MEASURED = {
     # bench.py: fp64 storage, refine on, deterministic, graph replay: 0.384 ms / 2520 dates
     "xs_wls_fp64_reg_per_s": 6.55e6,
     # eigen_risk_adjust at 2520 dates x M = 100: tridiagonal eigh of F0 + bias solver mode 5
-    # + finalize (draw covariances given)
-    "eigen_adjust_2520x100_ms": 14.45,
+    # + finalize (draw covariances given); round 4 after the padded eigenvector phase
+    # (profiles/r04/r04ze/perf_guards.log)
+    "eigen_adjust_2520x100_ms": 12.42,
     # Newey-West expanding series, T = 2520, K = 42, q = 2
     "newey_west_2520_ms": 0.100,
     # window-descriptor kernels, 5000 x 3780, round 4 (profiles/r04/rolling_ab.jsonl, r04q/): BETA/
