@@ -1008,9 +1008,12 @@ size_t bias_tri_lds(int K, int KP) { return ((size_t)K * (KP + 1) + 7 * 64 + 2) 
 // at KP = 44 (11.42-11.48 -> 11.36-11.38 ms, bitwise; `r04zc/`); mode 18 = the same kernel.
 // FL: the Laguerre loop's square root and divisions (laguerre_toward, sturm_gh_p's 1 / f) as
 // Newton-refined v_rsq / v_rcp (A/B bias mode 19).
+// BT (with PAD): the back-transform skips a step on tau = 0 alone -- tau is 0 for s >= K - 2 and
+// padded to 0 past K -- instead of also testing s + 2 >= K (a spilled scalar mask per step, A/B
+// bias mode 20).
 template <int KP, bool PF = false, int ABL = 0, int WPE = MFA_TRI2_WPE, bool EIG = false,
           int ACC = 8, int LB = 8, int NA = 2, bool PAD = false, bool ZR = false, bool SK = false,
-          bool FL = false>
+          bool FL = false, bool BT = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void
 mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* __restrict__ Cz,
                     const int* __restrict__ dvalid, double* __restrict__ vout,
@@ -1241,6 +1244,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
     if (lane >= K) {
       tb[lane] = double2{1e300, 0.0};
       be[lane] = 0.0;
+      if constexpr (BT) ta[lane] = 0.0;
     }
     lds_order();
   }
@@ -1365,7 +1369,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
   auto back = [&](auto J0c, int s_hi) {
     constexpr int J0 = decltype(J0c)::value;
     for (int s = s_hi; s >= J0; --s) {
-      if (s + 2 >= K) continue;
+      if (!(PAD && BT) && s + 2 >= K) continue;
       const double tau = ta[s];
       if (tau == 0.0) continue;
       const double* us = R + tri2_row_off<KP>(s) - J0;
@@ -2055,6 +2059,12 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
                          ws, nullptr, nullptr);
     return true;
   }
+  if (g_bias_mode == 20 && K <= 44) {  // A/B: the default + tau-only back-transform skips
+    hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, true, false, true, false, true>),
+                       dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws,
+                       nullptr, nullptr);
+    return true;
+  }
   if (g_bias_mode == 19 && K <= 44) {  // A/B: the default + Newton-refined Laguerre arithmetic
     hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, true, false, true, true>),
                        dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws,
@@ -2142,7 +2152,7 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
 
 #define MFA_BIAS_LAUNCH(NBV_)                                                                   \
   {                                                                                            \
-    if ((g_bias_mode >= 3 && g_bias_mode <= 11) || (g_bias_mode >= 13 && g_bias_mode <= 19) || \
+    if ((g_bias_mode >= 3 && g_bias_mode <= 11) || (g_bias_mode >= 13 && g_bias_mode <= 20) || \
         (g_bias_mode > 40 && g_bias_mode < 68) || g_bias_mode == 111 || g_bias_mode == 112)    \
       launch_bias_tri(D0, D, K, M, Cz, dvalid, ws, s);                                         \
     else if (g_bias_mode == 1)                                                                 \

@@ -177,12 +177,13 @@ def test_bias_padded_eigenvectors_bitwise_unpadded(cuda, K):
     lib = _native.lib()
     out = {}
     try:
-        for mode in (5, 14, 15, 16, 18):  # 15 / 16: every reflector row stored; 18: skipped no-op steps
+        for mode in (5, 14, 15, 16, 18, 20):  # 15 / 16: every reflector row stored; 18: skipped
+            # no-op steps; 20: tau-only back-transform skips
             lib.mfa_eigen_set_bias_mode(mode)
             out[mode] = eigen.eigen_risk_adjust(F.to(cuda), Cz=Cz, return_bias=True)[1].cpu()
     finally:
         lib.mfa_eigen_set_bias_mode(5)
-    for mode in (14, 15, 16, 18):
+    for mode in (14, 15, 16, 18, 20):
         assert torch.equal(out[5].isnan(), out[mode].isnan())
         assert torch.equal(out[mode].nan_to_num(7.0), out[5].nan_to_num(7.0)), mode
 
