@@ -441,6 +441,21 @@ __device__ __forceinline__ void ew_compose(EwMap<NS>& m, const EwMap<NS>& p) {  
   m.reset = p.reset;
 }
 
+// One step of the map scan on DPP moves instead of ds_bpermute (no LDS round trip per field):
+// lanes without a source (row_shr past the row start, rows outside ROW_MASK) compose with the
+// identity map, which leaves m unchanged.  Steps row_shr 1 / 2 / 4 / 8, row_bcast:15 into rows
+// 1 / 3, row_bcast:31 into rows 2 / 3 form the inclusive scan (associative compose).
+template <int CTRL, int ROW_MASK, int NS>
+__device__ __forceinline__ void ew_dpp_step(EwMap<NS>& m) {
+  EwMap<NS> p;
+  p.A = dpp_upd<CTRL, ROW_MASK>(m.A, 1.0);
+#pragma unroll
+  for (int k = 0; k < NS; ++k) p.B[k] = dpp_upd<CTRL, ROW_MASK>(m.B[k], 0.0);
+  p.cnt = __builtin_amdgcn_update_dpp(0, m.cnt, CTRL, ROW_MASK, 0xF, false);
+  p.reset = __builtin_amdgcn_update_dpp(0, m.reset, CTRL, ROW_MASK, 0xF, false);
+  ew_compose(m, p);
+}
+
 template <int NS>
 __device__ __forceinline__ EwMap<NS> ew_shfl_up(const EwMap<NS>& m, int d) {
   EwMap<NS> p;
@@ -764,7 +779,8 @@ void launch_ew_pipe(const float* a, const float* b, const int* seg, int R, int W
 // outside [0, R) (its distance bits all set: neither a stock start nor valid)
 constexpr unsigned kCdD = 0x3FFFu, kCdOk = 0x4000u, kCdOut = 0xBFFFu;
 
-template <class Op, int C, int TR, bool PF = false, bool SL = true>
+// DS: the chunk-map scan on DPP (ew_dpp_step) instead of __shfl_up (A/B variant 12)
+template <class Op, int C, int TR, bool PF = false, bool SL = true, bool DS = false>
 __global__ __launch_bounds__(TR / C) __attribute__((amdgpu_waves_per_eu(4))) void
 ew_window_san_kernel(
     const float* __restrict__ in_a, const float* __restrict__ in_b,
@@ -884,10 +900,19 @@ ew_window_san_kernel(
       m.reset |= st ? 1 : 0;
     }
     // B. inclusive scan over the NT chunks
+    if constexpr (DS) {
+      ew_dpp_step<0x111, 0xF>(m);
+      ew_dpp_step<0x112, 0xF>(m);
+      ew_dpp_step<0x114, 0xF>(m);
+      ew_dpp_step<0x118, 0xF>(m);
+      ew_dpp_step<0x142, 0xA>(m);
+      ew_dpp_step<0x143, 0xC>(m);
+    } else {
 #pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-      const EwMap<NS> pm = ew_shfl_up(m, d);
-      if (lane >= d) ew_compose(m, pm);
+      for (int d = 1; d < 64; d <<= 1) {
+        const EwMap<NS> pm = ew_shfl_up(m, d);
+        if (lane >= d) ew_compose(m, pm);
+      }
     }
     if (lane == 63) wtot[wid] = m;
     __syncthreads();
@@ -985,7 +1010,7 @@ ew_window_san_kernel(
   }
 }
 
-template <class Op, int C, int TR, bool PF = false, bool SL = true>
+template <class Op, int C, int TR, bool PF = false, bool SL = true, bool DS = false>
 void launch_ew_san(const float* a, const float* b, const int* seg, int R, int W, int H,
                    double lam, int minp, float* o0, float* o1, hipStream_t s) {
   static int blocks = 0;
@@ -993,13 +1018,13 @@ void launch_ew_san(const float* a, const float* b, const int* seg, int R, int W,
     int dev = 0, cus = 0, per = 0;
     (void)hipGetDevice(&dev);
     (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, ew_window_san_kernel<Op, C, TR, PF, SL>,
-                                                       TR / C, 0);
+    (void)hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per, ew_window_san_kernel<Op, C, TR, PF, SL, DS>, TR / C, 0);
     blocks = max(1, cus * max(per, 1));
   }
   const int ntiles = (R + TR - H - 1) / (TR - H);
-  hipLaunchKernelGGL((ew_window_san_kernel<Op, C, TR, PF, SL>), dim3(min(ntiles, blocks)), dim3(TR / C),
-                     0, s, a, b, seg, R, W, H, lam, minp, o0, o1, ntiles);
+  hipLaunchKernelGGL((ew_window_san_kernel<Op, C, TR, PF, SL, DS>), dim3(min(ntiles, blocks)),
+                     dim3(TR / C), 0, s, a, b, seg, R, W, H, lam, minp, o0, o1, ntiles);
 }
 
 // A/B geometry of the anchored-prefix kernel (mfa_rolling_set_ew_variant): 0 = sanitised rows,
@@ -1029,6 +1054,8 @@ void launch_ew(const float* a, const float* b, const int* seg, int R, int W, int
     launch_ew_san<Op, 16, 4096, true>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
   else if (g_ew_variant == 11)  // 16-row chunks, 2048-row tiles on 2-wave workgroups
     launch_ew_san<Op, 16, 2048, true>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
+  else if (g_ew_variant == 12)  // the default with the chunk-map scan on DPP moves
+    launch_ew_san<Op, 8, 2048, true, true, true>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
   else if (g_ew_variant == 1)
     launch_ew_pipe<Op, 8, 4096>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
   else if (g_ew_variant == 2)

@@ -45,7 +45,7 @@ variants = [("mode2_r01", 2, 0), ("r03_default", 0, 5), ("san_8x512", 0, 6),
             ("san_8x256_prefetch", 0, 7), ("san_8x512_prefetch", 0, 8),
             ("ew_8x512", 0, 1), ("ew_16x256", 0, 2), ("ew_8x256_prefetch", 0, 3),
             ("ew_8x512_nopf", 0, 4), ("san_prefix_per_row", 0, 9), ("san_16x256_pf", 0, 10),
-            ("san_16x128_pf", 0, 11), ("default", 0, 0)]
+            ("san_16x128_pf", 0, 11), ("san_dpp_scan", 0, 12), ("default", 0, 0)]
 _native.register("mfa_rolling_set_ew_variant", [__import__("ctypes").c_int])
 ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 ref = {}
