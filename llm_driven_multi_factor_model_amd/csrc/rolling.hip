@@ -779,7 +779,8 @@ void launch_ew_pipe(const float* a, const float* b, const int* seg, int R, int W
 // outside [0, R) (its distance bits all set: neither a stock start nor valid)
 constexpr unsigned kCdD = 0x3FFFu, kCdOk = 0x4000u, kCdOut = 0xBFFFu;
 
-// DS: the chunk-map scan on DPP (ew_dpp_step) instead of __shfl_up (A/B variant 12)
+// DS: the chunk-map scan on DPP (ew_dpp_step) instead of __shfl_up (A/B variant 12: 113 / 96
+// instead of 119 / 102 VGPRs for BETA / DASTD; not timed in round 4 -- tools/gpu_r04zh.sh)
 template <class Op, int C, int TR, bool PF = false, bool SL = true, bool DS = false>
 __global__ __launch_bounds__(TR / C) __attribute__((amdgpu_waves_per_eu(4))) void
 ew_window_san_kernel(
@@ -1035,7 +1036,8 @@ void launch_ew_san(const float* a, const float* b, const int* seg, int R, int W,
 // half the scan steps per row), 3 = round-3 geometry with the software prefetch of the next
 // tile (3 waves / SIMD), 4 = 4096-row tiles without the prefetch, 6 = sanitised rows, 4096-row
 // tiles, 8 = sanitised rows, 4096-row tiles with the prefetch, 9 = variant 0 with the per-row
-// prefix subtraction instead of the sliding window update.
+// prefix subtraction instead of the sliding window update, 10 / 11 = 16-row chunks (slower,
+// r04v), 12 = variant 0 with the chunk-map scan on DPP moves (untimed).
 int g_ew_variant = 0;
 template <class Op>
 void launch_ew(const float* a, const float* b, const int* seg, int R, int W, int H, double lam,
