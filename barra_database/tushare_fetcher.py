@@ -52,6 +52,14 @@ def fetch_daily_prices(start_date: str, end_date: str, fields=DAILY_BASIC_FIELDS
     return _call("daily_basic", start_date=start_date, end_date=end_date, fields=fields)
 
 
+def fetch_daily_basic_by_stock(ts_code: str, start_date: str, end_date: str,
+                               fields=DAILY_BASIC_FIELDS) -> pd.DataFrame:
+    """One stock's daily_basic rows over [start_date, end_date] (the per-stock pull of
+    Barra_database/database/backfill_data.py:56-60 and fill_missing_data.py:57)."""
+    return _call("daily_basic", ts_code=ts_code, start_date=start_date, end_date=end_date,
+                 fields=fields)
+
+
 def fetch_daily_basic_by_date(trade_date: str, fields=DAILY_BASIC_FIELDS) -> pd.DataFrame:
     return _call("daily_basic", trade_date=trade_date, fields=fields)
 
