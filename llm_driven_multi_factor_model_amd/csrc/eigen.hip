@@ -26,9 +26,12 @@
 //     blocks written straight to their next-round slots (all LDS addresses precomputed);
 //   * grid (date, sim) for the simulations, per-(date, sim) bias vectors reduced by a
 //     separate deterministic pass (no float atomics -> bitwise reproducible).
+#include <utility>
+
 #include "common.h"
 #include "jacobi.h"
 #include "tridiag.h"
+#include "wide_gram.h"
 
 namespace {
 
@@ -232,6 +235,92 @@ __global__ __launch_bounds__(64) void mc_cov_reduce_kernel(int K, int T, int C,
   colsum[lane] = cs;
   wsync();
   mc_cov_finish(acc, colsum, K, T, Cz + (size_t)mi * K * K);
+}
+
+// ---------------- wide draw covariances (64 < K <= 144) on the fp64 matrix cores ----------------
+// mc_cov_kernel's scheme on a 4-wave workgroup per (sim, time chunk): a 64-row block of the
+// sim's normals (the same Philox counters {sim, time row, factor pair, tag}, so factor k draws
+// the same number at any K) is staged in LDS as Z[64][KP], and the KT (KT + 1) / 2 upper
+// 16 x 16 tiles of Z^T Z (KT = KP / 16: 21 tiles at KP = 96, 45 at 144) are dealt round-robin
+// to the 4 waves, each tile one v_mfma_f64_16x16x4f64 chain over the block's 16 k-steps.
+// Every (sim, chunk) writes its raw tile sums + column sums (lane-major) to `part`; the reduce
+// kernel adds the chunks in chunk order (mc_cov_chunks: a function of T only) and centres, so a
+// sim's matrix is bitwise the same in any launch.  Replaces the philox_normals_kernel +
+// rocBLAS batched GEMM of round 4 (no [M][T][K] normals buffer in HBM either).
+template <int KP>
+__global__ __launch_bounds__(256) void mc_cov_wide_kernel(int K, int T, unsigned long long seed,
+                                                          int m0, int C,
+                                                          double* __restrict__ part) {
+  using G = WideCov<KP>;
+  const int mi = blockIdx.x / C, c = blockIdx.x - mi * C;
+  const int m = m0 + mi, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nblk = (T + 63) / 64;
+  const int per = (nblk + C - 1) / C;
+  const int b0 = c * per, b1 = min(nblk, b0 + per);
+  __shared__ double Z[64][KP + 2];  // +2: rows 2 banks apart, conflict-free column reads
+  f64x4g acc[G::TPW];
+#pragma unroll
+  for (int u = 0; u < G::TPW; ++u) acc[u] = f64x4g{0.0, 0.0, 0.0, 0.0};
+  double cs = 0.0;  // column sum of factor tid (tid < KP)
+  constexpr int NPAIR = KP / 2;
+  for (int blk = b0; blk < b1; ++blk) {
+    const int t0 = blk * 64;
+    for (int e = tid; e < 64 * NPAIR; e += 256) {
+      const int r = e / NPAIR, pr = e - r * NPAIR, tq = t0 + r;
+      const U4 u = philox(U4{(unsigned)m, (unsigned)tq, (unsigned)pr, 0x4D464131u},
+                          (unsigned)seed, (unsigned)(seed >> 32));
+      const double rr = sqrt(-2.0 * log(u01_53(u.x, u.y)));
+      double sn, cn;
+      sincospi(2.0 * u01_53(u.z, u.w), &sn, &cn);
+      const bool okr = tq < T;
+      Z[r][2 * pr] = (okr && 2 * pr < K) ? rr * cn : 0.0;
+      Z[r][2 * pr + 1] = (okr && 2 * pr + 1 < K) ? rr * sn : 0.0;
+    }
+    __syncthreads();
+    wide_gram_block<KP>(Z, wv, lane, acc);
+    if (tid < KP)
+      for (int r = 0; r < 64; ++r) cs += Z[r][tid];
+    __syncthreads();
+  }
+  double* pp = part + (size_t)blockIdx.x * G::PART;
+#pragma unroll
+  for (int u = 0; u < G::TPW; ++u) {
+    const int t = wv + G::NW * u;
+    if (t < G::NT)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) pp[(t * 4 + e) * 64 + lane] = acc[u][e];
+  }
+  if (tid < KP) pp[G::NT * 4 * 64 + tid] = cs;
+}
+
+// Chunk-ordered sum of the C partials of sim mi, centring, both triangles of C_z.  Grid (M),
+// 256 threads: thread e of tile t's 256 (register, lane) slots.
+template <int KP>
+__global__ __launch_bounds__(256) void mc_cov_wide_reduce_kernel(int K, int T, int C,
+                                                                 const double* __restrict__ part,
+                                                                 double* __restrict__ Cz) {
+  using G = WideCov<KP>;
+  const int mi = blockIdx.x, tid = threadIdx.x;
+  __shared__ double colsum[KP];
+  for (int k = tid; k < KP; k += 256) {
+    double s = 0.0;
+    for (int c = 0; c < C; ++c) s += part[((size_t)mi * C + c) * G::PART + G::NT * 4 * 64 + k];
+    colsum[k] = s;
+  }
+  __syncthreads();
+  const double invT1 = 1.0 / (double)(T - 1), invT = 1.0 / (double)T;
+  double* Cm = Cz + (size_t)mi * K * K;
+  for (int t = 0; t < G::NT; ++t) {
+    const int e = tid >> 6, lane = tid & 63;  // register e of lane `lane`
+    double s = 0.0;
+    for (int c = 0; c < C; ++c) s += part[((size_t)mi * C + c) * G::PART + (t * 4 + e) * 64 + lane];
+    const int i = 16 * G::ti(t) + (lane >> 4) + 4 * e, j = 16 * G::tj(t) + (lane & 15);
+    if (i < K && j < K && (G::ti(t) != G::tj(t) || i <= j)) {
+      const double v = (s - colsum[i] * colsum[j] * invT) * invT1;
+      Cm[i * K + j] = v;
+      Cm[j * K + i] = v;
+    }
+  }
 }
 
 // Wide factor sets (K > 64): the standard normals of sims [m0, m0 + M) as Z [M][T][Kp]
@@ -1963,7 +2052,7 @@ __global__ __launch_bounds__(256) void eigen_finalize_kernel(const double* __res
                                                              int K, int M, int M_sum, double scale,
                                                              double* __restrict__ Fout,
                                                              double* __restrict__ vbias) {
-  __shared__ double g[64];
+  extern __shared__ double g[];  // [K]
   const int d = blockIdx.x, tid = threadIdx.x;
   const bool ok = dvalid[d] != 0;
   for (int k = tid; k < K; k += blockDim.x) {
@@ -2226,6 +2315,30 @@ MFA_API int mfa_mc_cov_range(int M, int m0, int K, int T, unsigned long long see
   return (int)hipGetLastError();
 }
 
+// Wide draw covariances (64 < K <= 144, mc_cov_wide_kernel): scratch doubles for (M, K, T).
+MFA_API size_t mfa_mc_cov_wide_ws_doubles(int M, int K, int T) {
+  const int C = mc_cov_chunks(M, T);
+  return (size_t)M * C * (K <= 96 ? WideCov<96>::PART : WideCov<144>::PART);
+}
+
+// Draw covariances of sims [m0, m0 + M), 64 < K <= 144, on the fp64 matrix cores: a sim's
+// matrix is bitwise the same in any launch containing it (chunking by T only).
+MFA_API int mfa_mc_cov_wide(int M, int m0, int K, int T, unsigned long long seed, double* ws,
+                            double* Cz, void* stream) {
+  if (M <= 0) return 0;
+  if (K <= 64 || K > 144 || T < 2 || m0 < 0 || ws == nullptr) return (int)hipErrorInvalidValue;
+  const int C = mc_cov_chunks(M, T);
+  hipStream_t s = (hipStream_t)stream;
+  if (K <= 96) {
+    hipLaunchKernelGGL(mc_cov_wide_kernel<96>, dim3(M * C), dim3(256), 0, s, K, T, seed, m0, C, ws);
+    hipLaunchKernelGGL(mc_cov_wide_reduce_kernel<96>, dim3(M), dim3(256), 0, s, K, T, C, ws, Cz);
+  } else {
+    hipLaunchKernelGGL(mc_cov_wide_kernel<144>, dim3(M * C), dim3(256), 0, s, K, T, seed, m0, C, ws);
+    hipLaunchKernelGGL(mc_cov_wide_reduce_kernel<144>, dim3(M), dim3(256), 0, s, K, T, C, ws, Cz);
+  }
+  return (int)hipGetLastError();
+}
+
 // Normals of sims [m0, m0 + M) for any K (Z: [M][T][K + (K & 1)] doubles); see
 // philox_normals_kernel.
 MFA_API int mfa_philox_normals(int M, int m0, int K, int T, unsigned long long seed, double* Z,
@@ -2273,7 +2386,7 @@ MFA_API int mfa_eigen_adjust(const double* D0, const double* U0, const int* dval
     MFA_BIAS_LAUNCH(4)
   else
     MFA_BIAS_LAUNCH(9)
-  hipLaunchKernelGGL(eigen_finalize_kernel, dim3(D), dim3(256), 0, s, ws, D0, U0, dvalid, K, M,
+  hipLaunchKernelGGL(eigen_finalize_kernel, dim3(D), dim3(256), K * sizeof(double), s, ws, D0, U0, dvalid, K, M,
                      0, scale, Fout, vbias);
   return (int)hipGetLastError();
 }
@@ -2300,8 +2413,8 @@ MFA_API int mfa_eigen_finalize_sum(const double* S, int M_total, const double* D
                                    const int* dvalid, int D, int K, double scale, double* Fout,
                                    double* vbias, void* stream) {
   if (D <= 0) return 0;
-  if (K < 1 || K > 64 || M_total < 1) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(eigen_finalize_kernel, dim3(D), dim3(256), 0, (hipStream_t)stream, S, D0, U0,
+  if (K < 1 || K > 4096 || M_total < 1) return (int)hipErrorInvalidValue;  // any K (LDS: K doubles)
+  hipLaunchKernelGGL(eigen_finalize_kernel, dim3(D), dim3(256), K * sizeof(double), (hipStream_t)stream, S, D0, U0,
                      dvalid, K, 1, M_total, scale, Fout, vbias);
   return (int)hipGetLastError();
 }

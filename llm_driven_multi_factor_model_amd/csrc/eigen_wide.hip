@@ -4,6 +4,7 @@
 // sim) the bias ratios v[k] = V[:,k]^T D0 V[:,k] / Lambda[k] of A = S C_z S (descending).
 #include "common.h"
 #include "tridiag.h"
+#include "wide_gram.h"
 
 namespace {
 
@@ -806,13 +807,196 @@ __global__ __launch_bounds__(64) void wide_bias_sum_kernel(const double* __restr
   }
 }
 
+// ---------------- wide eigh: orthogonality check + device Jacobi re-solve ----------------
+// After the tridiagonal EIG kernel, one 256-thread workgroup per matrix: err = max |U^T U - I|
+// from the fp64 matrix cores (wide_gram_block over 64-row blocks of U), and a matrix with a
+// finite input and !(err <= tol) -- non-orthogonal twisted-factorisation vectors of a clustered
+// spectrum, or a NaN from a solver failure on a finite matrix -- is re-solved in place by a
+// cyclic round-robin Jacobi: A (symmetrised) in the scratch `ws` [B][K][K], V in U itself, both
+// global (L2-resident while the workgroup runs).  Replaces the host-side U^T U check, the
+// torch.nonzero host sync and the rocSOLVER re-solve of round 4; matrices that pass exit after
+// the check.  Deterministic (fixed rotation order, no atomics).
+// Rotation of pair (p, q), zeroing A_pq: J_pp = J_qq = c, J_pq = s, J_qp = -s
+// (Golub-Van Loan sym.schur2); A <- J^T A J on 2 x 2 pair blocks, V <- V J.
+template <int KP>
+__global__ __launch_bounds__(256) void eigh_wide_fix_kernel(const double* __restrict__ Ain, int K,
+                                                            double tol, double* __restrict__ w,
+                                                            double* __restrict__ U,
+                                                            double* __restrict__ ws,
+                                                            int* __restrict__ fixed) {
+  using G = WideCov<KP>;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  __shared__ double Z[64][KP + 2];
+  __shared__ double red[4];
+  __shared__ double cs_c[KP / 2 + 1], cs_s[KP / 2 + 1];
+  __shared__ int idx[KP + 2];
+  const double* A = Ain + (size_t)b * K * K;
+  double* Ub = U + (size_t)b * K * K;
+  double* S = ws + (size_t)b * K * K;
+  bool fin = true;
+  for (int e = tid; e < K * K; e += 256) fin = fin && __builtin_isfinite(A[e]);
+  if (block_total<4>(fin ? 0.0 : 1.0, red, tid) != 0.0) {  // the EIG kernel wrote NaN already
+    if (tid == 0 && fixed) fixed[b] = 0;
+    return;
+  }
+  // ---- err = max |U^T U - I| ----
+  f64x4g acc[G::TPW];
+#pragma unroll
+  for (int u = 0; u < G::TPW; ++u) acc[u] = f64x4g{0.0, 0.0, 0.0, 0.0};
+  for (int r0 = 0; r0 < K; r0 += 64) {
+    __syncthreads();
+    for (int e = tid; e < 64 * KP; e += 256) {
+      const int r = e / KP, c = e - r * KP;
+      Z[r][c] = (r0 + r < K && c < K) ? Ub[(size_t)(r0 + r) * K + c] : 0.0;
+    }
+    __syncthreads();
+    wide_gram_block<KP>(Z, wv, lane, acc);
+  }
+  double err = 0.0;
+#pragma unroll
+  for (int u = 0; u < G::TPW; ++u) {
+    const int t = wv + G::NW * u;
+    if (t < G::NT) {
+      const int ti = G::ti(t), tj = G::tj(t);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int i = 16 * ti + (lane >> 4) + 4 * e, j = 16 * tj + (lane & 15);
+        if (i < K && j < K) {
+          const double g = fabs(acc[u][e] - (i == j ? 1.0 : 0.0));
+          err = (g > err || g != g) ? g : err;  // NaN propagates
+        }
+      }
+    }
+  }
+  err = block_ext<4, true>(err != err ? INFINITY : err, red, tid);
+  if (err <= tol) {
+    if (tid == 0 && fixed) fixed[b] = 0;
+    return;
+  }
+  // ---- Jacobi re-solve ----
+  const int Ke = K + (K & 1), np = Ke / 2;
+  for (int e = tid; e < K * K; e += 256) {
+    const int i = e / K, j = e - i * K;
+    S[e] = 0.5 * (A[e] + A[(size_t)j * K + i]);
+    Ub[e] = i == j ? 1.0 : 0.0;
+  }
+  for (int k = tid; k < Ke; k += 256) idx[k] = k;
+  __syncthreads();
+  auto at = [&](int i, int j) -> double { return (i < K && j < K) ? S[(size_t)i * K + j] : 0.0; };
+  for (int sweep = 0; sweep < 40; ++sweep) {
+    double nrot = 0.0;
+    for (int round = 0; round < Ke - 1; ++round) {
+      for (int i = tid; i < np; i += 256) {
+        int p = idx[i], q = idx[Ke - 1 - i];
+        if (p > q) { const int t = p; p = q; q = t; }
+        double c = 1.0, s = 0.0;
+        if (q < K) {
+          const double apq = at(p, q), app = at(p, p), aqq = at(q, q);
+          if (fabs(apq) > 1e-300 && fabs(apq) > 1e-17 * sqrt(fabs(app) * fabs(aqq))) {
+            const double tau = (aqq - app) / (2.0 * apq);
+            const double t = (tau >= 0.0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+            c = 1.0 / sqrt(1.0 + t * t);
+            s = t * c;
+            nrot += 1.0;
+          }
+        }
+        cs_c[i] = c;
+        cs_s[i] = s;
+      }
+      __syncthreads();
+      for (int e = tid; e < np * np; e += 256) {  // A <- J^T A J, one 2 x 2 pair block each
+        const int bi = e / np, bj = e - bi * np;
+        int p = idx[bi], q = idx[Ke - 1 - bi], r = idx[bj], t = idx[Ke - 1 - bj];
+        if (p > q) { const int x = p; p = q; q = x; }
+        if (r > t) { const int x = r; r = t; t = x; }
+        const double ci = cs_c[bi], si = cs_s[bi], cj = cs_c[bj], sj = cs_s[bj];
+        if (si == 0.0 && sj == 0.0) continue;
+        const double b00 = at(p, r), b01 = at(p, t), b10 = at(q, r), b11 = at(q, t);
+        const double x00 = ci * b00 - si * b10, x01 = ci * b01 - si * b11;
+        const double x10 = si * b00 + ci * b10, x11 = si * b01 + ci * b11;
+        double y00 = cj * x00 - sj * x01, y01 = sj * x00 + cj * x01;
+        double y10 = cj * x10 - sj * x11, y11 = sj * x10 + cj * x11;
+        if (bi == bj) { y01 = 0.0; y10 = 0.0; }
+        if (p < K && r < K) S[(size_t)p * K + r] = y00;
+        if (p < K && t < K) S[(size_t)p * K + t] = y01;
+        if (q < K && r < K) S[(size_t)q * K + r] = y10;
+        if (q < K && t < K) S[(size_t)q * K + t] = y11;
+      }
+      for (int e = tid; e < K * np; e += 256) {  // V <- V J
+        const int r = e / np, i = e - r * np;
+        const double c = cs_c[i], s = cs_s[i];
+        if (s == 0.0) continue;
+        int p = idx[i], q = idx[Ke - 1 - i];
+        if (p > q) { const int x = p; p = q; q = x; }
+        const double vp = Ub[(size_t)r * K + p], vq = Ub[(size_t)r * K + q];
+        Ub[(size_t)r * K + p] = c * vp - s * vq;
+        Ub[(size_t)r * K + q] = s * vp + c * vq;
+      }
+      __syncthreads();
+      if (tid == 0) {  // round-robin: position 0 fixed, the others shift by one
+        const int last = idx[Ke - 1];
+        for (int k = Ke - 1; k > 1; --k) idx[k] = idx[k - 1];
+        idx[1] = last;
+      }
+      __syncthreads();
+    }
+    if (block_total<4>(nrot, red, tid) == 0.0) break;
+    __syncthreads();
+  }
+  // ---- eigenvalues descending, eigenvectors permuted to match (via the scratch) ----
+  for (int k = tid; k < K; k += 256) {
+    const double dk = S[(size_t)k * K + k];
+    int rank = 0;
+    for (int j = 0; j < K; ++j) {
+      const double dj = S[(size_t)j * K + j];
+      rank += (dj > dk) || (dj == dk && j < k);
+    }
+    idx[k] = rank;
+    w[(size_t)b * K + rank] = dk;
+  }
+  __syncthreads();
+  for (int e = tid; e < K * K; e += 256) {
+    const int r = e / K, k = e - r * K;
+    S[(size_t)r * K + idx[k]] = Ub[e];
+  }
+  __syncthreads();
+  for (int e = tid; e < K * K; e += 256) Ub[e] = S[e];
+  if (tid == 0 && fixed) fixed[b] = 1;
+}
+
 }  // namespace
 
 // Wide factor sets: S[d][k] += sum over this call's M sims of v_m[d][k] for 2 < K <= 144 with the
 // multi-wave solver (one workgroup of 2 / 3 waves per (date, sim) for K <= 96 / 144); ws: D*M*K
 // doubles.  Invalid dates (dvalid[d] = 0) accumulate NaN.
-// Batched eigendecomposition of symmetric [B][K][K] matrices, 96 < K <= 144 (two lanes per row):
-// w [B][K] descending, U [B][K][K] with U[:, k] = eigenvector k (NaN for non-finite inputs).
+// Batched eigendecomposition of symmetric [B][K][K] matrices, 64 < K <= 144 (two lanes per row,
+// 3 / 5 waves for K <= 96 / 144): w [B][K] descending, U [B][K][K] with U[:, k] = eigenvector k
+// (NaN for non-finite inputs); then eigh_wide_fix_kernel checks U^T U = I to `tol` and re-solves
+// the matrices that fail with the Jacobi (ws: B*K*K doubles; fixed [B] nullable: 1 = re-solved).
+MFA_API int mfa_eigh_wide_fix(const double* A, int B, int K, double tol, double* w, double* U,
+                              double* ws, int* fixed, void* stream) {
+  if (B <= 0) return 0;
+  if (K <= 64 || K > 144 || ws == nullptr) return (int)hipErrorInvalidValue;
+  hipStream_t s = (hipStream_t)stream;
+  if (K <= 96) {
+    const size_t lds = bias_wide2_lds(K, 96, 3);
+    (void)hipFuncSetAttribute((const void*)mc_bias_wide2_kernel<96, 3, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((mc_bias_wide2_kernel<96, 3, true>), dim3(B), dim3(3 * 64), lds, s, A, K, 1,
+                       (const double*)nullptr, (const int*)nullptr, w, 0, U);
+    hipLaunchKernelGGL(eigh_wide_fix_kernel<96>, dim3(B), dim3(256), 0, s, A, K, tol, w, U, ws, fixed);
+  } else {
+    const size_t lds = bias_wide2_lds(K, 144, 5);
+    (void)hipFuncSetAttribute((const void*)mc_bias_wide2_kernel<144, 5, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((mc_bias_wide2_kernel<144, 5, true>), dim3(B), dim3(5 * 64), lds, s, A, K, 1,
+                       (const double*)nullptr, (const int*)nullptr, w, 0, U);
+    hipLaunchKernelGGL(eigh_wide_fix_kernel<144>, dim3(B), dim3(256), 0, s, A, K, tol, w, U, ws, fixed);
+  }
+  return (int)hipGetLastError();
+}
+
+// The tridiagonal EIG kernel alone (no check), 96 < K <= 144: A/B and tests.
 MFA_API int mfa_eigh_wide(const double* A, int B, int K, double* w, double* U, void* stream) {
   if (B <= 0) return 0;
   if (K <= 96 || K > 144) return (int)hipErrorInvalidValue;

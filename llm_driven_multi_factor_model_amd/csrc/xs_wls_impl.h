@@ -60,6 +60,9 @@ enum XsStatus : int {
   XS_ZERO_PIVOT = 8,     // exactly-zero pivots / empty industries (pinv semantics -> f = 0)
   XS_BAD_SIGMA = 16,     // pooled style std is zero / NaN
   XS_REFINED = 32,       // re-solved on the device with the eigen pseudo-inverse (pinv)
+  XS_PINV_CUT = 128,     // that pinv dropped an eigen-direction below 1e-15 lambda_max (a
+                         // numerically rank-deficient system, not necessarily an exactly
+                         // singular one: np.linalg.inv would not raise on it)
 };
 constexpr int XS_BAD = XS_NO_ROWS | XS_BAD_SIGMA | XS_PIVOT_EMPTY;
 
@@ -2394,7 +2397,7 @@ __device__ int struct_pinv_wave(const double* md, double* ws, int P, int pivot_m
     co[Q] = cst;
   }
   wsync();
-  return ncut > 0 ? XS_REFINED | XS_ZERO_PIVOT : XS_REFINED;
+  return ncut > 0 ? XS_REFINED | XS_PINV_CUT : XS_REFINED;
 }
 
 // Full-matrix Jacobi pinv of the constrained normal matrix, K <= kXsRefineMaxK (the reference's
@@ -2530,8 +2533,8 @@ __device__ int jacobi_pinv_block(const double* md, double* ws, int P, int pivot_
     co[Q] = cst;
   }
   wsync();
-  // same status semantics as the structured pinv (K > 64): ZERO_PIVOT iff a direction was cut
-  return ncut > 0.0 ? XS_REFINED | XS_ZERO_PIVOT : XS_REFINED;
+  // same status semantics as the structured pinv (K > 64): PINV_CUT iff a direction was cut
+  return ncut > 0.0 ? XS_REFINED | XS_PINV_CUT : XS_REFINED;
 }
 
 template <int Q>

@@ -287,7 +287,7 @@ class RiskModel:
         out = {"dates": int(st.numel())}
         for name, bit in (("no_rows", xs.XS_NO_ROWS), ("pivot_empty", xs.XS_PIVOT_EMPTY),
                           ("near_singular", xs.XS_NEAR_SINGULAR), ("zero_pivot", xs.XS_ZERO_PIVOT),
-                          ("bad_sigma", xs.XS_BAD_SIGMA)):
+                          ("pinv_cut", xs.XS_PINV_CUT), ("bad_sigma", xs.XS_BAD_SIGMA)):
             out[name] = int(((st & bit) != 0).sum())
         for name, t in (("factor_ret", self.factor_ret), ("nw_cov", self.nw_cov),
                         ("eigen_cov", self.eigen_cov), ("vra_cov", self.vra_cov)):

@@ -38,6 +38,7 @@ XS_NEAR_SINGULAR = 4
 XS_ZERO_PIVOT = 8
 XS_BAD_SIGMA = 16
 XS_REFINED = 32          # re-solved by the device pseudo-inverse pass
+XS_PINV_CUT = 128        # that pinv cut a direction below 1e-15 lambda_max (rank-deficient)
 XS_DETERMINISTIC = 0x100  # pivot_mode flag of mfa_xs_wls: bitwise-deterministic kernel
 XS_REFINE = 0x200         # pivot_mode flag: device pinv pass for near-singular dates
 REFINE_MAX_K = 64         # full-matrix Jacobi pinv up to this K; structured device pinv above

@@ -46,6 +46,11 @@ _native.register("mfa_eigen_bias_accumulate_wide", [C.c_void_p, C.c_void_p, C.c_
 _native.register("mfa_eigen_wide_set_variant", [C.c_int])
 _native.register("mfa_eigh_wide", [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
                                    C.c_void_p])
+_native.register("mfa_eigh_wide_fix", [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p,
+                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p])
+_native.register("mfa_mc_cov_wide", [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_void_p,
+                                     C.c_void_p, C.c_void_p])
+_native.register("mfa_mc_cov_wide_ws_doubles", [C.c_int, C.c_int, C.c_int])
 _native.register("mfa_eigen_finalize_sum", [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                              C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p,
                                              C.c_void_p, C.c_void_p])
@@ -53,10 +58,14 @@ _native.register("mfa_eigen_finalize_sum", [C.c_void_p, C.c_int, C.c_void_p, C.c
 MAX_SWEEPS = 30
 TOL = 1e-15
 # Factor sets wider than one wave (K > 64, e.g. SW-L2 industries: K = 140) leave the
-# register-resident one-wave kernels: the draws are the same Philox stream (factor k < 64 of a
-# sim is the same number at any K) with the covariance as one batched rocBLAS GEMM, and the
-# eigen-decompositions go through rocSOLVER's batched symmetric solver in bounded chunks.
+# register-resident one-wave kernels.  Up to WIDE_HIP_MAX_K everything stays on hand-written
+# kernels: the draw covariances on the fp64 matrix cores (mc_cov_wide_kernel, the same Philox
+# stream: factor k < 64 of a sim is the same number at any K), the F0 eigh and the bias statistic
+# on the multi-wave tridiagonal solver (csrc/eigen_wide.hip, with a device orthogonality check
+# and Jacobi re-solve), the finalize on eigen_finalize_kernel.  Wider K falls back to rocSOLVER's
+# batched symmetric solver and a rocBLAS GEMM in bounded chunks.
 WIDE_K = 64
+ORTHO_TOL = 1e-10                # wide eigh: max |U^T U - I| above this -> device Jacobi re-solve
 WIDE_CHUNK_DOUBLES = 1 << 27     # ~1 GB of fp64 per batched eigh / draw chunk
 # Bias statistic for 64 < K <= WIDE_HIP_MAX_K: "hip" (default: csrc/eigen_wide.hip, mode 5's
 # tridiagonal solver on one 2-3-wave workgroup per (date, sim): 4.6 us per 140 x 140 problem at
@@ -163,25 +172,20 @@ def eigh(A: torch.Tensor, max_sweeps: int = MAX_SWEEPS, tol: float = TOL):
 
 
 def _eigh_wide(Ab, shp):
-    """K > 64 on the device: for 96 < K <= WIDE_HIP_MAX_K the multi-wave HIP solver
-    (``mfa_eigh_wide``; matrices whose eigenvectors come out non-orthogonal to 1e-10, i.e.
-    clustered spectra, are re-solved by rocSOLVER), otherwise rocSOLVER's batched eigh of the
-    finite (symmetrised) matrices in chunks of ~WIDE_CHUNK_DOUBLES; NaN for non-finite inputs.
-    Eigenvalues descending."""
+    """K > 64 on the device: for K <= WIDE_HIP_MAX_K the multi-wave HIP solver
+    (``mfa_eigh_wide_fix``: matrices whose eigenvectors come out non-orthogonal to ORTHO_TOL,
+    i.e. clustered spectra, or NaN for a finite input, are re-solved on the device by a Jacobi),
+    otherwise rocSOLVER's batched eigh of the finite (symmetrised) matrices in chunks of
+    ~WIDE_CHUNK_DOUBLES; NaN for non-finite inputs.  Eigenvalues descending."""
     B, K = Ab.shape[0], Ab.shape[-1]
-    if _wide_solver == "hip" and 96 < K <= WIDE_HIP_MAX_K:
+    if _wide_solver == "hip" and K <= WIDE_HIP_MAX_K:
         w = torch.empty(B, K, dtype=torch.float64, device=Ab.device)
         U = torch.empty(B, K, K, dtype=torch.float64, device=Ab.device)
-        _native.call("mfa_eigh_wide", _native.ptr(Ab), B, K, _native.ptr(w), _native.ptr(U),
-                     _native.stream(Ab.device))
-        eye = torch.eye(K, dtype=torch.float64, device=Ab.device)
-        err = (U.transpose(-1, -2) @ U - eye).abs().amax((-1, -2))
-        redo = torch.nonzero(err > 1e-10).flatten()       # NaN matrices: err is NaN, not > tol
-        if redo.numel():
-            S = Ab[redo]
-            ww, UU = torch.linalg.eigh(0.5 * (S + S.transpose(-1, -2)))
-            w[redo] = ww.flip(-1)
-            U[redo] = UU.flip(-1)
+        ws = torch.empty(B * K * K, dtype=torch.float64, device=Ab.device)
+        # tridiagonal EIG kernel, then per matrix max |U^T U - I| on the matrix cores and a
+        # device Jacobi re-solve of the finite matrices that fail it (no host synchronisation)
+        _native.call("mfa_eigh_wide_fix", _native.ptr(Ab), B, K, ORTHO_TOL, _native.ptr(w),
+                     _native.ptr(U), _native.ptr(ws), None, _native.stream(Ab.device))
         return w.reshape(shp[:-1]), U.reshape(shp)
     w = torch.full((B, K), float("nan"), dtype=torch.float64, device=Ab.device)
     U = torch.full((B, K, K), float("nan"), dtype=torch.float64, device=Ab.device)
@@ -239,10 +243,19 @@ def mc_cov(M: int, K: int, T: int, seed: int = 1, device="cuda", m0: int = 0) ->
 
 
 def _mc_cov_wide(M: int, K: int, T: int, seed: int, dev, m0: int) -> torch.Tensor:
-    """K > 64: Philox normals Z [sims, T, K] (HIP kernel, same stream keys as the one-wave
-    draw kernel), then cov = (Z^T Z - s s^T / T) / (T - 1) with s the column sums: one batched
-    fp64 GEMM per chunk of sims (rocBLAS).  Each sim's covariance depends on that sim only, so
-    any partition of the sims gives the same matrices."""
+    """K > 64.  K <= WIDE_HIP_MAX_K: ``mc_cov_wide_kernel`` draws each sim's normals block by
+    block into LDS and accumulates Z^T Z on the fp64 matrix cores (time chunks a function of T
+    only, summed in order).  Wider: Philox normals Z [sims, T, K] (same stream keys) and
+    cov = (Z^T Z - s s^T / T) / (T - 1) as one batched rocBLAS GEMM per chunk of sims.  Each
+    sim's covariance depends on that sim only, so any partition of the sims gives the same
+    matrices."""
+    if K <= WIDE_HIP_MAX_K:
+        Cz = torch.empty(M, K, K, dtype=torch.float64, device=dev)
+        ws = torch.empty(max(1, _native.query("mfa_mc_cov_wide_ws_doubles", M, K, T)),
+                         dtype=torch.float64, device=dev)
+        _native.call("mfa_mc_cov_wide", M, int(m0), K, T, int(seed) & 0xFFFFFFFFFFFFFFFF,
+                     _native.ptr(ws), _native.ptr(Cz), _native.stream(dev))
+        return Cz
     Kp = K + (K & 1)
     Cz = torch.empty(M, K, K, dtype=torch.float64, device=dev)
     step = max(1, WIDE_CHUNK_DOUBLES // (T * Kp))
@@ -309,11 +322,15 @@ def _bias_sum_wide_hip(w, valid, Cz):
     return S
 
 
-def _finalize_torch(S, M, w, U, valid, scale_coef):
-    v = scale_coef * (torch.sqrt(S / M) - 1.0) + 1.0
-    vb = torch.where(valid[:, None], v, torch.full_like(v, float("nan")))
-    Fh = (U * (vb * vb * w)[:, None, :]) @ U.transpose(-1, -2)
-    Fh[~valid] = float("nan")
+def _finalize_wide(S, M, w, U, valid, scale_coef):
+    """v = a (sqrt(S / M) - 1) + 1, F^ = U diag(v^2 w) U^T: eigen_finalize_kernel (any K)."""
+    D, K = w.shape
+    dev = w.device
+    Fh = torch.empty(D, K, K, dtype=torch.float64, device=dev)
+    vb = torch.empty(D, K, dtype=torch.float64, device=dev)
+    _native.call("mfa_eigen_finalize_sum", _native.ptr(S.contiguous()), int(M), _native.ptr(w.contiguous()),
+                 _native.ptr(U.contiguous()), _native.ptr(valid.to(torch.int32).contiguous()),
+                 D, K, float(scale_coef), _native.ptr(Fh), _native.ptr(vb), _native.stream(dev))
     return Fh, vb
 
 
@@ -370,7 +387,7 @@ def eigen_risk_adjust_sharded(F0: torch.Tensor, *, M: int = 10_000, scale_coef: 
     if ctx.enabled:
         pdist.all_reduce_sum(S, ctx)
     if wide:
-        Fh, vb = _finalize_torch(S, M, w, U, valid, scale_coef)
+        Fh, vb = _finalize_wide(S, M, w, U, valid, scale_coef)
     elif dev.type == "cuda":
         Fh = torch.empty(D, K, K, dtype=torch.float64, device=dev)
         vb = torch.empty(D, K, dtype=torch.float64, device=dev)
@@ -422,7 +439,7 @@ def eigen_risk_adjust(F0: torch.Tensor, *, M: int = 100, scale_coef: float = 1.4
     if dev.type != "cuda":
         return _eigen_adjust_reference(w, U, valid, Cz, scale_coef, return_bias)
     if K > WIDE_K:
-        Fh, vb = _finalize_torch(_bias_sum_wide(w, valid, Cz), M, w, U, valid, scale_coef)
+        Fh, vb = _finalize_wide(_bias_sum_wide(w, valid, Cz), M, w, U, valid, scale_coef)
         return (Fh, vb) if return_bias else Fh
     Fh = torch.empty(D, K, K, dtype=torch.float64, device=dev)
     vb = torch.empty(D, K, dtype=torch.float64, device=dev)

@@ -252,3 +252,70 @@ def test_hip_wide_eigh_native(cuda):
     with eigen.using_wide_bias_solver("rocsolver"):
         w2, _ = eigen.eigh(F.to(cuda))
     torch.testing.assert_close(w2.cpu()[ok], w.cpu()[ok], rtol=1e-10, atol=1e-13)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [80, 101, 140])
+def test_hip_wide_mc_cov_is_fp64_cov_of_its_philox_draws(cuda, K):
+    """K > 64 draw covariances (mc_cov_wide_kernel, fp64 matrix cores): every entry equals
+    numpy's fp64 cov of the same Philox normals (tile layout, odd K, centring)."""
+    from tests.test_eigen import _philox_normals
+    T, M, seed = 300, 2, 7
+    Cz = eigen.mc_cov(M, K, T, seed=seed, device=cuda).cpu().numpy()
+    for m in range(M):
+        Z = _philox_normals(m, T, K, seed)
+        np.testing.assert_allclose(Cz[m], np.cov(Z.T), rtol=1e-11, atol=1e-13)
+
+
+def _clustered(B, K, seed=0):
+    """SPD matrices with exactly repeated eigenvalues (clusters of 1..6) and a scaled identity."""
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for b in range(B):
+        Q, _ = torch.linalg.qr(torch.randn(K, K, generator=g, dtype=torch.float64))
+        lam, k = [], 0
+        while len(lam) < K:
+            lam += [float(np.exp(-0.05 * k))] * (1 + (k * 7 + b) % 6)
+            k += 1
+        lam = torch.tensor(lam[:K], dtype=torch.float64)
+        out.append((Q * lam) @ Q.T)
+    out[-1] = 3e-4 * torch.eye(K, dtype=torch.float64)
+    return torch.stack(out)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [80, 140])
+def test_hip_wide_eigh_clustered_spectra_resolved_on_device(cuda, K):
+    """Finite matrices with repeated eigenvalues: the tridiagonal solver's vectors
+    are checked on the device (max |U^T U - I| <= 1e-10) and the failures re-solved by the device
+    Jacobi -- orthonormal U, A U = U diag(w), LAPACK eigenvalues; no host sync, no rocSOLVER."""
+    from llm_driven_multi_factor_model_amd import _native
+    A = torch.cat([_clustered(4, K, seed=K), _spd(2, K, seed=K + 1, spread=2.0)])
+    Ag = A.to(cuda).contiguous()
+    B = A.shape[0]
+    w = torch.empty(B, K, dtype=torch.float64, device=cuda)
+    U = torch.empty(B, K, K, dtype=torch.float64, device=cuda)
+    ws = torch.empty(B * K * K, dtype=torch.float64, device=cuda)
+    fixed = torch.full((B,), -1, dtype=torch.int32, device=cuda)
+    _native.call("mfa_eigh_wide_fix", _native.ptr(Ag), B, K, eigen.ORTHO_TOL, _native.ptr(w),
+                 _native.ptr(U), _native.ptr(ws), _native.ptr(fixed), _native.stream(cuda))
+    torch.cuda.synchronize()
+    w, U, fixed = w.cpu(), U.cpu(), fixed.cpu()
+    assert (fixed >= 0).all()
+    assert fixed[-1] == 0 and fixed[-2] == 0          # distinct spectra pass the check
+    eye = torch.eye(K, dtype=torch.float64)
+    scale = A.abs().amax((-1, -2))
+    for b in range(B):
+        assert (U[b].T @ U[b] - eye).abs().max() < 1e-10, (b, int(fixed[b]))
+        r = (A[b] @ U[b] - U[b] * w[b]).abs().max() / scale[b]
+        assert r < 1e-10, (b, float(r))
+        torch.testing.assert_close(w[b], torch.linalg.eigvalsh(A[b]).flip(-1), rtol=1e-10,
+                                   atol=1e-14 * float(scale[b]))
+    # the public entry point takes the same path
+    w2, U2 = eigen.eigh(Ag)
+    torch.testing.assert_close(w2.cpu(), w, rtol=0, atol=0)
+    # a NaN input stays NaN (not "re-solved")
+    An = Ag.clone()
+    An[1, 3, 5] = float("nan")
+    wn, Un = eigen.eigh(An)
+    assert torch.isnan(wn[1]).all() and torch.isfinite(wn[0]).all()

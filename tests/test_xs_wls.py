@@ -159,9 +159,11 @@ def test_device_pinv_refine_matches_oracle(cuda):
     torch.cuda.synchronize()
     st = out.status.cpu()
     assert ((st & X.XS_REFINED) != 0).all(), st
-    # the collinear styles leave one direction the pinv cuts: ZERO_PIVOT on every date, as in
-    # the structured K > 64 refine (same status semantics on both paths)
-    assert ((st & X.XS_ZERO_PIVOT) != 0).all(), st
+    # the collinear styles leave one direction the pinv cuts: PINV_CUT on every date, as in
+    # the structured K > 64 refine (same status semantics on both paths); no
+    # ZERO_PIVOT (the np.linalg.inv 'Singular matrix' bit): no direction is exactly empty
+    assert ((st & X.XS_PINV_CUT) != 0).all(), st
+    assert ((st & X.XS_ZERO_PIVOT) == 0).all(), st
     torch.testing.assert_close(out.f.cpu(), ref.f, rtol=1e-9, atol=1e-12)
     torch.testing.assert_close(out.r2.cpu(), ref.r2, rtol=1e-9, atol=1e-12)
     torch.testing.assert_close(out.resid.cpu(), ref.resid, rtol=1e-9, atol=1e-12, equal_nan=True)
@@ -199,7 +201,7 @@ def test_device_pinv_refine_any_k(cuda, P, Q):
     torch.cuda.synchronize()
     st = out.status.cpu()
     assert ((st & X.XS_REFINED) != 0).all(), st
-    assert ((st & X.XS_ZERO_PIVOT) != 0).all(), st
+    assert ((st & X.XS_PINV_CUT) != 0).all(), st
     torch.testing.assert_close(out.f.cpu(), ref.f, rtol=1e-9, atol=1e-12)
     torch.testing.assert_close(out.r2.cpu(), ref.r2, rtol=1e-9, atol=1e-12)
     torch.testing.assert_close(out.resid.cpu(), ref.resid, rtol=1e-9, atol=1e-12, equal_nan=True)
@@ -228,7 +230,7 @@ def test_stock_sharded_device_refine(cuda, P, Q):
     out = S.xs_wls_stock_sharded(g.styles, g.cap, g.ret, g.ind, p.P)
     torch.cuda.synchronize()
     assert ((out.status.cpu() & X.XS_REFINED) != 0).all()
-    assert ((out.status.cpu() & X.XS_ZERO_PIVOT) != 0).all()
+    assert ((out.status.cpu() & X.XS_PINV_CUT) != 0).all()
     torch.testing.assert_close(out.f.cpu(), ref.f, rtol=1e-9, atol=1e-12)
     torch.testing.assert_close(out.r2.cpu(), ref.r2, rtol=1e-9, atol=1e-12)
     torch.testing.assert_close(out.resid.cpu(), ref.resid, rtol=1e-9, atol=1e-12, equal_nan=True)
