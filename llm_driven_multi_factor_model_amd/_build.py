@@ -8,7 +8,12 @@ snapshot to the GPU box.
 
 Usage::
 
-    python -m llm_driven_multi_factor_model_amd._build [--force] [-j 8]
+    python -m llm_driven_multi_factor_model_amd._build [--force] [-j 8] [--ab]
+
+``--ab`` builds the A/B library ``_lib/ab/libmfa_hip.so`` with ``-DMFA_AB=1``: the kernel
+variants that lost their measured A/B comparisons and the timing-only ablations, which the
+default (production) library does not contain.  The ``tools/`` A/B scripts load it through
+``MFA_HIP_LIB=.../_lib/ab/libmfa_hip.so``; tests of those variants skip on the production build.
 """
 from __future__ import annotations
 
@@ -25,6 +30,8 @@ PKG_DIR = Path(__file__).resolve().parent
 CSRC = PKG_DIR / "csrc"
 OBJ_DIR = PKG_DIR / "_lib" / "obj"
 LIB_PATH = PKG_DIR / "_lib" / "libmfa_hip.so"
+AB_OBJ_DIR = PKG_DIR / "_lib" / "ab" / "obj"
+AB_LIB_PATH = PKG_DIR / "_lib" / "ab" / "libmfa_hip.so"
 HOST_SRC = PKG_DIR / "csrc_host"
 HOST_LIB_PATH = PKG_DIR / "_lib" / "libmfa_host.so"
 ARCH = os.environ.get("MFA_OFFLOAD_ARCH", "gfx950")
@@ -37,8 +44,9 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found (set HIPCC or install ROCm at /opt/rocm)")
 
 
-def _flags() -> list[str]:
+def _flags(ab: bool = False) -> list[str]:
     return [
+        *(["-DMFA_AB=1"] if ab else []),
         f"--offload-arch={ARCH}",
         "-O3",
         "-std=c++20",
@@ -72,8 +80,8 @@ def _stale(src: Path, obj: Path, headers: list[Path]) -> bool:
     return src.stat().st_mtime > t or any(h.stat().st_mtime > t for h in deps)
 
 
-def _compile(src: Path, obj: Path) -> tuple[Path, str]:
-    cmd = [_hipcc(), *_flags(), "-c", str(src), "-o", str(obj)]
+def _compile(src: Path, obj: Path, ab: bool = False) -> tuple[Path, str]:
+    cmd = [_hipcc(), *_flags(ab), "-c", str(src), "-o", str(obj)]
     p = subprocess.run(cmd, capture_output=True, text=True)
     if p.returncode != 0:
         raise RuntimeError(f"hipcc failed for {src.name}:\n{p.stderr}")
@@ -101,40 +109,44 @@ def build_host(force: bool = False, verbose: bool = False) -> Path:
     return HOST_LIB_PATH
 
 
-def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> Path:
-    """Compile all kernels (incrementally) and link the shared library; returns its path."""
+def build(force: bool = False, jobs: int | None = None, verbose: bool = False,
+          ab: bool = False) -> Path:
+    """Compile all kernels (incrementally) and link the shared library; returns its path.
+    ``ab``: the A/B library (MFA_AB=1) in ``_lib/ab/`` instead of the production one."""
     build_host(force=force, verbose=verbose)
-    OBJ_DIR.mkdir(parents=True, exist_ok=True)
+    obj_dir, lib_path = (AB_OBJ_DIR, AB_LIB_PATH) if ab else (OBJ_DIR, LIB_PATH)
+    obj_dir.mkdir(parents=True, exist_ok=True)
     headers = sorted(CSRC.glob("*.h"))
     srcs = sources()
-    objs = [OBJ_DIR / (s.stem + ".o") for s in srcs]
+    objs = [obj_dir / (s.stem + ".o") for s in srcs]
     todo = [(s, o) for s, o in zip(srcs, objs) if force or _stale(s, o, headers)]
     jobs = jobs or min(8, max(1, (os.cpu_count() or 2)))
     if todo:
         with cf.ThreadPoolExecutor(max_workers=min(jobs, len(todo))) as ex:
-            for obj, err in ex.map(lambda so: _compile(*so), todo):
+            for obj, err in ex.map(lambda so: _compile(*so, ab=ab), todo):
                 if verbose:
                     print(f"[mfa-build] compiled {obj.name}", file=sys.stderr)
-    relink = force or bool(todo) or not LIB_PATH.exists() or any(
-        o.stat().st_mtime > LIB_PATH.stat().st_mtime for o in objs)
+    relink = force or bool(todo) or not lib_path.exists() or any(
+        o.stat().st_mtime > lib_path.stat().st_mtime for o in objs)
     if relink:
-        tmp = LIB_PATH.with_suffix(".so.tmp")
+        tmp = lib_path.with_suffix(".so.tmp")
         cmd = [_hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", *map(str, objs), "-o", str(tmp)]
         p = subprocess.run(cmd, capture_output=True, text=True)
         if p.returncode != 0:
             raise RuntimeError(f"link failed:\n{p.stderr}")
-        os.replace(tmp, LIB_PATH)
+        os.replace(tmp, lib_path)
         if verbose:
-            print(f"[mfa-build] linked {LIB_PATH}", file=sys.stderr)
-    return LIB_PATH
+            print(f"[mfa-build] linked {lib_path}", file=sys.stderr)
+    return lib_path
 
 
 def main(argv: list[str] | None = None) -> int:
     ap = argparse.ArgumentParser(description=__doc__)
     ap.add_argument("--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=None)
+    ap.add_argument("--ab", action="store_true", help="A/B library with the losing variants")
     a = ap.parse_args(argv)
-    print(build(force=a.force, jobs=a.jobs, verbose=True))
+    print(build(force=a.force, jobs=a.jobs, verbose=True, ab=a.ab))
     return 0
 
 

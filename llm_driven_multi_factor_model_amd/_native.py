@@ -33,6 +33,7 @@ _SIGS: dict[str, list] = {
     "mfa_xs_set_chunks": [_i],
     "mfa_xs_set_mode": [_i],
     "mfa_xs_set_coop": [_i],
+    "mfa_ab_build": [],
     "mfa_xs_set_pipe": [_i, _i],
     "mfa_xs_coop_chunks": [_i, _i],
     "mfa_xs_det_supported": [_i, _i],
@@ -79,7 +80,13 @@ def lib() -> C.CDLL:
 
 
 def loaded_path() -> str | None:
-    return str(LIB_PATH) if _lib is not None else None
+    return os.environ.get("MFA_HIP_LIB", str(LIB_PATH)) if _lib is not None else None
+
+
+def ab_build() -> bool:
+    """True when the loaded library is the A/B build (MFA_AB=1: the losing kernel variants and
+    the timing ablations are compiled in; ``_build --ab``)."""
+    return bool(lib().mfa_ab_build())
 
 
 def ptr(t: torch.Tensor | None) -> C.c_void_p:

@@ -12,6 +12,13 @@
 
 #define MFA_API extern "C" __attribute__((visibility("default")))
 
+// MFA_AB = 1 (python -m llm_driven_multi_factor_model_amd._build --ab -> _lib/ab/libmfa_hip.so)
+// also instantiates the kernel variants that lost their A/B measurements and the timing-only
+// ablations, for the tools/ scripts; the default library holds the production kernels only.
+#ifndef MFA_AB
+#define MFA_AB 0
+#endif
+
 namespace mfa {
 
 constexpr int kWave = 64;

@@ -68,6 +68,7 @@ __device__ void sort_desc(const double* A, int K, int lda, int* perm) {
 }
 
 // ---------------- kernels ----------------
+#if MFA_AB  // row/column cyclic Jacobi (eigh mode 1, A/B only)
 // batched eigh: A [B][K][K] -> w [B][K] (descending), U [B][K][K] (U[:, k] = eigenvector k)
 __global__ __launch_bounds__(64) void eigh_kernel(const double* __restrict__ Ain, int K,
                                                   int max_sweeps, double tol,
@@ -114,6 +115,7 @@ __global__ __launch_bounds__(64) void eigh_kernel(const double* __restrict__ Ain
   }
   if (lane == 0 && sweeps) sweeps[b] = ns;
 }
+#endif
 
 // C_z,m = cov(z_m) (ddof 1) for z_m [T x K] standard normals, all fp64 like the reference's
 // numpy draws (MFM.py:113-120 via utils.py:70-76): 53-bit uniforms from Philox4x32-10, fp64
@@ -1100,15 +1102,30 @@ size_t bias_tri_lds(int K, int KP) { return ((size_t)K * (KP + 1) + 7 * 64 + 2) 
 // BT (with PAD): the back-transform skips a step on tau = 0 alone -- tau is 0 for s >= K - 2 and
 // padded to 0 past K -- instead of also testing s + 2 >= K (a spilled scalar mask per step, A/B
 // bias mode 20).
+// CH: dates per wave (warm-started eigenvalues, bias mode 21).  Wave (c, m) solves the
+// problems of dates CH c .. CH c + CH - 1 of sim m in order; each lane starts its Laguerre
+// iteration for the k-th largest eigenvalue from the previous date's k-th eigenvalue (a
+// slowly moving Newey-West spectrum: Weyl's bound |lambda_k(A) - lambda_k(B)| <= ||A - B||)
+// instead of the k-th largest diagonal entry.  The first date of a chain and every date after
+// an invalid one start cold.  Chains begin at global multiples of CH (Dn = D, dates counted
+// from 0 in every launch), so a sims-sharded or chunked run reproduces the one-shot result.
 template <int KP, bool PF = false, int ABL = 0, int WPE = MFA_TRI2_WPE, bool EIG = false,
           int ACC = 8, int LB = 8, int NA = 2, bool PAD = false, bool ZR = false, bool SK = false,
-          bool FL = false, bool BT = false>
+          bool FL = false, bool BT = false, int CH = 1>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void
 mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* __restrict__ Cz,
                     const int* __restrict__ dvalid, double* __restrict__ vout,
-                    double* __restrict__ Uout, int* __restrict__ flag) {
+                    double* __restrict__ Uout, int* __restrict__ flag, int Dn) {
+  static_assert(CH == 1 || (!EIG && ABL == 0), "date chains: bias problems only");
   extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int d = blockIdx.x / M, m = blockIdx.x % M, lane = threadIdx.x;
+  const int m = blockIdx.x % M, lane = threadIdx.x;
+  const int d_first = (blockIdx.x / M) * CH;
+  double lam_prev = 0.0;  // this lane's eigenvalue of the previous date (CH > 1)
+  bool warm = false;
+  for (int ci = 0; ci < CH; ++ci) {
+  const int d = d_first + ci;
+  if (CH > 1 && d >= Dn) break;
+  lds_order();  // the previous date's LDS reads precede this date's writes
   double* vo = vout + ((size_t)d * M + m) * K;
   const double* Ain = D0 + (size_t)d * K * K;  // EIG input matrix
   if constexpr (EIG) {
@@ -1122,7 +1139,8 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
     }
   } else if (!dvalid[d]) {
     for (int k = lane; k < K; k += 64) vo[k] = qnan();
-    return;
+    warm = false;
+    continue;
   }
   const int nrow = (tri2_rows_doubles<KP>(ZR ? K + 2 : K) + 1) & ~1;
   double* R = sm;                          // packed reflector rows
@@ -1276,6 +1294,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
   const int jt = K - 1 - lane;
   double lo = gl - 2.0 * kEps * tnorm - pivmin, hi = gu + 2.0 * kEps * tnorm + pivmin;
   double x = lane < K ? fmin(fmax(gs[lane], lo), hi) : 0.5 * (lo + hi);
+  if (CH > 1 && warm && lane < K) x = fmin(fmax(lam_prev, lo), hi);
   double G = 0.0, H = 0.0;
   auto sturm = [&](double xx) {
     if constexpr (PF) return sturm_gh_p<FL>(tb, K, xx, G, H);
@@ -1320,6 +1339,8 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
     }
     lam = x;
   }
+  lam_prev = lam;
+  warm = true;
   if constexpr ((ABL & 2) != 0) {  // ablation: no eigenvectors / back-transform
     if (lane < K) vo[lane] = lam;
     return;
@@ -1530,6 +1551,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
       if (PAD || j < K) v = fma(dd[j] * dd[j], y[j] * y[j], v);
     vo[lane] = v / lam;
   }
+  }  // date chain
 }
 
 // ---------------- lane-dense tridiagonal bias solver (bias mode 11, K <= 42) ----------------
@@ -2088,16 +2110,36 @@ int g_bias_mode = 5;  // 0 = packed (A, M) double2; 1 = split fp64 A / fp64 M; 2
                       // 11.36-11.38 ms; 17.5 for mode 3);
                       // 14 = mode 5 without the padding (12.0 ms, profiles/r04/r04z/)
 
+#if MFA_AB
 size_t eigh_lds(int K) { return ((size_t)2 * K * (K + 1) + 4 * 64 + 64) * sizeof(double) + 64 * sizeof(int); }
+#endif
 
 }  // namespace
 
-MFA_API void mfa_eigh_set_mode(int mode) { g_eigh_mode = mode; }
-MFA_API void mfa_eigen_set_fast_rotation(int on) { g_fast_rot = on; }
-MFA_API void mfa_eigen_set_bias_mode(int mode) { g_bias_mode = mode; }
+MFA_API int mfa_ab_build() { return MFA_AB; }
 
-// Householder-tridiagonal solver: KP = K rounded up to an instantiated register width.
-bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, const int* dvalid,
+// Setters return hipErrorInvalidValue for a variant this build does not contain (the A/B
+// variants are compiled only with MFA_AB=1: python -m ..._build --ab).
+MFA_API int mfa_eigh_set_mode(int mode) {
+  if (!MFA_AB && mode == 1) return (int)hipErrorInvalidValue;
+  g_eigh_mode = mode;
+  return 0;
+}
+MFA_API int mfa_eigen_set_fast_rotation(int on) {
+  if (!MFA_AB && !on) return (int)hipErrorInvalidValue;
+  g_fast_rot = on;
+  return 0;
+}
+MFA_API int mfa_eigen_set_bias_mode(int mode) {
+  if (!MFA_AB && mode != 0 && mode != 5 && !(mode >= 21 && mode <= 23)) return (int)hipErrorInvalidValue;
+  g_bias_mode = mode;
+  return 0;
+}
+
+#if MFA_AB
+// A/B-only solvers and timing ablations (tools builds, MFA_AB=1): mode 4 (lean layout, pivot-form
+// Sturm), 3 (round-2 kernel), 11 (lane-dense), 6-20 (mode-5 variants), 41-67 (ablations).
+bool launch_bias_tri_ab(const double* D0, int D, int K, int M, const double* Cz, const int* dvalid,
                      double* ws, hipStream_t s) {
   if (g_bias_mode == 4 || g_bias_mode == 5) {
 #define MFA_TRI2(KP_)                                                                        \
@@ -2106,10 +2148,10 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
         hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, true, 0, MFA_TRI2_WPE, false, 8, 8, 2,  \
                                                 (KP_ == 44), false, (KP_ == 44)>),         \
                            dim3(D * M), dim3(64),                                          \
-                           bias_tri2_lds(K, KP_), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr);            \
+                           bias_tri2_lds(K, KP_), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D);            \
       else                                                                                 \
         hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, false>), dim3(D * M), dim3(64),       \
-                           bias_tri2_lds(K, KP_), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr);            \
+                           bias_tri2_lds(K, KP_), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D);            \
       return true;                                                                         \
     }
     MFA_TRI2(8)
@@ -2141,63 +2183,63 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
     if (g_bias_mode == 15)
       hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 4, 2, true, true>),
                          dim3(D * M), dim3(64), bias_tri2_lds(K + 2, 44), s, D0, K, M, Cz, dvalid,
-                         ws, nullptr, nullptr);
+                         ws, nullptr, nullptr, D);
     else
       hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 2, 2, true, true>),
                          dim3(D * M), dim3(64), bias_tri2_lds(K + 2, 44), s, D0, K, M, Cz, dvalid,
-                         ws, nullptr, nullptr);
+                         ws, nullptr, nullptr, D);
     return true;
   }
   if (g_bias_mode == 20 && K <= 44) {  // A/B: the default + tau-only back-transform skips
     hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, true, false, true, false, true>),
                        dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws,
-                       nullptr, nullptr);
+                       nullptr, nullptr, D);
     return true;
   }
   if (g_bias_mode == 19 && K <= 44) {  // A/B: the default + Newton-refined Laguerre arithmetic
     hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, true, false, true, true>),
                        dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws,
-                       nullptr, nullptr);
+                       nullptr, nullptr, D);
     return true;
   }
   if (g_bias_mode == 18 && K <= 44) {  // A/B: padded, steps s >= K-2 skip the update
     hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, true, false, true>),
                        dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws,
-                       nullptr, nullptr);
+                       nullptr, nullptr, D);
     return true;
   }
   if (g_bias_mode == 14 && K <= 44) {  // A/B: mode 5 with the unpadded eigenvector phase
     hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, false>),
                        dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws,
-                       nullptr, nullptr);
+                       nullptr, nullptr, D);
     return true;
   }
   if (g_bias_mode == 13 && K <= 44) {  // A/B: four accumulators per matvec / dot product
     hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 4>), dim3(D * M),
-                       dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr);
+                       dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D);
     return true;
   }
   if (g_bias_mode == 10 && K <= 44) {  // A/B: LDS broadcast reads fenced in batches of 8 x 16 B
     hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 16>), dim3(D * M),
-                       dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr);
+                       dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D);
     return true;
   }
   if ((g_bias_mode == 8 || g_bias_mode == 9) && K <= 44) {  // A/B: Laguerre stop at 1e-9 / 1e-7
     if (g_bias_mode == 8)
       hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 9>), dim3(D * M),
-                         dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr);
+                         dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D);
     else
       hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 7>), dim3(D * M),
-                         dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr);
+                         dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D);
     return true;
   }
   if ((g_bias_mode == 6 || g_bias_mode == 7) && K <= 44) {  // A/B: mode 5 at 4 / 5 waves per SIMD
     if (g_bias_mode == 6)
       hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, 4>), dim3(D * M), dim3(64),
-                         bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr);
+                         bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D);
     else
       hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, 5>), dim3(D * M), dim3(64),
-                         bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr);
+                         bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D);
     return true;
   }
   if (g_bias_mode > 60 && g_bias_mode < 68 && K <= 44) {  // timing-only ablations of mode 5
@@ -2205,7 +2247,7 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
 #define MFA_TRI2_ABL(A_)                                                                     \
     if (abl == A_)                                                                         \
       hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, A_>), dim3(D * M), dim3(64),       \
-                         bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr);
+                         bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D);
     MFA_TRI2_ABL(1) MFA_TRI2_ABL(2) MFA_TRI2_ABL(3) MFA_TRI2_ABL(4) MFA_TRI2_ABL(5)
     MFA_TRI2_ABL(6) MFA_TRI2_ABL(7)
 #undef MFA_TRI2_ABL
@@ -2239,22 +2281,74 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
   return false;
 }
 
-#define MFA_BIAS_LAUNCH(NBV_)                                                                   \
-  {                                                                                            \
-    if ((g_bias_mode >= 3 && g_bias_mode <= 11) || (g_bias_mode >= 13 && g_bias_mode <= 20) || \
-        (g_bias_mode > 40 && g_bias_mode < 68) || g_bias_mode == 111 || g_bias_mode == 112)    \
-      launch_bias_tri(D0, D, K, M, Cz, dvalid, ws, s);                                         \
+#endif  // MFA_AB
+
+// Householder-tridiagonal solver (mode 5, the default): KP = K rounded up to an instantiated
+// register width; the padded eigenvector phase and skipped no-op steps at the measured width
+// (K <= 44).  The losing variants live behind MFA_AB (launch_bias_tri_ab).
+bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, const int* dvalid,
+                     double* ws, hipStream_t s) {
+  if (g_bias_mode == 5) {
+#define MFA_TRI2(KP_)                                                                        \
+    if (K <= KP_) {                                                                        \
+      hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, true, 0, MFA_TRI2_WPE, false, 8, 8, 2,    \
+                                              (KP_ == 44), false, (KP_ == 44)>),           \
+                         dim3(D * M), dim3(64), bias_tri2_lds(K, KP_), s, D0, K, M, Cz,    \
+                         dvalid, ws, nullptr, nullptr, D);                                    \
+      return true;                                                                         \
+    }
+    MFA_TRI2(8)
+    MFA_TRI2(16)
+    MFA_TRI2(24)
+    MFA_TRI2(32)
+    MFA_TRI2(44)
+    MFA_TRI2(48)
+    MFA_TRI2(64)
+#undef MFA_TRI2
+    return false;
+  }
+  if (g_bias_mode >= 21 && g_bias_mode <= 23 && K <= 44) {  // mode 5 + warm-started date chains
+#define MFA_TRI2_CH(CH_)                                                                       \
+    hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, true, false, \
+                                            true, false, false, CH_>),                           \
+                       dim3(((D + CH_ - 1) / CH_) * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, \
+                       Cz, dvalid, ws, nullptr, nullptr, D);
+    if (g_bias_mode == 21) MFA_TRI2_CH(8)
+    else if (g_bias_mode == 22) MFA_TRI2_CH(4)
+    else MFA_TRI2_CH(16)
+#undef MFA_TRI2_CH
+    return true;
+  }
+#if MFA_AB
+  return launch_bias_tri_ab(D0, D, K, M, Cz, dvalid, ws, s);
+#else
+  return false;
+#endif
+}
+
+#if MFA_AB
+#define MFA_BIAS_LAUNCH_AB(NBV_)                                                                \
     else if (g_bias_mode == 1)                                                                 \
       hipLaunchKernelGGL((mc_bias_split_kernel<NBV_, 1, double>), dim3(D * M), dim3(64),       \
                          bias_lds(K), s, D0, K, M, Cz, dvalid, max_sweeps, tol, ws);           \
     else if (g_bias_mode == 2)                                                                 \
       hipLaunchKernelGGL((mc_bias_split_kernel<NBV_, 1, float>), dim3(D * M), dim3(64),        \
                          bias_lds(K), s, D0, K, M, Cz, dvalid, max_sweeps, tol, ws);           \
-    else if (g_fast_rot)                                                                       \
-      hipLaunchKernelGGL((mc_bias_kernel<NBV_, 1>), dim3(D * M), dim3(64), bias_lds(K), s, D0, \
-                         K, M, Cz, dvalid, max_sweeps, tol, ws);                               \
-    else                                                                                       \
+    else if (!g_fast_rot)                                                                      \
       hipLaunchKernelGGL((mc_bias_kernel<NBV_, 0>), dim3(D * M), dim3(64), bias_lds(K), s, D0, \
+                         K, M, Cz, dvalid, max_sweeps, tol, ws);
+#else
+#define MFA_BIAS_LAUNCH_AB(NBV_)
+#endif
+// mode 0: pair-block Jacobi (fast rotations); every other mode: the tridiagonal dispatcher
+#define MFA_BIAS_LAUNCH(NBV_)                                                                   \
+  {                                                                                            \
+    if (g_bias_mode != 0 && g_bias_mode != 1 && g_bias_mode != 2) {                            \
+      if (!launch_bias_tri(D0, D, K, M, Cz, dvalid, ws, s)) return (int)hipErrorInvalidValue;  \
+    }                                                                                          \
+    MFA_BIAS_LAUNCH_AB(NBV_)                                                                   \
+    else                                                                                       \
+      hipLaunchKernelGGL((mc_bias_kernel<NBV_, 1>), dim3(D * M), dim3(64), bias_lds(K), s, D0, \
                          K, M, Cz, dvalid, max_sweeps, tol, ws);                               \
   }
 
@@ -2274,7 +2368,7 @@ MFA_API int mfa_eigh_batched(const double* A, int B, int K, int max_sweeps, doub
     if (!done && K <= KP_) {                                                                 \
       hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, true, 0, MFA_TRI2_WPE, true>), dim3(B),   \
                          dim3(64), eigh_tri2_lds(K, KP_), s, A, K, 1, (const double*)nullptr, \
-                         (const int*)nullptr, w, U, sweeps);                                 \
+                         (const int*)nullptr, w, U, sweeps, B);                               \
       done = true;                                                                           \
     }
     MFA_EIGT(8) MFA_EIGT(16) MFA_EIGT(24) MFA_EIGT(32) MFA_EIGT(44) MFA_EIGT(48) MFA_EIGT(64)
@@ -2282,18 +2376,20 @@ MFA_API int mfa_eigh_batched(const double* A, int B, int K, int max_sweeps, doub
     only = sweeps;  // the Jacobi below re-solves the flagged matrices only
     sweeps = nullptr;
   }
-  if (g_eigh_mode != 1 && nb <= 4 * 64 && rows_per_lane <= 14 && g_fast_rot)
+  if (nb <= 4 * 64 && rows_per_lane <= 14 && (g_fast_rot || !MFA_AB))
     hipLaunchKernelGGL((eigh_pairs_kernel<4, 14, 1>), dim3(B), dim3(64), eigh_pairs_lds(K), s, A,
                        K, max_sweeps, tol, w, U, sweeps, only);
-  else if (g_eigh_mode != 1 && nb <= 4 * 64 && rows_per_lane <= 14)
-    hipLaunchKernelGGL((eigh_pairs_kernel<4, 14>), dim3(B), dim3(64), eigh_pairs_lds(K), s, A, K,
-                       max_sweeps, tol, w, U, sweeps, only);
-  else if (g_eigh_mode != 1)
-    hipLaunchKernelGGL((eigh_pairs_kernel<9, 32>), dim3(B), dim3(64), eigh_pairs_lds(K), s, A, K,
-                       max_sweeps, tol, w, U, sweeps, only);
-  else
+#if MFA_AB
+  else if (g_eigh_mode == 1)  // A/B: row/column cyclic Jacobi
     hipLaunchKernelGGL(eigh_kernel, dim3(B), dim3(64), eigh_lds(K), s, A, K, max_sweeps, tol, w, U,
                        sweeps);
+  else if (nb <= 4 * 64 && rows_per_lane <= 14)  // A/B: IEEE rotation parameters
+    hipLaunchKernelGGL((eigh_pairs_kernel<4, 14>), dim3(B), dim3(64), eigh_pairs_lds(K), s, A, K,
+                       max_sweeps, tol, w, U, sweeps, only);
+#endif
+  else
+    hipLaunchKernelGGL((eigh_pairs_kernel<9, 32>), dim3(B), dim3(64), eigh_pairs_lds(K), s, A, K,
+                       max_sweeps, tol, w, U, sweeps, only);
   return (int)hipGetLastError();
 }
 

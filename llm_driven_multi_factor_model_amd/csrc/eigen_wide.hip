@@ -1013,7 +1013,11 @@ int g_wide_abl = 0;  // timing-only phase ablations (bits: 1 Laguerre, 2 eigenve
 int g_wide_variant = 1;  // 1 = two lanes per row for K > 96 (default: 26.9 vs 28.3 ms at K = 140,
                          // 60 x 100 problems, no spills), 0 = one lane per row
 MFA_API void mfa_eigen_wide_set_ablation(int abl) { g_wide_abl = abl; }
-MFA_API void mfa_eigen_wide_set_variant(int v) { g_wide_variant = v; }
+MFA_API int mfa_eigen_wide_set_variant(int v) {
+  if (!MFA_AB && v != 1) return (int)hipErrorInvalidValue;  // row layout at K > 96: A/B builds
+  g_wide_variant = v;
+  return 0;
+}
 
 MFA_API int mfa_eigen_bias_accumulate_wide(const double* D0, const int* dvalid, int D, int K,
                                            int M, const double* Cz, double* ws, double* S,
@@ -1038,7 +1042,11 @@ MFA_API int mfa_eigen_bias_accumulate_wide(const double* D0, const int* dvalid, 
     hipLaunchKernelGGL((mc_bias_wide_kernel<KP_, NW_>), dim3(D * M), dim3(NW_ * 64), lds, s, \
                        D0, K, M, Cz, dvalid, ws, g_wide_abl);                                \
   } else
-  MFA_WIDE(96, 2) MFA_WIDE(144, 3) {}
+#if MFA_AB
+  MFA_WIDE(96, 2) MFA_WIDE(144, 3) {}  // 144: one lane per row (A/B layout 0)
+#else
+  MFA_WIDE(96, 2) {}
+#endif
 #undef MFA_WIDE
   hipLaunchKernelGGL(wide_bias_sum_kernel, dim3(D), dim3(64), 0, s, ws, K, M, S);
   return (int)hipGetLastError();

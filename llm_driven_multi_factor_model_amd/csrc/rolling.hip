@@ -1037,14 +1037,18 @@ void launch_ew_san(const float* a, const float* b, const int* seg, int R, int W,
 // tile (3 waves / SIMD), 4 = 4096-row tiles without the prefetch, 6 = sanitised rows, 4096-row
 // tiles, 8 = sanitised rows, 4096-row tiles with the prefetch, 9 = variant 0 with the per-row
 // prefix subtraction instead of the sliding window update, 10 / 11 = 16-row chunks (slower,
-// r04v), 12 = variant 0 with the chunk-map scan on DPP moves (untimed).
+// r04v), 12 = variant 0 with the chunk-map scan on DPP moves (BETA 0.139 vs 0.142, DASTD 0.108
+// vs 0.095 ms: not adopted, profiles/r05/r05a/rolling_ab.jsonl).  Variants != 0: MFA_AB builds.
 int g_ew_variant = 0;
 template <class Op>
 void launch_ew(const float* a, const float* b, const int* seg, int R, int W, int H, double lam,
                int minp, float* o0, float* o1, hipStream_t s) {
-  if (g_ew_variant == 0)  // the next tile's loads in flight (BETA 119, DASTD 102 VGPRs)
+  if (g_ew_variant == 0 || !MFA_AB) {  // the next tile's loads in flight (BETA 119, DASTD 102 VGPRs)
     launch_ew_san<Op, 8, 2048, true>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
-  else if (g_ew_variant == 6)
+    return;
+  }
+#if MFA_AB
+  if (g_ew_variant == 6)
     launch_ew_san<Op, 8, 4096>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
   else if (g_ew_variant == 7)
     launch_ew_san<Op, 8, 2048, true>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
@@ -1068,6 +1072,7 @@ void launch_ew(const float* a, const float* b, const int* seg, int R, int W, int
     launch_ew_pipe<Op, 8, 2048, true>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
   else
     launch_ew_pipe<Op, 8, 2048, false>(a, b, seg, R, W, H, lam, minp, o0, o1, s);
+#endif
 }
 
 template <int H>
@@ -1751,18 +1756,29 @@ int ew_halo(int W) { return (W + kChunk - 1) / kChunk * kChunk; }
 #define MFA_GRID(R) dim3(((R) + 255) / 256), dim3(256)
 #define MFA_SCAN_GRID(R) dim3(((R) + kBlockRows - 1) / kBlockRows), dim3(256)
 
-MFA_API void mfa_rolling_set_mode(int mode) { g_roll_mode = mode; }
-MFA_API void mfa_rolling_set_ew_variant(int v) { g_ew_variant = v; }
+// mode 2 and ew variants != 0 exist only in MFA_AB builds (hipErrorInvalidValue otherwise)
+MFA_API int mfa_rolling_set_mode(int mode) {
+  if (!MFA_AB && mode == 2) return (int)hipErrorInvalidValue;
+  g_roll_mode = mode;
+  return 0;
+}
+MFA_API int mfa_rolling_set_ew_variant(int v) {
+  if (!MFA_AB && v != 0) return (int)hipErrorInvalidValue;
+  g_ew_variant = v;
+  return 0;
+}
 
 MFA_API int mfa_beta_hsigma(const float* y, const float* x, const int* seg_lo, int R, int W,
                             double lam, int minp, float* beta, float* hsig, void* s) {
   if (R <= 0) return 0;
   if (g_roll_mode == 0 && W >= 1 && W <= 256) {
     launch_ew<BetaOp>(y, x, seg_lo, R, W, ew_halo(W), lam, minp, beta, hsig, (hipStream_t)s);
-  } else if (g_roll_mode == 2 && W <= 256)
+#if MFA_AB
+  } else if (g_roll_mode == 2 && W <= 256) {
     hipLaunchKernelGGL(beta_hsigma_scan_kernel<256>, MFA_SCAN_GRID(R), 0, (hipStream_t)s, y, x,
                        seg_lo, R, W, lam, minp, beta, hsig);
-  else
+#endif
+  } else
     hipLaunchKernelGGL(beta_hsigma_kernel, MFA_GRID(R), 0, (hipStream_t)s, y, x, seg_lo, R, W, lam,
                        minp, beta, hsig);
   return (int)hipGetLastError();
@@ -1771,11 +1787,13 @@ MFA_API int mfa_rstr(const float* lr, const int* seg_lo, int R, int L, int W, do
                      int minp, float* out, void* s) {
   if (R <= 0) return 0;
   if (g_roll_mode == 0 && L >= 1 && W >= 1 && W + L - 1 <= kRsH && W <= kRsWRows) {
+#if MFA_AB
     if (g_ew_variant == 5)  // A/B: the round-3 pass 2 (one row per lane)
       hipLaunchKernelGGL(rstr_ew_kernel<false>, dim3((R + kRsRows - 1) / kRsRows),
                          dim3(kRsWaves * 64), 0, (hipStream_t)s, lr, seg_lo, R, L, W, lam, minp,
                          out);
     else
+#endif
       hipLaunchKernelGGL(rstr_ew_kernel<true>, dim3((R + kRsRows - 1) / kRsRows),
                          dim3(kRsWaves * 64), 0, (hipStream_t)s, lr, seg_lo, R, L, W, lam, minp,
                          out);
@@ -1792,10 +1810,12 @@ MFA_API int mfa_dastd(const float* ret, const float* mret, const int* seg_lo, in
   if (R <= 0) return 0;
   if (g_roll_mode == 0 && W >= 1 && W <= 256) {
     launch_ew<DastdOp>(ret, mret, seg_lo, R, W, ew_halo(W), lam, minp, out, out, (hipStream_t)s);
-  } else if (g_roll_mode == 2 && W <= 256)
+#if MFA_AB
+  } else if (g_roll_mode == 2 && W <= 256) {
     hipLaunchKernelGGL(dastd_scan_kernel<256>, MFA_SCAN_GRID(R), 0, (hipStream_t)s, ret, mret,
                        seg_lo, R, W, lam, minp, out);
-  else
+#endif
+  } else
     hipLaunchKernelGGL(dastd_kernel, MFA_GRID(R), 0, (hipStream_t)s, ret, mret, seg_lo, R, W, lam,
                        minp, out);
   return (int)hipGetLastError();

@@ -10,24 +10,39 @@ int g_mfa_xs_coop = 0;
 int g_mfa_xs_lag = 1;
 int g_mfa_xs_pipe_wpc = 0;
 
-// Ablation: 0 = fused single-kernel path with the residual prefetch during the wave-0 solve
-// (default), 1 = three separate kernels, 7 = fused without the prefetch.  Applies to both the
-// fp32 and fp64 entry points.
-MFA_API void mfa_xs_set_mode(int mode) { g_mfa_xs_mode = mode; }
+// Kernel mode for the next calls (both storage types): 0 = the fused kernel (production).  The
+// A/B modes (1 = three separate kernels, 7 = fused without the prefetch, 10-12 MFMA moments,
+// 20-24 forced moment sources, 30-38 resident kernel) exist only in MFA_AB builds:
+// hipErrorInvalidValue otherwise.
+MFA_API int mfa_xs_set_mode(int mode) {
+  if (!MFA_AB && mode != 0) return (int)hipErrorInvalidValue;
+  g_mfa_xs_mode = mode;
+  return 0;
+}
 unsigned long long* g_mfa_xs_prof = nullptr;
 MFA_API void mfa_xs_set_prof(void* p) { g_mfa_xs_prof = (unsigned long long*)p; }
 
 // Stock chunks per date for the next calls: 0 = automatic (default: the fused kernel,
-// kXsChunkMinD = 0), > 0 = forced chunk count, < 0 = always one workgroup per date.
-MFA_API void mfa_xs_set_chunks(int S) { g_mfa_xs_chunks = S; }
+// kXsChunkMinD = 0), > 0 = forced chunk count (A/B builds only: the chunked path measured
+// slower at every shard size, profiles/r04/README.md), < 0 = always one workgroup per date.
+MFA_API int mfa_xs_set_chunks(int S) {
+  if (!MFA_AB && S > 0) return (int)hipErrorInvalidValue;
+  g_mfa_xs_chunks = S;
+  return 0;
+}
 
-// Pipelined team CS-WLS kernel for the next calls: 0 = off, C > 0 = C chunks per date,
-// < 0 = automatic chunk count (xs_coop_chunks).
-MFA_API void mfa_xs_set_coop(int C) { g_mfa_xs_coop = C; }
+// Pipelined team CS-WLS kernel for the next calls (A/B builds only): 0 = off, C > 0 = C chunks
+// per date, < 0 = automatic chunk count (xs_coop_chunks).
+MFA_API int mfa_xs_set_coop(int C) {
+  if (!MFA_AB && C != 0) return (int)hipErrorInvalidValue;
+  g_mfa_xs_coop = C;
+  return 0;
+}
 // Pipelined team kernel: residual-pass lag in tickets (1..3) and workgroups per CU (0 = max).
-MFA_API void mfa_xs_set_pipe(int lag, int wpc) {
+MFA_API int mfa_xs_set_pipe(int lag, int wpc) {
   g_mfa_xs_lag = lag;
   g_mfa_xs_pipe_wpc = wpc;
+  return 0;
 }
 MFA_API int mfa_xs_coop_chunks(int D, int N) { return xs_coop_chunks(D, N); }
 

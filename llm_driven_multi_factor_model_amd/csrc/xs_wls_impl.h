@@ -2753,7 +2753,12 @@ hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, 
   if (det && !rep8) return hipErrorNotSupported;
   const int16_t* indp = P > 0 ? ind : nullptr;
   constexpr bool PRE = sizeof(T) == 4;
+#if MFA_AB
   const size_t res_lds = (!team && !chunked) ? xs_resident_lds<Q, T>(mode, det, D, N, P) : 0;
+#else
+  (void)team; (void)chunked; (void)C; (void)sums; (void)sync; (void)mode;
+#endif
+#if MFA_AB  // team (pipelined) and chunked paths, MFMA / resident / forced-variant A/B modes
   if (team) {
     if (hipError_t err = hipMemsetAsync(sync, 0, (kPipeGroups + 3 * (size_t)D) * sizeof(int), s)) return err;
     const int lag = xs_pipe_lag();
@@ -2853,6 +2858,13 @@ hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, 
       hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR | 32 | 64, PRE, T>), dim3(D),
                          dim3(256), lds1, s, X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2,
                          stats, status, mom, okm);
+  } else
+#endif  // MFA_AB
+  if (det && xs_plain_moments<T>(D)) {
+    // moments from plain vector loads (default for fp32 panels and small fp64 shards)
+    hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR | 32 | 64, PRE, T>), dim3(D),
+                       dim3(256), lds1, s, X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2,
+                       stats, status, mom, okm);
   } else if (det) {  // bitwise-reproducible variant of the default path
     // residual prefetch during the solve on every storage type here (fp64 panels, D > 512:
     // 2520 dates 382 -> 370 us, profiles/r03_xs_pre64_ab.jsonl; no gain on the plain-load path)

@@ -231,7 +231,8 @@ class DeviceFactorEngine(FactorEngine):
         vb = vf[inv]
         if not bool(((v == vb) | (v.isnan() & vb.isnan())).all()):
             raise NeedsPandasPath("several cash-flow values for one (stock, end_date)")
-        self._ttm = RL.rolling_sum(vf.float(), RL.seg_lo_from_codes(seg_codes), 4, 4).double()[inv]
+        with RL.direct_kernels(self._direct()):
+            self._ttm = RL.rolling_sum(vf.float(), RL.seg_lo_from_codes(seg_codes), 4, 4).double()[inv]
         return self._ttm
 
     def compute_earnings_yield(self):
@@ -505,6 +506,9 @@ def exposures(prices, index, sw_industry: pd.DataFrame, factor_cfg: FactorConfig
         prices, index = _columns_from_frames(prices, index)
     if ctx is not None and ctx.enabled and device is None:
         device = ctx.device
+    # the pipeline's descriptors are rank-invariant by default: a date-sharded run equals the
+    # single-process run bit for bit at any world size (FactorConfig.rank_invariant)
+    factor_cfg = factor_cfg or FactorConfig(rank_invariant=True)
     full = DeviceFactorEngine(prices, index, device=device, config=factor_cfg)
     if ctx is not None and ctx.enabled:
         from ..parallel import dist as pdist

@@ -317,7 +317,8 @@ class FactorEngine:
         if not same.all():
             return None
         seg = RL.seg_lo_from_codes(torch.from_numpy(uk // (ne + 1))).to(self.device)
-        ttm = RL.rolling_sum(torch.from_numpy(vf.astype(np.float32)).to(self.device), seg, 4, 4)
+        with RL.direct_kernels(self._direct()):
+            ttm = RL.rolling_sum(torch.from_numpy(vf.astype(np.float32)).to(self.device), seg, 4, 4)
         return ttm.double()[torch.from_numpy(inv).to(self.device)]
 
     def _ttm_runs(self, m: pd.DataFrame):
@@ -349,7 +350,8 @@ class FactorEngine:
         if not bool(((v == vb) | (v.isnan() & vb.isnan())).all()):
             return None
         seg = RL.seg_lo_from_codes(sc[first].to(torch.int32))
-        ttm = RL.rolling_sum(vf.float(), seg, 4, 4)
+        with RL.direct_kernels(self._direct()):
+            ttm = RL.rolling_sum(vf.float(), seg, 4, 4)
         return ttm.double()[inv]
 
     def _ttm_by_merge(self, m: pd.DataFrame):
@@ -358,7 +360,8 @@ class FactorEngine:
         codes = torch.from_numpy(pd.factorize(fin["ts_code"].astype(str))[0].astype(np.int32))
         seg = RL.seg_lo_from_codes(codes).to(self.device)
         v = torch.from_numpy(fin["n_cashflow_act"].to_numpy(np.float32, na_value=np.nan)).to(self.device)
-        ttm = RL.rolling_sum(v, seg, 4, 4)  # statement-row TTM (quirk Q18)
+        with RL.direct_kernels(self._direct()):
+            ttm = RL.rolling_sum(v, seg, 4, 4)  # statement-row TTM (quirk Q18)
         fin["n_cashflow_act_ttm"] = ttm.double().cpu().numpy()
         tmp = m[["original_index", "ts_code", "end_date"]].merge(
             fin[["ts_code", "end_date", "n_cashflow_act_ttm"]], on=["ts_code", "end_date"], how="left")
@@ -393,17 +396,23 @@ class FactorEngine:
         "GROWTH": "select_growth_factors", "LEVERAGE": "compute_leverage",
     }
 
+    def _direct(self) -> bool:
+        """Direct per-row rolling kernels (FactorConfig.rank_invariant) on the GPU."""
+        return bool(getattr(self.cfg, "rank_invariant", False)) and self.device.type == "cuda"
+
     def compute(self, factors: list[str]) -> dict:
         """Run factor groups; returns ordered {column: flat tensor}."""
         out = {}
         self.timings = {}
+        direct = self._direct()
         for name in factors:
             meth = self.METHODS.get(name.upper())
             if meth is None:
                 print(f"Warning: Factor '{name}' not found.")
                 continue
             t0 = time.perf_counter()
-            res = getattr(self, meth)()
+            with RL.direct_kernels(direct):
+                res = getattr(self, meth)()
             if self.device.type == "cuda":
                 torch.cuda.synchronize(self.device)
             self.timings[name.upper()] = (time.perf_counter() - t0) * 1e3

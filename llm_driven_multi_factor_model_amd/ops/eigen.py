@@ -96,7 +96,8 @@ WIDE_LAYOUTS = {"row": 0, "pair": 1}
 def set_wide_kernel_layout(name: str) -> None:
     if name not in WIDE_LAYOUTS:
         raise ValueError(f"wide kernel layout must be one of {sorted(WIDE_LAYOUTS)}, got {name!r}")
-    _native.lib().mfa_eigen_wide_set_variant(WIDE_LAYOUTS[name])
+    if _native.lib().mfa_eigen_wide_set_variant(WIDE_LAYOUTS[name]) != 0:
+        raise ValueError(f"wide kernel layout {name!r} is an A/B variant (MFA_AB build only)")
 
 
 @contextlib.contextmanager
@@ -109,16 +110,23 @@ def using_wide_bias_solver(name: str):
     finally:
         _wide_solver = old
 
-# Per-(date, sim) solver of the bias statistic (csrc/eigen.hip): "jacobi" = pair-block
-# tournament Jacobi carrying M = V^T D0 V; "tridiag" = Householder tridiagonalisation,
-# count-guided Laguerre eigenvalues (division-free Sturm recurrence), twisted-factorisation
-# eigenvectors, back-transform, lean register / LDS layout (mode 5, the default);
-# "tridiag_v1" / "tridiag_lean" = the round-2 kernel (mode 3) / lean layout with the pivot-form
-# Sturm recurrence (mode 4), kept for A/B; "tridiag_dense" = mode 5's arithmetic with three
-# problems on the 126 lanes of a 2-wave workgroup (mode 11, K <= 42; wider K falls back to the
-# one-problem-per-wave kernel).
+# Per-(date, sim) solver of the bias statistic (csrc/eigen.hip): "tridiag" (mode 5, the default)
+# = Householder tridiagonalisation, count-guided Laguerre eigenvalues (division-free Sturm
+# recurrence), twisted-factorisation eigenvectors, back-transform, lean register / LDS layout;
+# "jacobi" = pair-block tournament Jacobi carrying M = V^T D0 V.  A/B builds only (``_build
+# --ab``, slower in their measurements): "tridiag_v1" / "tridiag_lean" = the round-2 kernel
+# (mode 3) / lean layout with the pivot-form Sturm recurrence (mode 4); "tridiag_dense" = mode
+# 5's arithmetic with three problems on the 126 lanes of a 2-wave workgroup (mode 11, K <= 42).
 BIAS_SOLVERS = {"jacobi": 0, "tridiag": 5, "tridiag_v1": 3, "tridiag_lean": 4, "tridiag_dense": 11}
+PRODUCTION_BIAS_SOLVERS = ("jacobi", "tridiag")
 _bias_solver = "tridiag"
+
+
+def available_bias_solvers() -> tuple[str, ...]:
+    """Solvers the loaded kernel library contains (all of BIAS_SOLVERS in an A/B build)."""
+    if torch.cuda.is_available() and _native.ab_build():
+        return tuple(sorted(BIAS_SOLVERS))
+    return PRODUCTION_BIAS_SOLVERS
 
 
 def set_bias_solver(name: str) -> None:
@@ -126,9 +134,12 @@ def set_bias_solver(name: str) -> None:
     global _bias_solver
     if name not in BIAS_SOLVERS:
         raise ValueError(f"bias solver must be one of {sorted(BIAS_SOLVERS)}, got {name!r}")
-    _bias_solver = name
     if torch.cuda.is_available():
-        _native.lib().mfa_eigen_set_bias_mode(BIAS_SOLVERS[name])
+        if _native.lib().mfa_eigen_set_bias_mode(BIAS_SOLVERS[name]) != 0:
+            raise ValueError(f"bias solver {name!r} is an A/B variant: not in this kernel library "
+                             f"(build it with python -m llm_driven_multi_factor_model_amd._build "
+                             f"--ab and set MFA_HIP_LIB)")
+    _bias_solver = name
 
 
 def bias_solver() -> str:

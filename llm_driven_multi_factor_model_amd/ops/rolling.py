@@ -7,6 +7,7 @@ CPU paths are direct float64 transcriptions of the pandas callbacks (used as tes
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import math
 
@@ -25,10 +26,29 @@ _native.register("mfa_returns", [_vp, _vp, _i, _vp, _vp, _vp])
 _native.register("mfa_ttm_flags", [_vp, _vp, _vp, _i, _vp, _vp, _vp])
 _native.register("mfa_ttm_finish", [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp])
 _native.register("mfa_leverage", [_vp, _vp, _vp, _i, _vp, _vp, _vp])
+_native.register("mfa_rolling_set_mode", [_i])
 
 
 def _f(t):
     return t.to(torch.float32).contiguous()
+
+
+@contextlib.contextmanager
+def direct_kernels(on: bool = True):
+    """GPU rolling descriptors from the direct per-row window kernels (``mfa_rolling_set_mode(1)``)
+    inside the block: every output row is a fixed-order sum over its own window, so a row's
+    value does not depend on which other rows share its launch (date shards reproduce the full
+    panel bitwise).  No-op without a GPU or with ``on=False``."""
+    if not (on and torch.cuda.is_available()):
+        yield
+        return
+    lib = _native.lib()
+    if lib.mfa_rolling_set_mode(1) != 0:
+        raise _native.NativeError("mfa_rolling_set_mode(1) failed")
+    try:
+        yield
+    finally:
+        lib.mfa_rolling_set_mode(0)
 
 
 def _i32(t):

@@ -37,6 +37,17 @@ def cuda():
 
 
 @pytest.fixture(scope="session")
+def ab_lib(cuda):
+    """Tests of kernel variants that lost their A/B measurements: they live only in the A/B
+    library (``python -m llm_driven_multi_factor_model_amd._build --ab``, loaded through
+    ``MFA_HIP_LIB=.../_lib/ab/libmfa_hip.so``); the production library skips them."""
+    from llm_driven_multi_factor_model_amd import _native
+    if not _native.ab_build():
+        pytest.skip("A/B kernel variant: not in the production library (build --ab)")
+    return _native.lib()
+
+
+@pytest.fixture(scope="session")
 def ref():
     from tests._refshim import load_reference
     r = load_reference()

@@ -8,8 +8,8 @@ single-process ``run_pipeline`` to 1e-12: factor returns, R^2, specific returns,
 eigen / VRA series, lambda, and the barra_data_csi.csv frame gathered to rank 0.
 
 The GPU variant (``-m gpu``) rehearses the same job with several gloo ranks on one MI355X
-(``MFA_DIST_BACKEND=gloo``); there the rolling kernels restart their running sums at the slice
-start, so descriptors agree to fp32 rounding, not bitwise.
+(``MFA_DIST_BACKEND=gloo``) and requires bitwise equality: the pipeline's descriptors are
+rank-invariant (FactorConfig.rank_invariant, direct per-row window kernels).
 """
 import os
 import socket
@@ -167,13 +167,16 @@ def test_owned_engine_local_grid():
 
 
 @pytest.mark.gpu
-def test_sharded_pipeline_gloo_rehearsal_on_one_gpu(cuda):
-    """3 gloo ranks sharing one MI355X (the RCCL path needs one GPU per rank).  The risk stages
-    see fp32-rounding-level differences in the descriptors (sliding-window kernels restart
-    their sums at the slice start), so the comparison is statistical-grade, not bitwise."""
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_pipeline_gloo_rehearsal_on_one_gpu(cuda, world):
+    """2 / 3 gloo ranks sharing one MI355X (the RCCL path needs one GPU per rank): every output
+    -- factor returns, R^2, specific returns, the Newey-West / eigen / VRA series, lambda and
+    the barra frame -- is BITWISE the single-process run: rank-invariant descriptors (direct
+    window kernels), per-date regression / post-processing, the full-series Newey-West scan,
+    per-date eigen adjustment and the block-partitioned VRA."""
     model, frame, info = _reference("cuda:0")
-    got = _run(3, "cuda")
-    _compare(got, model, frame, info, rtol=5e-3, atol=1e-6, frame_rtol=2e-4, frame_atol=2e-6)
+    got = _run(world, "cuda")
+    _compare(got, model, frame, info, rtol=0, atol=0, frame_rtol=0, frame_atol=0)
 
 
 def _torchrun_cli(nproc, *args, port=None):

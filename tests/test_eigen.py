@@ -105,10 +105,16 @@ def test_hip_mc_cov_statistics(cuda):
     assert torch.equal(Cz, again)  # counter-based RNG: bitwise reproducible
 
 
+def _need_solver(solver):
+    if solver not in eigen.available_bias_solvers():
+        pytest.skip(f"{solver}: A/B variant, not in the production library")
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("solver", sorted(eigen.BIAS_SOLVERS))
 @pytest.mark.parametrize("K", [42, 5, 17, 64])
 def test_hip_eigen_adjust_matches_reference_path(cuda, solver, K):
+    _need_solver(solver)
     D, M = 12, 16
     F = _spd(D, K, seed=9 + K, spread=2.0) * 1e-4
     F[3] = float("nan")
@@ -131,15 +137,15 @@ def test_hip_bias_solvers_agree_on_pipeline_like_inputs(cuda):
     F = ((Q * lam[:, None, :]) @ Q.transpose(1, 2)).to(cuda)
     Cz = eigen.mc_cov(M, K, 2520, seed=3, device=cuda)
     out = {}
-    for solver in eigen.BIAS_SOLVERS:
+    for solver in eigen.available_bias_solvers():
         with eigen.using_bias_solver(solver):
             out[solver] = eigen.eigen_risk_adjust(F, Cz=Cz, return_bias=True)[1].cpu()
-    for solver in eigen.BIAS_SOLVERS:
+    for solver in out:
         torch.testing.assert_close(out[solver], out["jacobi"], rtol=1e-10, atol=0)
 
 
 @pytest.mark.gpu
-def test_bias_mode13_four_accumulators_matches_mode5(cuda):
+def test_bias_mode13_four_accumulators_matches_mode5(cuda, ab_lib):
     """A/B mode 13 (mode 5 with four accumulators per matvec / back-transform dot product): the
     same bias ratios as mode 5 to rounding, on graded draw covariances and with a NaN date."""
     import ctypes as C
@@ -164,7 +170,7 @@ def test_bias_mode13_four_accumulators_matches_mode5(cuda):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("K", [42, 37, 44])
-def test_bias_padded_eigenvectors_bitwise_unpadded(cuda, K):
+def test_bias_padded_eigenvectors_bitwise_unpadded(cuda, ab_lib, K):
     """Mode 5 pads the tridiagonal to 44 rows with decoupled rows, so its eigenvector
     recurrences carry no `i < K` tests; mode 14 is the unpadded kernel.  Same arithmetic on every
     real row and the same twist index: bitwise the same bias ratios; NaN dates stay NaN."""
@@ -190,7 +196,7 @@ def test_bias_padded_eigenvectors_bitwise_unpadded(cuda, K):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("K", [42, 37])
-def test_bias_mode19_newton_laguerre_matches_default(cuda, K):
+def test_bias_mode19_newton_laguerre_matches_default(cuda, ab_lib, K):
     """A/B mode 19 (the default with Newton-refined reciprocal / square root in the Laguerre
     loop): the Sturm-guarded iteration lands within its stopping tolerance of the same roots, so
     the bias ratios agree with the default to rounding; NaN dates stay NaN."""
@@ -214,7 +220,7 @@ def test_bias_mode19_newton_laguerre_matches_default(cuda, K):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("K,D,M", [(42, 7, 5), (30, 5, 4), (42, 1, 1)])
-def test_hip_dense_bias_solver_tail_and_invalid_dates(cuda, K, D, M):
+def test_hip_dense_bias_solver_tail_and_invalid_dates(cuda, ab_lib, K, D, M):
     """Lane-dense solver (3 problems per 2-wave workgroup): a last workgroup with empty slots
     (D * M not a multiple of 3), a NaN date in the middle of a workgroup, K < 42 (inactive
     rows in every slot) -- same bias ratios as the one-problem-per-wave mode-5 kernel."""
@@ -280,6 +286,7 @@ def test_hip_mc_cov_range_is_a_slice(cuda, T, splits):
 @pytest.mark.parametrize("solver", sorted(eigen.BIAS_SOLVERS))
 def test_hip_sharded_eigen_matches_one_shot(cuda, solver):
     """Chunked sum-accumulate + finalize kernels == the one-shot per-sim kernel (same Philox sims)."""
+    _need_solver(solver)
     D, K, M = 10, 42, 20
     F = _spd(D, K, seed=4, spread=2.0) * 1e-4
     F[2] = float("nan")
@@ -290,3 +297,41 @@ def test_hip_sharded_eigen_matches_one_shot(cuda, solver):
                                                  return_bias=True)
     torch.testing.assert_close(v2.cpu(), v1.cpu(), rtol=1e-12, atol=1e-14, equal_nan=True)
     torch.testing.assert_close(F2.cpu(), F1.cpu(), rtol=1e-11, atol=1e-18, equal_nan=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [21, 22, 23])
+def test_bias_warm_date_chains_match_cold_solver(cuda, mode):
+    """Bias modes 21 / 22 / 23: mode 5's kernel walking 8 / 4 / 16 consecutive dates of a sim
+    per wave, each Laguerre iteration started from the previous date's eigenvalue of the same
+    rank.  A slowly drifting spectrum (the Newey-West series), a NaN date inside a chain (the
+    next date restarts cold) and a date count that is not a multiple of the chain: the same
+    bias ratios as the cold-start mode 5 to the Laguerre stopping rounding."""
+    import ctypes as C
+    from llm_driven_multi_factor_model_amd import _native
+    _native.register("mfa_eigen_set_bias_mode", [C.c_int])
+    D, K, M = 45, 42, 12
+    base = _spd(1, K, seed=21, spread=2.5)[0] * 1e-4
+    g = torch.Generator().manual_seed(5)
+    F = torch.empty(D, K, K, dtype=torch.float64)
+    cur = base.clone()
+    for d in range(D):  # a random walk of small symmetric perturbations
+        E = torch.randn(K, K, generator=g, dtype=torch.float64) * 2e-10   # ||E|| ~ 3e-9 << 3e-7
+        cur = cur + 0.5 * (E + E.T)
+        F[d] = cur
+    F[10] = float("nan")
+    Cz = eigen.mc_cov(M, K, 2520, seed=9, device=cuda)
+    lib = _native.lib()
+    out = {}
+    try:
+        for md in (5, mode):
+            assert lib.mfa_eigen_set_bias_mode(md) == 0
+            out[md] = eigen.eigen_risk_adjust(F.to(cuda), Cz=Cz, return_bias=True)[1].cpu()
+            # the sims-chunked accumulate path takes the same chains
+            out[(md, "sh")] = eigen.eigen_risk_adjust_sharded(
+                F.to(cuda), M=M, T_sim=2520, seed=9, chunk=5, return_bias=True)[1].cpu()
+    finally:
+        lib.mfa_eigen_set_bias_mode(5)
+    assert torch.isnan(out[mode][10]).all() and torch.isfinite(out[mode][11:]).all()
+    torch.testing.assert_close(out[mode], out[5], rtol=1e-12, atol=0, equal_nan=True)
+    torch.testing.assert_close(out[(mode, "sh")], out[(5, "sh")], rtol=1e-12, atol=0, equal_nan=True)

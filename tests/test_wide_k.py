@@ -162,6 +162,8 @@ def test_hip_wide_bias_solver_matches_oracle(cuda, layout):
     one-wave mode-5 kernel, K = 100 / 140 equal the CPU fp64 oracle, with one lane per row and
     with two lanes per row (K > 96); an invalid date gives NaN."""
     from llm_driven_multi_factor_model_amd import _native
+    if layout == "row" and not _native.ab_build():
+        pytest.skip("one lane per row at K > 96: A/B layout, not in the production library")
     g = torch.Generator().manual_seed(9)
     eigen.set_wide_kernel_layout(layout)
     try:

@@ -23,10 +23,12 @@ def _run(lib, mode, p, P, **kw):
 
 
 @pytest.fixture
-def lib():
+def lib(ab_lib):
+    """The resident kernel measured slower than the LDS-DMA fused kernel (530 vs 378 us; its
+    stream ablations, profiles/r05/README.md): an A/B-library variant."""
     from llm_driven_multi_factor_model_amd import _native
     _native.register("mfa_xs_set_mode", [C.c_int])
-    return _native.lib()
+    return ab_lib
 
 
 # N: 3000 = every tile resident; 5000 = the headline (4-5 re-read tiles per wave); 12000 = many

@@ -298,7 +298,7 @@ def test_deterministic_kernel_is_bitwise_reproducible(cuda):
 @pytest.mark.parametrize("S,D,N,P,Q,empty", [(2, 9, 1000, 31, 10, 1), (5, 6, 5000, 31, 10, 2),
                                              (8, 4, 2048, 12, 3, 0), (3, 5, 520, 0, 4, 0),
                                              (7, 3, 4000, 28, 16, 1)])
-def test_chunked_path_matches_oracle(cuda, dtype, S, D, N, P, Q, empty):
+def test_chunked_path_matches_oracle(cuda, ab_lib, dtype, S, D, N, P, Q, empty):
     """Strong-scaling path: each date split into S stock chunks (partial moments combined in
     chunk order -> one solve -> chunked residuals -> R^2 combine) == the float64 oracle."""
     from llm_driven_multi_factor_model_amd import _native
@@ -332,7 +332,7 @@ def test_chunked_path_matches_oracle(cuda, dtype, S, D, N, P, Q, empty):
                                                  (7, 3, 4000, 28, 16, 1, 3),
                                                  (4, 300, 5000, 31, 10, 1, 2),
                                                  (16, 61, 5000, 31, 10, 1, 1)])
-def test_team_path_matches_oracle(cuda, dtype, C, D, N, P, Q, empty, lag):
+def test_team_path_matches_oracle(cuda, ab_lib, dtype, C, D, N, P, Q, empty, lag):
     """Pipelined team kernel (persistent grid): C chunks per date, partial moments published
     and solved by the date's last arriver, each chunk's residual pass `lag` tickets later by
     the workgroup that streamed it == the float64 oracle; deterministic mode is bitwise
@@ -365,7 +365,7 @@ def test_team_path_matches_oracle(cuda, dtype, C, D, N, P, Q, empty, lag):
 
 
 @pytest.mark.gpu
-def test_team_path_refines_singular_dates(cuda):
+def test_team_path_refines_singular_dates(cuda, ab_lib):
     """A date with an exactly collinear style pair: the team kernel flags it and the device
     pinv pass (reading the team's partial-moment rows in chunk order) matches numpy's pinv."""
     from llm_driven_multi_factor_model_amd import _native
@@ -393,12 +393,17 @@ def test_path_selection_and_small_shards(cuda):
     assert _native.query("mfa_xs_chunks", 315, 5000) == 1
     assert _native.query("mfa_xs_chunks", 2520, 5000) == 1
     lib = _native.lib()
-    lib.mfa_xs_set_chunks(4)
-    try:
-        assert _native.query("mfa_xs_chunks", 315, 5000) == 4
-        assert _native.query("mfa_xs_chunks", 315, 600) == 2   # >= 256 stocks per chunk
-    finally:
-        lib.mfa_xs_set_chunks(0)
+    if _native.ab_build():
+        lib.mfa_xs_set_chunks(4)
+        try:
+            assert _native.query("mfa_xs_chunks", 315, 5000) == 4
+            assert _native.query("mfa_xs_chunks", 315, 600) == 2   # >= 256 stocks per chunk
+        finally:
+            lib.mfa_xs_set_chunks(0)
+    else:  # production library: the chunked / team paths and the A/B modes are not built in
+        assert lib.mfa_xs_set_chunks(4) != 0 and lib.mfa_xs_set_coop(2) != 0
+        assert lib.mfa_xs_set_mode(30) != 0
+        assert _native.query("mfa_xs_chunks", 315, 5000) == 1
     p = synthetic_panel(40, 5000, 31, 10, seed=2, missing_frac=0.01, dtype=torch.float64)
     ref = X.xs_wls_reference(p.styles, p.cap, p.ret, p.ind, 31)
     g = p.to(cuda)
@@ -408,7 +413,7 @@ def test_path_selection_and_small_shards(cuda):
 
 
 @pytest.mark.gpu
-def test_mfma_moments_ablation_matches_default(cuda):
+def test_mfma_moments_ablation_matches_default(cuda, ab_lib):
     """A/B mode: the MFMA-moments fused kernel (modes 10-12) gives the default's results."""
     from llm_driven_multi_factor_model_amd import _native
     lib = _native.lib()
@@ -429,7 +434,7 @@ def test_mfma_moments_ablation_matches_default(cuda):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
-def test_plain_load_and_lds_dma_moments_are_bitwise_equal(cuda, dtype):
+def test_plain_load_and_lds_dma_moments_are_bitwise_equal(cuda, ab_lib, dtype):
     """The fused kernel's two moment sources -- plain vector loads (default for fp32 panels and
     fp64 shards up to 512 dates) and the LDS-DMA ring (larger fp64 steps) -- feed the same
     per-wave accumulation in the same order: bitwise-identical f, R^2 and specific returns when
@@ -456,3 +461,21 @@ def test_plain_load_and_lds_dma_moments_are_bitwise_equal(cuda, dtype):
     assert torch.equal(a.resid.nan_to_num(7.0), b.resid.nan_to_num(7.0))
     assert torch.equal(c.f, b.f) and torch.equal(c.resid.nan_to_num(7.0), b.resid.nan_to_num(7.0))
     torch.testing.assert_close(c.r2, b.r2, rtol=0, atol=1e-14)
+
+
+@pytest.mark.gpu
+def test_production_moment_sources_agree(cuda):
+    """Production library: fp64 shards up to 512 dates take the plain-load moments (no residual
+    prefetch), longer ones the LDS-DMA ring (with the prefetch).  Both feed the same per-wave
+    accumulation in the same order, so the first 37 dates of a 600-date call equal a 37-date
+    call bitwise in f and the specific returns (R^2 sums its stocks in another order)."""
+    p = synthetic_panel(600, 5000, 31, 10, seed=78, missing_frac=0.02, empty_industries=1,
+                        dtype=torch.float64).to(cuda)
+    big = X.xs_wls(p.styles, p.cap, p.ret, p.ind, 31)
+    q = p.slice_dates(0, 37)
+    small = X.xs_wls(q.styles.contiguous(), q.cap.contiguous(), q.ret.contiguous(),
+                     q.ind.contiguous(), 31)
+    torch.cuda.synchronize()
+    assert torch.equal(small.f, big.f[:37])
+    assert torch.equal(small.resid.nan_to_num(7.0), big.resid[:37].nan_to_num(7.0))
+    torch.testing.assert_close(small.r2, big.r2[:37], rtol=1e-13, atol=1e-15)

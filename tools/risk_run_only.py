@@ -26,19 +26,26 @@ ap.add_argument("--load", default=None)
 ap.add_argument("--dates", type=int, default=2520)
 ap.add_argument("--stocks", type=int, default=5000)
 ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--P", type=int, default=31)
+ap.add_argument("--Q", type=int, default=10)
+ap.add_argument("--bias-mode", type=int, default=None, help="mfa_eigen_set_bias_mode (A/B)")
 a = ap.parse_args()
 if a.make:
-    p = synthetic_panel(a.dates, a.stocks, 31, 10, seed=3, missing_frac=0.01, dtype=torch.float64)
+    p = synthetic_panel(a.dates, a.stocks, a.P, a.Q, seed=3, missing_frac=0.01, dtype=torch.float64)
     torch.save({"styles": p.styles, "cap": p.cap, "ret": p.ret, "ind": p.ind,
                 "dates": torch.from_numpy(p.dates.astype("int64"))}, a.make)
     sys.exit(0)
 d = torch.load(a.load, weights_only=True)
 import numpy as np  # noqa: E402
-p = RiskPanel(styles=d["styles"], cap=d["cap"], ret=d["ret"], ind=d["ind"], P=31,
+P = int(d["ind"].max()) + 1 if d["ind"].numel() else 0
+p = RiskPanel(styles=d["styles"], cap=d["cap"], ret=d["ret"], ind=d["ind"], P=max(P, a.P),
               dates=d["dates"].numpy().astype("datetime64[ns]"),
               stocks=np.array([f"{i:06d}.SZ" for i in range(d["cap"].shape[1])], dtype=object)
               ).to("cuda:0")
 cfg = preset("reference")
+if a.bias_mode is not None:
+    from llm_driven_multi_factor_model_amd import _native
+    assert _native.lib().mfa_eigen_set_bias_mode(a.bias_mode) == 0, "bias mode not in this library"
 for rep in range(a.reps + 1):
     m = RiskModel(p, cfg)
     torch.cuda.synchronize()
@@ -46,5 +53,6 @@ for rep in range(a.reps + 1):
     m.run()
     torch.cuda.synchronize()
     tot = (time.perf_counter() - t0) * 1e3
-print(json.dumps({"total_ms": round(tot, 3),
+print(json.dumps({"K": 1 + p.P + p.Q, "dates": p.D, "bias_mode": a.bias_mode,
+                  "total_ms": round(tot, 3),
                   "stage_ms": {k: round(v, 3) for k, v in m.times.ms.items()}}))
