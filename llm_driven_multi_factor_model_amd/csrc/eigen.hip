@@ -1115,15 +1115,18 @@ template <int KP, bool PF = false, int ABL = 0, int WPE = MFA_TRI2_WPE, bool EIG
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void
 mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* __restrict__ Cz,
                     const int* __restrict__ dvalid, double* __restrict__ vout,
-                    double* __restrict__ Uout, int* __restrict__ flag, int Dn) {
+                    double* __restrict__ Uout, int* __restrict__ flag, int Dn, int doff) {
   static_assert(CH == 1 || (!EIG && ABL == 0), "date chains: bias problems only");
   extern __shared__ __attribute__((aligned(16))) double sm[];
   const int m = blockIdx.x % M, lane = threadIdx.x;
-  const int d_first = (blockIdx.x / M) * CH;
+  // chains start at global dates that are multiples of CH: local date d is global d + date0,
+  // and doff = date0 % CH shifts the first chain (CH == 1: doff = 0)
+  const int d_first = (blockIdx.x / M) * CH - (CH > 1 ? doff : 0);
   double lam_prev = 0.0;  // this lane's eigenvalue of the previous date (CH > 1)
   bool warm = false;
   for (int ci = 0; ci < CH; ++ci) {
   const int d = d_first + ci;
+  if (CH > 1 && d < 0) continue;
   if (CH > 1 && d >= Dn) break;
   lds_order();  // the previous date's LDS reads precede this date's writes
   double* vo = vout + ((size_t)d * M + m) * K;
@@ -2103,12 +2106,13 @@ int g_eigh_mode = 2;  // 0 = pair-block tournament Jacobi, 1 = row/column cyclic
                       // 2 = Householder tridiagonal (mc_bias_tri2_kernel<EIG>) + the pair-block
                       //     Jacobi for the matrices it flags (non-orthogonal eigenvectors)
 int g_fast_rot = 1;   // 1 = rcp/rsq + Newton rotation parameters (jacobi_cs<1>); 0 = IEEE div/sqrt
-int g_bias_mode = 5;  // 0 = packed (A, M) double2; 1 = split fp64 A / fp64 M; 2 = split, fp32 M;
-                      // 3 = Householder tridiagonal + Laguerre / twisted factorisation;
-                      // 4 = its lean-layout kernel; 5 = lean layout + division-free Sturm +
-                      // padded eigenvector phase + skipped no-op Householder steps (default:
-                      // 11.36-11.38 ms; 17.5 for mode 3);
-                      // 14 = mode 5 without the padding (12.0 ms, profiles/r04/r04z/)
+int g_bias_mode = 21;  // 21 (default) = mode 5 walking 8 consecutive dates per wave with warm-
+                       // started Laguerre eigenvalues (eigen stage 12.73-12.79 vs 13.10-13.26 ms,
+                       // profiles/r05/r05b/bias_chain_ab.jsonl); 5 = lean layout + division-free
+                       // Sturm + padded eigenvector phase + skipped no-op Householder steps, one
+                       // date per wave; 0 = packed (A, M) Jacobi.  A/B builds: 1 / 2 = split
+                       // Jacobi, 3 = round-2 tridiagonal, 4 = lean layout, 14 = mode 5 unpadded,
+                       // 22 / 23 = chains of 4 / 16 dates, 41-67 ablations.
 
 #if MFA_AB
 size_t eigh_lds(int K) { return ((size_t)2 * K * (K + 1) + 4 * 64 + 64) * sizeof(double) + 64 * sizeof(int); }
@@ -2117,6 +2121,16 @@ size_t eigh_lds(int K) { return ((size_t)2 * K * (K + 1) + 4 * 64 + 64) * sizeof
 }  // namespace
 
 MFA_API int mfa_ab_build() { return MFA_AB; }
+
+// Global index of date 0 of the next bias launches (date-chained modes 21-23: chains start at
+// global multiples of the chain length, so a date-sharded or resumed run reproduces one
+// process bit for bit).  0 by default.
+int g_bias_date0 = 0;
+MFA_API int mfa_eigen_set_date_origin(int d0) {
+  if (d0 < 0) return (int)hipErrorInvalidValue;
+  g_bias_date0 = d0;
+  return 0;
+}
 
 // Setters return hipErrorInvalidValue for a variant this build does not contain (the A/B
 // variants are compiled only with MFA_AB=1: python -m ..._build --ab).
@@ -2131,7 +2145,7 @@ MFA_API int mfa_eigen_set_fast_rotation(int on) {
   return 0;
 }
 MFA_API int mfa_eigen_set_bias_mode(int mode) {
-  if (!MFA_AB && mode != 0 && mode != 5 && !(mode >= 21 && mode <= 23)) return (int)hipErrorInvalidValue;
+  if (!MFA_AB && mode != 0 && mode != 5 && mode != 21) return (int)hipErrorInvalidValue;
   g_bias_mode = mode;
   return 0;
 }
@@ -2148,10 +2162,10 @@ bool launch_bias_tri_ab(const double* D0, int D, int K, int M, const double* Cz,
         hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, true, 0, MFA_TRI2_WPE, false, 8, 8, 2,  \
                                                 (KP_ == 44), false, (KP_ == 44)>),         \
                            dim3(D * M), dim3(64),                                          \
-                           bias_tri2_lds(K, KP_), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D);            \
+                           bias_tri2_lds(K, KP_), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D, 0);            \
       else                                                                                 \
         hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, false>), dim3(D * M), dim3(64),       \
-                           bias_tri2_lds(K, KP_), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D);            \
+                           bias_tri2_lds(K, KP_), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D, 0);            \
       return true;                                                                         \
     }
     MFA_TRI2(8)
@@ -2183,63 +2197,63 @@ bool launch_bias_tri_ab(const double* D0, int D, int K, int M, const double* Cz,
     if (g_bias_mode == 15)
       hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 4, 2, true, true>),
                          dim3(D * M), dim3(64), bias_tri2_lds(K + 2, 44), s, D0, K, M, Cz, dvalid,
-                         ws, nullptr, nullptr, D);
+                         ws, nullptr, nullptr, D, 0);
     else
       hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 2, 2, true, true>),
                          dim3(D * M), dim3(64), bias_tri2_lds(K + 2, 44), s, D0, K, M, Cz, dvalid,
-                         ws, nullptr, nullptr, D);
+                         ws, nullptr, nullptr, D, 0);
     return true;
   }
   if (g_bias_mode == 20 && K <= 44) {  // A/B: the default + tau-only back-transform skips
     hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, true, false, true, false, true>),
                        dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws,
-                       nullptr, nullptr, D);
+                       nullptr, nullptr, D, 0);
     return true;
   }
   if (g_bias_mode == 19 && K <= 44) {  // A/B: the default + Newton-refined Laguerre arithmetic
     hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, true, false, true, true>),
                        dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws,
-                       nullptr, nullptr, D);
+                       nullptr, nullptr, D, 0);
     return true;
   }
   if (g_bias_mode == 18 && K <= 44) {  // A/B: padded, steps s >= K-2 skip the update
     hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, true, false, true>),
                        dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws,
-                       nullptr, nullptr, D);
+                       nullptr, nullptr, D, 0);
     return true;
   }
   if (g_bias_mode == 14 && K <= 44) {  // A/B: mode 5 with the unpadded eigenvector phase
     hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, false>),
                        dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws,
-                       nullptr, nullptr, D);
+                       nullptr, nullptr, D, 0);
     return true;
   }
   if (g_bias_mode == 13 && K <= 44) {  // A/B: four accumulators per matvec / dot product
     hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 4>), dim3(D * M),
-                       dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D);
+                       dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D, 0);
     return true;
   }
   if (g_bias_mode == 10 && K <= 44) {  // A/B: LDS broadcast reads fenced in batches of 8 x 16 B
     hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 16>), dim3(D * M),
-                       dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D);
+                       dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D, 0);
     return true;
   }
   if ((g_bias_mode == 8 || g_bias_mode == 9) && K <= 44) {  // A/B: Laguerre stop at 1e-9 / 1e-7
     if (g_bias_mode == 8)
       hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 9>), dim3(D * M),
-                         dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D);
+                         dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D, 0);
     else
       hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 7>), dim3(D * M),
-                         dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D);
+                         dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D, 0);
     return true;
   }
   if ((g_bias_mode == 6 || g_bias_mode == 7) && K <= 44) {  // A/B: mode 5 at 4 / 5 waves per SIMD
     if (g_bias_mode == 6)
       hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, 4>), dim3(D * M), dim3(64),
-                         bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D);
+                         bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D, 0);
     else
       hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, 5>), dim3(D * M), dim3(64),
-                         bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D);
+                         bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D, 0);
     return true;
   }
   if (g_bias_mode > 60 && g_bias_mode < 68 && K <= 44) {  // timing-only ablations of mode 5
@@ -2247,7 +2261,7 @@ bool launch_bias_tri_ab(const double* D0, int D, int K, int M, const double* Cz,
 #define MFA_TRI2_ABL(A_)                                                                     \
     if (abl == A_)                                                                         \
       hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, A_>), dim3(D * M), dim3(64),       \
-                         bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D);
+                         bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D, 0);
     MFA_TRI2_ABL(1) MFA_TRI2_ABL(2) MFA_TRI2_ABL(3) MFA_TRI2_ABL(4) MFA_TRI2_ABL(5)
     MFA_TRI2_ABL(6) MFA_TRI2_ABL(7)
 #undef MFA_TRI2_ABL
@@ -2288,13 +2302,14 @@ bool launch_bias_tri_ab(const double* D0, int D, int K, int M, const double* Cz,
 // (K <= 44).  The losing variants live behind MFA_AB (launch_bias_tri_ab).
 bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, const int* dvalid,
                      double* ws, hipStream_t s) {
-  if (g_bias_mode == 5) {
+  const bool chain_mode = g_bias_mode == 21 || (MFA_AB && (g_bias_mode == 22 || g_bias_mode == 23));
+  if (g_bias_mode == 5 || (chain_mode && K > 44)) {  // chains are instantiated at KP = 44
 #define MFA_TRI2(KP_)                                                                        \
     if (K <= KP_) {                                                                        \
       hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, true, 0, MFA_TRI2_WPE, false, 8, 8, 2,    \
                                               (KP_ == 44), false, (KP_ == 44)>),           \
                          dim3(D * M), dim3(64), bias_tri2_lds(K, KP_), s, D0, K, M, Cz,    \
-                         dvalid, ws, nullptr, nullptr, D);                                    \
+                         dvalid, ws, nullptr, nullptr, D, 0);                                    \
       return true;                                                                         \
     }
     MFA_TRI2(8)
@@ -2307,15 +2322,21 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
 #undef MFA_TRI2
     return false;
   }
-  if (g_bias_mode >= 21 && g_bias_mode <= 23 && K <= 44) {  // mode 5 + warm-started date chains
+  if (chain_mode) {  // mode 5 + warm-started date chains (8 dates per wave; 4 / 16: A/B)
 #define MFA_TRI2_CH(CH_)                                                                       \
-    hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, true, false, \
-                                            true, false, false, CH_>),                           \
-                       dim3(((D + CH_ - 1) / CH_) * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, \
-                       Cz, dvalid, ws, nullptr, nullptr, D);
-    if (g_bias_mode == 21) MFA_TRI2_CH(8)
-    else if (g_bias_mode == 22) MFA_TRI2_CH(4)
-    else MFA_TRI2_CH(16)
+    {                                                                                          \
+      const int doff = g_bias_date0 % CH_;                                                     \
+      hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, true, false, \
+                                              true, false, false, CH_>),                         \
+                         dim3(((D + doff + CH_ - 1) / CH_) * M), dim3(64), bias_tri2_lds(K, 44), s, \
+                         D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D, doff);                  \
+    }
+#if MFA_AB
+    if (g_bias_mode == 22) MFA_TRI2_CH(4)
+    else if (g_bias_mode == 23) MFA_TRI2_CH(16)
+    else
+#endif
+    MFA_TRI2_CH(8)
 #undef MFA_TRI2_CH
     return true;
   }
@@ -2368,7 +2389,7 @@ MFA_API int mfa_eigh_batched(const double* A, int B, int K, int max_sweeps, doub
     if (!done && K <= KP_) {                                                                 \
       hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, true, 0, MFA_TRI2_WPE, true>), dim3(B),   \
                          dim3(64), eigh_tri2_lds(K, KP_), s, A, K, 1, (const double*)nullptr, \
-                         (const int*)nullptr, w, U, sweeps, B);                               \
+                         (const int*)nullptr, w, U, sweeps, B, 0);                               \
       done = true;                                                                           \
     }
     MFA_EIGT(8) MFA_EIGT(16) MFA_EIGT(24) MFA_EIGT(32) MFA_EIGT(44) MFA_EIGT(48) MFA_EIGT(64)

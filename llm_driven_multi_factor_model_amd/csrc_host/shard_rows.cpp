@@ -1,0 +1,192 @@
+// Host-side date-shard row selection for the date-sharded end-to-end job (one rank per GPU).
+//
+// Reference: the job of Barra_factor_cal/main.py:42-158 + Barra-master/demo.py:22-42 split over
+// ranks by date.  Round 4 had every rank upload ALL loader rows and build the full device master
+// (0.027 s per rank whatever the world size); here each rank scans the loader columns on the
+// host, keeps only its rows, and uploads those.
+//
+// Input: the loader's columns with rows grouped by stock in ascending code order and, within a
+// stock, strictly ascending trade dates (the stored panel's order; the caller falls back to the
+// full build otherwise).  One pass over the rows (threads over row ranges cut at stock
+// boundaries) finds, per stock segment [a, b):
+//   * its global stock id (the segment's rank = its code's rank among all codes);
+//   * k_lo / k_hi = the first rows with trade_date >= date_lo / >= date_hi (the rank's dates);
+//   * the kept range [start, k_hi): start = k_lo - halo rows (clamped to a), extended further
+//     back (statement rows) until the range holds the `nstmt` most recent distinct end dates
+//     before k_lo, so the trailing-twelve-month cash flow of every owned row is complete;
+//     a stock with no owned row keeps nothing.
+// mfa_date_mask marks every trade date that occurs (a bitmap over YYYYMMDD) in a first pass, so
+// every rank derives the same global date axis (and its block's date bounds) without a
+// collective.
+#include <algorithm>
+#include <atomic>
+#include <cstdint>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+namespace {
+
+inline int cmp16(const uint8_t* a, const uint8_t* b) { return std::memcmp(a, b, 16); }
+
+constexpr int32_t kDateLo = 19000101, kDateHi = 21000101;  // bitmap span of YYYYMMDD ints
+
+}  // namespace
+
+// mask [mfa_date_span()] bytes: 1 where a trade date (YYYYMMDD in [19000101, 21000101)) occurs.
+// Returns 0, or -2 for a date outside that span.
+extern "C" __attribute__((visibility("default"))) int64_t mfa_date_span() { return kDateHi - kDateLo; }
+extern "C" __attribute__((visibility("default"))) int mfa_date_mask(const int32_t* dates, int64_t R,
+                                                                  uint8_t* mask, int nthreads) {
+  const int nt = nthreads > 0 ? nthreads
+                              : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::atomic<int> err{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      const int64_t a = R * t / nt, b = R * (t + 1) / nt;
+      for (int64_t i = a; i < b; ++i) {
+        const int32_t d = dates[i];
+        if (d < kDateLo || d >= kDateHi) { err = -2; return; }
+        mask[d - kDateLo] = 1;  // same-value stores from several threads: benign
+      }
+    });
+  for (auto& x : th) x.join();
+  return err.load();
+}
+
+// codes: [R][16] bytes, dates: [R] int32 YYYYMMDD, end_dates: [R] int32 or null.
+// Outputs: ranges [2 * cap] (start, stop) of the kept rows of each stock that keeps rows, seg_id
+// [cap] global stock id of each range, seg_first [cap] first row of every stock segment (the
+// global stock axis: segment k = stock id k), n_ranges, n_stocks.  Returns 0, or
+//   -1 rows not grouped by stock in ascending code order / dates not ascending in a stock,
+//   -3 output capacity (cap) too small.
+extern "C" __attribute__((visibility("default"))) int mfa_shard_rows(
+    const uint8_t* codes, const int32_t* dates, const int32_t* end_dates, int64_t R,
+    int32_t date_lo, int32_t date_hi, int64_t halo, int nstmt, int64_t* ranges, int32_t* seg_id,
+    int64_t* seg_first, int64_t cap, int64_t* n_ranges, int64_t* n_stocks, int nthreads) {
+  *n_ranges = 0;
+  *n_stocks = 0;
+  if (R <= 0) return 0;
+  const int nt = nthreads > 0 ? nthreads
+                              : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  // cut the rows into nt pieces at stock boundaries
+  std::vector<int64_t> cut(nt + 1, R);
+  cut[0] = 0;
+  for (int t = 1; t < nt; ++t) {
+    int64_t c = std::max(R * t / nt, cut[t - 1]);
+    while (c < R && c > 0 && cmp16(codes + 16 * c, codes + 16 * (c - 1)) == 0) ++c;
+    cut[t] = c;
+  }
+  struct Part {
+    std::vector<int64_t> rg;   // (start, stop) per kept stock
+    std::vector<int64_t> seg;  // local segment index of each kept stock
+    std::vector<int64_t> first;  // first row of every segment
+    int64_t nseg = 0;
+    int err = 0;
+  };
+  std::vector<Part> parts(nt);
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      Part& P = parts[t];
+      int64_t a = cut[t];
+      const int64_t end = cut[t + 1];
+      while (a < end) {
+        int64_t b = a + 1;
+        while (b < end && cmp16(codes + 16 * b, codes + 16 * a) == 0) ++b;
+        // within the stock: strictly ascending dates
+        for (int64_t i = a + 1; i < b; ++i)
+          if (dates[i] <= dates[i - 1]) { P.err = -1; return; }
+        P.first.push_back(a);
+        const int64_t klo = std::lower_bound(dates + a, dates + b, date_lo) - dates;
+        const int64_t khi = std::lower_bound(dates + a, dates + b, date_hi) - dates;
+        if (klo < khi) {
+          int64_t s = std::max(a, klo - halo);
+          if (end_dates && nstmt > 0) {
+            // walk back from klo until nstmt distinct end dates precede it
+            int runs = 0;
+            int64_t j = klo - 1;
+            int32_t prev = 0;
+            bool have = false;
+            for (; j >= a; --j) {
+              if (!have || end_dates[j] != prev) {
+                if (runs == nstmt) break;
+                ++runs;
+                prev = end_dates[j];
+                have = true;
+              }
+            }
+            s = std::min(s, j + 1);
+          }
+          P.rg.push_back(s);
+          P.rg.push_back(khi);
+          P.seg.push_back(P.nseg);
+        }
+        ++P.nseg;
+        a = b;
+      }
+    });
+  for (auto& x : th) x.join();
+  int64_t nseg = 0, nr = 0;
+  for (int t = 0; t < nt; ++t) {
+    if (parts[t].err) return parts[t].err;
+    // ascending codes across the cut (the last stock of piece t-1 < the first of piece t)
+    if (t > 0 && cut[t] < R && cut[t] > 0 && cmp16(codes + 16 * cut[t], codes + 16 * (cut[t] - 1)) <= 0)
+      return -1;
+  }
+  for (int t = 0; t < nt; ++t) {
+    // ascending codes inside the piece: segment starts compared pairwise
+    int64_t a = cut[t];
+    const int64_t end = cut[t + 1];
+    int64_t prev = -1;
+    while (a < end) {
+      if (prev >= 0 && cmp16(codes + 16 * a, codes + 16 * prev) <= 0) return -1;
+      prev = a;
+      int64_t b = a + 1;
+      while (b < end && cmp16(codes + 16 * b, codes + 16 * a) == 0) ++b;
+      a = b;
+    }
+  }
+  for (int t = 0; t < nt; ++t) {
+    const Part& P = parts[t];
+    if (nseg + P.nseg > cap) return -3;
+    for (int64_t k = 0; k < P.nseg; ++k) seg_first[nseg + k] = P.first[k];
+    for (size_t k = 0; k < P.seg.size(); ++k) {
+      if (nr >= cap) return -3;
+      ranges[2 * nr] = P.rg[2 * k];
+      ranges[2 * nr + 1] = P.rg[2 * k + 1];
+      seg_id[nr] = (int32_t)(nseg + P.seg[k]);
+      ++nr;
+    }
+    nseg += P.nseg;
+  }
+  *n_ranges = nr;
+  *n_stocks = nseg;
+  return 0;
+}
+
+// dst = concatenation of src rows [ranges[2k], ranges[2k+1]) (elem bytes per row), threads over
+// ranges; offs [nr + 1] = exclusive prefix of the range lengths (filled by the caller).
+extern "C" __attribute__((visibility("default"))) int mfa_gather_ranges(
+    const uint8_t* src, int64_t elem, const int64_t* ranges, const int64_t* offs, int64_t nr,
+    uint8_t* dst, int nthreads) {
+  if (nr <= 0) return 0;
+  const int nt = nthreads > 0 ? nthreads
+                              : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::atomic<int64_t> next{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t)
+    th.emplace_back([&] {
+      for (;;) {
+        const int64_t k0 = next.fetch_add(64);
+        if (k0 >= nr) return;
+        const int64_t k1 = std::min(nr, k0 + 64);
+        for (int64_t k = k0; k < k1; ++k)
+          std::memcpy(dst + offs[k] * elem, src + ranges[2 * k] * elem,
+                      (size_t)(ranges[2 * k + 1] - ranges[2 * k]) * elem);
+      }
+    });
+  for (auto& x : th) x.join();
+  return 0;
+}

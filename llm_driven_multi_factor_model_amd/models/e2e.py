@@ -153,18 +153,26 @@ class DeviceFactorEngine(FactorEngine):
         if dup:
             raise NeedsPandasPath("duplicate (ts_code, trade_date) rows")
         perm = (lambda x: x[order]) if order is not None else (lambda x: x)
-        self.R, self.D = R, D
         names = np.asarray(prices["ts_code"], dtype="S16")[srep.cpu().numpy()]
+        self._finish_arrays(perm(scodes).to(torch.int32), perm(dcodes).to(torch.int32), names,
+                            dvals.cpu().numpy(), {c: perm(x) for c, x in up.items()},
+                            None if ed is None else perm(ed.long()), index)
+
+    def _finish_arrays(self, stock_id, date_id, names, dv, cols, end_date, index) -> None:
+        """Common tail of the full and the host-sharded builds: the global stock / date axes
+        (``names`` S16 codes in id order, ``dv`` YYYYMMDD ints in id order), the per-row ids and
+        columns already on the device, market returns, stock returns."""
+        dev = self.device
+        self.R, self.D = int(stock_id.numel()), int(len(dv))
         self.N = int(names.size)
         self.stock_names = pd.Index(names.astype("U16").astype(object))
-        dv = dvals.cpu().numpy()
         self.date_ints = dv
         y, m, d = dv // 10000, dv // 100 % 100, dv % 100
         self.date_names = pd.Index(np.char.add(np.char.add(np.char.add(
             np.char.zfill(y.astype(str), 4), "/"), np.char.add(np.char.zfill(m.astype(str), 2), "/")),
             np.char.zfill(d.astype(str), 2)).astype(object))
-        self.stock_id = perm(scodes).to(torch.int32)
-        self.date_id = perm(dcodes).to(torch.int32)
+        self.stock_id = stock_id
+        self.date_id = date_id
         self.seg_lo = RL.seg_lo_from_codes(self.stock_id)
         self.grid_idx = self.date_id.long() * self.N + self.stock_id.long()
         # market_ret: the index close's pct_change (float64), looked up by date, then float32 as
@@ -182,10 +190,81 @@ class DeviceFactorEngine(FactorEngine):
         hit = (pos < len(it)) & (it[np.minimum(pos, len(it) - 1)] == dv)
         mr_date = np.where(hit, mr_idx[np.minimum(pos, len(it) - 1)], np.nan)
         mr = torch.from_numpy(mr_date).to(dev)[self.date_id.long()]
-        self.cols = {c: perm(x).to(torch.float32) for c, x in up.items()}
+        self.cols = {c: x.to(torch.float32) for c, x in cols.items()}
         self.cols["market_ret"] = mr.to(torch.float32)
         self.cols["ret"], self.cols["log_ret"] = RL.returns(self.cols["close"], self.seg_lo)
-        self.end_date = None if ed is None else perm(ed.long())
+        self.end_date = end_date
+
+    # ------------------------------------------------------------ host-side date sharding
+    @classmethod
+    def from_host_shard(cls, prices: dict, index: dict, rank: int, world: int, device=None,
+                        config: FactorConfig | None = None):
+        """The rows of date block ``rank`` of ``world`` -- exactly what ``DeviceFactorEngine(
+        prices, index).date_shard(*shard_range(D, rank, world))`` keeps (its owned dates, each
+        stock's ``halo_rows()`` preceding rows, plus the statement rows of the four most recent
+        distinct end dates before them), selected on the HOST from the loader columns
+        (``csrc_host/shard_rows.cpp``, one threaded pass) so a rank uploads and builds only its
+        share instead of the whole master.  Global stock ids (code ranks) and the global date
+        axis come from the same pass, so every rank numbers stocks and dates identically
+        without a collective.  None when the loader rows are not sorted by (code, date) or the
+        native library is missing (the caller builds the full master and calls
+        :meth:`date_shard`)."""
+        from ..parallel.dist import shard_range
+        from ..utils import native_io
+        cfg = config or FactorConfig()
+        if "ts_code" not in prices or "trade_date" not in prices:
+            return None
+        codes = np.asarray(prices["ts_code"])
+        if codes.dtype != np.dtype("S16"):
+            return None
+        dv = native_io.trade_dates(prices["trade_date"])
+        if dv is None or dv.size == 0:
+            return None
+        D = int(dv.size)
+        lo, hi = shard_range(D, rank, world)
+        big = np.iinfo(np.int32).max
+        date_lo = int(dv[lo]) if lo < D else big
+        date_hi = int(dv[hi]) if hi < D else big
+        halo = FactorEngine.halo_rows(type("C", (), {"cfg": cfg})())
+        ed = prices.get("end_date")
+        got = native_io.shard_rows(codes, prices["trade_date"], ed, date_lo, date_hi, halo)
+        if got is None:
+            return None
+        ranges, seg_id, seg_first = got
+        lens = ranges[:, 1] - ranges[:, 0]
+        offs = np.zeros(lens.size + 1, np.int64)
+        np.cumsum(lens, out=offs[1:])
+        Rk = int(offs[-1])
+        pinned = _pin_default()
+        sel = {}
+        for c, x in prices.items():
+            if c != "ts_code" and c not in cls.NUMERIC and c not in ("trade_date", "end_date"):
+                continue
+            x = np.asarray(x)
+            t = x.dtype.type
+            # upload sources in pinned memory (asynchronous copies), as the reader's buffers
+            buf = native_io._host_buffer(Rk, t, pinned) if t in (np.float32, np.int32) \
+                else np.empty(Rk, dtype=x.dtype)
+            sel[c] = native_io.gather_ranges(x, ranges, offs, buf)
+        eng = object.__new__(cls)
+        eng.cfg = cfg
+        eng.device = torch.device(device) if device is not None else torch.device(
+            os.environ.get("MFA_DEVICE") or ("cuda:0" if torch.cuda.is_available() else "cpu"))
+        t0 = time.perf_counter()
+        eng.master = None
+        dev = eng.device
+        sid = _upload(np.repeat(seg_id, lens).astype(np.int32), dev)
+        td = _upload(sel["trade_date"], dev)
+        up = {c: _upload(sel[c], dev) for c in cls.NUMERIC if c in sel}
+        edv = _upload(sel["end_date"], dev).long() if "end_date" in sel else None
+        did = torch.searchsorted(torch.from_numpy(dv.astype(np.int64)).to(dev), td.long()).to(torch.int32)
+        names = codes[seg_first]
+        eng._finish_arrays(sid, did, names, dv, up, edv, index)
+        eng.prep_s = time.perf_counter() - t0
+        eng.own = (eng.date_id >= lo) & (eng.date_id < hi)
+        eng.lo, eng.hi = lo, hi
+        eng.host_shard_rows = Rk
+        return eng
 
     def _has_statements(self) -> bool:
         return "n_cashflow_act" in self.cols and self.end_date is not None
@@ -509,16 +588,26 @@ def exposures(prices, index, sw_industry: pd.DataFrame, factor_cfg: FactorConfig
     # the pipeline's descriptors are rank-invariant by default: a date-sharded run equals the
     # single-process run bit for bit at any world size (FactorConfig.rank_invariant)
     factor_cfg = factor_cfg or FactorConfig(rank_invariant=True)
-    full = DeviceFactorEngine(prices, index, device=device, config=factor_cfg)
     if ctx is not None and ctx.enabled:
         from ..parallel import dist as pdist
-        sh = full.date_shard(*pdist.shard_range(full.D, ctx.rank, ctx.world))
+        # each rank selects, uploads and builds only its rows (host-side selection from the
+        # sorted loader columns); unsorted input falls back to the full master + date_shard
+        sh = DeviceFactorEngine.from_host_shard(prices, index, ctx.rank, ctx.world, device,
+                                                factor_cfg) \
+            if os.environ.get("MFA_HOST_SHARD", "1") != "0" else None
+        if sh is None:
+            full = DeviceFactorEngine(prices, index, device=device, config=factor_cfg)
+            sh = full.date_shard(*pdist.shard_range(full.D, ctx.rank, ctx.world))
+        else:
+            full = sh  # global date axis (date_names, D) for the writers
+        t["host_shard"] = getattr(sh, "host_shard_rows", None) is not None
         res = sh.compute(factors or FACTORS_TO_RUN)
         own = torch.nonzero(sh.own).flatten()
         res = {k: v[own] for k, v in res.items()}
         eng = sh.owned()
         eng.timings = sh.timings
     else:
+        full = DeviceFactorEngine(prices, index, device=device, config=factor_cfg)
         eng = full
         res = eng.compute(factors or FACTORS_TO_RUN)
     t["descriptors_s"] = time.perf_counter() - t0

@@ -154,14 +154,14 @@ class RiskModel:
                 Fh, vb = eigen.eigen_risk_adjust_sharded(
                     nw_all, M=M, scale_coef=scale_coef, T_sim=T_sim, seed=seed,
                     chunk=self.cfg.eigen_chunk, ctx=self.ctx, psd_tol=self.cfg.psd_tol,
-                    return_bias=True)
+                    return_bias=True, date0=lo_new)
                 a = self.t_lo - lo_new
                 self.eigen_cov = Fh[a:a + self.panel.D].contiguous()
                 self.eigen_bias = vb[a:a + self.panel.D].contiguous()
             else:
                 self.eigen_cov, self.eigen_bias = eigen.eigen_risk_adjust(
                     self.nw_cov, M=M, scale_coef=scale_coef, T_sim=T_sim, seed=seed,
-                    psd_tol=self.cfg.psd_tol, return_bias=True)
+                    psd_tol=self.cfg.psd_tol, return_bias=True, date0=self.t_lo)
         return self.eigen_cov
 
     # --------------------------------------------------------------- stage 4: VRA

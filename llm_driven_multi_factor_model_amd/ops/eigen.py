@@ -51,6 +51,7 @@ _native.register("mfa_eigh_wide_fix", [C.c_void_p, C.c_int, C.c_int, C.c_double,
 _native.register("mfa_mc_cov_wide", [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_void_p,
                                      C.c_void_p, C.c_void_p])
 _native.register("mfa_mc_cov_wide_ws_doubles", [C.c_int, C.c_int, C.c_int])
+_native.register("mfa_eigen_set_date_origin", [C.c_int])
 _native.register("mfa_eigen_finalize_sum", [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                              C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p,
                                              C.c_void_p, C.c_void_p])
@@ -110,15 +111,19 @@ def using_wide_bias_solver(name: str):
     finally:
         _wide_solver = old
 
-# Per-(date, sim) solver of the bias statistic (csrc/eigen.hip): "tridiag" (mode 5, the default)
+# Per-(date, sim) solver of the bias statistic (csrc/eigen.hip): "tridiag" (mode 21, the default)
 # = Householder tridiagonalisation, count-guided Laguerre eigenvalues (division-free Sturm
-# recurrence), twisted-factorisation eigenvectors, back-transform, lean register / LDS layout;
+# recurrence), twisted-factorisation eigenvectors, back-transform, lean register / LDS layout,
+# each wave walking 8 consecutive dates of a sim with the Laguerre iteration of every eigenvalue
+# rank started from the previous date's (chains aligned to global date multiples of 8: pass
+# ``date0``); "tridiag_cold" (mode 5) = the same solver one date per wave, cold starts;
 # "jacobi" = pair-block tournament Jacobi carrying M = V^T D0 V.  A/B builds only (``_build
 # --ab``, slower in their measurements): "tridiag_v1" / "tridiag_lean" = the round-2 kernel
 # (mode 3) / lean layout with the pivot-form Sturm recurrence (mode 4); "tridiag_dense" = mode
 # 5's arithmetic with three problems on the 126 lanes of a 2-wave workgroup (mode 11, K <= 42).
-BIAS_SOLVERS = {"jacobi": 0, "tridiag": 5, "tridiag_v1": 3, "tridiag_lean": 4, "tridiag_dense": 11}
-PRODUCTION_BIAS_SOLVERS = ("jacobi", "tridiag")
+BIAS_SOLVERS = {"jacobi": 0, "tridiag": 21, "tridiag_cold": 5, "tridiag_v1": 3, "tridiag_lean": 4,
+                "tridiag_dense": 11}
+PRODUCTION_BIAS_SOLVERS = ("jacobi", "tridiag", "tridiag_cold")
 _bias_solver = "tridiag"
 
 
@@ -352,9 +357,23 @@ def sim_shard(M: int, rank: int, world: int) -> tuple[int, int]:
     return m0, m0 + base + (1 if rank < rem else 0)
 
 
+@contextlib.contextmanager
+def _date_origin(date0: int, dev):
+    """Global index of date 0 of the bias launches inside the block (date-chained solver)."""
+    if dev.type != "cuda" or not date0:
+        yield
+        return
+    _native.call("mfa_eigen_set_date_origin", int(date0))
+    try:
+        yield
+    finally:
+        _native.call("mfa_eigen_set_date_origin", 0)
+
+
 def eigen_risk_adjust_sharded(F0: torch.Tensor, *, M: int = 10_000, scale_coef: float = 1.4,
                               T_sim: int | None = None, seed: int = 1, chunk: int = 256,
-                              ctx=None, psd_tol: float = 0.0, return_bias: bool = False):
+                              ctx=None, psd_tol: float = 0.0, return_bias: bool = False,
+                              date0: int = 0):
     """Monte-Carlo eigen adjustment with the simulations sharded over ranks and chunked in time.
 
     For large M (the 10k-bootstrap configuration) the per-(date, sim) bias values are never
@@ -363,6 +382,7 @@ def eigen_risk_adjust_sharded(F0: torch.Tensor, *, M: int = 10_000, scale_coef: 
     ``all_reduce(SUM)`` of the [D, K] float64 sums over RCCL (collective C5 of SURVEY.md §2.5)
     then gives every rank the full-M mean.  ``F0`` must hold the SAME dates on every rank.
     Results equal :func:`eigen_risk_adjust` with the same M and seed up to summation order.
+    ``date0``: global index of ``F0[0]`` (the date-chained bias solver aligns its chains to it).
     """
     from ..parallel import dist as pdist
     ctx = ctx or pdist.context()
@@ -387,9 +407,10 @@ def eigen_risk_adjust_sharded(F0: torch.Tensor, *, M: int = 10_000, scale_coef: 
         for a in range(m0, m1, chunk):
             mc = min(chunk, m1 - a)
             Cz = mc_cov(mc, K, max(T_sim, 2), seed, dev, m0=a)
-            _native.call("mfa_eigen_bias_accumulate", _native.ptr(w), _native.ptr(dv), D, K, mc,
-                         _native.ptr(Cz), MAX_SWEEPS, TOL, _native.ptr(ws), _native.ptr(S),
-                         _native.stream(dev))
+            with _date_origin(date0, dev):
+                _native.call("mfa_eigen_bias_accumulate", _native.ptr(w), _native.ptr(dv), D, K,
+                             mc, _native.ptr(Cz), MAX_SWEEPS, TOL, _native.ptr(ws),
+                             _native.ptr(S), _native.stream(dev))
     else:
         for a in range(m0, m1, chunk):
             mc = min(chunk, m1 - a)
@@ -428,13 +449,15 @@ def _bias_sum_reference(w, valid, Cz):
 
 def eigen_risk_adjust(F0: torch.Tensor, *, M: int = 100, scale_coef: float = 1.4,
                       T_sim: int | None = None, seed: int = 1, Cz: torch.Tensor | None = None,
-                      psd_tol: float = 0.0, return_bias: bool = False):
+                      psd_tol: float = 0.0, return_bias: bool = False, date0: int = 0):
     """Eigenfactor risk adjustment of a batch of covariance matrices.
 
     ``F0`` [D, K, K] float64 (NaN matrices allowed -> NaN outputs).  ``T_sim`` defaults to D
     (the reference passes the total number of dates for every date, quirk Q9).  ``Cz`` may be
     supplied to share draw covariances between calls (and between CPU and GPU for testing).
     Returns ``F_hat`` [D, K, K] (and the bias multipliers ``v`` [D, K] if ``return_bias``).
+    ``date0``: global index of ``F0[0]`` (a date shard's offset: the date-chained bias solver
+    aligns its chains to global dates, so shards reproduce one process bit for bit).
     """
     F0 = F0.to(torch.float64).contiguous()
     D, K, _ = F0.shape
@@ -456,9 +479,10 @@ def eigen_risk_adjust(F0: torch.Tensor, *, M: int = 100, scale_coef: float = 1.4
     vb = torch.empty(D, K, dtype=torch.float64, device=dev)
     ws = torch.empty(D * M * K, dtype=torch.float64, device=dev)
     dv = valid.to(torch.int32).contiguous()
-    _native.call("mfa_eigen_adjust", _native.ptr(w.contiguous()), _native.ptr(U.contiguous()),
-                 _native.ptr(dv), D, K, M, _native.ptr(Cz), float(scale_coef), MAX_SWEEPS, TOL,
-                 _native.ptr(ws), _native.ptr(Fh), _native.ptr(vb), _native.stream(dev))
+    with _date_origin(date0, dev):
+        _native.call("mfa_eigen_adjust", _native.ptr(w.contiguous()), _native.ptr(U.contiguous()),
+                     _native.ptr(dv), D, K, M, _native.ptr(Cz), float(scale_coef), MAX_SWEEPS, TOL,
+                     _native.ptr(ws), _native.ptr(Fh), _native.ptr(vb), _native.stream(dev))
     return (Fh, vb) if return_bias else Fh
 
 

@@ -41,6 +41,18 @@ def _load():
         lib.mfa_write_matrix_csv.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(C.c_char_p),
                                              C.c_longlong, C.c_longlong, C.c_void_p, C.c_int]
         lib.mfa_write_matrix_csv.restype = C.c_int
+        lib.mfa_date_span.argtypes = []
+        lib.mfa_date_span.restype = C.c_int64
+        lib.mfa_date_mask.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int]
+        lib.mfa_date_mask.restype = C.c_int
+        lib.mfa_shard_rows.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int32,
+                                       C.c_int32, C.c_int64, C.c_int, C.c_void_p, C.c_void_p,
+                                       C.c_void_p, C.c_int64, C.POINTER(C.c_int64),
+                                       C.POINTER(C.c_int64), C.c_int]
+        lib.mfa_shard_rows.restype = C.c_int
+        lib.mfa_gather_ranges.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int64,
+                                          C.c_void_p, C.c_int]
+        lib.mfa_gather_ranges.restype = C.c_int
         _lib = lib
     return _lib
 
@@ -163,3 +175,67 @@ def write_matrix_csv(path: str, values: np.ndarray, row_labels, col_labels, inde
     if rc != 0:
         raise OSError(f"mfa_write_matrix_csv failed for {path}")
     return True
+
+
+DATE_BASE = 19000101  # csrc_host/shard_rows.cpp: bitmap span [19000101, 21000101)
+
+
+def trade_dates(dates: np.ndarray, nthreads: int = 0) -> np.ndarray | None:
+    """Sorted unique YYYYMMDD trade dates of a loader column (one threaded pass, a bitmap)."""
+    lib = _load_or_none()
+    if lib is None:
+        return None
+    d = np.ascontiguousarray(dates, dtype=np.int32)
+    mask = np.zeros(int(lib.mfa_date_span()), np.uint8)
+    if lib.mfa_date_mask(d.ctypes.data, d.size, mask.ctypes.data, nthreads) != 0:
+        return None
+    return (np.flatnonzero(mask) + DATE_BASE).astype(np.int32)
+
+
+def shard_rows(codes: np.ndarray, dates: np.ndarray, end_dates: np.ndarray | None,
+               date_lo: int, date_hi: int, halo: int, nstmt: int = 4, nthreads: int = 0):
+    """One rank's rows of a (stock, date)-sorted loader: per stock, its rows with trade date in
+    [date_lo, date_hi), the ``halo`` rows before them and the statement rows of the ``nstmt``
+    most recent distinct end dates before them (csrc_host/shard_rows.cpp).
+
+    Returns ``(ranges [n, 2] int64, seg_id [n] int32, seg_first [N] int64)`` -- kept row ranges,
+    the global stock id (code rank) of each range, the first row of every stock -- or None
+    when the native library is missing or the rows are not sorted by (code, date)."""
+    lib = _load_or_none()
+    if lib is None:
+        return None
+    c = np.ascontiguousarray(codes, dtype="S16")
+    d = np.ascontiguousarray(dates, dtype=np.int32)
+    e = None if end_dates is None else np.ascontiguousarray(end_dates, dtype=np.int32)
+    R = d.size
+    cap = 1 << 16
+    while True:
+        ranges = np.empty(2 * cap, np.int64)
+        seg_id = np.empty(cap, np.int32)
+        seg_first = np.empty(cap, np.int64)
+        nr, ns = C.c_int64(0), C.c_int64(0)
+        rc = lib.mfa_shard_rows(c.ctypes.data, d.ctypes.data, None if e is None else e.ctypes.data,
+                                R, int(date_lo), int(date_hi), int(halo), int(nstmt),
+                                ranges.ctypes.data, seg_id.ctypes.data, seg_first.ctypes.data,
+                                cap, C.byref(nr), C.byref(ns), nthreads)
+        if rc == -3 and cap < R + 1:
+            cap = min(4 * cap, R + 1)
+            continue
+        if rc != 0:
+            return None
+        return ranges[:2 * nr.value].reshape(-1, 2), seg_id[:nr.value], seg_first[:ns.value]
+
+
+def gather_ranges(x: np.ndarray, ranges: np.ndarray, offs: np.ndarray, out: np.ndarray,
+                  nthreads: int = 0) -> np.ndarray:
+    """out = concatenation of x[a:b] over ``ranges`` (threaded memcpy); ``offs`` = [0, cumsum of
+    the range lengths]."""
+    lib = _load()
+    xs = np.ascontiguousarray(x)
+    r = np.ascontiguousarray(ranges, dtype=np.int64)
+    o = np.ascontiguousarray(offs, dtype=np.int64)
+    rc = lib.mfa_gather_ranges(xs.ctypes.data, xs.itemsize, r.ctypes.data, o.ctypes.data,
+                               r.shape[0], out.ctypes.data, nthreads)
+    if rc != 0:
+        raise RuntimeError("mfa_gather_ranges failed")
+    return out

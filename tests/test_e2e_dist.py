@@ -38,7 +38,7 @@ def _free_port():
     return p
 
 
-def _data():
+def _data(sorted_rows=False):
     prices, index, sw = synthetic_prices(N=N, T=T, seed=SEED, n_ind=NIND, suspend_frac=0.03)
     # a stock that stops trading mid-sample (no rows in the last block: its t+1 return at the
     # block end must stay NaN) and one that only starts late (no rows in the first block)
@@ -49,6 +49,8 @@ def _data():
     drop |= (c == codes[5]) & (d < q70)
     drop |= (c == codes[7]) & (d > q30) & (d < q75)      # a gap spanning a whole middle block
     prices = prices[~drop]
+    if sorted_rows:  # the stored panel's (ts_code, trade_date) order: host-side shard selection
+        return prices.sort_values(["ts_code", "trade_date"]).reset_index(drop=True), index, sw
     prices = prices.sample(frac=1.0, random_state=2).reset_index(drop=True)
     return prices, index, sw
 
@@ -57,16 +59,17 @@ def _cfg(scan="gather"):
     return preset("reference", eigen_sims=3, time_scan=scan)
 
 
-def _worker(rank, world, port, out_path, device, scan="gather"):
+def _worker(rank, world, port, out_path, device, scan="gather", sorted_rows=False):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     if device != "cpu":
         os.environ["MFA_DIST_BACKEND"] = "gloo"
     from llm_driven_multi_factor_model_amd.parallel import dist as pdist
     ctx = pdist.init_distributed(device=device)
-    prices, index, sw = _data()
+    prices, index, sw = _data(sorted_rows)
     model, info, frame, t = e2e.run_pipeline(prices, index, sw, risk_cfg=_cfg(scan),
                                              want_barra=True, ctx=ctx)
+    assert t["host_shard"] == sorted_rows, t
     out = {k: pdist.gather_to_root(getattr(model, k).contiguous(), ctx) for k in KEYS}
     if ctx.rank == 0:
         out = {k: v.cpu() for k, v in out.items()}
@@ -81,10 +84,11 @@ def _worker(rank, world, port, out_path, device, scan="gather"):
     torch.distributed.destroy_process_group()
 
 
-def _run(world, device, scan="gather"):
+def _run(world, device, scan="gather", sorted_rows=False):
     with tempfile.TemporaryDirectory() as td:
         path = os.path.join(td, "dist.pt")
-        mp.spawn(_worker, args=(world, _free_port(), path, device, scan), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, _free_port(), path, device, scan, sorted_rows),
+                 nprocs=world, join=True)
         got = torch.load(path, weights_only=True)
         got["frame"] = pd.read_csv(path + ".barra.csv")
         got["info"] = pd.read_csv(path + ".info.csv")
@@ -123,6 +127,47 @@ def _compare(got, model, frame, info, rtol, atol, frame_rtol, frame_atol, keys=K
 def test_sharded_pipeline_equals_single_process_cpu(world):
     model, frame, info = _reference("cpu")
     got = _run(world, "cpu")
+    _compare(got, model, frame, info, rtol=1e-12, atol=1e-15, frame_rtol=1e-12, frame_atol=0)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_host_shard_selection_equals_device_date_shard(world):
+    """each rank selects its rows on the HOST (csrc_host/shard_rows.cpp) and
+    builds only those.  Its owned rows carry the same global stock / date ids, columns and
+    descriptors as the full master's date_shard; it holds the halo (+ statement rows) only."""
+    from llm_driven_multi_factor_model_amd.models.factor_engine import FACTORS_TO_RUN
+    from llm_driven_multi_factor_model_amd.parallel.dist import shard_range
+    from llm_driven_multi_factor_model_amd.utils.config import FactorConfig
+    prices, index, _ = _data(sorted_rows=True)
+    p, i = e2e._columns_from_frames(prices, index)
+    cfg = FactorConfig(rank_invariant=True)
+    full = e2e.DeviceFactorEngine(p, i, device="cpu", config=cfg)
+    for rank in range(world):
+        lo, hi = shard_range(full.D, rank, world)
+        ref = full.date_shard(lo, hi)
+        got = e2e.DeviceFactorEngine.from_host_shard(p, i, rank, world, "cpu", cfg)
+        assert got is not None and got.R <= full.R
+        assert got.R >= ref.R                      # + statement rows beyond the halo, at most
+        assert list(got.date_names) == list(full.date_names)
+        assert list(got.stock_names) == list(full.stock_names)
+        ra, rb = ref.compute(FACTORS_TO_RUN), got.compute(FACTORS_TO_RUN)
+        oa, ob = ref.owned(), got.owned()
+        assert torch.equal(oa.stock_id, ob.stock_id) and torch.equal(oa.date_id, ob.date_id)
+        ia, ib = torch.nonzero(ref.own).flatten(), torch.nonzero(got.own).flatten()
+        for k in ra:
+            a, b = ra[k][ia], rb[k][ib]
+            assert torch.equal(a.isnan(), b.isnan()), k
+            assert torch.equal(a.nan_to_num(0), b.nan_to_num(0)), k
+    # unsorted loader rows: no host selection (the caller builds the full master)
+    pu, iu = e2e._columns_from_frames(*_data()[:2])
+    assert e2e.DeviceFactorEngine.from_host_shard(pu, iu, 0, 2, "cpu", cfg) is None
+
+
+def test_sharded_pipeline_host_shard_cpu():
+    """The date-sharded job on (ts_code, trade_date)-sorted loader rows takes the host-side
+    selection on every rank and still equals the single-process run."""
+    model, frame, info = _reference("cpu")
+    got = _run(2, "cpu", sorted_rows=True)
     _compare(got, model, frame, info, rtol=1e-12, atol=1e-15, frame_rtol=1e-12, frame_atol=0)
 
 
@@ -167,15 +212,15 @@ def test_owned_engine_local_grid():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
-def test_sharded_pipeline_gloo_rehearsal_on_one_gpu(cuda, world):
+@pytest.mark.parametrize("world,sorted_rows", [(2, False), (3, True)])
+def test_sharded_pipeline_gloo_rehearsal_on_one_gpu(cuda, world, sorted_rows):
     """2 / 3 gloo ranks sharing one MI355X (the RCCL path needs one GPU per rank): every output
     -- factor returns, R^2, specific returns, the Newey-West / eigen / VRA series, lambda and
     the barra frame -- is BITWISE the single-process run: rank-invariant descriptors (direct
     window kernels), per-date regression / post-processing, the full-series Newey-West scan,
     per-date eigen adjustment and the block-partitioned VRA."""
     model, frame, info = _reference("cuda:0")
-    got = _run(world, "cuda")
+    got = _run(world, "cuda", sorted_rows=sorted_rows)   # sorted rows: host-side selection
     _compare(got, model, frame, info, rtol=0, atol=0, frame_rtol=0, frame_atol=0)
 
 

@@ -1,7 +1,14 @@
-"""Sub-step times of the date-sharded exposures path on ONE process (no collectives):
-full device engine, date_shard(lo, hi), descriptors on the shard, owned rows, post-processing.
+"""Per-rank cost of the date-sharded exposures path on ONE process (collectives stubbed):
+the work rank `rank` of `world` does at N stocks x T days, timed sub-step by sub-step.
 
-    python tools/shard_prof.py [N] [T] [world] [rank]
+  host  : host-side row selection + upload + build of the rank's rows only
+          (DeviceFactorEngine.from_host_shard, the default for sorted loader rows)
+  full  : round 4's path -- every rank uploads and builds the whole master, then date_shard
+
+then descriptors on the slice, owned rows, per-date post-processing.  The loader columns are
+staged like the native reader's (float32 numerics in pinned memory, S16 codes, int32 dates).
+
+    python tools/shard_prof.py [N] [T] [world] [rank]      # default 5000 2520 8 7
 """
 import json
 import os
@@ -14,44 +21,54 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from llm_driven_multi_factor_model_amd.models import e2e  # noqa: E402
 from llm_driven_multi_factor_model_amd.models import factor_engine as FE  # noqa: E402
 from llm_driven_multi_factor_model_amd.parallel.dist import shard_range  # noqa: E402
+from llm_driven_multi_factor_model_amd.utils.config import FactorConfig  # noqa: E402
 
 N = int(sys.argv[1]) if len(sys.argv) > 1 else 5000
 T = int(sys.argv[2]) if len(sys.argv) > 2 else 2520
-world = int(sys.argv[3]) if len(sys.argv) > 3 else 4
-rank = int(sys.argv[4]) if len(sys.argv) > 4 else 1
+world = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+rank = int(sys.argv[4]) if len(sys.argv) > 4 else 7
 dev = torch.device("cuda:0")
 prices, index, sw = FE.synthetic_prices_fast(N=N, T=T, seed=0, n_ind=31, suspend_frac=0.01)
+prices = prices.sort_values(["ts_code", "trade_date"], kind="stable").reset_index(drop=True)
 p, i = e2e._columns_from_frames(prices, index)
+p["trade_date"] = p["trade_date"].astype("int32")
+if "end_date" in p:
+    p["end_date"] = p["end_date"].astype("int32")
 p = e2e.stage_host_columns(p)
+cfg = FactorConfig(rank_invariant=True)
 small = FE.synthetic_prices(N=60, T=300, seed=1, n_ind=31)
 e2e.run_pipeline(*small, device=dev)
-rec = {}
 
 
-def tick(name, t0):
+def tick(rec, name, t0):
     torch.cuda.synchronize()
     rec[name] = round(time.perf_counter() - t0, 4)
-    print(json.dumps({name: rec[name]}), flush=True)
     return time.perf_counter()
 
 
-for rep in range(2):
-    t = time.perf_counter()
-    full = e2e.DeviceFactorEngine(dict(p), dict(i), device=dev)
-    t = tick("full_engine", t)
-    lo, hi = shard_range(full.D, rank, world)
-    full.cashflow_ttm()
-    t = tick("ttm_full", t)
-    sh = full.date_shard(lo, hi)
-    t = tick("date_shard", t)
-    res = sh.compute(FE.FACTORS_TO_RUN)
-    t = tick("compute_shard", t)
-    rec["kernel_ms"] = sh.timings
-    own = torch.nonzero(sh.own).flatten()
-    res = {k: v[own] for k, v in res.items()}
-    eng = sh.owned()
-    t = tick("owned", t)
-    col = FE.postprocess_columns(eng, res, eng.cfg)
-    t = tick("postprocess", t)
-    print(json.dumps({"rep": rep, "rows_full": full.R, "rows_shard": sh.R, "rows_own": eng.R,
-                      **rec}), flush=True)
+for rep in range(3):
+    for path in ("host", "full"):
+        rec = {"path": path, "rep": rep, "N": N, "T": T, "world": world, "rank": rank}
+        t00 = t = time.perf_counter()
+        if path == "host":
+            sh = e2e.DeviceFactorEngine.from_host_shard(dict(p), dict(i), rank, world, dev, cfg)
+            assert sh is not None
+            t = tick(rec, "select_upload_build", t)
+        else:
+            full = e2e.DeviceFactorEngine(dict(p), dict(i), device=dev, config=cfg)
+            t = tick(rec, "full_engine", t)
+            lo, hi = shard_range(full.D, rank, world)
+            full.cashflow_ttm()
+            sh = full.date_shard(lo, hi)
+            t = tick(rec, "date_shard", t)
+        res = sh.compute(FE.FACTORS_TO_RUN)
+        t = tick(rec, "descriptors", t)
+        own = torch.nonzero(sh.own).flatten()
+        res = {k: v[own] for k, v in res.items()}
+        eng = sh.owned()
+        t = tick(rec, "owned", t)
+        col = FE.postprocess_columns(eng, res, eng.cfg)
+        t = tick(rec, "postprocess", t)
+        rec["non_io_s"] = round(time.perf_counter() - t00, 4)
+        rec["rows_slice"], rec["rows_owned"] = sh.R, eng.R
+        print(json.dumps(rec), flush=True)
