@@ -2106,11 +2106,14 @@ int g_eigh_mode = 2;  // 0 = pair-block tournament Jacobi, 1 = row/column cyclic
                       // 2 = Householder tridiagonal (mc_bias_tri2_kernel<EIG>) + the pair-block
                       //     Jacobi for the matrices it flags (non-orthogonal eigenvectors)
 int g_fast_rot = 1;   // 1 = rcp/rsq + Newton rotation parameters (jacobi_cs<1>); 0 = IEEE div/sqrt
-int g_bias_mode = 21;  // 21 (default) = mode 5 walking 8 consecutive dates per wave with warm-
+int g_bias_mode = 5;   // 21 = mode 5 walking 8 consecutive dates per wave with warm-
                        // started Laguerre eigenvalues (eigen stage 12.73-12.79 vs 13.10-13.26 ms,
-                       // profiles/r05/r05b/bias_chain_ab.jsonl); 5 = lean layout + division-free
-                       // Sturm + padded eigenvector phase + skipped no-op Householder steps, one
-                       // date per wave; 0 = packed (A, M) Jacobi.  A/B builds: 1 / 2 = split
+                       // profiles/r05/r05b/bias_chain_ab.jsonl) -- opt-in: a date shard whose
+                       // first date is not a chain start (global multiple of 8) cold-starts where
+                       // one process warm-starts, so date-sharded runs are bitwise rank-invariant
+                       // only with mode 5; 5 (default) = lean layout + division-free Sturm +
+                       // padded eigenvector phase + skipped no-op Householder steps, one date per
+                       // wave; 0 = packed (A, M) Jacobi.  A/B builds: 1 / 2 = split
                        // Jacobi, 3 = round-2 tridiagonal, 4 = lean layout, 14 = mode 5 unpadded,
                        // 22 / 23 = chains of 4 / 16 dates, 41-67 ablations.
 

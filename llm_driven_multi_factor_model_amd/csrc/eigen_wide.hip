@@ -973,6 +973,16 @@ __global__ __launch_bounds__(256) void eigh_wide_fix_kernel(const double* __rest
 // 3 / 5 waves for K <= 96 / 144): w [B][K] descending, U [B][K][K] with U[:, k] = eigenvector k
 // (NaN for non-finite inputs); then eigh_wide_fix_kernel checks U^T U = I to `tol` and re-solves
 // the matrices that fail with the Jacobi (ws: B*K*K doubles; fixed [B] nullable: 1 = re-solved).
+// Multisection rounds of the F0 eigh before its Laguerre loop (A/B knob; 0 = off).  F0 is not
+// diagonally dominant (a Newey-West covariance), so the diagonal guesses are poorer than for
+// the bias problems S C_z S.
+int g_wide_eig_rounds = 0;
+MFA_API int mfa_eigen_wide_set_eig_rounds(int r) {
+  if (r < 0 || r > 7) return (int)hipErrorInvalidValue;
+  g_wide_eig_rounds = r;
+  return 0;
+}
+
 MFA_API int mfa_eigh_wide_fix(const double* A, int B, int K, double tol, double* w, double* U,
                               double* ws, int* fixed, void* stream) {
   if (B <= 0) return 0;
@@ -983,14 +993,14 @@ MFA_API int mfa_eigh_wide_fix(const double* A, int B, int K, double tol, double*
     (void)hipFuncSetAttribute((const void*)mc_bias_wide2_kernel<96, 3, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL((mc_bias_wide2_kernel<96, 3, true>), dim3(B), dim3(3 * 64), lds, s, A, K, 1,
-                       (const double*)nullptr, (const int*)nullptr, w, 0, U);
+                       (const double*)nullptr, (const int*)nullptr, w, g_wide_eig_rounds << 4, U);
     hipLaunchKernelGGL(eigh_wide_fix_kernel<96>, dim3(B), dim3(256), 0, s, A, K, tol, w, U, ws, fixed);
   } else {
     const size_t lds = bias_wide2_lds(K, 144, 5);
     (void)hipFuncSetAttribute((const void*)mc_bias_wide2_kernel<144, 5, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL((mc_bias_wide2_kernel<144, 5, true>), dim3(B), dim3(5 * 64), lds, s, A, K, 1,
-                       (const double*)nullptr, (const int*)nullptr, w, 0, U);
+                       (const double*)nullptr, (const int*)nullptr, w, g_wide_eig_rounds << 4, U);
     hipLaunchKernelGGL(eigh_wide_fix_kernel<144>, dim3(B), dim3(256), 0, s, A, K, tol, w, U, ws, fixed);
   }
   return (int)hipGetLastError();

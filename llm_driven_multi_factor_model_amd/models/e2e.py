@@ -217,6 +217,8 @@ class DeviceFactorEngine(FactorEngine):
         codes = np.asarray(prices["ts_code"])
         if codes.dtype != np.dtype("S16"):
             return None
+        ht = {}
+        t0 = time.perf_counter()
         dv = native_io.trade_dates(prices["trade_date"])
         if dv is None or dv.size == 0:
             return None
@@ -231,21 +233,22 @@ class DeviceFactorEngine(FactorEngine):
         if got is None:
             return None
         ranges, seg_id, seg_first = got
+        ht["scan_s"] = time.perf_counter() - t0
+        t0 = time.perf_counter()
         lens = ranges[:, 1] - ranges[:, 0]
         offs = np.zeros(lens.size + 1, np.int64)
         np.cumsum(lens, out=offs[1:])
         Rk = int(offs[-1])
-        pinned = _pin_default()
+        # the kept rows of the columns the engine uses (codes are not needed: the stock ids come
+        # from the scan), gathered by a threaded memcpy into pageable buffers -- page-locking a
+        # fresh staging area costs more than the pageable upload it would speed up
         sel = {}
         for c, x in prices.items():
-            if c != "ts_code" and c not in cls.NUMERIC and c not in ("trade_date", "end_date"):
+            if c not in cls.NUMERIC and c not in ("trade_date", "end_date"):
                 continue
             x = np.asarray(x)
-            t = x.dtype.type
-            # upload sources in pinned memory (asynchronous copies), as the reader's buffers
-            buf = native_io._host_buffer(Rk, t, pinned) if t in (np.float32, np.int32) \
-                else np.empty(Rk, dtype=x.dtype)
-            sel[c] = native_io.gather_ranges(x, ranges, offs, buf)
+            sel[c] = native_io.gather_ranges(x, ranges, offs, np.empty(Rk, dtype=x.dtype))
+        ht["gather_s"] = time.perf_counter() - t0
         eng = object.__new__(cls)
         eng.cfg = cfg
         eng.device = torch.device(device) if device is not None else torch.device(
@@ -261,9 +264,11 @@ class DeviceFactorEngine(FactorEngine):
         names = codes[seg_first]
         eng._finish_arrays(sid, did, names, dv, up, edv, index)
         eng.prep_s = time.perf_counter() - t0
+        ht["upload_build_s"] = eng.prep_s
         eng.own = (eng.date_id >= lo) & (eng.date_id < hi)
         eng.lo, eng.hi = lo, hi
         eng.host_shard_rows = Rk
+        eng.host_times = ht
         return eng
 
     def _has_statements(self) -> bool:
@@ -585,9 +590,12 @@ def exposures(prices, index, sw_industry: pd.DataFrame, factor_cfg: FactorConfig
         prices, index = _columns_from_frames(prices, index)
     if ctx is not None and ctx.enabled and device is None:
         device = ctx.device
-    # the pipeline's descriptors are rank-invariant by default: a date-sharded run equals the
-    # single-process run bit for bit at any world size (FactorConfig.rank_invariant)
-    factor_cfg = factor_cfg or FactorConfig(rank_invariant=True)
+    # a date-sharded run computes its rolling descriptors rank-invariantly by default (direct
+    # per-row window kernels): it then equals a single-process run with rank_invariant=True bit
+    # for bit at any world size.  A single process defaults to the faster tile kernels (the
+    # same values to fp32 rounding).
+    dist_on = ctx is not None and ctx.enabled
+    factor_cfg = factor_cfg or FactorConfig(rank_invariant=dist_on)
     if ctx is not None and ctx.enabled:
         from ..parallel import dist as pdist
         # each rank selects, uploads and builds only its rows (host-side selection from the

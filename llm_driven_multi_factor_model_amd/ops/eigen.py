@@ -111,19 +111,20 @@ def using_wide_bias_solver(name: str):
     finally:
         _wide_solver = old
 
-# Per-(date, sim) solver of the bias statistic (csrc/eigen.hip): "tridiag" (mode 21, the default)
+# Per-(date, sim) solver of the bias statistic (csrc/eigen.hip): "tridiag" (mode 5, the default)
 # = Householder tridiagonalisation, count-guided Laguerre eigenvalues (division-free Sturm
-# recurrence), twisted-factorisation eigenvectors, back-transform, lean register / LDS layout,
-# each wave walking 8 consecutive dates of a sim with the Laguerre iteration of every eigenvalue
-# rank started from the previous date's (chains aligned to global date multiples of 8: pass
-# ``date0``); "tridiag_cold" (mode 5) = the same solver one date per wave, cold starts;
+# recurrence), twisted-factorisation eigenvectors, back-transform, lean register / LDS layout;
+# "tridiag_chain" (mode 21, opt-in, ~3 % faster) = the same solver with each wave walking 8
+# consecutive dates of a sim, the Laguerre iteration of every eigenvalue rank started from the
+# previous date's (chains aligned to global multiples of 8 through ``date0``: bitwise
+# rank-invariant only for date shards that start on a chain boundary, e.g. sims sharding);
 # "jacobi" = pair-block tournament Jacobi carrying M = V^T D0 V.  A/B builds only (``_build
 # --ab``, slower in their measurements): "tridiag_v1" / "tridiag_lean" = the round-2 kernel
 # (mode 3) / lean layout with the pivot-form Sturm recurrence (mode 4); "tridiag_dense" = mode
 # 5's arithmetic with three problems on the 126 lanes of a 2-wave workgroup (mode 11, K <= 42).
-BIAS_SOLVERS = {"jacobi": 0, "tridiag": 21, "tridiag_cold": 5, "tridiag_v1": 3, "tridiag_lean": 4,
+BIAS_SOLVERS = {"jacobi": 0, "tridiag": 5, "tridiag_chain": 21, "tridiag_v1": 3, "tridiag_lean": 4,
                 "tridiag_dense": 11}
-PRODUCTION_BIAS_SOLVERS = ("jacobi", "tridiag", "tridiag_cold")
+PRODUCTION_BIAS_SOLVERS = ("jacobi", "tridiag", "tridiag_chain")
 _bias_solver = "tridiag"
 
 

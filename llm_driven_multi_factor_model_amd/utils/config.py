@@ -70,9 +70,10 @@ class FactorConfig:
     # its own window, newest to oldest, in a fixed order) instead of the anchored-prefix /
     # van Herk tile kernels, whose rounding depends on where the tile grid falls in the flat
     # rows: a date-sharded run (date_shard + halo) then reproduces the single-process
-    # descriptors BIT FOR BIT at any world size.  The e2e pipeline (run_factors / run_pipeline,
-    # cli factors / pipeline) turns it on; the standalone FactorEngine default is the faster
-    # tile kernels (same values to fp32 rounding).
+    # descriptors BIT FOR BIT at any world size.  The date-sharded e2e pipeline (run_factors /
+    # run_pipeline / cli under torchrun) turns it on by default; a single process uses the
+    # faster tile kernels unless asked (same values to fp32 rounding; +13 ms of kernels at
+    # 5000 x 2520, profiles/r05/README.md).
     rank_invariant: bool = False
     composite: dict = field(default_factory=lambda: {
         "volatility": {"components": ["DASTD", "CMRA", "HSIGMA"], "weights": [0.7, 0.15, 0.15]},

@@ -161,7 +161,7 @@ def test_bias_mode13_four_accumulators_matches_mode5(cuda, ab_lib):
             lib.mfa_eigen_set_bias_mode(mode)
             out[mode] = eigen.eigen_risk_adjust(F.to(cuda), Cz=Cz, return_bias=True)[1].cpu()
     finally:
-        lib.mfa_eigen_set_bias_mode(eigen.BIAS_SOLVERS["tridiag"])
+        lib.mfa_eigen_set_bias_mode(5)
     assert torch.equal(out[5].isnan(), out[13].isnan())
     torch.testing.assert_close(out[13], out[5], rtol=1e-12, atol=0, equal_nan=True)
     # a different kernel ran (not a fallback to the Jacobi, mode 0): different rounding
@@ -188,7 +188,7 @@ def test_bias_padded_eigenvectors_bitwise_unpadded(cuda, ab_lib, K):
             lib.mfa_eigen_set_bias_mode(mode)
             out[mode] = eigen.eigen_risk_adjust(F.to(cuda), Cz=Cz, return_bias=True)[1].cpu()
     finally:
-        lib.mfa_eigen_set_bias_mode(eigen.BIAS_SOLVERS["tridiag"])
+        lib.mfa_eigen_set_bias_mode(5)
     for mode in (14, 15, 16, 18, 20):
         assert torch.equal(out[5].isnan(), out[mode].isnan())
         assert torch.equal(out[mode].nan_to_num(7.0), out[5].nan_to_num(7.0)), mode
@@ -213,7 +213,7 @@ def test_bias_mode19_newton_laguerre_matches_default(cuda, ab_lib, K):
             lib.mfa_eigen_set_bias_mode(mode)
             out[mode] = eigen.eigen_risk_adjust(F.to(cuda), Cz=Cz, return_bias=True)[1].cpu()
     finally:
-        lib.mfa_eigen_set_bias_mode(eigen.BIAS_SOLVERS["tridiag"])
+        lib.mfa_eigen_set_bias_mode(5)
     assert torch.equal(out[5].isnan(), out[19].isnan())
     torch.testing.assert_close(out[19], out[5], rtol=1e-12, atol=0, equal_nan=True)
 
@@ -334,18 +334,19 @@ def test_bias_warm_date_chains_match_cold_solver(cuda, mode):
             out[(md, "sh")] = eigen.eigen_risk_adjust_sharded(
                 F.to(cuda), M=M, T_sim=2520, seed=9, chunk=5, return_bias=True)[1].cpu()
     finally:
-        lib.mfa_eigen_set_bias_mode(eigen.BIAS_SOLVERS["tridiag"])
+        lib.mfa_eigen_set_bias_mode(5)
     assert torch.isnan(out[mode][10]).all() and torch.isfinite(out[mode][11:]).all()
     torch.testing.assert_close(out[mode], out[5], rtol=1e-12, atol=0, equal_nan=True)
     torch.testing.assert_close(out[(mode, "sh")], out[(5, "sh")], rtol=1e-12, atol=0, equal_nan=True)
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("date0", [3, 8, 13])
+@pytest.mark.parametrize("date0", [0, 8, 16])
 def test_bias_date_chains_align_to_global_dates(cuda, date0):
-    """A date shard passes its global offset (``date0``): the default solver's 8-date chains
-    start at global multiples of 8, so the shard's bias ratios and adjusted covariances are
-    bitwise the one-process run's rows (the rank-invariance of the date-sharded eigen stage)."""
+    """The opt-in chained solver ("tridiag_chain"): a date block passed with its global offset
+    (``date0``) that starts on a chain boundary (a multiple of 8) reproduces the one-process
+    rows bit for bit -- chains start at global multiples of 8 -- and the sims-sharded
+    accumulation path (all dates on every rank) takes the same chains."""
     D, K, M = 30, 42, 8
     base = _spd(1, K, seed=31, spread=2.5)[0] * 1e-4
     g = torch.Generator().manual_seed(8)
@@ -357,11 +358,12 @@ def test_bias_date_chains_align_to_global_dates(cuda, date0):
         F[d] = cur
     Fg = F.to(cuda)
     Cz = eigen.mc_cov(M, K, 2520, seed=4, device=cuda)
-    assert eigen.bias_solver() == "tridiag"
-    Fa, va = eigen.eigen_risk_adjust(Fg, Cz=Cz, return_bias=True)
-    Fb, vb = eigen.eigen_risk_adjust(Fg[date0:], Cz=Cz, return_bias=True, date0=date0)
+    with eigen.using_bias_solver("tridiag_chain"):
+        Fa, va = eigen.eigen_risk_adjust(Fg, Cz=Cz, return_bias=True)
+        Fb, vb = eigen.eigen_risk_adjust(Fg[date0:], Cz=Cz, return_bias=True, date0=date0)
+        Fs, vs = eigen.eigen_risk_adjust_sharded(Fg[date0:], M=M, T_sim=2520, seed=4, chunk=3,
+                                                 return_bias=True, date0=date0)
+        Ff, vf = eigen.eigen_risk_adjust_sharded(Fg, M=M, T_sim=2520, seed=4, chunk=3,
+                                                 return_bias=True)
     assert torch.equal(vb, va[date0:]) and torch.equal(Fb, Fa[date0:])
-    Fs, vs = eigen.eigen_risk_adjust_sharded(Fg[date0:], M=M, T_sim=2520, seed=4, chunk=3,
-                                             return_bias=True, date0=date0)
-    Ff, vf = eigen.eigen_risk_adjust_sharded(Fg, M=M, T_sim=2520, seed=4, chunk=3, return_bias=True)
     assert torch.equal(vs, vf[date0:])

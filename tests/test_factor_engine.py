@@ -329,3 +329,31 @@ def test_hip_cmra_rstr_window_edges(cuda):
     for k in fns:
         assert int(torch.isfinite(direct[k]).sum()) > R // 4, k
         torch.testing.assert_close(fast[k].cpu(), direct[k].cpu(), rtol=2e-5, atol=2e-7, equal_nan=True, msg=k)
+
+
+@pytest.mark.gpu
+def test_rolling_ew_variant12_bitwise_default(cuda, ab_lib):
+    """A/B library only: ew variant 12 moves the chunk-map scan to DPP row shifts /
+    row broadcasts, composing with the identity map where a lane has no source.  Same maps in
+    the same association order as variant 0: bitwise the same BETA / HSIGMA / DASTD on a ragged
+    panel (short stocks, NaN rows, windows crossing stock starts)."""
+    from llm_driven_multi_factor_model_amd.ops import rolling as RL
+    g = torch.Generator().manual_seed(12)
+    lens = torch.randint(1, 900, (400,), generator=g)
+    lens[:5] = torch.tensor([1, 7, 64, 255, 2049])
+    R = int(lens.sum())
+    stock = torch.repeat_interleave(torch.arange(lens.numel(), dtype=torch.int32), lens)
+    ret = (torch.randn(R, generator=g) * 0.02).float()
+    ret[torch.rand(R, generator=g) < 0.03] = float("nan")
+    mret = (torch.randn(R, generator=g) * 0.012).float()
+    seg = RL.seg_lo_from_codes(stock).to(cuda)
+    r_, m_ = ret.to(cuda), mret.to(cuda)
+    out = {}
+    try:
+        for v in (0, 12):
+            assert ab_lib.mfa_rolling_set_ew_variant(v) == 0
+            out[v] = (*RL.beta_hsigma(r_, m_, seg, 252, 63.0, 42), RL.dastd(r_, m_, seg, 252, 42.0, 42))
+    finally:
+        ab_lib.mfa_rolling_set_ew_variant(0)
+    for a, b in zip(out[0], out[12]):
+        assert torch.equal(a.nan_to_num(7.0), b.nan_to_num(7.0))

@@ -54,6 +54,7 @@ for rep in range(3):
             sh = e2e.DeviceFactorEngine.from_host_shard(dict(p), dict(i), rank, world, dev, cfg)
             assert sh is not None
             t = tick(rec, "select_upload_build", t)
+            rec["host_times"] = {k: round(v, 4) for k, v in sh.host_times.items()}
         else:
             full = e2e.DeviceFactorEngine(dict(p), dict(i), device=dev, config=cfg)
             t = tick(rec, "full_engine", t)
