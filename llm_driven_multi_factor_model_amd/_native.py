@@ -34,6 +34,7 @@ _SIGS: dict[str, list] = {
     "mfa_xs_set_mode": [_i],
     "mfa_xs_set_coop": [_i],
     "mfa_ab_build": [],
+    "mfa_gather_host_ranges": [_vp, _vp, _vp, _i, _vp, _vp, C.c_int64, _vp],
     "mfa_xs_set_pipe": [_i, _i],
     "mfa_xs_coop_chunks": [_i, _i],
     "mfa_xs_det_supported": [_i, _i],

@@ -28,6 +28,15 @@
 namespace {
 
 inline int cmp16(const uint8_t* a, const uint8_t* b) { return std::memcmp(a, b, 16); }
+// equality of two 16-byte codes as two 8-byte words (the per-row test of the scans)
+inline bool eq16(const uint8_t* a, const uint8_t* b) {
+  uint64_t a0, a1, b0, b1;
+  std::memcpy(&a0, a, 8);
+  std::memcpy(&a1, a + 8, 8);
+  std::memcpy(&b0, b, 8);
+  std::memcpy(&b1, b + 8, 8);
+  return ((a0 ^ b0) | (a1 ^ b1)) == 0;
+}
 
 constexpr int32_t kDateLo = 19000101, kDateHi = 21000101;  // bitmap span of YYYYMMDD ints
 
@@ -48,7 +57,9 @@ extern "C" __attribute__((visibility("default"))) int mfa_date_mask(const int32_
       for (int64_t i = a; i < b; ++i) {
         const int32_t d = dates[i];
         if (d < kDateLo || d >= kDateHi) { err = -2; return; }
-        mask[d - kDateLo] = 1;  // same-value stores from several threads: benign
+        // test before storing: after a date's first sighting its line stays shared between the
+        // threads' caches instead of bouncing on every row
+        if (!mask[d - kDateLo]) mask[d - kDateLo] = 1;
       }
     });
   for (auto& x : th) x.join();
@@ -75,7 +86,7 @@ extern "C" __attribute__((visibility("default"))) int mfa_shard_rows(
   cut[0] = 0;
   for (int t = 1; t < nt; ++t) {
     int64_t c = std::max(R * t / nt, cut[t - 1]);
-    while (c < R && c > 0 && cmp16(codes + 16 * c, codes + 16 * (c - 1)) == 0) ++c;
+    while (c < R && c > 0 && eq16(codes + 16 * c, codes + 16 * (c - 1))) ++c;
     cut[t] = c;
   }
   struct Part {
@@ -84,6 +95,7 @@ extern "C" __attribute__((visibility("default"))) int mfa_shard_rows(
     std::vector<int64_t> first;  // first row of every segment
     int64_t nseg = 0;
     int err = 0;
+    bool asc = true;  // segment codes strictly ascending within the piece
   };
   std::vector<Part> parts(nt);
   std::vector<std::thread> th;
@@ -94,10 +106,11 @@ extern "C" __attribute__((visibility("default"))) int mfa_shard_rows(
       const int64_t end = cut[t + 1];
       while (a < end) {
         int64_t b = a + 1;
-        while (b < end && cmp16(codes + 16 * b, codes + 16 * a) == 0) ++b;
+        while (b < end && eq16(codes + 16 * b, codes + 16 * a)) ++b;
         // within the stock: strictly ascending dates
         for (int64_t i = a + 1; i < b; ++i)
           if (dates[i] <= dates[i - 1]) { P.err = -1; return; }
+        if (!P.first.empty() && cmp16(codes + 16 * a, codes + 16 * P.first.back()) <= 0) P.asc = false;
         P.first.push_back(a);
         const int64_t klo = std::lower_bound(dates + a, dates + b, date_lo) - dates;
         const int64_t khi = std::lower_bound(dates + a, dates + b, date_hi) - dates;
@@ -129,24 +142,18 @@ extern "C" __attribute__((visibility("default"))) int mfa_shard_rows(
     });
   for (auto& x : th) x.join();
   int64_t nseg = 0, nr = 0;
+  // ascending codes: consecutive segment starts within each piece (threads) and across the
+  // piece boundaries (here) -- O(segments), not another pass over the rows
   for (int t = 0; t < nt; ++t) {
     if (parts[t].err) return parts[t].err;
-    // ascending codes across the cut (the last stock of piece t-1 < the first of piece t)
-    if (t > 0 && cut[t] < R && cut[t] > 0 && cmp16(codes + 16 * cut[t], codes + 16 * (cut[t] - 1)) <= 0)
-      return -1;
+    if (!parts[t].asc) return -1;
   }
+  int64_t last = -1;
   for (int t = 0; t < nt; ++t) {
-    // ascending codes inside the piece: segment starts compared pairwise
-    int64_t a = cut[t];
-    const int64_t end = cut[t + 1];
-    int64_t prev = -1;
-    while (a < end) {
-      if (prev >= 0 && cmp16(codes + 16 * a, codes + 16 * prev) <= 0) return -1;
-      prev = a;
-      int64_t b = a + 1;
-      while (b < end && cmp16(codes + 16 * b, codes + 16 * a) == 0) ++b;
-      a = b;
-    }
+    const Part& P = parts[t];
+    if (P.first.empty()) continue;
+    if (last >= 0 && cmp16(codes + 16 * P.first.front(), codes + 16 * last) <= 0) return -1;
+    last = P.first.back();
   }
   for (int t = 0; t < nt; ++t) {
     const Part& P = parts[t];

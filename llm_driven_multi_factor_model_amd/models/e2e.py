@@ -99,6 +99,35 @@ def _ymd_to_datetime64(v: np.ndarray) -> np.ndarray:
         dtype="datetime64[ns]")
 
 
+def _device_gather(srcs, ranges, offs, Rk, dev):
+    """Row ranges of pinned host columns straight into device tensors (mfa_gather_host_ranges);
+    None when not on a GPU, a column is not in pinned memory or has an unsupported width."""
+    if dev.type != "cuda" or not srcs:
+        return None
+    try:
+        pinned = all(torch.from_numpy(np.ascontiguousarray(x)).is_pinned() for x in srcs)
+    except (TypeError, RuntimeError):
+        return None
+    if not pinned or any(x.dtype.itemsize not in (4, 8) or not x.flags.c_contiguous for x in srcs):
+        return None
+    from .. import _native
+    import ctypes as C
+    n = len(srcs)
+    outs = [torch.empty(Rk, dtype=_TORCH_OF_NP[x.dtype.type], device=dev) for x in srcs]
+    rg = torch.from_numpy(np.ascontiguousarray(ranges, dtype=np.int64)).to(dev)
+    of = torch.from_numpy(np.ascontiguousarray(offs[:-1], dtype=np.int64)).to(dev)
+    src_p = (C.c_void_p * n)(*[x.ctypes.data for x in srcs])
+    dst_p = (C.c_void_p * n)(*[o.data_ptr() for o in outs])
+    el = (C.c_int * n)(*[x.dtype.itemsize for x in srcs])
+    rc = _native.lib().mfa_gather_host_ranges(src_p, dst_p, el, n, _native.ptr(rg), _native.ptr(of),
+                                              int(rg.shape[0]), _native.stream(dev))
+    return outs if rc == 0 else None
+
+
+_TORCH_OF_NP = {np.float32: torch.float32, np.float64: torch.float64, np.int32: torch.int32,
+                np.int64: torch.int64}
+
+
 class DeviceFactorEngine(FactorEngine):
     """:class:`FactorEngine` whose master panel is built on the device from columnar arrays.
 
@@ -239,27 +268,32 @@ class DeviceFactorEngine(FactorEngine):
         offs = np.zeros(lens.size + 1, np.int64)
         np.cumsum(lens, out=offs[1:])
         Rk = int(offs[-1])
-        # the kept rows of the columns the engine uses (codes are not needed: the stock ids come
-        # from the scan), gathered by a threaded memcpy into pageable buffers -- page-locking a
-        # fresh staging area costs more than the pageable upload it would speed up
-        sel = {}
-        for c, x in prices.items():
-            if c not in cls.NUMERIC and c not in ("trade_date", "end_date"):
-                continue
-            x = np.asarray(x)
-            sel[c] = native_io.gather_ranges(x, ranges, offs, np.empty(Rk, dtype=x.dtype))
-        ht["gather_s"] = time.perf_counter() - t0
         eng = object.__new__(cls)
         eng.cfg = cfg
         eng.device = torch.device(device) if device is not None else torch.device(
             os.environ.get("MFA_DEVICE") or ("cuda:0" if torch.cuda.is_available() else "cpu"))
+        dev = eng.device
+        # the kept rows of the columns the engine uses (codes are not needed: the stock ids come
+        # from the scan).  Pinned reader buffers on a GPU: the device reads the ranges straight
+        # out of host memory (csrc/gather.hip, one pass over PCIe, only this rank's bytes);
+        # otherwise a threaded host memcpy into pageable buffers and their upload.
+        names_c = [c for c in prices if c in cls.NUMERIC or c in ("trade_date", "end_date")]
+        srcs = [np.asarray(prices[c]) for c in names_c]
+        dsel = _device_gather(srcs, ranges, offs, Rk, dev)
+        if dsel is not None:
+            sel = dict(zip(names_c, dsel))
+            ht["gather"] = "device"
+        else:
+            sel = {c: _upload(native_io.gather_ranges(x, ranges, offs, np.empty(Rk, dtype=x.dtype)), dev)
+                   for c, x in zip(names_c, srcs)}
+            ht["gather"] = "host"
+        ht["gather_s"] = time.perf_counter() - t0
         t0 = time.perf_counter()
         eng.master = None
-        dev = eng.device
         sid = _upload(np.repeat(seg_id, lens).astype(np.int32), dev)
-        td = _upload(sel["trade_date"], dev)
-        up = {c: _upload(sel[c], dev) for c in cls.NUMERIC if c in sel}
-        edv = _upload(sel["end_date"], dev).long() if "end_date" in sel else None
+        td = sel["trade_date"]
+        up = {c: sel[c] for c in cls.NUMERIC if c in sel}
+        edv = sel["end_date"].long() if "end_date" in sel else None
         did = torch.searchsorted(torch.from_numpy(dv.astype(np.int64)).to(dev), td.long()).to(torch.int32)
         names = codes[seg_first]
         eng._finish_arrays(sid, did, names, dv, up, edv, index)

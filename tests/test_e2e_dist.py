@@ -273,3 +273,24 @@ def test_cli_pipeline_and_factors_under_torchrun(tmp_path):
                                                equal_nan=True, err_msg=f"{one} {two} {f} {c}")
                 else:
                     assert (a[c].astype(str).values == b[c].astype(str).values).all(), c
+
+
+@pytest.mark.gpu
+def test_host_shard_device_gather_equals_host_gather(cuda):
+    """Pinned reader buffers: the GPU reads each stock's kept row range straight out of host
+    memory (csrc/gather.hip, zero-copy over PCIe); pageable buffers take the host memcpy +
+    upload.  Same rows, ids and columns either way."""
+    from llm_driven_multi_factor_model_amd.utils.config import FactorConfig
+    prices, index, _ = _data(sorted_rows=True)
+    p, i = e2e._columns_from_frames(prices, index)
+    cfg = FactorConfig(rank_invariant=True)
+    pinned = e2e.stage_host_columns(dict(p), pinned=True)
+    pageable = e2e.stage_host_columns(dict(p), pinned=False)
+    for rank in range(3):
+        a = e2e.DeviceFactorEngine.from_host_shard(pinned, i, rank, 3, cuda, cfg)
+        b = e2e.DeviceFactorEngine.from_host_shard(pageable, i, rank, 3, cuda, cfg)
+        assert a.host_times["gather"] == "device" and b.host_times["gather"] == "host"
+        assert a.R == b.R and torch.equal(a.stock_id, b.stock_id) and torch.equal(a.date_id, b.date_id)
+        for k in b.cols:
+            assert torch.equal(a.cols[k].nan_to_num(7.0), b.cols[k].nan_to_num(7.0)), k
+        assert torch.equal(a.end_date, b.end_date)

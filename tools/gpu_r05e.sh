@@ -1,0 +1,10 @@
+#!/bin/bash
+# round 5: zero-copy device gather of the host-sharded rows -- its GPU test, the e2e dist GPU
+# tests, and the slowest-rank stand-in (rank 7 of 8 at 5000 x 2520)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; O=gpurun_out/r05e; mkdir -p $O; export TMPDIR=/tmp
+T="timeout -k 10"
+$T 600 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests/test_e2e_dist.py > $O/pytest.log 2>&1
+prc=$?; tail -2 $O/pytest.log; grep -E "^FAILED|^ERROR" $O/pytest.log | head -8
+[ $prc -le 1 ] && $T 300 python tools/shard_prof.py 5000 2520 8 7 > $O/shard_prof_rank7of8.jsonl 2>&1
+rc=$?; [ $prc -le 1 ] || rc=$prc; grep -h non_io $O/shard_prof_rank7of8.jsonl | tail -2 | cut -c1-500; exit $rc
