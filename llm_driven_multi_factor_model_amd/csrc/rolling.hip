@@ -139,34 +139,34 @@ __global__ __launch_bounds__(256) void cmra_kernel(const float* __restrict__ lr,
   if (r >= R) return;
   const int s0 = seg_lo[r];
   float o = qnanf();
+  // Z = exp(c) - 1 is non-decreasing in the running sum c, so max Z = exp(max c) - 1 (and min
+  // likewise): two exp / log pairs per row instead of one exp per tap
   if (!partial) {
     if (r - W + 1 >= s0) {
-      double c = 0.0, zmax = -1e300, zmin = 1e300;
+      double c = 0.0, cmax = -INFINITY, cmin = INFINITY;
       bool ok = true;
       for (int j = r - W + 1; j <= r; ++j) {
         const float v = lr[j];
         if (!fin(v)) { ok = false; break; }
         c += (double)v;
-        const double z = exp(c) - 1.0;
-        zmax = fmax(zmax, z);
-        zmin = fmin(zmin, z);
+        cmax = fmax(cmax, c);
+        cmin = fmin(cmin, c);
       }
-      if (ok) o = (float)(log(1.0 + zmax) - log(1.0 + zmin));
+      if (ok) o = (float)(log(1.0 + (exp(cmax) - 1.0)) - log(1.0 + (exp(cmin) - 1.0)));
     }
   } else {  // factor.py: partial windows, pandas cumsum skips NaN, max/min skip NaN
     const int lo = max(s0, r - W + 1);
-    double c = 0.0, zmax = -1e300, zmin = 1e300;
+    double c = 0.0, cmax = -INFINITY, cmin = INFINITY;
     int n = 0;
     for (int j = lo; j <= r; ++j) {
       const float v = lr[j];
       if (!fin(v)) continue;
       c += (double)v;
-      const double z = exp(c) - 1.0;
-      zmax = fmax(zmax, z);
-      zmin = fmin(zmin, z);
+      cmax = fmax(cmax, c);
+      cmin = fmin(cmin, c);
       ++n;
     }
-    if (n > 0) o = (float)(log(1.0 + zmax) - log(1.0 + zmin));
+    if (n > 0) o = (float)(log(1.0 + (exp(cmax) - 1.0)) - log(1.0 + (exp(cmin) - 1.0)));
   }
   out[r] = o;
 }
@@ -1781,6 +1781,33 @@ MFA_API int mfa_beta_hsigma(const float* y, const float* x, const int* seg_lo, i
   } else
     hipLaunchKernelGGL(beta_hsigma_kernel, MFA_GRID(R), 0, (hipStream_t)s, y, x, seg_lo, R, W, lam,
                        minp, beta, hsig);
+  return (int)hipGetLastError();
+}
+// Rank-invariant BETA/HSIGMA and DASTD (FactorConfig.rank_invariant): the sanitised-row EW kernel
+// at a 512-row tile geometry (256 output rows + a 256-row halo) on a VIRTUAL row layout that the
+// caller builds (ops/rolling.py, _aligned_layout): every stock's rows sit at virtual positions
+// B_s + t - T0_s with B_s a multiple of 256 and t the row's ordinal in the stock's FULL history,
+// so the tiles, the 8-row chunks and the scan tree fall on global multiples of 256 whatever
+// slice of the history a launch holds.  A date shard whose rows reach 512 back from its first
+// owned row then computes every owned row with the same operations in the same order as the
+// full panel: bitwise rank-invariant, at ~2x the tile kernel's rows instead of the direct
+// kernels' W taps per row.  Rv: virtual rows (a multiple of 256); W <= 255 (the first owned row
+// of a tile must see a full window of its own rows in both layouts).
+MFA_API int mfa_beta_hsigma_aligned(const float* y, const float* x, const int* seg_lo, int Rv,
+                                    int W, double lam, int minp, float* beta, float* hsig,
+                                    void* s) {
+  if (Rv <= 0) return 0;
+  if (W < 1 || W > 255 || (Rv % 256) != 0) return (int)hipErrorInvalidValue;
+  launch_ew_san<BetaOp, 8, 512, true>(y, x, seg_lo, Rv, W, 256, lam, minp, beta, hsig,
+                                      (hipStream_t)s);
+  return (int)hipGetLastError();
+}
+MFA_API int mfa_dastd_aligned(const float* ret, const float* mret, const int* seg_lo, int Rv,
+                              int W, double lam, int minp, float* out, void* s) {
+  if (Rv <= 0) return 0;
+  if (W < 1 || W > 255 || (Rv % 256) != 0) return (int)hipErrorInvalidValue;
+  launch_ew_san<DastdOp, 8, 512, true>(ret, mret, seg_lo, Rv, W, 256, lam, minp, out, out,
+                                       (hipStream_t)s);
   return (int)hipGetLastError();
 }
 MFA_API int mfa_rstr(const float* lr, const int* seg_lo, int R, int L, int W, double lam,

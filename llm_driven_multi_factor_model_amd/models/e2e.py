@@ -297,6 +297,12 @@ class DeviceFactorEngine(FactorEngine):
         did = torch.searchsorted(torch.from_numpy(dv.astype(np.int64)).to(dev), td.long()).to(torch.int32)
         names = codes[seg_first]
         eng._finish_arrays(sid, did, names, dv, up, edv, index)
+        # each kept row's ordinal in its stock's full history (the aligned rank-invariant tiles)
+        lt = torch.from_numpy(lens).to(dev)
+        ord0 = torch.from_numpy(ranges[:, 0] - seg_first[seg_id]).to(dev)
+        o0 = torch.from_numpy(offs[:-1]).to(dev)
+        eng._row_ord = (torch.repeat_interleave(ord0 - o0, lt)
+                        + torch.arange(Rk, device=dev)).to(torch.int32)
         eng.prep_s = time.perf_counter() - t0
         ht["upload_build_s"] = eng.prep_s
         eng.own = (eng.date_id >= lo) & (eng.date_id < hi)

@@ -150,10 +150,24 @@ class FactorEngine:
 
     # ---------------------------------------------------------------- date sharding (DP + halo)
     def halo_rows(self) -> int:
-        """Rows of history any descriptor of this config reads before an output row."""
+        """Rows of history any descriptor of this config reads before an output row; with
+        ``rank_invariant`` at least 2 x 256 - 1, so the aligned tile (256-row halo + 256 rows)
+        holding a shard's first owned row lies inside the slice."""
         c = self.cfg
-        return max(c.beta_window, c.rstr_window, c.dastd_window, c.cmra_window,
-                   c.stom[0], c.stoq[0], c.stoa[0])
+        h = max(c.beta_window, c.rstr_window, c.dastd_window, c.cmra_window,
+                c.stom[0], c.stoq[0], c.stoa[0])
+        return max(h, 2 * RL.ALIGN) if getattr(c, "rank_invariant", False) else h
+
+    @property
+    def row_ord(self) -> torch.Tensor:
+        """Each row's ordinal in its stock's FULL history (int32; rows of a shard keep the
+        ordinals of the master they were cut from)."""
+        ro = getattr(self, "_row_ord", None)
+        if ro is None:
+            ro = (torch.arange(self.R, device=self.seg_lo.device, dtype=torch.int32)
+                  - self.seg_lo.to(torch.int32))
+            self._row_ord = ro
+        return ro
 
     def date_shard(self, lo: int, hi: int, halo: int | None = None) -> "FactorEngine":
         """Engine over the rows of dates [lo, hi) plus each stock's ``halo`` preceding rows.
@@ -207,6 +221,7 @@ class FactorEngine:
         sub.seg_lo = RL.seg_lo_from_codes(sub.stock_id)
         sub.grid_idx = sub.date_id.long() * sub.N + sub.stock_id.long()
         sub.cols = {k: v[idx] for k, v in self.cols.items()}
+        sub._row_ord = self.row_ord[idx]
         ttm = getattr(self, "_ttm", None)
         sub._ttm = None if ttm is None else ttm[idx]
         sub.own = None
@@ -236,7 +251,8 @@ class FactorEngine:
     def compute_beta_hsigma(self):
         c = self.cfg
         b, h = RL.beta_hsigma(self.cols["ret"], self.cols["market_ret"], self.seg_lo, c.beta_window,
-                              c.beta_half_life, c.beta_min_periods)
+                              c.beta_half_life, c.beta_min_periods,
+                              row_ord=self.row_ord if self._direct() else None)
         return {"BETA": b, "HSIGMA": h}
 
     def compute_rstr(self):
@@ -247,7 +263,8 @@ class FactorEngine:
     def compute_dastd(self):
         c = self.cfg
         return {"DASTD": RL.dastd(self.cols["ret"], self.cols["market_ret"], self.seg_lo, c.dastd_window,
-                                  c.dastd_half_life, c.dastd_min_periods)}
+                                  c.dastd_half_life, c.dastd_min_periods,
+                                  row_ord=self.row_ord if self._direct() else None)}
 
     def compute_cmra(self):
         c = self.cfg

@@ -27,6 +27,42 @@ _native.register("mfa_ttm_flags", [_vp, _vp, _vp, _i, _vp, _vp, _vp])
 _native.register("mfa_ttm_finish", [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp])
 _native.register("mfa_leverage", [_vp, _vp, _vp, _i, _vp, _vp, _vp])
 _native.register("mfa_rolling_set_mode", [_i])
+_native.register("mfa_beta_hsigma_aligned", [_vp, _vp, _vp, _i, _i, _d, _i, _vp, _vp, _vp])
+_native.register("mfa_dastd_aligned", [_vp, _vp, _vp, _i, _i, _d, _i, _vp, _vp])
+
+ALIGN = 256      # rank-invariant EW kernels: tiles on global multiples of 256 rows
+ALIGN_MAX_W = 255
+
+
+def _aligned_layout(seg_lo: torch.Tensor, row_ord: torch.Tensor):
+    """Virtual row layout of the rank-invariant EW kernels (csrc/rolling.hip,
+    mfa_beta_hsigma_aligned): the rows of each stock at B_s + t - T0_s, t = ``row_ord`` (the
+    row's ordinal in the stock's FULL history), T0_s = t_first rounded down to a multiple of
+    ALIGN, B_s = multiples of ALIGN.  Returns (v [R] int64 virtual position of every row,
+    seg_v [Rv] int32 virtual seg_lo, Rv)."""
+    dev = seg_lo.device
+    R = seg_lo.numel()
+    r = torch.arange(R, device=dev, dtype=torch.int64)
+    sl = seg_lo.long()
+    start = r == sl
+    sidx = torch.cumsum(start.to(torch.int64), 0) - 1
+    starts = torch.nonzero(start).flatten()
+    lens = torch.diff(starts, append=torch.tensor([R], device=dev))
+    t_first = row_ord.long()[starts]
+    T0 = torch.div(t_first, ALIGN, rounding_mode="floor") * ALIGN
+    padded = torch.div(t_first - T0 + lens + ALIGN - 1, ALIGN, rounding_mode="floor") * ALIGN
+    B = torch.cumsum(padded, 0) - padded
+    v = B[sidx] + (row_ord.long() - T0[sidx])
+    Rv = int(padded.sum())
+    seg_v = torch.arange(Rv, device=dev, dtype=torch.int32)   # padding rows: their own starts
+    seg_v[v] = (B + t_first - T0)[sidx].to(torch.int32)
+    return v, seg_v, Rv
+
+
+def _to_virtual(x: torch.Tensor, v: torch.Tensor, Rv: int) -> torch.Tensor:
+    out = torch.full((Rv,), float("nan"), dtype=torch.float32, device=x.device)
+    out[v] = x
+    return out
 
 
 def _f(t):
@@ -99,10 +135,21 @@ def returns(close, seg_lo):
 
 
 # ---------------------------------------------------------------- BETA / HSIGMA
-def beta_hsigma(ret, mret, seg_lo, window=252, half_life=63.0, min_periods=42):
+def beta_hsigma(ret, mret, seg_lo, window=252, half_life=63.0, min_periods=42, row_ord=None):
+    """``row_ord`` (GPU, window <= 255): the rows' ordinals in their stocks' full histories --
+    the rank-invariant aligned-tile kernel on the virtual layout (a date shard reproduces the
+    full panel bit for bit)."""
     ret, mret, seg_lo = _f(ret), _f(mret), _i32(seg_lo)
     R = ret.numel()
     lam = 0.5 ** (1.0 / half_life)
+    if ret.is_cuda and row_ord is not None and window <= ALIGN_MAX_W and R:
+        v, seg_v, Rv = _aligned_layout(seg_lo, row_ord)
+        bv = torch.empty(Rv, dtype=torch.float32, device=ret.device)
+        hv = torch.empty_like(bv)
+        _native.call("mfa_beta_hsigma_aligned", _native.ptr(_to_virtual(ret, v, Rv)),
+                     _native.ptr(_to_virtual(mret, v, Rv)), _native.ptr(seg_v), Rv, window, lam,
+                     min_periods, _native.ptr(bv), _native.ptr(hv), _native.stream(ret.device))
+        return bv[v].contiguous(), hv[v].contiguous()
     if ret.is_cuda:
         b, h = torch.empty_like(ret), torch.empty_like(ret)
         _native.call("mfa_beta_hsigma", _native.ptr(ret), _native.ptr(mret), _native.ptr(seg_lo), R,
@@ -155,10 +202,18 @@ def rstr(log_ret, seg_lo, T=504, L=21, half_life=126.0, min_periods=42):
 
 
 # ---------------------------------------------------------------- DASTD
-def dastd(ret, mret, seg_lo, window=252, half_life=42.0, min_periods=42):
+def dastd(ret, mret, seg_lo, window=252, half_life=42.0, min_periods=42, row_ord=None):
+    """``row_ord``: the rank-invariant aligned-tile kernel (see :func:`beta_hsigma`)."""
     ret, mret, seg_lo = _f(ret), _f(mret), _i32(seg_lo)
     R = ret.numel()
     lam = 0.5 ** (1.0 / half_life)
+    if ret.is_cuda and row_ord is not None and window <= ALIGN_MAX_W and R:
+        v, seg_v, Rv = _aligned_layout(seg_lo, row_ord)
+        ov = torch.empty(Rv, dtype=torch.float32, device=ret.device)
+        _native.call("mfa_dastd_aligned", _native.ptr(_to_virtual(ret, v, Rv)),
+                     _native.ptr(_to_virtual(mret, v, Rv)), _native.ptr(seg_v), Rv, window, lam,
+                     min_periods, _native.ptr(ov), _native.stream(ret.device))
+        return ov[v].contiguous()
     if ret.is_cuda:
         out = torch.empty_like(ret)
         _native.call("mfa_dastd", _native.ptr(ret), _native.ptr(mret), _native.ptr(seg_lo), R, window,

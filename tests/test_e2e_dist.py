@@ -294,3 +294,23 @@ def test_host_shard_device_gather_equals_host_gather(cuda):
         for k in b.cols:
             assert torch.equal(a.cols[k].nan_to_num(7.0), b.cols[k].nan_to_num(7.0)), k
         assert torch.equal(a.end_date, b.end_date)
+
+
+def test_host_shard_row_ordinals():
+    """The host-selected rows carry their ordinals in the full stock histories (the aligned
+    rank-invariant tiles key on them), equal to the full master's for the same rows."""
+    from llm_driven_multi_factor_model_amd.parallel.dist import shard_range
+    from llm_driven_multi_factor_model_amd.utils.config import FactorConfig
+    prices, index, _ = _data(sorted_rows=True)
+    p, i = e2e._columns_from_frames(prices, index)
+    cfg = FactorConfig(rank_invariant=True)
+    full = e2e.DeviceFactorEngine(p, i, device="cpu", config=cfg)
+    for rank in range(3):
+        got = e2e.DeviceFactorEngine.from_host_shard(p, i, rank, 3, "cpu", cfg)
+        lo, hi = shard_range(full.D, rank, 3)
+        ref = full.date_shard(lo, hi)
+        # the owned rows of both carry the full master's ordinals
+        a = got.row_ord[got.own]
+        b = ref.row_ord[ref.own]
+        assert torch.equal(a, b)
+        assert int(got.row_ord.min()) >= 0

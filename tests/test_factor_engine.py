@@ -357,3 +357,45 @@ def test_rolling_ew_variant12_bitwise_default(cuda, ab_lib):
         ab_lib.mfa_rolling_set_ew_variant(0)
     for a, b in zip(out[0], out[12]):
         assert torch.equal(a.nan_to_num(7.0), b.nan_to_num(7.0))
+
+
+@pytest.mark.gpu
+def test_aligned_ew_kernels_rank_invariant(cuda):
+    """rank_invariant BETA/HSIGMA and DASTD (aligned 512-row tiles on the virtual layout keyed by
+    each row's ordinal in its stock's full history): equal to the tile kernels to fp32 rounding,
+    and a slice of every stock that starts 512 rows (or fewer, at the stock start) before its
+    first output row reproduces those outputs BIT FOR BIT."""
+    from llm_driven_multi_factor_model_amd.ops import rolling as RL
+    g = torch.Generator().manual_seed(21)
+    lens = torch.randint(300, 2600, (60,), generator=g)
+    lens[:3] = torch.tensor([1, 40, 700])
+    R = int(lens.sum())
+    stock = torch.repeat_interleave(torch.arange(lens.numel(), dtype=torch.int32), lens)
+    ret = (torch.randn(R, generator=g) * 0.02).float()
+    ret[torch.rand(R, generator=g) < 0.03] = float("nan")
+    mret = (torch.randn(R, generator=g) * 0.012).float()
+    seg = RL.seg_lo_from_codes(stock).to(cuda)
+    r_, m_ = ret.to(cuda), mret.to(cuda)
+    ordv = (torch.arange(R, device=cuda, dtype=torch.int32) - seg)
+    b, h = RL.beta_hsigma(r_, m_, seg, 252, 63.0, 42, row_ord=ordv)
+    d = RL.dastd(r_, m_, seg, 252, 42.0, 42, row_ord=ordv)
+    bt, ht = RL.beta_hsigma(r_, m_, seg, 252, 63.0, 42)
+    dt = RL.dastd(r_, m_, seg, 252, 42.0, 42)
+    for a, t in ((b, bt), (h, ht), (d, dt)):
+        torch.testing.assert_close(a, t, rtol=2e-5, atol=2e-7, equal_nan=True)
+    # slices: per stock rows [t0, end) with t0 = max(0, own - 512), own = a random output start
+    starts = torch.cumsum(lens, 0) - lens
+    keep, own = [], []
+    for s_, n_ in zip(starts.tolist(), lens.tolist()):
+        o = int(torch.randint(0, n_, (1,), generator=g))
+        t0 = max(0, o - 512)
+        keep.append(torch.arange(s_ + t0, s_ + n_))
+        own.append(torch.arange(s_ + o, s_ + n_))
+    keep = torch.cat(keep).to(cuda)
+    own = torch.cat(own).to(cuda)
+    sseg = RL.seg_lo_from_codes(stock.to(cuda)[keep])
+    sb, sh = RL.beta_hsigma(r_[keep], m_[keep], sseg, 252, 63.0, 42, row_ord=ordv[keep])
+    sd = RL.dastd(r_[keep], m_[keep], sseg, 252, 42.0, 42, row_ord=ordv[keep])
+    pos = torch.searchsorted(keep, own)   # owned rows inside the slice
+    for full, part in ((b, sb), (h, sh), (d, sd)):
+        assert torch.equal(full[own].nan_to_num(7.0), part[pos].nan_to_num(7.0))
