@@ -73,28 +73,51 @@ __global__ __launch_bounds__(256) void beta_hsigma_kernel(const float* __restric
   hsig[r] = h;
 }
 
+// lam^k by binary powering (k < 512): no libm pow per table entry
+__device__ __forceinline__ double ipow(double lam, int k) {
+  double r = 1.0, b = lam;
+#pragma unroll
+  for (int i = 0; i < 9; ++i) {
+    if (k & (1 << i)) r *= b;
+    b *= b;
+  }
+  return r;
+}
+
+// Direct per-row RSTR (the reference kernel of the tests and the rank-invariant path): the
+// positional weights lam^k come from an LDS table (no dependent weight-update chain) and the
+// window sums alternate between two accumulators (half the dependent fma chain); every row's
+// window is still summed in one fixed order, independent of the launch it belongs to.
+constexpr int kRsDirectTab = 512;
 __global__ __launch_bounds__(256) void rstr_kernel(const float* __restrict__ lr,
                                                    const int* __restrict__ seg_lo, int R, int L,
                                                    int W, double lam, int minp,
                                                    float* __restrict__ out) {
+  __shared__ double pw[kRsDirectTab];
+  const bool tab = W <= kRsDirectTab;
+  if (tab) {
+    for (int k = threadIdx.x; k < W; k += blockDim.x) pw[k] = ipow(lam, k);
+    __syncthreads();
+  }
   const int r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= R) return;
   const int s0 = seg_lo[r];
   const int lo = max(s0, r - W + 1);
   // positional weight lam^(j - lo): oldest row of the (possibly partial) window gets 1
-  double num = 0.0, den = 0.0, wj = 1.0;
+  double num[2] = {0.0, 0.0}, den[2] = {0.0, 0.0}, wj = 1.0;
   int n = 0;
   for (int j = lo; j <= r; ++j) {
-    const int src = j - L;
+    const int src = j - L, k = j - lo;
     const float v = src >= s0 ? lr[src] : qnanf();
+    const double wk = tab ? pw[k] : wj;
     if (fin(v)) {
-      num = fma(wj, (double)v, num);
-      den += wj;
+      num[k & 1] = fma(wk, (double)v, num[k & 1]);
+      den[k & 1] += wk;
       ++n;
     }
-    wj *= lam;
+    if (!tab) wj *= lam;
   }
-  out[r] = (n >= minp) ? (float)(num / den) : qnanf();
+  out[r] = (n >= minp) ? (float)((num[0] + num[1]) / (den[0] + den[1])) : qnanf();
 }
 
 __global__ __launch_bounds__(256) void dastd_kernel(const float* __restrict__ ret,
@@ -579,17 +602,6 @@ struct DastdOp {  // e = ret - mret: sums of 1, e, ee; weighted population std
 // padded staging index for C-row chunks: one spare word per chunk (odd lane stride C + 1)
 template <int C>
 __device__ __forceinline__ int ew_idx(int p) { return p + p / C; }
-
-// lam^k by binary powering (k < 512): no libm pow per table entry
-__device__ __forceinline__ double ipow(double lam, int k) {
-  double r = 1.0, b = lam;
-#pragma unroll
-  for (int i = 0; i < 9; ++i) {
-    if (k & (1 << i)) r *= b;
-    b *= b;
-  }
-  return r;
-}
 
 // Persistent, software-pipelined variant: each block loops over tiles of TR staged rows; a
 // thread keeps its own C rows in registers (phase A and its own-row steps read them there, the

@@ -22,6 +22,8 @@
 #include <thread>
 #include <vector>
 
+#include "row_index.h"
+
 namespace {
 
 struct Map {
@@ -77,8 +79,11 @@ int32_t parse_date(const char* s, const char* e) {
   return nd >= 8 ? v / (int32_t)std::pow(10, nd - 8) : -1;
 }
 
+// ix (optional): the row-group index chunk of this range, fed each row right after it is parsed
+// (its code and date are still in cache); kc / dc = the code and date columns.
 void parse_range(const char* s, const char* e, int64_t row0, int ncol, const int* types,
-                 void** outs) {
+                 void** outs, mfa_ix::Chunk* ix = nullptr, int kc = -1, int dc = -1,
+                 uint8_t* mask = nullptr) {
   int64_t r = row0;
   while (s < e) {
     const char* le = next_line(s, e);
@@ -107,6 +112,7 @@ void parse_range(const char* s, const char* e, int64_t row0, int ncol, const int
       }
       f = fe < line_end ? fe + 1 : line_end;
     }
+    if (ix) ix->row((const uint8_t*)outs[kc], (const int32_t*)outs[dc], r, mask);
     ++r;
     s = le;
   }
@@ -146,10 +152,12 @@ __attribute__((visibility("default"))) int64_t mfa_csv_shape(const char* path, i
   return rows;
 }
 
-// Parse all data rows into caller buffers outs[c] (typed by types[c]); returns rows parsed.
-__attribute__((visibility("default"))) int64_t mfa_csv_parse(const char* path, int ncol,
-                                                              const int* types, void** outs,
-                                                              int nthreads) {
+}  // extern "C"
+
+namespace {
+
+int64_t parse_file(const char* path, int ncol, const int* types, void** outs, int nthreads,
+                   int kc, int dc, uint8_t* mask, void** index) {
   Map m;
   if (!m.open(path)) return -1;
   if (m.n == 0) return 0;
@@ -187,11 +195,42 @@ __attribute__((visibility("default"))) int64_t mfa_csv_parse(const char* path, i
     for (auto& x : th) x.join();
     for (int t = 0; t < nt; ++t) start[t + 1] = start[t] + cnt[t];
   }
+  const bool want_ix = index && kc >= 0 && dc >= 0 && mask;
+  std::vector<mfa_ix::Chunk> ch(want_ix ? nt : 0);
   std::vector<std::thread> th;
   for (int t = 0; t < nt; ++t)
-    th.emplace_back([&, t] { parse_range(b[t], b[t + 1], start[t], ncol, types, outs); });
+    th.emplace_back([&, t] {
+      mfa_ix::Chunk* c = want_ix ? &ch[t] : nullptr;
+      if (c) c->r0 = start[t];
+      parse_range(b[t], b[t + 1], start[t], ncol, types, outs, c, kc, dc, mask);
+    });
   for (auto& x : th) x.join();
+  if (want_ix) *index = mfa_ix::merge(ch, (const uint8_t*)outs[kc], (const int32_t*)outs[dc]);
   return start[nt];
+}
+
+}  // namespace
+
+extern "C" {
+
+// Parse all data rows into caller buffers outs[c] (typed by types[c]); returns rows parsed.
+__attribute__((visibility("default"))) int64_t mfa_csv_parse(const char* path, int ncol,
+                                                              const int* types, void** outs,
+                                                              int nthreads) {
+  return parse_file(path, ncol, types, outs, nthreads, -1, -1, nullptr, nullptr);
+}
+
+// mfa_csv_parse + the row-group index of the parsed rows (row_index.h), built while parsing:
+// kc = the code column (type 1), dc = the trade-date column (type 2), mask = caller's
+// mfa_date_span() zeroed bytes; *index = a handle for mfa_row_index_* (csrc_host/shard_rows.cpp).
+__attribute__((visibility("default"))) int64_t mfa_csv_parse_ix(const char* path, int ncol,
+                                                                 const int* types, void** outs,
+                                                                 int nthreads, int kc, int dc,
+                                                                 uint8_t* mask, void** index) {
+  *index = nullptr;
+  if (kc < 0 || dc < 0 || kc >= ncol || dc >= ncol || types[kc] != 1 || types[dc] != 2)
+    return parse_file(path, ncol, types, outs, nthreads, -1, -1, nullptr, nullptr);
+  return parse_file(path, ncol, types, outs, nthreads, kc, dc, mask, index);
 }
 
 }  // extern "C"

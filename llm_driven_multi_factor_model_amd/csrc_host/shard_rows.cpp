@@ -2,22 +2,19 @@
 //
 // Reference: the job of Barra_factor_cal/main.py:42-158 + Barra-master/demo.py:22-42 split over
 // ranks by date.  Round 4 had every rank upload ALL loader rows and build the full device master
-// (0.027 s per rank whatever the world size); here each rank scans the loader columns on the
-// host, keeps only its rows, and uploads those.
+// (0.027 s per rank whatever the world size); here each rank picks only its rows on the host and
+// uploads those.
 //
-// Input: the loader's columns with rows grouped by stock in ascending code order and, within a
-// stock, strictly ascending trade dates (the stored panel's order; the caller falls back to the
-// full build otherwise).  One pass over the rows (threads over row ranges cut at stock
-// boundaries) finds, per stock segment [a, b):
-//   * its global stock id (the segment's rank = its code's rank among all codes);
-//   * k_lo / k_hi = the first rows with trade_date >= date_lo / >= date_hi (the rank's dates);
-//   * the kept range [start, k_hi): start = k_lo - halo rows (clamped to a), extended further
-//     back (statement rows) until the range holds the `nstmt` most recent distinct end dates
-//     before k_lo, so the trailing-twelve-month cash flow of every owned row is complete;
-//     a stock with no owned row keeps nothing.
-// mfa_date_mask marks every trade date that occurs (a bitmap over YYYYMMDD) in a first pass, so
-// every rank derives the same global date axis (and its block's date bounds) without a
-// collective.
+// Two steps:
+//   1. the row-group index (row_index.h): the first row of every stock segment and the trade-date
+//      mask, with the (code, date) order checked.  The CSV reader builds it while parsing
+//      (csv_panel.cpp); mfa_row_index is the one-pass threaded build for columns from elsewhere.
+//   2. mfa_shard_rows_ix, per stock segment [a, b) (binary searches, no pass over the rows):
+//      k_lo / k_hi = the first rows with trade_date >= date_lo / >= date_hi (the rank's dates);
+//      the kept range [start, k_hi): start = k_lo - halo rows (clamped to a), extended further
+//      back (statement rows) until the range holds the `nstmt` most recent distinct end dates
+//      before k_lo, so the trailing-twelve-month cash flow of every owned row is complete; a
+//      stock with no owned row keeps nothing.
 #include <algorithm>
 #include <atomic>
 #include <cstdint>
@@ -25,20 +22,17 @@
 #include <thread>
 #include <vector>
 
+#include "row_index.h"
+
 namespace {
 
-inline int cmp16(const uint8_t* a, const uint8_t* b) { return std::memcmp(a, b, 16); }
-// equality of two 16-byte codes as two 8-byte words (the per-row test of the scans)
-inline bool eq16(const uint8_t* a, const uint8_t* b) {
-  uint64_t a0, a1, b0, b1;
-  std::memcpy(&a0, a, 8);
-  std::memcpy(&a1, a + 8, 8);
-  std::memcpy(&b0, b, 8);
-  std::memcpy(&b1, b + 8, 8);
-  return ((a0 ^ b0) | (a1 ^ b1)) == 0;
-}
+using mfa_ix::kDateHi;
+using mfa_ix::kDateLo;
 
-constexpr int32_t kDateLo = 19000101, kDateHi = 21000101;  // bitmap span of YYYYMMDD ints
+int threads_or_default(int nthreads) {
+  return nthreads > 0 ? nthreads
+                      : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+}
 
 }  // namespace
 
@@ -47,8 +41,7 @@ constexpr int32_t kDateLo = 19000101, kDateHi = 21000101;  // bitmap span of YYY
 extern "C" __attribute__((visibility("default"))) int64_t mfa_date_span() { return kDateHi - kDateLo; }
 extern "C" __attribute__((visibility("default"))) int mfa_date_mask(const int32_t* dates, int64_t R,
                                                                   uint8_t* mask, int nthreads) {
-  const int nt = nthreads > 0 ? nthreads
-                              : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const int nt = threads_or_default(nthreads);
   std::atomic<int> err{0};
   std::vector<std::thread> th;
   for (int t = 0; t < nt; ++t)
@@ -57,8 +50,6 @@ extern "C" __attribute__((visibility("default"))) int mfa_date_mask(const int32_
       for (int64_t i = a; i < b; ++i) {
         const int32_t d = dates[i];
         if (d < kDateLo || d >= kDateHi) { err = -2; return; }
-        // test before storing: after a date's first sighting its line stays shared between the
-        // threads' caches instead of bouncing on every row
         if (!mask[d - kDateLo]) mask[d - kDateLo] = 1;
       }
     });
@@ -66,111 +57,110 @@ extern "C" __attribute__((visibility("default"))) int mfa_date_mask(const int32_
   return err.load();
 }
 
-// codes: [R][16] bytes, dates: [R] int32 YYYYMMDD, end_dates: [R] int32 or null.
-// Outputs: ranges [2 * cap] (start, stop) of the kept rows of each stock that keeps rows, seg_id
-// [cap] global stock id of each range, seg_first [cap] first row of every stock segment (the
-// global stock axis: segment k = stock id k), n_ranges, n_stocks.  Returns 0, or
-//   -1 rows not grouped by stock in ascending code order / dates not ascending in a stock,
-//   -3 output capacity (cap) too small.
-extern "C" __attribute__((visibility("default"))) int mfa_shard_rows(
-    const uint8_t* codes, const int32_t* dates, const int32_t* end_dates, int64_t R,
-    int32_t date_lo, int32_t date_hi, int64_t halo, int nstmt, int64_t* ranges, int32_t* seg_id,
-    int64_t* seg_first, int64_t cap, int64_t* n_ranges, int64_t* n_stocks, int nthreads) {
-  *n_ranges = 0;
-  *n_stocks = 0;
-  if (R <= 0) return 0;
-  const int nt = nthreads > 0 ? nthreads
-                              : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  // cut the rows into nt pieces at stock boundaries
-  std::vector<int64_t> cut(nt + 1, R);
-  cut[0] = 0;
-  for (int t = 1; t < nt; ++t) {
-    int64_t c = std::max(R * t / nt, cut[t - 1]);
-    while (c < R && c > 0 && eq16(codes + 16 * c, codes + 16 * (c - 1))) ++c;
-    cut[t] = c;
+// Ascending dates of a mask: writes up to cap of them, returns how many there are.
+extern "C" __attribute__((visibility("default"))) int64_t mfa_mask_dates(const uint8_t* mask,
+                                                                       int32_t* out, int64_t cap) {
+  int64_t n = 0;
+  const int64_t span = kDateHi - kDateLo;
+  for (int64_t i = 0; i < span; i += 8) {
+    uint64_t w;  // 8 mask bytes at a time: most of the span (non-dates) is zero
+    std::memcpy(&w, mask + i, 8);
+    if (!w) continue;
+    for (int64_t j = i; j < i + 8 && j < span; ++j)
+      if (mask[j]) {
+        if (n < cap) out[n] = (int32_t)(kDateLo + j);
+        ++n;
+      }
   }
-  struct Part {
-    std::vector<int64_t> rg;   // (start, stop) per kept stock
-    std::vector<int64_t> seg;  // local segment index of each kept stock
-    std::vector<int64_t> first;  // first row of every segment
-    int64_t nseg = 0;
-    int err = 0;
-    bool asc = true;  // segment codes strictly ascending within the piece
-  };
-  std::vector<Part> parts(nt);
+  return n;
+}
+
+// One-pass threaded build of the row-group index of codes [R][16] / dates [R]; mask: zeroed
+// mfa_date_span() bytes.  Returns a handle (free with mfa_row_index_free).
+extern "C" __attribute__((visibility("default"))) void* mfa_row_index(const uint8_t* codes,
+                                                                    const int32_t* dates, int64_t R,
+                                                                    uint8_t* mask, int nthreads) {
+  const int nt = threads_or_default(nthreads);
+  std::vector<mfa_ix::Chunk> ch(nt);
   std::vector<std::thread> th;
   for (int t = 0; t < nt; ++t)
     th.emplace_back([&, t] {
-      Part& P = parts[t];
-      int64_t a = cut[t];
-      const int64_t end = cut[t + 1];
-      while (a < end) {
-        int64_t b = a + 1;
-        while (b < end && eq16(codes + 16 * b, codes + 16 * a)) ++b;
-        // within the stock: strictly ascending dates
-        for (int64_t i = a + 1; i < b; ++i)
-          if (dates[i] <= dates[i - 1]) { P.err = -1; return; }
-        if (!P.first.empty() && cmp16(codes + 16 * a, codes + 16 * P.first.back()) <= 0) P.asc = false;
-        P.first.push_back(a);
+      const int64_t a = R * t / nt, b = R * (t + 1) / nt;
+      ch[t].r0 = a;
+      for (int64_t r = a; r < b; ++r) ch[t].row(codes, dates, r, mask);
+    });
+  for (auto& x : th) x.join();
+  return mfa_ix::merge(ch, codes, dates);
+}
+
+// Number of segments (stocks) of an index, or its error (-1 rows not grouped by code in
+// ascending order / dates not strictly ascending in a stock, -2 date outside the mask span).
+extern "C" __attribute__((visibility("default"))) int64_t mfa_row_index_count(const void* h) {
+  const auto* ix = (const mfa_ix::Index*)h;
+  return ix->err ? ix->err : (int64_t)ix->seg_first.size();
+}
+extern "C" __attribute__((visibility("default"))) void mfa_row_index_get(const void* h,
+                                                                       int64_t* seg_first) {
+  const auto* ix = (const mfa_ix::Index*)h;
+  std::memcpy(seg_first, ix->seg_first.data(), ix->seg_first.size() * sizeof(int64_t));
+}
+extern "C" __attribute__((visibility("default"))) void mfa_row_index_free(void* h) {
+  delete (mfa_ix::Index*)h;
+}
+
+// seg_first [nseg] (ascending, seg_first[0] = 0) of R rows; dates [R] int32, end_dates [R] int32
+// or null.  Outputs (capacity nseg): ranges [2 * nseg] (start, stop) of the kept rows of each
+// stock that keeps rows, seg_id [nseg] global stock id of each range; returns the range count.
+extern "C" __attribute__((visibility("default"))) int64_t mfa_shard_rows_ix(
+    const int64_t* seg_first, int64_t nseg, int64_t R, const int32_t* dates,
+    const int32_t* end_dates, int32_t date_lo, int32_t date_hi, int64_t halo, int nstmt,
+    int64_t* ranges, int32_t* seg_id, int nthreads) {
+  if (nseg <= 0) return 0;
+  // threads over segments (the TTM walk-back reads a few hundred rows per stock); each writes
+  // its kept ranges at its segments' own slots, compacted below
+  const int nt = std::min<int64_t>(threads_or_default(nthreads), (nseg + 255) / 256);
+  std::vector<uint8_t> keep(nseg, 0);
+  std::vector<int64_t> rg(2 * nseg);
+  std::vector<std::thread> th;
+  for (int t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      for (int64_t k = nseg * t / nt; k < nseg * (t + 1) / nt; ++k) {
+        const int64_t a = seg_first[k], b = k + 1 < nseg ? seg_first[k + 1] : R;
         const int64_t klo = std::lower_bound(dates + a, dates + b, date_lo) - dates;
-        const int64_t khi = std::lower_bound(dates + a, dates + b, date_hi) - dates;
-        if (klo < khi) {
-          int64_t s = std::max(a, klo - halo);
-          if (end_dates && nstmt > 0) {
-            // walk back from klo until nstmt distinct end dates precede it
-            int runs = 0;
-            int64_t j = klo - 1;
-            int32_t prev = 0;
-            bool have = false;
-            for (; j >= a; --j) {
-              if (!have || end_dates[j] != prev) {
-                if (runs == nstmt) break;
-                ++runs;
-                prev = end_dates[j];
-                have = true;
-              }
+        const int64_t khi = std::lower_bound(dates + klo, dates + b, date_hi) - dates;
+        if (klo >= khi) continue;
+        int64_t s = std::max(a, klo - halo);
+        if (end_dates && nstmt > 0) {
+          // walk back from klo until nstmt distinct end dates precede it
+          int runs = 0;
+          int64_t j = klo - 1;
+          int32_t prev = 0;
+          bool have = false;
+          for (; j >= a; --j) {
+            if (!have || end_dates[j] != prev) {
+              if (runs == nstmt) break;
+              ++runs;
+              prev = end_dates[j];
+              have = true;
             }
-            s = std::min(s, j + 1);
           }
-          P.rg.push_back(s);
-          P.rg.push_back(khi);
-          P.seg.push_back(P.nseg);
+          s = std::min(s, j + 1);
         }
-        ++P.nseg;
-        a = b;
+        rg[2 * k] = s;
+        rg[2 * k + 1] = khi;
+        keep[k] = 1;
       }
     });
   for (auto& x : th) x.join();
-  int64_t nseg = 0, nr = 0;
-  // ascending codes: consecutive segment starts within each piece (threads) and across the
-  // piece boundaries (here) -- O(segments), not another pass over the rows
-  for (int t = 0; t < nt; ++t) {
-    if (parts[t].err) return parts[t].err;
-    if (!parts[t].asc) return -1;
-  }
-  int64_t last = -1;
-  for (int t = 0; t < nt; ++t) {
-    const Part& P = parts[t];
-    if (P.first.empty()) continue;
-    if (last >= 0 && cmp16(codes + 16 * P.first.front(), codes + 16 * last) <= 0) return -1;
-    last = P.first.back();
-  }
-  for (int t = 0; t < nt; ++t) {
-    const Part& P = parts[t];
-    if (nseg + P.nseg > cap) return -3;
-    for (int64_t k = 0; k < P.nseg; ++k) seg_first[nseg + k] = P.first[k];
-    for (size_t k = 0; k < P.seg.size(); ++k) {
-      if (nr >= cap) return -3;
-      ranges[2 * nr] = P.rg[2 * k];
-      ranges[2 * nr + 1] = P.rg[2 * k + 1];
-      seg_id[nr] = (int32_t)(nseg + P.seg[k]);
+  int64_t nr = 0;
+  for (int64_t k = 0; k < nseg; ++k)
+    if (keep[k]) {
+      ranges[2 * nr] = rg[2 * k];
+      ranges[2 * nr + 1] = rg[2 * k + 1];
+      seg_id[nr] = (int32_t)k;
       ++nr;
     }
-    nseg += P.nseg;
-  }
-  *n_ranges = nr;
-  *n_stocks = nseg;
-  return 0;
+  return nr;
 }
 
 // dst = concatenation of src rows [ranges[2k], ranges[2k+1]) (elem bytes per row), threads over
@@ -179,8 +169,7 @@ extern "C" __attribute__((visibility("default"))) int mfa_gather_ranges(
     const uint8_t* src, int64_t elem, const int64_t* ranges, const int64_t* offs, int64_t nr,
     uint8_t* dst, int nthreads) {
   if (nr <= 0) return 0;
-  const int nt = nthreads > 0 ? nthreads
-                              : (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  const int nt = threads_or_default(nthreads);
   std::atomic<int64_t> next{0};
   std::vector<std::thread> th;
   for (int t = 0; t < nt; ++t)

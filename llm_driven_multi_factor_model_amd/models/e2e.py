@@ -194,12 +194,11 @@ class DeviceFactorEngine(FactorEngine):
         dev = self.device
         self.R, self.D = int(stock_id.numel()), int(len(dv))
         self.N = int(names.size)
-        self.stock_names = pd.Index(names.astype("U16").astype(object))
+        # the label indexes are built on first use (the writers need them, the device pipeline
+        # does not): 6.5 ms of host string work at 5000 x 2520
+        self._names_s16 = names
+        self._stock_names = self._date_names = None
         self.date_ints = dv
-        y, m, d = dv // 10000, dv // 100 % 100, dv % 100
-        self.date_names = pd.Index(np.char.add(np.char.add(np.char.add(
-            np.char.zfill(y.astype(str), 4), "/"), np.char.add(np.char.zfill(m.astype(str), 2), "/")),
-            np.char.zfill(d.astype(str), 2)).astype(object))
         self.stock_id = stock_id
         self.date_id = date_id
         self.seg_lo = RL.seg_lo_from_codes(self.stock_id)
@@ -224,20 +223,50 @@ class DeviceFactorEngine(FactorEngine):
         self.cols["ret"], self.cols["log_ret"] = RL.returns(self.cols["close"], self.seg_lo)
         self.end_date = end_date
 
+    @property
+    def stock_names(self) -> pd.Index:
+        if self._stock_names is None:
+            self._stock_names = pd.Index(self._names_s16.astype("U16").astype(object))
+        return self._stock_names
+
+    @stock_names.setter
+    def stock_names(self, v) -> None:
+        self._stock_names = v
+
+    @property
+    def date_names(self) -> pd.Index:
+        """YYYY/MM/DD labels of the date axis."""
+        if self._date_names is None:
+            dv = np.asarray(self.date_ints)
+            y, m, d = dv // 10000, dv // 100 % 100, dv % 100
+            self._date_names = pd.Index(np.char.add(np.char.add(np.char.add(
+                np.char.zfill(y.astype(str), 4), "/"), np.char.add(np.char.zfill(m.astype(str), 2), "/")),
+                np.char.zfill(d.astype(str), 2)).astype(object))
+        return self._date_names
+
+    @date_names.setter
+    def date_names(self, v) -> None:
+        self._date_names = v
+
     # ------------------------------------------------------------ host-side date sharding
     @classmethod
     def from_host_shard(cls, prices: dict, index: dict, rank: int, world: int, device=None,
-                        config: FactorConfig | None = None):
+                        config: FactorConfig | None = None, timing: bool = False):
         """The rows of date block ``rank`` of ``world`` -- exactly what ``DeviceFactorEngine(
         prices, index).date_shard(*shard_range(D, rank, world))`` keeps (its owned dates, each
         stock's ``halo_rows()`` preceding rows, plus the statement rows of the four most recent
-        distinct end dates before them), selected on the HOST from the loader columns
-        (``csrc_host/shard_rows.cpp``, one threaded pass) so a rank uploads and builds only its
-        share instead of the whole master.  Global stock ids (code ranks) and the global date
-        axis come from the same pass, so every rank numbers stocks and dates identically
-        without a collective.  None when the loader rows are not sorted by (code, date) or the
-        native library is missing (the caller builds the full master and calls
-        :meth:`date_shard`)."""
+        distinct end dates before them), selected on the HOST so a rank uploads and builds only
+        its share instead of the whole master.
+
+        The selection runs on the loader's row-group index (``native_io.RowIndex``: the first
+        row of every stock and the trade-date set), which the CSV reader builds while it parses
+        (``prices[native_io.ROW_INDEX]``); for columns from elsewhere it is built here in one
+        threaded pass.  Per stock, binary searches find the kept range
+        (``csrc_host/shard_rows.cpp``); global stock ids (segment ranks) and the global date axis
+        come from the index, so every rank numbers stocks and dates identically without a
+        collective.  None when the loader rows are not sorted by (code, date) or the native
+        library is missing (the caller builds the full master and calls :meth:`date_shard`).
+        ``timing``: synchronise the device at each sub-step of ``host_times`` (profiling)."""
         from ..parallel.dist import shard_range
         from ..utils import native_io
         cfg = config or FactorConfig()
@@ -248,21 +277,27 @@ class DeviceFactorEngine(FactorEngine):
             return None
         ht = {}
         t0 = time.perf_counter()
-        dv = native_io.trade_dates(prices["trade_date"])
-        if dv is None or dv.size == 0:
-            return None
+        ix = prices.get(native_io.ROW_INDEX)
+        if ix is not None and ix.rows != codes.size:
+            ix = None   # the columns changed since the index was built
+        ht["index"] = "reader" if ix is not None else "scan"
+        if ix is None:
+            ix = native_io.row_index(codes, prices["trade_date"])
+            if ix is None:
+                return None
+        dv = ix.dates
         D = int(dv.size)
+        if D == 0:
+            return None
         lo, hi = shard_range(D, rank, world)
         big = np.iinfo(np.int32).max
         date_lo = int(dv[lo]) if lo < D else big
         date_hi = int(dv[hi]) if hi < D else big
         halo = FactorEngine.halo_rows(type("C", (), {"cfg": cfg})())
-        ed = prices.get("end_date")
-        got = native_io.shard_rows(codes, prices["trade_date"], ed, date_lo, date_hi, halo)
-        if got is None:
-            return None
-        ranges, seg_id, seg_first = got
-        ht["scan_s"] = time.perf_counter() - t0
+        ranges, seg_id = native_io.shard_rows_ix(ix, prices["trade_date"], prices.get("end_date"),
+                                                 date_lo, date_hi, halo)
+        seg_first = ix.seg_first
+        ht["select_s"] = time.perf_counter() - t0
         t0 = time.perf_counter()
         lens = ranges[:, 1] - ranges[:, 0]
         offs = np.zeros(lens.size + 1, np.int64)
@@ -273,8 +308,9 @@ class DeviceFactorEngine(FactorEngine):
         eng.device = torch.device(device) if device is not None else torch.device(
             os.environ.get("MFA_DEVICE") or ("cuda:0" if torch.cuda.is_available() else "cpu"))
         dev = eng.device
+        sync = (lambda: torch.cuda.synchronize(dev)) if timing and dev.type == "cuda" else (lambda: None)
         # the kept rows of the columns the engine uses (codes are not needed: the stock ids come
-        # from the scan).  Pinned reader buffers on a GPU: the device reads the ranges straight
+        # from the index).  Pinned reader buffers on a GPU: the device reads the ranges straight
         # out of host memory (csrc/gather.hip, one pass over PCIe, only this rank's bytes);
         # otherwise a threaded host memcpy into pageable buffers and their upload.
         names_c = [c for c in prices if c in cls.NUMERIC or c in ("trade_date", "end_date")]
@@ -287,22 +323,30 @@ class DeviceFactorEngine(FactorEngine):
             sel = {c: _upload(native_io.gather_ranges(x, ranges, offs, np.empty(Rk, dtype=x.dtype)), dev)
                    for c, x in zip(names_c, srcs)}
             ht["gather"] = "host"
+        sync()
         ht["gather_s"] = time.perf_counter() - t0
         t0 = time.perf_counter()
         eng.master = None
-        sid = _upload(np.repeat(seg_id, lens).astype(np.int32), dev)
+        # per-row stock ids and full-history ordinals expanded on the device from the per-range
+        # values (no host repeat of Rk rows, no sync: the output size is known)
+        lt = torch.from_numpy(lens).to(dev)
+        sid = torch.repeat_interleave(torch.from_numpy(seg_id).to(dev), lt, output_size=Rk)
+        ord0 = torch.from_numpy(ranges[:, 0] - seg_first[seg_id] - offs[:-1]).to(dev)
+        row_ord = (torch.repeat_interleave(ord0, lt, output_size=Rk)
+                   + torch.arange(Rk, device=dev)).to(torch.int32)
         td = sel["trade_date"]
         up = {c: sel[c] for c in cls.NUMERIC if c in sel}
         edv = sel["end_date"].long() if "end_date" in sel else None
         did = torch.searchsorted(torch.from_numpy(dv.astype(np.int64)).to(dev), td.long()).to(torch.int32)
         names = codes[seg_first]
+        sync()
+        ht["ids_s"] = time.perf_counter() - t0
+        t1 = time.perf_counter()
         eng._finish_arrays(sid, did, names, dv, up, edv, index)
         # each kept row's ordinal in its stock's full history (the aligned rank-invariant tiles)
-        lt = torch.from_numpy(lens).to(dev)
-        ord0 = torch.from_numpy(ranges[:, 0] - seg_first[seg_id]).to(dev)
-        o0 = torch.from_numpy(offs[:-1]).to(dev)
-        eng._row_ord = (torch.repeat_interleave(ord0 - o0, lt)
-                        + torch.arange(Rk, device=dev)).to(torch.int32)
+        eng._row_ord = row_ord
+        sync()
+        ht["finish_s"] = time.perf_counter() - t1
         eng.prep_s = time.perf_counter() - t0
         ht["upload_build_s"] = eng.prep_s
         eng.own = (eng.date_id >= lo) & (eng.date_id < hi)
@@ -313,6 +357,10 @@ class DeviceFactorEngine(FactorEngine):
 
     def _has_statements(self) -> bool:
         return "n_cashflow_act" in self.cols and self.end_date is not None
+
+    def _copy_labels(self, sub, d_lo, d_hi) -> None:
+        # still lazy in the sub-engine: its date labels come from its date_ints slice
+        sub._names_s16, sub._stock_names, sub._date_names = self._names_s16, self._stock_names, None
 
     def _take(self, idx, d_lo=0, d_hi=None):
         sub = super()._take(idx, d_lo, d_hi)
@@ -548,7 +596,8 @@ def read_price_columns(prices_csv: str, index_csv: str):
     types = {c: 3 for c in FactorEngine.NUMERIC}
     types.update({c: 1 for c in PRICE_STRING_COLS})
     types.update({c: 2 for c in PRICE_DATE_COLS})
-    p = native_io.read_columns(prices_csv, types, pinned=_pin_default())
+    # the parser also builds the row-group index the date-sharded ranks select their rows on
+    p = native_io.read_columns(prices_csv, types, pinned=_pin_default(), index=("ts_code", "trade_date"))
     i = native_io.read_columns(index_csv, {"ts_code": 1, "trade_date": 2})
     return p, i
 
@@ -567,11 +616,16 @@ def stage_host_columns(prices: dict, pinned: bool | None = None) -> dict:
     """The layout :func:`read_price_columns` produces, from float64 columnar arrays (e.g.
     :func:`_columns_from_frames`): the engine's numeric columns rounded to float32 (Q27), codes /
     dates / numerics in pinned host memory when a GPU is present.  This is the native reader's
-    parse-time work; benchmarks count it as I/O."""
+    parse-time work; benchmarks count it as I/O.  That includes the row-group index
+    (``native_io.ROW_INDEX``), which the reader builds while parsing: here one threaded pass over
+    the staged codes and dates."""
+    from ..utils import native_io
     from ..utils.native_io import _host_buffer
     pinned = _pin_default() if pinned is None else pinned
     out = {}
     for c, x in prices.items():
+        if c == native_io.ROW_INDEX:
+            continue
         x = np.asarray(x)
         if c in FactorEngine.NUMERIC:
             dt = np.float32
@@ -585,6 +639,10 @@ def stage_host_columns(prices: dict, pinned: bool | None = None) -> dict:
         buf = _host_buffer(len(x), dt, pinned)
         buf[...] = x
         out[c] = buf
+    if "ts_code" in out and "trade_date" in out and out["ts_code"].dtype == np.dtype("S16"):
+        ix = native_io.row_index(out["ts_code"], out["trade_date"])
+        if ix is not None:
+            out[native_io.ROW_INDEX] = ix
     return out
 
 

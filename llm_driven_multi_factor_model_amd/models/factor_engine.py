@@ -206,13 +206,16 @@ class FactorEngine:
         sub.date_lo = self.lo
         return sub
 
+    def _copy_labels(self, sub: "FactorEngine", d_lo: int, d_hi: int) -> None:
+        sub.stock_names, sub.date_names = self.stock_names, self.date_names[d_lo:d_hi]
+
     def _take(self, idx: torch.Tensor, d_lo: int = 0, d_hi: int | None = None) -> "FactorEngine":
         """Rows ``idx`` (increasing, so still sorted by stock then date) as a new engine; dates
         renumbered to [0, d_hi - d_lo)."""
         d_hi = self.D if d_hi is None else d_hi
         sub = object.__new__(type(self))
         sub.cfg, sub.device, sub.prep_s = self.cfg, self.device, 0.0
-        sub.stock_names, sub.date_names = self.stock_names, self.date_names[d_lo:d_hi]
+        self._copy_labels(sub, d_lo, d_hi)
         sub.D, sub.N, sub.R = d_hi - d_lo, self.N, int(idx.numel())
         sub.master = None if self.master is None else \
             self.master.iloc[idx.cpu().numpy()].reset_index(drop=True)

@@ -345,8 +345,11 @@ def _finalize_wide(S, M, w, U, valid, scale_coef):
     dev = w.device
     Fh = torch.empty(D, K, K, dtype=torch.float64, device=dev)
     vb = torch.empty(D, K, dtype=torch.float64, device=dev)
-    _native.call("mfa_eigen_finalize_sum", _native.ptr(S.contiguous()), int(M), _native.ptr(w.contiguous()),
-                 _native.ptr(U.contiguous()), _native.ptr(valid.to(torch.int32).contiguous()),
+    # operands bound to names: a temporary inside ptr(...) is freed before the launch and its block
+    # can be handed to the next temporary of the same call
+    Sc, wc, Uc, vi = S.contiguous(), w.contiguous(), U.contiguous(), valid.to(torch.int32).contiguous()
+    _native.call("mfa_eigen_finalize_sum", _native.ptr(Sc), int(M), _native.ptr(wc),
+                 _native.ptr(Uc), _native.ptr(vi),
                  D, K, float(scale_coef), _native.ptr(Fh), _native.ptr(vb), _native.stream(dev))
     return Fh, vb
 
@@ -424,8 +427,9 @@ def eigen_risk_adjust_sharded(F0: torch.Tensor, *, M: int = 10_000, scale_coef: 
     elif dev.type == "cuda":
         Fh = torch.empty(D, K, K, dtype=torch.float64, device=dev)
         vb = torch.empty(D, K, dtype=torch.float64, device=dev)
+        Uc, vi = U.contiguous(), valid.to(torch.int32).contiguous()   # named: see _finalize_wide
         _native.call("mfa_eigen_finalize_sum", _native.ptr(S), int(M), _native.ptr(w),
-                     _native.ptr(U.contiguous()), _native.ptr(valid.to(torch.int32).contiguous()),
+                     _native.ptr(Uc), _native.ptr(vi),
                      D, K, float(scale_coef), _native.ptr(Fh), _native.ptr(vb), _native.stream(dev))
     else:
         v = scale_coef * (torch.sqrt(S / M) - 1.0) + 1.0
@@ -481,7 +485,8 @@ def eigen_risk_adjust(F0: torch.Tensor, *, M: int = 100, scale_coef: float = 1.4
     ws = torch.empty(D * M * K, dtype=torch.float64, device=dev)
     dv = valid.to(torch.int32).contiguous()
     with _date_origin(date0, dev):
-        _native.call("mfa_eigen_adjust", _native.ptr(w.contiguous()), _native.ptr(U.contiguous()),
+        wc, Uc = w.contiguous(), U.contiguous()   # named: see _finalize_wide
+        _native.call("mfa_eigen_adjust", _native.ptr(wc), _native.ptr(Uc),
                      _native.ptr(dv), D, K, M, _native.ptr(Cz), float(scale_coef), MAX_SWEEPS, TOL,
                      _native.ptr(ws), _native.ptr(Fh), _native.ptr(vb), _native.stream(dev))
     return (Fh, vb) if return_bias else Fh

@@ -146,8 +146,10 @@ def beta_hsigma(ret, mret, seg_lo, window=252, half_life=63.0, min_periods=42, r
         v, seg_v, Rv = _aligned_layout(seg_lo, row_ord)
         bv = torch.empty(Rv, dtype=torch.float32, device=ret.device)
         hv = torch.empty_like(bv)
-        _native.call("mfa_beta_hsigma_aligned", _native.ptr(_to_virtual(ret, v, Rv)),
-                     _native.ptr(_to_virtual(mret, v, Rv)), _native.ptr(seg_v), Rv, window, lam,
+        # bound to names: a temporary passed as ptr(...) is freed before the launch, and the
+        # caching allocator then hands its block to the next temporary (the inputs alias)
+        yv, xv = _to_virtual(ret, v, Rv), _to_virtual(mret, v, Rv)
+        _native.call("mfa_beta_hsigma_aligned", _native.ptr(yv), _native.ptr(xv), _native.ptr(seg_v), Rv, window, lam,
                      min_periods, _native.ptr(bv), _native.ptr(hv), _native.stream(ret.device))
         return bv[v].contiguous(), hv[v].contiguous()
     if ret.is_cuda:
@@ -210,8 +212,8 @@ def dastd(ret, mret, seg_lo, window=252, half_life=42.0, min_periods=42, row_ord
     if ret.is_cuda and row_ord is not None and window <= ALIGN_MAX_W and R:
         v, seg_v, Rv = _aligned_layout(seg_lo, row_ord)
         ov = torch.empty(Rv, dtype=torch.float32, device=ret.device)
-        _native.call("mfa_dastd_aligned", _native.ptr(_to_virtual(ret, v, Rv)),
-                     _native.ptr(_to_virtual(mret, v, Rv)), _native.ptr(seg_v), Rv, window, lam,
+        yv, xv = _to_virtual(ret, v, Rv), _to_virtual(mret, v, Rv)   # named: see beta_hsigma
+        _native.call("mfa_dastd_aligned", _native.ptr(yv), _native.ptr(xv), _native.ptr(seg_v), Rv, window, lam,
                      min_periods, _native.ptr(ov), _native.stream(ret.device))
         return ov[v].contiguous()
     if ret.is_cuda:

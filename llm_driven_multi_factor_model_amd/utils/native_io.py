@@ -45,11 +45,23 @@ def _load():
         lib.mfa_date_span.restype = C.c_int64
         lib.mfa_date_mask.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int]
         lib.mfa_date_mask.restype = C.c_int
-        lib.mfa_shard_rows.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int32,
-                                       C.c_int32, C.c_int64, C.c_int, C.c_void_p, C.c_void_p,
-                                       C.c_void_p, C.c_int64, C.POINTER(C.c_int64),
-                                       C.POINTER(C.c_int64), C.c_int]
-        lib.mfa_shard_rows.restype = C.c_int
+        lib.mfa_csv_parse_ix.argtypes = [C.c_char_p, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_void_p),
+                                         C.c_int, C.c_int, C.c_int, C.c_void_p, C.POINTER(C.c_void_p)]
+        lib.mfa_csv_parse_ix.restype = C.c_int64
+        lib.mfa_mask_dates.argtypes = [C.c_void_p, C.c_void_p, C.c_int64]
+        lib.mfa_mask_dates.restype = C.c_int64
+        lib.mfa_row_index.argtypes = [C.c_void_p, C.c_void_p, C.c_int64, C.c_void_p, C.c_int]
+        lib.mfa_row_index.restype = C.c_void_p
+        lib.mfa_row_index_count.argtypes = [C.c_void_p]
+        lib.mfa_row_index_count.restype = C.c_int64
+        lib.mfa_row_index_get.argtypes = [C.c_void_p, C.c_void_p]
+        lib.mfa_row_index_get.restype = None
+        lib.mfa_row_index_free.argtypes = [C.c_void_p]
+        lib.mfa_row_index_free.restype = None
+        lib.mfa_shard_rows_ix.argtypes = [C.c_void_p, C.c_int64, C.c_int64, C.c_void_p, C.c_void_p,
+                                          C.c_int32, C.c_int32, C.c_int64, C.c_int, C.c_void_p,
+                                          C.c_void_p, C.c_int]
+        lib.mfa_shard_rows_ix.restype = C.c_int64
         lib.mfa_gather_ranges.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_int64,
                                           C.c_void_p, C.c_int]
         lib.mfa_gather_ranges.restype = C.c_int
@@ -120,12 +132,16 @@ def _host_buffer(rows: int, dtype, pinned: bool) -> np.ndarray:
     return np.zeros(rows, dtype=dtype) if dtype == "S16" else np.empty(rows, dtype=dtype)
 
 
-def read_columns(path: str, types: dict, nthreads: int = 0, pinned: bool = False):
+def read_columns(path: str, types: dict, nthreads: int = 0, pinned: bool = False,
+                 index: tuple | None = None):
     """Raw columnar parse: ``types`` maps column name -> 0 float64 / 1 bytes16 / 2 int YYYYMMDD /
     3 float32 (float64 parse rounded to float32, the reference's load downcast).
 
     Returns ``{name: ndarray}`` (bytes columns stay ``S16``), or None if unavailable.  With
-    ``pinned`` (a GPU is present) the buffers are page-locked host memory.
+    ``pinned`` (a GPU is present) the buffers are page-locked host memory.  ``index`` = (code
+    column, date column): the parser also builds the row-group index of the rows while it parses
+    them (:class:`RowIndex`, under ``ROW_INDEX``; absent when the rows are not (code, date)
+    sorted).
     """
     lib = _load_or_none()
     if lib is None:
@@ -142,8 +158,20 @@ def read_columns(path: str, types: dict, nthreads: int = 0, pinned: bool = False
         tl.append(t)
         dt = {1: "S16", 2: np.int32, 3: np.float32}.get(t, np.float64)
         bufs.append(_host_buffer(rows, dt, pinned))
-    got = lib.mfa_csv_parse(path.encode(), len(header), (C.c_int * len(tl))(*tl),
-                            (C.c_void_p * len(bufs))(*[b.ctypes.data for b in bufs]), nthreads)
+    t_arr = (C.c_int * len(tl))(*tl)
+    p_arr = (C.c_void_p * len(bufs))(*[b.ctypes.data for b in bufs])
+    if index is not None and index[0] in header and index[1] in header:
+        mask = np.zeros(int(lib.mfa_date_span()), np.uint8)
+        h = C.c_void_p()
+        got = lib.mfa_csv_parse_ix(path.encode(), len(header), t_arr, p_arr, nthreads,
+                                   header.index(index[0]), header.index(index[1]),
+                                   mask.ctypes.data, C.byref(h))
+        out = {n: b[:got] for n, b in zip(header, bufs)}
+        ix = _take_index(lib, h, mask, got)
+        if ix is not None:
+            out[ROW_INDEX] = ix
+        return out
+    got = lib.mfa_csv_parse(path.encode(), len(header), t_arr, p_arr, nthreads)
     return {n: b[:got] for n, b in zip(header, bufs)}
 
 
@@ -177,7 +205,58 @@ def write_matrix_csv(path: str, values: np.ndarray, row_labels, col_labels, inde
     return True
 
 
-DATE_BASE = 19000101  # csrc_host/shard_rows.cpp: bitmap span [19000101, 21000101)
+DATE_BASE = 19000101  # csrc_host/row_index.h: mask span [19000101, 21000101)
+ROW_INDEX = "__row_index__"   # key of the RowIndex in a loader's column dict
+
+
+class RowIndex:
+    """Row-group index of (code, date)-sorted loader rows (csrc_host/row_index.h):
+    ``seg_first`` [N] int64 first row of every stock (segment k = global stock id k, codes
+    ascending), ``dates`` [D] int32 the sorted distinct trade dates, ``rows`` the row count it
+    was built on (a column dict whose rows changed since no longer matches it)."""
+    __slots__ = ("seg_first", "dates", "rows")
+
+    def __init__(self, seg_first: np.ndarray, dates: np.ndarray, rows: int):
+        self.seg_first, self.dates, self.rows = seg_first, dates, int(rows)
+
+
+def _mask_dates(lib, mask: np.ndarray) -> np.ndarray:
+    n = int(lib.mfa_mask_dates(mask.ctypes.data, None, 0))
+    out = np.empty(n, np.int32)
+    lib.mfa_mask_dates(mask.ctypes.data, out.ctypes.data, n)
+    return out
+
+
+def _take_index(lib, h, mask, rows) -> RowIndex | None:
+    """RowIndex from a native index handle (freed here); None if the order check failed."""
+    if not h or not h.value:
+        return None
+    try:
+        n = int(lib.mfa_row_index_count(h))
+        if n < 0:
+            return None
+        seg_first = np.empty(n, np.int64)
+        lib.mfa_row_index_get(h, seg_first.ctypes.data)
+    finally:
+        lib.mfa_row_index_free(h)
+    return RowIndex(seg_first, _mask_dates(lib, mask), rows)
+
+
+def row_index(codes: np.ndarray, dates: np.ndarray, nthreads: int = 0) -> RowIndex | None:
+    """The row-group index of loader columns from a source other than the CSV reader (one
+    threaded pass over codes and dates); None when the rows are not grouped by code in ascending
+    order with strictly ascending dates per stock, a date is outside 1900-2100, or the native
+    library is missing."""
+    lib = _load_or_none()
+    if lib is None:
+        return None
+    c = np.ascontiguousarray(codes, dtype="S16")
+    d = np.ascontiguousarray(dates, dtype=np.int32)
+    if d.size == 0 or c.size != d.size:
+        return None
+    mask = np.zeros(int(lib.mfa_date_span()), np.uint8)
+    h = C.c_void_p(lib.mfa_row_index(c.ctypes.data, d.ctypes.data, d.size, mask.ctypes.data, nthreads))
+    return _take_index(lib, h, mask, d.size)
 
 
 def trade_dates(dates: np.ndarray, nthreads: int = 0) -> np.ndarray | None:
@@ -189,41 +268,40 @@ def trade_dates(dates: np.ndarray, nthreads: int = 0) -> np.ndarray | None:
     mask = np.zeros(int(lib.mfa_date_span()), np.uint8)
     if lib.mfa_date_mask(d.ctypes.data, d.size, mask.ctypes.data, nthreads) != 0:
         return None
-    return (np.flatnonzero(mask) + DATE_BASE).astype(np.int32)
+    return _mask_dates(lib, mask)
+
+
+def shard_rows_ix(ix: RowIndex, dates: np.ndarray, end_dates: np.ndarray | None, date_lo: int,
+                  date_hi: int, halo: int, nstmt: int = 4, nthreads: int = 0):
+    """One rank's rows of indexed loader rows: per stock, its rows with trade date in
+    [date_lo, date_hi), the ``halo`` rows before them and the statement rows of the ``nstmt``
+    most recent distinct end dates before them (csrc_host/shard_rows.cpp, binary searches per
+    stock).  Returns ``(ranges [n, 2] int64, seg_id [n] int32)``: the kept row ranges and the
+    global stock id of each."""
+    lib = _load()
+    d = np.ascontiguousarray(dates, dtype=np.int32)
+    e = None if end_dates is None else np.ascontiguousarray(end_dates, dtype=np.int32)
+    sf = np.ascontiguousarray(ix.seg_first, dtype=np.int64)
+    ns = sf.size
+    ranges = np.empty(2 * max(ns, 1), np.int64)
+    seg_id = np.empty(max(ns, 1), np.int32)
+    nr = int(lib.mfa_shard_rows_ix(sf.ctypes.data, ns, d.size, d.ctypes.data,
+                                   None if e is None else e.ctypes.data, int(date_lo), int(date_hi),
+                                   int(halo), int(nstmt), ranges.ctypes.data, seg_id.ctypes.data,
+                                   nthreads))
+    return ranges[:2 * nr].reshape(-1, 2), seg_id[:nr]
 
 
 def shard_rows(codes: np.ndarray, dates: np.ndarray, end_dates: np.ndarray | None,
                date_lo: int, date_hi: int, halo: int, nstmt: int = 4, nthreads: int = 0):
-    """One rank's rows of a (stock, date)-sorted loader: per stock, its rows with trade date in
-    [date_lo, date_hi), the ``halo`` rows before them and the statement rows of the ``nstmt``
-    most recent distinct end dates before them (csrc_host/shard_rows.cpp).
-
-    Returns ``(ranges [n, 2] int64, seg_id [n] int32, seg_first [N] int64)`` -- kept row ranges,
-    the global stock id (code rank) of each range, the first row of every stock -- or None
-    when the native library is missing or the rows are not sorted by (code, date)."""
-    lib = _load_or_none()
-    if lib is None:
+    """:func:`shard_rows_ix` on a fresh :func:`row_index` of the columns.  Returns ``(ranges,
+    seg_id, seg_first)``, or None when the native library is missing or the rows are not
+    sorted by (code, date)."""
+    ix = row_index(codes, dates, nthreads)
+    if ix is None:
         return None
-    c = np.ascontiguousarray(codes, dtype="S16")
-    d = np.ascontiguousarray(dates, dtype=np.int32)
-    e = None if end_dates is None else np.ascontiguousarray(end_dates, dtype=np.int32)
-    R = d.size
-    cap = 1 << 16
-    while True:
-        ranges = np.empty(2 * cap, np.int64)
-        seg_id = np.empty(cap, np.int32)
-        seg_first = np.empty(cap, np.int64)
-        nr, ns = C.c_int64(0), C.c_int64(0)
-        rc = lib.mfa_shard_rows(c.ctypes.data, d.ctypes.data, None if e is None else e.ctypes.data,
-                                R, int(date_lo), int(date_hi), int(halo), int(nstmt),
-                                ranges.ctypes.data, seg_id.ctypes.data, seg_first.ctypes.data,
-                                cap, C.byref(nr), C.byref(ns), nthreads)
-        if rc == -3 and cap < R + 1:
-            cap = min(4 * cap, R + 1)
-            continue
-        if rc != 0:
-            return None
-        return ranges[:2 * nr.value].reshape(-1, 2), seg_id[:nr.value], seg_first[:ns.value]
+    ranges, seg_id = shard_rows_ix(ix, dates, end_dates, date_lo, date_hi, halo, nstmt, nthreads)
+    return ranges, seg_id, ix.seg_first
 
 
 def gather_ranges(x: np.ndarray, ranges: np.ndarray, offs: np.ndarray, out: np.ndarray,

@@ -46,15 +46,17 @@ def tick(rec, name, t0):
     return time.perf_counter()
 
 
-for rep in range(3):
+for rep in range(4):
+    timing = rep == 3   # the last rep: device synchronised at every sub-step (breakdown only)
     for path in ("host", "full"):
-        rec = {"path": path, "rep": rep, "N": N, "T": T, "world": world, "rank": rank}
+        rec = {"path": path, "rep": rep, "synced_breakdown": timing, "N": N, "T": T, "world": world, "rank": rank}
         t00 = t = time.perf_counter()
         if path == "host":
-            sh = e2e.DeviceFactorEngine.from_host_shard(dict(p), dict(i), rank, world, dev, cfg)
+            sh = e2e.DeviceFactorEngine.from_host_shard(dict(p), dict(i), rank, world, dev, cfg,
+                                                        timing=timing)
             assert sh is not None
             t = tick(rec, "select_upload_build", t)
-            rec["host_times"] = {k: round(v, 4) for k, v in sh.host_times.items()}
+            rec["host_times"] = {k: round(v, 4) if isinstance(v, float) else v for k, v in sh.host_times.items()}
         else:
             full = e2e.DeviceFactorEngine(dict(p), dict(i), device=dev, config=cfg)
             t = tick(rec, "full_engine", t)
