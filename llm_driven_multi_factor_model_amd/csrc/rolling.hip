@@ -27,19 +27,43 @@ using namespace mfa;
 
 __device__ __forceinline__ bool fin(float v) { return __builtin_isfinite(v); }
 
+// The direct per-row kernels below (the reference kernels of the tests and the rank-invariant
+// path) stage the rows their 256-row block's windows read through LDS: the block loads its span
+// (255 + W rows, plus the lag) once, coalesced, and every row then sums its own window from LDS
+// in the same fixed order as the global-memory form -- bitwise the same outputs, W fewer L1 tap
+// loads per row.  Spans over kDirSpan rows read global memory as before.
+constexpr int kDirSpan = 1024;
+__device__ __forceinline__ void dir_stage(const float* __restrict__ x, int R, int base, int n,
+                                          float* sx) {
+  for (int k = threadIdx.x; k < n; k += 256) {
+    const int g = base + k;
+    sx[k] = (g >= 0 && g < R) ? x[g] : __builtin_nanf("");
+  }
+}
+
 __global__ __launch_bounds__(256) void beta_hsigma_kernel(const float* __restrict__ y,
                                                           const float* __restrict__ x,
                                                           const int* __restrict__ seg_lo, int R,
                                                           int W, double lam, int minp,
                                                           float* __restrict__ beta,
                                                           float* __restrict__ hsig) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ float sy[kDirSpan], sx[kDirSpan];
+  const int r0 = blockIdx.x * 256, base = r0 - W + 1, span = 255 + W;
+  const bool st = span <= kDirSpan;
+  if (st) {
+    dir_stage(y, R, base, span, sy);
+    dir_stage(x, R, base, span, sx);
+  }
+  __syncthreads();
+  const int r = r0 + threadIdx.x;
   if (r >= R) return;
+  auto Y = [&](int j) { return st ? sy[j - base] : y[j]; };
+  auto X = [&](int j) { return st ? sx[j - base] : x[j]; };
   const int lo = max(seg_lo[r], r - W + 1);
   double w = 1.0, Sw = 0, Sx = 0, Sy = 0, Sxx = 0, Sxy = 0;
   int n = 0;
   for (int j = r; j >= lo; --j) {
-    const float yv = y[j], xv = x[j];
+    const float yv = Y(j), xv = X(j);
     if (!(fin(yv) && fin(xv))) continue;
     const double xd = xv, yd = yv;
     Sw += w;
@@ -60,7 +84,7 @@ __global__ __launch_bounds__(256) void beta_hsigma_kernel(const float* __restric
     // residual sum of squares: second pass (exact, no cancellation)
     double ssr = 0.0, ww = 1.0;
     for (int j = r; j >= lo; --j) {
-      const float yv = y[j], xv = x[j];
+      const float yv = Y(j), xv = X(j);
       if (!(fin(yv) && fin(xv))) continue;
       const double e = (double)yv - aa - bb * (double)xv;
       ssr = fma(ww * e, e, ssr);
@@ -94,21 +118,45 @@ __global__ __launch_bounds__(256) void rstr_kernel(const float* __restrict__ lr,
                                                    int W, double lam, int minp,
                                                    float* __restrict__ out) {
   __shared__ double pw[kRsDirectTab];
+  __shared__ float sl[kDirSpan];
   const bool tab = W <= kRsDirectTab;
-  if (tab) {
+  if (tab)
     for (int k = threadIdx.x; k < W; k += blockDim.x) pw[k] = ipow(lam, k);
-    __syncthreads();
-  }
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  const int r0 = blockIdx.x * 256, base = r0 - W + 1 - L, span = 255 + W;
+  const bool st = span <= kDirSpan;
+  if (st) dir_stage(lr, R, base, span, sl);
+  __syncthreads();
+  const int r = r0 + threadIdx.x;
   if (r >= R) return;
   const int s0 = seg_lo[r];
   const int lo = max(s0, r - W + 1);
   // positional weight lam^(j - lo): oldest row of the (possibly partial) window gets 1
   double num[2] = {0.0, 0.0}, den[2] = {0.0, 0.0}, wj = 1.0;
   int n = 0;
-  for (int j = lo; j <= r; ++j) {
+  int j = lo;
+  if (st && tab) {
+    // 8 taps per step: their LDS loads issue together ahead of the (same-order) fma chain
+    for (; j + 8 <= r + 1; j += 8) {
+      float v[8];
+      double wk[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int src = j + u - L;
+        v[u] = src >= s0 ? sl[src - base] : qnanf();
+        wk[u] = pw[j + u - lo];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)  // j - lo is even here: tap u feeds accumulator u & 1
+        if (fin(v[u])) {
+          num[u & 1] = fma(wk[u], (double)v[u], num[u & 1]);
+          den[u & 1] += wk[u];
+          ++n;
+        }
+    }
+  }
+  for (; j <= r; ++j) {
     const int src = j - L, k = j - lo;
-    const float v = src >= s0 ? lr[src] : qnanf();
+    const float v = src >= s0 ? (st ? sl[src - base] : lr[src]) : qnanf();
     const double wk = tab ? pw[k] : wj;
     if (fin(v)) {
       num[k & 1] = fma(wk, (double)v, num[k & 1]);
@@ -125,13 +173,21 @@ __global__ __launch_bounds__(256) void dastd_kernel(const float* __restrict__ re
                                                     const int* __restrict__ seg_lo, int R, int W,
                                                     double lam, int minp,
                                                     float* __restrict__ out) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ float sa[kDirSpan], sb[kDirSpan];
+  const int r0 = blockIdx.x * 256, base = r0 - W + 1, span = 255 + W;
+  const bool st = span <= kDirSpan;
+  if (st) {
+    dir_stage(ret, R, base, span, sa);
+    dir_stage(mret, R, base, span, sb);
+  }
+  __syncthreads();
+  const int r = r0 + threadIdx.x;
   if (r >= R) return;
   const int lo = max(seg_lo[r], r - W + 1);
   double w = 1.0, Sw = 0.0, Sx = 0.0;
   int n = 0;
   for (int j = r; j >= lo; --j) {
-    const float a = ret[j], b = mret[j];
+    const float a = st ? sa[j - base] : ret[j], b = st ? sb[j - base] : mret[j];
     if (!(fin(a) && fin(b))) continue;
     const double e = (double)a - (double)b;
     Sw += w;
@@ -144,7 +200,7 @@ __global__ __launch_bounds__(256) void dastd_kernel(const float* __restrict__ re
     const double m = Sx / Sw;
     double v = 0.0, ww = 1.0;
     for (int j = r; j >= lo; --j) {
-      const float a = ret[j], b = mret[j];
+      const float a = st ? sa[j - base] : ret[j], b = st ? sb[j - base] : mret[j];
       if (!(fin(a) && fin(b))) continue;
       const double e = (double)a - (double)b - m;
       v = fma(ww * e, e, v);
@@ -158,7 +214,12 @@ __global__ __launch_bounds__(256) void dastd_kernel(const float* __restrict__ re
 __global__ __launch_bounds__(256) void cmra_kernel(const float* __restrict__ lr,
                                                    const int* __restrict__ seg_lo, int R, int W,
                                                    int partial, float* __restrict__ out) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ float sl[kDirSpan];
+  const int r0 = blockIdx.x * 256, base = r0 - W + 1, span = 255 + W;
+  const bool st = span <= kDirSpan;
+  if (st) dir_stage(lr, R, base, span, sl);
+  __syncthreads();
+  const int r = r0 + threadIdx.x;
   if (r >= R) return;
   const int s0 = seg_lo[r];
   float o = qnanf();
@@ -168,8 +229,25 @@ __global__ __launch_bounds__(256) void cmra_kernel(const float* __restrict__ lr,
     if (r - W + 1 >= s0) {
       double c = 0.0, cmax = -INFINITY, cmin = INFINITY;
       bool ok = true;
-      for (int j = r - W + 1; j <= r; ++j) {
-        const float v = lr[j];
+      int j = r - W + 1;
+      if (st) {
+        for (; j + 8 <= r + 1; j += 8) {  // 8 taps' LDS loads together, the same order
+          float v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = sl[j + u - base];
+          bool okb = true;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            okb = okb && fin(v[u]);
+            c += (double)v[u];
+            cmax = fmax(cmax, c);
+            cmin = fmin(cmin, c);
+          }
+          if (!okb) { ok = false; break; }
+        }
+      }
+      for (; ok && j <= r; ++j) {
+        const float v = st ? sl[j - base] : lr[j];
         if (!fin(v)) { ok = false; break; }
         c += (double)v;
         cmax = fmax(cmax, c);
@@ -182,7 +260,7 @@ __global__ __launch_bounds__(256) void cmra_kernel(const float* __restrict__ lr,
     double c = 0.0, cmax = -INFINITY, cmin = INFINITY;
     int n = 0;
     for (int j = lo; j <= r; ++j) {
-      const float v = lr[j];
+      const float v = st ? sl[j - base] : lr[j];
       if (!fin(v)) continue;
       c += (double)v;
       cmax = fmax(cmax, c);
@@ -199,13 +277,29 @@ __global__ __launch_bounds__(256) void rolling_sum_kernel(const float* __restric
                                                           const int* __restrict__ seg_lo, int R,
                                                           int W, int minp, double scale, int mode,
                                                           float* __restrict__ out) {
-  const int r = blockIdx.x * blockDim.x + threadIdx.x;
+  __shared__ float sx[kDirSpan];
+  const int r0 = blockIdx.x * 256, base = r0 - W + 1, span = 255 + W;
+  const bool st = span <= kDirSpan;
+  if (st) dir_stage(x, R, base, span, sx);
+  __syncthreads();
+  const int r = r0 + threadIdx.x;
   if (r >= R) return;
   const int lo = max(seg_lo[r], r - W + 1);
   double s = 0.0;
   int n = 0;
-  for (int j = r; j >= lo; --j) {
-    const float v = x[j];
+  int j = r;
+  if (st) {
+    for (; j - 8 >= lo - 1; j -= 8) {  // 8 taps' LDS loads together, the same summation order
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = sx[j - u - base];
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (fin(v[u])) { s += (double)v[u] * scale; ++n; }
+    }
+  }
+  for (; j >= lo; --j) {
+    const float v = st ? sx[j - base] : x[j];
     if (fin(v)) { s += (double)v * scale; ++n; }
   }
   float o = qnanf();

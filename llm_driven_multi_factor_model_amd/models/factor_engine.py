@@ -169,6 +169,14 @@ class FactorEngine:
             self._row_ord = ro
         return ro
 
+    def aligned_layout(self):
+        """The virtual row layout of the rank-invariant BETA / DASTD tiles
+        (:func:`ops.rolling.aligned_layout`), built once per engine."""
+        lay = getattr(self, "_aligned", None)
+        if lay is None:
+            lay = self._aligned = RL.aligned_layout(self.seg_lo, self.row_ord)
+        return lay
+
     def date_shard(self, lo: int, hi: int, halo: int | None = None) -> "FactorEngine":
         """Engine over the rows of dates [lo, hi) plus each stock's ``halo`` preceding rows.
 
@@ -225,6 +233,7 @@ class FactorEngine:
         sub.grid_idx = sub.date_id.long() * sub.N + sub.stock_id.long()
         sub.cols = {k: v[idx] for k, v in self.cols.items()}
         sub._row_ord = self.row_ord[idx]
+        sub._aligned = None
         ttm = getattr(self, "_ttm", None)
         sub._ttm = None if ttm is None else ttm[idx]
         sub.own = None
@@ -255,7 +264,7 @@ class FactorEngine:
         c = self.cfg
         b, h = RL.beta_hsigma(self.cols["ret"], self.cols["market_ret"], self.seg_lo, c.beta_window,
                               c.beta_half_life, c.beta_min_periods,
-                              row_ord=self.row_ord if self._direct() else None)
+                              row_ord=self.aligned_layout() if self._direct() else None)
         return {"BETA": b, "HSIGMA": h}
 
     def compute_rstr(self):
@@ -267,7 +276,7 @@ class FactorEngine:
         c = self.cfg
         return {"DASTD": RL.dastd(self.cols["ret"], self.cols["market_ret"], self.seg_lo, c.dastd_window,
                                   c.dastd_half_life, c.dastd_min_periods,
-                                  row_ord=self.row_ord if self._direct() else None)}
+                                  row_ord=self.aligned_layout() if self._direct() else None)}
 
     def compute_cmra(self):
         c = self.cfg

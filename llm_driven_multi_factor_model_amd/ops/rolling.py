@@ -34,7 +34,7 @@ ALIGN = 256      # rank-invariant EW kernels: tiles on global multiples of 256 r
 ALIGN_MAX_W = 255
 
 
-def _aligned_layout(seg_lo: torch.Tensor, row_ord: torch.Tensor):
+def aligned_layout(seg_lo: torch.Tensor, row_ord: torch.Tensor):
     """Virtual row layout of the rank-invariant EW kernels (csrc/rolling.hip,
     mfa_beta_hsigma_aligned): the rows of each stock at B_s + t - T0_s, t = ``row_ord`` (the
     row's ordinal in the stock's FULL history), T0_s = t_first rounded down to a multiple of
@@ -42,21 +42,30 @@ def _aligned_layout(seg_lo: torch.Tensor, row_ord: torch.Tensor):
     seg_v [Rv] int32 virtual seg_lo, Rv)."""
     dev = seg_lo.device
     R = seg_lo.numel()
-    r = torch.arange(R, device=dev, dtype=torch.int64)
     sl = seg_lo.long()
-    start = r == sl
-    sidx = torch.cumsum(start.to(torch.int64), 0) - 1
-    starts = torch.nonzero(start).flatten()
-    lens = torch.diff(starts, append=torch.tensor([R], device=dev))
-    t_first = row_ord.long()[starts]
-    T0 = torch.div(t_first, ALIGN, rounding_mode="floor") * ALIGN
-    padded = torch.div(t_first - T0 + lens + ALIGN - 1, ALIGN, rounding_mode="floor") * ALIGN
-    B = torch.cumsum(padded, 0) - padded
-    v = B[sidx] + (row_ord.long() - T0[sidx])
-    Rv = int(padded.sum())
+    ro = row_ord.long()
+    # per row: T0 of its stock (first row's ordinal rounded down to ALIGN); a stock's padded
+    # block count sits at its LAST row, so an exclusive prefix over rows gives, on every row of
+    # stock s, the blocks of the stocks before it (B_s / ALIGN) -- no per-stock compaction
+    T0 = torch.div(ro[sl], ALIGN, rounding_mode="floor") * ALIGN
+    last = torch.ones(R, dtype=torch.bool, device=dev)
+    if R > 1:
+        last[:-1] = sl[1:] != sl[:-1]
+    nb = torch.where(last, torch.div(ro - T0 + ALIGN, ALIGN, rounding_mode="floor"),
+                     torch.zeros((), dtype=torch.int64, device=dev))
+    cb = torch.cumsum(nb, 0) - nb
+    base = cb * ALIGN - T0
+    v = base + ro
+    Rv = int(cb[-1] + nb[-1]) * ALIGN   # the one host read
     seg_v = torch.arange(Rv, device=dev, dtype=torch.int32)   # padding rows: their own starts
-    seg_v[v] = (B + t_first - T0)[sidx].to(torch.int32)
+    seg_v[v] = (base + ro[sl]).to(torch.int32)
     return v, seg_v, Rv
+
+
+def _layout(seg_lo, row_ord):
+    """``row_ord`` is either the ordinals or an :func:`aligned_layout` built from them (an
+    engine builds it once for BETA and DASTD)."""
+    return tuple(row_ord) if isinstance(row_ord, tuple) else aligned_layout(seg_lo, row_ord)
 
 
 def _to_virtual(x: torch.Tensor, v: torch.Tensor, Rv: int) -> torch.Tensor:
@@ -136,14 +145,14 @@ def returns(close, seg_lo):
 
 # ---------------------------------------------------------------- BETA / HSIGMA
 def beta_hsigma(ret, mret, seg_lo, window=252, half_life=63.0, min_periods=42, row_ord=None):
-    """``row_ord`` (GPU, window <= 255): the rows' ordinals in their stocks' full histories --
-    the rank-invariant aligned-tile kernel on the virtual layout (a date shard reproduces the
-    full panel bit for bit)."""
+    """``row_ord`` (GPU, window <= 255): the rows' ordinals in their stocks' full histories (or
+    their :func:`aligned_layout`) -- the rank-invariant aligned-tile kernel on the virtual
+    layout (a date shard reproduces the full panel bit for bit)."""
     ret, mret, seg_lo = _f(ret), _f(mret), _i32(seg_lo)
     R = ret.numel()
     lam = 0.5 ** (1.0 / half_life)
     if ret.is_cuda and row_ord is not None and window <= ALIGN_MAX_W and R:
-        v, seg_v, Rv = _aligned_layout(seg_lo, row_ord)
+        v, seg_v, Rv = _layout(seg_lo, row_ord)
         bv = torch.empty(Rv, dtype=torch.float32, device=ret.device)
         hv = torch.empty_like(bv)
         # bound to names: a temporary passed as ptr(...) is freed before the launch, and the
@@ -210,7 +219,7 @@ def dastd(ret, mret, seg_lo, window=252, half_life=42.0, min_periods=42, row_ord
     R = ret.numel()
     lam = 0.5 ** (1.0 / half_life)
     if ret.is_cuda and row_ord is not None and window <= ALIGN_MAX_W and R:
-        v, seg_v, Rv = _aligned_layout(seg_lo, row_ord)
+        v, seg_v, Rv = _layout(seg_lo, row_ord)
         ov = torch.empty(Rv, dtype=torch.float32, device=ret.device)
         yv, xv = _to_virtual(ret, v, Rv), _to_virtual(mret, v, Rv)   # named: see beta_hsigma
         _native.call("mfa_dastd_aligned", _native.ptr(yv), _native.ptr(xv), _native.ptr(seg_v), Rv, window, lam,
