@@ -2860,8 +2860,9 @@ hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, 
                          stats, status, mom, okm);
   } else
 #endif  // MFA_AB
-  if (det && xs_plain_moments<T>(D)) {
-    // moments from plain vector loads (default for fp32 panels and small fp64 shards)
+  if (det && mode == 0 && xs_plain_moments<T>(D)) {
+    // moments from plain vector loads (default for fp32 panels and small fp64 shards; A/B mode 7
+    // forces the LDS-DMA ring below)
     hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR | 32 | 64, PRE, T>), dim3(D),
                        dim3(256), lds1, s, X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2,
                        stats, status, mom, okm);
