@@ -548,7 +548,9 @@ __global__ __launch_bounds__(NW * 64) void mc_bias_wide2_kernel(
   const double tnorm = fmax(fabs(gl), fabs(gu));
   const double pivmin = 2.2250738585072014e-308 * fmax(1.0, b2);
   constexpr double kEps = 2.220446049250313e-16;
-  const double abstol = 1e-22 * tnorm + pivmin;
+  // abl bit 8 (the F0 eigh knob mfa_eigen_wide_set_eig_abstol): LAPACK's absolute accuracy
+  // eps ||T|| for every eigenvalue instead of resolving the smallest ones to 1e-22 ||T||
+  const double abstol = ((abl & 256) ? kEps * tnorm : 1e-22 * tnorm) + pivmin;
   const int jt = K - 1 - i;
   double lo = gl - 2.0 * kEps * tnorm - pivmin, hi = gu + 2.0 * kEps * tnorm + pivmin;
   double x = row_ok ? fmin(fmax(gs[li], lo), hi) : 0.5 * (lo + hi);
@@ -602,7 +604,8 @@ __global__ __launch_bounds__(NW * 64) void mc_bias_wide2_kernel(
           st *= 8.0;
         }
         lag = __builtin_isfinite(xn) && xn >= lo && xn <= hi;
-        if (lag && prev == cnt && st <= 1e-8 * fabs(x) && st <= 0.25 * sprev) { x = xn; break; }
+        if (lag && prev == cnt && (st <= 1e-8 * fabs(x) || ((abl & 256) && st <= abstol)) &&
+            st <= 0.25 * sprev) { x = xn; break; }
         sprev = lag ? st : __builtin_inf();
       }
       if (!lag) { xn = 0.5 * (lo + hi); sprev = __builtin_inf(); }
@@ -977,6 +980,16 @@ __global__ __launch_bounds__(256) void eigh_wide_fix_kernel(const double* __rest
 // diagonally dominant (a Newey-West covariance), so the diagonal guesses are poorer than for
 // the bias problems S C_z S.
 int g_wide_eig_rounds = 0;
+// 1 (default) = LAPACK's absolute eigenvalue accuracy eps ||T|| for the F0 eigh; 0 = resolve the
+// smallest eigenvalues to 1e-22 ||T|| (round 4): K = 140 3.93 -> 1.24 ms, K = 80 2.31 -> 0.42 ms
+// for the risk model's 112 / 172 Newey-West covariances, the same errors against LAPACK
+// (profiles/r05/r05l)
+int g_wide_eig_abstol = 1;
+MFA_API int mfa_eigen_wide_set_eig_abstol(int on) {
+  if (on != 0 && on != 1) return (int)hipErrorInvalidValue;
+  g_wide_eig_abstol = on;
+  return 0;
+}
 MFA_API int mfa_eigen_wide_set_eig_rounds(int r) {
   if (r < 0 || r > 7) return (int)hipErrorInvalidValue;
   g_wide_eig_rounds = r;
@@ -993,14 +1006,16 @@ MFA_API int mfa_eigh_wide_fix(const double* A, int B, int K, double tol, double*
     (void)hipFuncSetAttribute((const void*)mc_bias_wide2_kernel<96, 3, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL((mc_bias_wide2_kernel<96, 3, true>), dim3(B), dim3(3 * 64), lds, s, A, K, 1,
-                       (const double*)nullptr, (const int*)nullptr, w, g_wide_eig_rounds << 4, U);
+                       (const double*)nullptr, (const int*)nullptr, w,
+                       (g_wide_eig_rounds << 4) | (g_wide_eig_abstol << 8), U);
     hipLaunchKernelGGL(eigh_wide_fix_kernel<96>, dim3(B), dim3(256), 0, s, A, K, tol, w, U, ws, fixed);
   } else {
     const size_t lds = bias_wide2_lds(K, 144, 5);
     (void)hipFuncSetAttribute((const void*)mc_bias_wide2_kernel<144, 5, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     hipLaunchKernelGGL((mc_bias_wide2_kernel<144, 5, true>), dim3(B), dim3(5 * 64), lds, s, A, K, 1,
-                       (const double*)nullptr, (const int*)nullptr, w, g_wide_eig_rounds << 4, U);
+                       (const double*)nullptr, (const int*)nullptr, w,
+                       (g_wide_eig_rounds << 4) | (g_wide_eig_abstol << 8), U);
     hipLaunchKernelGGL(eigh_wide_fix_kernel<144>, dim3(B), dim3(256), 0, s, A, K, tol, w, U, ws, fixed);
   }
   return (int)hipGetLastError();

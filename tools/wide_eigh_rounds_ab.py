@@ -4,6 +4,10 @@ P = K - 17 industries / Q = 16 styles panel.  Interleaved rounds; per setting th
 max relative eigenvalue difference to LAPACK (CPU) on the finite dates.
 
     python tools/wide_eigh_rounds_ab.py        # env: K=140 D=504 ROUNDS_LIST=0,1,2,3,4
+    ABSTOL=1 ROUNDS_LIST=0 ...                  # settings = abstol on/off (rounds fixed)
+
+With ABSTOL=1 the settings are mfa_eigen_wide_set_eig_abstol(0 / 1) (LAPACK-style absolute
+eigenvalue accuracy eps ||T||) and the report adds the max error relative to ||F||.
 """
 import json
 import os
@@ -21,7 +25,12 @@ from llm_driven_multi_factor_model_amd.utils.config import preset  # noqa: E402
 dev = torch.device("cuda:0")
 K = int(os.environ.get("K", "140"))
 D = int(os.environ.get("D", "504"))
-settings = [int(r) for r in os.environ.get("ROUNDS_LIST", "0,1,2,3,4").split(",")]
+ABS = os.environ.get("ABSTOL") == "1"
+settings = [0, 1] if ABS else [int(r) for r in os.environ.get("ROUNDS_LIST", "0,1,2,3,4").split(",")]
+
+
+def knob(lib, r):
+    return lib.mfa_eigen_wide_set_eig_abstol(r) if ABS else lib.mfa_eigen_wide_set_eig_rounds(r)
 p = synthetic_panel(D, 5000, K - 17, 16, seed=3, missing_frac=0.01, dtype=torch.float64, device=dev)
 m = RiskModel(p, preset("reference"))
 m.regress()
@@ -34,12 +43,12 @@ e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=Tr
 ts, ws = {r: [] for r in settings}, {}
 try:
     for r in settings:
-        assert lib.mfa_eigen_wide_set_eig_rounds(r) == 0
+        assert knob(lib, r) == 0
         ws[r] = eigen.eigh(Fv)[0]
     for rd in range(3):
         rec = {"round": rd}
         for r in settings:
-            lib.mfa_eigen_wide_set_eig_rounds(r)
+            knob(lib, r)
             torch.cuda.synchronize()
             e0.record()
             eigen.eigh(Fv)
@@ -50,9 +59,12 @@ try:
         print(json.dumps(rec), flush=True)
 finally:
     lib.mfa_eigen_wide_set_eig_rounds(0)
+    lib.mfa_eigen_wide_set_eig_abstol(0)
 ref = torch.linalg.eigvalsh(Fv.cpu()).flip(-1)
-out = {"K": K, "matrices": int(Fv.shape[0])}
+out = {"K": K, "matrices": int(Fv.shape[0]), "knob": "abstol" if ABS else "rounds"}
+nrm = ref.abs().amax(-1, keepdim=True)
 for r in settings:
     out[f"rounds{r}_min_ms"] = round(min(ts[r]), 3)
     out[f"rounds{r}_max_rel_vs_lapack"] = float(((ws[r].cpu() - ref).abs() / ref.abs().clamp_min(1e-300)).max())
+    out[f"rounds{r}_max_err_over_norm"] = float(((ws[r].cpu() - ref).abs() / nrm).max())
 print(json.dumps(out), flush=True)
