@@ -1293,11 +1293,13 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
   const double tnorm = fmax(fabs(gl), fabs(gu));
   const double pivmin = 2.2250738585072014e-308 * fmax(1.0, wave_max(b2max));
   constexpr double kEps = 2.220446049250313e-16;
-  // EIG (the F0 eigh): LAPACK's absolute accuracy eps ||T|| -- resolving the smallest eigenvalues
-  // of a Newey-West covariance to 1e-22 ||T|| by bisection cost 2-6x the solve and changed no
-  // result beyond LAPACK's own eps ||T|| (profiles/r05/r05l).  The bias problems keep 1e-22: their
-  // ratios divide by the eigenvalue.
-  const double abstol = (EIG ? kEps * tnorm : 1e-22 * tnorm) + pivmin;
+  // LAPACK's absolute eigenvalue accuracy eps ||T|| (dstebz's default), not 1e-22 ||T||: the
+  // smallest eigenvalues sit below what the fp64 Sturm recurrences resolve, so the extra
+  // accuracy was bought with bisection steps on one lane that the whole wave waited for.  F0
+  // eigh 0.86 -> 0.34 ms at K = 42, 4.0 -> 0.95 ms at K = 140 (same errors against LAPACK,
+  // profiles/r05/r05l, r05m); bias problems 12.54 -> 11.99 ms at 2520 x 100, ratios within
+  // 8.7e-16 of the 1e-22 setting and 5.9e-15 of LAPACK (r05n)
+  const double abstol = kEps * tnorm + pivmin;
   const int jt = K - 1 - lane;
   double lo = gl - 2.0 * kEps * tnorm - pivmin, hi = gu + 2.0 * kEps * tnorm + pivmin;
   double x = lane < K ? fmin(fmax(gs[lane], lo), hi) : 0.5 * (lo + hi);
@@ -1334,7 +1336,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
           st *= 8.0;
         }
         lag = __builtin_isfinite(xn) && xn >= lo && xn <= hi;
-        if (lag && prev == cnt && (st <= kAccTol * fabs(x) || (EIG && st <= abstol)) &&
+        if (lag && prev == cnt && (st <= kAccTol * fabs(x) || st <= abstol) &&
             st <= 0.25 * sprev) { x = xn; break; }
         sprev = lag ? st : __builtin_inf();
       }

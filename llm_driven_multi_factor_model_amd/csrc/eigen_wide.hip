@@ -185,7 +185,7 @@ mc_bias_wide_kernel(const double* __restrict__ D0, int K, int M, const double* _
   const double tnorm = fmax(fabs(gl), fabs(gu));
   const double pivmin = 2.2250738585072014e-308 * fmax(1.0, b2);
   constexpr double kEps = 2.220446049250313e-16;
-  const double abstol = 1e-22 * tnorm + pivmin;
+  const double abstol = kEps * tnorm + pivmin;  // LAPACK's accuracy (eigen.hip, mode 5)
   const int jt = K - 1 - t;
   double lo = gl - 2.0 * kEps * tnorm - pivmin, hi = gu + 2.0 * kEps * tnorm + pivmin;
   double x = t < K ? fmin(fmax(gs[t], lo), hi) : 0.5 * (lo + hi);
@@ -238,7 +238,10 @@ mc_bias_wide_kernel(const double* __restrict__ D0, int K, int M, const double* _
           st *= 8.0;
         }
         lag = __builtin_isfinite(xn) && xn >= lo && xn <= hi;
-        if (lag && prev == cnt && st <= 1e-8 * fabs(x) && st <= 0.25 * sprev) { x = xn; break; }
+        if (lag && prev == cnt && (st <= 1e-8 * fabs(x) || st <= abstol) && st <= 0.25 * sprev) {
+          x = xn;
+          break;
+        }
         sprev = lag ? st : __builtin_inf();
       }
       if (!lag) { xn = 0.5 * (lo + hi); sprev = __builtin_inf(); }
@@ -548,9 +551,9 @@ __global__ __launch_bounds__(NW * 64) void mc_bias_wide2_kernel(
   const double tnorm = fmax(fabs(gl), fabs(gu));
   const double pivmin = 2.2250738585072014e-308 * fmax(1.0, b2);
   constexpr double kEps = 2.220446049250313e-16;
-  // abl bit 8 (the F0 eigh knob mfa_eigen_wide_set_eig_abstol): LAPACK's absolute accuracy
-  // eps ||T|| for every eigenvalue instead of resolving the smallest ones to 1e-22 ||T||
-  const double abstol = ((abl & 256) ? kEps * tnorm : 1e-22 * tnorm) + pivmin;
+  // LAPACK's absolute eigenvalue accuracy eps ||T|| (eigen.hip, mode 5); abl bit 8 clear on
+  // the F0 eigh (mfa_eigen_wide_set_eig_abstol(0), A/B) restores round 4's 1e-22 ||T||
+  const double abstol = ((EIG && !(abl & 256)) ? 1e-22 * tnorm : kEps * tnorm) + pivmin;
   const int jt = K - 1 - i;
   double lo = gl - 2.0 * kEps * tnorm - pivmin, hi = gu + 2.0 * kEps * tnorm + pivmin;
   double x = row_ok ? fmin(fmax(gs[li], lo), hi) : 0.5 * (lo + hi);
@@ -604,7 +607,7 @@ __global__ __launch_bounds__(NW * 64) void mc_bias_wide2_kernel(
           st *= 8.0;
         }
         lag = __builtin_isfinite(xn) && xn >= lo && xn <= hi;
-        if (lag && prev == cnt && (st <= 1e-8 * fabs(x) || ((abl & 256) && st <= abstol)) &&
+        if (lag && prev == cnt && (st <= 1e-8 * fabs(x) || ((!EIG || (abl & 256)) && st <= abstol)) &&
             st <= 0.25 * sprev) { x = xn; break; }
         sprev = lag ? st : __builtin_inf();
       }
