@@ -1071,7 +1071,7 @@ size_t bias_tri_lds(int K, int KP) { return ((size_t)K * (KP + 1) + 7 * 64 + 2) 
 #define MFA_TRI2_WPE 3
 #endif
 // (lds_batch, tri2_rows_doubles / tri2_row_off: csrc/tridiag.h)
-// ABL: timing-only ablations (bias modes 61..67 = 60 + ABL, division-free Sturm, KP = 44):
+// ABL: timing-only ablations (bias modes 61..67 = 60 + ABL, the production mode-5 kernel, KP = 44):
 // 1 = no Laguerre iterations, 2 = no eigenvector / back-transform, 4 = no tridiagonalisation;
 // outputs meaningless.
 // EIG: batched symmetric eigendecomposition with the same machinery (eigh of F0): D0 = the input
@@ -2270,8 +2270,10 @@ bool launch_bias_tri_ab(const double* D0, int D, int K, int M, const double* Cz,
     const int abl = g_bias_mode - 60;
 #define MFA_TRI2_ABL(A_)                                                                     \
     if (abl == A_)                                                                         \
-      hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, A_>), dim3(D * M), dim3(64),       \
-                         bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D, 0);
+      hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, A_, MFA_TRI2_WPE, false, 8, 8, 2, true, \
+                                              false, true>),                                \
+                         dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, \
+                         ws, nullptr, nullptr, D, 0);
     MFA_TRI2_ABL(1) MFA_TRI2_ABL(2) MFA_TRI2_ABL(3) MFA_TRI2_ABL(4) MFA_TRI2_ABL(5)
     MFA_TRI2_ABL(6) MFA_TRI2_ABL(7)
 #undef MFA_TRI2_ABL
