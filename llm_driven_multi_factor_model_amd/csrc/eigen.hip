@@ -1322,6 +1322,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
   }
   double lam = x;
   constexpr double kAccTol = ACC == 9 ? 1e-9 : (ACC == 8 ? 1e-8 : (ACC == 7 ? 1e-7 : 1e-5));
+  int nit = 0;  // Sturm evaluations after the first (ABL & 32: the diagnostic output)
   if (lane < K && (ABL & 1) == 0) {
     int prev = -1;
     double sprev = __builtin_inf();
@@ -1345,12 +1346,17 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
       prev = lag ? cnt : -1;
       x = xn;
       cnt = sturm(x);
+      ++nit;
       if (cnt <= jt) lo = x; else hi = x;
     }
     lam = x;
   }
   lam_prev = lam;
   warm = true;
+  if constexpr ((ABL & 32) != 0) {  // diagnostic (A/B mode 68): each rank's Sturm evaluations
+    if (lane < K) vo[lane] = (double)(nit + 1);
+    return;
+  }
   if constexpr ((ABL & 2) != 0) {  // ablation: no eigenvectors / back-transform
     if (lane < K) vo[lane] = lam;
     return;
@@ -2266,8 +2272,8 @@ bool launch_bias_tri_ab(const double* D0, int D, int K, int M, const double* Cz,
                          bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D, 0);
     return true;
   }
-  if (g_bias_mode > 60 && g_bias_mode < 68 && K <= 44) {  // timing-only ablations of mode 5
-    const int abl = g_bias_mode - 60;
+  if (g_bias_mode > 60 && g_bias_mode < 69 && K <= 44) {  // timing-only ablations of mode 5
+    const int abl = g_bias_mode == 68 ? 32 : g_bias_mode - 60;  // 68: Sturm-evaluation counts
 #define MFA_TRI2_ABL(A_)                                                                     \
     if (abl == A_)                                                                         \
       hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, A_, MFA_TRI2_WPE, false, 8, 8, 2, true, \
@@ -2275,7 +2281,7 @@ bool launch_bias_tri_ab(const double* D0, int D, int K, int M, const double* Cz,
                          dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, \
                          ws, nullptr, nullptr, D, 0);
     MFA_TRI2_ABL(1) MFA_TRI2_ABL(2) MFA_TRI2_ABL(3) MFA_TRI2_ABL(4) MFA_TRI2_ABL(5)
-    MFA_TRI2_ABL(6) MFA_TRI2_ABL(7)
+    MFA_TRI2_ABL(6) MFA_TRI2_ABL(7) MFA_TRI2_ABL(32)
 #undef MFA_TRI2_ABL
     return true;
   }
