@@ -30,6 +30,7 @@ import pandas as pd
 import torch
 
 from ..ops import rolling as RL
+from ..ops import xs_reduce as XR
 from ..utils.config import FactorConfig, RiskConfig
 from .factor_engine import (BARRA_OUTPUT_COLUMNS, BARRA_RENAME, FACTORS_TO_RUN, FactorEngine,
                             next_return, postprocess_columns)
@@ -501,9 +502,13 @@ def risk_panel(eng: FactorEngine, cols: dict, l1_stock: np.ndarray, info: pd.Dat
     if missing:
         raise ValueError(f"exposure columns missing for the risk panel: {missing}")
     codes = info["code"].astype(str).to_numpy()
-    cpos = {c: i for i, c in enumerate(codes)}
-    ind_stock = np.array([cpos.get(str(x), -1) if isinstance(x, str) else -1 for x in l1_stock],
-                         dtype=np.int64)
+    cidx = pd.Index(codes)
+    if cidx.is_unique:  # l1_stock holds str codes or NaN (no membership: never a match)
+        ind_stock = cidx.get_indexer(pd.Index(l1_stock, dtype=object)).astype(np.int64)
+    else:  # a code listed twice in info: the last row wins, as a dict would
+        cpos = {c: i for i, c in enumerate(codes)}
+        ind_stock = np.array([cpos.get(str(x), -1) if isinstance(x, str) else -1 for x in l1_stock],
+                             dtype=np.int64)
     ind_row = torch.from_numpy(ind_stock).to(dev)[eng.stock_id.long()]
     keep = ind_row >= 0
     for c in ["capital", "ret", *STYLE_COLUMNS]:
@@ -528,15 +533,17 @@ def risk_panel(eng: FactorEngine, cols: dict, l1_stock: np.ndarray, info: pd.Dat
     flat = d_r * Np + s_r
     Q = len(STYLE_COLUMNS)
     nan = float("nan")
-    cap = torch.full((Dp * Np,), nan, dtype=dtype, device=dev)
-    ret = torch.full((Dp * Np,), nan, dtype=dtype, device=dev)
-    cap[flat] = cols["capital"][rows].to(dtype)
-    ret[flat] = cols["ret"][rows].to(dtype)
+    # the kept rows of every column onto the panel grids in two LDS-tiled transposes
+    # (ops.xs_reduce.GridMap: the kept rows are still sorted by (stock, date)): capital + ret
+    # onto [2, Dp * Np], the styles onto [Dp, Q, Np] (style q of cell (d, s) at
+    # d * Q * Np + q * Np + s: column stride Np, date stride Q * Np)
+    gm = XR.GridMap(s_r, d_r, Dp, Np)
+    Xk = torch.stack([cols[c].to(dtype) for c in ["capital", "ret", *STYLE_COLUMNS]])[:, rows]
+    cr = gm.scatter(Xk[:2].contiguous())
+    cap, ret = cr[0], cr[1]
     sty = torch.full((Dp, Q, Np), nan, dtype=dtype, device=dev)
-    sflat = d_r * (Q * Np) + s_r
-    sv = sty.view(-1)
-    for q, c in enumerate(STYLE_COLUMNS):
-        sv[sflat + q * Np] = cols[c][rows].to(dtype)
+    if Q:
+        gm.scatter(Xk[2:].contiguous(), out=sty.view(-1), gs=Np, ds=Q * Np)
     ind = torch.full((Dp * Np,), -1, dtype=torch.int16, device=dev)
     ind[flat] = ind_row[rows].to(torch.int16)
     dmask, smask = dk.cpu().numpy(), sk.cpu().numpy()

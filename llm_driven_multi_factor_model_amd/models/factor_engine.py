@@ -169,6 +169,13 @@ class FactorEngine:
             self._row_ord = ro
         return ro
 
+    def grid_map(self) -> "XR.GridMap":
+        """Rows <-> the (date, stock) grid as an LDS-tiled transpose (built once per engine)."""
+        gm = getattr(self, "_grid_map", None)
+        if gm is None:
+            gm = self._grid_map = XR.GridMap(self.stock_id, self.date_id, self.D, self.N)
+        return gm
+
     def aligned_layout(self):
         """The virtual row layout of the rank-invariant BETA / DASTD tiles
         (:func:`ops.rolling.aligned_layout`), built once per engine."""
@@ -234,6 +241,7 @@ class FactorEngine:
         sub.cols = {k: v[idx] for k, v in self.cols.items()}
         sub._row_ord = self.row_ord[idx]
         sub._aligned = None
+        sub._grid_map = None
         ttm = getattr(self, "_ttm", None)
         sub._ttm = None if ttm is None else ttm[idx]
         sub.own = None
@@ -599,18 +607,23 @@ def postprocess_columns(eng: "FactorEngine", res: dict, cfg: FactorConfig) -> di
     D, N, idx = eng.D, eng.N, eng.grid_idx
 
     def put(x):
-        g = torch.full((D * N,), nan, dtype=torch.float32, device=dev)
-        g[idx] = x.to(torch.float32)
-        return g.view(D, N)
+        return eng.grid_map().scatter(x.to(torch.float32)[None])[0].view(D, N)
 
     def take(g):
-        return g.reshape(-1)[idx]
+        return eng.grid_map().gather(g.contiguous(), 1)[0]
 
     col = {"ret": eng.cols["ret"],
            "circ_mv": eng.cols["circ_mv"] if "circ_mv" in eng.cols else torch.full((eng.R,), nan, device=dev)}
     col.update(res)
-    for f in list(col):  # winsorize every non-key column (incl. ret, circ_mv: quirk Q23)
-        col[f] = take(XR.winsorize(put(col[f]), cfg.winsor_n_std))
+    # winsorize every non-key column (incl. ret, circ_mv: quirk Q23): all columns scattered onto
+    # their (date, stock) grids in one launch, one per-date winsorize over the [C * D, N] stack,
+    # one gather back
+    names = list(col)
+    gm = eng.grid_map()
+    X = torch.stack([col[f].to(torch.float32) for f in names])
+    G = XR.winsorize_(gm.scatter(X).view(len(names) * D, N), cfg.winsor_n_std)
+    Xw = gm.gather(G, len(names))
+    col = {f: Xw[k] for k, f in enumerate(names)}
     for new, cc in cfg.composite.items():
         xs, ws = [], []
         for c, w in zip(cc["components"], cc["weights"]):

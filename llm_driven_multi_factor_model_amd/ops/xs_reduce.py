@@ -29,6 +29,13 @@ _native.register("mfa_style_norm", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.
                                      C.c_void_p, C.c_void_p])
 _native.register("mfa_bayes_shrink", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_double,
                                        C.c_void_p, C.c_void_p, C.c_void_p])
+_native.register("mfa_scatter_cols", [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int, C.c_int,
+                                      C.c_void_p, C.c_int64, C.c_void_p])
+_native.register("mfa_gather_cols", [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int, C.c_int,
+                                     C.c_void_p, C.c_int64, C.c_void_p])
+_native.register("mfa_rows_grid", [C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
+                                   C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_int64,
+                                   C.c_double, C.c_void_p])
 _native.register("mfa_bayes_shrink_presorted", [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int, C.c_int,
                                                  C.c_int, C.c_double, C.c_void_p, C.c_void_p,
                                                  C.c_void_p])
@@ -48,6 +55,118 @@ def winsorize(x: torch.Tensor, n_std: float = 2.5) -> torch.Tensor:
     _native.call("mfa_winsorize", _native.ptr(y), y.shape[0], y.shape[1], float(n_std),
                  _native.stream(y.device))
     return y.reshape(shp)
+
+
+def winsorize_(x: torch.Tensor, n_std: float = 2.5) -> torch.Tensor:
+    """:func:`winsorize` in place on a contiguous float32 tensor (rows = dates); returns it."""
+    if x.dtype != torch.float32 or not x.is_contiguous():
+        raise ValueError("winsorize_: contiguous float32 tensor")
+    y = x.view(-1, x.shape[-1])
+    if not y.is_cuda:
+        y.copy_(_winsorize_ref(y, n_std))
+        return x
+    _native.call("mfa_winsorize", _native.ptr(y), y.shape[0], y.shape[1], float(n_std),
+                 _native.stream(y.device))
+    return x
+
+
+# ------------------------------------------------------------------ rows <-> (date, stock) grid
+def scatter_cols(X: torch.Tensor, idx: torch.Tensor, cells: int, fill: float = float("nan"),
+                 out: torch.Tensor | None = None) -> torch.Tensor:
+    """``G[c, idx[r]] = X[c, r]`` for C columns at once (``csrc/gather.hip``: one launch, a plain
+    1:1 copy, no index sort); ``G`` [C, cells] is ``fill`` elsewhere (or ``out``, written in
+    place).  ``idx`` int64 [R], distinct cells."""
+    X = X.contiguous()
+    Cn, R = X.shape
+    G = out if out is not None else torch.full((Cn, cells), fill, dtype=X.dtype, device=X.device)
+    if not X.is_cuda:
+        G[:, idx] = X
+        return G
+    ix = idx.to(torch.int64).contiguous()
+    _native.call("mfa_scatter_cols", _native.ptr(X), R, _native.ptr(ix), R, Cn, X.element_size(),
+                 _native.ptr(G), G.stride(0), _native.stream(X.device))
+    return G
+
+
+def gather_cols(G: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
+    """``X[c, r] = G[c, idx[r]]`` for C columns at once (the inverse of :func:`scatter_cols`)."""
+    G = G.contiguous()
+    Cn = G.shape[0]
+    if not G.is_cuda:
+        return G[:, idx]
+    ix = idx.to(torch.int64).contiguous()
+    R = ix.numel()
+    X = torch.empty(Cn, R, dtype=G.dtype, device=G.device)
+    _native.call("mfa_gather_cols", _native.ptr(G), G.stride(0), _native.ptr(ix), R, Cn,
+                 G.element_size(), _native.ptr(X), R, _native.stream(G.device))
+    return X
+
+
+class GridMap:
+    """Rows sorted by (stock, date) <-> a date-major [Dg, Ng] grid, as an LDS-tiled transpose
+    (``csrc/gather.hip``, ``mfa_rows_grid``: 64-date x 64-stock tiles, coalesced on both
+    sides).  ``sid`` / ``did`` [R]: each row's stock (< Ng) and date (< Dg), (sid, did) strictly
+    increasing.  ``toff`` [Ng, ceil(Dg / 64) + 1]: the first row of every (stock, 64-date
+    block), from the sorted key."""
+
+    def __init__(self, sid: torch.Tensor, did: torch.Tensor, Dg: int, Ng: int):
+        dev = sid.device
+        key = sid.to(torch.int64) * Dg + did.to(torch.int64)
+        ntb = (Dg + 63) // 64
+        edges = torch.clamp(torch.arange(ntb + 1, device=dev, dtype=torch.int64) * 64, max=Dg)
+        q = torch.arange(Ng, device=dev, dtype=torch.int64)[:, None] * Dg + edges[None, :]
+        self.toff = torch.searchsorted(key, q.reshape(-1)).contiguous()
+        self.did = did.to(torch.int32).contiguous()
+        self.idx = did.to(torch.int64) * Ng + sid.to(torch.int64)   # flat cell (CPU path)
+        self.Dg, self.Ng, self.R = int(Dg), int(Ng), int(sid.numel())
+
+    def _cells(self, ds: int) -> torch.Tensor:
+        return torch.div(self.idx, self.Ng, rounding_mode="floor") * ds + self.idx % self.Ng
+
+    def scatter(self, X: torch.Tensor, fill: float = float("nan"), out: torch.Tensor | None = None,
+                gs: int | None = None, ds: int | None = None) -> torch.Tensor:
+        """``X`` [C, R] (float32 or float64) -> grids: cell (c, d, s) at ``c * gs + d * ds + s``
+        of ``out`` (contiguous, written in place), default a new [C, Dg * Ng] tensor with
+        ``fill`` in the cells without a row."""
+        if X.dtype not in (torch.float32, torch.float64):
+            X = X.to(torch.float32)
+        X = X.contiguous()
+        Cn = X.shape[0]
+        gs = self.Dg * self.Ng if gs is None else gs
+        ds = self.Ng if ds is None else ds
+        G = out if out is not None else torch.full((Cn, self.Dg * self.Ng), fill, dtype=X.dtype,
+                                                   device=X.device)
+        if G.dtype != X.dtype or not G.is_contiguous():
+            raise ValueError("GridMap.scatter: contiguous grids of the rows' dtype")
+        if not X.is_cuda or self.R == 0:
+            cell = self._cells(ds)
+            flat = G.view(-1)
+            for c in range(Cn):
+                flat[c * gs + cell] = X[c]
+            return G
+        _native.call("mfa_rows_grid", 1, X.element_size(), _native.ptr(X), X.stride(0),
+                     _native.ptr(self.did), _native.ptr(self.toff), self.Dg, self.Ng, Cn,
+                     _native.ptr(G), gs, ds, float(fill), _native.stream(X.device))
+        return G
+
+    def gather(self, G: torch.Tensor, C: int, gs: int | None = None,
+               ds: int | None = None) -> torch.Tensor:
+        """The inverse: C grids of ``G`` (same layout, contiguous) -> [C, R] of G's dtype."""
+        gs = self.Dg * self.Ng if gs is None else gs
+        ds = self.Ng if ds is None else ds
+        if not G.is_contiguous():
+            raise ValueError("GridMap.gather: contiguous grids")
+        X = torch.empty(C, self.R, dtype=G.dtype, device=G.device)
+        if not G.is_cuda or self.R == 0:
+            cell = self._cells(ds)
+            flat = G.reshape(-1)
+            for c in range(C):
+                X[c] = flat[c * gs + cell]
+            return X
+        _native.call("mfa_rows_grid", 0, G.element_size(), _native.ptr(X), X.stride(0),
+                     _native.ptr(self.did), _native.ptr(self.toff), self.Dg, self.Ng, C,
+                     _native.ptr(G), gs, ds, 0.0, _native.stream(G.device))
+        return X
 
 
 def _winsorize_ref(y: torch.Tensor, n_std: float) -> torch.Tensor:

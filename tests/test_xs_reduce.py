@@ -113,3 +113,35 @@ def test_hip_bayes_shrink_all_nan_date(cuda):
     got = R.bayes_shrink(vol.to(cuda), cap.to(cuda)).cpu()
     assert torch.isnan(got[0]).all()
     torch.testing.assert_close(got[1:], R.bayes_shrink(vol, cap)[1:], rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+def test_grid_map_transpose_equals_index_scatter(cuda, dtype):
+    """GridMap (csrc/gather.hip, LDS-tiled rows <-> grid transpose): on ragged (stock, date)
+    rows -- stocks with gaps, a stock with one row, grid edges not multiples of 64 -- the
+    scatter equals an index scatter bitwise (NaN in empty cells), a strided layout (column
+    stride / date stride of a [D, Q, N] panel) lands every value where the index formula says,
+    and the gather inverts the scatter."""
+    from llm_driven_multi_factor_model_amd.ops import xs_reduce as XR
+    g = torch.Generator().manual_seed(5)
+    Dg, Ng, C = 203, 131, 3
+    keep = torch.rand(Ng, Dg, generator=g) < 0.8
+    keep[7] = False
+    keep[7, 100] = True
+    sid, did = torch.nonzero(keep, as_tuple=True)          # sorted by (stock, date)
+    R = sid.numel()
+    X = torch.randn(C, R, generator=g, dtype=torch.float64).to(dtype)
+    gm = XR.GridMap(sid.to(cuda), did.to(cuda), Dg, Ng)
+    G = gm.scatter(X.to(cuda))
+    ref = torch.full((C, Dg * Ng), float("nan"), dtype=dtype)
+    ref[:, did * Ng + sid] = X
+    assert torch.equal(G.cpu().nan_to_num(7.0), ref.nan_to_num(7.0))
+    assert torch.equal(gm.gather(G, C).cpu(), X)
+    Q = C
+    P = torch.full((Dg, Q, Ng), float("nan"), dtype=dtype, device=cuda)
+    gm.scatter(X.to(cuda), out=P.view(-1), gs=Ng, ds=Q * Ng)
+    for q in range(Q):
+        assert torch.equal(P[did, q, sid].cpu(), X[q])
+    assert int(torch.isfinite(P).sum()) == C * R
+    assert torch.equal(gm.gather(P.view(-1), C, gs=Ng, ds=Q * Ng).cpu(), X)
