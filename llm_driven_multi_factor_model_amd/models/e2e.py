@@ -150,6 +150,11 @@ class DeviceFactorEngine(FactorEngine):
         self.own = None
 
     def _prepare_arrays(self, prices: dict, index: dict) -> None:
+        from ..utils import native_io
+        ix = prices.get(native_io.ROW_INDEX)
+        if ix is not None and ix.rows == len(prices["ts_code"]) and ix.seg_first.size:
+            self._prepare_indexed(prices, index, ix)
+            return
         dev = self.device
         # every host -> device copy is issued first (asynchronous from the reader's pinned
         # buffers), in the dtype the reader produced: float32 loader columns (the reference's
@@ -187,6 +192,29 @@ class DeviceFactorEngine(FactorEngine):
         self._finish_arrays(perm(scodes).to(torch.int32), perm(dcodes).to(torch.int32), names,
                             dvals.cpu().numpy(), {c: perm(x) for c, x in up.items()},
                             None if ed is None else perm(ed.long()), index)
+
+    def _prepare_indexed(self, prices: dict, index: dict, ix) -> None:
+        """The build from the reader's row-group index (``native_io.RowIndex``: segment starts in
+        ascending code order, the sorted trade-date set, the (code, date) order checked while
+        parsing): the stock ids are the segment ranks expanded on the device and the date ids a
+        device searchsorted, so the 16-byte code column never crosses PCIe and no device
+        unique / sort / order check runs.  Same ids, axes and columns as the key-based build."""
+        dev = self.device
+        codes = np.asarray(prices["ts_code"])
+        td32 = _upload(np.asarray(prices["trade_date"]), dev)
+        up = {c: _upload(np.asarray(prices[c]), dev) for c in self.NUMERIC if c in prices}
+        ed = _upload(np.asarray(prices["end_date"]), dev) if "end_date" in prices else None
+        R = int(codes.size)
+        sf = np.ascontiguousarray(ix.seg_first, dtype=np.int64)
+        N = int(sf.size)
+        lens = torch.from_numpy(np.diff(np.append(sf, R))).to(dev)
+        sid = torch.repeat_interleave(torch.arange(N, dtype=torch.int32, device=dev), lens,
+                                      output_size=R)
+        dv = np.asarray(ix.dates)
+        did = torch.searchsorted(torch.from_numpy(dv.astype(np.int64)).to(dev),
+                                 td32.long()).to(torch.int32)
+        self._finish_arrays(sid, did, codes[sf].astype("S16"), dv, up,
+                            None if ed is None else ed.long(), index)
 
     def _finish_arrays(self, stock_id, date_id, names, dv, cols, end_date, index) -> None:
         """Common tail of the full and the host-sharded builds: the global stock / date axes

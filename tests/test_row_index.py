@@ -119,3 +119,30 @@ def test_csv_reader_builds_the_index_while_parsing(tmp_path):
             f.write(f"{c.decode()},{d},{x:.6f}\n")
     got = nio.read_columns(str(path), types, nthreads=4, index=("ts_code", "trade_date"))
     assert nio.ROW_INDEX not in got and got["trade_date"].size == codes.size
+
+
+def test_device_engine_indexed_build_equals_key_build():
+    """DeviceFactorEngine built from the reader's row-group index (no code upload, ids from the
+    segments, dates by searchsorted) == the key-based build (device unique of the S16 codes and
+    dates): same ids, axes, columns and descriptors."""
+    import torch
+    from llm_driven_multi_factor_model_amd.models import e2e
+    from llm_driven_multi_factor_model_amd.models import factor_engine as FE
+    prices, index, _ = FE.synthetic_prices(N=40, T=300, seed=2, n_ind=31)
+    prices = prices.sort_values(["ts_code", "trade_date"], kind="stable").reset_index(drop=True)
+    p, i = e2e._columns_from_frames(prices, index)
+    p["trade_date"] = p["trade_date"].astype("int32")
+    if "end_date" in p:
+        p["end_date"] = p["end_date"].astype("int32")
+    ps = e2e.stage_host_columns(p, pinned=False)
+    assert nio.ROW_INDEX in ps
+    a = e2e.DeviceFactorEngine(dict(ps), dict(i), device="cpu")
+    b = e2e.DeviceFactorEngine({k: v for k, v in ps.items() if k != nio.ROW_INDEX}, dict(i),
+                               device="cpu")
+    assert torch.equal(a.stock_id, b.stock_id) and torch.equal(a.date_id, b.date_id)
+    assert (a.date_ints == b.date_ints).all() and list(a.stock_names) == list(b.stock_names)
+    for k in b.cols:
+        assert torch.equal(a.cols[k].nan_to_num(7.0), b.cols[k].nan_to_num(7.0)), k
+    ra, rb = a.compute(FE.FACTORS_TO_RUN), b.compute(FE.FACTORS_TO_RUN)
+    for k in rb:
+        assert torch.equal(ra[k].nan_to_num(7.0), rb[k].nan_to_num(7.0)), k
