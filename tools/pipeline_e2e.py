@@ -23,6 +23,10 @@ T = int(sys.argv[2]) if len(sys.argv) > 2 else 2520
 dev = "cuda:0" if torch.cuda.is_available() else "cpu"
 t0 = time.perf_counter()
 prices, index, sw = FE.synthetic_prices_fast(N=N, T=T, seed=0, n_ind=31, suspend_frac=0.01)
+# the stored loader panel's order, (ts_code, trade_date) -- the order FactorCalculator's
+# _prepare_data sorts the master into -- so the reader's row-group index applies; the generator
+# groups rows by stock in first-listed order
+prices = prices.sort_values(["ts_code", "trade_date"], kind="stable").reset_index(drop=True)
 gen_s = time.perf_counter() - t0
 print(json.dumps({"rows": len(prices), "gen_s": round(gen_s, 2)}), flush=True)
 cols = e2e._columns_from_frames(prices, index)
@@ -34,12 +38,18 @@ e2e.run_pipeline(small_p, small_i, small_sw, device=dev)  # warm-up: kernel load
 from llm_driven_multi_factor_model_amd.utils.config import FactorConfig  # noqa: E402
 # rank_invariant=True is the pipeline default (direct window kernels: a date-sharded run equals
 # one process bitwise); False = the tile kernels (faster, fp32-rounding-equal)
-for rep, ri in ((0, True), (1, True), (2, False), (3, False)):
+from llm_driven_multi_factor_model_amd.utils import native_io  # noqa: E402
+# reps 4 / 5: the same columns without the reader's row-group index (the key-based build:
+# S16 codes uploaded, device unique of codes and dates)
+for rep, ri, ixd in ((0, True, True), (1, True, True), (2, False, True), (3, False, True),
+                     (4, False, False), (5, False, False)):
+    pc = dict(cols[0]) if ixd else {k: v for k, v in cols[0].items() if k != native_io.ROW_INDEX}
     t0 = time.perf_counter()
-    model, info, _, t = e2e.run_pipeline(dict(cols[0]), dict(cols[1]), sw, device=dev,
+    model, info, _, t = e2e.run_pipeline(pc, dict(cols[1]), sw, device=dev,
                                          factor_cfg=FactorConfig(rank_invariant=ri))
     wall = time.perf_counter() - t0
     rec = {"N": N, "T": T, "D": model.panel.D, "K": model.K, "rep": rep, "rank_invariant": ri,
+           "row_index": ixd and native_io.ROW_INDEX in cols[0],
            **{k: round(v, 4) for k, v in t.items() if k.endswith("_s")}, "wall_s": round(wall, 4)}
     rec["non_io_s"] = round(sum(v for k, v in t.items() if k.endswith("_s")), 4)
     rec["kernel_ms"] = {k: round(v, 3) for k, v in t.get("kernel_ms", {}).items()}
