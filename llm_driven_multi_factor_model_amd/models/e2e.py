@@ -96,8 +96,16 @@ def _unique_pairs(hi: torch.Tensor, lo: torch.Tensor):
 
 
 def _ymd_to_datetime64(v: np.ndarray) -> np.ndarray:
-    return pd.to_datetime(pd.Series(v.astype(np.int64)).astype(str), format="%Y%m%d").to_numpy(
-        dtype="datetime64[ns]")
+    """YYYYMMDD ints -> datetime64[ns] (vectorised calendar arithmetic: pd.to_datetime on the
+    string forms took ~2 ms for 2,500 dates)."""
+    v = np.asarray(v, dtype=np.int64)
+    y, m, d = v // 10000, v // 100 % 100, v % 100
+    out = ((y - 1970).astype("datetime64[Y]") + (m - 1).astype("timedelta64[M]")).astype(
+        "datetime64[D]") + (d - 1).astype("timedelta64[D]")
+    if ((m < 1) | (m > 12) | (d < 1) | (d > 31)).any() or (
+            (out.astype("datetime64[M]") - (y - 1970).astype("datetime64[Y]")).astype(np.int64) != m - 1).any():
+        raise ValueError("invalid YYYYMMDD date")
+    return out.astype("datetime64[ns]")
 
 
 def _device_gather(srcs, ranges, offs, Rk, dev):
@@ -553,10 +561,10 @@ def risk_panel(eng: FactorEngine, cols: dict, l1_stock: np.ndarray, info: pd.Dat
     for c in ["capital", "ret", *STYLE_COLUMNS]:
         keep &= torch.isfinite(cols[c])
     sid, did = eng.stock_id.long(), eng.date_id.long()
-    dk = torch.zeros(eng.D, dtype=torch.bool, device=dev)
-    sk = torch.zeros(eng.N, dtype=torch.bool, device=dev)
-    dk[did[keep]] = True
-    sk[sid[keep]] = True
+    # dates / stocks with a kept row (counts, no boolean-mask compaction or sync)
+    kf = keep.to(torch.int32)
+    dk = torch.zeros(eng.D, dtype=torch.int32, device=dev).index_add_(0, did, kf) > 0
+    sk = torch.zeros(eng.N, dtype=torch.int32, device=dev).index_add_(0, sid, kf) > 0
     offset = 0
     if ctx is not None and ctx.enabled:
         ski = sk.to(torch.int32)
@@ -577,7 +585,10 @@ def risk_panel(eng: FactorEngine, cols: dict, l1_stock: np.ndarray, info: pd.Dat
     # onto [2, Dp * Np], the styles onto [Dp, Q, Np] (style q of cell (d, s) at
     # d * Q * Np + q * Np + s: column stride Np, date stride Q * Np)
     gm = XR.GridMap(s_r, d_r, Dp, Np)
-    Xk = torch.stack([cols[c].to(dtype) for c in ["capital", "ret", *STYLE_COLUMNS]])[:, rows]
+    names = ["capital", "ret", *STYLE_COLUMNS]
+    Xk = torch.empty(len(names), rows.numel(), dtype=dtype, device=dev)
+    for k, c in enumerate(names):
+        torch.index_select(cols[c].to(dtype), 0, rows, out=Xk[k])
     cr = gm.scatter(Xk[:2].contiguous())
     cap, ret = cr[0], cr[1]
     sty = torch.full((Dp, Q, Np), nan, dtype=dtype, device=dev)
