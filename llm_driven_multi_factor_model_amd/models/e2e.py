@@ -561,10 +561,12 @@ def risk_panel(eng: FactorEngine, cols: dict, l1_stock: np.ndarray, info: pd.Dat
     for c in ["capital", "ret", *STYLE_COLUMNS]:
         keep &= torch.isfinite(cols[c])
     sid, did = eng.stock_id.long(), eng.date_id.long()
-    # dates / stocks with a kept row (counts, no boolean-mask compaction or sync)
-    kf = keep.to(torch.int32)
-    dk = torch.zeros(eng.D, dtype=torch.int32, device=dev).index_add_(0, did, kf) > 0
-    sk = torch.zeros(eng.N, dtype=torch.int32, device=dev).index_add_(0, sid, kf) > 0
+    # dates / stocks with a kept row (an integer index_add here contends on ~5000 rows per
+    # date counter: slower than the compaction + plain stores)
+    dk = torch.zeros(eng.D, dtype=torch.bool, device=dev)
+    sk = torch.zeros(eng.N, dtype=torch.bool, device=dev)
+    dk[did[keep]] = True
+    sk[sid[keep]] = True
     offset = 0
     if ctx is not None and ctx.enabled:
         ski = sk.to(torch.int32)
