@@ -121,7 +121,7 @@ def test_csv_reader_builds_the_index_while_parsing(tmp_path):
     assert nio.ROW_INDEX not in got and got["trade_date"].size == codes.size
 
 
-def test_device_engine_indexed_build_equals_key_build():
+def _indexed_vs_key(device, pinned):
     """DeviceFactorEngine built from the reader's row-group index (no code upload, ids from the
     segments, dates by searchsorted) == the key-based build (device unique of the S16 codes and
     dates): same ids, axes, columns and descriptors."""
@@ -134,11 +134,11 @@ def test_device_engine_indexed_build_equals_key_build():
     p["trade_date"] = p["trade_date"].astype("int32")
     if "end_date" in p:
         p["end_date"] = p["end_date"].astype("int32")
-    ps = e2e.stage_host_columns(p, pinned=False)
+    ps = e2e.stage_host_columns(p, pinned=pinned)
     assert nio.ROW_INDEX in ps
-    a = e2e.DeviceFactorEngine(dict(ps), dict(i), device="cpu")
+    a = e2e.DeviceFactorEngine(dict(ps), dict(i), device=device)
     b = e2e.DeviceFactorEngine({k: v for k, v in ps.items() if k != nio.ROW_INDEX}, dict(i),
-                               device="cpu")
+                               device=device)
     assert torch.equal(a.stock_id, b.stock_id) and torch.equal(a.date_id, b.date_id)
     assert (a.date_ints == b.date_ints).all() and list(a.stock_names) == list(b.stock_names)
     for k in b.cols:
@@ -146,3 +146,12 @@ def test_device_engine_indexed_build_equals_key_build():
     ra, rb = a.compute(FE.FACTORS_TO_RUN), b.compute(FE.FACTORS_TO_RUN)
     for k in rb:
         assert torch.equal(ra[k].nan_to_num(7.0), rb[k].nan_to_num(7.0)), k
+
+
+def test_device_engine_indexed_build_equals_key_build():
+    _indexed_vs_key("cpu", False)
+
+
+@pytest.mark.gpu
+def test_device_engine_indexed_build_equals_key_build_gpu(cuda):
+    _indexed_vs_key(cuda, True)
