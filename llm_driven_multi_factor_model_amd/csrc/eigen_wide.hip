@@ -150,7 +150,10 @@ mc_bias_wide_kernel(const double* __restrict__ D0, int K, int M, const double* _
         a[j + 1] = fma(-u, ww.y, fma(-w, uu.y, a[j + 1]));
         if (((j - J0) & 7) == 6) lds_batch();
       }
-      __syncthreads();  // wb / red[1] / bc reused by the next step
+      // no barrier before the next step: its first LDS writes (bc, the partials of its first
+      // reduction) are to slots this step read before its second barrier, and the next writes
+      // of wb / the second partials come after the next step's own barriers, which no wave
+      // reaches before finishing this update
     }
   };
   if ((abl & 4) == 0) {
@@ -507,7 +510,8 @@ __global__ __launch_bounds__(NW * 64) void mc_bias_wide2_kernel(
         a[jj + 1] = fma(-u, ww.y, fma(-w, uu.y, a[jj + 1]));
         if (((jj - JL) & 7) == 6) lds_batch();
       }
-      __syncthreads();
+      // no barrier before the next step (see mc_bias_wide_kernel): every slot the next step
+      // writes before its first barrier was last read before this step's second barrier
     }
   };
   if ((abl & 4) == 0) {
