@@ -70,80 +70,15 @@ MFA_API int mfa_gather_host_ranges(const void* const* host_src, void* const* dst
 }
 
 // ---------------------------------------------------------------------------------------------
-// Column-batched scatter / gather between flat rows and a (date, stock) grid (the e2e job's
-// post-processing and RiskPanel build, models/factor_engine.py / models/e2e.py): C columns in
-// one launch, a simple 1:1 copy per element (the row -> cell map is injective), no index sort.
-// X: C columns of R elements (column stride xs), G: C grids (column stride gs), idx [R] the
-// flat grid cell of every row.  E = 4 or 8 byte elements.
-namespace {
-
-template <typename E>
-__global__ __launch_bounds__(256) void scatter_cols_kernel(const E* __restrict__ X, int64_t xs,
-                                                           const int64_t* __restrict__ idx,
-                                                           int64_t R, int C, E* __restrict__ G,
-                                                           int64_t gs) {
-  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < R; r += (int64_t)gridDim.x * 256) {
-    const int64_t g = idx[r];
-    for (int c = 0; c < C; ++c) G[c * gs + g] = X[c * xs + r];
-  }
-}
-
-template <typename E>
-__global__ __launch_bounds__(256) void gather_cols_kernel(const E* __restrict__ G, int64_t gs,
-                                                          const int64_t* __restrict__ idx,
-                                                          int64_t R, int C, E* __restrict__ X,
-                                                          int64_t xs) {
-  for (int64_t r = (int64_t)blockIdx.x * 256 + threadIdx.x; r < R; r += (int64_t)gridDim.x * 256) {
-    const int64_t g = idx[r];
-    for (int c = 0; c < C; ++c) X[c * xs + r] = G[c * gs + g];
-  }
-}
-
-inline int cols_grid(int64_t R) {
-  const int64_t b = (R + 255) / 256;
-  return (int)(b < 65536 ? (b > 0 ? b : 1) : 65536);
-}
-
-}  // namespace
-
-MFA_API int mfa_scatter_cols(const void* X, int64_t xs, const int64_t* idx, int64_t R, int C,
-                             int elem, void* G, int64_t gs, void* stream) {
-  if (R <= 0 || C <= 0) return 0;
-  hipStream_t s = (hipStream_t)stream;
-  if (elem == 4)
-    hipLaunchKernelGGL(scatter_cols_kernel<float>, dim3(cols_grid(R)), dim3(256), 0, s,
-                       (const float*)X, xs, idx, R, C, (float*)G, gs);
-  else if (elem == 8)
-    hipLaunchKernelGGL(scatter_cols_kernel<double>, dim3(cols_grid(R)), dim3(256), 0, s,
-                       (const double*)X, xs, idx, R, C, (double*)G, gs);
-  else
-    return (int)hipErrorInvalidValue;
-  return (int)hipGetLastError();
-}
-
-MFA_API int mfa_gather_cols(const void* G, int64_t gs, const int64_t* idx, int64_t R, int C,
-                            int elem, void* X, int64_t xs, void* stream) {
-  if (R <= 0 || C <= 0) return 0;
-  hipStream_t s = (hipStream_t)stream;
-  if (elem == 4)
-    hipLaunchKernelGGL(gather_cols_kernel<float>, dim3(cols_grid(R)), dim3(256), 0, s,
-                       (const float*)G, gs, idx, R, C, (float*)X, xs);
-  else if (elem == 8)
-    hipLaunchKernelGGL(gather_cols_kernel<double>, dim3(cols_grid(R)), dim3(256), 0, s,
-                       (const double*)G, gs, idx, R, C, (double*)X, xs);
-  else
-    return (int)hipErrorInvalidValue;
-  return (int)hipGetLastError();
-}
-
-// ---------------------------------------------------------------------------------------------
 // Rows <-> grid as an LDS-tiled transpose.  The rows are sorted by (stock, date), the grid is
-// date-major, so a per-element scatter writes one 4-byte word per 128-byte line (measured: the
-// column-batched scatter above is no faster than torch's index_put).  Here a 256-thread block
+// date-major, so a per-element scatter writes one 4-byte word per 128-byte line.  Here a
+// 256-thread block
 // owns a tile of 64 dates x 64 stocks: each stock's rows of those dates are one contiguous range
 // (toff[s][tb] .. toff[s][tb + 1], from the sorted (stock, date) key), read along the rows
 // (coalesced), placed in an LDS tile at their local date, and written out along the stocks
 // (coalesced); grid cells without a row get `fill`.  The gather is the same walk backwards.
+// (A plain per-element 1:1 scatter kernel measured no faster than torch's index_put: 5.6 ms for
+// 20 columns of 12.4 M rows, profiles/r05/r05s.)
 // X: C columns of R rows (column stride xs); did [R] the rows' date (< Dg); toff [Ng][NTB + 1]
 // with NTB = ceil(Dg / 64); grid cell (c, d, s) at c * gs + d * ds + s.
 namespace {

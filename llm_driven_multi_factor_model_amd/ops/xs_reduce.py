@@ -29,10 +29,6 @@ _native.register("mfa_style_norm", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.
                                      C.c_void_p, C.c_void_p])
 _native.register("mfa_bayes_shrink", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_double,
                                        C.c_void_p, C.c_void_p, C.c_void_p])
-_native.register("mfa_scatter_cols", [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int, C.c_int,
-                                      C.c_void_p, C.c_int64, C.c_void_p])
-_native.register("mfa_gather_cols", [C.c_void_p, C.c_int64, C.c_void_p, C.c_int64, C.c_int, C.c_int,
-                                     C.c_void_p, C.c_int64, C.c_void_p])
 _native.register("mfa_rows_grid", [C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p,
                                    C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int64, C.c_int64,
                                    C.c_double, C.c_void_p])
@@ -71,37 +67,6 @@ def winsorize_(x: torch.Tensor, n_std: float = 2.5) -> torch.Tensor:
 
 
 # ------------------------------------------------------------------ rows <-> (date, stock) grid
-def scatter_cols(X: torch.Tensor, idx: torch.Tensor, cells: int, fill: float = float("nan"),
-                 out: torch.Tensor | None = None) -> torch.Tensor:
-    """``G[c, idx[r]] = X[c, r]`` for C columns at once (``csrc/gather.hip``: one launch, a plain
-    1:1 copy, no index sort); ``G`` [C, cells] is ``fill`` elsewhere (or ``out``, written in
-    place).  ``idx`` int64 [R], distinct cells."""
-    X = X.contiguous()
-    Cn, R = X.shape
-    G = out if out is not None else torch.full((Cn, cells), fill, dtype=X.dtype, device=X.device)
-    if not X.is_cuda:
-        G[:, idx] = X
-        return G
-    ix = idx.to(torch.int64).contiguous()
-    _native.call("mfa_scatter_cols", _native.ptr(X), R, _native.ptr(ix), R, Cn, X.element_size(),
-                 _native.ptr(G), G.stride(0), _native.stream(X.device))
-    return G
-
-
-def gather_cols(G: torch.Tensor, idx: torch.Tensor) -> torch.Tensor:
-    """``X[c, r] = G[c, idx[r]]`` for C columns at once (the inverse of :func:`scatter_cols`)."""
-    G = G.contiguous()
-    Cn = G.shape[0]
-    if not G.is_cuda:
-        return G[:, idx]
-    ix = idx.to(torch.int64).contiguous()
-    R = ix.numel()
-    X = torch.empty(Cn, R, dtype=G.dtype, device=G.device)
-    _native.call("mfa_gather_cols", _native.ptr(G), G.stride(0), _native.ptr(ix), R, Cn,
-                 G.element_size(), _native.ptr(X), R, _native.stream(G.device))
-    return X
-
-
 class GridMap:
     """Rows sorted by (stock, date) <-> a date-major [Dg, Ng] grid, as an LDS-tiled transpose
     (``csrc/gather.hip``, ``mfa_rows_grid``: 64-date x 64-stock tiles, coalesced on both
