@@ -2000,14 +2000,16 @@ size_t eigh_pairs_lds(int K) {
          32 * sizeof(double2) + 64 * sizeof(int);
 }
 
-// only != nullptr: re-solve only the matrices with only[b] != 0 (the tridiagonal eigh's flags)
+// only != nullptr: re-solve only the matrices with only[b] != 0 (the tridiagonal eigh's flags),
+// warm-started from their tridiagonal eigenvectors when `warm`
 template <int NB, int NBV, int FAST = 0>
 __global__ __launch_bounds__(64) void eigh_pairs_kernel(const double* __restrict__ Ain, int K,
                                                         int max_sweeps, double tol,
                                                         double* __restrict__ w,
                                                         double* __restrict__ U,
                                                         int* __restrict__ sweeps,
-                                                        const int* __restrict__ only) {
+                                                        const int* __restrict__ only,
+                                                        int warm = 0) {
   extern __shared__ double sm[];
   const int b = blockIdx.x, lane = threadIdx.x;
   if (only && !only[b]) return;
@@ -2026,11 +2028,64 @@ __global__ __launch_bounds__(64) void eigh_pairs_kernel(const double* __restrict
     if (lane == 0 && sweeps) sweeps[b] = -1;
     return;
   }
-  // packed upper triangle of the symmetrised input (padding row / column zero), V = I
-  for (int i = 0; i < Ke; ++i)
-    for (int j = i + lane; j < Ke; j += 64)
-      A[pk(i, j, Ke)] = (i < K && j < K) ? 0.5 * (a[i * K + j] + a[j * K + i]) : 0.0;
-  for (int e = lane; e < K * Ke; e += 64) V[e] = (e / Ke == e % Ke) ? 1.0 : 0.0;
+  if (only && warm && K <= 64) {
+    // Warm start of a flagged matrix (the tridiagonal eigh's eigenvectors U of a clustered
+    // spectrum are accurate but not orthogonal to 1e-12): Q = U orthonormalised by modified
+    // Gram-Schmidt (twice; a column that vanishes -- a duplicated vector -- is replaced by the
+    // first unit vector that survives), then the Jacobi runs on B = Q^T A Q, nearly diagonal
+    // off the clusters, with V = Q accumulating its rotations: ~2 sweeps instead of ~8 from I.
+    // Lane i holds row i of V.
+    const bool row = lane < K;
+    if (row)
+      for (int x = 0; x < Ke; ++x) V[lane * Ke + x] = x < K ? U[(size_t)b * K * K + lane * K + x] : 0.0;
+    auto orth = [&](int x) {  // orthonormalise column x against columns 0 .. x-1
+      for (int pass = 0; pass < 2; ++pass)
+        for (int y = 0; y < x; ++y) {
+          const double r = wave_total(row ? V[lane * Ke + y] * V[lane * Ke + x] : 0.0);
+          if (row) V[lane * Ke + x] = fma(-r, V[lane * Ke + y], V[lane * Ke + x]);
+        }
+      const double n2 = wave_total(row ? V[lane * Ke + x] * V[lane * Ke + x] : 0.0);
+      if (n2 > 1e-16) {
+        if (row) V[lane * Ke + x] *= 1.0 / sqrt(n2);
+        return true;
+      }
+      return false;
+    };
+    for (int x = 0; x < K; ++x) {
+      if (orth(x)) continue;
+      for (int e = 0; e < K; ++e) {  // a unit vector outside the span of the columns so far
+        if (row) V[lane * Ke + x] = lane == e ? 1.0 : 0.0;
+        if (orth(x)) break;
+      }
+    }
+    wsync();  // Q's rows (each lane wrote its own) before the column reads below
+    // B = Q^T A Q one column at a time: t = A q_y (lane i = row i, A symmetrised on the fly),
+    // then B[x][y] = q_x^T t for x <= y (lane x); the padding row / column stay zero
+    double* t = (double*)rcs;  // 64 doubles of scratch before the Jacobi needs them
+    for (int y = 0; y < Ke; ++y) {
+      if (y >= K) {
+        for (int x = lane; x <= y; x += 64) A[pk(x, y, Ke)] = 0.0;
+        continue;
+      }
+      double ti = 0.0;
+      if (row)
+        for (int j = 0; j < K; ++j) ti = fma(0.5 * (a[lane * K + j] + a[j * K + lane]), V[j * Ke + y], ti);
+      t[lane] = ti;
+      wsync();
+      if (lane <= y) {
+        double bxy = 0.0;
+        for (int i = 0; i < K; ++i) bxy = fma(V[i * Ke + lane], t[i], bxy);
+        A[pk(lane, y, Ke)] = bxy;
+      }
+      wsync();
+    }
+  } else {
+    // packed upper triangle of the symmetrised input (padding row / column zero), V = I
+    for (int i = 0; i < Ke; ++i)
+      for (int j = i + lane; j < Ke; j += 64)
+        A[pk(i, j, Ke)] = (i < K && j < K) ? 0.5 * (a[i * K + j] + a[j * K + i]) : 0.0;
+    for (int e = lane; e < K * Ke; e += 64) V[e] = (e / Ke == e % Ke) ? 1.0 : 0.0;
+  }
   wsync();
   const int ns = jacobi_pairs_vec<NB, NBV, FAST>(A, V, rcs, K, Ke, max_sweeps, tol);
   // descending rank of each real position's eigenvalue (ties by position); padding excluded:
@@ -2119,6 +2174,7 @@ int g_eigh_mode = 2;  // 0 = pair-block tournament Jacobi, 1 = row/column cyclic
                       // 2 = Householder tridiagonal (mc_bias_tri2_kernel<EIG>) + the pair-block
                       //     Jacobi for the matrices it flags (non-orthogonal eigenvectors)
 int g_fast_rot = 1;   // 1 = rcp/rsq + Newton rotation parameters (jacobi_cs<1>); 0 = IEEE div/sqrt
+int g_eigh_warm = 1;  // flagged-matrix re-solve warm-started from the tridiagonal eigenvectors
 int g_bias_mode = 5;   // 21 = mode 5 walking 8 consecutive dates per wave with warm-
                        // started Laguerre eigenvalues (eigen stage 12.73-12.79 vs 13.10-13.26 ms,
                        // profiles/r05/r05b/bias_chain_ab.jsonl) -- opt-in: a date shard whose
@@ -2150,6 +2206,10 @@ MFA_API int mfa_eigen_set_date_origin(int d0) {
 
 // Setters return hipErrorInvalidValue for a variant this build does not contain (the A/B
 // variants are compiled only with MFA_AB=1: python -m ..._build --ab).
+MFA_API int mfa_eigh_set_warm(int on) {
+  g_eigh_warm = on != 0;
+  return 0;
+}
 MFA_API int mfa_eigh_set_mode(int mode) {
   if (!MFA_AB && mode == 1) return (int)hipErrorInvalidValue;
   g_eigh_mode = mode;
@@ -2417,7 +2477,7 @@ MFA_API int mfa_eigh_batched(const double* A, int B, int K, int max_sweeps, doub
   }
   if (nb <= 4 * 64 && rows_per_lane <= 14 && (g_fast_rot || !MFA_AB))
     hipLaunchKernelGGL((eigh_pairs_kernel<4, 14, 1>), dim3(B), dim3(64), eigh_pairs_lds(K), s, A,
-                       K, max_sweeps, tol, w, U, sweeps, only);
+                       K, max_sweeps, tol, w, U, sweeps, only, g_eigh_warm);
 #if MFA_AB
   else if (g_eigh_mode == 1)  // A/B: row/column cyclic Jacobi
     hipLaunchKernelGGL(eigh_kernel, dim3(B), dim3(64), eigh_lds(K), s, A, K, max_sweeps, tol, w, U,
