@@ -2001,15 +2001,16 @@ size_t eigh_pairs_lds(int K) {
 }
 
 // only != nullptr: re-solve only the matrices with only[b] != 0 (the tridiagonal eigh's flags),
-// warm-started from their tridiagonal eigenvectors when `warm`
-template <int NB, int NBV, int FAST = 0>
+// warm-started from their tridiagonal eigenvectors when WARM
+// (WARM: a separate instantiation -- its register-resident setup takes 256 VGPRs, which the
+// cold batched Jacobi must not pay in occupancy)
+template <int NB, int NBV, int FAST = 0, bool WARM = false>
 __global__ __launch_bounds__(64) void eigh_pairs_kernel(const double* __restrict__ Ain, int K,
                                                         int max_sweeps, double tol,
                                                         double* __restrict__ w,
                                                         double* __restrict__ U,
                                                         int* __restrict__ sweeps,
-                                                        const int* __restrict__ only,
-                                                        int warm = 0) {
+                                                        const int* __restrict__ only) {
   extern __shared__ double sm[];
   const int b = blockIdx.x, lane = threadIdx.x;
   if (only && !only[b]) return;
@@ -2028,57 +2029,131 @@ __global__ __launch_bounds__(64) void eigh_pairs_kernel(const double* __restrict
     if (lane == 0 && sweeps) sweeps[b] = -1;
     return;
   }
-  if (only && warm && K <= 64) {
+  bool diag_ok = false;  // warm start: B already diagonal to tol, the Jacobi has nothing to do
+  if constexpr (WARM) {
     // Warm start of a flagged matrix (the tridiagonal eigh's eigenvectors U of a clustered
-    // spectrum are accurate but not orthogonal to 1e-12): Q = U orthonormalised by modified
-    // Gram-Schmidt (twice; a column that vanishes -- a duplicated vector -- is replaced by the
-    // first unit vector that survives), then the Jacobi runs on B = Q^T A Q, nearly diagonal
-    // off the clusters, with V = Q accumulating its rotations: ~2 sweeps instead of ~8 from I.
-    // Lane i holds row i of V.
-    const bool row = lane < K;
-    if (row)
-      for (int x = 0; x < Ke; ++x) V[lane * Ke + x] = x < K ? U[(size_t)b * K * K + lane * K + x] : 0.0;
-    auto orth = [&](int x) {  // orthonormalise column x against columns 0 .. x-1
-      for (int pass = 0; pass < 2; ++pass)
-        for (int y = 0; y < x; ++y) {
-          const double r = wave_total(row ? V[lane * Ke + y] * V[lane * Ke + x] : 0.0);
-          if (row) V[lane * Ke + x] = fma(-r, V[lane * Ke + y], V[lane * Ke + x]);
-        }
-      const double n2 = wave_total(row ? V[lane * Ke + x] * V[lane * Ke + x] : 0.0);
-      if (n2 > 1e-16) {
-        if (row) V[lane * Ke + x] *= 1.0 / sqrt(n2);
-        return true;
+    // spectrum are accurate but not orthogonal to 1e-12): Q = U orthonormalised, then the
+    // Jacobi runs on B = Q^T A Q -- diagonal off the clusters -- with V = Q accumulating its
+    // rotations (0-1 sweeps instead of ~8 from I).
+    // (1) Q by right-looking modified Gram-Schmidt, twice, with lane x holding column x in
+    // registers: at step y lane y normalises its column and broadcasts it through LDS, every
+    // later column subtracts its projection locally (no cross-lane reductions).  A column that
+    // the second pass finds numerically inside the span of the earlier ones (a duplicated
+    // vector: it keeps < 1/2 of its norm) is replaced by the first unit vector e_k that keeps
+    // > 1/(2K) of its norm outside that span (one exists: the squared norms sum to K - y).
+    // Q is kept as a zero-padded 64 x 64 block Qs (LDS past the Jacobi's buffers), so every
+    // loop below runs over 64 rows / columns with no `< K` test: runtime-K tests in unrolled
+    // loops cost one scalar mask per element, which spill and reload on every pass.
+    double* t = (double*)rcs;  // 64 doubles of broadcast scratch before the Jacobi needs them
+    double* Qs = (double*)(perm + 64);
+    const bool col = lane < K;
+    {
+      double q[64];
+#pragma unroll
+      for (int i = 0; i < 64; ++i) {  // unconditional loads (all in flight), masked by a
+        // factor: a select lets the compiler sink each load into its own branch + wait
+        const double u = U[(size_t)b * K * K + (size_t)min(i, K - 1) * K + min(lane, K - 1)];
+        q[i] = u * ((col && i < K) ? 1.0 : 0.0);  // the input is finite (checked above)
       }
-      return false;
-    };
-    for (int x = 0; x < K; ++x) {
-      if (orth(x)) continue;
-      for (int e = 0; e < K; ++e) {  // a unit vector outside the span of the columns so far
-        if (row) V[lane * Ke + x] = lane == e ? 1.0 : 0.0;
-        if (orth(x)) break;
+      if (!col) {
+#pragma unroll
+        for (int i = 0; i < 64; ++i) Qs[i * 64 + lane] = 0.0;
+      }
+      for (int pass = 0; pass < 2; ++pass) {
+        for (int y = 0; y < K; ++y) {
+          if (lane == y) {
+            double n2 = 0.0;
+#pragma unroll
+            for (int i = 0; i < 64; ++i) n2 = fma(q[i], q[i], n2);
+            if (pass == 1 && !(n2 > 0.25)) {
+              for (int k = 0; k < K; ++k) {
+#pragma unroll
+                for (int i = 0; i < 64; ++i) q[i] = i == k ? 1.0 : 0.0;
+                for (int rep = 0; rep < 2; ++rep)
+                  for (int z = 0; z < y; ++z) {
+                    double r = 0.0;
+#pragma unroll
+                    for (int i = 0; i < 64; ++i) r = fma(Qs[i * 64 + z], q[i], r);
+#pragma unroll
+                    for (int i = 0; i < 64; ++i) q[i] = fma(-r, Qs[i * 64 + z], q[i]);
+                  }
+                n2 = 0.0;
+#pragma unroll
+                for (int i = 0; i < 64; ++i) n2 = fma(q[i], q[i], n2);
+                if (n2 > 0.5 / K) break;
+              }
+            }
+            const double sc = n2 > 1e-30 ? 1.0 / sqrt(n2) : 0.0;
+#pragma unroll
+            for (int i = 0; i < 64; ++i) {
+              q[i] *= sc;
+              t[i] = q[i];
+            }
+            if (pass == 1) {
+#pragma unroll
+              for (int i = 0; i < 64; ++i) Qs[i * 64 + y] = q[i];
+            }
+          }
+          wsync();
+          if (lane > y && col) {
+            double r0 = 0.0, r1 = 0.0;
+#pragma unroll
+            for (int i = 0; i < 64; i += 2) {
+              r0 = fma(t[i], q[i], r0);
+              r1 = fma(t[i + 1], q[i + 1], r1);
+            }
+            const double r = r0 + r1;
+#pragma unroll
+            for (int i = 0; i < 64; ++i) q[i] = fma(-r, t[i], q[i]);
+          }
+          wsync();
+        }
       }
     }
-    wsync();  // Q's rows (each lane wrote its own) before the column reads below
-    // B = Q^T A Q one column at a time: t = A q_y (lane i = row i, A symmetrised on the fly),
-    // then B[x][y] = q_x^T t for x <= y (lane x); the padding row / column stay zero
-    double* t = (double*)rcs;  // 64 doubles of scratch before the Jacobi needs them
+    // V = Q for the Jacobi (K x Ke; the padding column is Qs's zero column K)
+    for (int e = lane; e < K * Ke; e += 64) V[e] = Qs[(e / Ke) * 64 + e % Ke];
+    // (2) B = Q^T A Q one column at a time with lane i holding row i of the symmetrised A in
+    // registers: t = A q_y, then B[x][y] = q_x^T t for x <= y (lane x); the padding row /
+    // column stay zero.  Off-diagonal and diagonal mass of B feed the Jacobi's own
+    // convergence test, applied before its first sweep.
+    double ar[64];
+#pragma unroll
+    for (int j = 0; j < 64; ++j) {
+      const int jj = min(j, K - 1), ll = min(lane, K - 1);
+      const double v = 0.5 * (a[ll * K + jj] + a[jj * K + ll]);
+      ar[j] = v * ((col && j < K) ? 1.0 : 0.0);
+    }
+    wsync();
+    double offacc = 0.0, dgacc = 0.0;
     for (int y = 0; y < Ke; ++y) {
       if (y >= K) {
         for (int x = lane; x <= y; x += 64) A[pk(x, y, Ke)] = 0.0;
         continue;
       }
-      double ti = 0.0;
-      if (row)
-        for (int j = 0; j < K; ++j) ti = fma(0.5 * (a[lane * K + j] + a[j * K + lane]), V[j * Ke + y], ti);
-      t[lane] = ti;
+      double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+      for (int j = 0; j < 64; j += 2) {
+        t0 = fma(ar[j], Qs[j * 64 + y], t0);
+        t1 = fma(ar[j + 1], Qs[(j + 1) * 64 + y], t1);
+      }
+      t[lane] = t0 + t1;
       wsync();
       if (lane <= y) {
-        double bxy = 0.0;
-        for (int i = 0; i < K; ++i) bxy = fma(V[i * Ke + lane], t[i], bxy);
+        double b0 = 0.0, b1 = 0.0;
+#pragma unroll
+        for (int i = 0; i < 64; i += 2) {
+          b0 = fma(Qs[i * 64 + lane], t[i], b0);
+          b1 = fma(Qs[(i + 1) * 64 + lane], t[i + 1], b1);
+        }
+        const double bxy = b0 + b1;
         A[pk(lane, y, Ke)] = bxy;
+        if (lane == y) dgacc = fma(bxy, bxy, dgacc);
+        else offacc = fma(2.0 * bxy, bxy, offacc);
       }
       wsync();
     }
+    const double off = wave_total(offacc), dgt = wave_total(dgacc);
+    diag_ok = off <= tol * tol * dgt || off == 0.0;
   } else {
     // packed upper triangle of the symmetrised input (padding row / column zero), V = I
     for (int i = 0; i < Ke; ++i)
@@ -2087,7 +2162,7 @@ __global__ __launch_bounds__(64) void eigh_pairs_kernel(const double* __restrict
     for (int e = lane; e < K * Ke; e += 64) V[e] = (e / Ke == e % Ke) ? 1.0 : 0.0;
   }
   wsync();
-  const int ns = jacobi_pairs_vec<NB, NBV, FAST>(A, V, rcs, K, Ke, max_sweeps, tol);
+  const int ns = diag_ok ? 0 : jacobi_pairs_vec<NB, NBV, FAST>(A, V, rcs, K, Ke, max_sweeps, tol);
   // descending rank of each real position's eigenvalue (ties by position); padding excluded:
   // the padded position holds an exact-zero row/column that no rotation ever mixes in
   int pad = -1;
@@ -2475,9 +2550,15 @@ MFA_API int mfa_eigh_batched(const double* A, int B, int K, int max_sweeps, doub
     only = sweeps;  // the Jacobi below re-solves the flagged matrices only
     sweeps = nullptr;
   }
-  if (nb <= 4 * 64 && rows_per_lane <= 14 && (g_fast_rot || !MFA_AB))
-    hipLaunchKernelGGL((eigh_pairs_kernel<4, 14, 1>), dim3(B), dim3(64), eigh_pairs_lds(K), s, A,
-                       K, max_sweeps, tol, w, U, sweeps, only, g_eigh_warm);
+  if (nb <= 4 * 64 && rows_per_lane <= 14 && (g_fast_rot || !MFA_AB)) {
+    if (only && g_eigh_warm)  // + the 64 x 64 zero-padded Q block of the warm setup
+      hipLaunchKernelGGL((eigh_pairs_kernel<4, 14, 1, true>), dim3(B), dim3(64),
+                         eigh_pairs_lds(K) + 64 * 64 * sizeof(double), s, A, K, max_sweeps, tol, w,
+                         U, sweeps, only);
+    else
+      hipLaunchKernelGGL((eigh_pairs_kernel<4, 14, 1>), dim3(B), dim3(64), eigh_pairs_lds(K), s, A,
+                         K, max_sweeps, tol, w, U, sweeps, only);
+  }
 #if MFA_AB
   else if (g_eigh_mode == 1)  // A/B: row/column cyclic Jacobi
     hipLaunchKernelGGL(eigh_kernel, dim3(B), dim3(64), eigh_lds(K), s, A, K, max_sweeps, tol, w, U,

@@ -63,7 +63,7 @@ def test_hip_eigh_matches_torch(cuda, K, B):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("K", [42, 12])
+@pytest.mark.parametrize("K", [42, 12, 33])
 def test_hip_eigh_clustered_spectrum(cuda, K):
     """Exactly repeated and 1e-9-close eigenvalues: the tridiagonal eigh's eigenvectors of such
     clusters are not orthogonal, so those matrices are flagged and re-solved by the Jacobi in
