@@ -1111,7 +1111,7 @@ size_t bias_tri_lds(int K, int KP) { return ((size_t)K * (KP + 1) + 7 * 64 + 2) 
 // from 0 in every launch), so a sims-sharded or chunked run reproduces the one-shot result.
 template <int KP, bool PF = false, int ABL = 0, int WPE = MFA_TRI2_WPE, bool EIG = false,
           int ACC = 8, int LB = 8, int NA = 2, bool PAD = false, bool ZR = false, bool SK = false,
-          bool FL = false, bool BT = false, int CH = 1>
+          bool FL = false, bool BT = false, int CH = 1, int GS = 8>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void
 mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* __restrict__ Cz,
                     const int* __restrict__ dvalid, double* __restrict__ vout,
@@ -1145,7 +1145,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
     warm = false;
     continue;
   }
-  const int nrow = (tri2_rows_doubles<KP>(ZR ? K + 2 : K) + 1) & ~1;
+  const int nrow = (tri2_rows_doubles<KP, GS>(ZR ? K + 2 : K) + 1) & ~1;
   double* R = sm;                          // packed reflector rows
   double* wb = R + nrow;                   // [64] broadcast w; Sturm counts later
   double2* tb = (double2*)(wb + 64);       // [64] {alpha_i, beta_{i-1}^2}
@@ -1194,10 +1194,10 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
   // so tau = 0 and the step only records alpha_s / beta_s: s = K-2, K-1 are the final 2 x 2.
   auto steps = [&](auto J0c) {
     constexpr int J0 = decltype(J0c)::value;
-    for (int s = J0; s < J0 + 8 && s < K; ++s) {
+    for (int s = J0; s < J0 + GS && s < K; ++s) {
       double xs = a[J0];
 #pragma unroll
-      for (int k = 1; k < 8; ++k)
+      for (int k = 1; k < GS; ++k)
         if (J0 + k < KP) {
           double t = a[J0 + k];
           asm volatile("" : "+v"(t));
@@ -1218,7 +1218,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
         tau = rcp_nr(nrm * (nrm + fabs(x0)));
         u = act ? (lane == s + 1 ? x0 - beta : x) : 0.0;
       }
-      double* us = R + tri2_row_off<KP>(s) - J0;  // us[j], j in [J0, KP)
+      double* us = R + tri2_row_off<KP, GS>(s) - J0;  // us[j], j in [J0, KP)
       if ((ZR || s + 2 < K) && lane >= J0 && lane < KP) us[lane] = u;  // u_s, zero outside (s, K)
       if (lane == 0) {
         tb[s] = double2{alpha, s > 0 ? be[s - 1] * be[s - 1] : 0.0};
@@ -1234,7 +1234,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
       if constexpr (SK) {
         if (s + 2 >= K) continue;  // tau = 0: u = p = w = 0, nothing to update
       } else if (!ZR && s + 2 >= K) {
-        us = R + tri2_row_off<KP>(J0) - J0;
+        us = R + tri2_row_off<KP, GS>(J0) - J0;
       }
 #pragma unroll
       for (int j = J0; j < KP; j += 2) {
@@ -1268,8 +1268,8 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
   static_assert(KP % 4 == 0, "KP: multiple of 4");
   if constexpr ((ABL & 4) == 0) {
     [&]<int... G>(std::integer_sequence<int, G...>) {
-      (steps(std::integral_constant<int, 8 * G>{}), ...);
-    }(std::make_integer_sequence<int, (KP + 7) / 8>{});
+      (steps(std::integral_constant<int, GS * G>{}), ...);
+    }(std::make_integer_sequence<int, (KP + GS - 1) / GS>{});
   } else {  // ablation: T = the sorted diagonal with a weak coupling, no reflectors
     const double g = gs[lane];
     tb[lane] = double2{g, lane > 0 ? 1e-12 * g * g : 0.0};
@@ -1498,7 +1498,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
       if (!(PAD && BT) && s + 2 >= K) continue;
       const double tau = ta[s];
       if (tau == 0.0) continue;
-      const double* us = R + tri2_row_off<KP>(s) - J0;
+      const double* us = R + tri2_row_off<KP, GS>(s) - J0;
       double t0 = 0.0, t1 = 0.0, t2 = 0.0, t3 = 0.0;
 #pragma unroll
       for (int j = J0; j < KP; j += 2) {
@@ -1523,9 +1523,9 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
     }
   };
   [&]<int... G>(std::integer_sequence<int, G...>) {
-    constexpr int NG = (KP + 7) / 8;
-    (back(std::integral_constant<int, 8 * (NG - 1 - G)>{}, 8 * (NG - 1 - G) + 7), ...);
-  }(std::make_integer_sequence<int, (KP + 7) / 8>{});
+    constexpr int NG = (KP + GS - 1) / GS;
+    (back(std::integral_constant<int, GS * (NG - 1 - G)>{}, GS * (NG - 1 - G) + GS - 1), ...);
+  }(std::make_integer_sequence<int, (KP + GS - 1) / GS>{});
   if constexpr (EIG) {
     // w (descending by lane rank), U[:, k] = y of lane k, and the orthogonality check of the
     // eigenvectors through the rows of Y in LDS, over the reflector rows and tables (all dead
@@ -1877,15 +1877,24 @@ mc_bias_tri3_kernel(const double* __restrict__ D0, int K, int M, int DM,
   vo[r] = (ABL & 2) ? lam : v / lam;
 }
 
+// Householder steps per reflector-row group of the production tridiagonal kernels: a group of
+// GS steps stores / reads / updates columns [GS floor(s / GS), KP), so smaller groups waste
+// fewer fmas on the columns left of s (exact zeros: bitwise the same results) and select the
+// step's column from fewer registers, at more unrolled code.  Bias solver at 2520 x 100 (A/B
+// modes 27 / 25 / 5, profiles/r05/r05ai): GS = 8 11.64, 4 11.14, 2 10.82 ms (128 VGPRs, 4 waves
+// per SIMD, no scratch).  Used by the measured KP = 44 bias instantiation (K <= 44); the other
+// widths, the date chains and the EIG mode keep GS = 8 (at GS = 2 they spill to scratch).
+constexpr int kTri2GS = 2;
+
 size_t bias_tri3_lds() { return (3 * (size_t)kT3Slot + 8) * sizeof(double); }
 
-size_t bias_tri2_lds(int K, int KP) {
+size_t bias_tri2_lds(int K, int KP, int GS = 8) {
   int n = 0;
-  for (int s = 0; s + 2 < K; ++s) n += KP - 8 * (s / 8);
+  for (int s = 0; s + 2 < K; ++s) n += KP - GS * (s / GS);
   return ((size_t)((n + 1) & ~1) + 64 + 128 + 4 * 64) * sizeof(double);
 }
-size_t eigh_tri2_lds(int K, int KP) {
-  const size_t b = bias_tri2_lds(K, KP), y = (size_t)K * KP * sizeof(double);
+size_t eigh_tri2_lds(int K, int KP, int GS = 8) {
+  const size_t b = bias_tri2_lds(K, KP, GS), y = (size_t)K * KP * sizeof(double);
   return b > y ? b : y;
 }
 
@@ -2460,8 +2469,10 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
 #define MFA_TRI2(KP_)                                                                        \
     if (K <= KP_) {                                                                        \
       hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, true, 0, MFA_TRI2_WPE, false, 8, 8, 2,    \
-                                              (KP_ == 44), false, (KP_ == 44)>),           \
-                         dim3(D * M), dim3(64), bias_tri2_lds(K, KP_), s, D0, K, M, Cz,    \
+                                              (KP_ == 44), false, (KP_ == 44), false, false, 1, \
+                                              (KP_ == 44 ? kTri2GS : 8)>),                 \
+                         dim3(D * M), dim3(64), bias_tri2_lds(K, KP_, KP_ == 44 ? kTri2GS : 8), \
+                         s, D0, K, M, Cz,                                                  \
                          dvalid, ws, nullptr, nullptr, D, 0);                                    \
       return true;                                                                         \
     }
@@ -2475,6 +2486,21 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
 #undef MFA_TRI2
     return false;
   }
+#if MFA_AB
+  if ((g_bias_mode == 25 || g_bias_mode == 27) && K <= 44) {  // A/B: 4- / 8-step groups
+    if (g_bias_mode == 25)
+      hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, true, false,
+                                              true, false, false, 1, 4>),
+                         dim3(D * M), dim3(64), bias_tri2_lds(K, 44, 4), s, D0, K, M, Cz, dvalid,
+                         ws, nullptr, nullptr, D, 0);
+    else
+      hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, true, false,
+                                              true, false, false, 1, 8>),
+                         dim3(D * M), dim3(64), bias_tri2_lds(K, 44, 8), s, D0, K, M, Cz, dvalid,
+                         ws, nullptr, nullptr, D, 0);
+    return true;
+  }
+#endif
   if (chain_mode) {  // mode 5 + warm-started date chains (8 dates per wave; 4 / 16: A/B)
 #define MFA_TRI2_CH(CH_)                                                                       \
     {                                                                                          \

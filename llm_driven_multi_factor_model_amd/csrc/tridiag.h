@@ -136,18 +136,18 @@ __device__ __forceinline__ void lds_batch() { asm volatile("" ::: "memory"); }
 
 
 
-template <int KP>
+template <int KP, int GS = 8>
 __host__ __device__ constexpr int tri2_rows_doubles(int K) {
-  // rows s = 0 .. K-3, row s holds columns [8 floor(s/8), KP)
+  // rows s = 0 .. K-3, row s holds columns [GS floor(s/GS), KP) (GS-step groups)
   int n = 0;
-  for (int s = 0; s + 2 < K; ++s) n += KP - 8 * (s / 8);
+  for (int s = 0; s + 2 < K; ++s) n += KP - GS * (s / GS);
   return n;
 }
-template <int KP>
+template <int KP, int GS = 8>
 __device__ __forceinline__ int tri2_row_off(int s) {
-  // sum over earlier full groups g' < g of 8 (KP - 8 g') + (s - 8 g)(KP - 8 g)
-  const int g = s >> 3;
-  return 8 * (g * KP - 4 * g * (g - 1)) + (s - 8 * g) * (KP - 8 * g);
+  // sum over earlier full groups g' < g of GS (KP - GS g') + (s - GS g)(KP - GS g)
+  const int g = s / GS;
+  return GS * (g * KP - GS * g * (g - 1) / 2) + (s - GS * g) * (KP - GS * g);
 }
 
 
