@@ -1111,7 +1111,7 @@ size_t bias_tri_lds(int K, int KP) { return ((size_t)K * (KP + 1) + 7 * 64 + 2) 
 // from 0 in every launch), so a sims-sharded or chunked run reproduces the one-shot result.
 template <int KP, bool PF = false, int ABL = 0, int WPE = MFA_TRI2_WPE, bool EIG = false,
           int ACC = 8, int LB = 8, int NA = 2, bool PAD = false, bool ZR = false, bool SK = false,
-          bool FL = false, bool BT = false, int CH = 1, int GS = 8>
+          bool FL = false, bool BT = false, int CH = 1, int GS = 8, bool LT = false>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void
 mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* __restrict__ Cz,
                     const int* __restrict__ dvalid, double* __restrict__ vout,
@@ -1147,12 +1147,17 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
   }
   const int nrow = (tri2_rows_doubles<KP, GS>(ZR ? K + 2 : K) + 1) & ~1;
   double* R = sm;                          // packed reflector rows
-  double* wb = R + nrow;                   // [64] broadcast w; Sturm counts later
-  double2* tb = (double2*)(wb + 64);       // [64] {alpha_i, beta_{i-1}^2}
-  double* be = (double*)(tb + 64);         // [64] beta_i
-  double* ta = be + 64;                    // [64] tau_s
-  double* dd = ta + 64;                    // [64] sqrt(D0)
-  double* gs = dd + 64;                    // [64] diagonal of A, descending; Laguerre x later
+  // LT: tables of KP entries instead of 64 (every lane-indexed write is guarded by lane < TS,
+  // every read stays below KP; tb has one more entry, tb[KP] = {1e300, 0}, which the PAD
+  // backward pivots read as the row past the last): 10.5 instead of 11.6 KB of LDS per
+  // workgroup at K = 42, KP = 44 (15 workgroups per CU instead of 13), 9.7 KB at KP = 42 (16)
+  constexpr int TS = LT ? KP : 64;
+  double* wb = R + nrow;                   // [TS] broadcast w; Sturm counts later
+  double2* tb = (double2*)(wb + TS);       // [TS (+1)] {alpha_i, beta_{i-1}^2}
+  double* be = (double*)(tb + TS + (LT ? 1 : 0));  // [TS] beta_i
+  double* ta = be + TS;                    // [TS] tau_s
+  double* dd = ta + TS;                    // [TS] sqrt(D0)
+  double* gs = dd + TS;                    // [TS] diagonal of A, descending; Laguerre x later
   const int li = lane < K ? lane : 0;
   double a[KP];
   double di = 0.0;
@@ -1166,7 +1171,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
   } else {
     const double* d0 = D0 + (size_t)d * K;
     di = lane < K ? sqrt(fmax(d0[lane], 0.0)) : 0.0;
-    dd[lane] = di;
+    if (lane < TS) dd[lane] = di;
     lds_order();
     // lane i's row of A = S C_z S from the coalesced columns of the symmetric C_z
 #pragma unroll
@@ -1177,7 +1182,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
   }
   {
     const double g = lane < K ? (EIG ? Ain[li * K + li] : di * c[li * K + li] * di) : 0.0;
-    wb[lane] = g;
+    if (lane < TS) wb[lane] = g;
     lds_order();
     if (lane < K) {  // descending rank of the diagonal (ties by index): initial guesses
       int rank = 0;
@@ -1251,7 +1256,7 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
       const double p = act ? tau * (NA == 4 ? (p0 + p1) + (p2 + p3) : p0 + p1) : 0.0;
       const double kk = 0.5 * tau * wave_total(u * p);
       const double w = p - kk * u;
-      wb[lane] = w;
+      if (lane < TS) wb[lane] = w;
       lds_order();
 #pragma unroll
       for (int j = J0; j < KP; j += 2) {
@@ -1265,16 +1270,18 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
       lds_order();
     }
   };
-  static_assert(KP % 4 == 0, "KP: multiple of 4");
+  static_assert(KP % (GS < 4 ? 2 : 4) == 0, "KP: multiple of 4 (of 2 with 2-step groups)");
   if constexpr ((ABL & 4) == 0) {
     [&]<int... G>(std::integer_sequence<int, G...>) {
       (steps(std::integral_constant<int, GS * G>{}), ...);
     }(std::make_integer_sequence<int, (KP + GS - 1) / GS>{});
   } else {  // ablation: T = the sorted diagonal with a weak coupling, no reflectors
-    const double g = gs[lane];
-    tb[lane] = double2{g, lane > 0 ? 1e-12 * g * g : 0.0};
-    be[lane] = 1e-6 * g;
-    ta[lane] = 0.0;
+    const double g = gs[lane < TS ? lane : 0];
+    if (lane < TS) {
+      tb[lane] = double2{g, lane > 0 ? 1e-12 * g * g : 0.0};
+      be[lane] = 1e-6 * g;
+      ta[lane] = 0.0;
+    }
   }
   lds_order();
   // ---- 2. eigenvalue of rank `lane` (descending): as mc_bias_tri_kernel ----
@@ -1312,8 +1319,10 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
   int cnt = sturm(x);
   double* xsv = gs;  // each lane read its own gs slot above
   int* csv = (int*)wb;
-  xsv[lane] = x;
-  csv[lane] = cnt;
+  if (lane < TS) {
+    xsv[lane] = x;
+    csv[lane] = cnt;
+  }
   lds_order();
   for (int l = 0; l < K; ++l) {
     const double xl = xsv[l];
@@ -1367,11 +1376,12 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
     // rows K .. 63 decoupled: alpha huge (never an eigenvalue rank a lane targets, pivots finite),
     // beta = 0 (be[K-1] is 0 already: column K of the reduced matrix is zero)
     lds_order();
-    if (lane >= K) {
+    if (lane >= K && lane < TS) {
       tb[lane] = double2{1e300, 0.0};
       be[lane] = 0.0;
       if constexpr (BT) ta[lane] = 0.0;
     }
+    if (LT && lane == TS) tb[TS] = double2{1e300, 0.0};
     lds_order();
   }
   if (PAD && lane < K) {
@@ -1882,16 +1892,18 @@ mc_bias_tri3_kernel(const double* __restrict__ D0, int K, int M, int DM,
 // fewer fmas on the columns left of s (exact zeros: bitwise the same results) and select the
 // step's column from fewer registers, at more unrolled code.  Bias solver at 2520 x 100 (A/B
 // modes 27 / 25 / 5, profiles/r05/r05ai): GS = 8 11.64, 4 11.14, 2 10.82 ms (128 VGPRs, 4 waves
-// per SIMD, no scratch).  Used by the measured KP = 44 bias instantiation (K <= 44); the other
-// widths, the date chains and the EIG mode keep GS = 8 (at GS = 2 they spill to scratch).
+// per SIMD, no scratch).  Used by the measured bias instantiations at KP = 42 / 44 (K <= 44,
+// with KP-entry tables, LT); the other widths, the date chains and the EIG mode keep GS = 8 (at
+// GS = 2 they spill to scratch).
 constexpr int kTri2GS = 2;
 
 size_t bias_tri3_lds() { return (3 * (size_t)kT3Slot + 8) * sizeof(double); }
 
-size_t bias_tri2_lds(int K, int KP, int GS = 8) {
+size_t bias_tri2_lds(int K, int KP, int GS = 8, bool LT = false) {
   int n = 0;
   for (int s = 0; s + 2 < K; ++s) n += KP - GS * (s / GS);
-  return ((size_t)((n + 1) & ~1) + 64 + 128 + 4 * 64) * sizeof(double);
+  // tables (mc_bias_tri2_kernel's TS entries each; LT: tb has TS + 1)
+  return ((size_t)((n + 1) & ~1) + (LT ? 7 * KP + 2 : 7 * 64)) * sizeof(double);
 }
 size_t eigh_tri2_lds(int K, int KP, int GS = 8) {
   const size_t b = bias_tri2_lds(K, KP, GS), y = (size_t)K * KP * sizeof(double);
@@ -2466,13 +2478,24 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
                      double* ws, hipStream_t s) {
   const bool chain_mode = g_bias_mode == 21 || (MFA_AB && (g_bias_mode == 22 || g_bias_mode == 23));
   if (g_bias_mode == 5 || (chain_mode && K > 44)) {  // chains are instantiated at KP = 44
+    // 32 < K <= 42 (the reference's 1 + 31 + 10 factors): KP = 42, 2-step groups, KP-entry
+    // tables: 128 VGPRs and 9.7 KB of LDS -> 4 waves per SIMD, 16 per CU (profiles/r05/r05al:
+    // 10.74 -> 9.18 ms at 2520 x 100, bitwise the same ratios as the 64-entry-table kernel)
+    if (K > 32 && K <= 42) {
+      hipLaunchKernelGGL((mc_bias_tri2_kernel<42, true, 0, 4, false, 8, 8, 2, true, false, true,
+                                              false, false, 1, kTri2GS, true>),
+                         dim3(D * M), dim3(64), bias_tri2_lds(K, 42, kTri2GS, true), s, D0, K, M,
+                         Cz, dvalid, ws, nullptr, nullptr, D, 0);
+      return true;
+    }
 #define MFA_TRI2(KP_)                                                                        \
     if (K <= KP_) {                                                                        \
       hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, true, 0, MFA_TRI2_WPE, false, 8, 8, 2,    \
                                               (KP_ == 44), false, (KP_ == 44), false, false, 1, \
-                                              (KP_ == 44 ? kTri2GS : 8)>),                 \
-                         dim3(D * M), dim3(64), bias_tri2_lds(K, KP_, KP_ == 44 ? kTri2GS : 8), \
-                         s, D0, K, M, Cz,                                                  \
+                                              (KP_ == 44 ? kTri2GS : 8), (KP_ == 44)>),    \
+                         dim3(D * M), dim3(64),                                            \
+                         bias_tri2_lds(K, KP_, KP_ == 44 ? kTri2GS : 8, KP_ == 44), s, D0, K, \
+                         M, Cz,                                                            \
                          dvalid, ws, nullptr, nullptr, D, 0);                                    \
       return true;                                                                         \
     }
