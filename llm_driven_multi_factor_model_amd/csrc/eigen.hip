@@ -2234,6 +2234,8 @@ __global__ __launch_bounds__(64) void bias_sum_kernel(const double* __restrict__
 
 // finalize: v = sqrt(mean_m v_m); v = a (v - 1) + 1; F^ = U0 diag(v^2 D0) U0^T.  Grid (D).
 // `vin` holds per-sim values [D][M][K], or (M_sum > 0) per-date sums [D][K] over M_sum sims.
+// STAGE (K <= 64): U0 of the date staged in LDS; larger K (any-K finalize) reads it from L1 / L2.
+template <bool STAGE>
 __global__ __launch_bounds__(256) void eigen_finalize_kernel(const double* __restrict__ vin,
                                                              const double* __restrict__ D0,
                                                              const double* __restrict__ U0,
@@ -2241,15 +2243,28 @@ __global__ __launch_bounds__(256) void eigen_finalize_kernel(const double* __res
                                                              int K, int M, int M_sum, double scale,
                                                              double* __restrict__ Fout,
                                                              double* __restrict__ vbias) {
-  extern __shared__ double g[];  // [K]
+  extern __shared__ double g[];  // [K], then U0 of the date [K][K + 1] (odd row stride)
+  double* us = g + K;
   const int d = blockIdx.x, tid = threadIdx.x;
   const bool ok = dvalid[d] != 0;
+  const double* u = U0 + (size_t)d * K * K;
+  if constexpr (STAGE)
+    for (int e = tid; e < K * K; e += blockDim.x) us[(e / K) * (K + 1) + e % K] = u[e];
   for (int k = tid; k < K; k += blockDim.x) {
     double s = 0.0;
     if (M_sum > 0) {
       s = vin[(size_t)d * K + k];
-    } else {
-      for (int m = 0; m < M; ++m) s += vin[((size_t)d * M + m) * K + k];
+    } else {  // same left-to-right sum; 8 loads in flight instead of one per dependent add
+      const double* vk = vin + (size_t)d * M * K + k;
+      int m = 0;
+      for (; m + 8 <= M; m += 8) {
+        double t[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) t[q] = vk[(size_t)(m + q) * K];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s += t[q];
+      }
+      for (; m < M; ++m) s += vk[(size_t)m * K];
     }
     double v = sqrt(s / (M_sum > 0 ? M_sum : M));
     v = scale * (v - 1.0) + 1.0;
@@ -2257,13 +2272,19 @@ __global__ __launch_bounds__(256) void eigen_finalize_kernel(const double* __res
     g[k] = ok ? v * v * D0[(size_t)d * K + k] : qnan();
   }
   __syncthreads();
-  const double* u = U0 + (size_t)d * K * K;
+  // the same fma order as before, from LDS (U0 was re-read from L1 / L2 for every entry)
   for (int e = tid; e < K * K; e += blockDim.x) {
     const int i = e / K, j = e % K;
+    const double* ui = STAGE ? us + i * (K + 1) : u + (size_t)i * K;
+    const double* uj = STAGE ? us + j * (K + 1) : u + (size_t)j * K;
     double s = 0.0;
-    for (int k = 0; k < K; ++k) s = fma(u[i * K + k] * g[k], u[j * K + k], s);
+    for (int k = 0; k < K; ++k) s = fma(ui[k] * g[k], uj[k], s);
     Fout[(size_t)d * K * K + e] = ok ? s : qnan();
   }
+}
+
+size_t eigen_finalize_lds(int K, bool stage) {
+  return ((size_t)K + (stage ? (size_t)K * (K + 1) : 0)) * sizeof(double);
 }
 
 int g_eigh_mode = 2;  // 0 = pair-block tournament Jacobi, 1 = row/column cyclic Jacobi (A/B),
@@ -2711,8 +2732,8 @@ MFA_API int mfa_eigen_adjust(const double* D0, const double* U0, const int* dval
     MFA_BIAS_LAUNCH(4)
   else
     MFA_BIAS_LAUNCH(9)
-  hipLaunchKernelGGL(eigen_finalize_kernel, dim3(D), dim3(256), K * sizeof(double), s, ws, D0, U0, dvalid, K, M,
-                     0, scale, Fout, vbias);
+  hipLaunchKernelGGL(eigen_finalize_kernel<true>, dim3(D), dim3(256), eigen_finalize_lds(K, true), s,
+                     ws, D0, U0, dvalid, K, M, 0, scale, Fout, vbias);
   return (int)hipGetLastError();
 }
 
@@ -2739,7 +2760,11 @@ MFA_API int mfa_eigen_finalize_sum(const double* S, int M_total, const double* D
                                    double* vbias, void* stream) {
   if (D <= 0) return 0;
   if (K < 1 || K > 4096 || M_total < 1) return (int)hipErrorInvalidValue;  // any K (LDS: K doubles)
-  hipLaunchKernelGGL(eigen_finalize_kernel, dim3(D), dim3(256), K * sizeof(double), (hipStream_t)stream, S, D0, U0,
-                     dvalid, K, 1, M_total, scale, Fout, vbias);
+  if (K <= 64)
+    hipLaunchKernelGGL(eigen_finalize_kernel<true>, dim3(D), dim3(256), eigen_finalize_lds(K, true),
+                       (hipStream_t)stream, S, D0, U0, dvalid, K, 1, M_total, scale, Fout, vbias);
+  else
+    hipLaunchKernelGGL(eigen_finalize_kernel<false>, dim3(D), dim3(256), eigen_finalize_lds(K, false),
+                       (hipStream_t)stream, S, D0, U0, dvalid, K, 1, M_total, scale, Fout, vbias);
   return (int)hipGetLastError();
 }
