@@ -114,7 +114,10 @@ def using_wide_bias_solver(name: str):
 # Per-(date, sim) solver of the bias statistic (csrc/eigen.hip): "tridiag" (mode 5, the default)
 # = Householder tridiagonalisation, count-guided Laguerre eigenvalues (division-free Sturm
 # recurrence), twisted-factorisation eigenvectors, back-transform, lean register / LDS layout;
-# "tridiag_chain" (mode 21, opt-in, ~3 % faster) = the same solver with each wave walking 8
+# "tridiag_chain" (mode 21, opt-in; ~3 % faster before round 5's eps ||T|| tolerance, level after
+# it, and now ~25 % SLOWER: its date loop keeps the 8-step reflector groups and 64-entry LDS
+# tables, which the default's 2-step groups / KP-entry tables outrun, profiles/r05) = the same
+# solver with each wave walking 8
 # consecutive dates of a sim, the Laguerre iteration of every eigenvalue rank started from the
 # previous date's (chains aligned to global multiples of 8 through ``date0``: bitwise
 # rank-invariant only for date shards that start on a chain boundary, e.g. sims sharding);
