@@ -112,7 +112,7 @@ def _need_solver(solver):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("solver", sorted(eigen.BIAS_SOLVERS))
-@pytest.mark.parametrize("K", [42, 5, 17, 64])
+@pytest.mark.parametrize("K", [42, 5, 17, 64, 37, 43])
 def test_hip_eigen_adjust_matches_reference_path(cuda, solver, K):
     _need_solver(solver)
     D, M = 12, 16
