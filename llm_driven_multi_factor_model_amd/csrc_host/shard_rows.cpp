@@ -131,20 +131,35 @@ extern "C" __attribute__((visibility("default"))) int64_t mfa_shard_rows_ix(
         if (klo >= khi) continue;
         int64_t s = std::max(a, klo - halo);
         if (end_dates && nstmt > 0) {
-          // walk back from klo until nstmt distinct end dates precede it
-          int runs = 0;
-          int64_t j = klo - 1;
-          int32_t prev = 0;
-          bool have = false;
-          for (; j >= a; --j) {
-            if (!have || end_dates[j] != prev) {
-              if (runs == nstmt) break;
-              ++runs;
-              prev = end_dates[j];
-              have = true;
+          // The TTM's run path (end_date non-decreasing within the stock, a missing (-1) end
+          // date ordered last) sums the nstmt most recent runs; any other order sends the TTM to
+          // the sort path, whose distinct statements come from ALL the stock's rows (a later
+          // restatement can sort before an owned row's end date): then the stock keeps its whole
+          // history [a, b); rows outside the owned dates are halo to the caller.
+          auto key = [](int32_t e) { return e < 0 ? (int64_t)INT32_MAX + 1 : (int64_t)e; };
+          bool mono = true;
+          for (int64_t j = a + 1; j < b && mono; ++j) mono = key(end_dates[j]) >= key(end_dates[j - 1]);
+          if (!mono) {
+            rg[2 * k] = a;
+            rg[2 * k + 1] = b;
+            keep[k] = 1;
+            continue;
+          } else {
+            // walk back from klo until nstmt distinct end dates precede it
+            int runs = 0;
+            int64_t j = klo - 1;
+            int32_t prev = 0;
+            bool have = false;
+            for (; j >= a; --j) {
+              if (!have || end_dates[j] != prev) {
+                if (runs == nstmt) break;
+                ++runs;
+                prev = end_dates[j];
+                have = true;
+              }
             }
+            s = std::min(s, j + 1);
           }
-          s = std::min(s, j + 1);
         }
         rg[2 * k] = s;
         rg[2 * k + 1] = khi;

@@ -766,6 +766,17 @@ def exposures(prices, index, sw_industry: pd.DataFrame, factor_cfg: FactorConfig
         else:
             full = sh  # global date axis (date_names, D) for the writers
         t["host_shard"] = getattr(sh, "host_shard_rows", None) is not None
+        if t["host_shard"] and sh._has_statements():
+            # a host shard forms the statement TTM on its own rows, so a statement with two
+            # values may sit in one rank's rows only: the fall-back decision is collective
+            # (one MAX over ranks) so no rank walks on into the collectives alone
+            bad = 0.0
+            try:
+                sh.cashflow_ttm()
+            except NeedsPandasPath:
+                bad = 1.0
+            if pdist.all_reduce_max(bad, ctx) > 0:
+                raise NeedsPandasPath("several cash-flow values for one (stock, end_date)")
         res = sh.compute(factors or FACTORS_TO_RUN)
         own = torch.nonzero(sh.own).flatten()
         res = {k: v[own] for k, v in res.items()}

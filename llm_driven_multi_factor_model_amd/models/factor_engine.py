@@ -329,9 +329,12 @@ class FactorEngine:
             return None
         cf = self.cashflow_ttm()
         mv = self.cols["total_mv"].double()
+        pe = self.cols["pe_ttm"].double()
+        rows = getattr(self, "_ttm_rows", None)
+        if rows is not None:  # merge-multiplied rows (see _ttm_by_merge)
+            mv, pe = mv[rows], pe[rows]
         nan = torch.full_like(mv, float("nan"))
         cetop = torch.where((mv > 0) & (cf > 0), cf / mv, nan)  # unit mix-up kept (quirk Q17)
-        pe = self.cols["pe_ttm"].double()
         etop = torch.where(pe > 0, 1.0 / pe, nan)
         return {"CETOP": cetop.float(), "ETOP": etop.float()}
 
@@ -402,8 +405,23 @@ class FactorEngine:
         fin["n_cashflow_act_ttm"] = ttm.double().cpu().numpy()
         tmp = m[["original_index", "ts_code", "end_date"]].merge(
             fin[["ts_code", "end_date", "n_cashflow_act_ttm"]], on=["ts_code", "end_date"], how="left")
-        tmp = tmp.sort_values("original_index", kind="stable")
+        tmp = tmp.sort_values("original_index")  # the reference's (unstable) default sort: same tie order
+        if len(tmp) != len(m):
+            # one statement with several values: the left merge multiplies its rows
+            # (factor_calculator.py:403-410) and run() repeats every other column with them
+            self._ttm_rows = torch.from_numpy(tmp["original_index"].to_numpy(np.int64)).to(self.device)
         return torch.from_numpy(tmp["n_cashflow_act_ttm"].to_numpy(np.float64, na_value=np.nan)).to(self.device)
+
+    def ttm_multiplies_rows(self) -> bool:
+        """True when the statement TTM merge multiplied rows (a statement with several values):
+        the descriptor frame then has more rows than the master, as in the reference."""
+        if not (self._need_quiet("n_cashflow_act") and self._has_statements()):
+            return False
+        self.cashflow_ttm()
+        return getattr(self, "_ttm_rows", None) is not None
+
+    def _need_quiet(self, *names) -> bool:
+        return all(n in self.cols for n in names)
 
     def select_growth_factors(self):
         if not self._need("q_profit_yoy", "q_sales_yoy"):
@@ -465,6 +483,17 @@ class FactorEngine:
         df = self.master[["ts_code", "trade_date"]].copy()
         df["ret"] = self.cols["ret"].double().cpu().numpy()
         df["circ_mv"] = self.master["circ_mv"].to_numpy(np.float64, na_value=np.nan) if "circ_mv" in self.master else np.nan
+        rows = getattr(self, "_ttm_rows", None)
+        if rows is not None:
+            # a statement with several values multiplied its rows in the TTM merge: every column
+            # repeats with them, as the reference's merges on original_index do (:561-566)
+            rc = rows.cpu().numpy()
+            df = df.iloc[rc].reset_index(drop=True)
+            for k, v in res.items():
+                df[k] = v.double().cpu().numpy() if v.numel() == len(rc) else v.double().cpu().numpy()[rc]
+            if self.own is not None:
+                df = df.loc[self.own.cpu().numpy()[rc]].reset_index(drop=True)
+            return df
         for k, v in res.items():
             df[k] = v.double().cpu().numpy()
         if self.own is not None:  # date shard: drop the halo rows
@@ -734,7 +763,10 @@ def factor_pipeline(prices_df, index_df, sw_industry_df, factors=None, config: F
     t0 = time.perf_counter()
     eng = FactorEngine(prices_df, index_df, device=device, config=cfg)
     if (columnar and eng.R == len(prices_df) and sw_industry_df["ts_code"].is_unique
-            and len(eng.master) == eng.R):
+            and len(eng.master) == eng.R and eng.grid_map().strict
+            and not eng.ttm_multiplies_rows()):
+        # (duplicate (stock, date) rows take the frame path: its per-date grids give every row
+        # a column of its own)
         t["prep_s"] = time.perf_counter() - t0
         final, info = _pipeline_columnar(eng, factors or FACTORS_TO_RUN, cfg, sw_industry_df, t)
         return final, info, dict(t, kernel_ms=getattr(eng, "timings", {}))

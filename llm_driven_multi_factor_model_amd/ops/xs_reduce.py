@@ -71,7 +71,7 @@ class GridMap:
     """Rows sorted by (stock, date) <-> a date-major [Dg, Ng] grid, as an LDS-tiled transpose
     (``csrc/gather.hip``, ``mfa_rows_grid``: 64-date x 64-stock tiles, coalesced on both
     sides).  ``sid`` / ``did`` [R]: each row's stock (< Ng) and date (< Dg), (sid, did) strictly
-    increasing.  ``toff`` [Ng, ceil(Dg / 64) + 1]: the first row of every (stock, 64-date
+    increasing (else the index fallback).  ``toff`` [Ng, ceil(Dg / 64) + 1]: the first row of every (stock, 64-date
     block), from the sorted key."""
 
     def __init__(self, sid: torch.Tensor, did: torch.Tensor, Dg: int, Ng: int):
@@ -84,6 +84,9 @@ class GridMap:
         self.did = did.to(torch.int32).contiguous()
         self.idx = did.to(torch.int64) * Ng + sid.to(torch.int64)   # flat cell (CPU path)
         self.Dg, self.Ng, self.R = int(Dg), int(Ng), int(sid.numel())
+        # the tile kernel covers one row per (stock, date) cell; duplicate cells (the pandas
+        # engine's fall-back input) take the index path (last row of a cell wins on scatter)
+        self.strict = self.R < 2 or bool((key[1:] > key[:-1]).all())
 
     def _cells(self, ds: int) -> torch.Tensor:
         return torch.div(self.idx, self.Ng, rounding_mode="floor") * ds + self.idx % self.Ng
@@ -103,7 +106,7 @@ class GridMap:
                                                    device=X.device)
         if G.dtype != X.dtype or not G.is_contiguous():
             raise ValueError("GridMap.scatter: contiguous grids of the rows' dtype")
-        if not X.is_cuda or self.R == 0:
+        if not X.is_cuda or self.R == 0 or not self.strict:
             cell = self._cells(ds)
             flat = G.view(-1)
             for c in range(Cn):
@@ -122,7 +125,7 @@ class GridMap:
         if not G.is_contiguous():
             raise ValueError("GridMap.gather: contiguous grids")
         X = torch.empty(C, self.R, dtype=G.dtype, device=G.device)
-        if not G.is_cuda or self.R == 0:
+        if not G.is_cuda or self.R == 0 or not self.strict:
             cell = self._cells(ds)
             flat = G.reshape(-1)
             for c in range(C):

@@ -133,17 +133,42 @@ def test_sharded_pipeline_equals_single_process_cpu(world):
     _compare(got, model, frame, info, rtol=1e-12, atol=1e-15, frame_rtol=1e-12, frame_atol=0)
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_host_shard_selection_equals_device_date_shard(world):
+def _restated(prices):
+    """Sorted loader rows with the two statement orders the TTM's run path does not cover
+    (ADVICE r05): a restatement (end_date moves backwards mid-history, a new statement key
+    with one value) and a mid-history run of missing end dates (one value); both send the
+    TTM to the sort path, whose statements can lie anywhere in the stock's history."""
+    p = prices.copy()
+    codes = p["ts_code"].unique()
+    for code, kind in ((codes[3], "restate"), (codes[9], "missing")):
+        rows = np.flatnonzero((p["ts_code"] == code).to_numpy())
+        mid = rows[int(len(rows) * 0.62):int(len(rows) * 0.66)]
+        col_e = p.columns.get_loc("end_date")
+        col_v = p.columns.get_loc("n_cashflow_act")
+        if kind == "restate":
+            p.iloc[mid, col_e] = p.iloc[mid[0], col_e] - pd.Timedelta(days=200)
+            p.iloc[mid, col_v] = 7.0e7
+        else:
+            p.iloc[mid, col_e] = pd.NaT
+            p.iloc[mid, col_v] = 5.0e7
+    return p
+
+
+@pytest.mark.parametrize("world,restated", [(2, False), (3, False), (3, True), (4, True)])
+def test_host_shard_selection_equals_device_date_shard(world, restated):
     """each rank selects its rows on the HOST (csrc_host/shard_rows.cpp) and
     builds only those.  Its owned rows carry the same global stock / date ids, columns and
-    descriptors as the full master's date_shard; it holds the halo (+ statement rows) only."""
+    descriptors as the full master's date_shard; it holds the halo (+ statement rows) only.
+    ``restated``: a restated stock and a mid-history missing end date keep their whole history,
+    so CETOP of the owned rows still equals the full panel's."""
     from llm_driven_multi_factor_model_amd.models.factor_engine import FACTORS_TO_RUN
     from llm_driven_multi_factor_model_amd.parallel.dist import shard_range
     from llm_driven_multi_factor_model_amd.utils.config import FactorConfig
     prices, index, _ = _data(sorted_rows=True)
+    if restated:
+        prices = _restated(prices)
     p, i = e2e._columns_from_frames(prices, index)
-    cfg = FactorConfig(rank_invariant=True)
+    cfg = FactorConfig()
     full = e2e.DeviceFactorEngine(p, i, device="cpu", config=cfg)
     for rank in range(world):
         lo, hi = shard_range(full.D, rank, world)
@@ -161,6 +186,8 @@ def test_host_shard_selection_equals_device_date_shard(world):
             a, b = ra[k][ia], rb[k][ib]
             assert torch.equal(a.isnan(), b.isnan()), k
             assert torch.equal(a.nan_to_num(0), b.nan_to_num(0)), k
+    if restated:
+        return
     # unsorted loader rows: no host selection (the caller builds the full master)
     pu, iu = e2e._columns_from_frames(*_data()[:2])
     assert e2e.DeviceFactorEngine.from_host_shard(pu, iu, 0, 2, "cpu", cfg) is None
@@ -314,3 +341,47 @@ def test_host_shard_row_ordinals():
         b = ref.row_ord[ref.own]
         assert torch.equal(a, b)
         assert int(got.row_ord.min()) >= 0
+
+
+def _multivalue_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MFA_DIST_TIMEOUT_S="120")
+    from llm_driven_multi_factor_model_amd.models import factor_engine as FE
+    from llm_driven_multi_factor_model_amd.parallel import dist as pdist
+    ctx = pdist.init_distributed(device="cpu")
+    prices, index, sw = _multivalue_data()
+    final, info, _ = FE.factor_pipeline(prices, index, sw, device="cpu", ctx=ctx)
+    if ctx.rank == 0:
+        final.to_csv(os.path.join(out_dir, "final.csv"), index=False)
+    else:
+        assert final is None
+    pdist.barrier(ctx)
+    torch.distributed.destroy_process_group()
+
+
+def _multivalue_data():
+    """Sorted loader rows where ONE statement row of one stock, late in the history (inside the
+    last rank's owned dates only, past every halo), carries a second cash-flow value."""
+    prices, index, sw = _data(sorted_rows=True)
+    code = prices["ts_code"].unique()[4]
+    rows = np.flatnonzero((prices["ts_code"] == code).to_numpy())
+    r = rows[int(len(rows) * 0.95)]
+    assert prices["end_date"].iloc[r] == prices["end_date"].iloc[r - 1]
+    prices.iloc[r, prices.columns.get_loc("n_cashflow_act")] *= 1.5
+    return prices, index, sw
+
+
+def test_multivalue_statement_in_one_shard_falls_back_on_every_rank():
+    """with host-side shard selection only the rank holding the two-valued statement
+    sees it; the fall-back to the pandas path is decided collectively, so both ranks leave the
+    device path together (no rank waits alone in a collective) and rank 0's whole-panel result
+    equals the single-process pipeline."""
+    from llm_driven_multi_factor_model_amd.models import factor_engine as FE
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(_multivalue_worker, args=(2, _free_port(), td), nprocs=2, join=True)
+        got = pd.read_csv(os.path.join(td, "final.csv"))
+        prices, index, sw = _multivalue_data()
+        ref, _, _ = FE.factor_pipeline(prices, index, sw, device="cpu")
+        ref.to_csv(os.path.join(td, "ref.csv"), index=False)
+        ref = pd.read_csv(os.path.join(td, "ref.csv"))
+    pd.testing.assert_frame_equal(got, ref)

@@ -63,6 +63,29 @@ def test_post_processing_pipeline_matches_reference(ref, ref_out, data):
                                    atol=5e-5, equal_nan=True, err_msg=col)
 
 
+@pytest.mark.reference
+def test_multivalued_statement_multiplies_rows_like_reference(ref, data):
+    """One (stock, end_date) statement with two cash-flow values: the reference's TTM left merge
+    (factor_calculator.py:403-410) multiplies those rows and run() carries the extra rows into
+    every column (:561-566); the engine reproduces the frame row for row."""
+    prices, index, _ = data
+    p = prices.copy()
+    r = int(np.flatnonzero((p["ts_code"] == p["ts_code"].iloc[0]).to_numpy())[200])
+    p.iloc[r, p.columns.get_loc("n_cashflow_act")] *= 1.5
+    warnings.simplefilter("ignore")
+    with contextlib.redirect_stdout(io.StringIO()), contextlib.redirect_stderr(io.StringIO()):
+        want = ref.factor_calculator.FactorCalculator(p.copy(), index.copy()).run(FE.FACTORS_TO_RUN)
+        got = FE.FactorEngine(p, index, device="cpu").run(FE.FACTORS_TO_RUN)
+    assert len(want) > len(p) and len(got) == len(want)
+    assert (got["ts_code"].values == want["ts_code"].values).all()
+    assert (got["trade_date"].values == want["trade_date"].values).all()
+    for c in ["ret", "CETOP", "ETOP", "BETA", "RSTR", "STOM"]:
+        a, b = got[c].to_numpy(np.float64), want[c].to_numpy(np.float64)
+        assert (np.isnan(a) == np.isnan(b)).all(), c
+        m = np.isfinite(b)
+        np.testing.assert_allclose(a[m], b[m], rtol=2e-4, atol=1e-6, err_msg=c)
+
+
 def test_barra_export_schema(data):
     prices, index, sw = data
     with contextlib.redirect_stdout(io.StringIO()):

@@ -145,3 +145,41 @@ def test_grid_map_transpose_equals_index_scatter(cuda, dtype):
         assert torch.equal(P[did, q, sid].cpu(), X[q])
     assert int(torch.isfinite(P).sum()) == C * R
     assert torch.equal(gm.gather(P.view(-1), C, gs=Ng, ds=Q * Ng).cpu(), X)
+
+
+@pytest.mark.gpu
+def test_grid_map_duplicate_rows_take_index_path(cuda):
+    """the tile kernel covers one row per (stock, date) cell.  A stock with a
+    duplicated row inside a fully populated 64-date block (the pandas engine's fall-back input)
+    makes the map non-strict: scatter / gather then take the index path, so no row is left out
+    of the gather (every row reads its cell) -- identical to the CPU map."""
+    from llm_driven_multi_factor_model_amd.ops import xs_reduce as XR
+    Dg, Ng = 130, 5
+    sid, did = torch.nonzero(torch.ones(Ng, Dg, dtype=torch.bool), as_tuple=True)
+    dup = 2 * Dg + 10                                       # stock 2, date 10: full 64-date block
+    sid = torch.cat([sid[:dup + 1], sid[dup:dup + 1], sid[dup + 1:]])
+    did = torch.cat([did[:dup + 1], did[dup:dup + 1], did[dup + 1:]])
+    X = torch.randn(2, sid.numel(), dtype=torch.float32)
+    X[:, dup + 1] = X[:, dup]                              # same values: the winner is irrelevant
+    gm = XR.GridMap(sid.to(cuda), did.to(cuda), Dg, Ng)
+    gc = XR.GridMap(sid, did, Dg, Ng)
+    assert not gm.strict and not gc.strict
+    G = gm.scatter(X.to(cuda))
+    assert torch.equal(G.cpu().nan_to_num(7.0), gc.scatter(X).nan_to_num(7.0))
+    assert torch.equal(gm.gather(G, 2).cpu(), X)
+
+
+def test_factor_pipeline_duplicate_rows_columnar_equals_frame_path():
+    """Duplicate (stock, date) rows: the single-process pipeline routes them to the frame path
+    (its per-date grids give each row its own column), whichever ``columnar`` says."""
+    import contextlib
+    import io
+    from llm_driven_multi_factor_model_amd.models import factor_engine as FE
+    prices, index, sw = FE.synthetic_prices(N=8, T=140, seed=4)
+    prices = pd.concat([prices, prices.iloc[[300]]]).reset_index(drop=True)
+    with contextlib.redirect_stdout(io.StringIO()):
+        a, ia, _ = FE.factor_pipeline(prices, index, sw, device="cpu", columnar=True)
+        b, ib, _ = FE.factor_pipeline(prices, index, sw, device="cpu", columnar=False)
+    assert len(a) == len(prices)
+    pd.testing.assert_frame_equal(a, b)
+    pd.testing.assert_frame_equal(ia, ib)
