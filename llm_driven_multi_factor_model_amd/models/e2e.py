@@ -440,7 +440,7 @@ class DeviceFactorEngine(FactorEngine):
         vb = vf[inv]
         if not bool(((v == vb) | (v.isnan() & vb.isnan())).all()):
             raise NeedsPandasPath("several cash-flow values for one (stock, end_date)")
-        with RL.direct_kernels(self._direct()):
+        with RL.direct_kernels():   # newest-first sums, as the run kernel (ttm_rows)
             self._ttm = RL.rolling_sum(vf.float(), RL.seg_lo_from_codes(seg_codes), 4, 4).double()[inv]
         return self._ttm
 
@@ -747,12 +747,9 @@ def exposures(prices, index, sw_industry: pd.DataFrame, factor_cfg: FactorConfig
         prices, index = _columns_from_frames(prices, index)
     if ctx is not None and ctx.enabled and device is None:
         device = ctx.device
-    # a date-sharded run computes its rolling descriptors rank-invariantly by default (direct
-    # per-row window kernels): it then equals a single-process run with rank_invariant=True bit
-    # for bit at any world size.  A single process defaults to the faster tile kernels (the
-    # same values to fp32 rounding).
-    dist_on = ctx is not None and ctx.enabled
-    factor_cfg = factor_cfg or FactorConfig(rank_invariant=dist_on)
+    # the rolling descriptors are rank-invariant by construction (segment-anchored kernels on
+    # every path): a date-sharded run equals the single-process run bit for bit at any world size
+    factor_cfg = factor_cfg or FactorConfig()
     if ctx is not None and ctx.enabled:
         from ..parallel import dist as pdist
         # each rank selects, uploads and builds only its rows (host-side selection from the

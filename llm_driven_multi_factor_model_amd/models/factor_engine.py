@@ -150,13 +150,15 @@ class FactorEngine:
 
     # ---------------------------------------------------------------- date sharding (DP + halo)
     def halo_rows(self) -> int:
-        """Rows of history any descriptor of this config reads before an output row; with
-        ``rank_invariant`` at least 2 x 256 - 1, so the aligned tile (256-row halo + 256 rows)
-        holding a shard's first owned row lies inside the slice."""
+        """Rows of a stock's history before an output row that the row's descriptors depend on:
+        each window's reach back to the anchor of its segment-anchored kernel (ops.rolling
+        ``*_reach``: 566 for RSTR's 504-row reach and 64-row segments).  A date shard that holds
+        them computes its owned rows bit for bit as the full panel does."""
         c = self.cfg
-        h = max(c.beta_window, c.rstr_window, c.dastd_window, c.cmra_window,
-                c.stom[0], c.stoq[0], c.stoa[0])
-        return max(h, 2 * RL.ALIGN) if getattr(c, "rank_invariant", False) else h
+        return max(RL.ew_reach(c.beta_window), RL.ew_reach(c.dastd_window),
+                   RL.pos_reach(c.rstr_window - c.rstr_lag, c.rstr_lag),
+                   RL.cmra_reach(c.cmra_window, c.cmra_partial),
+                   *(RL.pos_reach(w) for w, _ in (c.stom, c.stoq, c.stoa)))
 
     @property
     def row_ord(self) -> torch.Tensor:
@@ -176,12 +178,17 @@ class FactorEngine:
             gm = self._grid_map = XR.GridMap(self.stock_id, self.date_id, self.D, self.N)
         return gm
 
-    def aligned_layout(self):
-        """The virtual row layout of the rank-invariant BETA / DASTD tiles
-        (:func:`ops.rolling.aligned_layout`), built once per engine."""
-        lay = getattr(self, "_aligned", None)
+    def seg_layout(self) -> "RL.SegLayout":
+        """The segment layout of the rolling descriptors (:class:`ops.rolling.SegLayout`, keyed
+        by the rows' full-history ordinals), built once per engine with its virtual input
+        series shared by every descriptor; None off the GPU."""
+        if self.device.type != "cuda":
+            return None
+        lay = getattr(self, "_seg", None)
         if lay is None:
-            lay = self._aligned = RL.aligned_layout(self.seg_lo, self.row_ord)
+            # the rolling descriptors' four input series placed in the layout's own pass
+            ser = [self.cols.get(c) for c in ("ret", "market_ret", "log_ret", "turnover_rate")]
+            lay = self._seg = RL.SegLayout(self.seg_lo, self.row_ord, series=ser)
         return lay
 
     def date_shard(self, lo: int, hi: int, halo: int | None = None) -> "FactorEngine":
@@ -240,7 +247,7 @@ class FactorEngine:
         sub.grid_idx = sub.date_id.long() * sub.N + sub.stock_id.long()
         sub.cols = {k: v[idx] for k, v in self.cols.items()}
         sub._row_ord = self.row_ord[idx]
-        sub._aligned = None
+        sub._seg = None
         sub._grid_map = None
         ttm = getattr(self, "_ttm", None)
         sub._ttm = None if ttm is None else ttm[idx]
@@ -271,24 +278,23 @@ class FactorEngine:
     def compute_beta_hsigma(self):
         c = self.cfg
         b, h = RL.beta_hsigma(self.cols["ret"], self.cols["market_ret"], self.seg_lo, c.beta_window,
-                              c.beta_half_life, c.beta_min_periods,
-                              row_ord=self.aligned_layout() if self._direct() else None)
+                              c.beta_half_life, c.beta_min_periods, row_ord=self.seg_layout())
         return {"BETA": b, "HSIGMA": h}
 
     def compute_rstr(self):
         c = self.cfg
         return {"RSTR": RL.rstr(self.cols["log_ret"], self.seg_lo, c.rstr_window, c.rstr_lag,
-                                c.rstr_half_life, c.rstr_min_periods)}
+                                c.rstr_half_life, c.rstr_min_periods, row_ord=self.seg_layout())}
 
     def compute_dastd(self):
         c = self.cfg
         return {"DASTD": RL.dastd(self.cols["ret"], self.cols["market_ret"], self.seg_lo, c.dastd_window,
-                                  c.dastd_half_life, c.dastd_min_periods,
-                                  row_ord=self.aligned_layout() if self._direct() else None)}
+                                  c.dastd_half_life, c.dastd_min_periods, row_ord=self.seg_layout())}
 
     def compute_cmra(self):
         c = self.cfg
-        return {"CMRA": RL.cmra(self.cols["log_ret"], self.seg_lo, c.cmra_window, c.cmra_partial)}
+        return {"CMRA": RL.cmra(self.cols["log_ret"], self.seg_lo, c.cmra_window, c.cmra_partial,
+                                row_ord=self.seg_layout())}
 
     def compute_nlsize(self):
         # per date: -residual of SIZE^3 on [1, SIZE], SIZE = ln(total_mv) formed in fp64 in-kernel
@@ -306,11 +312,10 @@ class FactorEngine:
         if not self._need("turnover_rate"):
             return None
         c = self.cfg
-        tr = self.cols["turnover_rate"]
-        out = {}
-        for name, (w, mp) in (("STOM", c.stom), ("STOQ", c.stoq), ("STOA", c.stoa)):
-            out[name] = RL.rolling_sum(tr, self.seg_lo, w, mp, scale=0.01, log=True)
-        return out
+        # the three turnover sums in one pass of the segment-anchored kernel
+        sums = RL.window_sums(self.cols["turnover_rate"], self.seg_lo, [c.stom, c.stoq, c.stoa],
+                              scale=0.01, log=True, row_ord=self.seg_layout())
+        return dict(zip(("STOM", "STOQ", "STOA"), sums))
 
     def _has_statements(self) -> bool:
         return "n_cashflow_act" in self.cols and "end_date" in self.master.columns
@@ -357,7 +362,7 @@ class FactorEngine:
         if not same.all():
             return None
         seg = RL.seg_lo_from_codes(torch.from_numpy(uk // (ne + 1))).to(self.device)
-        with RL.direct_kernels(self._direct()):
+        with RL.direct_kernels():   # newest-first sums, as the run kernel (ttm_rows)
             ttm = RL.rolling_sum(torch.from_numpy(vf.astype(np.float32)).to(self.device), seg, 4, 4)
         return ttm.double()[torch.from_numpy(inv).to(self.device)]
 
@@ -390,7 +395,7 @@ class FactorEngine:
         if not bool(((v == vb) | (v.isnan() & vb.isnan())).all()):
             return None
         seg = RL.seg_lo_from_codes(sc[first].to(torch.int32))
-        with RL.direct_kernels(self._direct()):
+        with RL.direct_kernels():
             ttm = RL.rolling_sum(vf.float(), seg, 4, 4)
         return ttm.double()[inv]
 
@@ -400,7 +405,7 @@ class FactorEngine:
         codes = torch.from_numpy(pd.factorize(fin["ts_code"].astype(str))[0].astype(np.int32))
         seg = RL.seg_lo_from_codes(codes).to(self.device)
         v = torch.from_numpy(fin["n_cashflow_act"].to_numpy(np.float32, na_value=np.nan)).to(self.device)
-        with RL.direct_kernels(self._direct()):
+        with RL.direct_kernels():
             ttm = RL.rolling_sum(v, seg, 4, 4)  # statement-row TTM (quirk Q18)
         fin["n_cashflow_act_ttm"] = ttm.double().cpu().numpy()
         tmp = m[["original_index", "ts_code", "end_date"]].merge(
@@ -451,23 +456,17 @@ class FactorEngine:
         "GROWTH": "select_growth_factors", "LEVERAGE": "compute_leverage",
     }
 
-    def _direct(self) -> bool:
-        """Direct per-row rolling kernels (FactorConfig.rank_invariant) on the GPU."""
-        return bool(getattr(self.cfg, "rank_invariant", False)) and self.device.type == "cuda"
-
     def compute(self, factors: list[str]) -> dict:
         """Run factor groups; returns ordered {column: flat tensor}."""
         out = {}
         self.timings = {}
-        direct = self._direct()
         for name in factors:
             meth = self.METHODS.get(name.upper())
             if meth is None:
                 print(f"Warning: Factor '{name}' not found.")
                 continue
             t0 = time.perf_counter()
-            with RL.direct_kernels(direct):
-                res = getattr(self, meth)()
+            res = getattr(self, meth)()
             if self.device.type == "cuda":
                 torch.cuda.synchronize(self.device)
             self.timings[name.upper()] = (time.perf_counter() - t0) * 1e3

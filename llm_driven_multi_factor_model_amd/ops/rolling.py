@@ -17,29 +17,59 @@ import torch
 from .. import _native
 
 _vp, _i, _d = C.c_void_p, C.c_int, C.c_double
+# direct per-row kernels (reference kernels, fallback beyond the segment kernels' limits)
 _native.register("mfa_beta_hsigma", [_vp, _vp, _vp, _i, _i, _d, _i, _vp, _vp, _vp])
 _native.register("mfa_rstr", [_vp, _vp, _i, _i, _i, _d, _i, _vp, _vp])
 _native.register("mfa_dastd", [_vp, _vp, _vp, _i, _i, _d, _i, _vp, _vp])
 _native.register("mfa_cmra", [_vp, _vp, _i, _i, _i, _vp, _vp])
 _native.register("mfa_rolling_sum", [_vp, _vp, _i, _i, _i, _d, _i, _vp, _vp])
+# segment-anchored kernels on the segment layout (the production path)
+_native.register("mfa_beta_hsigma_seg", [_vp, _vp, _vp, _vp, _i, _i, _d, _i, _vp, _vp, _vp])
+_native.register("mfa_dastd_seg", [_vp, _vp, _vp, _vp, _i, _i, _d, _i, _vp, _vp])
+_native.register("mfa_rstr_seg", [_vp, _vp, _vp, _i, _i, _i, _d, _i, _vp, _vp])
+_native.register("mfa_window_sums_seg", [_vp, _vp, _vp, _i, _i, _vp, _vp, _d, _i, _vp, _vp, _vp, _vp])
+_native.register("mfa_cmra_seg", [_vp, _vp, _vp, _i, _i, _vp, _vp])
+_native.register("mfa_seg_count", [_vp, _vp, _i, _vp, _vp])
+_native.register("mfa_seg_place", [_vp, _vp, _vp, _i, _i, _vp, _vp, _i, _vp, _vp, _vp])
 _native.register("mfa_returns", [_vp, _vp, _i, _vp, _vp, _vp])
 _native.register("mfa_ttm_flags", [_vp, _vp, _vp, _i, _vp, _vp, _vp])
 _native.register("mfa_ttm_finish", [_vp, _vp, _vp, _vp, _i, _vp, _vp, _vp, _vp])
 _native.register("mfa_leverage", [_vp, _vp, _vp, _i, _vp, _vp, _vp])
-_native.register("mfa_rolling_set_mode", [_i])
-_native.register("mfa_beta_hsigma_aligned", [_vp, _vp, _vp, _i, _i, _d, _i, _vp, _vp, _vp])
-_native.register("mfa_dastd_aligned", [_vp, _vp, _vp, _i, _i, _d, _i, _vp, _vp])
 
-ALIGN = 256      # rank-invariant EW kernels: tiles on global multiples of 256 rows
-ALIGN_MAX_W = 255
+# Segment layout (csrc/rolling.hip, "segment-anchored window kernels"): every stock's rows sit
+# at virtual positions B_s + t - T0_s, t = the row's ordinal in the stock's FULL history, B_s and
+# T0_s multiples of ALIGN, so the kernels' anchor segments fall on fixed ordinals whatever slice
+# of the history a launch holds.
+ALIGN = 256        # virtual block size (stock histories padded to multiples of it)
+EW_SEG = 256       # BETA / DASTD anchor segments (prefixes anchored one segment back)
+POS_SEG = 64       # RSTR / window sums / CMRA anchor segments (the window's first row's segment)
+EW_MAX_W = 256     # segment kernels' window limits; larger windows take the direct kernels
+POS_MAX_REACH = 512
+CMRA_MIN_W, CMRA_MAX_W = 65, 257
+
+
+def ew_reach(window: int) -> int:
+    """Rows of a stock's history before an output row that BETA / DASTD of that row depend on
+    (the anchor: the start of the 256-row segment before the row's own)."""
+    return 2 * EW_SEG - 1 if window <= EW_MAX_W else window - 1
+
+
+def pos_reach(window: int, lag: int = 0) -> int:
+    """The same for a positional window over sources [r - window + 1 - lag, r - lag] (RSTR,
+    the turnover sums): its first source's 64-row segment."""
+    r = window + lag - 1
+    return r + POS_SEG - 1 if r <= POS_MAX_REACH else r
+
+
+def cmra_reach(window: int, partial: bool = False) -> int:
+    seg = not partial and CMRA_MIN_W <= window <= CMRA_MAX_W
+    return window - 1 + (POS_SEG - 1 if seg else 0)
 
 
 def aligned_layout(seg_lo: torch.Tensor, row_ord: torch.Tensor):
-    """Virtual row layout of the rank-invariant EW kernels (csrc/rolling.hip,
-    mfa_beta_hsigma_aligned): the rows of each stock at B_s + t - T0_s, t = ``row_ord`` (the
-    row's ordinal in the stock's FULL history), T0_s = t_first rounded down to a multiple of
-    ALIGN, B_s = multiples of ALIGN.  Returns (v [R] int64 virtual position of every row,
-    seg_v [Rv] int32 virtual seg_lo, Rv)."""
+    """The segment layout's index vectors: (v [R] int64 virtual position of every row,
+    seg_v [Rv] int32 virtual stock start of every virtual position -- a padding position is its
+    own start --, Rv)."""
     dev = seg_lo.device
     R = seg_lo.numel()
     sl = seg_lo.long()
@@ -62,38 +92,97 @@ def aligned_layout(seg_lo: torch.Tensor, row_ord: torch.Tensor):
     return v, seg_v, Rv
 
 
-def _layout(seg_lo, row_ord):
-    """``row_ord`` is either the ordinals or an :func:`aligned_layout` built from them (an
-    engine builds it once for BETA and DASTD)."""
-    return tuple(row_ord) if isinstance(row_ord, tuple) else aligned_layout(seg_lo, row_ord)
+class SegLayout:
+    """The segment layout of a set of flat stock-sorted rows (built once per engine and shared
+    by every descriptor): ``seg_v`` [Rv] virtual stock starts, ``omap`` [Rv] the real row of
+    every virtual position (-1 on padding), and :meth:`virt` -- a series in virtual positions
+    (NaN padding), cached per source tensor.  ``row_ord``: each row's ordinal in its stock's
+    full history (default: the rows ARE the full histories).  ``series``: float32 [R] tensors
+    placed in the same pass as the layout (GPU: csrc/rolling.hip seg_count / seg_place, three
+    row-parallel kernels around one int32 prefix sum)."""
+
+    def __init__(self, seg_lo: torch.Tensor, row_ord: torch.Tensor | None = None, series=()):
+        seg_lo = _i32(seg_lo)
+        R = seg_lo.numel()
+        dev = seg_lo.device
+        self.R = R
+        self._virt = {}
+        if dev.type != "cuda":
+            if row_ord is None:
+                row_ord = torch.arange(R, device=dev, dtype=torch.int32) - seg_lo
+            self.v, self.seg_v, self.Rv = aligned_layout(seg_lo, row_ord)
+            self.omap = torch.full((self.Rv,), -1, dtype=torch.int32, device=dev)
+            self.omap[self.v] = torch.arange(R, device=dev, dtype=torch.int32)
+            for x in series:
+                self.virt(x)
+            return
+        ro = None if row_ord is None else _i32(row_ord)
+        st = _native.stream(dev)
+        nb = torch.empty(R, dtype=torch.int32, device=dev)
+        _native.call("mfa_seg_count", _native.ptr(seg_lo), _native.ptr(ro), R, _native.ptr(nb), st)
+        incl = torch.cumsum(nb, 0, dtype=torch.int32)
+        self.Rv = int(incl[-1]) * ALIGN if R else 0   # the one host read
+        self.seg_v = torch.empty(self.Rv, dtype=torch.int32, device=dev)
+        self.omap = torch.empty(self.Rv, dtype=torch.int32, device=dev)
+        self._ro, self._incl, self._seg_lo = ro, incl, seg_lo   # for virt() of later series
+        series = [x for x in series if x is not None]
+        for k in range(0, max(len(series), 1), 4):
+            self._place(series[k:k + 4], first=k == 0)
+
+    def _place(self, xs, first: bool) -> None:
+        """GPU: place up to 4 series (and, on the first call, the layout vectors themselves)."""
+        dev = self.seg_v.device
+        srcs = [_f(x) for x in xs]
+        dsts = [torch.empty(self.Rv, dtype=torch.float32, device=dev) for _ in xs]
+        sv, om = (self.seg_v, self.omap) if first else (None, None)   # None: series only
+        S = (C.c_void_p * 4)(*[x.data_ptr() for x in srcs], *[0] * (4 - len(srcs)))
+        D = (C.c_void_p * 4)(*[x.data_ptr() for x in dsts], *[0] * (4 - len(dsts)))
+        _native.call("mfa_seg_place", _native.ptr(self._seg_lo), _native.ptr(self._ro),
+                     _native.ptr(self._incl), self.R, self.Rv, _native.ptr(sv), _native.ptr(om),
+                     len(xs), C.cast(S, _vp), C.cast(D, _vp), _native.stream(dev))
+        for x, d in zip(xs, dsts):
+            self._virt[id(x)] = (x, d)   # the source stays referenced: its id cannot be reused
+
+    def virt(self, x: torch.Tensor) -> torch.Tensor:
+        hit = self._virt.get(id(x))
+        if hit is not None and hit[0] is x:
+            return hit[1]
+        if x.is_cuda:
+            self._place([x], first=False)
+            return self._virt[id(x)][1]
+        out = torch.full((self.Rv,), float("nan"), dtype=torch.float32, device=x.device)
+        out[self.v] = x.to(torch.float32)
+        self._virt[id(x)] = (x, out)
+        return out
 
 
-def _to_virtual(x: torch.Tensor, v: torch.Tensor, Rv: int) -> torch.Tensor:
-    out = torch.full((Rv,), float("nan"), dtype=torch.float32, device=x.device)
-    out[v] = x
-    return out
+def _layout(seg_lo, row_ord) -> SegLayout:
+    """``row_ord``: None (the rows are full histories), ordinals, or a ready :class:`SegLayout`."""
+    return row_ord if isinstance(row_ord, SegLayout) else SegLayout(seg_lo, row_ord)
 
 
 def _f(t):
     return t.to(torch.float32).contiguous()
 
 
+_DIRECT = [False]
+
+
 @contextlib.contextmanager
 def direct_kernels(on: bool = True):
-    """GPU rolling descriptors from the direct per-row window kernels (``mfa_rolling_set_mode(1)``)
-    inside the block: every output row is a fixed-order sum over its own window, so a row's
-    value does not depend on which other rows share its launch (date shards reproduce the full
-    panel bitwise).  No-op without a GPU or with ``on=False``."""
-    if not (on and torch.cuda.is_available()):
-        yield
-        return
-    lib = _native.lib()
-    if lib.mfa_rolling_set_mode(1) != 0:
-        raise _native.NativeError("mfa_rolling_set_mode(1) failed")
+    """Run the GPU descriptors on the direct per-row kernels inside the block (every row sums
+    its own window in one fixed order: the tests' reference kernels).  Nests: the previous
+    setting comes back on exit."""
+    prev = _DIRECT[0]
+    _DIRECT[0] = bool(on)
     try:
         yield
     finally:
-        lib.mfa_rolling_set_mode(0)
+        _DIRECT[0] = prev
+
+
+def _seg_path(x: torch.Tensor) -> bool:
+    return x.is_cuda and x.numel() > 0 and not _DIRECT[0]
 
 
 def _i32(t):
@@ -145,22 +234,25 @@ def returns(close, seg_lo):
 
 # ---------------------------------------------------------------- BETA / HSIGMA
 def beta_hsigma(ret, mret, seg_lo, window=252, half_life=63.0, min_periods=42, row_ord=None):
-    """``row_ord`` (GPU, window <= 255): the rows' ordinals in their stocks' full histories (or
-    their :func:`aligned_layout`) -- the rank-invariant aligned-tile kernel on the virtual
-    layout (a date shard reproduces the full panel bit for bit)."""
-    ret, mret, seg_lo = _f(ret), _f(mret), _i32(seg_lo)
+    """GPU: the segment-anchored kernel (window <= 256) on the segment layout of ``row_ord``
+    (None = the rows are full histories; ordinals; or a :class:`SegLayout`), else the direct
+    per-row kernel.  Either way a row's value depends only on its stock's rows from its anchor
+    on: a date shard holding :func:`ew_reach` rows before its first owned row reproduces the
+    full-panel outputs bit for bit."""
     R = ret.numel()
     lam = 0.5 ** (1.0 / half_life)
-    if ret.is_cuda and row_ord is not None and window <= ALIGN_MAX_W and R:
-        v, seg_v, Rv = _layout(seg_lo, row_ord)
-        bv = torch.empty(Rv, dtype=torch.float32, device=ret.device)
-        hv = torch.empty_like(bv)
+    if _seg_path(ret) and window <= EW_MAX_W:
+        lay = _layout(seg_lo, row_ord)
+        b = torch.empty(R, dtype=torch.float32, device=ret.device)
+        h = torch.empty_like(b)
         # bound to names: a temporary passed as ptr(...) is freed before the launch, and the
         # caching allocator then hands its block to the next temporary (the inputs alias)
-        yv, xv = _to_virtual(ret, v, Rv), _to_virtual(mret, v, Rv)
-        _native.call("mfa_beta_hsigma_aligned", _native.ptr(yv), _native.ptr(xv), _native.ptr(seg_v), Rv, window, lam,
-                     min_periods, _native.ptr(bv), _native.ptr(hv), _native.stream(ret.device))
-        return bv[v].contiguous(), hv[v].contiguous()
+        yv, xv = lay.virt(ret), lay.virt(mret)
+        _native.call("mfa_beta_hsigma_seg", _native.ptr(yv), _native.ptr(xv), _native.ptr(lay.seg_v),
+                     _native.ptr(lay.omap), lay.Rv, window, lam, min_periods, _native.ptr(b),
+                     _native.ptr(h), _native.stream(ret.device))
+        return b, h
+    ret, mret, seg_lo = _f(ret), _f(mret), _i32(seg_lo)
     if ret.is_cuda:
         b, h = torch.empty_like(ret), torch.empty_like(ret)
         _native.call("mfa_beta_hsigma", _native.ptr(ret), _native.ptr(mret), _native.ptr(seg_lo), R,
@@ -188,11 +280,20 @@ def beta_hsigma(ret, mret, seg_lo, window=252, half_life=63.0, min_periods=42, r
 
 
 # ---------------------------------------------------------------- RSTR
-def rstr(log_ret, seg_lo, T=504, L=21, half_life=126.0, min_periods=42):
-    lr, seg_lo = _f(log_ret), _i32(seg_lo)
-    R = lr.numel()
+def rstr(log_ret, seg_lo, T=504, L=21, half_life=126.0, min_periods=42, row_ord=None):
+    """GPU: the segment-anchored positional-window kernel (reach T - 1 <= 512) on the segment
+    layout of ``row_ord`` (see :func:`beta_hsigma`), else the direct kernel."""
+    R = log_ret.numel()
     W = T - L
     lam = 0.5 ** (1.0 / half_life)
+    if _seg_path(log_ret) and W >= 1 and L >= 0 and W + L - 1 <= POS_MAX_REACH:
+        lay = _layout(seg_lo, row_ord)
+        out = torch.empty(R, dtype=torch.float32, device=log_ret.device)
+        xv = lay.virt(log_ret)
+        _native.call("mfa_rstr_seg", _native.ptr(xv), _native.ptr(lay.seg_v), _native.ptr(lay.omap),
+                     lay.Rv, L, W, lam, min_periods, _native.ptr(out), _native.stream(out.device))
+        return out
+    lr, seg_lo = _f(log_ret), _i32(seg_lo)
     if lr.is_cuda:
         out = torch.empty_like(lr)
         _native.call("mfa_rstr", _native.ptr(lr), _native.ptr(seg_lo), R, L, W, lam, min_periods,
@@ -214,17 +315,18 @@ def rstr(log_ret, seg_lo, T=504, L=21, half_life=126.0, min_periods=42):
 
 # ---------------------------------------------------------------- DASTD
 def dastd(ret, mret, seg_lo, window=252, half_life=42.0, min_periods=42, row_ord=None):
-    """``row_ord``: the rank-invariant aligned-tile kernel (see :func:`beta_hsigma`)."""
-    ret, mret, seg_lo = _f(ret), _f(mret), _i32(seg_lo)
+    """GPU: the segment-anchored kernel (see :func:`beta_hsigma`)."""
     R = ret.numel()
     lam = 0.5 ** (1.0 / half_life)
-    if ret.is_cuda and row_ord is not None and window <= ALIGN_MAX_W and R:
-        v, seg_v, Rv = _layout(seg_lo, row_ord)
-        ov = torch.empty(Rv, dtype=torch.float32, device=ret.device)
-        yv, xv = _to_virtual(ret, v, Rv), _to_virtual(mret, v, Rv)   # named: see beta_hsigma
-        _native.call("mfa_dastd_aligned", _native.ptr(yv), _native.ptr(xv), _native.ptr(seg_v), Rv, window, lam,
-                     min_periods, _native.ptr(ov), _native.stream(ret.device))
-        return ov[v].contiguous()
+    if _seg_path(ret) and window <= EW_MAX_W:
+        lay = _layout(seg_lo, row_ord)
+        out = torch.empty(R, dtype=torch.float32, device=ret.device)
+        yv, xv = lay.virt(ret), lay.virt(mret)   # named: see beta_hsigma
+        _native.call("mfa_dastd_seg", _native.ptr(yv), _native.ptr(xv), _native.ptr(lay.seg_v),
+                     _native.ptr(lay.omap), lay.Rv, window, lam, min_periods, _native.ptr(out),
+                     _native.stream(ret.device))
+        return out
+    ret, mret, seg_lo = _f(ret), _f(mret), _i32(seg_lo)
     if ret.is_cuda:
         out = torch.empty_like(ret)
         _native.call("mfa_dastd", _native.ptr(ret), _native.ptr(mret), _native.ptr(seg_lo), R, window,
@@ -247,9 +349,19 @@ def dastd(ret, mret, seg_lo, window=252, half_life=42.0, min_periods=42, row_ord
 
 
 # ---------------------------------------------------------------- CMRA
-def cmra(log_ret, seg_lo, window=252, partial=False):
+def cmra(log_ret, seg_lo, window=252, partial=False, row_ord=None):
+    """GPU: full windows with 64 < window <= 257 take the segment-anchored kernel on the
+    segment layout of ``row_ord`` (see :func:`beta_hsigma`); the partial-window variant (quirk
+    Q15) and other windows the direct kernel (rank-invariant too)."""
+    R = log_ret.numel()
+    if _seg_path(log_ret) and not partial and CMRA_MIN_W <= window <= CMRA_MAX_W:
+        lay = _layout(seg_lo, row_ord)
+        out = torch.empty(R, dtype=torch.float32, device=log_ret.device)
+        xv = lay.virt(log_ret)
+        _native.call("mfa_cmra_seg", _native.ptr(xv), _native.ptr(lay.seg_v), _native.ptr(lay.omap),
+                     lay.Rv, window, _native.ptr(out), _native.stream(out.device))
+        return out
     lr, seg_lo = _f(log_ret), _i32(seg_lo)
-    R = lr.numel()
     if lr.is_cuda:
         out = torch.empty_like(lr)
         _native.call("mfa_cmra", _native.ptr(lr), _native.ptr(seg_lo), R, window, int(partial),
@@ -275,7 +387,33 @@ def cmra(log_ret, seg_lo, window=252, partial=False):
 
 
 # ---------------------------------------------------------------- rolling sums (liquidity)
-def rolling_sum(x, seg_lo, window, min_periods, scale=1.0, log=False):
+def window_sums(x, seg_lo, windows, scale=1.0, log=False, row_ord=None):
+    """Several NaN-skipping window sums of ``x * scale`` (``windows``: [(window, min_periods)],
+    at most 3 per pass; ``log``: ln(sum), a zero sum -> NaN) -- STOM / STOQ / STOA in one pass
+    of the segment-anchored kernel.  Returns a list of tensors."""
+    R = x.numel()
+    windows = [(int(w), int(m)) for w, m in windows]
+    if not _seg_path(x) or any(w < 1 or w - 1 > POS_MAX_REACH for w, _ in windows):
+        return [rolling_sum(x, seg_lo, w, m, scale, log) for w, m in windows]
+    lay = _layout(seg_lo, row_ord)
+    xv = lay.virt(x)
+    outs = []
+    for k in range(0, len(windows), 3):
+        grp = windows[k:k + 3]
+        o = [torch.empty(R, dtype=torch.float32, device=x.device) for _ in grp]
+        W = (C.c_int * 3)(*[w for w, _ in grp], *[0] * (3 - len(grp)))
+        M = (C.c_int * 3)(*[m for _, m in grp], *[0] * (3 - len(grp)))
+        op = [_native.ptr(t) for t in o] + [None] * (3 - len(o))
+        _native.call("mfa_window_sums_seg", _native.ptr(xv), _native.ptr(lay.seg_v), _native.ptr(lay.omap),
+                     lay.Rv, len(grp), C.cast(W, _vp), C.cast(M, _vp), float(scale), int(log), *op,
+                     _native.stream(x.device))
+        outs += o
+    return outs
+
+
+def rolling_sum(x, seg_lo, window, min_periods, scale=1.0, log=False, row_ord=None):
+    if _seg_path(x) and 1 <= window and window - 1 <= POS_MAX_REACH:
+        return window_sums(x, seg_lo, [(window, min_periods)], scale, log, row_ord)[0]
     x, seg_lo = _f(x), _i32(seg_lo)
     R = x.numel()
     if x.is_cuda:

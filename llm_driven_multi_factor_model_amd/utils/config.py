@@ -66,15 +66,6 @@ class FactorConfig:
     stoq: tuple = (63, 42)
     stoa: tuple = (252, 126)
     winsor_n_std: float = 2.5
-    # GPU rolling descriptors from the direct per-row window kernels (each output row summed over
-    # its own window, newest to oldest, in a fixed order) instead of the anchored-prefix /
-    # van Herk tile kernels, whose rounding depends on where the tile grid falls in the flat
-    # rows: a date-sharded run (date_shard + halo) then reproduces the single-process
-    # descriptors BIT FOR BIT at any world size.  The date-sharded e2e pipeline (run_factors /
-    # run_pipeline / cli under torchrun) turns it on by default; a single process uses the
-    # faster tile kernels unless asked (same values to fp32 rounding; +13 ms of kernels at
-    # 5000 x 2520, profiles/r05/README.md).
-    rank_invariant: bool = False
     composite: dict = field(default_factory=lambda: {
         "volatility": {"components": ["DASTD", "CMRA", "HSIGMA"], "weights": [0.7, 0.15, 0.15]},
         "leverage": {"components": ["MLEV", "DTOA", "BLEV"], "weights": [1 / 3, 1 / 3, 1 / 3]},

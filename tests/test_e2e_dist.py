@@ -8,8 +8,8 @@ single-process ``run_pipeline`` to 1e-12: factor returns, R^2, specific returns,
 eigen / VRA series, lambda, and the barra_data_csi.csv frame gathered to rank 0.
 
 The GPU variant (``-m gpu``) rehearses the same job with several gloo ranks on one MI355X
-(``MFA_DIST_BACKEND=gloo``) and requires bitwise equality: the pipeline's descriptors are
-rank-invariant (FactorConfig.rank_invariant, direct per-row window kernels).
+(``MFA_DIST_BACKEND=gloo``) and requires bitwise equality against the DEFAULT single-process
+run: the rolling descriptors are rank-invariant by construction (segment-anchored kernels).
 """
 import os
 import socket
@@ -96,12 +96,10 @@ def _run(world, device, scan="gather", sorted_rows=False):
 
 
 def _reference(device):
-    from llm_driven_multi_factor_model_amd.utils.config import FactorConfig
     prices, index, sw = _data()
-    # the sharded job's default descriptor kernels (rank_invariant) on one process
+    # the default single-process job (no factor config: the same kernels as every shard)
     model, info, frame, _ = e2e.run_pipeline(prices, index, sw, risk_cfg=_cfg(), device=device,
-                                             want_barra=True,
-                                             factor_cfg=FactorConfig(rank_invariant=True))
+                                             want_barra=True)
     with tempfile.TemporaryDirectory() as td:  # the same CSV round trip as the ranks' frame
         frame.to_csv(os.path.join(td, "f.csv"), index=False)
         info.to_csv(os.path.join(td, "i.csv"), index=False)
@@ -246,8 +244,8 @@ def test_owned_engine_local_grid():
 def test_sharded_pipeline_gloo_rehearsal_on_one_gpu(cuda, world, sorted_rows):
     """2 / 3 gloo ranks sharing one MI355X (the RCCL path needs one GPU per rank): every output
     -- factor returns, R^2, specific returns, the Newey-West / eigen / VRA series, lambda and
-    the barra frame -- is BITWISE the single-process run: rank-invariant descriptors (direct
-    window kernels), per-date regression / post-processing, the full-series Newey-West scan,
+    the barra frame -- is BITWISE the default single-process run: rank-invariant descriptors
+    (segment-anchored kernels), per-date regression / post-processing, the full-series Newey-West scan,
     per-date eigen adjustment and the block-partitioned VRA."""
     model, frame, info = _reference("cuda:0")
     got = _run(world, "cuda", sorted_rows=sorted_rows)   # sorted rows: host-side selection
@@ -310,7 +308,7 @@ def test_host_shard_device_gather_equals_host_gather(cuda):
     from llm_driven_multi_factor_model_amd.utils.config import FactorConfig
     prices, index, _ = _data(sorted_rows=True)
     p, i = e2e._columns_from_frames(prices, index)
-    cfg = FactorConfig(rank_invariant=True)
+    cfg = FactorConfig()
     pinned = e2e.stage_host_columns(dict(p), pinned=True)
     pageable = e2e.stage_host_columns(dict(p), pinned=False)
     for rank in range(3):
@@ -330,7 +328,7 @@ def test_host_shard_row_ordinals():
     from llm_driven_multi_factor_model_amd.utils.config import FactorConfig
     prices, index, _ = _data(sorted_rows=True)
     p, i = e2e._columns_from_frames(prices, index)
-    cfg = FactorConfig(rank_invariant=True)
+    cfg = FactorConfig()
     full = e2e.DeviceFactorEngine(p, i, device="cpu", config=cfg)
     for rank in range(3):
         got = e2e.DeviceFactorEngine.from_host_shard(p, i, rank, 3, "cpu", cfg)

@@ -115,10 +115,7 @@ def test_hip_rolling_kernels_match_cpu(cuda):
 
 @pytest.mark.gpu
 def test_hip_sliding_window_kernels_match_direct(cuda):
-    """O(1)-per-row sliding kernels == the direct per-row kernels (suspensions, stock edges)."""
-    import ctypes as C
-    from llm_driven_multi_factor_model_amd import _native
-    _native.register("mfa_rolling_set_mode", [C.c_int])
+    """Segment-anchored kernels == the direct per-row kernels (suspensions, stock edges)."""
     g = torch.Generator().manual_seed(4)
     N, T = 37, 700                      # T not a multiple of the 64-row chunk
     R = N * T
@@ -143,13 +140,9 @@ def test_hip_sliding_window_kernels_match_direct(cuda):
         "cmra": lambda: RL.cmra(l_, seg, 252),
         "cmra_partial": lambda: RL.cmra(l_, seg, 252, partial=True),
     }
-    try:
-        _native.lib().mfa_rolling_set_mode(1)
+    with RL.direct_kernels():
         direct = {k: f() for k, f in fns.items()}
-        _native.lib().mfa_rolling_set_mode(0)
-        scan = {k: f() for k, f in fns.items()}
-    finally:
-        _native.lib().mfa_rolling_set_mode(0)
+    scan = {k: f() for k, f in fns.items()}
     del lens
     for k in fns:
         a = direct[k] if isinstance(direct[k], tuple) else (direct[k],)
@@ -193,10 +186,9 @@ def test_hip_descriptors_match_reference_fixture_n50_t800(cuda):
 @pytest.mark.gpu
 def test_hip_rolling_kernels_large_ragged_panel(cuda):
     """500 stocks with ragged histories of 300..9000 rows (2.3 M flat rows; many stocks longer
-    than the 4096-row LDS block, stock starts anywhere inside blocks), 2 % suspensions: the
-    default kernels == the direct per-row kernels, and the anchored-prefix BETA / DASTD ==
-    the round-1 sliding-window kernels."""
-    from llm_driven_multi_factor_model_amd import _native
+    than a 2048-row tile, stock starts anywhere inside tiles), 2 % suspensions: the default
+    (segment-anchored) kernels == the direct per-row kernels, including the three turnover sums
+    of one window_sums pass."""
     g = torch.Generator().manual_seed(11)
     N = 500
     lens = torch.randint(300, 9000, (N,), generator=g)
@@ -223,25 +215,19 @@ def test_hip_rolling_kernels_large_ragged_panel(cuda):
         "stoa": lambda: RL.rolling_sum(t_, seg, 252, 126, 0.01, log=True),
         "cmra": lambda: RL.cmra(l_, seg, 252),
         "cmra_partial": lambda: RL.cmra(l_, seg, 252, partial=True),
+        "sto3": lambda: tuple(RL.window_sums(t_, seg, [(21, 15), (63, 42), (252, 126)], 0.01, log=True)),
     }
-    lib = _native.lib()
-    out = {}
-    modes = (1, 2, 0) if _native.ab_build() else (1, 0)   # 2 = round-1 kernels: A/B builds
-    try:
-        for mode in modes:
-            lib.mfa_rolling_set_mode(mode)
-            out[mode] = {k: f() for k, f in fns.items()}
-    finally:
-        lib.mfa_rolling_set_mode(0)
+    with RL.direct_kernels():
+        direct = {k: f() for k, f in fns.items()}
+        direct["sto3"] = (direct["stom"], RL.rolling_sum(t_, seg, 63, 42, 0.01, log=True), direct["stoa"])
+    fast = {k: f() for k, f in fns.items()}
     for k in fns:
-        for ref_mode in modes[:-1]:
-            a = out[ref_mode][k] if isinstance(out[ref_mode][k], tuple) else (out[ref_mode][k],)
-            b = out[0][k] if isinstance(out[0][k], tuple) else (out[0][k],)
-            for x, y in zip(a, b):
-                # full-window CMRA needs 252 NaN-free rows: rare at 2 % suspensions
-                assert int(torch.isfinite(x).sum()) > (1000 if k == "cmra" else R // 2), k
-                torch.testing.assert_close(y.cpu(), x.cpu(), rtol=2e-5, atol=2e-7, equal_nan=True,
-                                           msg=f"{k} vs mode {ref_mode}")
+        a = direct[k] if isinstance(direct[k], tuple) else (direct[k],)
+        b = fast[k] if isinstance(fast[k], tuple) else (fast[k],)
+        for x, y in zip(a, b):
+            # full-window CMRA needs 252 NaN-free rows: rare at 2 % suspensions
+            assert int(torch.isfinite(x).sum()) > (1000 if k == "cmra" else R // 2), k
+            torch.testing.assert_close(y.cpu(), x.cpu(), rtol=2e-5, atol=2e-7, equal_nan=True, msg=k)
 
 
 def _pipeline_paths_equal(device):
@@ -317,12 +303,11 @@ def test_cetop_ttm_run_path_equals_merge_path_and_falls_back():
 
 @pytest.mark.gpu
 def test_hip_cmra_rstr_window_edges(cuda):
-    """The van Herk CMRA and backward-anchored RSTR kernels at the edges of their window ranges
-    (CMRA W = 65 / 128 / 129 / 257: just above one 64-row block, the last window of the one-row-
-    per-lane kernel, the first of the two-rows-per-lane kernel (a window spanning exactly two
-    128-row blocks), the 256-row halo; RSTR reach W + L - 1 =
-    512 = the halo, W = 1, L = 1) == the direct per-row kernels, on ragged stocks with NaNs."""
-    from llm_driven_multi_factor_model_amd import _native
+    """The segment-anchored CMRA and RSTR kernels at the edges of their window ranges (CMRA W =
+    65 / 128 / 129 / 200 / 257: just above one 64-row segment, whole segments, the 256-row tile
+    halo; RSTR reach W + L - 1 = 512 = its tile halo, W = 1, L = 1, a short half-life; a sum
+    window of 513 rows = the 512 reach) == the direct per-row kernels, on ragged stocks with
+    NaNs."""
     g = torch.Generator().manual_seed(21)
     lens = torch.randint(30, 3000, (300,), generator=g)
     R = int(lens.sum())
@@ -340,85 +325,93 @@ def test_hip_cmra_rstr_window_edges(cuda):
         "rstr_max_reach": lambda: RL.rstr(l_, seg, 512, 21, 126.0, 42),
         "rstr_w1": lambda: RL.rstr(l_, seg, 2, 1, 5.0, 1),
         "rstr_short_hl": lambda: RL.rstr(l_, seg, 100, 3, 2.0, 10),
+        "sum513": lambda: RL.rolling_sum(l_.abs(), seg, 513, 10),
+        "sum1": lambda: RL.rolling_sum(l_, seg, 1, 1),
     }
-    lib = _native.lib()
-    try:
-        lib.mfa_rolling_set_mode(1)
+    with RL.direct_kernels():
         direct = {k: f() for k, f in fns.items()}
-        lib.mfa_rolling_set_mode(0)
-        fast = {k: f() for k, f in fns.items()}
-    finally:
-        lib.mfa_rolling_set_mode(0)
+    fast = {k: f() for k, f in fns.items()}
     for k in fns:
         assert int(torch.isfinite(direct[k]).sum()) > R // 4, k
         torch.testing.assert_close(fast[k].cpu(), direct[k].cpu(), rtol=2e-5, atol=2e-7, equal_nan=True, msg=k)
 
 
 @pytest.mark.gpu
-def test_rolling_ew_variant12_bitwise_default(cuda, ab_lib):
-    """A/B library only: ew variant 12 moves the chunk-map scan to DPP row shifts /
-    row broadcasts, composing with the identity map where a lane has no source.  Same maps in
-    the same association order as variant 0: bitwise the same BETA / HSIGMA / DASTD on a ragged
-    panel (short stocks, NaN rows, windows crossing stock starts)."""
-    from llm_driven_multi_factor_model_amd.ops import rolling as RL
-    g = torch.Generator().manual_seed(12)
-    lens = torch.randint(1, 900, (400,), generator=g)
-    lens[:5] = torch.tensor([1, 7, 64, 255, 2049])
+def test_seg_kernels_rank_invariant(cuda):
+    """Every segment-anchored descriptor (BETA/HSIGMA, DASTD, RSTR, CMRA, the turnover sums) on
+    a ragged panel: a slice of every stock that starts halo_rows() rows (or fewer, at the stock
+    start) before its first output row, with the rows' full-history ordinals, reproduces the
+    full-panel outputs BIT FOR BIT -- a shard boundary anywhere relative to the segments."""
+    from llm_driven_multi_factor_model_amd.utils.config import FactorConfig
+    g = torch.Generator().manual_seed(21)
+    lens = torch.randint(300, 2600, (60,), generator=g)
+    lens[:4] = torch.tensor([1, 40, 700, 2049])
     R = int(lens.sum())
     stock = torch.repeat_interleave(torch.arange(lens.numel(), dtype=torch.int32), lens)
     ret = (torch.randn(R, generator=g) * 0.02).float()
-    ret[torch.rand(R, generator=g) < 0.03] = float("nan")
+    ret[torch.rand(R, generator=g) < 0.002] = float("nan")
     mret = (torch.randn(R, generator=g) * 0.012).float()
+    lr = torch.log1p(ret)
+    turn = torch.rand(R, generator=g) * 5
+    turn[torch.rand(R, generator=g) < 0.1] = 0.0
     seg = RL.seg_lo_from_codes(stock).to(cuda)
-    r_, m_ = ret.to(cuda), mret.to(cuda)
-    out = {}
-    try:
-        for v in (0, 12):
-            assert ab_lib.mfa_rolling_set_ew_variant(v) == 0
-            out[v] = (*RL.beta_hsigma(r_, m_, seg, 252, 63.0, 42), RL.dastd(r_, m_, seg, 252, 42.0, 42))
-    finally:
-        ab_lib.mfa_rolling_set_ew_variant(0)
-    for a, b in zip(out[0], out[12]):
-        assert torch.equal(a.nan_to_num(7.0), b.nan_to_num(7.0))
+    r_, m_, l_, t_ = (x.to(cuda) for x in (ret, mret, lr, turn))
+    ordv = torch.arange(R, device=cuda, dtype=torch.int32) - seg
+
+    def run(r, m, lg, tt, sg, ro):
+        lay = RL.SegLayout(sg, ro)
+        out = [*RL.beta_hsigma(r, m, sg, 252, 63.0, 42, row_ord=lay),
+               RL.dastd(r, m, sg, 252, 42.0, 42, row_ord=lay),
+               RL.rstr(lg, sg, 504, 21, 126.0, 42, row_ord=lay),
+               RL.cmra(lg, sg, 252, row_ord=lay),
+               *RL.window_sums(tt, sg, [(21, 15), (63, 42), (252, 126)], 0.01, log=True, row_ord=lay)]
+        return out
+
+    full = run(r_, m_, l_, t_, seg, ordv)
+    halo = FE.FactorEngine.halo_rows(type("C", (), {"cfg": FactorConfig()})())
+    assert halo == 566
+    starts = torch.cumsum(lens, 0) - lens
+    for trial in range(3):
+        keep, own = [], []
+        for s_, n_ in zip(starts.tolist(), lens.tolist()):
+            o = int(torch.randint(0, n_, (1,), generator=g))
+            t0 = max(0, o - halo)
+            keep.append(torch.arange(s_ + t0, s_ + n_))
+            own.append(torch.arange(s_ + o, s_ + n_))
+        keep = torch.cat(keep).to(cuda)
+        own = torch.cat(own).to(cuda)
+        sseg = RL.seg_lo_from_codes(stock.to(cuda)[keep])
+        part = run(r_[keep], m_[keep], l_[keep], t_[keep], sseg, ordv[keep])
+        pos = torch.searchsorted(keep, own)   # owned rows inside the slice
+        for k, (a, b) in enumerate(zip(full, part)):
+            assert int(torch.isfinite(a[own]).sum()) > own.numel() // 4, k
+            assert torch.equal(a[own].nan_to_num(7.0), b[pos].nan_to_num(7.0)), (trial, k)
 
 
 @pytest.mark.gpu
-def test_aligned_ew_kernels_rank_invariant(cuda):
-    """rank_invariant BETA/HSIGMA and DASTD (aligned 512-row tiles on the virtual layout keyed by
-    each row's ordinal in its stock's full history): equal to the tile kernels to fp32 rounding,
-    and a slice of every stock that starts 512 rows (or fewer, at the stock start) before its
-    first output row reproduces those outputs BIT FOR BIT."""
-    from llm_driven_multi_factor_model_amd.ops import rolling as RL
-    g = torch.Generator().manual_seed(21)
-    lens = torch.randint(300, 2600, (60,), generator=g)
-    lens[:3] = torch.tensor([1, 40, 700])
+def test_seg_layout_kernels_equal_torch_build(cuda):
+    """The GPU segment layout (seg_count / seg_place kernels around one prefix sum) equals the
+    tensor-op build: the same Rv, virtual stock starts, output map and NaN-padded series, for
+    full histories and for a slice whose rows start mid-history (ordinals not multiples of
+    256, one stock with a gap in its ordinals)."""
+    g = torch.Generator().manual_seed(3)
+    lens = torch.randint(1, 1500, (40,), generator=g)
+    lens[:3] = torch.tensor([1, 256, 257])
     R = int(lens.sum())
     stock = torch.repeat_interleave(torch.arange(lens.numel(), dtype=torch.int32), lens)
-    ret = (torch.randn(R, generator=g) * 0.02).float()
-    ret[torch.rand(R, generator=g) < 0.03] = float("nan")
-    mret = (torch.randn(R, generator=g) * 0.012).float()
-    seg = RL.seg_lo_from_codes(stock).to(cuda)
-    r_, m_ = ret.to(cuda), mret.to(cuda)
-    ordv = (torch.arange(R, device=cuda, dtype=torch.int32) - seg)
-    b, h = RL.beta_hsigma(r_, m_, seg, 252, 63.0, 42, row_ord=ordv)
-    d = RL.dastd(r_, m_, seg, 252, 42.0, 42, row_ord=ordv)
-    bt, ht = RL.beta_hsigma(r_, m_, seg, 252, 63.0, 42)
-    dt = RL.dastd(r_, m_, seg, 252, 42.0, 42)
-    for a, t in ((b, bt), (h, ht), (d, dt)):
-        torch.testing.assert_close(a, t, rtol=2e-5, atol=2e-7, equal_nan=True)
-    # slices: per stock rows [t0, end) with t0 = max(0, own - 512), own = a random output start
-    starts = torch.cumsum(lens, 0) - lens
-    keep, own = [], []
-    for s_, n_ in zip(starts.tolist(), lens.tolist()):
-        o = int(torch.randint(0, n_, (1,), generator=g))
-        t0 = max(0, o - 512)
-        keep.append(torch.arange(s_ + t0, s_ + n_))
-        own.append(torch.arange(s_ + o, s_ + n_))
-    keep = torch.cat(keep).to(cuda)
-    own = torch.cat(own).to(cuda)
-    sseg = RL.seg_lo_from_codes(stock.to(cuda)[keep])
-    sb, sh = RL.beta_hsigma(r_[keep], m_[keep], sseg, 252, 63.0, 42, row_ord=ordv[keep])
-    sd = RL.dastd(r_[keep], m_[keep], sseg, 252, 42.0, 42, row_ord=ordv[keep])
-    pos = torch.searchsorted(keep, own)   # owned rows inside the slice
-    for full, part in ((b, sb), (h, sh), (d, sd)):
-        assert torch.equal(full[own].nan_to_num(7.0), part[pos].nan_to_num(7.0))
+    seg = RL.seg_lo_from_codes(stock)
+    x = torch.randn(R, generator=g)
+    y = torch.randn(R, generator=g)
+    ordv = torch.arange(R, dtype=torch.int32) - seg
+    keep = torch.nonzero((ordv % 7 != 3) | (stock != 5)).flatten()   # stock 5: ordinal gaps
+    keep = keep[ordv[keep] >= (stock[keep] % 3) * 300]               # slices start mid-history
+    cases = [(seg, None, x, y), (RL.seg_lo_from_codes(stock[keep]), ordv[keep], x[keep], y[keep])]
+    for sl, ro, a, b in cases:
+        cpu = RL.SegLayout(sl, ro if ro is not None else torch.arange(sl.numel(), dtype=torch.int32) - sl)
+        gpu = RL.SegLayout(sl.to(cuda), None if ro is None else ro.to(cuda), series=[a.to(cuda)])
+        assert gpu.Rv == cpu.Rv
+        assert torch.equal(gpu.seg_v.cpu(), cpu.seg_v) and torch.equal(gpu.omap.cpu(), cpu.omap)
+        ag = gpu._virt[next(iter(gpu._virt))][1]
+        assert torch.equal(ag.cpu().nan_to_num(7.0), cpu.virt(a).nan_to_num(7.0))
+        bg = gpu.virt(b.to(cuda))   # a later series-only pass
+        assert torch.equal(bg.cpu().nan_to_num(7.0), cpu.virt(b).nan_to_num(7.0))

@@ -3,8 +3,7 @@
 Every rank generates the same synthetic loader frames (stand-in for reading the loader CSVs),
 runs ``e2e.run_pipeline(..., ctx)`` on its date block + halo, and the risk model over the ranks'
 blocks.  Prints one JSON line per timed repetition with the slowest rank's phase times; rank 0
-then reruns the whole panel in one process with the sharded job's rank-invariant descriptors
-(FactorConfig(rank_invariant=True)) and prints the max differences of the gathered outputs and
+then reruns the whole panel in one process with the DEFAULT config and prints the max differences of the gathered outputs and
 whether each is bitwise equal.  Sorted loader rows: every rank selects and uploads only its rows
 (DeviceFactorEngine.from_host_shard).
 
@@ -68,10 +67,8 @@ def main():
     got = {k: pdist.gather_to_root(getattr(model, k).contiguous(), ctx) for k in KEYS}
     note("gathered")
     if ctx.rank == 0:
-        from llm_driven_multi_factor_model_amd.utils.config import FactorConfig
         one, _, _, t1 = e2e.run_pipeline(dict(cols[0]), dict(cols[1]), sw, risk_cfg=cfg,
-                                         device=ctx.device,
-                                         factor_cfg=FactorConfig(rank_invariant=True))
+                                         device=ctx.device)
         diff = {}
         for k in KEYS:
             a, b = got[k], getattr(one, k)

@@ -3,8 +3,7 @@ on synthetic loader frames held in memory (non-I/O time only).
 
     python tools/pipeline_e2e.py [N] [T]      # default 5000 x 2520
 
-Timed with the pipeline's rank-invariant descriptors (default) and with the tile kernels.
-Prints one JSON line per timed run: descriptors (device factor engine incl. its host prep),
+The descriptors are the rank-invariant segment-anchored kernels (the only GPU path).  Prints one JSON line per timed run: descriptors (device factor engine incl. its host prep),
 exposures -> RiskPanel scatter, RiskModel.run (all four stages), their sum (non_io_s).
 """
 import json
@@ -35,20 +34,15 @@ cols = (e2e.stage_host_columns(cols[0]), cols[1])   # the native reader's output
 print(json.dumps({"stage_host_s": round(time.perf_counter() - t0, 3)}), flush=True)
 small_p, small_i, small_sw = FE.synthetic_prices(N=60, T=300, seed=1, n_ind=31)
 e2e.run_pipeline(small_p, small_i, small_sw, device=dev)  # warm-up: kernel load, allocator
-from llm_driven_multi_factor_model_amd.utils.config import FactorConfig  # noqa: E402
-# rank_invariant=True is the pipeline default (direct window kernels: a date-sharded run equals
-# one process bitwise); False = the tile kernels (faster, fp32-rounding-equal)
 from llm_driven_multi_factor_model_amd.utils import native_io  # noqa: E402
-# reps 4 / 5: the same columns without the reader's row-group index (the key-based build:
+# reps 3 / 4: the same columns without the reader's row-group index (the key-based build:
 # S16 codes uploaded, device unique of codes and dates)
-for rep, ri, ixd in ((0, True, True), (1, True, True), (2, False, True), (3, False, True),
-                     (4, False, False), (5, False, False)):
+for rep, ixd in ((0, True), (1, True), (2, True), (3, False), (4, False)):
     pc = dict(cols[0]) if ixd else {k: v for k, v in cols[0].items() if k != native_io.ROW_INDEX}
     t0 = time.perf_counter()
-    model, info, _, t = e2e.run_pipeline(pc, dict(cols[1]), sw, device=dev,
-                                         factor_cfg=FactorConfig(rank_invariant=ri))
+    model, info, _, t = e2e.run_pipeline(pc, dict(cols[1]), sw, device=dev)
     wall = time.perf_counter() - t0
-    rec = {"N": N, "T": T, "D": model.panel.D, "K": model.K, "rep": rep, "rank_invariant": ri,
+    rec = {"N": N, "T": T, "D": model.panel.D, "K": model.K, "rep": rep,
            "row_index": ixd and native_io.ROW_INDEX in cols[0],
            **{k: round(v, 4) for k, v in t.items() if k.endswith("_s")}, "wall_s": round(wall, 4)}
     rec["non_io_s"] = round(sum(v for k, v in t.items() if k.endswith("_s")), 4)

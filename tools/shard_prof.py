@@ -35,7 +35,7 @@ p["trade_date"] = p["trade_date"].astype("int32")
 if "end_date" in p:
     p["end_date"] = p["end_date"].astype("int32")
 p = e2e.stage_host_columns(p)
-cfg = FactorConfig(rank_invariant=True)
+cfg = FactorConfig()
 small = FE.synthetic_prices(N=60, T=300, seed=1, n_ind=31)
 e2e.run_pipeline(*small, device=dev)
 
