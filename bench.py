@@ -96,17 +96,21 @@ def main() -> int:
                                                                      xs_wls_workspace)
 
     N, P, Q = args.stocks, args.industries, args.styles
+
+    def block(G):
+        """This rank's balanced contiguous share of G global dates (ranks past G % world get
+        one date fewer; with G < world some own none) and the largest share (gather rows)."""
+        base, rem = divmod(G, world)
+        return base + (1 if rank < rem else 0), base + (1 if rem else 0)
+
     if args.scaling == "strong":  # fixed global problem: this rank's contiguous date block
-        base, rem = divmod(args.dates, world)
-        if rem:
-            raise SystemExit(f"--scaling strong needs --dates divisible by the world size {world}")
-        D = base
+        D, Dpad = block(args.dates)
     else:
-        D = args.dates
+        D, Dpad = args.dates, args.dates
     K = 1 + P + Q
     sdt = torch.float64 if args.storage == "fp64" else torch.float32
-    panel = synthetic_panel(D, N, P, Q, seed=1234 + rank, device=dev, missing_frac=0.01,
-                            dtype=sdt)
+    panel = synthetic_panel(max(D, Dpad, 1), N, P, Q, seed=1234 + rank, device=dev,
+                            missing_frac=0.01, dtype=sdt)
 
     def sync():
         if use_cuda:
@@ -114,25 +118,34 @@ def main() -> int:
         if coll:
             dist.barrier()
 
-    def make_runner(Dl):
+    def make_runner(Dl, Dpad=None):
         """Step closure over the first ``Dl`` dates of the panel (a contiguous view).
 
         Two output / gather buffers: step i's RCCL all-gather of the factor-return series runs
         on the collective stream underneath step i+1's regression (the write of buffer i%2 at
         step i+2 first waits for that gather).  Every collective completes inside the timed
-        region (``drain``)."""
+        region (``drain``).  ``Dpad`` > ``Dl`` (an uneven strong split): every rank gathers
+        ``Dpad`` rows, its factor returns copied into a zero-padded send buffer inside the step;
+        a rank with no date only takes part in the gather."""
+        Dpad = Dl if Dpad is None else Dpad
         sty, cap, ret = panel.styles[:Dl], panel.cap[:Dl], panel.ret[:Dl]
         ind = None if panel.ind is None else panel.ind[:Dl]
         NB = 2 if coll else 1
-        gathered = [torch.empty(world * Dl, K, dtype=torch.float64, device=dev)
+        gathered = [torch.empty(world * Dpad, K, dtype=torch.float64, device=dev)
                     for _ in range(NB)] if coll else None
+        send = [torch.zeros(Dpad, K, dtype=torch.float64, device=dev)
+                for _ in range(NB)] if coll and Dpad != Dl else None
         outs, handles, graphs = [None] * NB, [None] * NB, [None] * NB
-        ws = xs_wls_workspace(Dl, P, Q, dev, N) if use_cuda else None
+        ws = xs_wls_workspace(Dl, P, Q, dev, N) if use_cuda and Dl else None
         it = [0]
 
         def regress(b):
+            if Dl == 0:
+                return
             outs[b] = xs_wls(sty, cap, ret, ind, P, want_resid=not args.no_resid, refine=True,
                              out=outs[b], workspace=ws)
+            if send is not None:
+                send[b][:Dl].copy_(outs[b].f)
 
         def drain():
             for b in range(NB):
@@ -151,11 +164,12 @@ def main() -> int:
             else:
                 regress(b)
             if coll:
-                handles[b] = dist.all_gather_into_tensor(gathered[b], outs[b].f, async_op=True)
+                src = send[b] if send is not None else outs[b].f
+                handles[b] = dist.all_gather_into_tensor(gathered[b], src, async_op=True)
 
         for b in range(NB):
             regress(b)
-        if use_cuda and not args.no_graph:
+        if use_cuda and not args.no_graph and Dl:
             # The kernel of a step is captured once per buffer into a HIP graph and replayed:
             # the same work, without per-launch host overhead.  The RCCL all-gather stays eager.
             # thread_local capture: the process group's watchdog thread keeps polling the events
@@ -193,7 +207,7 @@ def main() -> int:
     # Setup (prewarm): bring the GPU to its steady-state clocks (a cold MI355X runs the first
     # ~100 steps ~10 % slower: 0.308 vs 0.278 ms/step measured).  Same step, same count on every
     # rank (the all-gathers pair up), all before the W warmup steps and the timed region.
-    step, drain, outs = make_runner(D)
+    step, drain, outs = make_runner(D, Dpad)
     el = timed(step, drain, args.prewarm, args.warmup, args.steps)
     out = outs[0]
 
@@ -203,14 +217,12 @@ def main() -> int:
     strong = None
     G = args.strong_dates if args.strong_dates is not None else args.dates
     if G > 0 and args.scaling == "weak":
-        if G % world:
-            raise SystemExit(f"--strong-dates {G} must be divisible by the world size {world}")
-        Ds = G // world
-        if Ds > D:
-            raise SystemExit(f"--strong-dates {G} needs {Ds} dates per rank, the panel has {D}")
-        s_step, s_drain, _ = make_runner(Ds)
+        Ds, Dsp = block(G)
+        if Dsp > D:
+            raise SystemExit(f"--strong-dates {G} needs {Dsp} dates per rank, the panel has {D}")
+        s_step, s_drain, _ = make_runner(Ds, Dsp)
         s_el = timed(s_step, s_drain, max(1, args.prewarm // 4), args.warmup, args.steps)
-        strong = {"global_dates": G, "dates_per_gpu": Ds, "steps": args.steps,
+        strong = {"global_dates": G, "dates_per_gpu": Dsp, "steps": args.steps,
                   "ms_per_step": round(s_el / args.steps * 1e3, 4),
                   "value": round(G * args.steps / s_el, 1), "unit": "regressions/s"}
 
@@ -222,8 +234,9 @@ def main() -> int:
         print(f"check: max |f - oracle| = {err:.3e}", file=sys.stderr)
         assert err < 1e-9
 
-    chunks = _native.query("mfa_xs_chunks", D, (N + 7) // 8 * 8) if use_cuda else 1
-    regs = world * D * args.steps  # == --dates * steps under strong scaling
+    chunks = _native.query("mfa_xs_chunks", max(D, 1), (N + 7) // 8 * 8) if use_cuda else 1
+    # regressions actually run: every rank's dates (== --dates * steps under strong scaling)
+    regs = (args.dates if args.scaling == "strong" else world * D) * args.steps
     value = regs / el
     ms = el / args.steps * 1e3
     if rank == 0:
@@ -244,11 +257,11 @@ def main() -> int:
             "config": {
                 "model": f"Barra CS-WLS: 1 country + {P} SW-L1 industries + {Q} styles, "
                          "industry-neutral constraint",
-                "global_batch": world * D,
+                "global_batch": args.dates if args.scaling == "strong" else world * D,
                 "seq_len": N,
                 "stocks": N,
                 "factors": K,
-                "dates_per_gpu": D,
+                "dates_per_gpu": Dpad,
                 "stock_chunks_per_date": chunks,
                 "parallelism": f"dp{world}",
                 "specific_returns": not args.no_resid,

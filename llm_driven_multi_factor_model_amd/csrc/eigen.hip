@@ -1381,7 +1381,9 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
       be[lane] = 0.0;
       if constexpr (BT) ta[lane] = 0.0;
     }
-    if (LT && lane == TS) tb[TS] = double2{1e300, 0.0};
+    // the row past the last (read by the backward pivots at i = KP - 1): lane TS, or lane 0
+    // when the table spans the whole wave (KP = 64)
+    if (LT && lane == (TS < 64 ? TS : 0)) tb[TS] = double2{1e300, 0.0};
     lds_order();
   }
   if (PAD && lane < K) {
@@ -2499,34 +2501,28 @@ bool launch_bias_tri(const double* D0, int D, int K, int M, const double* Cz, co
                      double* ws, hipStream_t s) {
   const bool chain_mode = g_bias_mode == 21 || (MFA_AB && (g_bias_mode == 22 || g_bias_mode == 23));
   if (g_bias_mode == 5 || (chain_mode && K > 44)) {  // chains are instantiated at KP = 44
-    // 32 < K <= 42 (the reference's 1 + 31 + 10 factors): KP = 42, 2-step groups, KP-entry
-    // tables: 128 VGPRs and 9.7 KB of LDS -> 4 waves per SIMD, 16 per CU (profiles/r05/r05al:
-    // 10.74 -> 9.18 ms at 2520 x 100, bitwise the same ratios as the 64-entry-table kernel)
-    if (K > 32 && K <= 42) {
-      hipLaunchKernelGGL((mc_bias_tri2_kernel<42, true, 0, 4, false, 8, 8, 2, true, false, true,
-                                              false, false, 1, kTri2GS, true>),
-                         dim3(D * M), dim3(64), bias_tri2_lds(K, 42, kTri2GS, true), s, D0, K, M,
-                         Cz, dvalid, ws, nullptr, nullptr, D, 0);
-      return true;
+    // Every register width runs the lean form measured at K = 42 (profiles/r05/r05al: 10.74 ->
+    // 9.18 ms at 2520 x 100): the padded eigenvector phase, skipped no-op Householder steps,
+    // 2-step reflector groups and KP-entry LDS tables; the waves per SIMD are the most each
+    // width holds without scratch (-Rpass-analysis=kernel-resource-usage: KP 8 / 16 -> 58 / 64
+    // VGPRs, 8 waves; 24 -> 85, 5; 32 -> 101, 4; 42 / 44 -> 128, 4; 48 -> 132, 3; 64 -> 166, 3).
+    // KP = 42 serves 32 < K <= 42 (the reference's 1 + 31 + 10 factors), KP = 32 the SSE50 run.
+#define MFA_TRI2(KP_, WPE_)                                                                      \
+    if (K <= KP_) {                                                                            \
+      hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, true, 0, WPE_, false, 8, 8, 2, true, false,   \
+                                              true, false, false, 1, kTri2GS, true>),           \
+                         dim3(D * M), dim3(64), bias_tri2_lds(K, KP_, kTri2GS, true), s, D0, K, \
+                         M, Cz, dvalid, ws, nullptr, nullptr, D, 0);                            \
+      return true;                                                                             \
     }
-#define MFA_TRI2(KP_)                                                                        \
-    if (K <= KP_) {                                                                        \
-      hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, true, 0, MFA_TRI2_WPE, false, 8, 8, 2,    \
-                                              (KP_ == 44), false, (KP_ == 44), false, false, 1, \
-                                              (KP_ == 44 ? kTri2GS : 8), (KP_ == 44)>),    \
-                         dim3(D * M), dim3(64),                                            \
-                         bias_tri2_lds(K, KP_, KP_ == 44 ? kTri2GS : 8, KP_ == 44), s, D0, K, \
-                         M, Cz,                                                            \
-                         dvalid, ws, nullptr, nullptr, D, 0);                                    \
-      return true;                                                                         \
-    }
-    MFA_TRI2(8)
-    MFA_TRI2(16)
-    MFA_TRI2(24)
-    MFA_TRI2(32)
-    MFA_TRI2(44)
-    MFA_TRI2(48)
-    MFA_TRI2(64)
+    MFA_TRI2(8, 8)
+    MFA_TRI2(16, 8)
+    MFA_TRI2(24, 5)
+    MFA_TRI2(32, 4)
+    MFA_TRI2(42, 4)
+    MFA_TRI2(44, 4)
+    MFA_TRI2(48, 3)
+    MFA_TRI2(64, 3)
 #undef MFA_TRI2
     return false;
   }

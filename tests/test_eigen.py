@@ -49,6 +49,42 @@ def test_eigen_adjust_statistical_parity_with_reference(ref):
     np.testing.assert_allclose(wo / w0, wr / w0, rtol=0.03)
 
 
+def _parity_k42(ref, sorted_eig):
+    """Multipliers v^2 of the 42 eigenvalues (ours / reference's eigen_risk_adj at K = 42,
+    M = 100, T = 400, independent Monte-Carlo draws)."""
+    K, T, M = 42, 400, 100
+    F = _spd(1, K, seed=5, spread=1.5)[0] * 1e-4
+    cols = [f"f{i}" for i in range(K)]
+    df = pd.DataFrame(F.numpy(), columns=cols, index=cols)
+    eig = np.linalg.eig
+    if sorted_eig:
+        np.linalg.eig = lambda a: tuple(x[..., ::-1] for x in np.linalg.eigh(a))
+    try:
+        R = ref.utils.eigen_risk_adj(df, T=T, M=M, scale_coef=1.4).values
+    finally:
+        np.linalg.eig = eig
+    Cz = eigen.mc_cov(M, K, T, seed=11, device="cpu")
+    Fh = eigen.eigen_risk_adjust(F[None], Cz=Cz, scale_coef=1.4)[0].numpy()
+    w0 = np.linalg.eigvalsh(F.numpy())[::-1]
+    return np.linalg.eigvalsh(Fh)[::-1] / w0, np.linalg.eigvalsh(R)[::-1] / w0
+
+
+@pytest.mark.reference
+def test_eigen_adjust_statistical_parity_with_reference_k42(ref):
+    """VERDICT r05 item 5, at the headline K = 42.  The reference pairs simulated and real
+    eigenvalues by np.linalg.eig's UNSORTED output order (quirk Q7, utils.py:64,79); with that
+    order fixed to descending (an eigh shim) every multiplier agrees within Monte-Carlo noise
+    (3 %).  Against the raw reference the bulk agrees the same way; the tail of the spectrum,
+    where eig's order is not descending (F0's smallest eigenvalues come out ascending), pairs
+    differently and differs by up to ~15 % -- a reference artefact, not noise."""
+    ours, want = _parity_k42(ref, sorted_eig=True)
+    np.testing.assert_allclose(ours, want, rtol=0.03)
+    ours, raw = _parity_k42(ref, sorted_eig=False)
+    rel = np.abs(ours - raw) / raw
+    assert np.median(rel) < 0.02 and rel[:21].max() < 0.04
+    assert rel[-2:].min() > 0.05      # the eig-order pairing of the two smallest is visible
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("K,B", [(42, 50), (7, 10), (64, 5), (1, 3), (33, 9)])
 def test_hip_eigh_matches_torch(cuda, K, B):
@@ -112,8 +148,10 @@ def _need_solver(solver):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("solver", sorted(eigen.BIAS_SOLVERS))
-@pytest.mark.parametrize("K", [42, 5, 17, 64, 37, 43])
+@pytest.mark.parametrize("K", [42, 5, 17, 64, 37, 43, 9, 16, 25, 32, 45, 48, 49])
 def test_hip_eigen_adjust_matches_reference_path(cuda, solver, K):
+    """Every instantiated register width of the tridiagonal bias solver (KP = 8 / 16 / 24 / 32 /
+    42 / 44 / 48 / 64: K at and just past each width) against the CPU path at 1e-8."""
     _need_solver(solver)
     D, M = 12, 16
     F = _spd(D, K, seed=9 + K, spread=2.0) * 1e-4
