@@ -2862,8 +2862,11 @@ hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, 
 #endif  // MFA_AB
   if (det && mode == 0 && xs_plain_moments<T>(D)) {
     // moments from plain vector loads (default for fp32 panels and small fp64 shards; A/B mode 7
-    // forces the LDS-DMA ring below)
-    hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR | 32 | 64, PRE, T>), dim3(D),
+    // forces the LDS-DMA ring below).  The residual prefetch is on for every storage type, as
+    // on the LDS-DMA path: its R^2 sums accumulate in the prefetch path's order, so a date's
+    // R^2 is bitwise the same whichever path its launch's date count selects -- a date-sharded
+    // run reproduces one process (fp64 D = 315: 65.3 vs 65.5 us, profiles/r03_xs_pre64_ab.jsonl)
+    hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR | 32 | 64, true, T>), dim3(D),
                        dim3(256), lds1, s, X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2,
                        stats, status, mom, okm);
   } else if (det) {  // bitwise-reproducible variant of the default path

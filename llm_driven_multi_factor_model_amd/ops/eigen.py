@@ -165,6 +165,9 @@ def using_bias_solver(name: str):
         set_bias_solver(old)
 
 
+LAST_EIGH_FLAGS: torch.Tensor | None = None
+
+
 def eigh(A: torch.Tensor, max_sweeps: int = MAX_SWEEPS, tol: float = TOL):
     """Batched symmetric eigendecomposition, eigenvalues DESCENDING.
 
@@ -188,6 +191,8 @@ def eigh(A: torch.Tensor, max_sweeps: int = MAX_SWEEPS, tol: float = TOL):
     flags = torch.empty(B, dtype=torch.int32, device=A.device)
     _native.call("mfa_eigh_batched", _native.ptr(Ab), B, K, max_sweeps, tol, _native.ptr(w),
                  _native.ptr(U), _native.ptr(flags), _native.stream(A.device))
+    global LAST_EIGH_FLAGS
+    LAST_EIGH_FLAGS = flags   # diagnostics (tools/risk_timing.py): matrices re-solved by Jacobi
     return w.reshape(shp[:-1]), U.reshape(shp)
 
 

@@ -19,10 +19,9 @@ import time
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from llm_driven_multi_factor_model_amd.models.panel import synthetic_panel  # noqa: E402
-from llm_driven_multi_factor_model_amd.models.risk_model import RiskModel  # noqa: E402
 from llm_driven_multi_factor_model_amd.ops import rolling as RL  # noqa: E402
 from llm_driven_multi_factor_model_amd.utils.config import preset  # noqa: E402
+from tools.risk_timing import risk_model_timing  # noqa: E402
 
 
 def timed(fn, reps=2):
@@ -37,16 +36,10 @@ def timed(fn, reps=2):
     return (time.perf_counter() - t0) / reps, out
 
 
-def risk_run(D, N, P, Q, cfg, device, attribution=False):
-    # fp64 panel: the reference reads float64 exposures / caps / returns (demo.py:21)
-    p = synthetic_panel(D, N, P, Q, seed=7, device=device, missing_frac=0.01, dtype=torch.float64)
-
-    def go():
-        m = RiskModel(p, cfg).run()
-        if attribution:
-            m.risk_attribution(torch.full((N,), 1.0 / N, dtype=torch.float64, device=device))
-        return m
-    return timed(go)
+def risk_run(D, N, P, Q, cfg, device, attribution=False, reps=5):
+    """The canonical timing (tools/risk_timing.py): median over seeds 3 / 7 / 11 x ``reps``."""
+    r = risk_model_timing(D, N, P, Q, cfg, device, reps=reps, attribution=attribution)
+    return r["median_ms"] / 1e3, r
 
 
 def main():
@@ -68,12 +61,12 @@ def main():
     res["1_toy_cpu_demo"] = {"seconds": round(t, 3), "reference_seconds": 3.5}
     dev = torch.device("cuda:0")
     # 2: CSI300 x 5y, K = 42, full risk model (M = 100)
-    t, m = risk_run(1250, 300, 31, 10, preset("reference"), dev)
-    res["2_csi300_5y_risk_model"] = {"seconds": round(t, 4), "stage_ms": {k: round(v, 3) for k, v in m.times.ms.items()},
+    t, r = risk_run(1250, 300, 31, 10, preset("reference"), dev)
+    res["2_csi300_5y_risk_model"] = {"seconds": round(t, 4), "timing": r,
                                      "reference_seconds": 6.9 + 28 + 11.5 * 60}
     # 3: All-A 5000 x 10y, full risk model on one GPU
-    t, m = risk_run(2520, 5000, 31, 10, preset("reference"), dev)
-    res["3_alla_10y_risk_model_1gpu"] = {"seconds": round(t, 4), "stage_ms": {k: round(v, 3) for k, v in m.times.ms.items()},
+    t, r = risk_run(2520, 5000, 31, 10, preset("reference"), dev)
+    res["3_alla_10y_risk_model_1gpu"] = {"seconds": round(t, 4), "timing": r,
                                          "reference_seconds": 4.4 * 60 + 1.9 * 60 + 45 * 60}
     # 4: 252-day rolling beta / hsigma, 5000 x 15y
     N, T = 5000, 3780
@@ -86,8 +79,8 @@ def main():
     res["4_rolling_beta_5000x15y"] = {"seconds": round(t, 5), "stock_days": N * T,
                                       "reference_seconds": 4.3 * 3600}
     # 5: NW + 10k-sim eigen bootstrap + attribution (CSI300 x 5y shape; sims-sharded mode)
-    t, m = risk_run(1250, 300, 31, 10, preset("bootstrap10k"), dev, attribution=True)
-    res["5_nw_bootstrap10k_attribution"] = {"seconds": round(t, 3), "stage_ms": {k: round(v, 2) for k, v in m.times.ms.items()},
+    t, r = risk_run(1250, 300, 31, 10, preset("bootstrap10k"), dev, attribution=True, reps=3)
+    res["5_nw_bootstrap10k_attribution"] = {"seconds": round(t, 3), "timing": r,
                                             "reference_seconds": 57.0 * 1250}
     for v in res.values():
         v["speedup_vs_reference"] = round(v["reference_seconds"] / v["seconds"], 1)

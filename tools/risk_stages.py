@@ -8,21 +8,21 @@ all-reduce across 8 GPU"):
 
 Under torchrun the dates are sharded over ranks (regression, NW, VRA); with ``--preset
 bootstrap10k`` the 10k Monte-Carlo sims of the eigen adjustment are sharded over ranks and
-combined with one all_reduce.  Rank 0 prints one JSON line with per-stage ms (max over ranks).
+combined with one all_reduce.  Rank 0 prints one JSON line: the canonical timing of
+tools/risk_timing.py (median over panel seeds x reps of the max over ranks, per-seed stage
+medians and Jacobi re-solve counts).
 """
 import argparse
 import json
 import os
 import sys
-import time
 
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from llm_driven_multi_factor_model_amd.models.panel import synthetic_panel  # noqa: E402
-from llm_driven_multi_factor_model_amd.models.risk_model import RiskModel  # noqa: E402
 from llm_driven_multi_factor_model_amd.parallel import dist as pdist  # noqa: E402
 from llm_driven_multi_factor_model_amd.utils.config import preset  # noqa: E402
+from tools.risk_timing import risk_model_timing  # noqa: E402
 
 ap = argparse.ArgumentParser()
 ap.add_argument("--dates", type=int, default=2520, help="total dates (sharded under torchrun)")
@@ -33,39 +33,19 @@ ap.add_argument("--sims", type=int, default=None, help="override the preset's ei
 ap.add_argument("--preset", default="reference")
 ap.add_argument("--storage", choices=["fp64", "fp32"], default="fp64",
                 help="panel storage dtype (fp64 = the reference's input precision)")
-ap.add_argument("--reps", type=int, default=2)
+ap.add_argument("--reps", type=int, default=5)
+ap.add_argument("--seeds", default="3,7,11", help="panel seeds (the median is over seeds x reps)")
 ap.add_argument("--attribution", action="store_true", help="also time an equal-weight attribution")
 a = ap.parse_args()
 ctx = pdist.init_distributed()
-dev = ctx.device
-full_D = a.dates
-lo, hi = pdist.shard_range(full_D, ctx.rank, ctx.world)
-# every rank generates the same panel (seeded) and keeps its date block
-p = synthetic_panel(full_D, a.stocks, a.P, a.Q, seed=3, device=dev, missing_frac=0.01,
-                    dtype=torch.float64 if a.storage == "fp64" else torch.float32).slice_dates(lo, hi)
 over = {"eigen_sims": a.sims} if a.sims else {}
 cfg = preset(a.preset, **over)
-stage = {}
-for rep in range(a.reps):
-    m = RiskModel(p, cfg, T_global=full_D, ctx=ctx)
-    pdist.barrier(ctx)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    m.run()
-    if a.attribution:
-        with m._stage("attribution"):
-            r = m.risk_attribution(torch.full((p.N,), 1.0 / p.N, device=dev, dtype=torch.float64))
-    torch.cuda.synchronize()
-    tot = (time.perf_counter() - t0) * 1e3
-    pdist.barrier(ctx)
-stage = {k: pdist.all_reduce_max(v, ctx) for k, v in m.times.ms.items()}
-tot = pdist.all_reduce_max(tot, ctx)
-ok = bool(torch.isfinite(m.vra_cov[-1]).all().item())
+res = risk_model_timing(a.dates, a.stocks, a.P, a.Q, cfg, ctx.device,
+                        seeds=[int(x) for x in a.seeds.split(",")], reps=a.reps, ctx=ctx,
+                        attribution=a.attribution,
+                        dtype=torch.float64 if a.storage == "fp64" else torch.float32)
 if ctx.rank == 0:
-    print(json.dumps({"shape": vars(a), "world": ctx.world, "eigen_sims": cfg.eigen_sims,
-                      "eigen_shard": cfg.eigen_shard,
-                      "stage_ms": {k: round(v, 3) for k, v in stage.items()},
-                      "total_ms": round(tot, 3), "last_vra_finite": ok,
-                      "nan_eigen_dates_rank0": int(torch.isnan(m.eigen_cov[:, 0, 0]).sum())}))
+    print(json.dumps({"shape": vars(a), "eigen_sims": cfg.eigen_sims,
+                      "eigen_shard": cfg.eigen_shard, **res}))
 if ctx.enabled:
     torch.distributed.destroy_process_group()
