@@ -116,7 +116,7 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False,
     build_host(force=force, verbose=verbose)
     obj_dir, lib_path = (AB_OBJ_DIR, AB_LIB_PATH) if ab else (OBJ_DIR, LIB_PATH)
     obj_dir.mkdir(parents=True, exist_ok=True)
-    headers = sorted(CSRC.glob("*.h"))
+    headers = sorted(CSRC.rglob("*.h"))   # csrc/ab/*.h: the A/B-only kernels (MFA_AB builds)
     srcs = sources()
     objs = [obj_dir / (s.stem + ".o") for s in srcs]
     todo = [(s, o) for s, o in zip(srcs, objs) if force or _stale(s, o, headers)]

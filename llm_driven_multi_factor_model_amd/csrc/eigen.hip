@@ -69,52 +69,7 @@ __device__ void sort_desc(const double* A, int K, int lda, int* perm) {
 
 // ---------------- kernels ----------------
 #if MFA_AB  // row/column cyclic Jacobi (eigh mode 1, A/B only)
-// batched eigh: A [B][K][K] -> w [B][K] (descending), U [B][K][K] (U[:, k] = eigenvector k)
-__global__ __launch_bounds__(64) void eigh_kernel(const double* __restrict__ Ain, int K,
-                                                  int max_sweeps, double tol,
-                                                  double* __restrict__ w, double* __restrict__ U,
-                                                  int* __restrict__ sweeps) {
-  extern __shared__ double sm[];
-  const int b = blockIdx.x, lane = threadIdx.x;
-  const int lda = K + 1;
-  double* A = sm;
-  double* V = A + K * lda;
-  double* rot = V + K * lda;
-  int* perm = (int*)(rot + 4 * 64);
-  const double* a = Ain + (size_t)b * K * K;
-  bool finite = true;
-  for (int e = lane; e < K * K; e += 64) {
-    const double x = a[e];
-    finite = finite && __builtin_isfinite(x);
-    A[(e / K) * lda + e % K] = x;
-  }
-  const bool ok = __all(finite);
-  wsync();
-  if (!ok) {  // propagate NaN (reference: eig raises -> empty frame)
-    for (int k = lane; k < K; k += 64) w[(size_t)b * K + k] = qnan();
-    for (int e = lane; e < K * K; e += 64) U[(size_t)b * K * K + e] = qnan();
-    if (lane == 0 && sweeps) sweeps[b] = -1;
-    return;
-  }
-  // symmetrise (NW matrices are symmetric up to rounding)
-  for (int e = lane; e < K * K; e += 64) {
-    const int i = e / K, j = e % K;
-    if (i < j) {
-      const double m = 0.5 * (A[i * lda + j] + A[j * lda + i]);
-      A[i * lda + j] = m;
-      A[j * lda + i] = m;
-    }
-  }
-  wsync();
-  const int ns = jacobi_wave(A, V, K, lda, rot, max_sweeps, tol);
-  sort_desc(A, K, lda, perm);
-  for (int k = lane; k < K; k += 64) w[(size_t)b * K + k] = A[perm[k] * lda + perm[k]];
-  for (int e = lane; e < K * K; e += 64) {
-    const int i = e / K, k = e % K;
-    U[(size_t)b * K * K + e] = V[i * lda + perm[k]];
-  }
-  if (lane == 0 && sweeps) sweeps[b] = ns;
-}
+#include "ab/eigen_cyclic.h"
 #endif
 
 // C_z,m = cov(z_m) (ddof 1) for z_m [T x K] standard normals, all fp64 like the reference's
@@ -576,484 +531,13 @@ __global__ __launch_bounds__(64) void mc_bias_kernel(const double* __restrict__ 
   }
 }
 
-// ---------------- split-layout variant of the bias Jacobi (A/B, mfa_eigen_set_bias_mode) --------
-// Same tournament / pair-block schedule as jacobi_pairs, but A and M live in two separate
-// packed arrays (same pk() slot index): A as fp64, M as MT (double, or float = storage-only
-// fp32 with the rotation itself in fp64).  Per entry one ds_*_b64 (+ one b64 / b32) instead of
-// one b128: with MT = float the LDS bytes per round drop by 25 %.  M only feeds the bias ratio
-// diag(M)/diag(A); A (which decides convergence and Lambda) stays fp64.
-template <int NB, int FAST, typename MT>
-__device__ int jacobi_pairs_split(double* A, MT* Mm, double2* rcs, int Ke, int max_sweeps,
-                                  double tol) {
-  const int lane = threadIdx.x & 63;
-  const int npair = Ke >> 1;
-  const int nb = npair * (npair + 1) / 2;
-  auto nxt = [&](int x) { return x == 0 ? 0 : (x == Ke - 1 ? 1 : x + 1); };
-  int rd[NB][4], wr[NB][4];
-  bool has[NB], diag[NB];
-  int bT[NB], bU[NB];
-#pragma unroll
-  for (int k = 0; k < NB; ++k) {
-    const int b = lane + 64 * k;
-    int t = 0, rem = b;
-    while (t < npair && rem >= npair - t) { rem -= npair - t; ++t; }
-    has[k] = b < nb;
-    const int T = has[k] ? t : 0, U = has[k] ? t + rem : 0;
-    bT[k] = T;
-    bU[k] = U;
-    diag[k] = T == U;
-    const int x0 = T, x1 = Ke - 1 - T, y0 = U, y1 = Ke - 1 - U;
-    rd[k][0] = pk(x0, y0, Ke); rd[k][1] = pk(x0, y1, Ke);
-    rd[k][2] = pk(x1, y0, Ke); rd[k][3] = pk(x1, y1, Ke);
-    wr[k][0] = pk(nxt(x0), nxt(y0), Ke); wr[k][1] = pk(nxt(x0), nxt(y1), Ke);
-    wr[k][2] = pk(nxt(x1), nxt(y0), Ke); wr[k][3] = pk(nxt(x1), nxt(y1), Ke);
-  }
-  const int ipp = pk(lane, lane, Ke), iqq = pk(Ke - 1 - lane, Ke - 1 - lane, Ke);
-  const int ipq = pk(lane, Ke - 1 - lane, Ke);
-  int sweep = 0;
-  for (; sweep < max_sweeps; ++sweep) {
-    double offacc = 0.0, dgacc = 0.0;
-    for (int r = 0; r < Ke - 1; ++r) {
-      const bool last = r == Ke - 2;
-      if (lane < npair) rcs[lane] = jacobi_cs<FAST>(A[ipp], A[iqq], A[ipq]);
-      wsync();
-      double av[NB][4], mv[NB][4];
-      double2 rt[NB], ru[NB];
-#pragma unroll
-      for (int k = 0; k < NB; ++k) {
-        if (has[k]) {
-          rt[k] = rcs[bT[k]];
-          ru[k] = rcs[bU[k]];
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            av[k][e] = A[rd[k][e]];
-            mv[k][e] = (double)Mm[rd[k][e]];
-          }
-        }
-      }
-#pragma unroll
-      for (int k = 0; k < NB; ++k) {
-        if (!has[k]) continue;
-        rot_block(av[k][0], av[k][1], av[k][2], av[k][3], rt[k].x, rt[k].y, ru[k].x, ru[k].y);
-        rot_block(mv[k][0], mv[k][1], mv[k][2], mv[k][3], rt[k].x, rt[k].y, ru[k].x, ru[k].y);
-        if (diag[k]) {
-          const double apq_new = (rt[k].y != 0.0) ? 0.0 : av[k][1];
-          A[wr[k][0]] = av[k][0];
-          A[wr[k][1]] = apq_new;
-          A[wr[k][3]] = av[k][3];
-          Mm[wr[k][0]] = (MT)mv[k][0];
-          Mm[wr[k][1]] = (MT)(0.5 * (mv[k][1] + mv[k][2]));
-          Mm[wr[k][3]] = (MT)mv[k][3];
-          if (last) {
-            dgacc = fma(av[k][0], av[k][0], fma(av[k][3], av[k][3], dgacc));
-            offacc = fma(2.0 * apq_new, apq_new, offacc);
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            A[wr[k][e]] = av[k][e];
-            Mm[wr[k][e]] = (MT)mv[k][e];
-            if (last) offacc = fma(2.0 * av[k][e], av[k][e], offacc);
-          }
-        }
-      }
-      wsync();
-    }
-    const double off = wave_total(offacc), dgt = wave_total(dgacc);
-    if (off <= tol * tol * dgt || off == 0.0) { ++sweep; break; }
-  }
-  return sweep;
-}
-
-template <int NB, int FAST, typename MT>
-__global__ __launch_bounds__(64) void mc_bias_split_kernel(const double* __restrict__ D0, int K,
-                                                           int M, const double* __restrict__ Cz,
-                                                           const int* __restrict__ dvalid,
-                                                           int max_sweeps, double tol,
-                                                           double* __restrict__ vout) {
-  extern __shared__ double sm[];
-  const int d = blockIdx.x / M, m = blockIdx.x % M, lane = threadIdx.x;
-  double* vo = vout + ((size_t)d * M + m) * K;
-  if (!dvalid[d]) {
-    for (int k = lane; k < K; k += 64) vo[k] = qnan();
-    return;
-  }
-  const int Ke = K + (K & 1);
-  const int np = pk_size(Ke);
-  double* A = sm;                              // [np] fp64
-  MT* Mm = (MT*)(A + np);                      // [np] MT (fits in the [np] doubles after A)
-  double* dd = A + 2 * np;                     // [64]
-  double2* rcs = (double2*)(dd + 64);          // [32]
-  int* perm = (int*)(rcs + 32);                // [64]
-  const double* d0 = D0 + (size_t)d * K;
-  for (int k = lane; k < 64; k += 64) dd[k] = k < K ? sqrt(fmax(d0[k], 0.0)) : 0.0;
-  wsync();
-  const double* c = Cz + (size_t)m * K * K;
-  for (int i = 0; i < Ke; ++i)
-    for (int j = i + lane; j < Ke; j += 64) {
-      const int s = pk(i, j, Ke);
-      A[s] = (i < K && j < K) ? dd[i] * c[i * K + j] * dd[j] : 0.0;
-      Mm[s] = (MT)((i == j && i < K) ? dd[i] * dd[i] : 0.0);
-    }
-  wsync();
-  jacobi_pairs_split<NB, FAST, MT>(A, Mm, rcs, Ke, max_sweeps, tol);
-  for (int k = lane; k < K; k += 64) {
-    const double lk = A[pk(k, k, Ke)];
-    int rank = 0;
-    for (int j = 0; j < K; ++j) {
-      const double lj = A[pk(j, j, Ke)];
-      rank += (lj > lk) || (lj == lk && j < k);
-    }
-    perm[rank] = k;
-  }
-  wsync();
-  for (int k = lane; k < K; k += 64) {
-    const int s = pk(perm[k], perm[k], Ke);
-    vo[k] = (double)Mm[s] / A[s];
-  }
-}
-
-// ---------------- Householder-tridiagonal bias solver (bias mode 3) ----------------
-// Per (date, sim) the same output as mc_bias_kernel, v[k] = V[:,k]^T D0 V[:,k] / Lambda[k]
-// (descending), from one O(K^3) reduction instead of ~6 Jacobi sweeps of 2 LDS passes each:
-//   1. tridiagonalise A = S C_z S with K-2 Householder reflections H_s = I - tau_s u_s u_s^T:
-//      lane i owns row i (LDS, odd stride: conflict-free row-per-lane reads), p = tau A u,
-//      w = p - (tau/2)(u^T p) u, A -= u w^T + w u^T on the trailing block; u_s is kept,
-//      zero-padded to KP, in row s (that row is finished once its column is reduced);
-//   2. lane k finds the k-th largest eigenvalue of T by count-guided Laguerre iteration on
-//      det(T - x I) (f'/f and its derivative from the LDL^T pivot recurrence), bracketed by
-//      the pivots' Sturm count, started from the k-th largest diagonal entry of A (C_b is
-//      close to diagonal) and with the first brackets shared between all lanes;
-//   3. eigenvector of T by the twisted factorisation at that eigenvalue (forward / backward
-//      pivots, twist at min |gamma|), in registers;
-//   4. y = H_0 ... H_{K-3} z (u_s broadcast from LDS) and v = sum_l D0[l] y_l^2 / lambda.
-// Everything stays fp64; the outputs are sorted by construction (lane k = rank k).
-// ABL: timing-only ablations (bias modes 41..47, KP = 44): 1 = no Laguerre iterations,
-// 2 = no eigenvector / back-transform, 4 = no tridiagonalisation, 8 = setup only (mode 48),
-// 16 = setup + tridiagonalisation only (mode 56); outputs meaningless
-#ifndef MFA_TRI_WPE
-#define MFA_TRI_WPE 1
+#if MFA_AB
+#include "ab/eigen_split.h"
 #endif
-template <int KP, int ABL = 0>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(MFA_TRI_WPE))) void mc_bias_tri_kernel(const double* __restrict__ D0, int K, int M,
-                                                         const double* __restrict__ Cz,
-                                                         const int* __restrict__ dvalid,
-                                                         double* __restrict__ vout) {
-  extern __shared__ double sm[];
-  constexpr int LD = KP + 1;  // staging stride of C_z (odd: row-per-lane ds_read_b64 conflict-free)
-  constexpr int LU = KP;      // reflector rows (16-B aligned: broadcast ds_read_b128 pairs)
-  const int d = blockIdx.x / M, m = blockIdx.x % M, lane = threadIdx.x;
-  double* vo = vout + ((size_t)d * M + m) * K;
-  if (!dvalid[d]) {
-    for (int k = lane; k < K; k += 64) vo[k] = qnan();
-    return;
-  }
-  double* A = sm;                          // [K][LD]: row s <- reflector u_s (zero-padded)
-  double* ub = A + (((size_t)K * LD + 1) & ~(size_t)1);  // [64] broadcast u (16-B aligned)
-  double* wb = ub + 64;                    // [64] broadcast w
-  double2* tb = (double2*)(wb + 64);       // [64] {alpha_i, beta_{i-1}^2}
-  double* be = (double*)(tb + 64);         // [64] beta_i
-  double* ta = be + 64;                    // [64] tau_s
-  double* dd = ta + 64;                    // [64] sqrt(D0)
-  double* gs = dd + 64;                    // [64] diagonal of A, descending
-  const double* d0 = D0 + (size_t)d * K;
-  dd[lane] = lane < K ? sqrt(fmax(d0[lane], 0.0)) : 0.0;
-  lds_order();
-  // C_z (shared by every date of sim m, L2-resident) staged coalesced into LDS, then lane i
-  // keeps row i of A = S C_z S in registers (static indices; padding columns zero)
-  const double* c = Cz + (size_t)m * K * K;
-  for (int e = lane; e < K * K; e += 64) {
-    const int i = e / K;
-    A[i * LD + (e - i * K)] = c[e];
-  }
-  lds_order();
-  double a[KP];
-  {
-    const int i = lane < K ? lane : 0;
-    const double di = lane < K ? dd[i] : 0.0;
-#pragma unroll
-    for (int j = 0; j < KP; ++j) a[j] = j < K ? di * A[i * LD + j] * dd[j] : 0.0;
-  }
-  if (lane < K) {  // descending rank of the diagonal (ties by index): initial eigenvalue guesses
-    const double g = dd[lane] * A[lane * LD + lane] * dd[lane];
-    int rank = 0;
-    for (int j = 0; j < K; ++j) {
-      const double h = dd[j] * A[j * LD + j] * dd[j];
-      rank += (h > g) || (h == g && j < lane);
-    }
-    gs[rank] = g;
-  }
-  lds_order();  // the staging area becomes the reflector store (stride LU)
-  if constexpr ((ABL & 8) != 0) {  // timing: setup only
-    if (lane < K) vo[lane] = a[lane % KP] + gs[lane];
-    return;
-  }
-  // ---- 1. Householder tridiagonalisation (rows in registers) ----
-  // Step s takes column s from each lane's own row (x_i = A[i][s], a static select within the
-  // step group), forms u_s, p = tau A u, w = p - (tau/2)(u^T p) u and updates its own row
-  // a -= u_i w + w_i u with u, w broadcast as 16-B LDS pairs.  Columns j < 8 floor(s / 8) are
-  // finished, so each group of 8 steps runs a static column range [J0, KP): ~35 % fewer FMAs.
-  auto steps = [&](auto J0c, int s_begin) {
-    constexpr int J0 = decltype(J0c)::value;
-    for (int s = s_begin; s < s_begin + 8 && s + 2 < K; ++s) {
-      // column s of the (symmetric) matrix is each lane's own a[s]: select it from the group's
-      // 8 static candidates (publishing row s through LDS cost ~22 single-lane 16-B stores per
-      // step, each paying the whole wave's VGPR transfer: the phase's LDS-array time)
-      // (each candidate goes through an empty asm: without it the compiler turns the select
-      // chain into a dynamically indexed load, which demotes the whole row to scratch memory
-      // and re-stores it after every step)
-      double xs = a[J0];
-#pragma unroll
-      for (int k = 1; k < 8; ++k)
-        if (J0 + k < KP) {
-          double t = a[J0 + k];
-          asm volatile("" : "+v"(t));
-          xs = s == J0 + k ? t : xs;
-        }
-      const bool act = lane > s && lane < K;
-      const double x = act ? xs : 0.0;
-      const double x0 = readlane(xs, s + 1);
-      const double sig = wave_total(lane > s + 1 && lane < K ? x * x : 0.0);
-      const double alpha = readlane(xs, s);
-      double u = 0.0, tau = 0.0, beta = x0;
-      if (sig != 0.0) {
-        const double nrm = sqrt(fma(x0, x0, sig));
-        beta = x0 >= 0.0 ? -nrm : nrm;
-        tau = 1.0 / (nrm * (nrm + fabs(x0)));
-        u = act ? (lane == s + 1 ? x0 - beta : x) : 0.0;
-      }
-      ub[lane] = u;
-      if (lane < KP) A[s * LU + lane] = u;  // u_s, zero outside (s, K)
-      if (lane == 0) {
-        tb[s] = double2{alpha, s > 0 ? be[s - 1] * be[s - 1] : 0.0};
-        be[s] = beta;
-        ta[s] = tau;
-      }
-      lds_order();
-      if (tau != 0.0) {
-        double p0 = 0.0, p1 = 0.0;
-#pragma unroll
-        for (int j = J0; j < KP; j += 2) {
-          const double2 uu = *(const double2*)(ub + j);
-          p0 = fma(a[j], uu.x, p0);
-          p1 = fma(a[j + 1], uu.y, p1);
-        }
-        const double p = act ? tau * (p0 + p1) : 0.0;
-        const double kk = 0.5 * tau * wave_total(u * p);
-        const double w = p - kk * u;
-        wb[lane] = w;
-        lds_order();
-        if (act) {
-#pragma unroll
-          for (int j = J0; j < KP; j += 2) {
-            const double2 ww = *(const double2*)(wb + j), uu = *(const double2*)(ub + j);
-            a[j] -= fma(u, ww.x, w * uu.x);
-            a[j + 1] -= fma(u, ww.y, w * uu.y);
-          }
-        }
-      }
-      lds_order();
-    }
-  };
-  if constexpr ((ABL & 4) != 0) {
-    if (lane < K) {
-      tb[lane] = double2{gs[lane], 0.0};
-      be[lane] = 0.0;
-      ta[lane] = 0.0;
-    }
-    lds_order();
-  } else {
-    static_assert(KP % 8 == 0 || KP % 4 == 0, "KP: multiple of 4");
-    [&]<int... G>(std::integer_sequence<int, G...>) {
-      (steps(std::integral_constant<int, (8 * G < KP ? 8 * G : 0)>{}, 8 * G), ...);
-    }(std::make_integer_sequence<int, (KP + 7) / 8>{});
-    // final 2 x 2: alpha_{K-2} = A[K-2][K-2], beta_{K-2} = A[K-1][K-2], alpha_{K-1}
-    double c2 = 0.0, c1 = 0.0;  // each lane's a[K-2], a[K-1] (dynamic index: static select)
-#pragma unroll
-    for (int j = 0; j < KP; ++j) {
-      double t = a[j];
-      asm volatile("" : "+v"(t));  // keep `a` in registers (see the step select above)
-      c2 = j == K - 2 ? t : c2;
-      c1 = j == K - 1 ? t : c1;
-    }
-    const double a22 = K >= 2 ? readlane(c2, K - 2) : readlane(c1, 0);
-    const double b21 = K >= 2 ? readlane(c2, K - 1) : 0.0;
-    const double a11 = readlane(c1, K - 1);
-    if (lane == 0) {
-      if (K >= 2) {
-        tb[K - 2] = double2{a22, K > 2 ? be[K - 3] * be[K - 3] : 0.0};
-        be[K - 2] = b21;
-        tb[K - 1] = double2{a11, b21 * b21};
-      } else {
-        tb[0] = double2{a11, 0.0};
-      }
-    }
-    lds_order();
-  }
-  if constexpr ((ABL & 16) != 0) {  // timing: setup + tridiagonalisation only
-    if (lane < K) vo[lane] = tb[lane].x + be[lane];
-    return;
-  }
-  // ---- 2. eigenvalue of rank `lane` (descending) ----
-  double lo_l = 0.0, hi_l = 0.0, b2max = 0.0;
-  if (lane < K) {
-    const double a = tb[lane].x;
-    const double r = (lane > 0 ? fabs(be[lane - 1]) : 0.0) + (lane + 1 < K ? fabs(be[lane]) : 0.0);
-    lo_l = a - r;
-    hi_l = a + r;
-    b2max = tb[lane].y;
-  } else {
-    lo_l = tb[0].x;
-    hi_l = tb[0].x;
-  }
-  const double gl = wave_min(lo_l), gu = wave_max(hi_l);
-  const double tnorm = fmax(fabs(gl), fabs(gu));
-  const double pivmin = 2.2250738585072014e-308 * fmax(1.0, wave_max(b2max));
-  constexpr double kEps = 2.220446049250313e-16;
-  const double abstol = 1e-22 * tnorm + pivmin;
-  const int jt = K - 1 - lane;  // ascending index of the target eigenvalue
-  // first evaluation at the guess; every lane's (x, count) sample brackets every target
-  double lo = gl - 2.0 * kEps * tnorm - pivmin, hi = gu + 2.0 * kEps * tnorm + pivmin;
-  double x = lane < K ? fmin(fmax(gs[lane], lo), hi) : 0.5 * (lo + hi);
-  double G = 0.0, H = 0.0;
-  int cnt = sturm_gh(tb, K, x, pivmin, G, H);
-  double* xs = ub;  // the tridiagonalisation's broadcast buffers are free now
-  int* cs = (int*)wb;
-  xs[lane] = x;
-  cs[lane] = cnt;
-  lds_order();
-  for (int l = 0; l < K; ++l) {
-    const double xl = xs[l];
-    const int cl = cs[l];
-    if (cl <= jt) lo = fmax(lo, xl); else hi = fmin(hi, xl);
-  }
-  double lam = x;
-  if (lane < K && (ABL & 1) == 0) {
-    int prev = -1;
-    double sprev = __builtin_inf();
-    for (int it = 0; it < 256; ++it) {
-      // Laguerre toward the adjacent root on the target's side: with count(x) == jt the
-      // nearest root above x IS lambda_jt, with count(x) == jt + 1 the nearest below is
-      // (for a real-rooted polynomial the step never passes it).  A tiny step alone is not
-      // convergence: next to a root on the OTHER side the steps are tiny too but grow (~2x);
-      // accept only a tiny step that shrank, and extrapolate growing (escaping) steps 8x.
-      bool lag = false;
-      double xn = 0.0;
-      if (cnt == jt || cnt == jt + 1) {
-        xn = laguerre_toward(x, G, H, K, cnt == jt);
-        double st = fabs(xn - x);
-        if (prev == cnt && st >= 1.5 * sprev) {
-          xn = fma(8.0, xn - x, x);
-          st *= 8.0;
-        }
-        lag = __builtin_isfinite(xn) && xn >= lo && xn <= hi;
-        if (lag && prev == cnt && st <= 1e-9 * fabs(x) && st <= 0.25 * sprev) { x = xn; break; }
-        sprev = lag ? st : __builtin_inf();
-      }
-      if (!lag) { xn = 0.5 * (lo + hi); sprev = __builtin_inf(); }
-      if (hi - lo <= 2.0 * kEps * (fabs(lo) + fabs(hi)) + abstol) { x = 0.5 * (lo + hi); break; }
-      prev = lag ? cnt : -1;
-      x = xn;
-      cnt = sturm_gh(tb, K, x, pivmin, G, H);
-      if (cnt <= jt) lo = x; else hi = x;
-    }
-    lam = x;
-  }
-  if constexpr ((ABL & 2) != 0) {
-    if (lane < K) vo[lane] = lam;
-    return;
-  }
-  // ---- 3. eigenvector of T at lam: twisted factorisation ----
-  double y[KP];
-  if (lane < K) {
-    double P[KP], Q[KP];
-    double dp = 0.0;
-#pragma unroll
-    for (int i = 0; i < KP; ++i) {
-      if (i < K) {
-        const double2 t = tb[i];
-        dp = guard_pivot(i == 0 ? t.x - lam : (t.x - lam) - t.y * rcp_nr(dp), pivmin);
-        P[i] = dp;
-      }
-    }
-    double dm = 0.0, gmin = 0.0;
-    int r = K - 1;
-#pragma unroll
-    for (int i = KP - 1; i >= 0; --i) {
-      if (i < K) {
-        const double a = tb[i].x - lam;
-        dm = guard_pivot(i == K - 1 ? a : a - tb[i + 1].y * rcp_nr(dm), pivmin);
-        Q[i] = dm;
-        const double g = fabs(P[i] + dm - a);
-        if (i == K - 1 || g < gmin) { gmin = g; r = i; }
-      }
-    }
-    double cz = 1.0, nrm = 1.0;
-#pragma unroll
-    for (int i = KP - 1; i >= 0; --i) {
-      if (i < r) {
-        cz = -be[i] * cz * rcp_nr(P[i]);
-        nrm = fma(cz, cz, nrm);
-      }
-      y[i] = i < r ? cz : 0.0;
-    }
-    cz = 1.0;
-#pragma unroll
-    for (int i = 0; i < KP; ++i) {
-      if (i == r) y[i] = 1.0;
-      if (i > r && i < K) {
-        cz = -be[i - 1] * cz * rcp_nr(Q[i]);
-        nrm = fma(cz, cz, nrm);
-        y[i] = cz;
-      }
-    }
-    const double sc = rsq_nr(nrm);
-#pragma unroll
-    for (int i = 0; i < KP; ++i) y[i] *= sc;
-  } else {
-#pragma unroll
-    for (int i = 0; i < KP; ++i) y[i] = 0.0;
-  }
-  // ---- 4. back-transform y = H_0 ... H_{K-3} z and the bias ratio ----
-  // u_s is zero in columns <= s, so steps s in [8g, 8g + 8) run the static column range
-  // [8g, KP) (broadcast 16-B pairs of the reflector row)
-  auto back = [&](auto J0c, int s_hi) {
-    constexpr int J0 = decltype(J0c)::value;
-    for (int s = s_hi; s >= J0; --s) {
-      if (s + 2 >= K) continue;
-      const double tau = ta[s];
-      if (tau == 0.0) continue;
-      const double* us = A + s * LU;
-      double t0 = 0.0, t1 = 0.0;
-#pragma unroll
-      for (int j = J0; j < KP; j += 2) {
-        const double2 uu = *(const double2*)(us + j);
-        t0 = fma(uu.x, y[j], t0);
-        t1 = fma(uu.y, y[j + 1], t1);
-      }
-      const double f = tau * (t0 + t1);
-#pragma unroll
-      for (int j = J0; j < KP; j += 2) {
-        const double2 uu = *(const double2*)(us + j);
-        y[j] = fma(-f, uu.x, y[j]);
-        y[j + 1] = fma(-f, uu.y, y[j + 1]);
-      }
-    }
-  };
-  [&]<int... G>(std::integer_sequence<int, G...>) {
-    constexpr int NG = (KP + 7) / 8;
-    (back(std::integral_constant<int, 8 * (NG - 1 - G)>{}, 8 * (NG - 1 - G) + 7), ...);
-  }(std::make_integer_sequence<int, (KP + 7) / 8>{});
-  if (lane < K) {
-    double v = 0.0;
-#pragma unroll
-    for (int j = 0; j < KP; ++j)
-      if (j < K) v = fma(dd[j] * dd[j], y[j] * y[j], v);
-    vo[lane] = v / lam;
-  }
-}
 
-size_t bias_tri_lds(int K, int KP) { return ((size_t)K * (KP + 1) + 7 * 64 + 2) * sizeof(double); }
+#if MFA_AB
+#include "ab/eigen_tri_v1.h"
+#endif
 
 // ---------------- lean tridiagonal bias solver (bias mode 4, the default) ----------------
 // The same four phases and the same arithmetic as mc_bias_tri_kernel, re-laid-out for
@@ -1582,324 +1066,20 @@ mc_bias_tri2_kernel(const double* __restrict__ D0, int K, int M, const double* _
   }  // date chain
 }
 
-// ---------------- lane-dense tridiagonal bias solver (bias mode 11, K <= 42) ----------------
-// mc_bias_tri2_kernel keeps one 42 x 42 problem per wave: 42 of 64 lanes do useful work in every
-// phase (34 % of each VALU issue slot idles).  Here a 128-thread workgroup (2 waves) carries
-// THREE problems on 126 lanes:
-//   lanes 0..41 of wave w  -> slot w, row (or eigenvalue rank) = lane;
-//   lanes 42..63 of wave w -> slot 2, row = lane - 42 + 22 w  (rows 0..21 in wave 0, 22..43 in 1).
-// Slots 0 / 1 are wave-local; slot 2 spans both waves, so the Householder step publishes its
-// column and its partial sums through LDS around 4 workgroup barriers (slot 2's sums: the two
-// waves' halves added in a fixed order).  Eigenvalues, eigenvectors and the back-transform are
-// per lane, as in mode 5, and use the same arithmetic (sturm_gh_p, 1e-8 Laguerre stop,
-// one-Newton reciprocals); only slot 2's wave sums associate differently.
-// Per slot LDS: packed reflector rows + tables, zero-initialised (rows / columns beyond K
-// read as exact zeros) -> 36.9 KB per workgroup at K = 42: 4 workgroups (8 waves) per CU, each
-// wave under a 256-VGPR budget.
-constexpr int kT3Slot = 1120 + 8 * 48;  // reflector rows (K = 42, KP = 44) + 8 tables of 48
-
-__device__ __forceinline__ void split_total(double v, bool hi_lane, double& lo, double& hi) {
-  const double a = row16_sum(hi_lane ? 0.0 : v);
-  const double b = row16_sum(hi_lane ? v : 0.0);
-  lo = (readlane(a, 0) + readlane(a, 16)) + readlane(a, 32);
-  hi = readlane(b, 32) + readlane(b, 48);
-}
-
-template <int ABL = 0>
-__global__ __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(2))) void
-mc_bias_tri3_kernel(const double* __restrict__ D0, int K, int M, int DM,
-                    const double* __restrict__ Cz, const int* __restrict__ dvalid,
-                    double* __restrict__ vout) {
-  constexpr int KP = 44;
-  extern __shared__ __attribute__((aligned(16))) double sm[];
-  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
-  const bool hiL = l >= 42;
-  const int slot = hiL ? 2 : w;
-  const int r = hiL ? l - 42 + 22 * w : l;
-  const bool live = r < K;
-  const int q = blockIdx.x * 3 + slot;
-  const bool qok = q < DM;
-  const int d = qok ? q / M : 0, m = qok ? q % M : 0;
-  const bool dok = qok && dvalid[d] != 0;
-  for (int e = tid; e < 3 * kT3Slot + 8; e += 128) sm[e] = 0.0;
-  double* S = sm + slot * kT3Slot;
-  double* R = S;                        // packed reflector rows (tri2 layout)
-  double* wb = S + 1120;                // [48] broadcast w
-  double2* tb = (double2*)(wb + 48);    // [48] {alpha_i, beta_{i-1}^2}
-  double* be = (double*)(tb + 48);      // [48] beta_i
-  double* ta = be + 48;                 // [48] tau_s
-  double* dd = ta + 48;                 // [48] sqrt(D0)
-  double* gs = dd + 48;                 // [48] sorted diagonal; Laguerre x later
-  double* xc = gs + 48;                 // [48] column s of the step; Sturm counts later
-  double* part = sm + 3 * kT3Slot;      // [2] slot-2 sig halves, [2] slot-2 kk halves
-  __syncthreads();
-  const double* d0 = D0 + (size_t)d * K;
-  const double di = (dok && live) ? sqrt(fmax(d0[r], 0.0)) : 0.0;
-  if (live) dd[r] = di;
-  __syncthreads();
-  double a[KP];
-  const double* c = Cz + (size_t)m * K * K;
-  const int ri = live ? r : 0;
-#pragma unroll
-  for (int j = 0; j < KP; ++j) {
-    a[j] = (j < K && dok && live) ? di * c[j * K + ri] * dd[j] : 0.0;
-    if ((j & 7) == 7) lds_batch();
-  }
-  {
-    const double g = (dok && live) ? di * c[ri * K + ri] * di : 0.0;
-    if (live) wb[r] = g;
-    __syncthreads();
-    if (live) {
-      int rank = 0;
-      for (int j = 0; j < K; ++j) {
-        const double h = wb[j];
-        rank += (h > g) || (h == g && j < r);
-      }
-      gs[rank] = g;
-    }
-    __syncthreads();
-  }
-  // ---- 1. Householder tridiagonalisation, 3 problems in lock step ----
-  auto steps = [&](auto J0c) {
-    constexpr int J0 = decltype(J0c)::value;
-    for (int s = J0; s < J0 + 8 && s < K; ++s) {
-      double xs = a[J0];
-#pragma unroll
-      for (int k = 1; k < 8; ++k)
-        if (J0 + k < KP) {
-          double t = a[J0 + k];
-          asm volatile("" : "+v"(t));
-          xs = s == J0 + k ? t : xs;
-        }
-      const bool act = live && r > s;
-      const double x = act ? xs : 0.0;
-      if (live) xc[r] = xs;
-      double slo, shi;
-      split_total(live && r > s + 1 ? x * x : 0.0, hiL, slo, shi);
-      if (l == 0) part[w] = shi;
-      __syncthreads();  // B1: column s and slot 2's partial norms
-      const double x0 = s + 1 < K ? xc[s + 1] : 0.0;
-      const double alpha = xc[s];
-      const double sig = hiL ? part[0] + part[1] : slo;
-      double u = 0.0, tau = 0.0, beta = x0;
-      if (sig != 0.0) {
-        const double n2 = fma(x0, x0, sig);
-        const double nrm = n2 * rsq_nr(n2);
-        beta = x0 >= 0.0 ? -nrm : nrm;
-        tau = rcp_nr(nrm * (nrm + fabs(x0)));
-        u = act ? (r == s + 1 ? x0 - beta : x) : 0.0;
-      }
-      double* us = R + tri2_row_off<KP>(s) - J0;
-      if (s + 2 < K && live && r >= J0 && r < KP) us[r] = u;
-      if (r == 0) {
-        tb[s] = double2{alpha, s > 0 ? be[s - 1] * be[s - 1] : 0.0};
-        be[s] = beta;
-        ta[s] = tau;
-      }
-      __syncthreads();  // B2: u_s of every slot
-      double p0 = 0.0, p1 = 0.0;
-      if (s + 2 >= K) us = R + tri2_row_off<KP>(J0) - J0;
-#pragma unroll
-      for (int j = J0; j < KP; j += 2) {
-        const double2 uu = *(const double2*)(us + j);
-        p0 = fma(a[j], uu.x, p0);
-        p1 = fma(a[j + 1], uu.y, p1);
-        if (((j - J0) & 7) == 6) lds_batch();
-      }
-      const double p = act ? tau * (p0 + p1) : 0.0;
-      double klo, khi;
-      split_total(u * p, hiL, klo, khi);
-      if (l == 0) part[2 + w] = khi;
-      __syncthreads();  // B3: slot 2's partial u^T p
-      const double kk = 0.5 * tau * (hiL ? part[2] + part[3] : klo);
-      const double wv = p - kk * u;
-      if (live) wb[r] = wv;
-      __syncthreads();  // B4: w of every slot
-#pragma unroll
-      for (int j = J0; j < KP; j += 2) {
-        const double2 ww = *(const double2*)(wb + j), uu = *(const double2*)(us + j);
-        a[j] = fma(-u, ww.x, fma(-wv, uu.x, a[j]));
-        a[j + 1] = fma(-u, ww.y, fma(-wv, uu.y, a[j + 1]));
-        if (((j - J0) & 7) == 6) lds_batch();
-      }
-    }
-  };
-  [&]<int... G>(std::integer_sequence<int, G...>) {
-    (steps(std::integral_constant<int, 8 * G>{}), ...);
-  }(std::make_integer_sequence<int, (KP + 7) / 8>{});
-  __syncthreads();
-  // ---- 2. eigenvalue of rank r (descending), as mode 5; Gershgorin bounds from the tables ----
-  double gl = __builtin_inf(), gu = -__builtin_inf(), b2max = 0.0;
-  for (int i = 0; i < K; ++i) {
-    const double ad = tb[i].x;
-    const double rr = (i > 0 ? fabs(be[i - 1]) : 0.0) + (i + 1 < K ? fabs(be[i]) : 0.0);
-    gl = fmin(gl, ad - rr);
-    gu = fmax(gu, ad + rr);
-    b2max = fmax(b2max, tb[i].y);
-  }
-  const double tnorm = fmax(fabs(gl), fabs(gu));
-  const double pivmin = 2.2250738585072014e-308 * fmax(1.0, b2max);
-  constexpr double kEps = 2.220446049250313e-16;
-  const double abstol = 1e-22 * tnorm + pivmin;
-  const int jt = K - 1 - r;
-  double lo = gl - 2.0 * kEps * tnorm - pivmin, hi = gu + 2.0 * kEps * tnorm + pivmin;
-  double x = live ? fmin(fmax(gs[r], lo), hi) : 0.5 * (lo + hi);
-  double G = 0.0, H = 0.0;
-  int cnt = sturm_gh_p(tb, K, x, G, H);
-  __syncthreads();  // every lane has read its gs slot
-  int* csv = (int*)xc;
-  if (live) {
-    gs[r] = x;
-    csv[r] = cnt;
-  }
-  __syncthreads();
-  for (int i = 0; i < K; ++i) {
-    const double xl = gs[i];
-    const int cl = csv[i];
-    if (cl <= jt) lo = fmax(lo, xl); else hi = fmin(hi, xl);
-  }
-  double lam = x;
-  if (live && dok && (ABL & 1) == 0) {
-    int prev = -1;
-    double sprev = __builtin_inf();
-    for (int it = 0; it < 256; ++it) {
-      bool lag = false;
-      double xn = 0.0;
-      if (cnt == jt || cnt == jt + 1) {
-        xn = laguerre_toward(x, G, H, K, cnt == jt);
-        double st = fabs(xn - x);
-        if (prev == cnt && st >= 1.5 * sprev) {
-          xn = fma(8.0, xn - x, x);
-          st *= 8.0;
-        }
-        lag = __builtin_isfinite(xn) && xn >= lo && xn <= hi;
-        if (lag && prev == cnt && st <= 1e-8 * fabs(x) && st <= 0.25 * sprev) { x = xn; break; }
-        sprev = lag ? st : __builtin_inf();
-      }
-      if (!lag) { xn = 0.5 * (lo + hi); sprev = __builtin_inf(); }
-      if (hi - lo <= 2.0 * kEps * (fabs(lo) + fabs(hi)) + abstol) { x = 0.5 * (lo + hi); break; }
-      prev = lag ? cnt : -1;
-      x = xn;
-      cnt = sturm_gh_p(tb, K, x, G, H);
-      if (cnt <= jt) lo = x; else hi = x;
-    }
-    lam = x;
-  }
-  // ---- 3. eigenvector of T at lam (twisted factorisation), as mode 5 ----
-  double y[KP];
-  if (live && dok && (ABL & 2) == 0) {
-    double dp = 0.0;
-#pragma unroll
-    for (int i = 0; i < KP; ++i) {
-      if (i < K) {
-        const double2 t = tb[i];
-        dp = guard_pivot(i == 0 ? t.x - lam : (t.x - lam) - t.y * rcp_nr1(dp), pivmin);
-      }
-      y[i] = i < K ? dp : 0.0;
-    }
-    double dm = 0.0, gmin = 0.0;
-    int rt = K - 1;
-#pragma unroll
-    for (int i = KP - 1; i >= 0; --i) {
-      if (i < K) {
-        const double ai = tb[i].x - lam;
-        dm = guard_pivot(i == K - 1 ? ai : ai - tb[i + 1].y * rcp_nr1(dm), pivmin);
-        const double g = fabs(y[i] + dm - ai);
-        if (i == K - 1 || g < gmin) { gmin = g; rt = i; }
-      }
-    }
-    double cz = 1.0, nrm = 1.0;
-#pragma unroll
-    for (int i = KP - 1; i >= 0; --i) {
-      if (i < rt) {
-        cz = -be[i] * cz * rcp_nr1(y[i]);
-        nrm = fma(cz, cz, nrm);
-        y[i] = cz;
-      }
-    }
-    dm = 0.0;
-#pragma unroll
-    for (int i = KP - 1; i >= 0; --i) {
-      if (i < K && i > rt) {
-        const double ai = tb[i].x - lam;
-        dm = guard_pivot(i == K - 1 ? ai : ai - tb[i + 1].y * rcp_nr1(dm), pivmin);
-        y[i] = dm;
-      }
-    }
-    cz = 1.0;
-#pragma unroll
-    for (int i = 0; i < KP; ++i) {
-      if (i == rt) y[i] = 1.0;
-      if (i > rt && i < K) {
-        cz = -be[i - 1] * cz * rcp_nr1(y[i]);
-        nrm = fma(cz, cz, nrm);
-        y[i] = cz;
-      }
-      if (i >= K) y[i] = 0.0;
-    }
-    const double sc = rsq_nr(nrm);
-#pragma unroll
-    for (int i = 0; i < KP; ++i) y[i] *= sc;
-  } else {
-#pragma unroll
-    for (int i = 0; i < KP; ++i) y[i] = 0.0;
-  }
-  // ---- 4. back-transform and the bias ratio ----
-  if ((ABL & 2) == 0) {
-    auto back = [&](auto J0c, int s_hi) {
-      constexpr int J0 = decltype(J0c)::value;
-      for (int s = s_hi; s >= J0; --s) {
-        if (s + 2 >= K) continue;
-        const double tau = ta[s];
-        if (tau == 0.0) continue;
-        const double* us = R + tri2_row_off<KP>(s) - J0;
-        double t0 = 0.0, t1 = 0.0;
-#pragma unroll
-        for (int j = J0; j < KP; j += 2) {
-          const double2 uu = *(const double2*)(us + j);
-          t0 = fma(uu.x, y[j], t0);
-          t1 = fma(uu.y, y[j + 1], t1);
-          if (((j - J0) & 7) == 6) lds_batch();
-        }
-        const double f = tau * (t0 + t1);
-#pragma unroll
-        for (int j = J0; j < KP; j += 2) {
-          const double2 uu = *(const double2*)(us + j);
-          y[j] = fma(-f, uu.x, y[j]);
-          y[j + 1] = fma(-f, uu.y, y[j + 1]);
-          if (((j - J0) & 7) == 6) lds_batch();
-        }
-      }
-    };
-    [&]<int... G>(std::integer_sequence<int, G...>) {
-      constexpr int NG = (KP + 7) / 8;
-      (back(std::integral_constant<int, 8 * (NG - 1 - G)>{}, 8 * (NG - 1 - G) + 7), ...);
-    }(std::make_integer_sequence<int, (KP + 7) / 8>{});
-  }
-  if (!qok || !live) return;
-  double* vo = vout + (size_t)q * K;
-  if (!dok) {
-    vo[r] = qnan();
-    return;
-  }
-  double v = 0.0;
-#pragma unroll
-  for (int j = 0; j < KP; ++j)
-    if (j < K) v = fma(dd[j] * dd[j], y[j] * y[j], v);
-  vo[r] = (ABL & 2) ? lam : v / lam;
-}
+#if MFA_AB
+#include "ab/eigen_tri3.h"
+#endif
 
 // Householder steps per reflector-row group of the production tridiagonal kernels: a group of
 // GS steps stores / reads / updates columns [GS floor(s / GS), KP), so smaller groups waste
 // fewer fmas on the columns left of s (exact zeros: bitwise the same results) and select the
 // step's column from fewer registers, at more unrolled code.  Bias solver at 2520 x 100 (A/B
-// modes 27 / 25 / 5, profiles/r05/r05ai): GS = 8 11.64, 4 11.14, 2 10.82 ms (128 VGPRs, 4 waves
-// per SIMD, no scratch).  Used by the measured bias instantiations at KP = 42 / 44 (K <= 44,
-// with KP-entry tables, LT); the other widths, the date chains and the EIG mode keep GS = 8 (at
-// GS = 2 they spill to scratch).
+// modes 27 / 25 / 5, profiles/r05/r05ai): GS = 8 11.64, 4 11.14, 2 10.82 ms.  Every bias
+// instantiation runs GS = 2 with KP-entry tables (round 6: K = 32 6.65 -> 5.77 ms, K = 48 / 64
+// -20 %, bitwise the same ratios, profiles/r06/bias_k_bench_*.log); the date chains and the
+// EIG mode keep GS = 8.
 constexpr int kTri2GS = 2;
 
-size_t bias_tri3_lds() { return (3 * (size_t)kT3Slot + 8) * sizeof(double); }
 
 size_t bias_tri2_lds(int K, int KP, int GS = 8, bool LT = false) {
   int n = 0;
@@ -2346,152 +1526,7 @@ MFA_API int mfa_eigen_set_bias_mode(int mode) {
 }
 
 #if MFA_AB
-// A/B-only solvers and timing ablations (tools builds, MFA_AB=1): mode 4 (lean layout, pivot-form
-// Sturm), 3 (round-2 kernel), 11 (lane-dense), 6-20 (mode-5 variants), 41-67 (ablations).
-bool launch_bias_tri_ab(const double* D0, int D, int K, int M, const double* Cz, const int* dvalid,
-                     double* ws, hipStream_t s) {
-  if (g_bias_mode == 4 || g_bias_mode == 5) {
-#define MFA_TRI2(KP_)                                                                        \
-    if (K <= KP_) {                                                                        \
-      if (g_bias_mode == 5) /* padded eigenvector phase at the measured width (K <= 44) */ \
-        hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, true, 0, MFA_TRI2_WPE, false, 8, 8, 2,  \
-                                                (KP_ == 44), false, (KP_ == 44)>),         \
-                           dim3(D * M), dim3(64),                                          \
-                           bias_tri2_lds(K, KP_), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D, 0);            \
-      else                                                                                 \
-        hipLaunchKernelGGL((mc_bias_tri2_kernel<KP_, false>), dim3(D * M), dim3(64),       \
-                           bias_tri2_lds(K, KP_), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D, 0);            \
-      return true;                                                                         \
-    }
-    MFA_TRI2(8)
-    MFA_TRI2(16)
-    MFA_TRI2(24)
-    MFA_TRI2(32)
-    MFA_TRI2(44)
-    MFA_TRI2(48)
-    MFA_TRI2(64)
-#undef MFA_TRI2
-    return false;
-  }
-  if ((g_bias_mode == 11 || g_bias_mode == 111 || g_bias_mode == 112) && K <= 42 &&
-      tri2_rows_doubles<44>(K) <= 1120) {  // lane-dense: 3 problems per 2-wave workgroup
-    const int DM = D * M, blocks = (DM + 2) / 3;
-    if (g_bias_mode == 11)
-      hipLaunchKernelGGL((mc_bias_tri3_kernel<0>), dim3(blocks), dim3(128), bias_tri3_lds(), s, D0,
-                         K, M, DM, Cz, dvalid, ws);
-    else if (g_bias_mode == 111)  // timing: no Laguerre iterations
-      hipLaunchKernelGGL((mc_bias_tri3_kernel<1>), dim3(blocks), dim3(128), bias_tri3_lds(), s, D0,
-                         K, M, DM, Cz, dvalid, ws);
-    else  // timing: no eigenvectors / back-transform
-      hipLaunchKernelGGL((mc_bias_tri3_kernel<2>), dim3(blocks), dim3(128), bias_tri3_lds(), s, D0,
-                         K, M, DM, Cz, dvalid, ws);
-    return true;
-  }
-  if ((g_bias_mode == 15 || g_bias_mode == 16) && K <= 44) {  // A/B: padded + every reflector
-    // row stored, LDS reads fenced every 2 (15) / 1 (16) double2 steps (LB 4 / 2: fewer spills)
-    if (g_bias_mode == 15)
-      hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 4, 2, true, true>),
-                         dim3(D * M), dim3(64), bias_tri2_lds(K + 2, 44), s, D0, K, M, Cz, dvalid,
-                         ws, nullptr, nullptr, D, 0);
-    else
-      hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 2, 2, true, true>),
-                         dim3(D * M), dim3(64), bias_tri2_lds(K + 2, 44), s, D0, K, M, Cz, dvalid,
-                         ws, nullptr, nullptr, D, 0);
-    return true;
-  }
-  if (g_bias_mode == 20 && K <= 44) {  // A/B: the default + tau-only back-transform skips
-    hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, true, false, true, false, true>),
-                       dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws,
-                       nullptr, nullptr, D, 0);
-    return true;
-  }
-  if (g_bias_mode == 19 && K <= 44) {  // A/B: the default + Newton-refined Laguerre arithmetic
-    hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, true, false, true, true>),
-                       dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws,
-                       nullptr, nullptr, D, 0);
-    return true;
-  }
-  if (g_bias_mode == 18 && K <= 44) {  // A/B: padded, steps s >= K-2 skip the update
-    hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, true, false, true>),
-                       dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws,
-                       nullptr, nullptr, D, 0);
-    return true;
-  }
-  if (g_bias_mode == 14 && K <= 44) {  // A/B: mode 5 with the unpadded eigenvector phase
-    hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 2, false>),
-                       dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws,
-                       nullptr, nullptr, D, 0);
-    return true;
-  }
-  if (g_bias_mode == 13 && K <= 44) {  // A/B: four accumulators per matvec / dot product
-    hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 8, 4>), dim3(D * M),
-                       dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D, 0);
-    return true;
-  }
-  if (g_bias_mode == 10 && K <= 44) {  // A/B: LDS broadcast reads fenced in batches of 8 x 16 B
-    hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 8, 16>), dim3(D * M),
-                       dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D, 0);
-    return true;
-  }
-  if ((g_bias_mode == 8 || g_bias_mode == 9) && K <= 44) {  // A/B: Laguerre stop at 1e-9 / 1e-7
-    if (g_bias_mode == 8)
-      hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 9>), dim3(D * M),
-                         dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D, 0);
-    else
-      hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, MFA_TRI2_WPE, false, 7>), dim3(D * M),
-                         dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D, 0);
-    return true;
-  }
-  if ((g_bias_mode == 6 || g_bias_mode == 7) && K <= 44) {  // A/B: mode 5 at 4 / 5 waves per SIMD
-    if (g_bias_mode == 6)
-      hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, 4>), dim3(D * M), dim3(64),
-                         bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D, 0);
-    else
-      hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, 0, 5>), dim3(D * M), dim3(64),
-                         bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D, 0);
-    return true;
-  }
-  if (g_bias_mode > 60 && g_bias_mode < 69 && K <= 44) {  // timing-only ablations of mode 5
-    const int abl = g_bias_mode == 68 ? 32 : g_bias_mode - 60;  // 68: Sturm-evaluation counts
-#define MFA_TRI2_ABL(A_)                                                                     \
-    if (abl == A_)                                                                         \
-      hipLaunchKernelGGL((mc_bias_tri2_kernel<44, true, A_, MFA_TRI2_WPE, false, 8, 8, 2, true, \
-                                              false, true>),                                \
-                         dim3(D * M), dim3(64), bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, \
-                         ws, nullptr, nullptr, D, 0);
-    MFA_TRI2_ABL(1) MFA_TRI2_ABL(2) MFA_TRI2_ABL(3) MFA_TRI2_ABL(4) MFA_TRI2_ABL(5)
-    MFA_TRI2_ABL(6) MFA_TRI2_ABL(7) MFA_TRI2_ABL(32)
-#undef MFA_TRI2_ABL
-    return true;
-  }
-#define MFA_TRI(KP_)                                                                         \
-  if (K <= KP_) {                                                                          \
-    hipLaunchKernelGGL((mc_bias_tri_kernel<KP_>), dim3(D * M), dim3(64), bias_tri_lds(K, KP_), s, \
-                       D0, K, M, Cz, dvalid, ws);                                          \
-    return true;                                                                           \
-  }
-  if (g_bias_mode > 40 && g_bias_mode < 60 && K <= 44) {  // timing-only ablations
-    const int abl = g_bias_mode - 40;
-#define MFA_TRI_ABL(A_)                                                                      \
-    if (abl == A_)                                                                         \
-      hipLaunchKernelGGL((mc_bias_tri_kernel<44, A_>), dim3(D * M), dim3(64), bias_tri_lds(K, 44), \
-                         s, D0, K, M, Cz, dvalid, ws);
-    MFA_TRI_ABL(1) MFA_TRI_ABL(2) MFA_TRI_ABL(3) MFA_TRI_ABL(4) MFA_TRI_ABL(5) MFA_TRI_ABL(6)
-    MFA_TRI_ABL(7) MFA_TRI_ABL(8) MFA_TRI_ABL(16)
-#undef MFA_TRI_ABL
-    return true;
-  }
-  MFA_TRI(8)
-  MFA_TRI(16)
-  MFA_TRI(24)
-  MFA_TRI(32)
-  MFA_TRI(44)
-  MFA_TRI(48)
-  MFA_TRI(64)
-#undef MFA_TRI
-  return false;
-}
-
+#include "ab/eigen_ab_launch.h"
 #endif  // MFA_AB
 
 // Householder-tridiagonal solver (mode 5, the default): KP = K rounded up to an instantiated

@@ -687,11 +687,14 @@ void launch_ew_seg(const float* a, const float* b, const int* seg_v, const int* 
 // r - L], source k weighted lam^(k - kl) (RSTR's oldest row weighs 1, quirk Q14; lam = 1 for
 // the sums).  With 64-row segments j and the segment-local prefix G_j(p) = sum_(64j <= i <= p)
 // lam^(i - 64j) x_i (one DPP scan per segment), the window sum anchored at jl = kl / 64 is
-//   (T_jl + lam^64 (T_(jl+1) + ... + lam^64 G_jr(kr))) - G_jl(kl - 1)
-// (T = segment totals; the RSTR ratio's common factor lam^(kl - 64 jl) cancels): <= 9 fmas per
-// row.  A 256-thread block stages 2048 output rows plus an H-row halo (H >= the reach W + L - 1
-// rounded up to 64), every row loaded once into registers and scanned per 64-row segment.
+//   S_jl(m) + lam^(64 m) G_jr(kr) - G_jl(kl - 1),   m = jr - jl,
+// S_j(m) = T_j + lam^64 T_(j+1) + ... + lam^(64 (m-1)) T_(j+m-1) (T = segment totals) -- a
+// left-fold table of <= 9 entries per segment built once per tile, so a row costs one fma and a
+// handful of LDS reads whatever its window spans (the RSTR ratio's common factor lam^(kl - 64 jl)
+// cancels).  A 256-thread block stages 2048 output rows plus an H-row halo (H >= the reach
+// W + L - 1 rounded up to 64), every row loaded once and scanned per 64-row segment.
 constexpr int kPosOut = 2048;
+constexpr int kPosMF = 9;  // fold-table entries per segment: m = 0 .. 8 (reach <= 512)
 
 template <int H, bool RATIO, int NW>
 __global__ __launch_bounds__(256) void poswin_seg_kernel(
@@ -705,6 +708,9 @@ __global__ __launch_bounds__(256) void poswin_seg_kernel(
   __shared__ unsigned char gc[NSEG * 64];
   __shared__ double tn[NSEG], td[NSEG];
   __shared__ int tc[NSEG];
+  __shared__ double fn[NSEG][kPosMF], fd[RATIO ? NSEG : 1][kPosMF];
+  __shared__ int fc[NSEG][kPosMF];
+  __shared__ double lpm[kPosMF];  // lam^(64 m)
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g0 = blockIdx.x * kPosOut - H;
   // lam^lane and lam^64 from one product scan: the same bits in every workgroup
@@ -737,6 +743,30 @@ __global__ __launch_bounds__(256) void poswin_seg_kernel(
       tc[s] = c;
     }
   }
+  if (threadIdx.x == 0) {
+    double p = 1.0;
+    for (int m = 0; m < kPosMF; ++m, p *= l64) lpm[m] = p;
+  }
+  __syncthreads();
+  // the fold tables: one thread per segment, m = 0 .. 8 in order (within the tile)
+  if (threadIdx.x < NSEG) {
+    const int j = threadIdx.x;
+    double an = 0.0, ad = 0.0;
+    int ac = 0;
+    fn[j][0] = 0.0;
+    if constexpr (RATIO) fd[j][0] = 0.0;
+    fc[j][0] = 0;
+    for (int m = 1; m < kPosMF; ++m) {
+      if (j + m - 1 < NSEG) {
+        an = fma(lpm[m - 1], tn[j + m - 1], an);
+        if constexpr (RATIO) ad = fma(lpm[m - 1], td[j + m - 1], ad);
+        ac += tc[j + m - 1];
+      }
+      fn[j][m] = an;
+      if constexpr (RATIO) fd[j][m] = ad;
+      fc[j][m] = ac;
+    }
+  }
   __syncthreads();
 #pragma unroll
   for (int k = 0; k < kPosOut / 256; ++k) {
@@ -752,22 +782,20 @@ __global__ __launch_bounds__(256) void poswin_seg_kernel(
       const int kr = r - L, kl = max(s0, r - W + 1 - L);
       float res = qnanf();
       if (kr >= kl) {
-        const int tl = kl - g0, tr = kr - g0, jl = tl >> 6, jr = tr >> 6;
-        double an = gn[tr], ad = RATIO ? gd[tr] : 0.0;
-        int c = gc[tr];
-        for (int j = jr - 1; j >= jl; --j) {
-          an = fma(l64, an, tn[j]);
-          if constexpr (RATIO) ad = fma(l64, ad, td[j]);
-          c += tc[j];
-        }
-        if (tl & 63) {
-          an -= gn[tl - 1];
-          if constexpr (RATIO) ad -= gd[tl - 1];
-          c -= gc[tl - 1];
-        }
+        const int tl = kl - g0, tr = kr - g0, jl = tl >> 6, m = (tr >> 6) - jl;
+        const bool mid = (tl & 63) != 0;
+        const double f = lpm[m];
+        double an = fma(f, gn[tr], fn[jl][m]);
+        if (mid) an -= gn[tl - 1];
+        int c = fc[jl][m] + gc[tr] - (mid ? gc[tl - 1] : 0);
         if (c >= mp) {
-          if constexpr (RATIO) res = (float)(an * frcp(ad));
-          else res = log_out ? (an == 0.0 ? qnanf() : (float)log(an)) : (float)an;
+          if constexpr (RATIO) {
+            double ad = fma(f, gd[tr], fd[jl][m]);
+            if (mid) ad -= gd[tl - 1];
+            res = (float)(an * frcp(ad));
+          } else {
+            res = log_out ? (an == 0.0 ? qnanf() : (float)log(an)) : (float)an;
+          }
         }
       }
       o[ro] = res;
@@ -775,21 +803,23 @@ __global__ __launch_bounds__(256) void poswin_seg_kernel(
   }
 }
 
-// ---- CMRA (full windows): max - min of the window's cumulative log returns,
+// ---- CMRA (full windows): max - min of the window's cumulative log returns (the reference's
+// ln(1 + max Z) - ln(1 + min Z), Z = exp(cumsum) - 1, is that difference: no exp / log per row),
 // c_i = P(i) - P(r - W) over i in [r - W + 1, r], P anchored at the 64-row segment of the
-// window's first row.  P(i) = B_j + G_j(i) on segment j (B = the left fold of the segment
-// totals), and since x -> fl(B + x) is monotone, the window max is the max of the pieces
-// fl(B_j + max G_j over the piece): the first segment's suffix extremum (an LDS table from a
-// lane-reversed DPP scan), whole middle segments, and the last segment's prefix extremum (a DPP
-// scan of the row's own segment).  Any non-finite row in the window (or a window crossing the
-// stock start) gives NaN.  64 < W <= 257.
+// window's first row; the base P(r - W) cancels in max - min.  P(i) = B_j + G_j(i) on segment j
+// (B = the left fold of the segment totals), and since x -> fl(B + x) is monotone, the window
+// max is the max of the pieces fl(B_j + max G_j over the piece): the first segment's suffix
+// extremum (an LDS table from a lane-reversed DPP scan), whole middle segments, and the last
+// segment's prefix extremum (registers: each wave scans the segments it outputs).  Any
+// non-finite row in the window (or a window crossing the stock start) gives NaN.  64 < W <= 257.
+// Waves: wave w scans halo segment w and output segments 4 + 8w .. 4 + 8w + 7.
 template <int H>
 __global__ __launch_bounds__(256) void cmra_seg_kernel(const float* __restrict__ x,
                                                        const int* __restrict__ seg_v,
                                                        const int* __restrict__ omap, int Rv, int W,
                                                        float* __restrict__ out) {
-  constexpr int NSEG = (H + kPosOut) / 64, SPW = NSEG / 4;
-  static_assert(NSEG % 4 == 0, "segments split over the 4 waves");
+  constexpr int HS = H / 64, NSEG = HS + kPosOut / 64, OPW = kPosOut / 256;
+  static_assert(HS == 4, "one halo segment per wave");
   __shared__ double g[NSEG * 64], smx[NSEG * 64], smn[NSEG * 64];
   __shared__ unsigned char gbad[NSEG * 64];
   __shared__ double tot[NSEG];
@@ -797,15 +827,17 @@ __global__ __launch_bounds__(256) void cmra_seg_kernel(const float* __restrict__
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int g0 = blockIdx.x * kPosOut - H;
   const unsigned long long below = lane == 63 ? ~0ull : (2ull << lane) - 1;
-  float v[SPW];
+  auto seg_of = [&](int k) { return k == OPW ? wid : HS + wid * OPW + k; };  // k = OPW: halo
+  float v[OPW + 1];
 #pragma unroll
-  for (int k = 0; k < SPW; ++k) {
-    const int gi = g0 + (wid * SPW + k) * 64 + lane;
+  for (int k = 0; k <= OPW; ++k) {
+    const int gi = g0 + seg_of(k) * 64 + lane;
     v[k] = (gi >= 0 && gi < Rv) ? x[gi] : qnanf();
   }
+  double pmx[OPW], pmn[OPW];
 #pragma unroll
-  for (int k = 0; k < SPW; ++k) {
-    const int s = wid * SPW + k;
+  for (int k = 0; k <= OPW; ++k) {
+    const int s = seg_of(k);
     const bool ok = fin(v[k]);
     const double G = wave_scan_sum(ok ? (double)v[k] : 0.0);
     const int bad = __popcll(__ballot(!ok) & below);
@@ -819,13 +851,15 @@ __global__ __launch_bounds__(256) void cmra_seg_kernel(const float* __restrict__
       tot[s] = G;
       tbad[s] = bad;
     }
+    if (k < OPW) {  // an output segment: its prefix extrema stay in registers
+      pmx[k] = wave_scan_ext<true>(G);
+      pmn[k] = wave_scan_ext<false>(G);
+    }
   }
   __syncthreads();
 #pragma unroll
-  for (int k = 0; k < kPosOut / 256; ++k) {
-    const int tr = H + (wid * (kPosOut / 256) + k) * 64 + lane, r = g0 + tr;
-    const double Gv = g[tr];
-    const double pmax = wave_scan_ext<true>(Gv), pmin = wave_scan_ext<false>(Gv);
+  for (int k = 0; k < OPW; ++k) {
+    const int tr = seg_of(k) * 64 + lane, r = g0 + tr;
     if (r >= Rv) continue;
     const int ro = omap[r];
     if (ro < 0) continue;
@@ -836,22 +870,21 @@ __global__ __launch_bounds__(256) void cmra_seg_kernel(const float* __restrict__
       int bad = gbad[tr] - ((tl & 63) ? gbad[tl - 1] : 0);
       for (int j = jl; j < jr; ++j) bad += tbad[j];
       if (bad == 0) {
-        const double base = (tl & 63) ? g[tl - 1] : 0.0;
         double mx = smx[tl], mn = smn[tl], B = tot[jl];
         for (int j = jl + 1; j < jr; ++j) {
           mx = vmax64(mx, B + smx[j * 64]);
           mn = vmin64(mn, B + smn[j * 64]);
           B += tot[j];
         }
-        mx = vmax64(mx, B + pmax);
-        mn = vmin64(mn, B + pmin);
-        const double cmax = mx - base, cmin = mn - base;
-        o = (float)(log(1.0 + (exp(cmax) - 1.0)) - log(1.0 + (exp(cmin) - 1.0)));
+        mx = vmax64(mx, B + pmx[k]);
+        mn = vmin64(mn, B + pmn[k]);
+        o = (float)(mx - mn);
       }
     }
     out[ro] = o;
   }
 }
+
 // ------------------------------------------------------------------------------------------
 // Statement-row TTM (factor_calculator.py:392-410, quirk Q18): the rows of a stock form runs of
 // one (ts_code, end_date) statement (a point-in-time as-of join keeps end_date non-decreasing),
@@ -933,7 +966,6 @@ __global__ __launch_bounds__(256) void leverage_kernel(const float* __restrict__
   mlev[r] = __builtin_isinf(ml) ? qnanf() : (float)ml;
   blev[r] = b > 0.0 ? (float)((b + n) / b) : qnanf();
 }
-
 
 // ---- the segment layout itself (ops/rolling.py SegLayout), in three row-parallel passes
 // around one int32 prefix sum instead of ~30 tensor ops:

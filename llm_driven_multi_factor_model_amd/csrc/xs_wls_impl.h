@@ -1188,282 +1188,9 @@ __global__ __launch_bounds__(256) void xs_r2_combine_kernel(const double* __rest
   r2out[d] = (status[d] & XS_BAD) ? qnan() : 1.0 - ve / vr;
 }
 
-// ------------------------------------------------------------------------------------------
-// K1 on the matrix cores: the dense moments as ONE 16 x 16 fp64 MFMA accumulator per wave.
-//
-// Lane l owns Gram channel c = l & 15 and, per k-step, stock k0 + (l >> 4) of its 64-stock
-// tile: v_mfma_f64_16x16x4f64 accumulates G[i][j] += sum_k alpha_i(k) beta_j(k) over 4 stocks
-// with (for a valid stock, weight w = sqrt(cap); invalid stocks contribute 0):
-//   channel  c < Q : alpha = x_c,  beta = w x_c        -> G[p][q] = Swxx,  G[p][Q] = Swxr
-//            c = Q : alpha = r,    beta = w r           G[p][Q+1] = Scx (beta = w w = cap)
-//          c = Q+1 : alpha = w,    beta = w w           G[Q+2][Q+1] = Sc, G[Q+2][Q+2] = n
-//          c = Q+2 : alpha = 1,    beta = 1             G[p][Q+2] summed over p = Sx
-//          c = Q+3 : alpha = sum_q x_q^2, beta = 0      G[Q+3][Q+2] = Sxx
-// The 79 per-lane fp64 accumulators of the VALU body (158 VGPRs: 2 waves / SIMD) become 8
-// VGPRs per lane, so 3-4 workgroups fit on a CU.  A per-stock prep pass (lane = stock) checks
-// validity, does the industry segment atomics and writes {w or -1, sum x^2} to a per-wave aux
-// row; ring rows are padded (+8 B fp32 / +16 B fp64) so the 16 channel reads of one k-step hit
-// distinct LDS banks.  The 4 waves' accumulators are summed in wave order (deterministic).
-// ------------------------------------------------------------------------------------------
-template <typename T> struct MfGeo;
-template <> struct MfGeo<float> {
-  static constexpr int ROWP = kWT * 4 + 8;    // padded fp32 row
-  static constexpr int NB = 2;                // ring slots per wave
-};
-template <> struct MfGeo<double> {
-  static constexpr int ROWP = kWT * 8 + 16;   // padded fp64 row
-  static constexpr int NB = 2;
-};
-
-template <int Q, typename T>
-struct RingMF {
-  static constexpr int ROWP = MfGeo<T>::ROWP;
-  static constexpr int NB = MfGeo<T>::NB;
-  static constexpr int WSLOT = (Q + 2) * ROWP + kWT * 2;     // rows | int16 ids
-  static constexpr int AUX = kWT * 16;                        // {w | -1, sum x^2} per stock
-  static constexpr int RED = 256 * 8;                          // this wave's 16x16 tile
-  static constexpr int RW0 = NB * WSLOT + AUX;
-  static constexpr int RINGW = RW0 > RED ? RW0 : RED;
-  static constexpr int BYTES = 4 * RINGW;
-};
-
-template <int Q, typename T>
-__device__ __forceinline__ constexpr int dma_per_tile_mf(bool has_ind) {
-  return Q + 2 + (has_ind ? 1 : 0);  // one (padded) row per instruction
-}
-
-template <int Q, int VAR, int R, typename T>
-__device__ __forceinline__ void moments_body_mf(
-    const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
-    const int16_t* __restrict__ ind, int N, int Pseg, int d, char* ring, double* dyn,
-    double* md, int nb = 0, int ne = -1, double* __restrict__ gout = nullptr) {
-  static_assert(Q + 4 <= 16, "one 16x16 MFMA tile: Q <= 12");
-  using L = Layout<Q, T>;
-  using G = RingMF<Q, T>;
-  constexpr int NS = L::NS, NG = L::NG, NACC = L::NACC;
-  constexpr int WSLOT = G::WSLOT, RINGW = G::RINGW, NB = G::NB, ROWP = G::ROWP;
-  if (ne < 0) ne = N;
-  const int tid = threadIdx.x, nthr = blockDim.x;
-  const int lane = tid & 63, wid = tid >> 6, nw = nthr >> 6;
-  constexpr bool DET = (VAR & 32) != 0;
-  const int rep = DET ? wid * (R / 4) + (lane & (R / 4 - 1)) : (lane & (R - 1));
-  const unsigned seg_a = lds_addr(dyn + rep);
-  for (int i = tid; i < R * Pseg * NS; i += nthr) dyn[i] = 0.0;
-  __syncthreads();
-
-  const T* Xd = X + (size_t)d * Q * N;
-  const T* cd = cap + (size_t)d * N;
-  const T* rd = ret + (size_t)d * N;
-  const int16_t* id = ind ? ind + (size_t)d * N : nullptr;
-
-  char* wring = ring + wid * RINGW;
-  double2* aux = (double2*)(wring + NB * WSLOT);
-  const int nrows = dma_per_tile_mf<Q, T>(id != nullptr);
-  const int ntile_all = (ne - nb + kWT - 1) / kWT;
-  const int ntile = ntile_all > wid ? (ntile_all - wid + nw - 1) / nw : 0;
-  auto issue = [&](int i) {
-    char* slot = wring + (i % NB) * WSLOT;
-    const int s0 = nb + (wid + i * nw) * kWT;
-    if constexpr (sizeof(T) == 4) {
-      const bool in = s0 + lane < ne;
-      if (in) glds4(cd + s0 + lane, slot);
-      if (in) glds4(rd + s0 + lane, slot + ROWP);
-#pragma unroll
-      for (int q = 0; q < Q; ++q)
-        if (in) glds4(Xd + (size_t)q * N + s0 + lane, slot + (2 + q) * ROWP);
-    } else {  // one 512-B fp64 row per instruction (lanes 0-31, 16 B each)
-      const int s = s0 + 2 * (lane & 31);
-      const bool in = lane < 32 && s < ne;
-      if (in) glds16(cd + s, slot);
-      if (in) glds16(rd + s, slot + ROWP);
-#pragma unroll
-      for (int q = 0; q < Q; ++q)
-        if (in) glds16(Xd + (size_t)q * N + s, slot + (2 + q) * ROWP);
-    }
-    if (id && lane < kWT / 2 && s0 + 2 * lane < ne) glds4(id + s0 + 2 * lane, slot + (Q + 2) * ROWP);
-  };
-  // this lane's Gram channel: ring row (x_c: 2 + c, r: 1, aux channels: row 0 as a dummy)
-  const int ch = lane & 15, kq = lane >> 4;
-  const int crow = ch < Q ? 2 + ch : (ch == Q ? 1 : 0);
-  v4d acc4[4];  // 4 independent accumulation chains (the f64 MFMA's dependent latency)
-#pragma unroll
-  for (int a = 0; a < 4; ++a) acc4[a] = v4d{0.0, 0.0, 0.0, 0.0};
-  for (int i = 0; i < NB - 1 && i < ntile; ++i) issue(i);
-  for (int i = 0; i < ntile; ++i) {
-    const bool tail = (i + NB - 1 >= ntile);
-    wait_vmcnt(tail ? 0 : (NB - 2) * nrows);
-    __builtin_amdgcn_wave_barrier();
-    if (i + NB - 1 < ntile) issue(i + NB - 1);
-    const char* slot = wring + (i % NB) * WSLOT;
-    const T* bf = (const T*)slot;
-    // ---- prep: lane = stock
-    {
-      const int s = nb + (wid + i * nw) * kWT + lane;
-      const T cf = *(const T*)(slot + lane * sizeof(T));
-      const T rf = *(const T*)(slot + ROWP + lane * sizeof(T));
-      const int j = id ? (int)((const int16_t*)(slot + (Q + 2) * ROWP))[lane] : 0;
-      T xf[Q];
-#pragma unroll
-      for (int q = 0; q < Q; ++q) xf[q] = *(const T*)(slot + (2 + q) * ROWP + lane * sizeof(T));
-      bool ok = (s < ne) && (j >= 0) && (j < Pseg) && finite_v(cf) && (cf >= T(0)) && finite_v(rf);
-#pragma unroll
-      for (int q = 0; q < Q; ++q) ok = ok && finite_v(xf[q]);
-      double w = -1.0, s2 = 0.0;
-      if (ok) {
-        const double c = cf, r = rf;
-        w = sqrt(c);
-        double wx[Q];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) {
-          wx[q] = w * (double)xf[q];
-          s2 = fma((double)xf[q], (double)xf[q], s2);
-        }
-        if (VAR & 1) {  // timing-only ablation: skip the segment atomics
-          asm volatile("" ::"v"(w), "v"(r));
-        } else {
-          const unsigned a = seg_a + (unsigned)(j * NS * R * 8);
-          lds_add_nowait<0>(a, w);
-          [&]<int... I>(std::integer_sequence<int, I...>) {
-            (lds_add_nowait<8 * R * (1 + I)>(a, wx[I]), ...);
-          }(std::make_integer_sequence<int, Q>{});
-          lds_add_nowait<8 * R * (Q + 1)>(a, w * r);
-          lds_add_nowait<8 * R * (Q + 2)>(a, c);
-        }
-      }
-      // aux row: asm store (like the segment atomics) so hipcc's waitcnt pass does not drain
-      // the in-flight DMA tile for it; LDS ops of one wave complete in order
-      const unsigned aa = lds_addr(aux + lane);
-      asm volatile("ds_write_b64 %0, %1\n\tds_write_b64 %0, %2 offset:8" ::"v"(aa), "v"(w),
-                   "v"(s2) : "memory");
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    // ---- matrix cores: 16 k-steps of 4 stocks
-    if constexpr ((VAR & 2) == 0) {
-      const T* rowp = (const T*)(slot + crow * ROWP);
-#pragma unroll
-      for (int k0 = 0; k0 < kWT; k0 += 4) {
-        const int k = k0 + kq;
-        const double2 a2 = aux[k];
-        const double raw = (double)rowp[k];
-        const bool okk = a2.x >= 0.0;
-        const double wp = okk ? a2.x : 0.0;
-        double al, be;
-        if (ch <= Q) {
-          al = okk ? raw : 0.0;
-          be = al * wp;
-        } else if (ch == Q + 1) {
-          al = wp;
-          be = wp * wp;
-        } else if (ch == Q + 2) {
-          al = okk ? 1.0 : 0.0;
-          be = al;
-        } else {
-          al = ch == Q + 3 ? a2.y : 0.0;
-          be = 0.0;
-        }
-        acc4[(k0 >> 2) & 3] = __builtin_amdgcn_mfma_f64_16x16x4f64(al, be, acc4[(k0 >> 2) & 3], 0, 0, 0);
-      }
-    }
-    __builtin_amdgcn_wave_barrier();
-  }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __syncthreads();
-  const v4d acc = (acc4[0] + acc4[1]) + (acc4[2] + acc4[3]);
-  // the 4 waves' 16x16 tiles, summed in wave order
-  double* tile = (double*)wring;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) tile[((lane >> 4) + 4 * r) * 16 + (lane & 15)] = acc[r];
-  __syncthreads();
-  auto gsum = [&](int i, int j) {
-    double t = 0.0;
-    for (int w = 0; w < nw; ++w) t += ((const double*)(ring + w * RINGW))[i * 16 + j];
-    return t;
-  };
-  double mv = 0.0;
-  if (tid < NG) {
-    int q = 0;
-    while ((q + 1) * (q + 2) / 2 <= tid) ++q;
-    mv = gsum(q, tid - q * (q + 1) / 2);
-  } else if (tid < NG + Q) {
-    mv = gsum(tid - NG, Q);
-  } else if (tid < NG + 2 * Q) {
-    mv = gsum(tid - NG - Q, Q + 1);
-  } else if (tid == NG + 2 * Q) {
-    mv = gsum(Q + 2, Q + 1);
-  } else if (tid == NG + 2 * Q + 1) {
-    for (int q = 0; q < Q; ++q) mv += gsum(q, Q + 2);
-  } else if (tid == NG + 2 * Q + 2) {
-    mv = gsum(Q + 3, Q + 2);
-  } else if (tid == NG + 2 * Q + 3) {
-    mv = gsum(Q + 2, Q + 2);
-  }
-  static_assert(NACC <= 256, "one thread per moment");
-  __syncthreads();  // md may alias the ring
-  if (tid < NACC) {
-    md[tid] = mv;
-    if (gout) gout[tid] = mv;
-  }
-  for (int i = tid; i < Pseg * NS; i += nthr) {
-    const double* row = dyn + i * R;  // unpadded [Pseg * NS][R] table (MFMA A/B kernels)
-    double t = 0.0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) t += row[r];
-    md[NACC + i] = t;
-    if (gout) gout[NACC + i] = t;
-  }
-  __syncthreads();
-}
-
-template <int Q, int VAR, int R, typename T>
-__global__ __launch_bounds__(256) void xs_moments_mf_kernel(
-    const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
-    const int16_t* __restrict__ ind, int N, int Pseg, int S, int C, double* __restrict__ mom) {
-  __shared__ __attribute__((aligned(16))) char ring[RingMF<Q, T>::BYTES];
-  extern __shared__ double dyn[];
-  const int b = blockIdx.x, d = b / S, sc = b - d * S;
-  const int nb = sc * C, ne = min(N, nb + C);
-  moments_body_mf<Q, VAR, R, T>(X, cap, ret, ind, N, Pseg, d, ring, dyn,
-                                mom + (size_t)b * Layout<Q, T>::msize(Pseg), nb, ne);
-}
-
-// High-occupancy fused kernel: MFMA moments (few VGPRs, small padded ring) -> wave-0 solve
-// -> residual pass with UU iterations in flight; 3-4 workgroups per CU.
-template <int Q, typename T>
-constexpr int fused_mf_ring_bytes() {
-  constexpr int a = RingMF<Q, T>::BYTES;
-  constexpr int b = (int)(solve_lds_doubles<Q>(128) * 8);
-  return a > b ? a : b;
-}
-
-template <int Q, int R, int VAR, typename T, int WPE>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void xs_fused_mf_kernel(
-    const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
-    const int16_t* __restrict__ ind, int N, int P, int Pseg, int pivot_mode, double tol,
-    double* __restrict__ fout, T* __restrict__ eout, double* __restrict__ r2out,
-    double* __restrict__ stats, int* __restrict__ status, double* __restrict__ mom_out) {
-  __shared__ __attribute__((aligned(16))) char ring[fused_mf_ring_bytes<Q, T>()];
-  __shared__ double cf_s[Q + 1 + 128];
-  __shared__ double red[4][5];
-  __shared__ int st_s;
-  extern __shared__ double dyn[];
-  const int d = blockIdx.x;
-  double* sm = (double*)ring;
-  moments_body_mf<Q, VAR & 35, R, T>(X, cap, ret, ind, N, Pseg, d, ring, dyn, sm, 0, -1,
-                                     mom_out ? mom_out + (size_t)d * Layout<Q, T>::msize(Pseg)
-                                             : nullptr);
-  if constexpr ((VAR & 8) != 0) {  // timing-only ablation: no solve
-    for (int i = threadIdx.x; i < Q + 1 + P; i += blockDim.x) cf_s[i] = sm[i] * 1e-30;
-    if (threadIdx.x == 0) st_s = 0;
-  } else if (threadIdx.x < 64) {
-    solve_body<Q, true>(sm, d, P, Pseg, pivot_mode, tol, fout, cf_s, stats, status, &st_s);
-  }
-  __syncthreads();
-  constexpr int UR = sizeof(T) == 4 ? 2 : 1;
-  if constexpr ((VAR & 4) == 0)
-    resid_body<Q, T, false, UR>(X, cap, ret, ind, d, N, P, cf_s, (st_s & XS_BAD) != 0, eout,
-                                r2out, red);
-}
+#if MFA_AB
+#include "ab/xs_mfma_moments.h"
+#endif
 
 // ------------------------------------------------------------------------------------------
 // Fused K1 -> K2 -> K3: one 4-wave workgroup per date streams the date's panel slice once
@@ -1528,392 +1255,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Q <= 10 ? 2
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// Resident fused CS-WLS.  The fused kernel above re-reads the date's panel
-// slice for the residual pass: ~2.35 GB fetched per 2520-date fp64 step for 1.24 GB of panel,
-// because ~512 dates are in flight and the re-read misses every cache.  Here ONE 4-wave
-// workgroup per CU (waves_per_eu 1: 512 registers per lane, ~150 KB of LDS) streams its date
-// with plain loads (lane = stock, `A` tiles in flight per wave) and KEEPS the residual-pass inputs
-// of its first tiles on chip until the coefficients exist:
-//   * tiles 0 .. TL-1 of each wave in LDS ([r | x_q | industry-or--1] rows, written after the
-//     tile's moments),
-//   * tiles TL .. TL+TR-1 in AGPRs (v_accvgpr_write after the moments, v_accvgpr_read in the
-//     residual pass: 2Q + 3 registers per fp64 tile),
-// and only the tiles past TL + TR are re-read (validity from per-tile ballots in LDS, no cap
-// row); waves 1..3 issue their first re-read loads while wave 0 solves.  The moments use the
-// per-lane order and the wave-ordered reduction of the deterministic fused kernel (same tile
-// assignment: tile wid + 4 i of the date), so they are bitwise the same.
-// ------------------------------------------------------------------------------------------
-template <typename T> struct AgT;
-template <> struct AgT<double> {  // one fp64 value in an AGPR pair
-  int lo, hi;
-  __device__ __forceinline__ void put(double v) {
-    const long long b = __builtin_bit_cast(long long, v);
-    asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(lo) : "v"((int)b));
-    asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(hi) : "v"((int)(b >> 32)));
-  }
-  __device__ __forceinline__ double get() const {
-    int l, h;
-    asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(l) : "a"(lo));
-    asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(h) : "a"(hi));
-    return __builtin_bit_cast(double, ((long long)h << 32) | (long long)(unsigned)l);
-  }
-};
-template <> struct AgT<float> {
-  int v;
-  __device__ __forceinline__ void put(float f) {
-    asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(v) : "v"(__builtin_bit_cast(int, f)));
-  }
-  __device__ __forceinline__ float get() const {
-    int r;
-    asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(r) : "a"(v));
-    return __builtin_bit_cast(float, r);
-  }
-};
-struct AgI {
-  int v;
-  __device__ __forceinline__ void put(int x) { asm volatile("v_accvgpr_write_b32 %0, %1" : "=a"(v) : "v"(x)); }
-  __device__ __forceinline__ int get() const {
-    int r;
-    asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(r) : "a"(v));
-    return r;
-  }
-};
+#if MFA_AB
+#include "ab/xs_resident.h"
+#endif
 
-template <int Q, typename T>
-struct ResGeo {
-  using L = Layout<Q, T>;
-  static constexpr int R = 8;                                   // segment replicas (2 per wave)
-  static constexpr int TILE_B = (Q + 1) * kWT * (int)sizeof(T) + kWT * 4;  // one stored tile
-  static constexpr int RED = 8 * 65 + L::NACC;                  // wg_reduce tile + partial row
-  __host__ __device__ static constexpr int seg_region(int Pseg) {  // doubles, even
-    const int a = Pseg * L::seg_stride(R), b = 4 * RED;
-    return ((a > b ? a : b) + 1) & ~1;
-  }
-  __host__ __device__ static constexpr int okl_words(int N) { return (N + kWT - 1) / kWT; }
-  __host__ __device__ static constexpr size_t lds_bytes(int Pseg, int N, int TL) {
-    return ((size_t)seg_region(Pseg) + ((solve_lds_doubles<Q>(Pseg) + 1) & ~(size_t)1) +
-            okl_words(N)) * 8 + (size_t)4 * TL * TILE_B;
-  }
-};
-
-// VAR & 1 / & 2: timing-only ablations (no segment atomics / no style-Gram FMAs)
-template <int Q, int TL, int TR, int A, typename T, int VAR = 0>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void xs_resident_kernel(
-    const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
-    const int16_t* __restrict__ ind, int N, int P, int Pseg, int pivot_mode, double tol,
-    double* __restrict__ fout, T* __restrict__ eout, double* __restrict__ r2out,
-    double* __restrict__ stats, int* __restrict__ status, double* __restrict__ mom_out,
-    unsigned long long* __restrict__ tprof) {
-  using L = Layout<Q, T>;
-  using G = ResGeo<Q, T>;
-  constexpr int NS = L::NS, NG = L::NG, NACC = L::NACC, R = G::R;
-  constexpr int SJ = L::seg_stride(R);
-  constexpr int NRES = TL + TR;
-  constexpr int NB = A + 1;  // tile buffers: A in flight + the one being consumed
-  extern __shared__ double dyn[];
-  __shared__ double cf_s[Q + 1 + 128];
-  __shared__ double red5[4][5];
-  __shared__ int st_s;
-  const int d = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int MS = L::msize(Pseg);
-  // phase timestamps (tools/xs_resident_phases.py): start, moments, reduction, solve, end
-  auto stamp = [&](int k) {
-    if (tprof && tid == 0) tprof[(size_t)d * 6 + k] = wall_clock64();
-  };
-  stamp(0);
-  double* seg = dyn;                                   // segment table, then wg_reduce scratch
-  double* sm = dyn + G::seg_region(Pseg);              // moments (md) + solve scratch
-  unsigned long long* okl =
-      (unsigned long long*)(sm + ((solve_lds_doubles<Q>(Pseg) + 1) & ~(size_t)1));
-  char* store = (char*)(okl + G::okl_words(N));        // [4 waves][TL tiles][TILE_B]
-  for (int i = tid; i < Pseg * SJ; i += 256) seg[i] = 0.0;
-  __syncthreads();
-
-  const T* Xd = X + (size_t)d * Q * N;
-  const T* cd = cap + (size_t)d * N;
-  const T* rd = ret + (size_t)d * N;
-  const int16_t* id = ind ? ind + (size_t)d * N : nullptr;
-  const int ntile_all = (N + kWT - 1) / kWT;
-  const int ntile = ntile_all > wid ? (ntile_all - wid + 3) >> 2 : 0;  // tiles wid + 4 i
-  const unsigned seg_a = lds_addr(seg + wid * (R / 4) + (lane & (R / 4 - 1)));
-
-  struct Tile {
-    T c, r, x[Q];
-    int j;
-  };
-  Tile buf[NB];
-  // WITHC: the moments pass (cap row too); NT: non-temporal (the tile is never re-read)
-  auto ldt = [&](int i, Tile& t, bool withc, bool nt) {
-    const int s = (wid + 4 * i) * kWT + lane;
-    const bool in = s < N;
-    auto ld = [&](const T* p) -> T {
-      return in ? (nt ? __builtin_nontemporal_load(p + s) : p[s]) : T(0);
-    };
-    if (withc) t.c = ld(cd);
-    t.r = ld(rd);
-#pragma unroll
-    for (int q = 0; q < Q; ++q) t.x[q] = ld(Xd + (size_t)q * N);
-    t.j = (in && id) ? (int)id[s] : 0;
-  };
-
-  double v[NACC];
-#pragma unroll
-  for (int i = 0; i < NACC; ++i) v[i] = 0.0;
-  // moments of one tile (lane = stock); returns the industry of a valid stock, else -1
-  auto consume = [&](int i, const Tile& t, bool keep_bits) -> int {
-    const int s = (wid + 4 * i) * kWT + lane;
-    const int j = t.j;
-    bool ok = (s < N) && (j >= 0) && (j < Pseg) && finite_v(t.c) && (t.c >= T(0)) && finite_v(t.r);
-#pragma unroll
-    for (int q = 0; q < Q; ++q) ok = ok && finite_v(t.x[q]);
-    if (keep_bits) {
-      const unsigned long long m = __ballot(ok);
-      if (lane == 0) okl[wid + 4 * i] = m;
-    }
-    if (ok) {
-      const double c = t.c, r = t.r, w = sqrt(c);
-      double x[Q], wx[Q];
-#pragma unroll
-      for (int q = 0; q < Q; ++q) { x[q] = t.x[q]; wx[q] = w * x[q]; }
-      if constexpr ((VAR & 2) != 0) {
-#pragma unroll
-        for (int q = 0; q < Q; ++q) asm volatile("" ::"v"(wx[q]));
-      } else {
-#pragma unroll
-        for (int q = 0; q < Q; ++q)
-#pragma unroll
-          for (int u = 0; u <= q; ++u) v[q * (q + 1) / 2 + u] = fma(wx[q], x[u], v[q * (q + 1) / 2 + u]);
-      }
-      double sx = 0.0, sxx = 0.0;
-#pragma unroll
-      for (int q = 0; q < Q; ++q) {
-        v[NG + q] = fma(wx[q], r, v[NG + q]);
-        v[NG + Q + q] = fma(c, x[q], v[NG + Q + q]);
-        sx += x[q];
-        sxx = fma(x[q], x[q], sxx);
-      }
-      v[NG + 2 * Q + 0] += c;
-      v[NG + 2 * Q + 1] += sx;
-      v[NG + 2 * Q + 2] += sxx;
-      v[NG + 2 * Q + 3] += 1.0;
-      const unsigned a = seg_a + (unsigned)(j * SJ * 8);
-      const double wr = w * r;
-      if constexpr ((VAR & 1) != 0) {
-        asm volatile("" ::"v"(w), "v"(wr));
-      } else {
-        lds_add_nowait<0>(a, w);
-        [&]<int... I>(std::integer_sequence<int, I...>) {
-          (lds_add_nowait<8 * R * (1 + I)>(a, wx[I]), ...);
-        }(std::make_integer_sequence<int, Q>{});
-        lds_add_nowait<8 * R * (Q + 1)>(a, wr);
-        lds_add_nowait<8 * R * (Q + 2)>(a, c);
-      }
-    }
-    return ok ? j : -1;
-  };
-
-  AgT<T> kr[TR > 0 ? TR : 1], kx[TR > 0 ? TR : 1][Q];
-  AgI kj[TR > 0 ? TR : 1];
-  auto tile_lds = [&](int i) { return store + (size_t)(wid * TL + i) * G::TILE_B; };
-
-  // ---- moments pass: resident tiles (unrolled: compile-time buffer / AGPR indices) ----
-#pragma unroll
-  for (int i = 0; i < A; ++i)
-    if (i < ntile) ldt(i, buf[i], true, i < NRES);
-#pragma unroll
-  for (int i = 0; i < NRES; ++i) {
-    if (i < ntile) {
-      __builtin_amdgcn_sched_barrier(0);
-      if (i + A < ntile) ldt(i + A, buf[(i + A) % NB], true, i + A < NRES);
-      __builtin_amdgcn_sched_barrier(0);
-      const Tile& t = buf[i % NB];
-      const int jj = consume(i, t, false);
-      if (i < TL) {
-        char* b = tile_lds(i);
-        ((T*)b)[lane] = t.r;
-#pragma unroll
-        for (int q = 0; q < Q; ++q) ((T*)(b + (1 + q) * kWT * sizeof(T)))[lane] = t.x[q];
-        ((int*)(b + (Q + 1) * kWT * sizeof(T)))[lane] = jj;
-      } else if constexpr (TR > 0) {
-        const int k = i - TL < TR ? i - TL : 0;  // always i - TL here
-        kr[k].put(t.r);
-#pragma unroll
-        for (int q = 0; q < Q; ++q) kx[k][q].put(t.x[q]);
-        kj[k].put(jj);
-      }
-    }
-  }
-  // ---- moments pass: tiles past the resident ones (re-read later), NB tiles per trip ----
-  for (int i0 = NRES; i0 < ntile; i0 += NB) {
-#pragma unroll
-    for (int u = 0; u < NB; ++u) {
-      const int i = i0 + u;
-      if (i < ntile) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (i + A < ntile) ldt(i + A, buf[(NRES + u + A) % NB], true, false);
-        __builtin_amdgcn_sched_barrier(0);
-        consume(i, buf[(NRES + u) % NB], true);
-      }
-    }
-  }
-  __syncthreads();
-  stamp(1);
-  // ---- deterministic reduction (as the DET fused kernel) ----
-  for (int i = tid; i < Pseg * NS; i += 256) {
-    const double* row = seg + (i / NS) * SJ + (i % NS) * R;
-    double t = 0.0;
-#pragma unroll
-    for (int r = 0; r < R; ++r) t += row[r];
-    sm[NACC + i] = t;
-    if (mom_out) aux_store(mom_out + (size_t)d * MS + NACC + i, t);
-  }
-  __syncthreads();
-  double* wred = seg + wid * G::RED;  // the segment table is consumed: reuse it
-  wg_reduce<NACC, true>(v, wred, wred + 8 * 65);
-  __syncthreads();
-  if (tid < NACC) {
-    double t = 0.0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) t += seg[w * G::RED + 8 * 65 + tid];
-    sm[tid] = t;
-    if (mom_out) aux_store(mom_out + (size_t)d * MS + tid, t);
-  }
-  __syncthreads();
-  stamp(2);
-
-  // ---- solve (wave 0) while waves 1..3 start their re-read loads ----
-  auto reread = [&](int i, Tile& t) { ldt(i, t, false, true); };
-  auto prologue = [&]() {
-#pragma unroll
-    for (int k = 0; k < A; ++k)
-      if (NRES + k < ntile) reread(NRES + k, buf[(NRES + k) % NB]);
-  };
-  // row-per-lane Cholesky (ROWL): the in-register triangle would need more VGPRs than the
-  // AGPR-resident tiles leave (it spilled the whole kernel to scratch)
-  if (wid == 0) solve_body<Q, true>(sm, d, P, Pseg, pivot_mode, tol, fout, cf_s, stats, status, &st_s);
-  else prologue();
-  __syncthreads();
-  stamp(3);
-  if (wid == 0) prologue();
-
-  // ---- residual pass: specific returns + R^2 sums ----
-  double beta[Q];
-#pragma unroll
-  for (int q = 0; q < Q; ++q) beta[q] = cf_s[q];
-  const double cst = cf_s[Q];
-  const double* fI = cf_s + Q + 1;
-  T* ed = eout ? eout + (size_t)d * N : nullptr;
-  double se = 0.0, see = 0.0, sr = 0.0, srr = 0.0, nn = 0.0;
-  auto res1 = [&](int i, T rf, const T (&xf)[Q], int jj) {
-    const int s = (wid + 4 * i) * kWT + lane;
-    double e = (double)rf - cst;
-#pragma unroll
-    for (int q = 0; q < Q; ++q) e = fma(-beta[q], (double)xf[q], e);
-    T eo = (T)qnan();
-    if (jj >= 0) {
-      if (P > 0) e -= fI[jj];
-      se += e;
-      see = fma(e, e, see);
-      sr += (double)rf;
-      srr = fma((double)rf, (double)rf, srr);
-      nn += 1.0;
-      eo = (T)e;
-    }
-    if (ed && s < N) {
-      if constexpr (MFA_XS_NT_E) __builtin_nontemporal_store(eo, ed + s);
-      else ed[s] = eo;
-    }
-  };
-#pragma unroll
-  for (int i = 0; i < NRES; ++i) {
-    __builtin_amdgcn_sched_barrier(0);
-    if (i < ntile) {
-      T rf, xf[Q];
-      int jj;
-      if (i < TL) {
-        const char* b = tile_lds(i);
-        rf = ((const T*)b)[lane];
-#pragma unroll
-        for (int q = 0; q < Q; ++q) xf[q] = ((const T*)(b + (1 + q) * kWT * sizeof(T)))[lane];
-        jj = ((const int*)(b + (Q + 1) * kWT * sizeof(T)))[lane];
-      } else {
-        const int k = i - TL < TR ? i - TL : 0;
-        rf = kr[k].get();
-#pragma unroll
-        for (int q = 0; q < Q; ++q) xf[q] = kx[k][q].get();
-        jj = kj[k].get();
-      }
-      res1(i, rf, xf, jj);
-    }
-  }
-  for (int i0 = NRES; i0 < ntile; i0 += NB) {
-#pragma unroll
-    for (int u = 0; u < NB; ++u) {
-      const int i = i0 + u;
-      if (i < ntile) {
-        __builtin_amdgcn_sched_barrier(0);
-        if (i + A < ntile) reread(i + A, buf[(NRES + u + A) % NB]);
-        __builtin_amdgcn_sched_barrier(0);
-        const Tile& t = buf[(NRES + u) % NB];
-        const bool ok = (okl[wid + 4 * i] >> lane) & 1ull;
-        res1(i, t.r, t.x, ok ? t.j : -1);
-      }
-    }
-  }
-  se = wave_sum(se); see = wave_sum(see); sr = wave_sum(sr); srr = wave_sum(srr); nn = wave_sum(nn);
-  if (lane == 0) {
-    red5[wid][0] = se; red5[wid][1] = see; red5[wid][2] = sr; red5[wid][3] = srr; red5[wid][4] = nn;
-  }
-  __syncthreads();
-  if (tid == 0) {
-    double a = 0, b = 0, c = 0, e2 = 0, n = 0;
-    for (int w = 0; w < 4; ++w) {
-      a += red5[w][0]; b += red5[w][1]; c += red5[w][2]; e2 += red5[w][3]; n += red5[w][4];
-    }
-    const double ve = b / n - (a / n) * (a / n);
-    const double vr = e2 / n - (c / n) * (c / n);
-    r2out[d] = (st_s & XS_BAD) ? qnan() : 1.0 - ve / vr;
-  }
-  stamp(4);
-  if (tprof && tid == 0) tprof[(size_t)d * 6 + 5] = __smid();
-}
-
-// ------------------------------------------------------------------------------------------
-// Pipelined team CS-WLS (persistent grid, deferred residuals): C stock chunks per date, each
-// chunk's moments and residuals done by the same workgroup, dates solved by their team's last
-// arriver, and no workgroup ever idles while its team catches up.
-//
-// The fused kernel's residual pass re-reads the date's panel slice: one workgroup streams a
-// whole 490 KB fp64 date in ~35 us, ~512 dates are in flight, so ~250 MB of other dates pass
-// through the 256 MB Infinity Cache between a line's first read and its re-read and most
-// re-reads go to HBM (2.46 GB moved per 1.34 GB compulsory, profiles/r02_xs_cluster_ab.md).  A
-// one-wave-per-date team that WAITS for its partners (round-3 first try, r03_team_ab.md) pays
-// the wait and a redundant solve per member on the 2 workgroup slots of a CU and lost 25-260 %.
-// Here a persistent workgroup loops over tickets:
-//   1. take a ticket t of its group (blockIdx & 7: the blocks of one XCD), t -> chunk c = t % C
-//      of date d = group + 8 (t / C); stream the chunk once (LDS-DMA ring) into raw moments;
-//   2. publish the partial row (write-through sc1 stores), arrive on the date's counter; the
-//      LAST arriver sums the C partials in chunk order (bitwise-deterministic), solves in wave 0
-//      and publishes the residual coefficients + a ready flag carrying the status word;
-//   3. `lag` tickets later (the chunk's date has been solved by then), the same workgroup
-//      re-reads ITS chunk for the residual pass: ~10-20 us after the first read instead of
-//      ~40, so the re-read is an Infinity-Cache hit; partial R^2 sums are combined in chunk
-//      order by the last member to finish.
-// Progress (no co-residency assumption): tickets are taken in order by running workgroups, and a
-// workgroup always finishes step 2 of a ticket it took before it waits on anything, so every
-// fully ticketed date gets solved.  A workgroup waits (step 3) only for a date whose ticket it
-// took `lag` or more tickets ago; if that date is not fully ticketed, every ticket taken since
-// belongs to it, so a waiting workgroup holds lag + 1 of its C tickets: with lag >= 1 and
-// C <= 16, all resident workgroups of a group can be waiting at once only if fewer than
-// (C - 1) / (lag + 1) + 1 <= 8 of them are resident.  Every poll is bounded anyway
-// (XS_COOP_TIMEOUT status bit): the grid always drains.
-// Hand-offs (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the sc1 table):
-// payloads stored sc1, every storing wave waits vmcnt(0), a workgroup barrier, then ONE lane
-// adds / stores the counter or flag; readers poll with sc1 loads from one lane, barrier, and
-// load the payload with sc1 loads.
-// sync = [tickets 8 | arrive[D] | done[D] | ready[D]] ints, zeroed before every launch.
-// ------------------------------------------------------------------------------------------
 constexpr int XS_COOP_TIMEOUT = 64;  // status bit: a team wait gave up (results invalid)
 constexpr int kCoopSpin = 1 << 21;   // poll iterations (s_sleep 4 each, ~0.2 s) before giving up
 constexpr int kCoopMaxC = 16;        // chunks per date at most
@@ -1921,149 +1266,9 @@ constexpr int kPipeGroups = 8;       // ticket groups: blockIdx & 7 (the blocks 
 constexpr int kPipeMaxLag = 3;       // residual pass at most 3 tickets behind the moments
 constexpr int kReadyBit = 1 << 30;   // ready flag = status | kReadyBit
 
-__device__ __forceinline__ double ld_sc1(const double* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(double* p, double v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int Q, int R, int VAR, typename T>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(Q <= 10 ? 2 : MFA_XS_WPE_BIGQ, Q <= 10 ? 2 : MFA_XS_WPE_BIGQ))) void xs_pipe_kernel(
-    const T* __restrict__ X, const T* __restrict__ cap, const T* __restrict__ ret,
-    const int16_t* __restrict__ ind, int D, int N, int P, int Pseg, int C, int Cs, int lag,
-    int pivot_mode, double tol, double* __restrict__ fout, T* __restrict__ eout,
-    double* __restrict__ r2out, double* __restrict__ stats, int* __restrict__ status,
-    double* __restrict__ mom, double* __restrict__ coef, double* __restrict__ sums,
-    unsigned long long* __restrict__ okm, int* __restrict__ sync) {
-  __shared__ __attribute__((aligned(16))) char ring[fused_ring_bytes<Q, T>()];
-  __shared__ double cf_s[Q + 1 + 128];
-  __shared__ double red[4][5];
-  __shared__ double rs[5];
-  __shared__ int tk_s, last_s, st_s, flag_s;
-  extern __shared__ double dyn[];
-  const int tid = threadIdx.x;
-  const int grp = (int)blockIdx.x & (kPipeGroups - 1);
-  const int ndg = D > grp ? (D - grp + kPipeGroups - 1) / kPipeGroups : 0;
-  const int ntk = ndg * C;  // this group's tickets
-  const int MS = Layout<Q, T>::msize(Pseg);
-  const int NT = (N + kWT - 1) / kWT;
-  const int KC = Q + 1 + P;
-  int* tick = sync;
-  int* arrive = sync + kPipeGroups;
-  int* done = arrive + D;
-  int* ready = done + D;
-  double* sm = (double*)ring;  // the chunk's moments, then the solve's scratch
-  int pend[kPipeMaxLag + 1];   // tickets whose residual pass is pending (oldest first)
-  int np = 0;
-  bool more = true;
-  for (;;) {
-    int t = ntk;
-    if (more) {
-      __syncthreads();  // tk_s of the previous iteration has been read by every thread
-      if (tid == 0) tk_s = __hip_atomic_fetch_add(tick + grp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __syncthreads();
-      t = tk_s;
-      more = t < ntk;
-    }
-    if (t < ntk) {
-      // ---- 1 + 2: moments of the chunk, publish, arrive; the last arriver solves the date ----
-      const int k = t / C, c = t - k * C, d = grp + kPipeGroups * k;
-      const int nb = c * Cs, ne = min(N, nb + Cs);
-      moments_body<Q, VAR & 35, R, T>(X, cap, ret, ind, N, Pseg, d, ring, dyn, sm, nb, ne, nullptr,
-                                      okm + (size_t)d * NT);
-      double* mp = mom + ((size_t)d * C + c) * MS;
-      for (int i = tid; i < MS; i += blockDim.x) st_sc1(mp + i, sm[i]);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0)
-        last_s = __hip_atomic_fetch_add(arrive + d, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == C - 1;
-      __syncthreads();
-      if (last_s) {
-        // the date's moments: the C partials summed in chunk order (all loads of a thread are
-        // issued before its first add: a load -> add chain pays the round trip C times)
-        const double* md = mom + (size_t)d * C * MS;
-        for (int i = tid; i < MS; i += blockDim.x) {
-          double v[kCoopMaxC];
-#pragma unroll
-          for (int kk = 0; kk < kCoopMaxC; ++kk) v[kk] = kk < C ? ld_sc1(md + (size_t)kk * MS + i) : 0.0;
-          double s = v[0];
-#pragma unroll
-          for (int kk = 1; kk < kCoopMaxC; ++kk)
-            if (kk < C) s += v[kk];
-          sm[i] = s;
-        }
-        __syncthreads();
-        if (tid < 64) solve_body<Q>(sm, d, P, Pseg, pivot_mode, tol, fout, cf_s, stats, status, &st_s);
-        __syncthreads();
-        double* co = coef + (size_t)d * KC;
-        for (int i = tid; i < KC; i += blockDim.x) st_sc1(co + i, cf_s[i]);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (tid == 0) __hip_atomic_store(ready + d, st_s | kReadyBit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-#pragma unroll
-      for (int i = 0; i <= kPipeMaxLag; ++i)
-        if (i == np) pend[i] = t;
-      ++np;
-    }
-    if (np > 0 && (np > lag || !more)) {
-      // ---- 3: residual pass of the oldest pending chunk ----
-      const int t2 = pend[0];
-#pragma unroll
-      for (int i = 0; i < kPipeMaxLag; ++i) pend[i] = pend[i + 1];
-      --np;
-      const int k2 = t2 / C, c2 = t2 - k2 * C, d2 = grp + kPipeGroups * k2;
-      const int nb2 = c2 * Cs, ne2 = min(N, nb2 + Cs);
-      if (tid == 0) {
-        int v = 0;
-        for (int it = 0; it < kCoopSpin; ++it) {
-          v = __hip_atomic_load(ready + d2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (v) break;
-          __builtin_amdgcn_s_sleep(4);
-        }
-        flag_s = v ? v : (kReadyBit | XS_COOP_TIMEOUT);
-      }
-      __syncthreads();
-      const int st2 = flag_s & ~kReadyBit;
-      const double* co2 = coef + (size_t)d2 * KC;
-      for (int i = tid; i < KC; i += blockDim.x) cf_s[i] = ld_sc1(co2 + i);
-      __syncthreads();
-      const bool bad = (st2 & (XS_BAD | XS_COOP_TIMEOUT)) != 0;
-      resid_body<Q, T>(X, cap, ret, ind, d2, N, P, cf_s, bad, eout, nullptr, red, ResidPre<Q, T>{}, rs,
-                       nb2, ne2, okm + (size_t)d2 * NT);
-      // R^2: the last member of the team to finish combines the C chunk sums in chunk order
-      if (tid < 64) {
-        double* sd = sums + (size_t)d2 * C * 5;
-        int lastd = 0;
-        if (tid == 0) {
-#pragma unroll
-          for (int j = 0; j < 5; ++j) st_sc1(sd + c2 * 5 + j, rs[j]);
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          lastd = __hip_atomic_fetch_add(done + d2, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == C - 1;
-          if ((st2 & XS_COOP_TIMEOUT) != 0) atomicOr(status + d2, XS_COOP_TIMEOUT);
-        }
-        if (__builtin_amdgcn_readfirstlane(lastd)) {
-          double v[5];
-#pragma unroll
-          for (int j = 0; j < 5; ++j) v[j] = tid < C ? ld_sc1(sd + tid * 5 + j) : 0.0;
-          double a[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-          for (int kk = 0; kk < C; ++kk)  // chunk order, wave-uniform
-#pragma unroll
-            for (int j = 0; j < 5; ++j) a[j] += readlane(v[j], kk);
-          if (tid == 0) {
-            const double n = a[4];
-            const double ve = a[1] / n - (a[0] / n) * (a[0] / n);
-            const double vr = a[3] / n - (a[2] / n) * (a[2] / n);
-            r2out[d2] = bad ? qnan() : 1.0 - ve / vr;
-          }
-        }
-      }
-    } else if (!more) {
-      break;
-    }
-  }
-}
+#if MFA_AB
+#include "ab/xs_team.h"
+#endif
 
 // ------------------------------------------------------------------------------------------
 // Device pseudo-inverse refinement (pinv semantics of CrossSection.py:76,98) for dates the
@@ -2708,19 +1913,9 @@ inline bool xs_plain_moments(int D) {
   return sizeof(T) == 4 || D <= kXsPlainMaxD64;
 }
 
-// Resident fused kernel (xs_resident_kernel): instantiated for the headline fp64 Q = 10 panel;
-// mode 30 forces it, mode 31 forces the LDS-DMA fused kernel, mode 0 picks it for
-// deterministic fp64 steps past kXsPlainMaxD64 dates.  Returns its dynamic LDS bytes, 0 = not used.
-constexpr int kResQ = 10, kResTL = 5, kResTR = 10, kResA = 2;
-template <int Q, typename T>
-inline size_t xs_resident_lds(int mode, bool det, int D, int N, int P) {
-  if (Q != kResQ || sizeof(T) != 8 || !det || P > 128) return 0;
-  const bool ab = mode >= 32 && mode <= 38;  // A/B geometries and timing ablations
-  if (!(mode == 30 || ab || (mode == 0 && MFA_XS_RESIDENT_DEFAULT && !xs_plain_moments<T>(D))))
-    return 0;
-  const size_t b = ResGeo<Q, T>::lds_bytes(P > 0 ? P : 1, N, mode == 34 ? 0 : kResTL);
-  return b + (Q + 1 + 128) * 8 + 4 * 5 * 8 + 16 <= 160 * 1024 ? b : 0;
-}
+#if MFA_AB
+#include "ab/xs_resident_lds.h"
+#endif
 
 template <int Q, int VAR, typename T>
 hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, int D, int N,
