@@ -107,6 +107,24 @@ bool launch_bias_tri_ab(const double* D0, int D, int K, int M, const double* Cz,
                          bias_tri2_lds(K, 44), s, D0, K, M, Cz, dvalid, ws, nullptr, nullptr, D, 0);
     return true;
   }
+  if (g_bias_mode > 70 && g_bias_mode < 78 && K > 32 && K <= 42) {
+    // round 6: phase ablations of the PRODUCTION K = 42 instantiation (KP = 42, 2-step groups,
+    // KP-entry tables, 4 waves / SIMD) for the per-phase instruction budget
+    // (tools/bias_phase_budget.py): 71 = no Laguerre iterations, 72 = no eigenvectors /
+    // back-transform, 74 = no tridiagonalisation, 73 / 75 / 76 / 77 their unions; outputs
+    // meaningless
+    const int abl = g_bias_mode - 70;
+#define MFA_TRI2_ABL42(A_)                                                                   \
+    if (abl == A_)                                                                         \
+      hipLaunchKernelGGL((mc_bias_tri2_kernel<42, true, A_, 4, false, 8, 8, 2, true, false, true, \
+                                              false, false, 1, kTri2GS, true>),             \
+                         dim3(D * M), dim3(64), bias_tri2_lds(K, 42, kTri2GS, true), s, D0, K, M, \
+                         Cz, dvalid, ws, nullptr, nullptr, D, 0);
+    MFA_TRI2_ABL42(1) MFA_TRI2_ABL42(2) MFA_TRI2_ABL42(3) MFA_TRI2_ABL42(4) MFA_TRI2_ABL42(5)
+    MFA_TRI2_ABL42(6) MFA_TRI2_ABL42(7)
+#undef MFA_TRI2_ABL42
+    return true;
+  }
   if (g_bias_mode > 60 && g_bias_mode < 69 && K <= 44) {  // timing-only ablations of mode 5
     const int abl = g_bias_mode == 68 ? 32 : g_bias_mode - 60;  // 68: Sturm-evaluation counts
 #define MFA_TRI2_ABL(A_)                                                                     \

@@ -1483,7 +1483,8 @@ int g_bias_mode = 5;   // 21 = mode 5 walking 8 consecutive dates per wave with 
                        // padded eigenvector phase + skipped no-op Householder steps, one date per
                        // wave; 0 = packed (A, M) Jacobi.  A/B builds: 1 / 2 = split
                        // Jacobi, 3 = round-2 tridiagonal, 4 = lean layout, 14 = mode 5 unpadded,
-                       // 22 / 23 = chains of 4 / 16 dates, 41-67 ablations.
+                       // 22 / 23 = chains of 4 / 16 dates, 41-67 ablations, 71-77 phase
+                       // ablations of the production K = 42 instantiation.
 
 #if MFA_AB
 size_t eigh_lds(int K) { return ((size_t)2 * K * (K + 1) + 4 * 64 + 64) * sizeof(double) + 64 * sizeof(int); }

@@ -2043,7 +2043,7 @@ hipError_t launch_q(const T* X, const T* cap, const T* ret, const int16_t* ind, 
       hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR | 32, true, T>), dim3(D), dim3(256),
                          lds1, s, X, cap, ret, indp, N, P, Pseg, pm, tol, f, e, r2, stats, status,
                          mom, okm);
-  } else if ((mode == 20 || mode == 21 || (mode == 0 && xs_plain_moments<T>(D))) && det) {
+  } else if ((mode == 20 || mode == 21) && det) {  // mode 0 takes the production branch below
     // moments from plain vector loads (default for fp32 panels and small fp64 shards)
     if (mode == 21)  // two tiles in flight
       hipLaunchKernelGGL((xs_fused_kernel<Q, kRepMax, VAR | 32 | 64 | 128, PRE, T>), dim3(D),

@@ -12,23 +12,26 @@ from llm_driven_multi_factor_model_amd.ops import rolling as RL
 
 pytestmark = pytest.mark.gpu
 
-# measured on 1x MI355X (ROCm 7.2), rounds 3-4 (profiles/r03_risk/, r04/):
+# measured on 1x MI355X (ROCm 7.2), round 6 (profiles/r06/):
 MEASURED = {
     # bench.py: fp64 storage, refine on, deterministic, graph replay: 0.384 ms / 2520 dates
     "xs_wls_fp64_reg_per_s": 6.55e6,
-    # eigen_risk_adjust at 2520 dates x M = 100: tridiagonal eigh of F0 + bias solver mode 5
-    # + finalize (draw covariances given); round 4 after the padded eigenvector phase
-    # (profiles/r04/r04ze/perf_guards.log)
-    "eigen_adjust_2520x100_ms": 12.42,
+    # eigen_risk_adjust at 2520 dates x M = 100: tridiagonal eigh of F0 + bias solver (lean
+    # 2-step / KP-table form) + finalize (draw covariances given)
+    "eigen_adjust_2520x100_ms": 8.31,
+    # RiskModel.run, 5000 x 2520, K = 42, M = 100: the canonical median of tools/risk_timing.py
+    # (3 panel seeds x 5 runs; profiles/r06/risk_stages_canonical.log)
+    "risk_model_run_2520_ms": 10.45,
     # Newey-West expanding series, T = 2520, K = 42, q = 2
     "newey_west_2520_ms": 0.100,
-    # window-descriptor kernels, 5000 x 3780, round 4 (profiles/r04/rolling_ab.jsonl, r04q/): BETA/
-    # HSIGMA and DASTD sanitised-row sliding kernel with count-implied weight sums, CMRA two-rows-
-    # per-lane van Herk, RSTR backward-anchored sums with tile-absolute prefixes
-    "beta_hsigma_5000x3780_ms": 0.141,
-    "dastd_5000x3780_ms": 0.095,
-    "cmra_5000x3780_ms": 0.089,
-    "rstr_5000x3780_ms": 0.089,
+    # window-descriptor kernels, 5000 x 3780, round 6: the segment-anchored (rank-invariant)
+    # kernels on one SegLayout -- BETA/HSIGMA and DASTD EW prefixes anchored one 256-row segment
+    # back, CMRA / RSTR / the three turnover sums on 64-row segments with fold tables
+    "beta_hsigma_5000x3780_ms": 0.190,
+    "dastd_5000x3780_ms": 0.122,
+    "cmra_5000x3780_ms": 0.154,
+    "rstr_5000x3780_ms": 0.175,
+    "liquidity_5000x3780_ms": 0.25,
     # point-in-time trailing specific vol, 2520 x 5000, W = 252 (profiles/r03_risk/)
     "trailing_vol_2520x5000_ms": 1.075,
 }
