@@ -19,7 +19,8 @@ using namespace mfa;
 // What changes against the one-wave kernel is only where lanes meet: the Householder column
 // norm, u^T p and the Gershgorin / pivot bounds are block reductions (per-wave DPP totals, then
 // the NW partials in wave order: deterministic), the pivot row's entries are LDS broadcasts, and
-// every cross-wave LDS exchange is behind a barrier (4 per Householder step).  Replaces
+// every cross-wave LDS exchange is behind a barrier (2 per Householder step, each carrying one
+// reduction's partials and one broadcast vector; 4 until round 6).  Replaces
 // rocSOLVER's batched syevd (~27 us per 140 x 140 problem at the GPU's throughput) for the bias
 // statistic; eigenvalues, eigenvectors and back-transform are per lane as before.
 // Multisection rounds before the Laguerre loop: bits 4-6 of the kernels' `abl` argument
@@ -61,8 +62,9 @@ mc_bias_wide_kernel(const double* __restrict__ D0, int K, int M, const double* _
   }
   const int nrow = (tri2_rows_doubles<KP>(K) + 1) & ~1;
   double* R = sm;                          // packed reflector rows
-  double* wb = R + nrow;                   // [NW*64] broadcast w; Sturm counts later
-  double2* tb = (double2*)(wb + NW * 64);  // [KP] {alpha_i, beta_{i-1}^2}
+  double* wb = R + nrow;                   // [NW*64] broadcast p; Sturm counts later
+  double* xb = wb + NW * 64;               // [NW*64] broadcast column s
+  double2* tb = (double2*)(xb + NW * 64);  // [KP] {alpha_i, beta_{i-1}^2}
   double* be = (double*)(tb + KP);         // [KP] beta_i
   double* ta = be + KP;                    // [KP] tau_s
   double* dd = ta + KP;                    // [NW*64] sqrt(D0)
@@ -109,10 +111,15 @@ mc_bias_wide_kernel(const double* __restrict__ D0, int K, int M, const double* _
         }
       const bool act = t > s && t < K;
       const double x = act ? xs : 0.0;
+      xb[t] = x;
       if (t == s) bc[0] = xs;
-      if (t == s + 1) bc[1] = xs;
-      const double sig = block_total<NW>(t > s + 1 && t < K ? x * x : 0.0, red, t);  // barrier
-      const double alpha = bc[0], x0 = s + 1 < K ? bc[1] : 0.0;
+      const double v = wave_total(t > s + 1 && t < K ? x * x : 0.0);
+      if ((t & 63) == 0) red[t >> 6] = v;
+      __syncthreads();  // A: column s, alpha, the sigma partials
+      double sig = red[0];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) sig += red[w];
+      const double alpha = bc[0], x0 = s + 1 < K ? xb[s + 1] : 0.0;
       double u = 0.0, tau = 0.0, beta = x0;
       if (sig != 0.0) {
         const double n2 = fma(x0, x0, sig);
@@ -121,39 +128,51 @@ mc_bias_wide_kernel(const double* __restrict__ D0, int K, int M, const double* _
         tau = rcp_nr(nrm * (nrm + fabs(x0)));
         u = act ? (t == s + 1 ? x0 - beta : x) : 0.0;
       }
-      double* us = R + tri2_row_off<KP>(s) - J0;  // us[j], j in [J0, KP)
-      if (s + 2 < K && t >= J0 && t < KP) us[t] = u;
       if (t == 0) {
         tb[s] = double2{alpha, s > 0 ? be[s - 1] * be[s - 1] : 0.0};
         be[s] = beta;
         ta[s] = tau;
       }
-      __syncthreads();  // u_s complete (and bc / red[0] free again)
-      double p0 = 0.0, p1 = 0.0;
-      if (s + 2 >= K) us = R + tri2_row_off<KP>(J0) - J0;
+      if (s + 2 >= K) {  // no reflection (tau = 0)
+        __syncthreads();
+        continue;
+      }
+      double* us = R + tri2_row_off<KP>(s) - J0;  // us[j], j in [J0, KP)
+      if (t >= J0 && t < KP) us[t] = u;
+      double p0 = 0.0, p1 = 0.0;  // p = tau (A x - beta A[:, s+1]) = tau A u
 #pragma unroll
       for (int j = J0; j < KP; j += 2) {
-        const double2 uu = *(const double2*)(us + j);
-        p0 = fma(a[j], uu.x, p0);
-        p1 = fma(a[j + 1], uu.y, p1);
+        const double2 xx = *(const double2*)(xb + j);
+        p0 = fma(a[j], xx.x, p0);
+        p1 = fma(a[j + 1], xx.y, p1);
         if (((j - J0) & 7) == 6) lds_batch();
       }
-      const double p = act ? tau * (p0 + p1) : 0.0;
-      const double kk = 0.5 * tau * block_total<NW>(u * p, red + NW, t);  // barrier
-      const double w = p - kk * u;
-      wb[t] = w;
-      __syncthreads();  // w complete
+      double as1 = a[J0];  // column s + 1
+#pragma unroll
+      for (int k = 1; k < 9; ++k)
+        if (J0 + k < KP) {
+          double tt = a[J0 + k];
+          asm volatile("" : "+v"(tt));
+          as1 = s + 1 == J0 + k ? tt : as1;
+        }
+      const double p = act ? tau * fma(-beta, as1, p0 + p1) : 0.0;
+      const double v2 = wave_total(u * p);
+      if ((t & 63) == 0) red[NW + (t >> 6)] = v2;
+      wb[t] = p;
+      __syncthreads();  // B: p, the u^T p partials, the reflector row
+      double up = red[NW];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) up += red[NW + w];
+      const double kk = 0.5 * tau * up;
+      const double w2 = fma(-2.0 * kk, u, p);  // A -= u p^T + (p - 2 kk u) u^T
 #pragma unroll
       for (int j = J0; j < KP; j += 2) {
-        const double2 ww = *(const double2*)(wb + j), uu = *(const double2*)(us + j);
-        a[j] = fma(-u, ww.x, fma(-w, uu.x, a[j]));
-        a[j + 1] = fma(-u, ww.y, fma(-w, uu.y, a[j + 1]));
+        const double2 pp = *(const double2*)(wb + j), uu = *(const double2*)(us + j);
+        a[j] = fma(-u, pp.x, fma(-w2, uu.x, a[j]));
+        a[j + 1] = fma(-u, pp.y, fma(-w2, uu.y, a[j + 1]));
         if (((j - J0) & 7) == 6) lds_batch();
       }
-      // no barrier before the next step: its first LDS writes (bc, the partials of its first
-      // reduction) are to slots this step read before its second barrier, and the next writes
-      // of wb / the second partials come after the next step's own barriers, which no wave
-      // reaches before finishing this update
+      // no barrier after the update (mc_bias_wide2_kernel below has the hazard argument)
     }
   };
   if ((abl & 4) == 0) {
@@ -405,9 +424,10 @@ __global__ __launch_bounds__(NW * 64) void mc_bias_wide2_kernel(
     return;
   }
   const int nrow = (tri2_rows_doubles<KP>(K) + 1) & ~1;
-  double* R = sm;                          // packed reflector rows
-  double* wb = R + nrow;                   // [KP] broadcast w; Sturm counts later
-  double2* tb = (double2*)(wb + KP);       // [KP] {alpha_i, beta_{i-1}^2}
+  double* R = sm;                          // packed reflector rows (column-interleaved halves)
+  double* wb = R + nrow;                   // [KP] broadcast p (interleaved); Sturm counts later
+  double* xb = wb + KP;                    // [KP] broadcast column s (interleaved)
+  double2* tb = (double2*)(xb + KP);       // [KP] {alpha_i, beta_{i-1}^2}
   double* be = (double*)(tb + KP);         // [KP] beta_i
   double* ta = be + KP;                    // [KP] tau_s
   double* dd = ta + KP;                    // [KP] sqrt(D0)
@@ -425,7 +445,7 @@ __global__ __launch_bounds__(NW * 64) void mc_bias_wide2_kernel(
   __syncthreads();
 #pragma unroll
   for (int jj = 0; jj < HP; ++jj) {
-    const int j = h * HP + jj;
+    const int j = 2 * jj + h;  // phase 1: lane h holds the columns of parity h
     if constexpr (EIG)  // this lane's half of row i of the symmetrised input
       a[jj] = (j < K && row_ok) ? 0.5 * (Ain[li * K + j] + Ain[j * K + li]) : 0.0;
     else
@@ -447,26 +467,48 @@ __global__ __launch_bounds__(NW * 64) void mc_bias_wide2_kernel(
     __syncthreads();
   }
   // ---- 1. Householder tridiagonalisation ----
+  // Lane h holds the columns j = 2 jj + h of its row (register jj), so both lanes of a pair keep
+  // (KP - s) / 2 live columns at step s: the loops below run over registers [J0 / 2, HP) instead
+  // of a contiguous half that stays whole until s passes HP.  Vectors broadcast through the LDS
+  // (the column x, p, the reflector rows) are stored de-interleaved, entry j at
+  // (j & 1) * half + (j >> 1), so a lane reads its parity's entries as contiguous double2.
+  // Two barriers per step, each carrying a block reduction:
+  //   A: column s (x, rows > s) and the partials of sigma = |x_{s+2..}|^2;
+  //   B: p = tau A u and the partials of u^T p.
+  // u differs from x only at s + 1 (u_{s+1} = x_{s+1} - beta), so p = tau (A x - beta A[:, s+1])
+  // is formed from the broadcast x before u is published; the reflector row u (written after A)
+  // feeds the rank-2 update after B, in the form A -= u p^T + (p - 2 kk u) u^T
+  // (= u w^T + w u^T with w = p - kk u, kk = tau u^T p / 2: no per-element w).
+  // No barrier after the update: every LDS slot a step writes before its barrier A (x, alpha, the
+  // sigma partials) was last read before the previous step's barrier B, and the slots it writes
+  // between A and B (p, the u^T p partials, its reflector row) were last read after the previous
+  // B, which no wave leaves behind before reaching this A.
   auto steps = [&](auto J0c) {
     constexpr int J0 = decltype(J0c)::value;
-    constexpr int HS = J0 / HP;              // half holding columns J0 .. J0 + 7
-    constexpr int JL = J0 > HP ? J0 - HP : 0;  // first register of the static column range
+    constexpr int JH = J0 / 2;          // first register holding a column >= J0
+    constexpr int L2 = (KP - J0) / 2;   // half length of the packed reflector rows of group J0
     for (int s = J0; s < J0 + 8 && s < K; ++s) {
-      double xo = a[J0 - HS * HP];
+      double xo = a[JH];  // column 2 (s >> 1) + h
 #pragma unroll
-      for (int k = 1; k < 8; ++k) {
-        double tt = a[J0 - HS * HP + k];
+      for (int k = 1; k < 4; ++k) {
+        double tt = a[JH + k];
         asm volatile("" : "+v"(tt));
-        xo = s == J0 + k ? tt : xo;
+        xo = (s >> 1) == JH + k ? tt : xo;
       }
       const double xp = pair_swap(xo);
-      const double xs = h == HS ? xo : xp;   // column s of row i, on both lanes of the pair
+      const double xs = h == (s & 1) ? xo : xp;  // column s of row i, on both lanes of the pair
       const bool act = i > s && row_ok;
       const double x = act ? xs : 0.0;
+      if (lead) xb[(i & 1) * HP + (i >> 1)] = x;
       if (t == 2 * s) bc[0] = xs;
-      if (t == 2 * s + 2) bc[1] = xs;
-      const double sig = block_total<NW>(h == 0 && i > s + 1 && row_ok ? x * x : 0.0, red, t);
-      const double alpha = bc[0], x0 = s + 1 < K ? bc[1] : 0.0;
+      double v = wave_total(h == 0 && i > s + 1 && row_ok ? x * x : 0.0);
+      if ((t & 63) == 0) red[t >> 6] = v;
+      __syncthreads();  // A
+      double sig = red[0];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) sig += red[w];
+      const double alpha = bc[0];
+      const double x0 = s + 1 < K ? xb[((s + 1) & 1) * HP + ((s + 1) >> 1)] : 0.0;
       double u = 0.0, tau = 0.0, beta = x0;
       if (sig != 0.0) {
         const double n2 = fma(x0, x0, sig);
@@ -475,43 +517,57 @@ __global__ __launch_bounds__(NW * 64) void mc_bias_wide2_kernel(
         tau = rcp_nr(nrm * (nrm + fabs(x0)));
         u = act ? (i == s + 1 ? x0 - beta : x) : 0.0;
       }
-      double* us = R + tri2_row_off<KP>(s) - J0;  // us[j], j in [J0, KP)
-      if (s + 2 < K && lead && i >= J0) us[i] = u;
       if (t == 0) {
         tb[s] = double2{alpha, s > 0 ? be[s - 1] * be[s - 1] : 0.0};
         be[s] = beta;
         ta[s] = tau;
       }
-      __syncthreads();
-      if (s + 2 >= K) us = R + tri2_row_off<KP>(J0) - J0;
-      const double* uh = us + h * HP;
+      if (s + 2 >= K) {  // x has at most one entry: no reflection (tau = 0)
+        __syncthreads();  // the next step's x / partials overwrite what this step read after A
+        continue;
+      }
+      double* us = R + tri2_row_off<KP>(s);  // entries j in [J0, KP), de-interleaved
+      if (lead && i >= J0) us[(i & 1) * L2 + ((i - J0) >> 1)] = u;
+      const double* xh = xb + h * HP;
       double p0 = 0.0, p1 = 0.0;
 #pragma unroll
-      for (int jj = JL; jj < HP; jj += 2) {
-        double2 uu = *(const double2*)(uh + jj);
-        if (jj < J0) uu = h ? uu : double2{0.0, 0.0};  // lower half left of the row: u = 0
-        p0 = fma(a[jj], uu.x, p0);
-        p1 = fma(a[jj + 1], uu.y, p1);
-        if (((jj - JL) & 7) == 6) lds_batch();
+      for (int jj = JH; jj < HP; jj += 2) {
+        const double2 xx = *(const double2*)(xh + jj);
+        p0 = fma(a[jj], xx.x, p0);
+        p1 = fma(a[jj + 1], xx.y, p1);
+        if (((jj - JH) & 7) == 6) lds_batch();
       }
-      const double pl = p0 + p1, pr = pair_swap(pl);
-      const double p = act ? tau * (h ? pr + pl : pl + pr) : 0.0;
-      const double kk = 0.5 * tau * block_total<NW>(h == 0 ? u * p : 0.0, red + NW, t);
-      const double w = p - kk * u;
-      if (lead) wb[i] = w;
-      __syncthreads();
-      const double* wh = wb + h * HP;
+      double yo = a[JH];  // column s + 1 of row i
 #pragma unroll
-      for (int jj = JL; jj < HP; jj += 2) {
-        const double2 ww = *(const double2*)(wh + jj);
-        double2 uu = *(const double2*)(uh + jj);
-        if (jj < J0) uu = h ? uu : double2{0.0, 0.0};
-        a[jj] = fma(-u, ww.x, fma(-w, uu.x, a[jj]));
-        a[jj + 1] = fma(-u, ww.y, fma(-w, uu.y, a[jj + 1]));
-        if (((jj - JL) & 7) == 6) lds_batch();
+      for (int k = 1; k < 5; ++k)
+        if (JH + k < HP) {
+          double tt = a[JH + k];
+          asm volatile("" : "+v"(tt));
+          yo = ((s + 1) >> 1) == JH + k ? tt : yo;
+        }
+      const double yp = pair_swap(yo);
+      const double as1 = h == ((s + 1) & 1) ? yo : yp;
+      const double pl = p0 + p1, pr = pair_swap(pl);
+      const double p = act ? tau * fma(-beta, as1, h ? pr + pl : pl + pr) : 0.0;
+      double v2 = wave_total(h == 0 ? u * p : 0.0);
+      if ((t & 63) == 0) red[NW + (t >> 6)] = v2;
+      if (lead) wb[(i & 1) * HP + (i >> 1)] = p;
+      __syncthreads();  // B
+      double up = red[NW];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) up += red[NW + w];
+      const double kk = 0.5 * tau * up;
+      const double w2 = fma(-2.0 * kk, u, p);
+      const double* ph = wb + h * HP;
+      const double* uh = us + h * L2 - JH;
+#pragma unroll
+      for (int jj = JH; jj < HP; jj += 2) {
+        const double2 pp = *(const double2*)(ph + jj);
+        const double2 uu = *(const double2*)(uh + jj);
+        a[jj] = fma(-u, pp.x, fma(-w2, uu.x, a[jj]));
+        a[jj + 1] = fma(-u, pp.y, fma(-w2, uu.y, a[jj + 1]));
+        if (((jj - JH) & 7) == 6) lds_batch();
       }
-      // no barrier before the next step (see mc_bias_wide_kernel): every slot the next step
-      // writes before its first barrier was last read before this step's second barrier
     }
   };
   if ((abl & 4) == 0) {
@@ -735,34 +791,42 @@ __global__ __launch_bounds__(NW * 64) void mc_bias_wide2_kernel(
 #pragma unroll
       for (int q = 0; q < HP; ++q) y[q] = 0.0;
     }
+    // to the reflector rows' interleaved layout, in place: lane h trades the entries of the other
+    // parity with its partner, after which register 2 m holds entry 2 m + h and register 2 m + 1
+    // entry HP + 2 m + h (interleaved position jj at register yr(jj) below)
+#pragma unroll
+    for (int m = 0; m < HP / 2; ++m) {
+      const double rv = pair_swap(h ? y[2 * m] : y[2 * m + 1]);
+      if (h) y[2 * m] = rv; else y[2 * m + 1] = rv;
+      __builtin_amdgcn_sched_barrier(0);  // one pair at a time (no register pressure spike)
+    }
   }
-  // ---- 4. back-transform and the bias ratio ----
+  // ---- 4. back-transform (interleaved, as phase 1) and the bias ratio ----
+  constexpr auto yr = [](int jj) { return jj < HP / 2 ? 2 * jj : 2 * (jj - HP / 2) + 1; };
   auto back = [&](auto J0c, int s_hi) {
     constexpr int J0 = decltype(J0c)::value;
-    constexpr int JL = J0 > HP ? J0 - HP : 0;
+    constexpr int JH = J0 / 2, L2 = (KP - J0) / 2;
     for (int s = s_hi; s >= J0; --s) {
       if (s + 2 >= K) continue;
       const double tau = ta[s];
       if (tau == 0.0) continue;
-      const double* uh = R + tri2_row_off<KP>(s) - J0 + h * HP;
+      const double* uh = R + tri2_row_off<KP>(s) + h * L2 - JH;
       double t0 = 0.0, t1 = 0.0;
 #pragma unroll
-      for (int jj = JL; jj < HP; jj += 2) {
-        double2 uu = *(const double2*)(uh + jj);
-        if (jj < J0) uu = h ? uu : double2{0.0, 0.0};
-        t0 = fma(uu.x, y[jj], t0);
-        t1 = fma(uu.y, y[jj + 1], t1);
-        if (((jj - JL) & 7) == 6) lds_batch();
+      for (int jj = JH; jj < HP; jj += 2) {
+        const double2 uu = *(const double2*)(uh + jj);
+        t0 = fma(uu.x, y[yr(jj)], t0);
+        t1 = fma(uu.y, y[yr(jj + 1)], t1);
+        if (((jj - JH) & 7) == 6) lds_batch();
       }
       const double tl = t0 + t1, tr = pair_swap(tl);
       const double f = tau * (h ? tr + tl : tl + tr);
 #pragma unroll
-      for (int jj = JL; jj < HP; jj += 2) {
-        double2 uu = *(const double2*)(uh + jj);
-        if (jj < J0) uu = h ? uu : double2{0.0, 0.0};
-        y[jj] = fma(-f, uu.x, y[jj]);
-        y[jj + 1] = fma(-f, uu.y, y[jj + 1]);
-        if (((jj - JL) & 7) == 6) lds_batch();
+      for (int jj = JH; jj < HP; jj += 2) {
+        const double2 uu = *(const double2*)(uh + jj);
+        y[yr(jj)] = fma(-f, uu.x, y[yr(jj)]);
+        y[yr(jj + 1)] = fma(-f, uu.y, y[yr(jj + 1)]);
+        if (((jj - JH) & 7) == 6) lds_batch();
       }
     }
   };
@@ -776,8 +840,8 @@ __global__ __launch_bounds__(NW * 64) void mc_bias_wide2_kernel(
       double* Ub = Uout + (size_t)d * K * K;
 #pragma unroll
       for (int jj = 0; jj < HP; ++jj) {
-        const int j = h * HP + jj;
-        if (j < K) Ub[(size_t)j * K + i] = y[jj];
+        const int j = 2 * jj + h;
+        if (j < K) Ub[(size_t)j * K + i] = y[yr(jj)];
       }
     }
     return;
@@ -785,8 +849,8 @@ __global__ __launch_bounds__(NW * 64) void mc_bias_wide2_kernel(
   double v = 0.0;
 #pragma unroll
   for (int jj = 0; jj < HP; ++jj) {
-    const double dj = dd[h * HP + jj];  // 0 for the padded entries
-    v = fma(dj * dj, y[jj] * y[jj], v);
+    const double dj = dd[2 * jj + h];  // 0 for the padded entries
+    v = fma(dj * dj, y[yr(jj)] * y[yr(jj)], v);
     if ((jj & 7) == 7) lds_batch();
   }
   const double vo2 = pair_swap(v);
@@ -796,13 +860,13 @@ __global__ __launch_bounds__(NW * 64) void mc_bias_wide2_kernel(
 size_t bias_wide2_lds(int K, int KP, int NW) {
   int n = 0;
   for (int s = 0; s + 2 < K; ++s) n += KP - 8 * (s / 8);
-  return ((size_t)((n + 1) & ~1) + 7 * KP + 2 * NW + 2) * sizeof(double);
+  return ((size_t)((n + 1) & ~1) + 8 * KP + 2 * NW + 2) * sizeof(double);
 }
 
 size_t bias_wide_lds(int K, int KP, int NW) {
   int n = 0;
   for (int s = 0; s + 2 < K; ++s) n += KP - 8 * (s / 8);
-  return ((size_t)((n + 1) & ~1) + NW * 64 + 2 * KP + 2 * KP + 3 * NW * 64 + 2 * NW + 2) *
+  return ((size_t)((n + 1) & ~1) + 2 * NW * 64 + 2 * KP + 2 * KP + 3 * NW * 64 + 2 * NW + 2) *
          sizeof(double);
 }
 
