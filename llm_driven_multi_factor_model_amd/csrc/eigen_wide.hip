@@ -1106,11 +1106,13 @@ MFA_API int mfa_eigh_wide(const double* A, int B, int K, double* w, double* U, v
 }
 
 int g_wide_abl = 0;  // timing-only phase ablations (bits: 1 Laguerre, 2 eigenvectors, 4 Householder)
-int g_wide_variant = 1;  // 1 = two lanes per row for K > 96 (default: 26.9 vs 28.3 ms at K = 140,
-                         // 60 x 100 problems, no spills), 0 = one lane per row
+// 2 = two lanes per row at every K (default since round 6: K = 80 bias 10.1 -> 8.2 ms,
+// profiles/r06/wide_householder/layout_ab.log), 1 = one lane per row for K <= 96 and two for
+// K > 96 (round 5: 26.9 vs 28.3 ms at K = 140, 60 x 100 problems), 0 = one lane per row (A/B)
+int g_wide_variant = 2;
 MFA_API void mfa_eigen_wide_set_ablation(int abl) { g_wide_abl = abl; }
 MFA_API int mfa_eigen_wide_set_variant(int v) {
-  if (!MFA_AB && v != 1) return (int)hipErrorInvalidValue;  // row layout at K > 96: A/B builds
+  if (v < 0 || v > 2 || (!MFA_AB && v == 0)) return (int)hipErrorInvalidValue;  // 0: A/B builds
   g_wide_variant = v;
   return 0;
 }
@@ -1121,12 +1123,21 @@ MFA_API int mfa_eigen_bias_accumulate_wide(const double* D0, const int* dvalid, 
   if (D <= 0 || M <= 0) return 0;
   if (K < 3 || K > 144) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  if (g_wide_variant == 1 && K > 96) {
-    const size_t lds = bias_wide2_lds(K, 144, 5);
-    (void)hipFuncSetAttribute((const void*)mc_bias_wide2_kernel<144, 5>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    hipLaunchKernelGGL((mc_bias_wide2_kernel<144, 5>), dim3(D * M), dim3(5 * 64), lds, s, D0, K, M,
-                       Cz, dvalid, ws, g_wide_abl);
+  if ((g_wide_variant == 1 && K > 96) || g_wide_variant == 2) {
+    // two lanes per row: 5 waves per problem for K > 96, 3 for K <= 96
+    if (K > 96) {
+      const size_t lds = bias_wide2_lds(K, 144, 5);
+      (void)hipFuncSetAttribute((const void*)mc_bias_wide2_kernel<144, 5>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL((mc_bias_wide2_kernel<144, 5>), dim3(D * M), dim3(5 * 64), lds, s, D0, K,
+                         M, Cz, dvalid, ws, g_wide_abl);
+    } else {
+      const size_t lds = bias_wide2_lds(K, 96, 3);
+      (void)hipFuncSetAttribute((const void*)mc_bias_wide2_kernel<96, 3>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL((mc_bias_wide2_kernel<96, 3>), dim3(D * M), dim3(3 * 64), lds, s, D0, K,
+                         M, Cz, dvalid, ws, g_wide_abl);
+    }
     hipLaunchKernelGGL(wide_bias_sum_kernel, dim3(D), dim3(64), 0, s, ws, K, M, S);
     return (int)hipGetLastError();
   }

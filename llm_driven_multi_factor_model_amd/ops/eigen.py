@@ -88,10 +88,11 @@ def set_wide_bias_solver(name: str) -> None:
     _wide_solver = name
 
 
-# Layout of the "hip" wide solver: "pair" = two lanes per matrix row for K > 96 (default: half
-# the registers per lane, no spills, 5 waves per problem; 4.48 vs 4.72 us per 140 x 140
-# problem), "row" = one lane per row.
-WIDE_LAYOUTS = {"row": 0, "pair": 1}
+# Layout of the "hip" wide solver: "pair" = two lanes per matrix row (default: half the registers
+# per lane; 3 waves per problem for K <= 96, 5 for K > 96; K = 80 bias 8.2 vs 10.1 ms with
+# "mixed", profiles/r06/wide_householder/layout_ab.log), "mixed" = one lane per row for K <= 96 and
+# two for K > 96 (round 5's default), "row" = one lane per row at every K (A/B builds only).
+WIDE_LAYOUTS = {"row": 0, "mixed": 1, "pair": 2}
 
 
 def set_wide_kernel_layout(name: str) -> None:

@@ -156,11 +156,12 @@ def test_rocsolver_strided_batched_eigh(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("layout", ["row", "pair"])
+@pytest.mark.parametrize("layout", ["row", "mixed", "pair"])
 def test_hip_wide_bias_solver_matches_oracle(cuda, layout):
-    """csrc/eigen_wide.hip (the "hip" wide solver): K = 42 on the 2-wave kernel equals the
-    one-wave mode-5 kernel, K = 100 / 140 equal the CPU fp64 oracle, with one lane per row and
-    with two lanes per row (K > 96); an invalid date gives NaN."""
+    """csrc/eigen_wide.hip (the "hip" wide solver): K = 42 on the multi-wave kernels equals the
+    one-wave mode-5 kernel, K = 80 / 100 / 140 equal the CPU fp64 oracle, with one lane per row,
+    two lanes per row (every K, the default) and the round-5 mix (one lane per row up to K = 96);
+    an invalid date gives NaN."""
     from llm_driven_multi_factor_model_amd import _native
     if layout == "row" and not _native.ab_build():
         pytest.skip("one lane per row at K > 96: A/B layout, not in the production library")
@@ -173,7 +174,7 @@ def test_hip_wide_bias_solver_matches_oracle(cuda, layout):
 
 
 def _wide_oracle_cases(cuda, g, _native):
-    for K, D, M in ((42, 12, 8), (100, 5, 4), (140, 6, 5)):
+    for K, D, M in ((42, 12, 8), (80, 5, 4), (100, 5, 4), (140, 6, 5)):
         X = torch.randn(D, 400, K, generator=g, dtype=torch.float64)
         F = X.transpose(1, 2) @ X / 400
         F[2] = float("nan")

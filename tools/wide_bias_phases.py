@@ -5,6 +5,7 @@ meaningless): 1 = no Laguerre iterations, 2 = no eigenvectors / back-transform, 
 tridiagonalisation.  Interleaved rounds; prints JSON lines and the min ms per setting.
 
     python tools/wide_bias_phases.py        # env: K=140 D=252
+    LAYOUTS=mixed,pair K=80 python tools/wide_bias_phases.py   # full solver per kernel layout
 """
 import json
 import os
@@ -34,7 +35,31 @@ w = torch.where(valid[:, None], w.clamp_min(0.0), w).contiguous()
 Cz = eigen.mc_cov(cfg.eigen_sims, K, D, seed=cfg.eigen_seed, device=dev)
 lib = _native.lib()
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-settings = [0, 1, 2, 4]
+if os.environ.get("LAYOUTS"):  # full solver per kernel layout, results compared to the first
+    names = os.environ["LAYOUTS"].split(",")
+    out, tl = {}, {n: [] for n in names}
+    try:
+        for rd in range(4):
+            for n in names:
+                eigen.set_wide_kernel_layout(n)
+                torch.cuda.synchronize()
+                e0.record()
+                out[n] = eigen._bias_sum_wide(w, valid, Cz)
+                e1.record()
+                e1.synchronize()
+                if rd:
+                    tl[n].append(e0.elapsed_time(e1))
+    finally:
+        eigen.set_wide_kernel_layout("pair")
+    ref = out[names[0]]
+    for n in names:
+        fin = torch.isfinite(ref)
+        rel = float(((out[n] - ref).abs() / ref.abs().clamp_min(1e-300))[fin].max())
+        print(json.dumps({"K": K, "D": D, "layout": n, "ms": sorted(round(t, 3) for t in tl[n]),
+                          "max_rel_vs_" + names[0]: rel}), flush=True)
+    sys.exit(0)
+# SETTINGS=0,16,32: multisection rounds (bits 4-6) instead of the phase ablations
+settings = [int(a) for a in os.environ.get("SETTINGS", "0,1,2,4").split(",")]
 ts = {a: [] for a in settings}
 try:
     for a in settings:
