@@ -973,9 +973,9 @@ __global__ __launch_bounds__(256) void leverage_kernel(const float* __restrict__
 //              ((t_last - T0) / 256 + 1, T0 = the stock's first ordinal rounded down to 256);
 //   (caller)   incl = inclusive prefix sum of the counts: the virtual base of stock s is
 //              256 * incl[first row of s - 1] and Rv = 256 * incl[R - 1];
-//   seg_fill:  every virtual position a padding position (its own stock start, no real row,
-//              NaN series values);
-//   seg_place: every real row r at v = base_s - T0 + t_r: its omap, seg_v and series values.
+//   seg_place: every real row r at v = base_s - T0 + t_r: its omap, seg_v and series values;
+//              the padding positions (their own stock start, no real row, NaN series values)
+//              by the real row before them.
 // t_r = the row's full-history ordinal (row_ord; null = r - seg_lo[r], the rows are histories).
 struct SegSeries {
   const float* src[4];
@@ -999,15 +999,16 @@ __global__ __launch_bounds__(256) void seg_count_kernel(const int* __restrict__ 
   nb[r] = last ? ((seg_ord(ro, seg_lo, r) - T0) >> 8) + 1 : 0;
 }
 
-__global__ __launch_bounds__(256) void seg_fill_kernel(int Rv, int* __restrict__ seg_v,
-                                                       int* __restrict__ omap, SegSeries ser) {
-  const int p = blockIdx.x * 256 + threadIdx.x;
-  if (p >= Rv) return;
-  if (seg_v) {  // null: a series-only pass over an existing layout
-    seg_v[p] = p;
-    omap[p] = -1;
+// padding positions [p0, p1): their own stock start, no real row, NaN series values
+__device__ __forceinline__ void seg_pad(int p0, int p1, int* __restrict__ seg_v,
+                                        int* __restrict__ omap, const SegSeries& ser) {
+  for (int p = p0; p < p1; ++p) {
+    if (seg_v) {
+      seg_v[p] = p;
+      omap[p] = -1;
+    }
+    for (int k = 0; k < ser.n; ++k) ser.dst[k][p] = qnanf();
   }
-  for (int k = 0; k < ser.n; ++k) ser.dst[k][p] = qnanf();
 }
 
 __global__ __launch_bounds__(256) void seg_place_kernel(const int* __restrict__ seg_lo,
@@ -1019,13 +1020,20 @@ __global__ __launch_bounds__(256) void seg_place_kernel(const int* __restrict__ 
   if (r >= R) return;
   const int sl = seg_lo[r];
   const int t0 = seg_ord(ro, seg_lo, sl);
-  const int base = (sl > 0 ? incl[sl - 1] * 256 : 0) - (t0 & ~255);
+  const int bs = sl > 0 ? incl[sl - 1] * 256 : 0;  // the stock's first virtual position
+  const int base = bs - (t0 & ~255);
   const int v = base + seg_ord(ro, seg_lo, r);
   if (seg_v) {
     omap[v] = r;
     seg_v[v] = base + t0;
   }
   for (int k = 0; k < ser.n; ++k) ser.dst[k][v] = ser.src[k][r];
+  // the padding around this row, written by the row before it: the stock's leading positions
+  // by its first row, a gap in the ordinals or the tail of the stock's last block by the row
+  // before the gap / the last row (no separate fill pass over all Rv positions)
+  if (r == sl) seg_pad(bs, v, seg_v, omap, ser);
+  const bool last = r + 1 == R || seg_lo[r + 1] != sl;
+  seg_pad(v + 1, last ? incl[r] * 256 : base + seg_ord(ro, seg_lo, r + 1), seg_v, omap, ser);
 }
 
 }  // namespace
@@ -1140,7 +1148,7 @@ MFA_API int mfa_cmra_seg(const float* lr, const int* seg_v, const int* omap, int
   return (int)hipGetLastError();
 }
 
-// ---- segment layout construction (see seg_count / seg_fill / seg_place above)
+// ---- segment layout construction (see seg_count / seg_place above)
 MFA_API int mfa_seg_count(const int* seg_lo, const int* row_ord, int R, int* nb, void* s) {
   if (R <= 0) return 0;
   hipLaunchKernelGGL(seg_count_kernel, MFA_GRID(R), 0, (hipStream_t)s, seg_lo, row_ord, R, nb);
@@ -1158,8 +1166,6 @@ MFA_API int mfa_seg_place(const int* seg_lo, const int* row_ord, const int* incl
     ser.src[k] = src[k];
     ser.dst[k] = dst[k];
   }
-  if (Rv > 0)
-    hipLaunchKernelGGL(seg_fill_kernel, MFA_GRID(Rv), 0, (hipStream_t)s, Rv, seg_v, omap, ser);
   if (R > 0)
     hipLaunchKernelGGL(seg_place_kernel, MFA_GRID(R), 0, (hipStream_t)s, seg_lo, row_ord, incl, R,
                        seg_v, omap, ser);

@@ -156,9 +156,10 @@ class SegLayout:
         return out
 
 
-def _layout(seg_lo, row_ord) -> SegLayout:
-    """``row_ord``: None (the rows are full histories), ordinals, or a ready :class:`SegLayout`."""
-    return row_ord if isinstance(row_ord, SegLayout) else SegLayout(seg_lo, row_ord)
+def _layout(seg_lo, row_ord, series=()) -> SegLayout:
+    """``row_ord``: None (the rows are full histories), ordinals, or a ready :class:`SegLayout`.
+    A layout built here places ``series`` in its first pass (one launch for layout + inputs)."""
+    return row_ord if isinstance(row_ord, SegLayout) else SegLayout(seg_lo, row_ord, series)
 
 
 def _f(t):
@@ -242,7 +243,7 @@ def beta_hsigma(ret, mret, seg_lo, window=252, half_life=63.0, min_periods=42, r
     R = ret.numel()
     lam = 0.5 ** (1.0 / half_life)
     if _seg_path(ret) and window <= EW_MAX_W:
-        lay = _layout(seg_lo, row_ord)
+        lay = _layout(seg_lo, row_ord, (ret, mret))
         b = torch.empty(R, dtype=torch.float32, device=ret.device)
         h = torch.empty_like(b)
         # bound to names: a temporary passed as ptr(...) is freed before the launch, and the
@@ -287,7 +288,7 @@ def rstr(log_ret, seg_lo, T=504, L=21, half_life=126.0, min_periods=42, row_ord=
     W = T - L
     lam = 0.5 ** (1.0 / half_life)
     if _seg_path(log_ret) and W >= 1 and L >= 0 and W + L - 1 <= POS_MAX_REACH:
-        lay = _layout(seg_lo, row_ord)
+        lay = _layout(seg_lo, row_ord, (log_ret,))
         out = torch.empty(R, dtype=torch.float32, device=log_ret.device)
         xv = lay.virt(log_ret)
         _native.call("mfa_rstr_seg", _native.ptr(xv), _native.ptr(lay.seg_v), _native.ptr(lay.omap),
@@ -319,7 +320,7 @@ def dastd(ret, mret, seg_lo, window=252, half_life=42.0, min_periods=42, row_ord
     R = ret.numel()
     lam = 0.5 ** (1.0 / half_life)
     if _seg_path(ret) and window <= EW_MAX_W:
-        lay = _layout(seg_lo, row_ord)
+        lay = _layout(seg_lo, row_ord, (ret, mret))
         out = torch.empty(R, dtype=torch.float32, device=ret.device)
         yv, xv = lay.virt(ret), lay.virt(mret)   # named: see beta_hsigma
         _native.call("mfa_dastd_seg", _native.ptr(yv), _native.ptr(xv), _native.ptr(lay.seg_v),
@@ -355,7 +356,7 @@ def cmra(log_ret, seg_lo, window=252, partial=False, row_ord=None):
     Q15) and other windows the direct kernel (rank-invariant too)."""
     R = log_ret.numel()
     if _seg_path(log_ret) and not partial and CMRA_MIN_W <= window <= CMRA_MAX_W:
-        lay = _layout(seg_lo, row_ord)
+        lay = _layout(seg_lo, row_ord, (log_ret,))
         out = torch.empty(R, dtype=torch.float32, device=log_ret.device)
         xv = lay.virt(log_ret)
         _native.call("mfa_cmra_seg", _native.ptr(xv), _native.ptr(lay.seg_v), _native.ptr(lay.omap),
@@ -395,7 +396,7 @@ def window_sums(x, seg_lo, windows, scale=1.0, log=False, row_ord=None):
     windows = [(int(w), int(m)) for w, m in windows]
     if not _seg_path(x) or any(w < 1 or w - 1 > POS_MAX_REACH for w, _ in windows):
         return [rolling_sum(x, seg_lo, w, m, scale, log) for w, m in windows]
-    lay = _layout(seg_lo, row_ord)
+    lay = _layout(seg_lo, row_ord, (x,))
     xv = lay.virt(x)
     outs = []
     for k in range(0, len(windows), 3):

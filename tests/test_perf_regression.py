@@ -21,7 +21,11 @@ MEASURED = {
     "eigen_adjust_2520x100_ms": 8.31,
     # RiskModel.run, 5000 x 2520, K = 42, M = 100: the canonical median of tools/risk_timing.py
     # (3 panel seeds x 5 runs; profiles/r06/risk_stages_canonical.log)
-    "risk_model_run_2520_ms": 10.45,
+    "risk_model_run_2520_ms": 10.05,
+    # the same canonical timing at K = 140 (P = 123 + Q = 16), 252 dates: the wide multi-wave
+    # bias solver (2 barriers per Householder step, column-interleaved row halves;
+    # profiles/r06/wide_householder/risk_k140.log)
+    "risk_model_run_k140_252_ms": 25.3,
     # Newey-West expanding series, T = 2520, K = 42, q = 2
     "newey_west_2520_ms": 0.100,
     # window-descriptor kernels, 5000 x 3780, round 6: the segment-anchored (rank-invariant)
@@ -112,6 +116,17 @@ def test_risk_model_run_canonical_2520():
     ceil = MEASURED["risk_model_run_2520_ms"] / SLACK
     print(f"RiskModel.run 2520 x 5000: median {r['median_ms']:.3f} ms (ceiling {ceil:.3f}); "
           f"per seed {[v['median_ms'] for v in r['per_seed'].values()]}")
+    assert r["median_ms"] < ceil
+
+
+def test_risk_model_run_canonical_k140():
+    """RiskModel.run at K = 140, 252 dates (the wide HIP bias solver): canonical timing."""
+    from llm_driven_multi_factor_model_amd.utils.config import preset
+    from tools.risk_timing import risk_model_timing
+    _warm_clocks()
+    r = risk_model_timing(252, 5000, 123, 16, preset("reference"), torch.device("cuda:0"))
+    ceil = MEASURED["risk_model_run_k140_252_ms"] / SLACK
+    print(f"RiskModel.run K=140 252 x 5000: median {r['median_ms']:.3f} ms (ceiling {ceil:.3f})")
     assert r["median_ms"] < ceil
 
 

@@ -75,8 +75,13 @@ def main():
     ret = (mkt[None, :] * 1.1 + torch.randn(N, T, device=dev, generator=g) * 0.02).reshape(-1).float()
     mret = mkt[None, :].expand(N, T).reshape(-1).contiguous().float()
     seg = RL.seg_lo_from_codes(torch.arange(N, device=dev, dtype=torch.int32).repeat_interleave(T))
+    # the whole recompute: segment layout (+ host read of its size) and inputs placed, kernel;
+    # and the kernel alone on a layout the engine already holds (shared by every descriptor)
     t, _ = timed(lambda: RL.beta_hsigma(ret, mret, seg, 252, 63.0, 42), reps=5)
+    lay = RL.SegLayout(seg, None, (ret, mret))
+    tk, _ = timed(lambda: RL.beta_hsigma(ret, mret, seg, 252, 63.0, 42, row_ord=lay), reps=20)
     res["4_rolling_beta_5000x15y"] = {"seconds": round(t, 5), "stock_days": N * T,
+                                      "kernel_on_built_layout_seconds": round(tk, 5),
                                       "reference_seconds": 4.3 * 3600}
     # 5: NW + 10k-sim eigen bootstrap + attribution (CSI300 x 5y shape; sims-sharded mode)
     t, r = risk_run(1250, 300, 31, 10, preset("bootstrap10k"), dev, attribution=True, reps=3)
