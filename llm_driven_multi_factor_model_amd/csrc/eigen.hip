@@ -280,6 +280,116 @@ __global__ __launch_bounds__(256) void mc_cov_wide_reduce_kernel(int K, int T, i
   }
 }
 
+// ---------------- draw covariances for any K (K > 144) ----------------
+// Output-tiled: a 4-wave workgroup per (sim, 64 x 64 block pair (bi <= bj), time chunk) draws
+// the two 64-factor column blocks of its 64-row time blocks into LDS (the same Philox counters
+// {sim, time row, factor pair, tag}: factor k draws the same number at every K) and accumulates
+// Z_bi^T Z_bj on the fp64 matrix cores, wave w owning the 16-row strip w of the block (4 tiles);
+// diagonal pairs also form their block's column sums.  Raw partials per (sim, pair, chunk) go
+// to `part`; mc_cov_xl_reduce_kernel adds the chunks in chunk order (a function of T only) and
+// centres, so a sim's matrix is bitwise the same in any launch.
+constexpr int kXlPart = 64 * 64 + 64;  // doubles per (sim, pair, chunk)
+
+__device__ __forceinline__ void xl_pair(int p, int KB, int& bi, int& bj) {
+  int r = 0;
+  while (p >= KB - r) { p -= KB - r; ++r; }
+  bi = r;
+  bj = r + p;
+}
+
+__device__ __forceinline__ void xl_draw_block(double (*Z)[66], int m, int t0, int T, int K, int b,
+                                              unsigned long long seed, int tid) {
+  for (int e = tid; e < 64 * 32; e += 256) {
+    const int r = e >> 5, pc = e & 31, tq = t0 + r, pr = 32 * b + pc;
+    const U4 u = philox(U4{(unsigned)m, (unsigned)tq, (unsigned)pr, 0x4D464131u},
+                        (unsigned)seed, (unsigned)(seed >> 32));
+    const double rr = sqrt(-2.0 * log(u01_53(u.x, u.y)));
+    double sn, cn;
+    sincospi(2.0 * u01_53(u.z, u.w), &sn, &cn);
+    const bool okr = tq < T;
+    Z[r][2 * pc] = (okr && 2 * pr < K) ? rr * cn : 0.0;
+    Z[r][2 * pc + 1] = (okr && 2 * pr + 1 < K) ? rr * sn : 0.0;
+  }
+}
+
+__global__ __launch_bounds__(256) void mc_cov_xl_kernel(int K, int T, unsigned long long seed,
+                                                        int m0, int NP, int C,
+                                                        double* __restrict__ part) {
+  const int c = blockIdx.x % C, p = (blockIdx.x / C) % NP, mi = blockIdx.x / (C * NP);
+  const int m = m0 + mi, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int KB = (K + 63) / 64;
+  int bi, bj;
+  xl_pair(p, KB, bi, bj);
+  const int nblk = (T + 63) / 64;
+  const int per = (nblk + C - 1) / C;
+  const int b0 = c * per, b1 = min(nblk, b0 + per);
+  __shared__ double Za[64][66], Zb[64][66];  // +2: conflict-free column reads
+  const bool diag = bi == bj;
+  f64x4 acc[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) acc[u] = f64x4{0.0, 0.0, 0.0, 0.0};
+  double cs = 0.0;
+  const int r16 = lane & 15, k4 = lane >> 4;
+  for (int blk = b0; blk < b1; ++blk) {
+    const int t0 = blk * 64;
+    xl_draw_block(Za, m, t0, T, K, bi, seed, tid);
+    if (!diag) xl_draw_block(Zb, m, t0, T, K, bj, seed, tid);
+    __syncthreads();
+    const double (*ZB)[66] = diag ? Za : Zb;
+#pragma unroll 2
+    for (int k = 0; k < 64; k += 4) {
+      const double a = Za[k + k4][16 * wv + r16];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, ZB[k + k4][16 * u + r16], acc[u], 0, 0, 0);
+    }
+    if (diag && tid < 64)
+      for (int r = 0; r < 64; ++r) cs += Za[r][tid];
+    __syncthreads();
+  }
+  double* pp = part + (size_t)blockIdx.x * kXlPart;
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) pp[((wv * 4 + u) * 4 + e) * 64 + lane] = acc[u][e];
+  if (tid < 64) pp[64 * 64 + tid] = cs;
+}
+
+// Grid (M x NP), 256 threads: the chunk-ordered sums of one (sim, block pair), centred with the
+// two blocks' column sums (from their diagonal pairs), written to both triangles.
+__global__ __launch_bounds__(256) void mc_cov_xl_reduce_kernel(int K, int T, int NP, int C,
+                                                               const double* __restrict__ part,
+                                                               double* __restrict__ Cz) {
+  const int p = blockIdx.x % NP, mi = blockIdx.x / NP, tid = threadIdx.x;
+  const int KB = (K + 63) / 64;
+  int bi, bj;
+  xl_pair(p, KB, bi, bj);
+  __shared__ double ca[64], cb[64];
+  if (tid < 128) {
+    const int bb = tid < 64 ? bi : bj, q = bb * KB - bb * (bb - 1) / 2;  // pair index of (bb, bb)
+    double s = 0.0;
+    for (int c = 0; c < C; ++c)
+      s += part[(((size_t)mi * NP + q) * C + c) * kXlPart + 64 * 64 + (tid & 63)];
+    (tid < 64 ? ca : cb)[tid & 63] = s;
+  }
+  __syncthreads();
+  const double invT1 = 1.0 / (double)(T - 1), invT = 1.0 / (double)T;
+  double* Cm = Cz + (size_t)mi * K * K;
+  for (int x = tid; x < 64 * 64; x += 256) {
+    double s = 0.0;
+    for (int c = 0; c < C; ++c) s += part[(((size_t)mi * NP + p) * C + c) * kXlPart + x];
+    // x = ((w * 4 + u) * 4 + e) * 64 + lane: D[(lane >> 4) + 4 e][lane & 15] of tile (w, u)
+    const int ln = x & 63, e = (x >> 6) & 3, u = (x >> 8) & 3, w = x >> 10;
+    const int li = 16 * w + (ln >> 4) + 4 * e, lj = 16 * u + (ln & 15);
+    const int i = 64 * bi + li, j = 64 * bj + lj;
+    if (i < K && j < K && (bi != bj || li <= lj)) {
+      const double v = (s - ca[li] * cb[lj] * invT) * invT1;
+      Cm[(size_t)i * K + j] = v;
+      Cm[(size_t)j * K + i] = v;
+    }
+  }
+}
+
 // Wide factor sets (K > 64): the standard normals of sims [m0, m0 + M) as Z [M][T][Kp]
 // (Kp = K rounded up to even, the padding column is a real draw the caller ignores), keyed
 // exactly like mc_cov_kernel (Philox counter {sim, time row, factor pair, tag}, one Box-Muller
@@ -1714,6 +1824,26 @@ MFA_API int mfa_mc_cov_wide(int M, int m0, int K, int T, unsigned long long seed
     hipLaunchKernelGGL(mc_cov_wide_kernel<144>, dim3(M * C), dim3(256), 0, s, K, T, seed, m0, C, ws);
     hipLaunchKernelGGL(mc_cov_wide_reduce_kernel<144>, dim3(M), dim3(256), 0, s, K, T, C, ws, Cz);
   }
+  return (int)hipGetLastError();
+}
+
+// Draw covariances for any K (mc_cov_xl_kernel): scratch doubles for (M, K, T).
+MFA_API size_t mfa_mc_cov_xl_ws_doubles(int M, int K, int T) {
+  if (M <= 0 || K < 1 || T < 2) return 0;
+  const int KB = (K + 63) / 64;
+  return (size_t)M * (KB * (KB + 1) / 2) * mc_cov_chunks(M, T) * kXlPart;
+}
+
+// Draw covariances of sims [m0, m0 + M) for any K on the fp64 matrix cores (bitwise the same
+// matrix for a sim in any launch containing it).
+MFA_API int mfa_mc_cov_xl(int M, int m0, int K, int T, unsigned long long seed, double* ws,
+                          double* Cz, void* stream) {
+  if (M <= 0) return 0;
+  if (K < 1 || T < 2 || m0 < 0 || ws == nullptr) return (int)hipErrorInvalidValue;
+  const int KB = (K + 63) / 64, NP = KB * (KB + 1) / 2, C = mc_cov_chunks(M, T);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(mc_cov_xl_kernel, dim3(M * NP * C), dim3(256), 0, s, K, T, seed, m0, NP, C, ws);
+  hipLaunchKernelGGL(mc_cov_xl_reduce_kernel, dim3(M * NP), dim3(256), 0, s, K, T, NP, C, ws, Cz);
   return (int)hipGetLastError();
 }
 

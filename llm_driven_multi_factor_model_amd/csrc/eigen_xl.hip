@@ -1,0 +1,571 @@
+// Eigen solver and Monte-Carlo eigenfactor bias statistic for factor sets wider than the
+// register / LDS-resident kernels (144 < K <= 1024, e.g. SW-L3 industries) on gfx950.
+//
+// Reference: Barra-master/mfm/utils.py:55-92 (eigen_risk_adj: np.linalg.eig of every simulated
+// covariance, v_m = diag(U_m^T F0 U_m) / D_m) applied per date by MFM.py:105-126, which works
+// at any K.  The K <= 144 solvers (csrc/eigen.hip, csrc/eigen_wide.hip) keep a problem's rows in
+// registers and its reflectors in LDS; a 200 x 200 fp64 matrix alone is 320 KB, twice a CU's
+// LDS, so here a problem's working matrix lives in a per-workgroup global slot (L2 / MALL
+// resident while the workgroup works on it) and only vectors sit in LDS:
+//   * one 8-wave workgroup per problem, persistent over the batch (grid = slots, problem
+//     b = blockIdx.x + q gridDim.x): no host synchronisation and no vendor library;
+//   * Householder tridiagonalisation with the rank-2 update of step s fused into the
+//     matrix-vector product of step s + 1: one read + one write of the trailing matrix per step.
+//     Waves own rows and lanes own 64-column chunks, so every access is a coalesced row segment,
+//     and by symmetry the product y = A v is a column sum: each lane accumulates its own column,
+//     the 8 wave partials meet in LDS in wave order (no cross-lane reduction);
+//   * eigenvalues by bisection on the division-free Sturm recurrence (tridiag.h's determinant
+//     form, count only), one lane per eigenvalue, the tridiagonal scaled to unit norm and every
+//     eigenvalue resolved to LAPACK's eps ||T||;
+//   * eigenvectors by twisted factorisation (one lane per eigenvalue; its pivots in a
+//     lane-interleaved global scratch), written column-wise: coalesced over the lanes;
+//   * eigh only: max |Y^T Y - I| of the tridiagonal eigenvectors on the fp64 matrix cores (the
+//     back-transform is orthogonal, so that is U's orthogonality); a matrix that fails it (a
+//     clustered spectrum) is re-solved in its slot by a cyclic round-robin Jacobi;
+//   * the back-transform by the reflectors stored in the working matrix's rows: waves own
+//     64-column chunks of Y, so the K - 2 reflector applications need no barrier.
+// Deterministic: fixed reduction orders, no atomics.  Replaces rocSOLVER's batched syevd, a
+// rocBLAS GEMM and a host-syncing torch.nonzero (round 5's K > 144 path).
+#include "common.h"
+#include "tridiag.h"
+#include "wide_gram.h"
+
+namespace {
+
+using namespace mfa;
+
+constexpr int XW = 8;        // waves per workgroup
+constexpr int XT = XW * 64;  // threads per workgroup
+constexpr int XL_MAX_K = 1024;
+
+__device__ __forceinline__ double xl_ext(double v, double* red, bool mx) {
+  v = mx ? wave_max(v) : wave_min(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double s = red[0];
+  for (int w = 1; w < XW; ++w) s = mx ? fmax(s, red[w]) : fmin(s, red[w]);
+  return s;
+}
+
+// #{eigenvalues of T < x}, T scaled to unit norm (tb[i] = {d_i, e_{i-1}^2}): the leading
+// minors' recurrence f_i = (d_{i-1} - x) f_{i-1} - e_{i-2}^2 f_{i-2}, rescaled by a power of
+// two every 4 steps (exact), sign changes counted.
+__device__ __forceinline__ int xl_sturm(const double2* tb, int K, double x) {
+  double f2 = 1.0, f1 = tb[0].x - x;
+  int cnt = f1 < 0.0;
+  int i = 1;
+  for (; i + 3 < K; i += 4) {
+    const double2 t0 = tb[i], t1 = tb[i + 1], t2 = tb[i + 2], t3 = tb[i + 3];
+    double f0 = fma(t0.x - x, f1, -t0.y * f2);
+    cnt += (f0 < 0.0) != (f1 < 0.0);
+    f2 = fma(t1.x - x, f0, -t1.y * f1);
+    cnt += (f2 < 0.0) != (f0 < 0.0);
+    f1 = fma(t2.x - x, f2, -t2.y * f0);
+    cnt += (f1 < 0.0) != (f2 < 0.0);
+    f0 = fma(t3.x - x, f1, -t3.y * f2);
+    cnt += (f0 < 0.0) != (f1 < 0.0);
+    f2 = f1;
+    f1 = f0;
+    int e;
+    frexp(fmax(fabs(f1), fabs(f2)), &e);
+    f1 = ldexp(f1, -e);
+    f2 = ldexp(f2, -e);
+  }
+  for (; i < K; ++i) {
+    const double2 t = tb[i];
+    const double f0 = fma(t.x - x, f1, -t.y * f2);
+    cnt += (f0 < 0.0) != (f1 < 0.0);
+    f2 = f1;
+    f1 = f0;
+  }
+  return cnt;
+}
+
+__host__ __device__ constexpr int xl_ld(int K) { return (K + 7) & ~7; }
+__host__ __device__ constexpr int xl_ts(int K) { return ((K + 63) & ~63) < XT ? ((K + 63) & ~63) : XT; }
+__host__ __device__ constexpr size_t xl_slot_doubles(int K) {
+  return 2 * (size_t)K * xl_ld(K) + 2 * (size_t)K * xl_ts(K);
+}
+constexpr size_t xl_lds_bytes(int K) { return (17 * (size_t)K + 16) * sizeof(double); }
+
+// Cyclic round-robin Jacobi of the symmetric S (global, row stride LD) with V <- V J (V starts
+// at I): the eigh re-solve of a matrix whose tridiagonal eigenvectors failed the orthogonality
+// test.  Rotation of pair (p, q), zeroing S_pq: J_pp = J_qq = c, J_pq = s, J_qp = -s.
+__device__ void xl_jacobi(double* S, double* V, int K, int LD, int* idx, double* cs_c,
+                          double* cs_s, double* red) {
+  const int tid = threadIdx.x;
+  const int Ke = K + (K & 1), np = Ke / 2;
+  for (int k = tid; k < Ke; k += XT) idx[k] = k;
+  __syncthreads();
+  auto at = [&](int i, int j) -> double { return (i < K && j < K) ? S[(size_t)i * LD + j] : 0.0; };
+  for (int sweep = 0; sweep < 40; ++sweep) {
+    double nrot = 0.0;
+    for (int round = 0; round < Ke - 1; ++round) {
+      for (int i = tid; i < np; i += XT) {
+        int p = idx[i], q = idx[Ke - 1 - i];
+        if (p > q) { const int t = p; p = q; q = t; }
+        double c = 1.0, s = 0.0;
+        if (q < K) {
+          const double apq = at(p, q), app = at(p, p), aqq = at(q, q);
+          if (fabs(apq) > 1e-300 && fabs(apq) > 1e-17 * sqrt(fabs(app) * fabs(aqq))) {
+            const double tau = (aqq - app) / (2.0 * apq);
+            const double t = (tau >= 0.0 ? 1.0 : -1.0) / (fabs(tau) + sqrt(1.0 + tau * tau));
+            c = 1.0 / sqrt(1.0 + t * t);
+            s = t * c;
+            nrot += 1.0;
+          }
+        }
+        cs_c[i] = c;
+        cs_s[i] = s;
+      }
+      __syncthreads();
+      for (int e = tid; e < np * np; e += XT) {  // S <- J^T S J, one 2 x 2 pair block each
+        const int bi = e / np, bj = e - bi * np;
+        int p = idx[bi], q = idx[Ke - 1 - bi], r = idx[bj], t = idx[Ke - 1 - bj];
+        if (p > q) { const int x = p; p = q; q = x; }
+        if (r > t) { const int x = r; r = t; t = x; }
+        const double ci = cs_c[bi], si = cs_s[bi], cj = cs_c[bj], sj = cs_s[bj];
+        if (si == 0.0 && sj == 0.0) continue;
+        const double b00 = at(p, r), b01 = at(p, t), b10 = at(q, r), b11 = at(q, t);
+        const double x00 = ci * b00 - si * b10, x01 = ci * b01 - si * b11;
+        const double x10 = si * b00 + ci * b10, x11 = si * b01 + ci * b11;
+        double y00 = cj * x00 - sj * x01, y01 = sj * x00 + cj * x01;
+        double y10 = cj * x10 - sj * x11, y11 = sj * x10 + cj * x11;
+        if (bi == bj) { y01 = 0.0; y10 = 0.0; }
+        if (p < K && r < K) S[(size_t)p * LD + r] = y00;
+        if (p < K && t < K) S[(size_t)p * LD + t] = y01;
+        if (q < K && r < K) S[(size_t)q * LD + r] = y10;
+        if (q < K && t < K) S[(size_t)q * LD + t] = y11;
+      }
+      for (int e = tid; e < K * np; e += XT) {  // V <- V J
+        const int r = e / np, i = e - r * np;
+        const double c = cs_c[i], s = cs_s[i];
+        if (s == 0.0) continue;
+        int p = idx[i], q = idx[Ke - 1 - i];
+        if (p > q) { const int x = p; p = q; q = x; }
+        if (q >= K) continue;
+        const double vp = V[(size_t)r * LD + p], vq = V[(size_t)r * LD + q];
+        V[(size_t)r * LD + p] = c * vp - s * vq;
+        V[(size_t)r * LD + q] = s * vp + c * vq;
+      }
+      __syncthreads();
+      if (tid == 0) {  // round-robin: position 0 fixed, the others shift by one
+        const int last = idx[Ke - 1];
+        for (int k = Ke - 1; k > 1; --k) idx[k] = idx[k - 1];
+        idx[1] = last;
+      }
+      __syncthreads();
+    }
+    if (block_sum(nrot, red) == 0.0) break;
+  }
+}
+
+// EIG: problem b = matrix Ain[b] -> w[b] (descending), U[b] (U[:, k] = eigenvector k), flags[b]
+// (1 = re-solved by the Jacobi; nullable).  !EIG: problem b = (date d = b / M, sim m = b % M),
+// A = S C_z[m] S with S = diag(sqrt D0[d]) -> v[b][k] = sum_i D0[d][i] V[i][k]^2 / Lambda[k].
+template <bool EIG>
+__global__ __launch_bounds__(XT) void eig_xl_kernel(int B, int K, const double* __restrict__ Ain,
+                                                    const double* __restrict__ D0,
+                                                    const int* __restrict__ dvalid, int M,
+                                                    const double* __restrict__ Cz, double tol,
+                                                    double* __restrict__ wout,
+                                                    double* __restrict__ out,
+                                                    int* __restrict__ flags,
+                                                    double* __restrict__ scratch) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int LD = xl_ld(K), TS = xl_ts(K);
+  double2* tb = reinterpret_cast<double2*>(sm);  // {d_i, e_{i-1}^2}
+  double* es = sm + 2 * K;                       // e_i (signed)
+  double* tau = es + K;
+  double* lam = tau + K;                         // sqrt D0 during the setup, then eigenvalues
+  double* dd = lam + K;                          // D0 (bias)
+  double* va = dd + K;
+  double* vb = va + K;
+  double* wp = vb + K;
+  double* yp = wp + K;                           // [XW][K] wave partials
+  double* red = yp + XW * K;
+  double* Aw = scratch + (size_t)blockIdx.x * xl_slot_doubles(K);
+  double* Y = Aw + (size_t)K * LD;
+  double* tw = Y + (size_t)K * LD;               // [2K][TS] twisted-factorisation pivots
+  for (int b = blockIdx.x; b < B; b += gridDim.x) {
+    __syncthreads();  // LDS of the previous problem
+    // ---- working matrix ----
+    bool fin = true;
+    if (EIG) {
+      const double* A = Ain + (size_t)b * K * K;
+      for (int e = tid; e < K * K; e += XT) {
+        const int i = e / K, j = e - i * K;
+        const double a = 0.5 * (A[e] + A[(size_t)j * K + i]);
+        fin = fin && __builtin_isfinite(a);
+        Aw[(size_t)i * LD + j] = a;
+      }
+    } else {
+      const int d = b / M, m = b - d * M;
+      fin = dvalid[d] != 0;
+      for (int i = tid; i < K; i += XT) {
+        const double x = D0[(size_t)d * K + i];
+        dd[i] = x;
+        lam[i] = sqrt(x);
+      }
+      __syncthreads();
+      const double* C = Cz + (size_t)m * K * K;
+      for (int e = tid; e < K * K; e += XT) {
+        const int i = e / K, j = e - i * K;
+        Aw[(size_t)i * LD + j] = lam[i] * C[e] * lam[j];
+      }
+    }
+    if (block_sum(fin ? 0.0 : 1.0, red) != 0.0) {
+      if (EIG) {
+        for (int k = tid; k < K; k += XT) wout[(size_t)b * K + k] = qnan();
+        for (int e = tid; e < K * K; e += XT) out[(size_t)b * K * K + e] = qnan();
+        if (tid == 0 && flags) flags[b] = 0;
+      } else {
+        for (int k = tid; k < K; k += XT) out[(size_t)b * K + k] = qnan();
+      }
+      continue;
+    }
+    // ---- Householder tridiagonalisation, update of step s fused into the product of s + 1 ----
+    double* vp = va;  // v of step s - 1 (pending update with wp)
+    double* vc = vb;  // v of step s
+    for (int s = 0; s + 2 < K; ++s) {
+      const bool pend = s > 0;
+      double sg = 0.0;
+      for (int j = s + tid; j < K; j += XT) {  // row s, final after the pending update
+        double a = Aw[(size_t)s * LD + j];
+        if (pend) a = fma(-vp[s], wp[j], fma(-wp[s], vp[j], a));
+        if (j == s) {
+          tb[s].x = a;
+        } else {
+          vc[j] = a;
+          if (j >= s + 2) sg = fma(a, a, sg);
+        }
+      }
+      const double sigma = block_sum(sg, red);
+      const double alpha = vc[s + 1];
+      double ts = 0.0, beta = alpha, scal = 0.0;
+      if (sigma != 0.0) {
+        const double nrm = sqrt(fma(alpha, alpha, sigma));
+        beta = alpha >= 0.0 ? -nrm : nrm;
+        ts = (beta - alpha) / beta;
+        scal = 1.0 / (alpha - beta);
+      }
+      if (tid == 0) {
+        es[s] = beta;
+        tau[s] = ts;
+      }
+      for (int j = s + 1 + tid; j < K; j += XT) {
+        const double v = j == s + 1 ? 1.0 : vc[j] * scal;
+        vc[j] = v;
+        if (j >= s + 2) Aw[(size_t)s * LD + j] = v;  // reflector s, v_{s+1} = 1 implied
+      }
+      __syncthreads();
+      for (int i0 = s + 1; i0 < K; i0 += 64) {
+        const int i = i0 + lane;
+        if (i < K) {
+          const double vpi = pend ? vp[i] : 0.0, wpi = pend ? wp[i] : 0.0;
+          double acc = 0.0;
+          int j = s + 1 + wv;
+          for (; j + 3 * XW < K; j += 4 * XW) {
+            double a0 = Aw[(size_t)j * LD + i], a1 = Aw[(size_t)(j + XW) * LD + i];
+            double a2 = Aw[(size_t)(j + 2 * XW) * LD + i], a3 = Aw[(size_t)(j + 3 * XW) * LD + i];
+            if (pend) {
+              a0 = fma(-vp[j], wpi, fma(-wp[j], vpi, a0));
+              a1 = fma(-vp[j + XW], wpi, fma(-wp[j + XW], vpi, a1));
+              a2 = fma(-vp[j + 2 * XW], wpi, fma(-wp[j + 2 * XW], vpi, a2));
+              a3 = fma(-vp[j + 3 * XW], wpi, fma(-wp[j + 3 * XW], vpi, a3));
+              Aw[(size_t)j * LD + i] = a0;
+              Aw[(size_t)(j + XW) * LD + i] = a1;
+              Aw[(size_t)(j + 2 * XW) * LD + i] = a2;
+              Aw[(size_t)(j + 3 * XW) * LD + i] = a3;
+            }
+            acc = fma(a0, vc[j], acc);
+            acc = fma(a1, vc[j + XW], acc);
+            acc = fma(a2, vc[j + 2 * XW], acc);
+            acc = fma(a3, vc[j + 3 * XW], acc);
+          }
+          for (; j < K; j += XW) {
+            double a = Aw[(size_t)j * LD + i];
+            if (pend) {
+              a = fma(-vp[j], wpi, fma(-wp[j], vpi, a));
+              Aw[(size_t)j * LD + i] = a;
+            }
+            acc = fma(a, vc[j], acc);
+          }
+          yp[wv * K + i] = acc;
+        }
+      }
+      __syncthreads();
+      double dp = 0.0;
+      for (int i = s + 1 + tid; i < K; i += XT) {
+        double y = yp[i];
+        for (int w = 1; w < XW; ++w) y += yp[w * K + i];
+        const double p = ts * y;
+        wp[i] = p;
+        dp = fma(p, vc[i], dp);
+      }
+      const double hc = 0.5 * ts * block_sum(dp, red);
+      for (int i = s + 1 + tid; i < K; i += XT) wp[i] = fma(-hc, vc[i], wp[i]);
+      __syncthreads();
+      double* t = vp;
+      vp = vc;
+      vc = t;
+    }
+    if (tid == 0) {  // the last 2 x 2 block with the pending update of step K - 3
+      const int p = K - 2, q = K - 1;
+      double a00 = Aw[(size_t)p * LD + p], a01 = Aw[(size_t)p * LD + q], a11 = Aw[(size_t)q * LD + q];
+      if (K >= 3) {
+        a00 -= 2.0 * vp[p] * wp[p];
+        a01 -= vp[p] * wp[q] + wp[p] * vp[q];
+        a11 -= 2.0 * vp[q] * wp[q];
+      }
+      tb[p].x = a00;
+      tb[q].x = a11;
+      es[p] = a01;
+      es[q] = 0.0;
+      tau[p] = 0.0;
+      tau[q] = 0.0;
+    }
+    __syncthreads();
+    // ---- scale T to unit norm (Gershgorin) ----
+    double lo = INFINITY, hi = -INFINITY;
+    for (int i = tid; i < K; i += XT) {
+      const double r = (i > 0 ? fabs(es[i - 1]) : 0.0) + fabs(es[i]);
+      lo = fmin(lo, tb[i].x - r);
+      hi = fmax(hi, tb[i].x + r);
+    }
+    lo = xl_ext(lo, red, false);
+    hi = xl_ext(hi, red, true);
+    double tn = fmax(fabs(lo), fabs(hi));
+    if (!(tn > 0.0) || !__builtin_isfinite(tn)) tn = 1.0;
+    const double is = 1.0 / tn;
+    for (int i = tid; i < K; i += XT) {
+      const double e0 = i > 0 ? es[i - 1] * is : 0.0;
+      tb[i] = double2{tb[i].x * is, e0 * e0};
+    }
+    __syncthreads();
+    for (int i = tid; i < K; i += XT) es[i] *= is;
+    lo = lo * is - 1e-15;
+    hi = hi * is + 1e-15;
+    // ---- eigenvalues (descending: lane k finds ascending index K - 1 - k) ----
+    for (int k = tid; k < K; k += XT) {
+      const int ix = K - 1 - k;
+      double a = lo, c = hi;
+      for (int it = 0; it < 128; ++it) {
+        if (!(c - a > fmax(2.3e-16, 4.5e-16 * fmax(fabs(a), fabs(c))))) break;
+        const double mid = 0.5 * (a + c);
+        if (xl_sturm(tb, K, mid) > ix) c = mid; else a = mid;
+      }
+      lam[k] = 0.5 * (a + c);
+    }
+    __syncthreads();
+    // ---- eigenvectors of T by twisted factorisation ----
+    const double pivmin = 1e-290;
+    for (int k = tid; k < K; k += XT) {
+      const double x = lam[k];
+      double* tp = tw + tid;
+      double* tm = tw + (size_t)K * TS + tid;
+      double dp = guard_pivot(tb[0].x - x, pivmin);
+      tp[0] = dp;
+      for (int i = 1; i < K; ++i) {
+        dp = guard_pivot((tb[i].x - x) - tb[i].y / dp, pivmin);
+        tp[(size_t)i * TS] = dp;
+      }
+      double dm = guard_pivot(tb[K - 1].x - x, pivmin);
+      tm[(size_t)(K - 1) * TS] = dm;
+      double best = fabs(dp);
+      int r = K - 1;
+      for (int i = K - 2; i >= 0; --i) {
+        const double di = tb[i].x - x;
+        dm = guard_pivot(di - tb[i + 1].y / dm, pivmin);
+        tm[(size_t)i * TS] = dm;
+        const double g = fabs(tp[(size_t)i * TS] + dm - di);
+        if (g < best) {
+          best = g;
+          r = i;
+        }
+      }
+      double z = 1.0, nrm = 1.0;
+      Y[(size_t)r * LD + k] = 1.0;
+      for (int i = r - 1; i >= 0; --i) {
+        z = -(es[i] / tp[(size_t)i * TS]) * z;
+        Y[(size_t)i * LD + k] = z;
+        nrm = fma(z, z, nrm);
+      }
+      z = 1.0;
+      for (int i = r + 1; i < K; ++i) {
+        z = -(es[i - 1] / tm[(size_t)i * TS]) * z;
+        Y[(size_t)i * LD + k] = z;
+        nrm = fma(z, z, nrm);
+      }
+      const double sc = 1.0 / sqrt(nrm);
+      for (int i = 0; i < K; ++i) Y[(size_t)i * LD + k] *= sc;
+    }
+    __syncthreads();
+    // ---- eigh: orthogonality of the tridiagonal eigenvectors; Jacobi re-solve on failure ----
+    if (EIG) {
+      const int KT = (K + 15) / 16, NT = KT * (KT + 1) / 2;
+      double err = 0.0;
+      for (int t = wv; t < NT; t += XW) {
+        int ti = 0, tt = t;
+        while (tt >= KT - ti) { tt -= KT - ti; ++ti; }
+        const int tj = ti + tt;
+        const int ca = 16 * ti + (lane & 15), cb = 16 * tj + (lane & 15);
+        f64x4g acc = f64x4g{0.0, 0.0, 0.0, 0.0};
+        for (int r0 = 0; r0 < K; r0 += 4) {
+          const int r = r0 + (lane >> 4);
+          const double a = (r < K && ca < K) ? Y[(size_t)r * LD + ca] : 0.0;
+          const double c = (r < K && cb < K) ? Y[(size_t)r * LD + cb] : 0.0;
+          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, c, acc, 0, 0, 0);
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 16 * ti + (lane >> 4) + 4 * e, j = 16 * tj + (lane & 15);
+          if (i < K && j < K) {
+            const double g = fabs(acc[e] - (i == j ? 1.0 : 0.0));
+            err = (g > err || g != g) ? g : err;
+          }
+        }
+      }
+      err = xl_ext(err != err ? INFINITY : err, red, true);
+      if (!(err <= tol)) {
+        const double* A = Ain + (size_t)b * K * K;
+        for (int e = tid; e < K * K; e += XT) {
+          const int i = e / K, j = e - i * K;
+          Aw[(size_t)i * LD + j] = 0.5 * (A[e] + A[(size_t)j * K + i]);
+          Y[(size_t)i * LD + j] = i == j ? 1.0 : 0.0;
+        }
+        __syncthreads();
+        int* idx = reinterpret_cast<int*>(yp);
+        double* cs_c = yp + (K + 2) / 2 + 2;
+        double* cs_s = cs_c + K / 2 + 2;
+        xl_jacobi(Aw, Y, K, LD, idx, cs_c, cs_s, red);
+        __syncthreads();
+        for (int k = tid; k < K; k += XT) {  // descending rank of diag entry k (ties by index)
+          const double dk = Aw[(size_t)k * LD + k];
+          int rank = 0;
+          for (int j = 0; j < K; ++j) {
+            const double dj = Aw[(size_t)j * LD + j];
+            rank += (dj > dk) || (dj == dk && j < k);
+          }
+          idx[k] = rank;
+          wout[(size_t)b * K + rank] = dk;
+        }
+        __syncthreads();
+        double* Ub = out + (size_t)b * K * K;
+        for (int e = tid; e < K * K; e += XT) {
+          const int r = e / K, k = e - r * K;
+          Ub[(size_t)r * K + idx[k]] = Y[(size_t)r * LD + k];
+        }
+        if (tid == 0 && flags) flags[b] = 1;
+        continue;
+      }
+      if (tid == 0 && flags) flags[b] = 0;
+    }
+    // ---- back-transform Y <- H_0 ... H_{K-3} Y (waves own 64-column chunks), outputs ----
+    for (int c0 = 64 * wv; c0 < K; c0 += 64 * XW) {
+      const int k = c0 + lane;
+      if (k >= K) continue;
+      for (int s = K - 3; s >= 0; --s) {
+        const double t = tau[s];
+        if (t == 0.0) continue;
+        const double* vr = Aw + (size_t)s * LD;
+        double d0 = Y[(size_t)(s + 1) * LD + k], d1 = 0.0;
+        int r = s + 2;
+        for (; r + 1 < K; r += 2) {
+          d0 = fma(vr[r], Y[(size_t)r * LD + k], d0);
+          d1 = fma(vr[r + 1], Y[(size_t)(r + 1) * LD + k], d1);
+        }
+        if (r < K) d0 = fma(vr[r], Y[(size_t)r * LD + k], d0);
+        const double f = t * (d0 + d1);
+        Y[(size_t)(s + 1) * LD + k] -= f;
+        for (r = s + 2; r < K; ++r) Y[(size_t)r * LD + k] = fma(-f, vr[r], Y[(size_t)r * LD + k]);
+      }
+      const double lk = lam[k] * tn;
+      if (EIG) {
+        wout[(size_t)b * K + k] = lk;
+        double* Ub = out + (size_t)b * K * K;
+        for (int r = 0; r < K; ++r) Ub[(size_t)r * K + k] = Y[(size_t)r * LD + k];
+      } else {
+        double sm0 = 0.0;
+        for (int r = 0; r < K; ++r) {
+          const double y = Y[(size_t)r * LD + k];
+          sm0 = fma(dd[r] * y, y, sm0);
+        }
+        out[(size_t)b * K + k] = sm0 / lk;
+      }
+    }
+  }
+}
+
+// S[d][k] += sum over m < M of v[d * M + m][k] (sim order: deterministic)
+__global__ __launch_bounds__(256) void xl_bias_sum_kernel(const double* __restrict__ v, int K, int M,
+                                                          double* __restrict__ S) {
+  const int d = blockIdx.x;
+  for (int k = threadIdx.x; k < K; k += 256) {
+    double s = 0.0;
+    for (int m = 0; m < M; ++m) s += v[((size_t)d * M + m) * K + k];
+    S[(size_t)d * K + k] += s;
+  }
+}
+
+int xl_slots(int B, int K) {
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    (void)hipGetDevice(&dev);
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+      cus = 256;
+  }
+  const int per = K <= 512 ? 2 : 1;
+  return B < per * cus ? B : per * cus;
+}
+
+template <bool EIG>
+int xl_prepare() {
+  return (int)hipFuncSetAttribute((const void*)eig_xl_kernel<EIG>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)xl_lds_bytes(XL_MAX_K));
+}
+
+}  // namespace
+
+// Scratch doubles of the XL solvers for a batch of B problems of order K (144 < K <= 1024).
+MFA_API size_t mfa_eigen_xl_ws_doubles(int B, int K) {
+  if (B <= 0 || K < 3 || K > XL_MAX_K) return 0;
+  return (size_t)xl_slots(B, K) * xl_slot_doubles(K);
+}
+
+// Batched eigendecomposition of symmetric [B][K][K] fp64 matrices (3 <= K <= 1024): w [B][K]
+// descending, U [B][K][K] with U[:, k] = eigenvector k, NaN for non-finite inputs; a matrix
+// whose tridiagonal eigenvectors miss max |Y^T Y - I| <= tol is re-solved by the Jacobi
+// (fixed[b] = 1; nullable).  ws: mfa_eigen_xl_ws_doubles(B, K).
+MFA_API int mfa_eigh_xl(const double* A, int B, int K, double tol, double* w, double* U,
+                        int* fixed, double* ws, void* stream) {
+  if (B <= 0) return 0;
+  if (K < 3 || K > XL_MAX_K || ws == nullptr) return (int)hipErrorInvalidValue;
+  if (int e = xl_prepare<true>()) return e;
+  hipLaunchKernelGGL((eig_xl_kernel<true>), dim3(xl_slots(B, K)), dim3(XT), xl_lds_bytes(K),
+                     (hipStream_t)stream, B, K, A, (const double*)nullptr, (const int*)nullptr, 1,
+                     (const double*)nullptr, tol, w, U, fixed, ws);
+  return (int)hipGetLastError();
+}
+
+// Bias statistic, 3 <= K <= 1024: S[d][k] += sum over this call's M sims of v_m[d][k] (A =
+// S C_z[m] S per (date, sim)); w [D][K] the clamped F0 eigenvalues, dvalid [D] (0 -> NaN),
+// vws: D * M * K doubles, ws: mfa_eigen_xl_ws_doubles(D * M, K).
+MFA_API int mfa_eigen_bias_accumulate_xl(const double* w, const int* dvalid, int D, int K, int M,
+                                         const double* Cz, double* vws, double* ws, double* S,
+                                         void* stream) {
+  if (D <= 0 || M <= 0) return 0;
+  if (K < 3 || K > XL_MAX_K || ws == nullptr || vws == nullptr) return (int)hipErrorInvalidValue;
+  if (int e = xl_prepare<false>()) return e;
+  const int B = D * M;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL((eig_xl_kernel<false>), dim3(xl_slots(B, K)), dim3(XT), xl_lds_bytes(K), s,
+                     B, K, (const double*)nullptr, w, dvalid, M, Cz, 0.0, (double*)nullptr, vws,
+                     (int*)nullptr, ws);
+  hipLaunchKernelGGL(xl_bias_sum_kernel, dim3(D), dim3(256), 0, s, vws, K, M, S);
+  return (int)hipGetLastError();
+}

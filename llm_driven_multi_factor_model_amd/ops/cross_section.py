@@ -38,6 +38,9 @@ XS_NEAR_SINGULAR = 4
 XS_ZERO_PIVOT = 8
 XS_BAD_SIGMA = 16
 XS_REFINED = 32          # re-solved by the device pseudo-inverse pass
+# Industry count bound: the kernels size their LDS segment tables by P and refuse a launch that
+# does not fit (hipErrorInvalidValue); 512 keeps every path's table inside a CU's LDS at Q <= 16.
+XS_MAX_P = 512
 XS_PINV_CUT = 128        # that pinv cut a direction below 1e-15 lambda_max (rank-deficient)
 XS_DETERMINISTIC = 0x100  # pivot_mode flag of mfa_xs_wls: bitwise-deterministic kernel
 XS_REFINE = 0x200         # pivot_mode flag: device pinv pass for near-singular dates
@@ -72,8 +75,8 @@ def _validate(X, cap, ret, ind, P):
         raise ValueError("ind must be [D, N] when P > 0")
     if not 1 <= Q <= 16:
         raise ValueError(f"Q={Q} outside the supported 1..16 range")
-    if P > 128:
-        raise ValueError(f"P={P} > 128 industries is not supported")
+    if P > XS_MAX_P:
+        raise ValueError(f"P={P} > {XS_MAX_P} industries is not supported")
     return D, Q, N
 
 

@@ -52,6 +52,15 @@ _native.register("mfa_mc_cov_wide", [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uin
                                      C.c_void_p, C.c_void_p])
 _native.register("mfa_mc_cov_wide_ws_doubles", [C.c_int, C.c_int, C.c_int])
 _native.register("mfa_eigen_set_date_origin", [C.c_int])
+_native.register("mfa_eigen_xl_ws_doubles", [C.c_int, C.c_int])
+_native.register("mfa_eigh_xl", [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_void_p,
+                                 C.c_void_p, C.c_void_p, C.c_void_p])
+_native.register("mfa_eigen_bias_accumulate_xl", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
+                                                  C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                  C.c_void_p])
+_native.register("mfa_mc_cov_xl_ws_doubles", [C.c_int, C.c_int, C.c_int])
+_native.register("mfa_mc_cov_xl", [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_void_p,
+                                   C.c_void_p, C.c_void_p])
 _native.register("mfa_eigen_finalize_sum", [C.c_void_p, C.c_int, C.c_void_p, C.c_void_p,
                                              C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p,
                                              C.c_void_p, C.c_void_p])
@@ -63,8 +72,11 @@ TOL = 1e-15
 # kernels: the draw covariances on the fp64 matrix cores (mc_cov_wide_kernel, the same Philox
 # stream: factor k < 64 of a sim is the same number at any K), the F0 eigh and the bias statistic
 # on the multi-wave tridiagonal solver (csrc/eigen_wide.hip, with a device orthogonality check
-# and Jacobi re-solve), the finalize on eigen_finalize_kernel.  Wider K falls back to rocSOLVER's
-# batched symmetric solver and a rocBLAS GEMM in bounded chunks.
+# and Jacobi re-solve), the finalize on eigen_finalize_kernel.  From WIDE_HIP_MAX_K to XL_MAX_K the
+# XL kernels take over (csrc/eigen_xl.hip: one persistent 8-wave workgroup per problem with its
+# working matrix in a global slot; output-tiled MFMA draw covariances in csrc/eigen.hip), still
+# with no vendor library and no host synchronisation.  Only K > XL_MAX_K (or the "rocsolver"
+# A/B setting) uses rocSOLVER's batched symmetric solver and a rocBLAS GEMM in bounded chunks.
 WIDE_K = 64
 ORTHO_TOL = 1e-10                # wide eigh: max |U^T U - I| above this -> device Jacobi re-solve
 WIDE_CHUNK_DOUBLES = 1 << 27     # ~1 GB of fp64 per batched eigh / draw chunk
@@ -74,6 +86,7 @@ WIDE_CHUNK_DOUBLES = 1 << 27     # ~1 GB of fp64 per batched eigh / draw chunk
 # "rocsolver" (batched syevd through torch: 27.7 us).  Wider K always takes rocSOLVER.
 # MFA_WIDE_BIAS selects the solver at import.
 WIDE_HIP_MAX_K = 144
+XL_MAX_K = 1024
 WIDE_BIAS_SOLVERS = ("rocsolver", "hip")
 _wide_solver = os.environ.get("MFA_WIDE_BIAS", "hip")
 if _wide_solver not in WIDE_BIAS_SOLVERS:  # a typo must not silently select rocSOLVER
@@ -213,6 +226,8 @@ def _eigh_wide(Ab, shp):
         _native.call("mfa_eigh_wide_fix", _native.ptr(Ab), B, K, ORTHO_TOL, _native.ptr(w),
                      _native.ptr(U), _native.ptr(ws), None, _native.stream(Ab.device))
         return w.reshape(shp[:-1]), U.reshape(shp)
+    if _wide_solver == "hip" and K <= XL_MAX_K:
+        return _eigh_xl(Ab, shp)
     w = torch.full((B, K), float("nan"), dtype=torch.float64, device=Ab.device)
     U = torch.full((B, K, K), float("nan"), dtype=torch.float64, device=Ab.device)
     ok = torch.isfinite(Ab).all(-1).all(-1)
@@ -224,6 +239,25 @@ def _eigh_wide(Ab, shp):
         ww, UU = torch.linalg.eigh(0.5 * (S + S.transpose(-1, -2)))
         w[sel] = ww.flip(-1)
         U[sel] = UU.flip(-1)
+    return w.reshape(shp[:-1]), U.reshape(shp)
+
+
+def _eigh_xl(Ab, shp):
+    """WIDE_HIP_MAX_K < K <= XL_MAX_K: ``mfa_eigh_xl`` (csrc/eigen_xl.hip) -- Householder with the
+    working matrix in a per-workgroup global slot, bisection eigenvalues, twisted-factorisation
+    eigenvectors, an MFMA orthogonality check and an in-slot Jacobi re-solve of the matrices that
+    fail it; no host synchronisation."""
+    B, K = Ab.shape[0], Ab.shape[-1]
+    dev = Ab.device
+    w = torch.empty(B, K, dtype=torch.float64, device=dev)
+    U = torch.empty(B, K, K, dtype=torch.float64, device=dev)
+    flags = torch.empty(B, dtype=torch.int32, device=dev)
+    ws = torch.empty(max(1, _native.query("mfa_eigen_xl_ws_doubles", B, K)), dtype=torch.float64,
+                     device=dev)
+    _native.call("mfa_eigh_xl", _native.ptr(Ab), B, K, ORTHO_TOL, _native.ptr(w), _native.ptr(U),
+                 _native.ptr(flags), _native.ptr(ws), _native.stream(dev))
+    global LAST_EIGH_FLAGS
+    LAST_EIGH_FLAGS = flags
     return w.reshape(shp[:-1]), U.reshape(shp)
 
 
@@ -282,6 +316,18 @@ def _mc_cov_wide(M: int, K: int, T: int, seed: int, dev, m0: int) -> torch.Tenso
         _native.call("mfa_mc_cov_wide", M, int(m0), K, T, int(seed) & 0xFFFFFFFFFFFFFFFF,
                      _native.ptr(ws), _native.ptr(Cz), _native.stream(dev))
         return Cz
+    if _wide_solver == "hip" and K <= XL_MAX_K:
+        # output-tiled MFMA kernel (mc_cov_xl_kernel), sims chunked to bound the partials
+        Cz = torch.empty(M, K, K, dtype=torch.float64, device=dev)
+        per = max(1, _native.query("mfa_mc_cov_xl_ws_doubles", 1, K, T))
+        step = max(1, WIDE_CHUNK_DOUBLES // per)
+        ws = torch.empty(per * min(step, M), dtype=torch.float64, device=dev)
+        for a in range(0, M, step):
+            mc = min(step, M - a)
+            Cc = Cz[a:a + mc]
+            _native.call("mfa_mc_cov_xl", mc, int(m0 + a), K, T, int(seed) & 0xFFFFFFFFFFFFFFFF,
+                         _native.ptr(ws), _native.ptr(Cc), _native.stream(dev))
+        return Cz
     Kp = K + (K & 1)
     Cz = torch.empty(M, K, K, dtype=torch.float64, device=dev)
     step = max(1, WIDE_CHUNK_DOUBLES // (T * Kp))
@@ -307,6 +353,8 @@ def _bias_sum_wide(w, valid, Cz):
     dev = w.device
     if _wide_solver == "hip" and K <= WIDE_HIP_MAX_K:
         return _bias_sum_wide_hip(w, valid, Cz)
+    if _wide_solver == "hip" and K <= XL_MAX_K:
+        return _bias_sum_xl(w, valid, Cz)
     S = torch.zeros(D, K, dtype=torch.float64, device=dev)
     dd = torch.nonzero(valid).flatten()
     sq = torch.sqrt(w.clamp_min(0.0))
@@ -345,6 +393,28 @@ def _bias_sum_wide_hip(w, valid, Cz):
         cz = Cz[a:a + n].contiguous()
         _native.call("mfa_eigen_bias_accumulate_wide", _native.ptr(wc), _native.ptr(dv), D, K, n,
                      _native.ptr(cz), _native.ptr(ws), _native.ptr(S), _native.stream(dev))
+    return S
+
+
+def _bias_sum_xl(w, valid, Cz):
+    """WIDE_HIP_MAX_K < K <= XL_MAX_K: the XL solver (``mfa_eigen_bias_accumulate_xl``) over
+    chunks of sims, each chunk's per-(date, sim) values summed into S in sim order."""
+    D, K = w.shape
+    M = Cz.shape[0]
+    dev = w.device
+    S = torch.zeros(D, K, dtype=torch.float64, device=dev)
+    wc = w.contiguous()
+    dv = valid.to(torch.int32).contiguous()
+    mc = max(1, min(M, WIDE_CHUNK_DOUBLES // max(1, D * K)))
+    vws = torch.empty(D * mc * K, dtype=torch.float64, device=dev)
+    ws = torch.empty(max(1, _native.query("mfa_eigen_xl_ws_doubles", D * mc, K)),
+                     dtype=torch.float64, device=dev)
+    for a in range(0, M, mc):
+        n = min(mc, M - a)
+        cz = Cz[a:a + n].contiguous()
+        _native.call("mfa_eigen_bias_accumulate_xl", _native.ptr(wc), _native.ptr(dv), D, K, n,
+                     _native.ptr(cz), _native.ptr(vws), _native.ptr(ws), _native.ptr(S),
+                     _native.stream(dev))
     return S
 
 
