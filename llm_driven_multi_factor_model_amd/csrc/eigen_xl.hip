@@ -22,8 +22,9 @@
 //   * eigh only: max |Y^T Y - I| of the tridiagonal eigenvectors on the fp64 matrix cores (the
 //     back-transform is orthogonal, so that is U's orthogonality); a matrix that fails it (a
 //     clustered spectrum) is re-solved in its slot by a cyclic round-robin Jacobi;
-//   * the back-transform by the reflectors stored in the working matrix's rows: waves own
-//     64-column chunks of Y, so the K - 2 reflector applications need no barrier.
+//   * the back-transform by the reflectors stored in the working matrix's rows, in compact-WY
+//     blocks of 16 on the fp64 matrix cores (xl_back_wy): waves own 32- or 64-column chunks of
+//     Y, so the K - 2 reflector applications need no workgroup barrier.
 // Deterministic: fixed reduction orders, no atomics.  Replaces rocSOLVER's batched syevd, a
 // rocBLAS GEMM and a host-syncing torch.nonzero (round 5's K > 144 path).
 #include "common.h"
@@ -87,7 +88,10 @@ __host__ __device__ constexpr int xl_ts(int K) { return ((K + 63) & ~63) < XT ? 
 __host__ __device__ constexpr size_t xl_slot_doubles(int K) {
   return 2 * (size_t)K * xl_ld(K) + 2 * (size_t)K * xl_ts(K);
 }
-constexpr size_t xl_lds_bytes(int K) { return (17 * (size_t)K + 16) * sizeof(double); }
+// wave partials of the tridiagonalisation [XW][K], reused by the back-transform (512 doubles of
+// G / T per wave) and the Jacobi re-solve (round-robin order, rotations)
+__host__ __device__ constexpr int xl_yp(int K) { return XW * K > 512 * XW ? XW * K : 512 * XW; }
+constexpr size_t xl_lds_bytes(int K) { return (9 * (size_t)K + xl_yp(K) + 16) * sizeof(double); }
 
 // Cyclic round-robin Jacobi of the symmetric S (global, row stride LD) with V <- V J (V starts
 // at I): the eigh re-solve of a matrix whose tridiagonal eigenvectors failed the orthogonality
@@ -161,6 +165,98 @@ __device__ void xl_jacobi(double* S, double* V, int K, int LD, int* idx, double*
   }
 }
 
+__device__ __forceinline__ void xl_wsync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Back-transform Y <- H_0 H_1 ... H_{K-3} Y of the wave's NU x 16 columns [c0, c0 + 16 NU) in
+// compact-WY blocks of 16 reflectors (LAPACK dlarft, forward: H_s0 ... H_s0+15 = I - V T V^T,
+// T upper triangular), last block first, on the fp64 matrix cores (v_mfma_f64_16x16x4f64):
+//   G = V^T V and W = V^T Y share one pass over the rows (same A operand), T from G (lanes
+//   0..15, wave-private LDS), W2 = T W straight from W's registers (the MFMA output layout of
+//   W is the B-operand layout of the next product), Y -= V W2 tile by tile (16 rows x 16 cols,
+//   Y loaded as the accumulator).  Y is read twice and written once per 16 reflectors instead
+//   of read twice and written once per reflector.  Reflector s: v[s + 1] = 1, v[r] = Aw[s][r]
+//   for r > s + 1.  16x16x4 f64 layouts: A lane l = A[l & 15][l >> 4], B lane l =
+//   B[l >> 4][l & 15], register e of lane l = D[(l >> 4) + 4 e][l & 15].
+template <int NU>
+__device__ void xl_back_wy(const double* __restrict__ Aw, double* __restrict__ Y,
+                           const double* tau, int K, int LD, int c0, double* wl, int lane) {
+  const int hi = lane >> 4, lo = lane & 15;
+  double* gl = wl;        // G [16][16]
+  double* tl = wl + 256;  // T [16][16]
+  auto vat = [&](int s, int r) -> double {  // reflector s at row r (0 outside)
+    if (s > K - 3 || r >= K || r <= s) return 0.0;
+    return r == s + 1 ? 1.0 : Aw[(size_t)s * LD + r];
+  };
+  const int nblk = (K - 2 + 15) / 16;
+  for (int bk = nblk - 1; bk >= 0; --bk) {
+    const int s0 = 16 * bk, r_lo = s0 + 1;
+    f64x4g G = f64x4g{0.0, 0.0, 0.0, 0.0};
+    f64x4g W[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) W[u] = f64x4g{0.0, 0.0, 0.0, 0.0};
+    for (int r = r_lo; r < K; r += 4) {
+      const int rr = r + hi;
+      const double a = vat(s0 + lo, rr);
+      G = __builtin_amdgcn_mfma_f64_16x16x4f64(a, a, G, 0, 0, 0);
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int c = c0 + 16 * u + lo;
+        const double y = (rr < K && c < K) ? Y[(size_t)rr * LD + c] : 0.0;
+        W[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, y, W[u], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) gl[(hi + 4 * e) * 16 + lo] = G[e];
+    xl_wsync();
+    // T[j][i] = -tau_i sum_{m = j}^{i - 1} T[j][m] G[m][i] (j < i), T[i][i] = tau_i
+    for (int i = 0; i < 16; ++i) {
+      if (lane < 16) {
+        const double ti = s0 + i <= K - 3 ? tau[s0 + i] : 0.0;
+        double acc = 0.0;
+        for (int m = lane; m < i; ++m) acc = fma(tl[lane * 16 + m], gl[m * 16 + i], acc);
+        tl[lane * 16 + i] = lane < i ? -ti * acc : (lane == i ? ti : 0.0);
+      }
+      xl_wsync();
+    }
+    f64x4g W2[NU];
+#pragma unroll
+    for (int u = 0; u < NU; ++u) W2[u] = f64x4g{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const double ta = tl[lo * 16 + 4 * q + hi];
+#pragma unroll
+      for (int u = 0; u < NU; ++u) W2[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(ta, W[u][q], W2[u], 0, 0, 0);
+    }
+    for (int r0 = r_lo; r0 < K; r0 += 16) {
+      double va[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) va[q] = -vat(s0 + 4 * q + hi, r0 + lo);
+#pragma unroll
+      for (int u = 0; u < NU; ++u) {
+        const int c = c0 + 16 * u + lo;
+        f64x4g acc;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = r0 + hi + 4 * e;
+          acc[e] = (r < K && c < K) ? Y[(size_t)r * LD + c] : 0.0;
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f64_16x16x4f64(va[q], W2[u][q], acc, 0, 0, 0);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = r0 + hi + 4 * e;
+          if (r < K && c < K) Y[(size_t)r * LD + c] = acc[e];
+        }
+      }
+    }
+    xl_wsync();  // gl / tl reused by the next block
+  }
+}
+
 // EIG: problem b = matrix Ain[b] -> w[b] (descending), U[b] (U[:, k] = eigenvector k), flags[b]
 // (1 = re-solved by the Jacobi; nullable).  !EIG: problem b = (date d = b / M, sim m = b % M),
 // A = S C_z[m] S with S = diag(sqrt D0[d]) -> v[b][k] = sum_i D0[d][i] V[i][k]^2 / Lambda[k].
@@ -184,8 +280,8 @@ __global__ __launch_bounds__(XT) void eig_xl_kernel(int B, int K, const double* 
   double* va = dd + K;
   double* vb = va + K;
   double* wp = vb + K;
-  double* yp = wp + K;                           // [XW][K] wave partials
-  double* red = yp + XW * K;
+  double* yp = wp + K;                           // [XW][K] wave partials (xl_yp doubles)
+  double* red = yp + xl_yp(K);
   double* Aw = scratch + (size_t)blockIdx.x * xl_slot_doubles(K);
   double* Y = Aw + (size_t)K * LD;
   double* tw = Y + (size_t)K * LD;               // [2K][TS] twisted-factorisation pivots
@@ -463,25 +559,17 @@ __global__ __launch_bounds__(XT) void eig_xl_kernel(int B, int K, const double* 
       }
       if (tid == 0 && flags) flags[b] = 0;
     }
-    // ---- back-transform Y <- H_0 ... H_{K-3} Y (waves own 64-column chunks), outputs ----
-    for (int c0 = 64 * wv; c0 < K; c0 += 64 * XW) {
-      const int k = c0 + lane;
-      if (k >= K) continue;
-      for (int s = K - 3; s >= 0; --s) {
-        const double t = tau[s];
-        if (t == 0.0) continue;
-        const double* vr = Aw + (size_t)s * LD;
-        double d0 = Y[(size_t)(s + 1) * LD + k], d1 = 0.0;
-        int r = s + 2;
-        for (; r + 1 < K; r += 2) {
-          d0 = fma(vr[r], Y[(size_t)r * LD + k], d0);
-          d1 = fma(vr[r + 1], Y[(size_t)(r + 1) * LD + k], d1);
-        }
-        if (r < K) d0 = fma(vr[r], Y[(size_t)r * LD + k], d0);
-        const double f = t * (d0 + d1);
-        Y[(size_t)(s + 1) * LD + k] -= f;
-        for (r = s + 2; r < K; ++r) Y[(size_t)r * LD + k] = fma(-f, vr[r], Y[(size_t)r * LD + k]);
-      }
+    // ---- back-transform Y <- H_0 ... H_{K-3} Y: waves own 32- (K <= 448) or 64-column chunks ----
+    if ((K + 63) / 64 < XW) {
+      for (int c0 = 32 * wv; c0 < K; c0 += 32 * XW)
+        xl_back_wy<2>(Aw, Y, tau, K, LD, c0, yp + 512 * wv, lane);
+    } else {
+      for (int c0 = 64 * wv; c0 < K; c0 += 64 * XW)
+        xl_back_wy<4>(Aw, Y, tau, K, LD, c0, yp + 512 * wv, lane);
+    }
+    __syncthreads();
+    // ---- outputs: lane k owns column k ----
+    for (int k = tid; k < K; k += XT) {
       const double lk = lam[k] * tn;
       if (EIG) {
         wout[(size_t)b * K + k] = lk;
@@ -510,6 +598,16 @@ __global__ __launch_bounds__(256) void xl_bias_sum_kernel(const double* __restri
   }
 }
 
+template <bool EIG>
+int xl_prepare() {
+  return (int)hipFuncSetAttribute((const void*)eig_xl_kernel<EIG>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)xl_lds_bytes(XL_MAX_K));
+}
+
+// Persistent grid: as many workgroups as can be resident at once (a slot beyond that would start
+// only after a resident one has finished its whole share of the batch), at most B.
+template <bool EIG>
 int xl_slots(int B, int K) {
   static int cus = 0;
   if (cus == 0) {
@@ -518,23 +616,23 @@ int xl_slots(int B, int K) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       cus = 256;
   }
-  const int per = K <= 512 ? 2 : 1;
+  (void)xl_prepare<EIG>();
+  int per = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, eig_xl_kernel<EIG>, XT, xl_lds_bytes(K)) !=
+          hipSuccess || per <= 0)
+    per = 1;
   return B < per * cus ? B : per * cus;
 }
 
-template <bool EIG>
-int xl_prepare() {
-  return (int)hipFuncSetAttribute((const void*)eig_xl_kernel<EIG>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)xl_lds_bytes(XL_MAX_K));
-}
 
 }  // namespace
 
 // Scratch doubles of the XL solvers for a batch of B problems of order K (144 < K <= 1024).
 MFA_API size_t mfa_eigen_xl_ws_doubles(int B, int K) {
   if (B <= 0 || K < 3 || K > XL_MAX_K) return 0;
-  return (size_t)xl_slots(B, K) * xl_slot_doubles(K);
+  return (size_t)(xl_slots<true>(B, K) > xl_slots<false>(B, K) ? xl_slots<true>(B, K)
+                                                                 : xl_slots<false>(B, K)) *
+         xl_slot_doubles(K);
 }
 
 // Batched eigendecomposition of symmetric [B][K][K] fp64 matrices (3 <= K <= 1024): w [B][K]
@@ -546,7 +644,7 @@ MFA_API int mfa_eigh_xl(const double* A, int B, int K, double tol, double* w, do
   if (B <= 0) return 0;
   if (K < 3 || K > XL_MAX_K || ws == nullptr) return (int)hipErrorInvalidValue;
   if (int e = xl_prepare<true>()) return e;
-  hipLaunchKernelGGL((eig_xl_kernel<true>), dim3(xl_slots(B, K)), dim3(XT), xl_lds_bytes(K),
+  hipLaunchKernelGGL((eig_xl_kernel<true>), dim3(xl_slots<true>(B, K)), dim3(XT), xl_lds_bytes(K),
                      (hipStream_t)stream, B, K, A, (const double*)nullptr, (const int*)nullptr, 1,
                      (const double*)nullptr, tol, w, U, fixed, ws);
   return (int)hipGetLastError();
@@ -563,7 +661,7 @@ MFA_API int mfa_eigen_bias_accumulate_xl(const double* w, const int* dvalid, int
   if (int e = xl_prepare<false>()) return e;
   const int B = D * M;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL((eig_xl_kernel<false>), dim3(xl_slots(B, K)), dim3(XT), xl_lds_bytes(K), s,
+  hipLaunchKernelGGL((eig_xl_kernel<false>), dim3(xl_slots<false>(B, K)), dim3(XT), xl_lds_bytes(K), s,
                      B, K, (const double*)nullptr, w, dvalid, M, Cz, 0.0, (double*)nullptr, vws,
                      (int*)nullptr, ws);
   hipLaunchKernelGGL(xl_bias_sum_kernel, dim3(D), dim3(256), 0, s, vws, K, M, S);

@@ -167,6 +167,11 @@ __device__ __forceinline__ void wave_sync_lds() {
 constexpr int kRepMax = MFA_XS_REP;
 constexpr int kXsSegPad = 2;  // doubles of padding per industry segment (LDS bank spread)
 constexpr int kSegLdsBudget = 48 * 1024;  // R = 8 only while the table leaves 2 WGs / CU
+// Industries of the split path (moments -> solve -> refine -> residual kernels): the fused
+// kernel's in-kernel solve is sized for P <= 128 (its ring doubles as the solve's LDS); wider
+// industry sets (K > 145 risk models) take the split kernels, whose per-date solve LDS stays
+// within 64 KB and structured pinv within 160 KB up to 256 industries at Q = 16.
+constexpr int kXsSplitMaxP = 256;
 constexpr int kWT = 64;                   // stocks per wave tile (K1: one stock per lane)
 
 // Per-type streaming parameters.  fp32: 4-slot ring of 3.2 KB tiles; fp64: 2-slot ring of
@@ -1160,7 +1165,7 @@ __global__ __launch_bounds__(256) void xs_resid_kernel(
     const int16_t* __restrict__ ind, int D, int N, int P, int S, int C,
     const double* __restrict__ coef, const int* __restrict__ status, T* __restrict__ eout,
     double* __restrict__ r2out, double* __restrict__ sums_out = nullptr) {
-  __shared__ double cf_s[Q + 1 + 128];
+  __shared__ double cf_s[Q + 1 + kXsSplitMaxP];
   __shared__ double red[16][5];
   const int b = (int)(gridDim.x - 1 - blockIdx.x), d = b / S, sc = b - d * S;
   const int nb = sc * C, ne = min(N, nb + C);
@@ -1769,7 +1774,7 @@ __global__ __launch_bounds__(256) void xs_refine_kernel(
   const int st0 = status[d];
   if (!(st0 & XS_NEAR_SINGULAR) || (st0 & XS_BAD)) return;  // uniform: whole workgroup exits
   extern __shared__ double sm[];
-  __shared__ double cf_s[Q + 1 + 128];
+  __shared__ double cf_s[Q + 1 + kXsSplitMaxP];
   __shared__ double red[4][5];
   __shared__ double sc[4];   // W_tot, B_tot, sigma, s_pivot
   __shared__ int piv_s;
@@ -2161,7 +2166,7 @@ int split_dispatch(int what, const T* X, const T* cap, const T* ret, const int16
                    int N, int P, int Q, int pivot_mode, double tol, double* mom, double* f,
                    double* coef, double* stats, int* status, T* e, double* sums, void* stream) {
   if (D <= 0) return 0;
-  if (Q < 1 || Q > 16 || P < 0 || P > 128 || N < 0 || (N % 8) != 0)
+  if (Q < 1 || Q > 16 || P < 0 || P > kXsSplitMaxP || N < 0 || (N % 8) != 0)
     return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
   switch (Q) {

@@ -38,9 +38,11 @@ XS_NEAR_SINGULAR = 4
 XS_ZERO_PIVOT = 8
 XS_BAD_SIGMA = 16
 XS_REFINED = 32          # re-solved by the device pseudo-inverse pass
-# Industry count bound: the kernels size their LDS segment tables by P and refuse a launch that
-# does not fit (hipErrorInvalidValue); 512 keeps every path's table inside a CU's LDS at Q <= 16.
-XS_MAX_P = 512
+# Industry count bounds: the fused kernel's in-kernel solve is sized for FUSED_MAX_P industries;
+# up to XS_MAX_P the GPU runs the split kernels instead (moments -> solve -> device pinv ->
+# residuals, the stock-sharded path at world size 1: csrc/xs_wls_impl.h kXsSplitMaxP).
+FUSED_MAX_P = 128
+XS_MAX_P = 256
 XS_PINV_CUT = 128        # that pinv cut a direction below 1e-15 lambda_max (rank-deficient)
 XS_DETERMINISTIC = 0x100  # pivot_mode flag of mfa_xs_wls: bitwise-deterministic kernel
 XS_REFINE = 0x200         # pivot_mode flag: device pinv pass for near-singular dates
@@ -108,6 +110,10 @@ def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Ten
     K = 1 + P + Q
     if not X.is_cuda:
         return xs_wls_reference(X, cap, ret, ind, P, pivot_mode=pivot_mode, want_resid=want_resid)
+    if P > FUSED_MAX_P:
+        from .xs_sharded import xs_wls_stock_sharded
+        return xs_wls_stock_sharded(X, cap, ret, ind, P, None, pivot_mode=pivot_mode, tol=tol,
+                                    want_resid=want_resid, refine=refine)
     dev = X.device
     dt = X.dtype
     if dt not in (torch.float32, torch.float64):

@@ -107,8 +107,11 @@ def test_xl_eigen_adjust_matches_cpu(cuda, K):
 
 @pytest.mark.gpu
 def test_xl_risk_model_matches_cpu(cuda):
-    """RiskModel.run at P = 163, Q = 16 (K = 180) on the GPU: the eigen stage equals the CPU fp64
-    path on the GPU's own draw covariances, and the run is deterministic (bitwise twice)."""
+    """RiskModel.run at P = 163, Q = 16 (K = 180) on the GPU: the CS-WLS takes the split kernels
+    (P > 128), the eigen stage the XL kernels and equals the CPU fp64 path on the GPU's own draw
+    covariances.  Run twice it agrees to rounding only: above 57 industries at Q = 10 the
+    moments' industry table is one shared LDS replica (order-dependent fp64 atomics), and the
+    eigen adjustment amplifies that ~1e-16 to ~1e-9."""
     D, N, P, Q, M = 230, 1200, 163, 16, 3
     p = synthetic_panel(D, N, P, Q, seed=21, missing_frac=0.01, dtype=torch.float64)
     cfg = preset("reference", eigen_sims=M, nw_half_life=1000.0, vra_half_life=10.0,
@@ -116,7 +119,8 @@ def test_xl_risk_model_matches_cpu(cuda):
     g = RiskModel(p.to(cuda), cfg).run()
     assert g.K == 180
     g2 = RiskModel(p.to(cuda), cfg).run()
-    torch.testing.assert_close(g.eigen_bias, g2.eigen_bias, rtol=0, atol=0, equal_nan=True)
+    torch.testing.assert_close(g.factor_ret, g2.factor_ret, rtol=1e-12, atol=1e-15)
+    torch.testing.assert_close(g.eigen_bias, g2.eigen_bias, rtol=1e-7, atol=1e-10, equal_nan=True)
     fin = torch.isfinite(g.nw_cov.reshape(D, -1)).all(-1).cpu()
     assert fin[180:].all()
     Cz = eigen.mc_cov(M, 180, 400, seed=cfg.eigen_seed, device=cuda).cpu()
@@ -128,11 +132,11 @@ def test_xl_risk_model_matches_cpu(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("P,Q", [(163, 16), (300, 10), (500, 16)])
+@pytest.mark.parametrize("P,Q", [(129, 10), (163, 16), (256, 16)])
 def test_xs_wls_many_industries(cuda, P, Q):
-    """CS-WLS beyond 128 industries (the K > 145 risk models): the fused kernel's shared-replica
-    segment table, the constrained solve and the structured device pinv against the fp64 oracle
-    (near-singular dates included: two industries empty)."""
+    """CS-WLS beyond the fused kernel's 128 industries (the K > 145 risk models): the split
+    kernels (moments -> constrained solve -> structured device pinv -> residuals) against the
+    fp64 oracle, near-singular dates included (two industries empty)."""
     from llm_driven_multi_factor_model_amd.ops import cross_section as X
     p = synthetic_panel(4, 6000, P, Q, seed=P, missing_frac=0.01, empty_industries=2,
                         dtype=torch.float64)
