@@ -23,8 +23,8 @@
 //     back-transform is orthogonal, so that is U's orthogonality); a matrix that fails it (a
 //     clustered spectrum) is re-solved in its slot by a cyclic round-robin Jacobi;
 //   * the back-transform by the reflectors stored in the working matrix's rows, in compact-WY
-//     blocks of 16 on the fp64 matrix cores (xl_back_wy): waves own 32- or 64-column chunks of
-//     Y, so the K - 2 reflector applications need no workgroup barrier.
+//     blocks of 16 on the fp64 matrix cores (xl_back_wy): waves own 32-column chunks of Y, so
+//     the K - 2 reflector applications need no workgroup barrier.
 // Deterministic: fixed reduction orders, no atomics.  Replaces rocSOLVER's batched syevd, a
 // rocBLAS GEMM and a host-syncing torch.nonzero (round 5's K > 144 path).
 #include "common.h"
@@ -38,6 +38,10 @@ using namespace mfa;
 constexpr int XW = 8;        // waves per workgroup
 constexpr int XT = XW * 64;  // threads per workgroup
 constexpr int XL_MAX_K = 1024;
+// Waves per SIMD the solver is compiled for (both instantiated, mfa_eigen_xl_set_wpe): 2 = one
+// 8-wave workgroup per CU without spills (~200 VGPRs), 4 = two workgroups per CU in 128 VGPRs
+// (some scratch spills) -- more problems in flight to cover the tridiagonalisation's memory trips.
+int g_xl_wpe = 2;
 
 __device__ __forceinline__ double xl_ext(double v, double* red, bool mx) {
   v = mx ? wave_max(v) : wave_min(v);
@@ -260,8 +264,8 @@ __device__ void xl_back_wy(const double* __restrict__ Aw, double* __restrict__ Y
 // EIG: problem b = matrix Ain[b] -> w[b] (descending), U[b] (U[:, k] = eigenvector k), flags[b]
 // (1 = re-solved by the Jacobi; nullable).  !EIG: problem b = (date d = b / M, sim m = b % M),
 // A = S C_z[m] S with S = diag(sqrt D0[d]) -> v[b][k] = sum_i D0[d][i] V[i][k]^2 / Lambda[k].
-template <bool EIG>
-__global__ __launch_bounds__(XT) void eig_xl_kernel(int B, int K, const double* __restrict__ Ain,
+template <bool EIG, int WPE>
+__global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void eig_xl_kernel(int B, int K, const double* __restrict__ Ain,
                                                     const double* __restrict__ D0,
                                                     const int* __restrict__ dvalid, int M,
                                                     const double* __restrict__ Cz, double tol,
@@ -335,11 +339,12 @@ __global__ __launch_bounds__(XT) void eig_xl_kernel(int B, int K, const double* 
           tb[s].x = a;
         } else {
           vc[j] = a;
-          if (j >= s + 2) sg = fma(a, a, sg);
+          if (j == s + 1) red[XW + 1] = a;  // alpha: vc[s + 1] becomes 1 below while slower
+          if (j >= s + 2) sg = fma(a, a, sg);  // waves may still be reading
         }
       }
       const double sigma = block_sum(sg, red);
-      const double alpha = vc[s + 1];
+      const double alpha = red[XW + 1];
       double ts = 0.0, beta = alpha, scal = 0.0;
       if (sigma != 0.0) {
         const double nrm = sqrt(fma(alpha, alpha, sigma));
@@ -357,40 +362,59 @@ __global__ __launch_bounds__(XT) void eig_xl_kernel(int B, int K, const double* 
         if (j >= s + 2) Aw[(size_t)s * LD + j] = v;  // reflector s, v_{s+1} = 1 implied
       }
       __syncthreads();
-      for (int i0 = s + 1; i0 < K; i0 += 64) {
-        const int i = i0 + lane;
-        if (i < K) {
-          const double vpi = pend ? vp[i] : 0.0, wpi = pend ? wp[i] : 0.0;
-          double acc = 0.0;
-          int j = s + 1 + wv;
-          for (; j + 3 * XW < K; j += 4 * XW) {
-            double a0 = Aw[(size_t)j * LD + i], a1 = Aw[(size_t)(j + XW) * LD + i];
-            double a2 = Aw[(size_t)(j + 2 * XW) * LD + i], a3 = Aw[(size_t)(j + 3 * XW) * LD + i];
-            if (pend) {
-              a0 = fma(-vp[j], wpi, fma(-wp[j], vpi, a0));
-              a1 = fma(-vp[j + XW], wpi, fma(-wp[j + XW], vpi, a1));
-              a2 = fma(-vp[j + 2 * XW], wpi, fma(-wp[j + 2 * XW], vpi, a2));
-              a3 = fma(-vp[j + 3 * XW], wpi, fma(-wp[j + 3 * XW], vpi, a3));
-              Aw[(size_t)j * LD + i] = a0;
-              Aw[(size_t)(j + XW) * LD + i] = a1;
-              Aw[(size_t)(j + 2 * XW) * LD + i] = a2;
-              Aw[(size_t)(j + 3 * XW) * LD + i] = a3;
-            }
-            acc = fma(a0, vc[j], acc);
-            acc = fma(a1, vc[j + XW], acc);
-            acc = fma(a2, vc[j + 2 * XW], acc);
-            acc = fma(a3, vc[j + 3 * XW], acc);
-          }
-          for (; j < K; j += XW) {
-            double a = Aw[(size_t)j * LD + i];
-            if (pend) {
-              a = fma(-vp[j], wpi, fma(-wp[j], vpi, a));
-              Aw[(size_t)j * LD + i] = a;
-            }
-            acc = fma(a, vc[j], acc);
-          }
-          yp[wv * K + i] = acc;
+      {
+        // the wave's rows j = s + 1 + wv + XW q (q < nrw) x its 64-column chunks, as one stream
+        // of NB-row batches; the next batch's loads are issued before the current batch's
+        // updates are stored (the counter that tracks loads also tracks stores), and a chunk's
+        // column sum goes to yp when its last batch is done
+        constexpr int NB = 8;
+        const int n1 = K - s - 1;
+        const int nrw = n1 > wv ? (n1 - wv + XW - 1) / XW : 0;
+        const int nch = (n1 + 63) / 64;
+        const int nbr = (nrw + NB - 1) / NB;
+        const int tot = nch * nbr;
+        double cur[NB], nxt[NB];
+#pragma unroll
+        for (int u = 0; u < NB; ++u) {
+          const int j = s + 1 + wv + XW * u, i = s + 1 + lane;
+          cur[u] = (tot > 0 && u < nrw && i < K) ? Aw[(size_t)j * LD + i] : 0.0;
         }
+        double acc = 0.0;
+        for (int bi = 0; bi < tot; ++bi) {
+          if (bi + 1 < tot) {
+            const int c = (bi + 1) / nbr, q0 = (bi + 1 - c * nbr) * NB;
+            const int i = s + 1 + 64 * c + lane;
+#pragma unroll
+            for (int u = 0; u < NB; ++u) {
+              const int j = s + 1 + wv + XW * (q0 + u);
+              nxt[u] = (q0 + u < nrw && i < K) ? Aw[(size_t)j * LD + i] : 0.0;
+            }
+          }
+          const int c = bi / nbr, q0 = (bi - c * nbr) * NB;
+          const int i = s + 1 + 64 * c + lane;
+          const bool ci = i < K;
+          const double vpi = (pend && ci) ? vp[i] : 0.0, wpi = (pend && ci) ? wp[i] : 0.0;
+#pragma unroll
+          for (int u = 0; u < NB; ++u) {
+            if (q0 + u < nrw) {
+              const int j = s + 1 + wv + XW * (q0 + u);
+              double a = cur[u];
+              if (pend) {
+                a = fma(-vp[j], wpi, fma(-wp[j], vpi, a));
+                if (ci) Aw[(size_t)j * LD + i] = a;
+              }
+              acc = fma(a, vc[j], acc);
+            }
+          }
+          if (q0 + NB >= nrw) {
+            if (ci) yp[wv * K + i] = acc;
+            acc = 0.0;
+          }
+#pragma unroll
+          for (int u = 0; u < NB; ++u) cur[u] = nxt[u];
+        }
+        if (nrw == 0)
+          for (int i = s + 1 + lane; i < K; i += 64) yp[wv * K + i] = 0.0;
       }
       __syncthreads();
       double dp = 0.0;
@@ -559,14 +583,9 @@ __global__ __launch_bounds__(XT) void eig_xl_kernel(int B, int K, const double* 
       }
       if (tid == 0 && flags) flags[b] = 0;
     }
-    // ---- back-transform Y <- H_0 ... H_{K-3} Y: waves own 32- (K <= 448) or 64-column chunks ----
-    if ((K + 63) / 64 < XW) {
-      for (int c0 = 32 * wv; c0 < K; c0 += 32 * XW)
-        xl_back_wy<2>(Aw, Y, tau, K, LD, c0, yp + 512 * wv, lane);
-    } else {
-      for (int c0 = 64 * wv; c0 < K; c0 += 64 * XW)
-        xl_back_wy<4>(Aw, Y, tau, K, LD, c0, yp + 512 * wv, lane);
-    }
+    // ---- back-transform Y <- H_0 ... H_{K-3} Y: waves own 32-column chunks ----
+    for (int c0 = 32 * wv; c0 < K; c0 += 32 * XW)
+      xl_back_wy<2>(Aw, Y, tau, K, LD, c0, yp + 512 * wv, lane);
     __syncthreads();
     // ---- outputs: lane k owns column k ----
     for (int k = tid; k < K; k += XT) {
@@ -598,16 +617,16 @@ __global__ __launch_bounds__(256) void xl_bias_sum_kernel(const double* __restri
   }
 }
 
-template <bool EIG>
+template <bool EIG, int WPE>
 int xl_prepare() {
-  return (int)hipFuncSetAttribute((const void*)eig_xl_kernel<EIG>,
+  return (int)hipFuncSetAttribute((const void*)eig_xl_kernel<EIG, WPE>,
                                   hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)xl_lds_bytes(XL_MAX_K));
 }
 
 // Persistent grid: as many workgroups as can be resident at once (a slot beyond that would start
 // only after a resident one has finished its whole share of the batch), at most B.
-template <bool EIG>
+template <bool EIG, int WPE>
 int xl_slots(int B, int K) {
   static int cus = 0;
   if (cus == 0) {
@@ -616,9 +635,9 @@ int xl_slots(int B, int K) {
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
       cus = 256;
   }
-  (void)xl_prepare<EIG>();
+  (void)xl_prepare<EIG, WPE>();
   int per = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, eig_xl_kernel<EIG>, XT, xl_lds_bytes(K)) !=
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, eig_xl_kernel<EIG, WPE>, XT, xl_lds_bytes(K)) !=
           hipSuccess || per <= 0)
     per = 1;
   return B < per * cus ? B : per * cus;
@@ -630,9 +649,11 @@ int xl_slots(int B, int K) {
 // Scratch doubles of the XL solvers for a batch of B problems of order K (144 < K <= 1024).
 MFA_API size_t mfa_eigen_xl_ws_doubles(int B, int K) {
   if (B <= 0 || K < 3 || K > XL_MAX_K) return 0;
-  return (size_t)(xl_slots<true>(B, K) > xl_slots<false>(B, K) ? xl_slots<true>(B, K)
-                                                                 : xl_slots<false>(B, K)) *
-         xl_slot_doubles(K);
+  int n = xl_slots<true, 2>(B, K);
+  n = n > xl_slots<false, 2>(B, K) ? n : xl_slots<false, 2>(B, K);
+  n = n > xl_slots<true, 4>(B, K) ? n : xl_slots<true, 4>(B, K);
+  n = n > xl_slots<false, 4>(B, K) ? n : xl_slots<false, 4>(B, K);
+  return (size_t)n * xl_slot_doubles(K);
 }
 
 // Batched eigendecomposition of symmetric [B][K][K] fp64 matrices (3 <= K <= 1024): w [B][K]
@@ -643,10 +664,15 @@ MFA_API int mfa_eigh_xl(const double* A, int B, int K, double tol, double* w, do
                         int* fixed, double* ws, void* stream) {
   if (B <= 0) return 0;
   if (K < 3 || K > XL_MAX_K || ws == nullptr) return (int)hipErrorInvalidValue;
-  if (int e = xl_prepare<true>()) return e;
-  hipLaunchKernelGGL((eig_xl_kernel<true>), dim3(xl_slots<true>(B, K)), dim3(XT), xl_lds_bytes(K),
-                     (hipStream_t)stream, B, K, A, (const double*)nullptr, (const int*)nullptr, 1,
-                     (const double*)nullptr, tol, w, U, fixed, ws);
+#define MFA_XL_EIG(W)                                                                          \
+  {                                                                                            \
+    if (int e = xl_prepare<true, W>()) return e;                                               \
+    hipLaunchKernelGGL((eig_xl_kernel<true, W>), dim3(xl_slots<true, W>(B, K)), dim3(XT),      \
+                       xl_lds_bytes(K), (hipStream_t)stream, B, K, A, (const double*)nullptr,  \
+                       (const int*)nullptr, 1, (const double*)nullptr, tol, w, U, fixed, ws);   \
+  }
+  if (g_xl_wpe == 4) MFA_XL_EIG(4) else MFA_XL_EIG(2)
+#undef MFA_XL_EIG
   return (int)hipGetLastError();
 }
 
@@ -658,12 +684,24 @@ MFA_API int mfa_eigen_bias_accumulate_xl(const double* w, const int* dvalid, int
                                          void* stream) {
   if (D <= 0 || M <= 0) return 0;
   if (K < 3 || K > XL_MAX_K || ws == nullptr || vws == nullptr) return (int)hipErrorInvalidValue;
-  if (int e = xl_prepare<false>()) return e;
   const int B = D * M;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL((eig_xl_kernel<false>), dim3(xl_slots<false>(B, K)), dim3(XT), xl_lds_bytes(K), s,
-                     B, K, (const double*)nullptr, w, dvalid, M, Cz, 0.0, (double*)nullptr, vws,
-                     (int*)nullptr, ws);
+#define MFA_XL_BIAS(W)                                                                         \
+  {                                                                                            \
+    if (int e = xl_prepare<false, W>()) return e;                                              \
+    hipLaunchKernelGGL((eig_xl_kernel<false, W>), dim3(xl_slots<false, W>(B, K)), dim3(XT),    \
+                       xl_lds_bytes(K), s, B, K, (const double*)nullptr, w, dvalid, M, Cz, 0.0, \
+                       (double*)nullptr, vws, (int*)nullptr, ws);                              \
+  }
+  if (g_xl_wpe == 4) MFA_XL_BIAS(4) else MFA_XL_BIAS(2)
+#undef MFA_XL_BIAS
   hipLaunchKernelGGL(xl_bias_sum_kernel, dim3(D), dim3(256), 0, s, vws, K, M, S);
   return (int)hipGetLastError();
+}
+
+// Waves per SIMD of the XL solver for the next calls: 2 (default) or 4.
+MFA_API int mfa_eigen_xl_set_wpe(int w) {
+  if (w != 2 && w != 4) return (int)hipErrorInvalidValue;
+  g_xl_wpe = w;
+  return 0;
 }

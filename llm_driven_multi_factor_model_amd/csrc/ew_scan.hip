@@ -28,14 +28,15 @@ namespace {
 
 using namespace mfa;
 
-constexpr int CH = 32;  // dates per chunk
+constexpr int CH = 32;  // dates per chunk (fewer for wide K: nw_chunk)
 constexpr int G = 8;    // lags per launch group (register state: 1 + 2G fp64 per thread)
 
 struct NwDims {
   int T, K, q;      // series length, factors, total lag count (weights 1 - i/(q+1))
   int i0, i1;       // this launch's lag group [i0, i1), 1-based lags
   double lam;
-  int org;          // first date of the scanned range: chunk c = [org + c CH, org + (c+1) CH)
+  int org;          // first date of the scanned range: chunk c = [org + c ch, org + (c+1) ch)
+  int ch;           // dates per chunk (nw_chunk(K, q): CH unless a chunk's LDS image is too big)
 };
 
 // LDS image of a chunk: F rows [t0 - i1 + 1, t1) and M rows [t0 - i1 + 1, t1), then M rows
@@ -134,7 +135,7 @@ __global__ __launch_bounds__(256) void nw_chunk_sums(const double* __restrict__ 
                                                      double* __restrict__ C) {
   extern __shared__ double Fs[];
   const int c = blockIdx.x;
-  const int t0 = dm.org + c * CH, t1 = min(dm.T, t0 + CH);
+  const int t0 = dm.org + c * dm.ch, t1 = min(dm.T, t0 + dm.ch);
   stage_rows(F, nullptr, nullptr, Fs, nullptr, nullptr, t0, t1, dm, false);
   __syncthreads();
   const int KK = dm.K * dm.K;
@@ -161,15 +162,15 @@ __global__ __launch_bounds__(256) void nw_carry_scan(NwDims dm, int nchunks, dou
   const int ns = nstate(dm);
   const int e = blockIdx.x * blockDim.x + threadIdx.x;  // (m, kk)
   if (e >= ns * KK) return;
-  const double dch = pow(dm.lam, (double)CH);
+  const double dch = pow(dm.lam, (double)dm.ch);
   double carry = Cin ? Cin[e] : 0.0;
   for (int c = 0; c < nchunks; ++c) {
-    const int t0 = dm.org + c * CH;
-    const int len = min(dm.T, t0 + CH) - t0;
+    const int t0 = dm.org + c * dm.ch;
+    const int len = min(dm.T, t0 + dm.ch) - t0;
     double* p = C + (size_t)c * ns * KK + e;
     const double loc = *p;
     *p = carry;
-    carry = fma(len == CH ? dch : pow(dm.lam, (double)len), carry, loc);
+    carry = fma(len == dm.ch ? dch : pow(dm.lam, (double)len), carry, loc);
   }
   if (Ctot) Ctot[e] = carry;
 }
@@ -183,11 +184,11 @@ __global__ __launch_bounds__(256) void nw_emit(const double* __restrict__ F,
                                                int add) {
   extern __shared__ double Fs[];
   const int c = c_first + blockIdx.x;
-  const int t0 = dm.org + c * CH, t1 = min(dm.T, t0 + CH);
+  const int t0 = dm.org + c * dm.ch, t1 = min(dm.T, t0 + dm.ch);
   const int rows = t1 - t0 + dm.i1 - 1;
   double* Ms = Fs + (size_t)rows * dm.K;
   double* M0 = Ms + (size_t)rows * dm.K;
-  double* tab = M0 + (size_t)(dm.i1 - 1) * dm.K;  // [CH][1 + G]
+  double* tab = M0 + (size_t)(dm.i1 - 1) * dm.K;  // [ch][1 + G]
   stage_rows(F, M, Mg, Fs, Ms, M0, t0, t1, dm, true);
   for (int e = threadIdx.x; e < (t1 - t0) * (1 + G); e += blockDim.x) {
     const int du = e / (1 + G), g = e % (1 + G);
@@ -294,8 +295,23 @@ __global__ __launch_bounds__(64) void ew_prefix_mean(const double* __restrict__ 
     }
 }
 
+// LDS doubles of the emit pass's chunk image (the larger of the two passes) at ch dates per
+// chunk and lags up to q
+size_t nw_lds_doubles(int ch, int K, int q) {
+  return (size_t)(2 * (ch + q) + q) * K + (size_t)ch * (1 + G);
+}
+// Dates per chunk: CH, halved (down to 4) while a chunk's LDS image exceeds the CU's 160 KB --
+// a function of (K, q) only, so every shard and rank chunks the same way; K <= ~190 at q = 2
+// keeps CH (bitwise the round-5 scan)
+int nw_chunk(int K, int q) {
+  int ch = CH;
+  while (ch > 4 && nw_lds_doubles(ch, K, q) * sizeof(double) > 160 * 1024) ch >>= 1;
+  return ch;
+}
+
 size_t nw_carry_bytes(int T, int K, int q) {
-  const int nch = (T + CH - 1) / CH;
+  const int ch = nw_chunk(K, q);
+  const int nch = (T + ch - 1) / ch;
   const int g = q < G ? q : G;
   return (size_t)nch * (1 + 2 * g) * K * K * sizeof(double);
 }
@@ -311,8 +327,9 @@ MFA_API size_t mfa_nw_workspace_bytes(int T, int K, int q) {
 
 // Largest lag count the kernels accept for K factors (LDS rows of one chunk).
 MFA_API int mfa_nw_max_lags(int K) {
-  const int rows = (int)((160 * 1024 - CH * (1 + G) * sizeof(double)) / (3 * (size_t)K * sizeof(double)));
-  return rows - CH;
+  int q = 0;
+  while (nw_lds_doubles(4, K, q + 1) * sizeof(double) <= 160 * 1024) ++q;
+  return q;
 }
 
 MFA_API int mfa_nw_series(const double* F, int T, int K, int q, double tau, int t_lo, int t_hi,
@@ -326,21 +343,22 @@ MFA_API int mfa_nw_series(const double* F, int T, int K, int q, double tau, int 
   // emits only its own window [t_lo, t_hi) computes every date bitwise like the one-process
   // run (same chunking and carries); the extra scan is ~0.1 ms at T = 2520
   const int Tn = T;
-  const int nch = (Tn - 1) / CH + 1;
+  const int ch = nw_chunk(K, q);
+  const int nch = (Tn - 1) / ch + 1;
   const int KK = K * K;
   double* C = (double*)ws;
   double* M = (double*)((char*)ws + nw_carry_bytes(Tn, K, q));
   hipLaunchKernelGGL(ew_cumsum_cols, dim3(K), dim3(64), 0, s, F, 0, Tn, K, lam,
                      (const double*)nullptr, M);
-  const int c_first = t_lo / CH;
+  const int c_first = t_lo / ch;
   dim3 blk(256);
   // lag groups [i0, i1): group 0 also carries S0 and writes V; later groups add their lags
   for (int i0 = 1, grp = 0; grp == 0 || i0 <= q; i0 += G, ++grp) {
     const int i1 = std::min(q + 1, i0 + G);
-    NwDims dm{Tn, K, q, i0, i1, lam, 0};
+    NwDims dm{Tn, K, q, i0, i1, lam, 0, ch};
     const int ns = (i0 == 1 ? 1 : 0) + 2 * (i1 - i0);
-    const size_t ldsA = (size_t)(CH + i1 - 1) * K * sizeof(double);
-    const size_t ldsC = ((size_t)(2 * (CH + i1 - 1) + (i1 - 1)) * K + CH * (1 + G)) * sizeof(double);
+    const size_t ldsA = (size_t)(ch + i1 - 1) * K * sizeof(double);
+    const size_t ldsC = ((size_t)(2 * (ch + i1 - 1) + (i1 - 1)) * K + ch * (1 + G)) * sizeof(double);
     hipLaunchKernelGGL(nw_chunk_sums, dim3(nch, (KK + 255) / 256), blk, ldsA, s, F, dm, C);
     hipLaunchKernelGGL(nw_carry_scan, dim3((ns * KK + 255) / 256), blk, 0, s, dm, nch, C,
                        (const double*)nullptr, (double*)nullptr);
@@ -386,7 +404,8 @@ MFA_API int mfa_nw_series_shard(const double* Fsh, const double* Mh, const doubl
   const double lam = pow(0.5, 1.0 / tau);
   const int h = q > 1 ? q : 1;
   const int lo = T0 - h > 0 ? T0 - h : 0;
-  const int nch = (T1 - T0 - 1) / CH + 1;
+  const int ch = nw_chunk(K, q);
+  const int nch = (T1 - T0 - 1) / ch + 1;
   const int KK = K * K;
   const double* Fb = Fsh - (size_t)lo * K;  // indexed by global date (rows >= lo only)
   double* C = (double*)ws;
@@ -408,10 +427,10 @@ MFA_API int mfa_nw_series_shard(const double* Fsh, const double* Mh, const doubl
   size_t off = 0;
   for (int i0 = 1, grp = 0; grp == 0 || i0 <= q; i0 += G, ++grp) {
     const int i1 = std::min(q + 1, i0 + G);
-    NwDims dm{T1, K, q, i0, i1, lam, T0};
+    NwDims dm{T1, K, q, i0, i1, lam, T0, ch};
     const int ns = (i0 == 1 ? 1 : 0) + 2 * (i1 - i0);
-    const size_t ldsA = (size_t)(CH + i1 - 1) * K * sizeof(double);
-    const size_t ldsC = ((size_t)(2 * (CH + i1 - 1) + (i1 - 1)) * K + CH * (1 + G)) * sizeof(double);
+    const size_t ldsA = (size_t)(ch + i1 - 1) * K * sizeof(double);
+    const size_t ldsC = ((size_t)(2 * (ch + i1 - 1) + (i1 - 1)) * K + ch * (1 + G)) * sizeof(double);
     hipLaunchKernelGGL(nw_chunk_sums, dim3(nch, (KK + 255) / 256), blk, ldsA, s, Fb, dm, C);
     if (Ctot)  // own contribution: scan from zero, keep the total, then rescan from Cin below
       hipLaunchKernelGGL(nw_carry_scan, dim3((ns * KK + 255) / 256), blk, 0, s, dm, nch, C,

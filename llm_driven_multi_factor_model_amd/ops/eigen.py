@@ -58,6 +58,7 @@ _native.register("mfa_eigh_xl", [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_v
 _native.register("mfa_eigen_bias_accumulate_xl", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                                   C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                                   C.c_void_p])
+_native.register("mfa_eigen_xl_set_wpe", [C.c_int])
 _native.register("mfa_mc_cov_xl_ws_doubles", [C.c_int, C.c_int, C.c_int])
 _native.register("mfa_mc_cov_xl", [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_void_p,
                                    C.c_void_p, C.c_void_p])
@@ -259,6 +260,13 @@ def _eigh_xl(Ab, shp):
     global LAST_EIGH_FLAGS
     LAST_EIGH_FLAGS = flags
     return w.reshape(shp[:-1]), U.reshape(shp)
+
+
+def set_xl_waves_per_simd(w: int) -> None:
+    """XL solver occupancy (process-wide): 2 = one 8-wave workgroup per CU (default), 4 = two
+    workgroups per CU in 128 VGPRs."""
+    if _native.lib().mfa_eigen_xl_set_wpe(int(w)) != 0:
+        raise ValueError(f"XL waves per SIMD must be 2 or 4, got {w!r}")
 
 
 def _eigh_reference(Ab, shp):

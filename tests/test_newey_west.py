@@ -66,7 +66,10 @@ def test_hip_scan_matches_oracle(cuda, T, K, q, tau, lo, hi):
 @pytest.mark.gpu
 @pytest.mark.parametrize("T,K,q,tau,lo,hi", [(600, 42, 5, 84.0, 0, 600), (1000, 42, 8, 84.0, 100, 1000),
                                              (400, 12, 10, 42.0, 0, 400), (300, 9, 17, 60.0, 250, 300),
-                                             (200, 6, 40, 90.0, 0, 200)])
+                                             (200, 6, 40, 90.0, 0, 200),
+                                             # wide K: the chunk shrinks to 16 / 8 dates so its LDS
+                                             # image fits (nw_chunk), any window
+                                             (500, 200, 2, 252.0, 0, 500), (400, 273, 5, 90.0, 150, 400)])
 def test_hip_scan_any_lag_count(cuda, T, K, q, tau, lo, hi):
     """q beyond one register lag group (8): the launch loops over lag groups and accumulates."""
     F = _series(T, K, seed=q)
