@@ -38,10 +38,13 @@ using namespace mfa;
 constexpr int XW = 8;        // waves per workgroup
 constexpr int XT = XW * 64;  // threads per workgroup
 constexpr int XL_MAX_K = 1024;
-// Waves per SIMD the solver is compiled for (both instantiated, mfa_eigen_xl_set_wpe): 2 = one
-// 8-wave workgroup per CU without spills (~200 VGPRs), 4 = two workgroups per CU in 128 VGPRs
-// (some scratch spills) -- more problems in flight to cover the tridiagonalisation's memory trips.
-int g_xl_wpe = 2;
+// Waves per SIMD the solver is compiled for (both instantiated, bitwise the same results;
+// mfa_eigen_xl_set_wpe): 2 = one 8-wave workgroup per CU without spills (~200 VGPRs), 4 = two
+// workgroups per CU in 128 VGPRs (some scratch spills): more problems in flight to cover the
+// tridiagonalisation's memory round trips.  0 (default) = 4 for the bias batches (25k problems:
+// 193 -> 137 ms at K = 150, 351 -> 280 ms at K = 200), 2 for the eigh (a few hundred matrices:
+// 2.48 -> 2.21 ms at K = 150; profiles/r06/xl/xl_bench.log).
+int g_xl_wpe = 0;
 
 __device__ __forceinline__ double xl_ext(double v, double* red, bool mx) {
   v = mx ? wave_max(v) : wave_min(v);
@@ -269,6 +272,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
                                                     const double* __restrict__ D0,
                                                     const int* __restrict__ dvalid, int M,
                                                     const double* __restrict__ Cz, double tol,
+                                                    double psd_tol,
                                                     double* __restrict__ wout,
                                                     double* __restrict__ out,
                                                     int* __restrict__ flags,
@@ -549,7 +553,12 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         }
       }
       err = xl_ext(err != err ? INFINITY : err, red, true);
-      if (!(err <= tol)) {
+      // psd_tol >= 0 (the eigen adjustment): a matrix with an eigenvalue below -psd_tol lambda_max
+      // is an invalid date whose eigenvectors nobody reads -- flagged 2, not re-solved
+      const bool need = psd_tol < 0.0 || lam[K - 1] >= -psd_tol * fabs(lam[0]);
+      if (!(err <= tol) && !need) {
+        if (tid == 0 && flags) flags[b] = 2;
+      } else if (!(err <= tol)) {
         const double* A = Ain + (size_t)b * K * K;
         for (int e = tid; e < K * K; e += XT) {
           const int i = e / K, j = e - i * K;
@@ -580,8 +589,9 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         }
         if (tid == 0 && flags) flags[b] = 1;
         continue;
+      } else if (tid == 0 && flags) {
+        flags[b] = 0;
       }
-      if (tid == 0 && flags) flags[b] = 0;
     }
     // ---- back-transform Y <- H_0 ... H_{K-3} Y: waves own 32-column chunks ----
     for (int c0 = 32 * wv; c0 < K; c0 += 32 * XW)
@@ -659,9 +669,11 @@ MFA_API size_t mfa_eigen_xl_ws_doubles(int B, int K) {
 // Batched eigendecomposition of symmetric [B][K][K] fp64 matrices (3 <= K <= 1024): w [B][K]
 // descending, U [B][K][K] with U[:, k] = eigenvector k, NaN for non-finite inputs; a matrix
 // whose tridiagonal eigenvectors miss max |Y^T Y - I| <= tol is re-solved by the Jacobi
-// (fixed[b] = 1; nullable).  ws: mfa_eigen_xl_ws_doubles(B, K).
-MFA_API int mfa_eigh_xl(const double* A, int B, int K, double tol, double* w, double* U,
-                        int* fixed, double* ws, void* stream) {
+// (fixed[b] = 1; nullable) -- with psd_tol >= 0 only if its smallest eigenvalue is >= -psd_tol
+// lambda_max (else fixed[b] = 2: an invalid date of the eigen adjustment; psd_tol < 0 = always).
+// ws: mfa_eigen_xl_ws_doubles(B, K).
+MFA_API int mfa_eigh_xl(const double* A, int B, int K, double tol, double psd_tol, double* w,
+                        double* U, int* fixed, double* ws, void* stream) {
   if (B <= 0) return 0;
   if (K < 3 || K > XL_MAX_K || ws == nullptr) return (int)hipErrorInvalidValue;
 #define MFA_XL_EIG(W)                                                                          \
@@ -669,9 +681,9 @@ MFA_API int mfa_eigh_xl(const double* A, int B, int K, double tol, double* w, do
     if (int e = xl_prepare<true, W>()) return e;                                               \
     hipLaunchKernelGGL((eig_xl_kernel<true, W>), dim3(xl_slots<true, W>(B, K)), dim3(XT),      \
                        xl_lds_bytes(K), (hipStream_t)stream, B, K, A, (const double*)nullptr,  \
-                       (const int*)nullptr, 1, (const double*)nullptr, tol, w, U, fixed, ws);   \
+                       (const int*)nullptr, 1, (const double*)nullptr, tol, psd_tol, w, U, fixed, ws);   \
   }
-  if (g_xl_wpe == 4) MFA_XL_EIG(4) else MFA_XL_EIG(2)
+  if (g_xl_wpe == 4) MFA_XL_EIG(4) else MFA_XL_EIG(2)  // auto: 2
 #undef MFA_XL_EIG
   return (int)hipGetLastError();
 }
@@ -690,18 +702,18 @@ MFA_API int mfa_eigen_bias_accumulate_xl(const double* w, const int* dvalid, int
   {                                                                                            \
     if (int e = xl_prepare<false, W>()) return e;                                              \
     hipLaunchKernelGGL((eig_xl_kernel<false, W>), dim3(xl_slots<false, W>(B, K)), dim3(XT),    \
-                       xl_lds_bytes(K), s, B, K, (const double*)nullptr, w, dvalid, M, Cz, 0.0, \
+                       xl_lds_bytes(K), s, B, K, (const double*)nullptr, w, dvalid, M, Cz, 0.0, -1.0,\
                        (double*)nullptr, vws, (int*)nullptr, ws);                              \
   }
-  if (g_xl_wpe == 4) MFA_XL_BIAS(4) else MFA_XL_BIAS(2)
+  if (g_xl_wpe == 2) MFA_XL_BIAS(2) else MFA_XL_BIAS(4)  // auto: 4
 #undef MFA_XL_BIAS
   hipLaunchKernelGGL(xl_bias_sum_kernel, dim3(D), dim3(256), 0, s, vws, K, M, S);
   return (int)hipGetLastError();
 }
 
-// Waves per SIMD of the XL solver for the next calls: 2 (default) or 4.
+// Waves per SIMD of the XL solver for the next calls: 0 (auto, default), 2 or 4.
 MFA_API int mfa_eigen_xl_set_wpe(int w) {
-  if (w != 2 && w != 4) return (int)hipErrorInvalidValue;
+  if (w != 0 && w != 2 && w != 4) return (int)hipErrorInvalidValue;
   g_xl_wpe = w;
   return 0;
 }

@@ -53,8 +53,8 @@ _native.register("mfa_mc_cov_wide", [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uin
 _native.register("mfa_mc_cov_wide_ws_doubles", [C.c_int, C.c_int, C.c_int])
 _native.register("mfa_eigen_set_date_origin", [C.c_int])
 _native.register("mfa_eigen_xl_ws_doubles", [C.c_int, C.c_int])
-_native.register("mfa_eigh_xl", [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p, C.c_void_p,
-                                 C.c_void_p, C.c_void_p, C.c_void_p])
+_native.register("mfa_eigh_xl", [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_double, C.c_void_p,
+                                 C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p])
 _native.register("mfa_eigen_bias_accumulate_xl", [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int,
                                                   C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                                   C.c_void_p])
@@ -183,7 +183,8 @@ def using_bias_solver(name: str):
 LAST_EIGH_FLAGS: torch.Tensor | None = None
 
 
-def eigh(A: torch.Tensor, max_sweeps: int = MAX_SWEEPS, tol: float = TOL):
+def eigh(A: torch.Tensor, max_sweeps: int = MAX_SWEEPS, tol: float = TOL, *,
+         resolve_psd_tol: float | None = None):
     """Batched symmetric eigendecomposition, eigenvalues DESCENDING.
 
     ``A`` [..., K, K] float64 (any K; K > 64 on the GPU goes through :func:`_eigh_wide`).  Returns ``(w [..., K], U [..., K, K])``
@@ -197,7 +198,7 @@ def eigh(A: torch.Tensor, max_sweeps: int = MAX_SWEEPS, tol: float = TOL):
     if not A.is_cuda:
         return _eigh_reference(Ab, shp)
     if K > WIDE_K:
-        return _eigh_wide(Ab, shp)
+        return _eigh_wide(Ab, shp, resolve_psd_tol)
     B = Ab.shape[0]
     w = torch.empty(B, K, dtype=torch.float64, device=A.device)
     U = torch.empty(B, K, K, dtype=torch.float64, device=A.device)
@@ -211,7 +212,7 @@ def eigh(A: torch.Tensor, max_sweeps: int = MAX_SWEEPS, tol: float = TOL):
     return w.reshape(shp[:-1]), U.reshape(shp)
 
 
-def _eigh_wide(Ab, shp):
+def _eigh_wide(Ab, shp, resolve_psd_tol=None):
     """K > 64 on the device: for K <= WIDE_HIP_MAX_K the multi-wave HIP solver
     (``mfa_eigh_wide_fix``: matrices whose eigenvectors come out non-orthogonal to ORTHO_TOL,
     i.e. clustered spectra, or NaN for a finite input, are re-solved on the device by a Jacobi),
@@ -228,7 +229,7 @@ def _eigh_wide(Ab, shp):
                      _native.ptr(U), _native.ptr(ws), None, _native.stream(Ab.device))
         return w.reshape(shp[:-1]), U.reshape(shp)
     if _wide_solver == "hip" and K <= XL_MAX_K:
-        return _eigh_xl(Ab, shp)
+        return _eigh_xl(Ab, shp, resolve_psd_tol)
     w = torch.full((B, K), float("nan"), dtype=torch.float64, device=Ab.device)
     U = torch.full((B, K, K), float("nan"), dtype=torch.float64, device=Ab.device)
     ok = torch.isfinite(Ab).all(-1).all(-1)
@@ -243,7 +244,7 @@ def _eigh_wide(Ab, shp):
     return w.reshape(shp[:-1]), U.reshape(shp)
 
 
-def _eigh_xl(Ab, shp):
+def _eigh_xl(Ab, shp, resolve_psd_tol=None):
     """WIDE_HIP_MAX_K < K <= XL_MAX_K: ``mfa_eigh_xl`` (csrc/eigen_xl.hip) -- Householder with the
     working matrix in a per-workgroup global slot, bisection eigenvalues, twisted-factorisation
     eigenvectors, an MFMA orthogonality check and an in-slot Jacobi re-solve of the matrices that
@@ -255,7 +256,8 @@ def _eigh_xl(Ab, shp):
     flags = torch.empty(B, dtype=torch.int32, device=dev)
     ws = torch.empty(max(1, _native.query("mfa_eigen_xl_ws_doubles", B, K)), dtype=torch.float64,
                      device=dev)
-    _native.call("mfa_eigh_xl", _native.ptr(Ab), B, K, ORTHO_TOL, _native.ptr(w), _native.ptr(U),
+    psd = -1.0 if resolve_psd_tol is None else float(resolve_psd_tol)
+    _native.call("mfa_eigh_xl", _native.ptr(Ab), B, K, ORTHO_TOL, psd, _native.ptr(w), _native.ptr(U),
                  _native.ptr(flags), _native.ptr(ws), _native.stream(dev))
     global LAST_EIGH_FLAGS
     LAST_EIGH_FLAGS = flags
@@ -263,10 +265,11 @@ def _eigh_xl(Ab, shp):
 
 
 def set_xl_waves_per_simd(w: int) -> None:
-    """XL solver occupancy (process-wide): 2 = one 8-wave workgroup per CU (default), 4 = two
-    workgroups per CU in 128 VGPRs."""
+    """XL solver occupancy (process-wide; bitwise the same results): 2 = one 8-wave workgroup per
+    CU, 4 = two workgroups per CU in 128 VGPRs, 0 = auto (default: 4 for the bias batches, 2 for
+    the eigh)."""
     if _native.lib().mfa_eigen_xl_set_wpe(int(w)) != 0:
-        raise ValueError(f"XL waves per SIMD must be 2 or 4, got {w!r}")
+        raise ValueError(f"XL waves per SIMD must be 0, 2 or 4, got {w!r}")
 
 
 def _eigh_reference(Ab, shp):
@@ -481,7 +484,7 @@ def eigen_risk_adjust_sharded(F0: torch.Tensor, *, M: int = 10_000, scale_coef: 
     D, K, _ = F0.shape
     T_sim = D if T_sim is None else T_sim
     dev = F0.device
-    w, U = eigh(F0)
+    w, U = eigh(F0, resolve_psd_tol=psd_tol)
     valid = torch.isfinite(w).all(-1) & (w.min(-1).values >= -psd_tol * w.abs().max(-1).values.clamp_min(0))
     w = torch.where(valid[:, None], w.clamp_min(0.0), w).contiguous()
     rank, world = (ctx.rank, ctx.world) if ctx.enabled else (0, 1)
@@ -555,7 +558,7 @@ def eigen_risk_adjust(F0: torch.Tensor, *, M: int = 100, scale_coef: float = 1.4
     D, K, _ = F0.shape
     T_sim = D if T_sim is None else T_sim
     dev = F0.device
-    w, U = eigh(F0)
+    w, U = eigh(F0, resolve_psd_tol=psd_tol)
     valid = torch.isfinite(w).all(-1) & (w.min(-1).values >= -psd_tol * w.abs().max(-1).values.clamp_min(0))
     w = torch.where(valid[:, None], w.clamp_min(0.0), w)
     if Cz is None:

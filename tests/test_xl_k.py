@@ -163,7 +163,7 @@ def test_xl_occupancy_variants_bitwise(cuda):
             valid = torch.isfinite(ww).all(-1)
             out.append((ww, U, eigen._bias_sum_xl(ww.clamp_min(0.0).contiguous(), valid, Cz)))
     finally:
-        eigen.set_xl_waves_per_simd(2)
+        eigen.set_xl_waves_per_simd(0)
     for a, b in zip(out[0], out[1]):
         assert torch.equal(a, b)
 
@@ -186,6 +186,6 @@ def test_xl_bias_many_problems_per_slot(cuda, wpe):
         eigen.set_xl_waves_per_simd(wpe)
         S = eigen._bias_sum_xl(w.to(cuda), valid.to(cuda), Cz).cpu()
     finally:
-        eigen.set_xl_waves_per_simd(2)
+        eigen.set_xl_waves_per_simd(0)
     ref = eigen._bias_sum_reference(w, valid, Cz.cpu())
     torch.testing.assert_close(S, ref, rtol=1e-9, atol=1e-12, equal_nan=True)

@@ -29,6 +29,8 @@ ap.add_argument("--reps", type=int, default=2)
 ap.add_argument("--P", type=int, default=31)
 ap.add_argument("--Q", type=int, default=10)
 ap.add_argument("--bias-mode", type=int, default=None, help="mfa_eigen_set_bias_mode (A/B)")
+ap.add_argument("--nw-half-life", type=float, default=None,
+                help="wide K: a long half-life keeps the Newey-West covariances positive definite")
 a = ap.parse_args()
 if a.make:
     p = synthetic_panel(a.dates, a.stocks, a.P, a.Q, seed=3, missing_frac=0.01, dtype=torch.float64)
@@ -42,7 +44,8 @@ p = RiskPanel(styles=d["styles"], cap=d["cap"], ret=d["ret"], ind=d["ind"], P=ma
               dates=d["dates"].numpy().astype("datetime64[ns]"),
               stocks=np.array([f"{i:06d}.SZ" for i in range(d["cap"].shape[1])], dtype=object)
               ).to("cuda:0")
-cfg = preset("reference")
+cfg = preset("reference") if a.nw_half_life is None else \
+    preset("reference", nw_half_life=a.nw_half_life, eigen_sim_length=2 * (1 + p.P + p.Q))
 if a.bias_mode is not None:
     from llm_driven_multi_factor_model_amd import _native
     assert _native.lib().mfa_eigen_set_bias_mode(a.bias_mode) == 0, "bias mode not in this library"
@@ -53,6 +56,9 @@ for rep in range(a.reps + 1):
     m.run()
     torch.cuda.synchronize()
     tot = (time.perf_counter() - t0) * 1e3
+from llm_driven_multi_factor_model_amd.ops import eigen  # noqa: E402
+fl = eigen.LAST_EIGH_FLAGS
 print(json.dumps({"K": 1 + p.P + p.Q, "dates": p.D, "bias_mode": a.bias_mode,
+                  "eigh_flags": {int(v): int((fl == v).sum()) for v in fl.unique()} if fl is not None else None,
                   "total_ms": round(tot, 3),
                   "stage_ms": {k: round(v, 3) for k, v in m.times.ms.items()}}))
