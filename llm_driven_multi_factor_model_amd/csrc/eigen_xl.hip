@@ -9,11 +9,12 @@
 // resident while the workgroup works on it) and only vectors sit in LDS:
 //   * one 8-wave workgroup per problem, persistent over the batch (grid = slots, problem
 //     b = blockIdx.x + q gridDim.x): no host synchronisation and no vendor library;
-//   * Householder tridiagonalisation with the rank-2 update of step s fused into the
-//     matrix-vector product of step s + 1: one read + one write of the trailing matrix per step.
-//     Waves own rows and lanes own 64-column chunks, so every access is a coalesced row segment,
-//     and by symmetry the product y = A v is a column sum: each lane accumulates its own column,
-//     the 8 wave partials meet in LDS in wave order (no cross-lane reduction);
+//   * Householder tridiagonalisation on the lower triangle with the rank-2 update of step s fused
+//     into the matrix-vector product of step s + 1: one read + one write of the trailing
+//     triangle per step.  Waves own rows and lanes own 64-column chunks, so every access is a
+//     coalesced row segment; by symmetry y = A v is a column sum over the rows below (each lane
+//     its own column, the 8 wave partials meet in LDS in wave order) plus a row sum left of the
+//     diagonal (one wave total per row);
 //   * eigenvalues by bisection on the division-free Sturm recurrence (tridiag.h's determinant
 //     form, count only), one lane per eigenvalue, the tridiagonal scaled to unit norm and every
 //     eigenvalue resolved to LAPACK's eps ||T||;
@@ -53,6 +54,18 @@ __device__ __forceinline__ double xl_ext(double v, double* red, bool mx) {
   __syncthreads();
   double s = red[0];
   for (int w = 1; w < XW; ++w) s = mx ? fmax(s, red[w]) : fmin(s, red[w]);
+  return s;
+}
+
+// Block sum in wave order WITHOUT the leading barrier of common.h's block_sum: for call sites
+// where a barrier already separates this write of red[0..XW) from the previous reads of it.
+__device__ __forceinline__ double xl_sum_nb(double v, double* red) {
+  v = wave_total(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double s = red[0];
+#pragma unroll
+  for (int w = 1; w < XW; ++w) s += red[w];
   return s;
 }
 
@@ -98,7 +111,7 @@ __host__ __device__ constexpr size_t xl_slot_doubles(int K) {
 // wave partials of the tridiagonalisation [XW][K], reused by the back-transform (512 doubles of
 // G / T per wave) and the Jacobi re-solve (round-robin order, rotations)
 __host__ __device__ constexpr int xl_yp(int K) { return XW * K > 512 * XW ? XW * K : 512 * XW; }
-constexpr size_t xl_lds_bytes(int K) { return (9 * (size_t)K + xl_yp(K) + 16) * sizeof(double); }
+constexpr size_t xl_lds_bytes(int K) { return (10 * (size_t)K + xl_yp(K) + 16) * sizeof(double); }
 
 // Cyclic round-robin Jacobi of the symmetric S (global, row stride LD) with V <- V J (V starts
 // at I): the eigh re-solve of a matrix whose tridiagonal eigenvectors failed the orthogonality
@@ -288,7 +301,8 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   double* va = dd + K;
   double* vb = va + K;
   double* wp = vb + K;
-  double* yp = wp + K;                           // [XW][K] wave partials (xl_yp doubles)
+  double* yr = wp + K;                           // row parts of y = A v (lower triangle)
+  double* yp = yr + K;                           // [XW][K] column parts per wave (xl_yp doubles)
   double* red = yp + xl_yp(K);
   double* Aw = scratch + (size_t)blockIdx.x * xl_slot_doubles(K);
   double* Y = Aw + (size_t)K * LD;
@@ -303,7 +317,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         const int i = e / K, j = e - i * K;
         const double a = 0.5 * (A[e] + A[(size_t)j * K + i]);
         fin = fin && __builtin_isfinite(a);
-        Aw[(size_t)i * LD + j] = a;
+        if (j <= i) Aw[(size_t)i * LD + j] = a;  // the lower triangle is the working matrix
       }
     } else {
       const int d = b / M, m = b - d * M;
@@ -317,7 +331,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       const double* C = Cz + (size_t)m * K * K;
       for (int e = tid; e < K * K; e += XT) {
         const int i = e / K, j = e - i * K;
-        Aw[(size_t)i * LD + j] = lam[i] * C[e] * lam[j];
+        if (j <= i) Aw[(size_t)i * LD + j] = lam[i] * C[e] * lam[j];
       }
     }
     if (block_sum(fin ? 0.0 : 1.0, red) != 0.0) {
@@ -330,14 +344,15 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       }
       continue;
     }
+    __syncthreads();  // the finiteness sum's reads of red precede step 0's writes (xl_sum_nb)
     // ---- Householder tridiagonalisation, update of step s fused into the product of s + 1 ----
     double* vp = va;  // v of step s - 1 (pending update with wp)
     double* vc = vb;  // v of step s
     for (int s = 0; s + 2 < K; ++s) {
       const bool pend = s > 0;
       double sg = 0.0;
-      for (int j = s + tid; j < K; j += XT) {  // row s, final after the pending update
-        double a = Aw[(size_t)s * LD + j];
+      for (int j = s + tid; j < K; j += XT) {  // column s, final after the pending update
+        double a = Aw[(size_t)j * LD + s];
         if (pend) a = fma(-vp[s], wp[j], fma(-wp[s], vp[j], a));
         if (j == s) {
           tb[s].x = a;
@@ -347,7 +362,8 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
           if (j >= s + 2) sg = fma(a, a, sg);  // waves may still be reading
         }
       }
-      const double sigma = block_sum(sg, red);
+      // the previous step's last barrier follows its reads of red
+      const double sigma = xl_sum_nb(sg, red);
       const double alpha = red[XW + 1];
       double ts = 0.0, beta = alpha, scal = 0.0;
       if (sigma != 0.0) {
@@ -367,69 +383,77 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       }
       __syncthreads();
       {
-        // the wave's rows j = s + 1 + wv + XW q (q < nrw) x its 64-column chunks, as one stream
-        // of NB-row batches; the next batch's loads are issued before the current batch's
-        // updates are stored (the counter that tracks loads also tracks stores), and a chunk's
-        // column sum goes to yp when its last batch is done
-        constexpr int NB = 8;
+        // Lower triangle only (half the traffic of the full square): the wave's rows
+        // j = s + 1 + wv + XW q (q < nrw), columns s + 1 <= i <= j in batches of NC 64-column
+        // chunks, streamed with the next batch's loads issued before the current batch's
+        // updates are stored.  By symmetry y_i = sum_{j >= i} A_ji v_j (column part: lane i,
+        // this wave's partial in yp[wv][i], wave-private) + sum_{i' < i} A_ii' v_i' (row part:
+        // a wave total per row j, yr[j]).
+        constexpr int NC = 4;
         const int n1 = K - s - 1;
         const int nrw = n1 > wv ? (n1 - wv + XW - 1) / XW : 0;
-        const int nch = (n1 + 63) / 64;
-        const int nbr = (nrw + NB - 1) / NB;
-        const int tot = nch * nbr;
-        double cur[NB], nxt[NB];
+        double* ypw = yp + wv * K;
+        for (int i = s + 1 + lane; i < K; i += 64) ypw[i] = 0.0;
+        double cur[NC], nxt[NC];
+        int q = 0, bt = 0;
 #pragma unroll
-        for (int u = 0; u < NB; ++u) {
-          const int j = s + 1 + wv + XW * u, i = s + 1 + lane;
-          cur[u] = (tot > 0 && u < nrw && i < K) ? Aw[(size_t)j * LD + i] : 0.0;
+        for (int u = 0; u < NC; ++u) {
+          const int j = s + 1 + wv, i = s + 1 + 64 * u + lane;
+          cur[u] = (nrw > 0 && i <= j) ? Aw[(size_t)j * LD + i] : 0.0;
         }
-        double acc = 0.0;
-        for (int bi = 0; bi < tot; ++bi) {
-          if (bi + 1 < tot) {
-            const int c = (bi + 1) / nbr, q0 = (bi + 1 - c * nbr) * NB;
-            const int i = s + 1 + 64 * c + lane;
+        double rsum = 0.0;
+        while (q < nrw) {
+          const int j = s + 1 + wv + XW * q;
+          const int nbt = (j - s - 1) / (64 * NC) + 1;
+          int qn = q, bn = bt + 1;
+          if (bn >= nbt) {
+            qn = q + 1;
+            bn = 0;
+          }
+          if (qn < nrw) {
+            const int jn = s + 1 + wv + XW * qn;
 #pragma unroll
-            for (int u = 0; u < NB; ++u) {
-              const int j = s + 1 + wv + XW * (q0 + u);
-              nxt[u] = (q0 + u < nrw && i < K) ? Aw[(size_t)j * LD + i] : 0.0;
+            for (int u = 0; u < NC; ++u) {
+              const int i = s + 1 + 64 * (NC * bn + u) + lane;
+              nxt[u] = i <= jn ? Aw[(size_t)jn * LD + i] : 0.0;
             }
           }
-          const int c = bi / nbr, q0 = (bi - c * nbr) * NB;
-          const int i = s + 1 + 64 * c + lane;
-          const bool ci = i < K;
-          const double vpi = (pend && ci) ? vp[i] : 0.0, wpi = (pend && ci) ? wp[i] : 0.0;
+          const double vj = vc[j], vpj = pend ? vp[j] : 0.0, wpj = pend ? wp[j] : 0.0;
 #pragma unroll
-          for (int u = 0; u < NB; ++u) {
-            if (q0 + u < nrw) {
-              const int j = s + 1 + wv + XW * (q0 + u);
-              double a = cur[u];
+          for (int u = 0; u < NC; ++u) {
+            const int i = s + 1 + 64 * (NC * bt + u) + lane;
+            if (i <= j) {
+              double x = cur[u];
               if (pend) {
-                a = fma(-vp[j], wpi, fma(-wp[j], vpi, a));
-                if (ci) Aw[(size_t)j * LD + i] = a;
+                x = fma(-vpj, wp[i], fma(-wpj, vp[i], x));
+                Aw[(size_t)j * LD + i] = x;
               }
-              acc = fma(a, vc[j], acc);
+              ypw[i] = fma(x, vj, ypw[i]);
+              if (i < j) rsum = fma(x, vc[i], rsum);
             }
           }
-          if (q0 + NB >= nrw) {
-            if (ci) yp[wv * K + i] = acc;
-            acc = 0.0;
+          if (bn == 0) {  // row j done: its row part
+            const double t = wave_total(rsum);
+            if (lane == 0) yr[j] = t;
+            rsum = 0.0;
           }
 #pragma unroll
-          for (int u = 0; u < NB; ++u) cur[u] = nxt[u];
+          for (int u = 0; u < NC; ++u) cur[u] = nxt[u];
+          q = qn;
+          bt = bn;
         }
-        if (nrw == 0)
-          for (int i = s + 1 + lane; i < K; i += 64) yp[wv * K + i] = 0.0;
       }
       __syncthreads();
       double dp = 0.0;
       for (int i = s + 1 + tid; i < K; i += XT) {
-        double y = yp[i];
-        for (int w = 1; w < XW; ++w) y += yp[w * K + i];
+        double y = yr[i];
+        for (int w = 0; w < XW; ++w) y += yp[w * K + i];
         const double p = ts * y;
         wp[i] = p;
         dp = fma(p, vc[i], dp);
       }
-      const double hc = 0.5 * ts * block_sum(dp, red);
+      // red was last read before the barrier that follows the v broadcast
+      const double hc = 0.5 * ts * xl_sum_nb(dp, red);
       for (int i = s + 1 + tid; i < K; i += XT) wp[i] = fma(-hc, vc[i], wp[i]);
       __syncthreads();
       double* t = vp;
@@ -438,7 +462,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     }
     if (tid == 0) {  // the last 2 x 2 block with the pending update of step K - 3
       const int p = K - 2, q = K - 1;
-      double a00 = Aw[(size_t)p * LD + p], a01 = Aw[(size_t)p * LD + q], a11 = Aw[(size_t)q * LD + q];
+      double a00 = Aw[(size_t)p * LD + p], a01 = Aw[(size_t)q * LD + p], a11 = Aw[(size_t)q * LD + q];
       if (K >= 3) {
         a00 -= 2.0 * vp[p] * wp[p];
         a01 -= vp[p] * wp[q] + wp[p] * vp[q];
