@@ -277,6 +277,61 @@ __device__ void xl_back_wy(const double* __restrict__ Aw, double* __restrict__ Y
   }
 }
 
+// max |U^T U - I| of the K columns of U (row stride LD) on the fp64 matrix cores: the
+// KT (KT + 1) / 2 upper 16 x 16 tiles of U^T U dealt round-robin to the waves; NaN -> +inf.
+__device__ double xl_ortho_err(const double* U, int K, int LD, double* red) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int KT = (K + 15) / 16, NT = KT * (KT + 1) / 2;
+  double err = 0.0;
+  for (int t = wv; t < NT; t += XW) {
+    int ti = 0, tt = t;
+    while (tt >= KT - ti) { tt -= KT - ti; ++ti; }
+    const int tj = ti + tt;
+    const int ca = 16 * ti + (lane & 15), cb = 16 * tj + (lane & 15);
+    f64x4g acc = f64x4g{0.0, 0.0, 0.0, 0.0};
+    for (int r0 = 0; r0 < K; r0 += 4) {
+      const int r = r0 + (lane >> 4);
+      const double a = (r < K && ca < K) ? U[(size_t)r * LD + ca] : 0.0;
+      const double c = (r < K && cb < K) ? U[(size_t)r * LD + cb] : 0.0;
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, c, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int i = 16 * ti + (lane >> 4) + 4 * e, j = 16 * tj + (lane & 15);
+      if (i < K && j < K) {
+        const double g = fabs(acc[e] - (i == j ? 1.0 : 0.0));
+        err = (g > err || g != g) ? g : err;
+      }
+    }
+  }
+  return xl_ext(err != err ? INFINITY : err, red, true);
+}
+
+// C = op(A) B for K x K operands (op(A) = A^T if TA), 16 x 16 output tiles dealt to the waves,
+// fp64 matrix cores; leading dimensions lda / ldb / ldc.  Caller brackets with barriers.
+template <bool TA>
+__device__ void xl_mm(const double* A, int lda, const double* B, int ldb, double* C, int ldc,
+                      int K) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, hi = lane >> 4, lo = lane & 15;
+  const int KT = (K + 15) / 16;
+  for (int t = wv; t < KT * KT; t += XW) {
+    const int ti = t / KT, tj = t - ti * KT;
+    const int i = 16 * ti + lo, j = 16 * tj + lo;
+    f64x4g acc = f64x4g{0.0, 0.0, 0.0, 0.0};
+    for (int k0 = 0; k0 < K; k0 += 4) {
+      const int k = k0 + hi;
+      const double a = (i < K && k < K) ? (TA ? A[(size_t)k * lda + i] : A[(size_t)i * lda + k]) : 0.0;
+      const double bb = (k < K && j < K) ? B[(size_t)k * ldb + j] : 0.0;
+      acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bb, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int r = 16 * ti + hi + 4 * e;
+      if (r < K && j < K) C[(size_t)r * ldc + j] = acc[e];
+    }
+  }
+}
+
 // EIG: problem b = matrix Ain[b] -> w[b] (descending), U[b] (U[:, k] = eigenvector k), flags[b]
 // (1 = re-solved by the Jacobi; nullable).  !EIG: problem b = (date d = b / M, sim m = b % M),
 // A = S C_z[m] S with S = diag(sqrt D0[d]) -> v[b][k] = sum_i D0[d][i] V[i][k]^2 / Lambda[k].
@@ -553,41 +608,54 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     __syncthreads();
     // ---- eigh: orthogonality of the tridiagonal eigenvectors; Jacobi re-solve on failure ----
     if (EIG) {
-      const int KT = (K + 15) / 16, NT = KT * (KT + 1) / 2;
-      double err = 0.0;
-      for (int t = wv; t < NT; t += XW) {
-        int ti = 0, tt = t;
-        while (tt >= KT - ti) { tt -= KT - ti; ++ti; }
-        const int tj = ti + tt;
-        const int ca = 16 * ti + (lane & 15), cb = 16 * tj + (lane & 15);
-        f64x4g acc = f64x4g{0.0, 0.0, 0.0, 0.0};
-        for (int r0 = 0; r0 < K; r0 += 4) {
-          const int r = r0 + (lane >> 4);
-          const double a = (r < K && ca < K) ? Y[(size_t)r * LD + ca] : 0.0;
-          const double c = (r < K && cb < K) ? Y[(size_t)r * LD + cb] : 0.0;
-          acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, c, acc, 0, 0, 0);
-        }
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 16 * ti + (lane >> 4) + 4 * e, j = 16 * tj + (lane & 15);
-          if (i < K && j < K) {
-            const double g = fabs(acc[e] - (i == j ? 1.0 : 0.0));
-            err = (g > err || g != g) ? g : err;
-          }
-        }
-      }
-      err = xl_ext(err != err ? INFINITY : err, red, true);
+      const double err = xl_ortho_err(Y, K, LD, red);
       // psd_tol >= 0 (the eigen adjustment): a matrix with an eigenvalue below -psd_tol lambda_max
       // is an invalid date whose eigenvectors nobody reads -- flagged 2, not re-solved
       const bool need = psd_tol < 0.0 || lam[K - 1] >= -psd_tol * fabs(lam[0]);
       if (!(err <= tol) && !need) {
         if (tid == 0 && flags) flags[b] = 2;
       } else if (!(err <= tol)) {
+        // Warm start: U0 = Q Y (back-transform), orthonormalised by Newton-Schulz steps
+        // U <- U (3 I - U^T U) / 2 (quadratic once |U^T U - I| < 1: the small-gap case, where
+        // the twisted vectors are nearly orthonormal); then the Jacobi only has to rotate
+        // S = U0^T A U0 inside its clusters, and U = U0 V.  Exactly repeated eigenvalues give
+        // (nearly) parallel vectors the iteration cannot separate: cold Jacobi on A, V = I.
         const double* A = Ain + (size_t)b * K * K;
-        for (int e = tid; e < K * K; e += XT) {
-          const int i = e / K, j = e - i * K;
-          Aw[(size_t)i * LD + j] = 0.5 * (A[e] + A[(size_t)j * K + i]);
-          Y[(size_t)i * LD + j] = i == j ? 1.0 : 0.0;
+        double* T2 = tw;  // one K x LD matrix (tw holds 2K x TS >= K x LD doubles)
+        for (int c0 = 32 * wv; c0 < K; c0 += 32 * XW)
+          xl_back_wy<2>(Aw, Y, tau, K, LD, c0, yp + 512 * wv, lane);
+        __syncthreads();
+        double e2 = err;
+        for (int it = 0; it < 4 && e2 < 0.5; ++it) {
+          xl_mm<true>(Y, LD, Y, LD, Aw, LD, K);       // G = U^T U
+          __syncthreads();
+          xl_mm<false>(Y, LD, Aw, LD, T2, LD, K);      // H = U G
+          __syncthreads();
+          for (int e = tid; e < K * K; e += XT) {
+            const int i = e / K, j = e - i * K;
+            Y[(size_t)i * LD + j] = 1.5 * Y[(size_t)i * LD + j] - 0.5 * T2[(size_t)i * LD + j];
+          }
+          __syncthreads();
+          e2 = xl_ortho_err(Y, K, LD, red);
+          if (e2 <= 1e-14) break;
+        }
+        const bool warm = e2 <= 1e-14;
+        if (warm) {
+          xl_mm<false>(A, K, Y, LD, T2, LD, K);        // A U0 (A symmetric up to rounding)
+          __syncthreads();
+          xl_mm<true>(Y, LD, T2, LD, Aw, LD, K);       // S = U0^T A U0
+          __syncthreads();
+          for (int e = tid; e < K * K; e += XT) {      // U0 -> T2, V = I
+            const int i = e / K, j = e - i * K;
+            T2[(size_t)i * LD + j] = Y[(size_t)i * LD + j];
+            Y[(size_t)i * LD + j] = i == j ? 1.0 : 0.0;
+          }
+        } else {
+          for (int e = tid; e < K * K; e += XT) {
+            const int i = e / K, j = e - i * K;
+            Aw[(size_t)i * LD + j] = 0.5 * (A[e] + A[(size_t)j * K + i]);
+            Y[(size_t)i * LD + j] = i == j ? 1.0 : 0.0;
+          }
         }
         __syncthreads();
         int* idx = reinterpret_cast<int*>(yp);
@@ -595,6 +663,18 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         double* cs_s = cs_c + K / 2 + 2;
         xl_jacobi(Aw, Y, K, LD, idx, cs_c, cs_s, red);
         __syncthreads();
+        if (warm) {  // eigenvalues to LDS, then U = U0 V into Aw, read back as Y below
+          for (int k = tid; k < K; k += XT) lam[k] = Aw[(size_t)k * LD + k];
+          __syncthreads();
+          xl_mm<false>(T2, LD, Y, LD, Aw, LD, K);
+          __syncthreads();
+          for (int e = tid; e < K * K; e += XT) {
+            const int i = e / K, j = e - i * K;
+            Y[(size_t)i * LD + j] = Aw[(size_t)i * LD + j];
+          }
+          for (int k = tid; k < K; k += XT) Aw[(size_t)k * LD + k] = lam[k];
+          __syncthreads();
+        }
         for (int k = tid; k < K; k += XT) {  // descending rank of diag entry k (ties by index)
           const double dk = Aw[(size_t)k * LD + k];
           int rank = 0;

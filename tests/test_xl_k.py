@@ -189,3 +189,30 @@ def test_xl_bias_many_problems_per_slot(cuda, wpe):
         eigen.set_xl_waves_per_simd(0)
     ref = eigen._bias_sum_reference(w, valid, Cz.cpu())
     torch.testing.assert_close(S, ref, rtol=1e-9, atol=1e-12, equal_nan=True)
+
+
+@pytest.mark.gpu
+def test_xl_eigh_close_pairs_warm_resolve(cuda):
+    """Eigenvalue pairs 1e-9 apart (relative) at K = 180: the twisted-factorisation vectors of a
+    pair are not orthogonal to 1e-10, so the matrix is re-solved -- warm-started from its own
+    vectors made orthonormal by Newton-Schulz steps, the Jacobi rotating only inside the pairs;
+    the result is orthonormal with LAPACK eigenvalues."""
+    K, B = 180, 3
+    g = torch.Generator().manual_seed(8)
+    out = []
+    for b in range(B):
+        Q, _ = torch.linalg.qr(torch.randn(K, K, generator=g, dtype=torch.float64))
+        lam = torch.exp(torch.linspace(0.0, -6.0, K, dtype=torch.float64))
+        lam[1::7] = lam[0::7][:lam[1::7].numel()] * (1 + 1e-9)   # close pairs
+        out.append((Q * lam) @ Q.T)
+    A = torch.stack(out)
+    w, U = eigen.eigh(A.to(cuda))
+    flags = eigen.LAST_EIGH_FLAGS.cpu()
+    w, U = w.cpu(), U.cpu()
+    assert int((flags == 1).sum()) >= 1, flags
+    eye = torch.eye(K, dtype=torch.float64)
+    for b in range(B):
+        assert (U[b].T @ U[b] - eye).abs().max() < 1e-10, (b, int(flags[b]))
+        assert (A[b] @ U[b] - U[b] * w[b]).abs().max() < 1e-12, b
+        torch.testing.assert_close(w[b], torch.linalg.eigvalsh(A[b]).flip(-1), rtol=1e-10,
+                                   atol=1e-15)
