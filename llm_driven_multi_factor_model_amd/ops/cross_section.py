@@ -75,10 +75,12 @@ def _validate(X, cap, ret, ind, P):
         raise ValueError(f"cap/ret must be [D, N] = {(D, N)}; got {tuple(cap.shape)}, {tuple(ret.shape)}")
     if P > 0 and (ind is None or ind.shape != (D, N)):
         raise ValueError("ind must be [D, N] when P > 0")
-    if not 1 <= Q <= 16:
-        raise ValueError(f"Q={Q} outside the supported 1..16 range")
-    if P > XS_MAX_P:
-        raise ValueError(f"P={P} > {XS_MAX_P} industries is not supported")
+    if Q < 1:
+        raise ValueError(f"Q={Q}: at least one style factor is needed (the pooled style sigma)")
+    if X.is_cuda and Q > 16:  # the kernels' register / LDS layouts; the CPU path takes any Q, P
+        raise ValueError(f"Q={Q} outside the GPU kernels' 1..16 range")
+    if X.is_cuda and P > XS_MAX_P:
+        raise ValueError(f"P={P} > {XS_MAX_P} industries is not supported on the GPU")
     return D, Q, N
 
 

@@ -216,3 +216,17 @@ def test_xl_eigh_close_pairs_warm_resolve(cuda):
         assert (A[b] @ U[b] - U[b] * w[b]).abs().max() < 1e-12, b
         torch.testing.assert_close(w[b], torch.linalg.eigvalsh(A[b]).flip(-1), rtol=1e-10,
                                    atol=1e-15)
+
+
+def test_cpu_paths_take_any_industry_and_style_count():
+    """The CPU fp64 paths (the oracles, and the reference's own range: any K) are not bound by
+    the GPU kernels' P <= 256 / Q <= 16: the dense oracle and the moment-space path agree at
+    P = 300 industries, Q = 18 styles (K = 319)."""
+    from llm_driven_multi_factor_model_amd.ops import cross_section as X
+    from llm_driven_multi_factor_model_amd.ops.xs_sharded import xs_wls_stock_sharded
+    p = synthetic_panel(3, 900, 300, 18, seed=2, missing_frac=0.01, dtype=torch.float64)
+    a = X.xs_wls(p.styles, p.cap, p.ret, p.ind, 300)
+    b = xs_wls_stock_sharded(p.styles, p.cap, p.ret, p.ind, 300)
+    assert a.f.shape == (3, 319) and torch.isfinite(a.f).all()
+    torch.testing.assert_close(b.f, a.f, rtol=1e-8, atol=1e-10)
+    torch.testing.assert_close(b.r2, a.r2, rtol=1e-9, atol=1e-11)
