@@ -47,6 +47,16 @@ constexpr int XL_MAX_K = 1024;
 // 2.48 -> 2.21 ms at K = 150; profiles/r06/xl/xl_bench.log).
 int g_xl_wpe = 0;
 
+// Timing-only phase ablations (A/B builds: mfa_eigen_xl_set_ablation): bit 1 skips the fused
+// Householder pass, 2 the eigenvalues, 4 the twisted-factorisation vectors, 8 the back-transform.
+// Results are meaningless with any bit set.  Production builds compile the checks out.
+#if MFA_AB
+__device__ int d_xl_abl = 0;
+#define XL_SKIP(bit) ((d_xl_abl & (bit)) != 0)
+#else
+#define XL_SKIP(bit) false
+#endif
+
 __device__ __forceinline__ double xl_ext(double v, double* red, bool mx) {
   v = mx ? wave_max(v) : wave_min(v);
   __syncthreads();
@@ -437,7 +447,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         if (j >= s + 2) Aw[(size_t)s * LD + j] = v;  // reflector s, v_{s+1} = 1 implied
       }
       __syncthreads();
-      {
+      if (!XL_SKIP(1)) {
         // Lower triangle only (half the traffic of the full square): the wave's rows
         // j = s + 1 + wv + XW q (q < nrw), columns s + 1 <= i <= j in batches of NC 64-column
         // chunks, streamed with the next batch's loads issued before the current batch's
@@ -449,11 +459,24 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         const int nrw = n1 > wv ? (n1 - wv + XW - 1) / XW : 0;
         double* ypw = yp + wv * K;
         for (int i = s + 1 + lane; i < K; i += 64) ypw[i] = 0.0;
+        // the first NC chunks' per-column constants and column partials stay in registers for
+        // the whole step (they do not depend on the row); chunks beyond (K > 257) use LDS
+        double rv[NC], rw[NC], rc[NC], cacc[NC];
+#pragma unroll
+        for (int u = 0; u < NC; ++u) {
+          const int i = s + 1 + 64 * u + lane;
+          const bool ok = i < K;
+          rv[u] = (ok && pend) ? vp[i] : 0.0;
+          rw[u] = (ok && pend) ? wp[i] : 0.0;
+          rc[u] = ok ? vc[i] : 0.0;
+          cacc[u] = 0.0;
+        }
         double cur[NC], nxt[NC];
         int q = 0, bt = 0;
 #pragma unroll
         for (int u = 0; u < NC; ++u) {
           const int j = s + 1 + wv, i = s + 1 + 64 * u + lane;
+          if (64 * u > wv) break;  // chunk u starts right of the diagonal of row s + 1 + wv
           cur[u] = (nrw > 0 && i <= j) ? Aw[(size_t)j * LD + i] : 0.0;
         }
         double rsum = 0.0;
@@ -469,6 +492,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             const int jn = s + 1 + wv + XW * qn;
 #pragma unroll
             for (int u = 0; u < NC; ++u) {
+              if (64 * (NC * bn + u) > jn - s - 1) break;  // past the diagonal: no load
               const int i = s + 1 + 64 * (NC * bn + u) + lane;
               nxt[u] = i <= jn ? Aw[(size_t)jn * LD + i] : 0.0;
             }
@@ -476,15 +500,25 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
           const double vj = vc[j], vpj = pend ? vp[j] : 0.0, wpj = pend ? wp[j] : 0.0;
 #pragma unroll
           for (int u = 0; u < NC; ++u) {
+            if (64 * (NC * bt + u) > j - s - 1) break;
             const int i = s + 1 + 64 * (NC * bt + u) + lane;
             if (i <= j) {
               double x = cur[u];
-              if (pend) {
-                x = fma(-vpj, wp[i], fma(-wpj, vp[i], x));
-                Aw[(size_t)j * LD + i] = x;
+              if (bt == 0) {
+                if (pend) {
+                  x = fma(-vpj, rw[u], fma(-wpj, rv[u], x));
+                  Aw[(size_t)j * LD + i] = x;
+                }
+                cacc[u] = fma(x, vj, cacc[u]);
+                if (i < j) rsum = fma(x, rc[u], rsum);
+              } else {
+                if (pend) {
+                  x = fma(-vpj, wp[i], fma(-wpj, vp[i], x));
+                  Aw[(size_t)j * LD + i] = x;
+                }
+                ypw[i] = fma(x, vj, ypw[i]);
+                if (i < j) rsum = fma(x, vc[i], rsum);
               }
-              ypw[i] = fma(x, vj, ypw[i]);
-              if (i < j) rsum = fma(x, vc[i], rsum);
             }
           }
           if (bn == 0) {  // row j done: its row part
@@ -496,6 +530,11 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
           for (int u = 0; u < NC; ++u) cur[u] = nxt[u];
           q = qn;
           bt = bn;
+        }
+#pragma unroll
+        for (int u = 0; u < NC; ++u) {
+          const int i = s + 1 + 64 * u + lane;
+          if (i < K) ypw[i] = cacc[u];  // chunks 0..NC-1 were never accumulated in LDS
         }
       }
       __syncthreads();
@@ -553,6 +592,10 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     hi = hi * is + 1e-15;
     // ---- eigenvalues (descending: lane k finds ascending index K - 1 - k) ----
     for (int k = tid; k < K; k += XT) {
+      if (XL_SKIP(2)) {
+        lam[k] = tb[k].x;
+        continue;
+      }
       const int ix = K - 1 - k;
       double a = lo, c = hi;
       for (int it = 0; it < 128; ++it) {
@@ -565,7 +608,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     __syncthreads();
     // ---- eigenvectors of T by twisted factorisation ----
     const double pivmin = 1e-290;
-    for (int k = tid; k < K; k += XT) {
+    for (int k = tid; k < K && !XL_SKIP(4); k += XT) {
       const double x = lam[k];
       double* tp = tw + tid;
       double* tm = tw + (size_t)K * TS + tid;
@@ -698,7 +741,7 @@ __global__ __launch_bounds__(XT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       }
     }
     // ---- back-transform Y <- H_0 ... H_{K-3} Y: waves own 32-column chunks ----
-    for (int c0 = 32 * wv; c0 < K; c0 += 32 * XW)
+    for (int c0 = 32 * wv; c0 < K && !XL_SKIP(8); c0 += 32 * XW)
       xl_back_wy<2>(Aw, Y, tau, K, LD, c0, yp + 512 * wv, lane);
     __syncthreads();
     // ---- outputs: lane k owns column k ----
@@ -820,4 +863,13 @@ MFA_API int mfa_eigen_xl_set_wpe(int w) {
   if (w != 0 && w != 2 && w != 4) return (int)hipErrorInvalidValue;
   g_xl_wpe = w;
   return 0;
+}
+
+// Timing-only phase ablation bits of the XL solver (A/B builds; hipErrorInvalidValue otherwise).
+MFA_API int mfa_eigen_xl_set_ablation(int bits) {
+#if MFA_AB
+  return (int)hipMemcpyToSymbol(HIP_SYMBOL(d_xl_abl), &bits, sizeof(int));
+#else
+  return bits == 0 ? 0 : (int)hipErrorInvalidValue;
+#endif
 }

@@ -127,7 +127,14 @@ def test_xl_risk_model_matches_cpu(cuda):
     Fh, vb = eigen.eigen_risk_adjust(g.nw_cov.cpu(), Cz=Cz, scale_coef=cfg.eigen_scale,
                                      return_bias=True)
     torch.testing.assert_close(g.eigen_bias.cpu(), vb, rtol=1e-8, atol=1e-10, equal_nan=True)
-    torch.testing.assert_close(g.eigen_cov.cpu(), Fh, rtol=1e-8, atol=1e-16, equal_nan=True)
+    # F^ = U diag(v^2 w) U^T is not defined by the eigenvalues alone where F0 has a nearly
+    # degenerate pair with different multipliers (any rotation inside the pair is an eigenbasis):
+    # compare the dates whose F0 eigenvalue gaps exceed 1e-7 of the largest eigenvalue
+    w0 = torch.linalg.eigvalsh(torch.nan_to_num(g.nw_cov.cpu()))
+    gap = (w0[:, 1:] - w0[:, :-1]).min(-1).values / w0.abs().amax(-1).clamp_min(1e-300)
+    ok = (gap > 1e-7) & fin
+    assert int(ok.sum()) >= 20
+    torch.testing.assert_close(g.eigen_cov.cpu()[ok], Fh[ok], rtol=1e-8, atol=1e-16, equal_nan=True)
     assert torch.isfinite(g.eigen_cov.reshape(D, -1)[-10:]).all()   # not vacuously NaN
 
 
