@@ -107,6 +107,10 @@ def xs_wls(X: torch.Tensor, cap: torch.Tensor, ret: torch.Tensor, ind: torch.Ten
     bitwise-reproducible kernel: each LDS segment replica is owned by one wave and the wave
     partials are summed in a fixed order.  It costs 0-3 % (profiles/r02_xs_deterministic.md);
     ``False`` shares the replicas across waves (reproducible to rounding only).
+    More than FUSED_MAX_P = 128 industries (up to XS_MAX_P = 256) run on the split kernels
+    (moments -> solve -> device pinv -> residuals, :func:`.xs_sharded.xs_wls_stock_sharded` at
+    world size 1): fresh outputs every call (``out`` / ``workspace`` are not used there) and a
+    shared-replica industry table (reproducible to rounding only).
     """
     D, Q, N = _validate(X, cap, ret, ind, P)
     K = 1 + P + Q
