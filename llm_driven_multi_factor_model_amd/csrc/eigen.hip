@@ -1806,7 +1806,8 @@ MFA_API int mfa_mc_cov_range(int M, int m0, int K, int T, unsigned long long see
 // Wide draw covariances (64 < K <= 144, mc_cov_wide_kernel): scratch doubles for (M, K, T).
 MFA_API size_t mfa_mc_cov_wide_ws_doubles(int M, int K, int T) {
   const int C = mc_cov_chunks(M, T);
-  return (size_t)M * C * (K <= 96 ? WideCov<96>::PART : WideCov<144>::PART);
+  return (size_t)M * C * (K <= 96 ? WideCov<96>::PART : K <= 144 ? WideCov<144>::PART
+                                                                : WideCov<160>::PART);
 }
 
 // Draw covariances of sims [m0, m0 + M), 64 < K <= 144, on the fp64 matrix cores: a sim's
@@ -1814,10 +1815,13 @@ MFA_API size_t mfa_mc_cov_wide_ws_doubles(int M, int K, int T) {
 MFA_API int mfa_mc_cov_wide(int M, int m0, int K, int T, unsigned long long seed, double* ws,
                             double* Cz, void* stream) {
   if (M <= 0) return 0;
-  if (K <= 64 || K > 144 || T < 2 || m0 < 0 || ws == nullptr) return (int)hipErrorInvalidValue;
+  if (K <= 64 || K > 160 || T < 2 || m0 < 0 || ws == nullptr) return (int)hipErrorInvalidValue;
   const int C = mc_cov_chunks(M, T);
   hipStream_t s = (hipStream_t)stream;
-  if (K <= 96) {
+  if (K > 144) {
+    hipLaunchKernelGGL(mc_cov_wide_kernel<160>, dim3(M * C), dim3(256), 0, s, K, T, seed, m0, C, ws);
+    hipLaunchKernelGGL(mc_cov_wide_reduce_kernel<160>, dim3(M), dim3(256), 0, s, K, T, C, ws, Cz);
+  } else if (K <= 96) {
     hipLaunchKernelGGL(mc_cov_wide_kernel<96>, dim3(M * C), dim3(256), 0, s, K, T, seed, m0, C, ws);
     hipLaunchKernelGGL(mc_cov_wide_reduce_kernel<96>, dim3(M), dim3(256), 0, s, K, T, C, ws, Cz);
   } else {

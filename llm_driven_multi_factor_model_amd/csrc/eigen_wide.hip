@@ -1,4 +1,4 @@
-// Monte-Carlo eigenfactor bias statistic for wide factor sets (64 < K <= 144) on gfx950.
+// Monte-Carlo eigenfactor bias statistic for wide factor sets (64 < K <= 160) on gfx950.
 //
 // Reference: Barra-master/mfm/utils.py:55-92 (eigen_risk_adj), as csrc/eigen.hip: per (date,
 // sim) the bias ratios v[k] = V[:,k]^T D0 V[:,k] / Lambda[k] of A = S C_z S (descending).
@@ -1070,9 +1070,17 @@ MFA_API int mfa_eigen_wide_set_eig_rounds(int r) {
 MFA_API int mfa_eigh_wide_fix(const double* A, int B, int K, double tol, double* w, double* U,
                               double* ws, int* fixed, void* stream) {
   if (B <= 0) return 0;
-  if (K <= 64 || K > 144 || ws == nullptr) return (int)hipErrorInvalidValue;
+  if (K <= 64 || K > 160 || ws == nullptr) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  if (K <= 96) {
+  if (K > 144) {  // 144 < K <= 160: the same 5-wave pair layout at KP = 160 (LDS ~118 KB)
+    const size_t lds = bias_wide2_lds(K, 160, 5);
+    (void)hipFuncSetAttribute((const void*)mc_bias_wide2_kernel<160, 5, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((mc_bias_wide2_kernel<160, 5, true>), dim3(B), dim3(5 * 64), lds, s, A, K, 1,
+                       (const double*)nullptr, (const int*)nullptr, w,
+                       (g_wide_eig_rounds << 4) | (g_wide_eig_abstol << 8), U);
+    hipLaunchKernelGGL(eigh_wide_fix_kernel<160>, dim3(B), dim3(256), 0, s, A, K, tol, w, U, ws, fixed);
+  } else if (K <= 96) {
     const size_t lds = bias_wide2_lds(K, 96, 3);
     (void)hipFuncSetAttribute((const void*)mc_bias_wide2_kernel<96, 3, true>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1095,8 +1103,16 @@ MFA_API int mfa_eigh_wide_fix(const double* A, int B, int K, double tol, double*
 // The tridiagonal EIG kernel alone (no check), 96 < K <= 144: A/B and tests.
 MFA_API int mfa_eigh_wide(const double* A, int B, int K, double* w, double* U, void* stream) {
   if (B <= 0) return 0;
-  if (K <= 96 || K > 144) return (int)hipErrorInvalidValue;
+  if (K <= 96 || K > 160) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
+  if (K > 144) {
+    const size_t lds = bias_wide2_lds(K, 160, 5);
+    (void)hipFuncSetAttribute((const void*)mc_bias_wide2_kernel<160, 5, true>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipLaunchKernelGGL((mc_bias_wide2_kernel<160, 5, true>), dim3(B), dim3(5 * 64), lds, s, A, K,
+                       1, (const double*)nullptr, (const int*)nullptr, w, 0, U);
+    return (int)hipGetLastError();
+  }
   const size_t lds = bias_wide2_lds(K, 144, 5);
   (void)hipFuncSetAttribute((const void*)mc_bias_wide2_kernel<144, 5, true>,
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -1121,11 +1137,17 @@ MFA_API int mfa_eigen_bias_accumulate_wide(const double* D0, const int* dvalid, 
                                            int M, const double* Cz, double* ws, double* S,
                                            void* stream) {
   if (D <= 0 || M <= 0) return 0;
-  if (K < 3 || K > 144) return (int)hipErrorInvalidValue;
+  if (K < 3 || K > 160) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
-  if ((g_wide_variant == 1 && K > 96) || g_wide_variant == 2) {
-    // two lanes per row: 5 waves per problem for K > 96, 3 for K <= 96
-    if (K > 96) {
+  if ((g_wide_variant == 1 && K > 96) || g_wide_variant == 2 || K > 144) {
+    // two lanes per row: 5 waves per problem for K > 96 (KP = 160 above 144), 3 for K <= 96
+    if (K > 144) {
+      const size_t lds = bias_wide2_lds(K, 160, 5);
+      (void)hipFuncSetAttribute((const void*)mc_bias_wide2_kernel<160, 5>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      hipLaunchKernelGGL((mc_bias_wide2_kernel<160, 5>), dim3(D * M), dim3(5 * 64), lds, s, D0, K,
+                         M, Cz, dvalid, ws, g_wide_abl);
+    } else if (K > 96) {
       const size_t lds = bias_wide2_lds(K, 144, 5);
       (void)hipFuncSetAttribute((const void*)mc_bias_wide2_kernel<144, 5>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);

@@ -73,7 +73,8 @@ TOL = 1e-15
 # kernels: the draw covariances on the fp64 matrix cores (mc_cov_wide_kernel, the same Philox
 # stream: factor k < 64 of a sim is the same number at any K), the F0 eigh and the bias statistic
 # on the multi-wave tridiagonal solver (csrc/eigen_wide.hip, with a device orthogonality check
-# and Jacobi re-solve), the finalize on eigen_finalize_kernel.  From WIDE_HIP_MAX_K to XL_MAX_K the
+# and Jacobi re-solve; KP = 96 / 144 / 160 instantiations), the finalize on eigen_finalize_kernel.
+# From WIDE_HIP_MAX_K to XL_MAX_K the
 # XL kernels take over (csrc/eigen_xl.hip: one persistent 8-wave workgroup per problem with its
 # working matrix in a global slot; output-tiled MFMA draw covariances in csrc/eigen.hip), still
 # with no vendor library and no host synchronisation.  Only K > XL_MAX_K (or the "rocsolver"
@@ -86,7 +87,7 @@ WIDE_CHUNK_DOUBLES = 1 << 27     # ~1 GB of fp64 per batched eigh / draw chunk
 # the GPU's throughput, within 3e-14 of rocSOLVER, profiles/r04/wide_bias_ab.jsonl) or
 # "rocsolver" (batched syevd through torch: 27.7 us).  Wider K always takes rocSOLVER.
 # MFA_WIDE_BIAS selects the solver at import.
-WIDE_HIP_MAX_K = 144
+WIDE_HIP_MAX_K = 160   # KP = 96 / 144 / 160 instantiations of the multi-wave kernels
 XL_MAX_K = 1024
 WIDE_BIAS_SOLVERS = ("rocsolver", "hip")
 _wide_solver = os.environ.get("MFA_WIDE_BIAS", "hip")

@@ -53,7 +53,7 @@ def test_hip_wide_mc_cov_same_draws(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("K", [65, 140])
+@pytest.mark.parametrize("K", [65, 140, 145, 160])
 def test_hip_wide_eigh_and_adjust_match_cpu(cuda, K):
     D, M = 6, 5
     F = _spd(D, K, seed=K, spread=2.0) * 1e-4
@@ -258,7 +258,7 @@ def test_hip_wide_eigh_native(cuda):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("K", [80, 101, 140])
+@pytest.mark.parametrize("K", [80, 101, 140, 157])
 def test_hip_wide_mc_cov_is_fp64_cov_of_its_philox_draws(cuda, K):
     """K > 64 draw covariances (mc_cov_wide_kernel, fp64 matrix cores): every entry equals
     numpy's fp64 cov of the same Philox normals (tile layout, odd K, centring)."""

@@ -66,7 +66,7 @@ def main():
             print(json.dumps({"what": "eigh", "path": path, "K": K, "B": a.B, "ms": round(ms, 3),
                               "dw_rel": float(((w - ref).abs() / ref.abs().amax(-1, keepdim=True)).max()),
                               "resid": res,
-                              "flagged": int(eigen.LAST_EIGH_FLAGS.sum()) if path.startswith("hip") else None}),
+                              "flagged": int(eigen.LAST_EIGH_FLAGS.sum()) if path.startswith("hip") and K > eigen.WIDE_HIP_MAX_K else None}),
                   flush=True)
         with use(paths[0]):
             Cz, ms = timed(lambda: eigen.mc_cov(a.M, K, a.T, seed=1, device=dev))
