@@ -894,7 +894,8 @@ __global__ __launch_bounds__(64) void wide_bias_sum_kernel(const double* __restr
 // (Golub-Van Loan sym.schur2); A <- J^T A J on 2 x 2 pair blocks, V <- V J.
 template <int KP>
 __global__ __launch_bounds__(256) void eigh_wide_fix_kernel(const double* __restrict__ Ain, int K,
-                                                            double tol, double* __restrict__ w,
+                                                            double tol, double psd_tol,
+                                                            double* __restrict__ w,
                                                             double* __restrict__ U,
                                                             double* __restrict__ ws,
                                                             int* __restrict__ fixed) {
@@ -945,6 +946,12 @@ __global__ __launch_bounds__(256) void eigh_wide_fix_kernel(const double* __rest
   err = block_ext<4, true>(err != err ? INFINITY : err, red, tid);
   if (err <= tol) {
     if (tid == 0 && fixed) fixed[b] = 0;
+    return;
+  }
+  // psd_tol >= 0 (the eigen adjustment): an indefinite matrix is an invalid date whose
+  // eigenvectors are never read -- flagged 2, not re-solved (uniform: w is global)
+  if (psd_tol >= 0.0 && w[(size_t)b * K + K - 1] < -psd_tol * fabs(w[(size_t)b * K])) {
+    if (tid == 0 && fixed) fixed[b] = 2;
     return;
   }
   // ---- Jacobi re-solve ----
@@ -1046,7 +1053,8 @@ __global__ __launch_bounds__(256) void eigh_wide_fix_kernel(const double* __rest
 // Batched eigendecomposition of symmetric [B][K][K] matrices, 64 < K <= 144 (two lanes per row,
 // 3 / 5 waves for K <= 96 / 144): w [B][K] descending, U [B][K][K] with U[:, k] = eigenvector k
 // (NaN for non-finite inputs); then eigh_wide_fix_kernel checks U^T U = I to `tol` and re-solves
-// the matrices that fail with the Jacobi (ws: B*K*K doubles; fixed [B] nullable: 1 = re-solved).
+// the matrices that fail with the Jacobi (ws: B*K*K doubles; fixed [B] nullable: 1 = re-solved,
+// 2 = not re-solved: psd_tol >= 0 and an eigenvalue below -psd_tol lambda_max).
 // Multisection rounds of the F0 eigh before its Laguerre loop (A/B knob; 0 = off).  F0 is not
 // diagonally dominant (a Newey-West covariance), so the diagonal guesses are poorer than for
 // the bias problems S C_z S.
@@ -1067,8 +1075,8 @@ MFA_API int mfa_eigen_wide_set_eig_rounds(int r) {
   return 0;
 }
 
-MFA_API int mfa_eigh_wide_fix(const double* A, int B, int K, double tol, double* w, double* U,
-                              double* ws, int* fixed, void* stream) {
+MFA_API int mfa_eigh_wide_fix_psd(const double* A, int B, int K, double tol, double psd_tol,
+                                  double* w, double* U, double* ws, int* fixed, void* stream) {
   if (B <= 0) return 0;
   if (K <= 64 || K > 160 || ws == nullptr) return (int)hipErrorInvalidValue;
   hipStream_t s = (hipStream_t)stream;
@@ -1079,7 +1087,8 @@ MFA_API int mfa_eigh_wide_fix(const double* A, int B, int K, double tol, double*
     hipLaunchKernelGGL((mc_bias_wide2_kernel<160, 5, true>), dim3(B), dim3(5 * 64), lds, s, A, K, 1,
                        (const double*)nullptr, (const int*)nullptr, w,
                        (g_wide_eig_rounds << 4) | (g_wide_eig_abstol << 8), U);
-    hipLaunchKernelGGL(eigh_wide_fix_kernel<160>, dim3(B), dim3(256), 0, s, A, K, tol, w, U, ws, fixed);
+    hipLaunchKernelGGL(eigh_wide_fix_kernel<160>, dim3(B), dim3(256), 0, s, A, K, tol, psd_tol, w, U, ws,
+                       fixed);
   } else if (K <= 96) {
     const size_t lds = bias_wide2_lds(K, 96, 3);
     (void)hipFuncSetAttribute((const void*)mc_bias_wide2_kernel<96, 3, true>,
@@ -1087,7 +1096,8 @@ MFA_API int mfa_eigh_wide_fix(const double* A, int B, int K, double tol, double*
     hipLaunchKernelGGL((mc_bias_wide2_kernel<96, 3, true>), dim3(B), dim3(3 * 64), lds, s, A, K, 1,
                        (const double*)nullptr, (const int*)nullptr, w,
                        (g_wide_eig_rounds << 4) | (g_wide_eig_abstol << 8), U);
-    hipLaunchKernelGGL(eigh_wide_fix_kernel<96>, dim3(B), dim3(256), 0, s, A, K, tol, w, U, ws, fixed);
+    hipLaunchKernelGGL(eigh_wide_fix_kernel<96>, dim3(B), dim3(256), 0, s, A, K, tol, psd_tol, w, U, ws,
+                       fixed);
   } else {
     const size_t lds = bias_wide2_lds(K, 144, 5);
     (void)hipFuncSetAttribute((const void*)mc_bias_wide2_kernel<144, 5, true>,
@@ -1095,9 +1105,16 @@ MFA_API int mfa_eigh_wide_fix(const double* A, int B, int K, double tol, double*
     hipLaunchKernelGGL((mc_bias_wide2_kernel<144, 5, true>), dim3(B), dim3(5 * 64), lds, s, A, K, 1,
                        (const double*)nullptr, (const int*)nullptr, w,
                        (g_wide_eig_rounds << 4) | (g_wide_eig_abstol << 8), U);
-    hipLaunchKernelGGL(eigh_wide_fix_kernel<144>, dim3(B), dim3(256), 0, s, A, K, tol, w, U, ws, fixed);
+    hipLaunchKernelGGL(eigh_wide_fix_kernel<144>, dim3(B), dim3(256), 0, s, A, K, tol, psd_tol, w, U, ws,
+                       fixed);
   }
   return (int)hipGetLastError();
+}
+
+// As mfa_eigh_wide_fix_psd with every failing matrix re-solved (psd_tol < 0).
+MFA_API int mfa_eigh_wide_fix(const double* A, int B, int K, double tol, double* w, double* U,
+                              double* ws, int* fixed, void* stream) {
+  return mfa_eigh_wide_fix_psd(A, B, K, tol, -1.0, w, U, ws, fixed, stream);
 }
 
 // The tridiagonal EIG kernel alone (no check), 96 < K <= 144: A/B and tests.

@@ -46,6 +46,9 @@ _native.register("mfa_eigen_bias_accumulate_wide", [C.c_void_p, C.c_void_p, C.c_
 _native.register("mfa_eigen_wide_set_variant", [C.c_int])
 _native.register("mfa_eigh_wide", [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
                                    C.c_void_p])
+_native.register("mfa_eigh_wide_fix_psd", [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_double,
+                                           C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                           C.c_void_p])
 _native.register("mfa_eigh_wide_fix", [C.c_void_p, C.c_int, C.c_int, C.c_double, C.c_void_p,
                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p])
 _native.register("mfa_mc_cov_wide", [C.c_int, C.c_int, C.c_int, C.c_int, C.c_uint64, C.c_void_p,
@@ -226,8 +229,12 @@ def _eigh_wide(Ab, shp, resolve_psd_tol=None):
         ws = torch.empty(B * K * K, dtype=torch.float64, device=Ab.device)
         # tridiagonal EIG kernel, then per matrix max |U^T U - I| on the matrix cores and a
         # device Jacobi re-solve of the finite matrices that fail it (no host synchronisation)
-        _native.call("mfa_eigh_wide_fix", _native.ptr(Ab), B, K, ORTHO_TOL, _native.ptr(w),
-                     _native.ptr(U), _native.ptr(ws), None, _native.stream(Ab.device))
+        flags = torch.empty(B, dtype=torch.int32, device=Ab.device)
+        psd = -1.0 if resolve_psd_tol is None else float(resolve_psd_tol)
+        _native.call("mfa_eigh_wide_fix_psd", _native.ptr(Ab), B, K, ORTHO_TOL, psd, _native.ptr(w),
+                     _native.ptr(U), _native.ptr(ws), _native.ptr(flags), _native.stream(Ab.device))
+        global LAST_EIGH_FLAGS
+        LAST_EIGH_FLAGS = flags
         return w.reshape(shp[:-1]), U.reshape(shp)
     if _wide_solver == "hip" and K <= XL_MAX_K:
         return _eigh_xl(Ab, shp, resolve_psd_tol)

@@ -322,3 +322,26 @@ def test_hip_wide_eigh_clustered_spectra_resolved_on_device(cuda, K):
     An[1, 3, 5] = float("nan")
     wn, Un = eigen.eigh(An)
     assert torch.isnan(wn[1]).all() and torch.isfinite(wn[0]).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K", [80, 170])
+def test_hip_eigh_skips_resolve_of_indefinite_dates(cuda, K):
+    """The eigen adjustment passes resolve_psd_tol: a clustered (re-solve-needing) matrix with a
+    negative eigenvalue -- an invalid date, whose eigenvectors are never read -- is flagged 2 and
+    not re-solved; without the tolerance it is re-solved (flag 1).  Eigenvalues agree both ways."""
+    A = _clustered(2, K, seed=K)
+    g = torch.Generator().manual_seed(K)
+    Q, _ = torch.linalg.qr(torch.randn(K, K, generator=g, dtype=torch.float64))
+    lam = torch.linalg.eigvalsh(A[0]).flip(-1)
+    lam[-3:] = -1e-6                                     # indefinite, with a repeated value
+    A[0] = (Q * lam) @ Q.T
+    Ag = A.to(cuda)
+    w1, _ = eigen.eigh(Ag)
+    f1 = eigen.LAST_EIGH_FLAGS.cpu()
+    w2, _ = eigen.eigh(Ag, resolve_psd_tol=0.0)
+    f2 = eigen.LAST_EIGH_FLAGS.cpu()
+    assert int(f1[0]) == 1 and int(f2[0]) == 2, (f1, f2)
+    assert int(f2[1]) == int(f1[1])                       # the PSD matrix is handled alike
+    torch.testing.assert_close(w2[0].cpu(), torch.linalg.eigvalsh(A[0]).flip(-1), rtol=1e-9,
+                               atol=1e-13)
